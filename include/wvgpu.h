@@ -1,0 +1,166 @@
+/*
+ * wvgpu.h -- C ABI of the MI355X (gfx950) vector-scoring backend for
+ * Weaviate's flat / BQ / PQ hot path.  Go binds it through cgo (see
+ * INTEGRATION.md); the test and bench harness binds it through ctypes.
+ *
+ * Citations are relative to the reference tree (antas-marcin/weaviate):
+ *   D/  = adapters/repos/db/vector/hnsw/distancer/
+ *   CH/ = adapters/repos/db/vector/compressionhelpers/
+ *   V/  = adapters/repos/db/vector/
+ *
+ * Conventions:
+ *  - every function returns WVG_OK (0) or a negative WVG_ERR_*; the message is
+ *    available from wvg_last_error() on the calling thread.  Nothing aborts.
+ *  - host buffers are borrowed for the duration of the call only and never
+ *    retained (cgo pointer rules); device memory belongs to the handles.
+ *  - distances are float32, smaller is closer; results are ascending by
+ *    (distance, id); ids are uint64 docIDs.
+ *  - handles are safe for concurrent searches; upsert/delete/reserve take an
+ *    exclusive lock on the corpus.
+ */
+#ifndef WVGPU_H
+#define WVGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WVG_ABI_VERSION 1
+
+#define WVG_OK 0
+#define WVG_ERR_INVALID -1       /* bad argument (null, k < 0 analogue, bad kind) */
+#define WVG_ERR_DIM_MISMATCH -2  /* "vector lengths don't match" (D/l2.go:47-50) */
+#define WVG_ERR_NOMEM -3
+#define WVG_ERR_DEVICE -4        /* HIP runtime error */
+#define WVG_ERR_NOT_FOUND -5     /* id not present (deleted / never added) */
+#define WVG_ERR_UNSUPPORTED -6
+#define WVG_ERR_CAPACITY -7      /* id outside [id_base, id_base + capacity) */
+
+/* corpus kinds */
+#define WVG_KIND_F32 0 /* float32 rows (flat "vectors" bucket, V/flat/index.go:259-260) */
+#define WVG_KIND_BQ 1  /* sign-bit codes (CH/binary_quantization.go:32) */
+#define WVG_KIND_PQ 2  /* PQ byte codes (CH/product_quantization.go:420) */
+
+/* metrics: entities/vectorindex/common/config.go:22-31 */
+#define WVG_METRIC_L2 0     /* "l2-squared" D/l2.go */
+#define WVG_METRIC_DOT 1    /* "dot"        D/dot_product.go */
+#define WVG_METRIC_COSINE 2 /* "cosine-dot" D/cosine_dist.go (rows/queries normalized) */
+
+typedef struct wvg_ctx wvg_ctx;
+typedef struct wvg_corpus wvg_corpus;
+
+/* ---- library / device ---------------------------------------------------- */
+int wvg_abi_version(void);
+const char *wvg_last_error(void);
+int wvg_device_count(int *out);
+/* One context per GPU (one process per GPU in the multi-GPU deployment). */
+int wvg_open(int device, wvg_ctx **out);
+int wvg_close(wvg_ctx *ctx);
+int wvg_synchronize(wvg_ctx *ctx);
+
+/* ---- corpus: the device-resident copy of a flat index's rows --------------
+ * Replaces the LSM cursor scan of V/flat/index.go:411-452 and the BQ cache of
+ * V/cache/sharded_lock_cache.go:29-60 (docID-indexed).  Slot = id - id_base.
+ * id_base must be a multiple of 64; capacity is rounded up to 64 rows.      */
+int wvg_corpus_create(wvg_ctx *ctx, int kind, int metric, uint32_t dim, uint64_t id_base,
+                      uint64_t capacity, wvg_corpus **out);
+int wvg_corpus_destroy(wvg_corpus *c);
+/* cache.Grow analogue (V/cache/sharded_lock_cache.go:251): keeps contents. */
+int wvg_corpus_reserve(wvg_corpus *c, uint64_t capacity);
+int wvg_corpus_info(wvg_corpus *c, uint64_t *count, uint64_t *high_water, uint64_t *capacity);
+/* flat.Add / AddBatch (V/flat/index.go:247-274): validates the dimension
+ * ("insert called with a vector of the wrong size"), normalizes for cosine,
+ * and for kind BQ encodes on device (index.go:262-270), for PQ encodes with
+ * the codebook (CH/product_quantization.go:420).  vectors: [n][dim] float32. */
+int wvg_corpus_upsert(wvg_corpus *c, const uint64_t *ids, const float *vectors, uint64_t n,
+                      uint32_t dim);
+/* Load already-encoded rows (restart from the "vectors_compressed" bucket,
+ * V/flat/index.go:640-681): BQ = [n][ceil(dim/64)] uint64 LE words,
+ * PQ = [n][m] bytes.  Stored as given (no normalization / encoding). */
+int wvg_corpus_upsert_codes(wvg_corpus *c, const uint64_t *ids, const void *codes, uint64_t n);
+/* flat.Delete (V/flat/index.go:276-295): clears the validity bit. */
+int wvg_corpus_delete(wvg_corpus *c, const uint64_t *ids, uint64_t n);
+/* flat.vectorById (V/flat/index.go:401-407): copies the stored row
+ * (F32: dim floats, BQ: words u64, PQ: m bytes); WVG_ERR_NOT_FOUND if absent. */
+int wvg_corpus_get(wvg_corpus *c, uint64_t id, void *out);
+/* Bench / test helper: fills slots [0, n) with synthetic rows generated in
+ * place from a counter-based RNG keyed by (seed, id_base + slot, column);
+ * distribution 0 = uniform [-1,1), 1 = integers 0..255.  F32 and BQ only.  */
+int wvg_corpus_fill_synthetic(wvg_corpus *c, uint64_t seed, uint64_t n, int distribution);
+/* PQ codebook: centers [m][ks][dim/m] float32 (KMeans centers, CH/kmeans.go:85-93).
+ * Validation as NewProductQuantizer (CH/product_quantization.go:187-197).  */
+int wvg_pq_set_codebook(wvg_corpus *c, const float *centers, uint32_t m, uint32_t ks);
+
+/* ---- search ---------------------------------------------------------------
+ * flat.SearchByVector (V/flat/index.go:307-334) for F32 corpora; for BQ the
+ * Hamming top-k of findTopVectorsCached (index.go:456-495); for PQ the ADC
+ * top-k (PQDistancer.Distance, CH/product_quantization.go:352-361).
+ * queries: [nq][dim] float32 (normalized internally for cosine, index.go:323).
+ * allow_bits: optional bitmap over global docIDs (helpers.AllowList), bit i of
+ * word i/64; an empty allow list yields empty results (index.go:425-427).
+ * Outputs: [nq][k] ids/dists, counts[nq] = min(k, live allowed rows).       */
+int wvg_search(wvg_corpus *c, const float *queries, uint32_t nq, uint32_t k,
+               const uint64_t *allow_bits, uint64_t allow_words, uint64_t *out_ids,
+               float *out_dists, uint32_t *out_counts);
+/* flat.searchByVectorBQ (V/flat/index.go:347-389): Hamming top-R over `bq`,
+ * R = max(rescore_limit, k) (index.go:297-305), exact rescore of the R
+ * candidates against the device-resident float rows of `f32`, top-k.      */
+int wvg_search_bq_rescore(wvg_corpus *bq, wvg_corpus *f32, const float *queries, uint32_t nq,
+                          uint32_t k, uint32_t rescore_limit, const uint64_t *allow_bits,
+                          uint64_t allow_words, uint64_t *out_ids, float *out_dists,
+                          uint32_t *out_counts);
+
+/* Device-pointer variants: inputs/outputs in HBM, asynchronous on `stream`
+ * (a hipStream_t, NULL = default stream); no host synchronization, no
+ * allocation (caller supplies a workspace of wvg_search_workspace_size bytes),
+ * so a call can be captured in a hipGraph.  Queries must already be
+ * normalized for cosine.                                                   */
+size_t wvg_search_workspace_size(wvg_corpus *c, uint32_t nq, uint32_t k);
+int wvg_search_device(wvg_corpus *c, const float *d_queries, uint32_t nq, uint32_t k,
+                      uint64_t *d_ids, float *d_dists, uint32_t *d_counts, void *d_workspace,
+                      size_t workspace_bytes, void *stream);
+/* Multi-shard merge (Index.objectVectorSearch, adapters/repos/db/index.go:1644-1648):
+ * [nlists][nq][k_in] (dist, id) lists (the layout an all-gather of per-GPU
+ * [nq][k_in] results produces) -> [nq][k] ascending, ties by id; missing
+ * entries carry id UINT64_MAX.                                            */
+int wvg_topk_merge_device(wvg_ctx *ctx, const float *d_dists, const uint64_t *d_ids, uint32_t nq,
+                          uint32_t nlists, uint32_t k_in, uint32_t k, uint64_t *d_out_ids,
+                          float *d_out_dists, uint32_t *d_out_counts, void *stream);
+
+/* Profiling: while enabled, every scan-kernel launch of this context is
+ * bracketed by a pair of HIP events on its stream; stop() synchronizes and
+ * returns the summed scan-kernel time and the launch count (feeds the
+ * vector_index_durations_ms metric, usecases/monitoring/prometheus.go:292). */
+int wvg_profile_start(wvg_ctx *ctx);
+int wvg_profile_stop(wvg_ctx *ctx, double *scan_ms_total, uint64_t *scan_launches);
+
+/* ---- bulk primitives (distancer.BatchProvider / compressionhelpers bulk) --- */
+/* Provider.SingleDist of q against n rows X [n][dim] (D/provider.go:14-20). */
+int wvg_distance_batch(wvg_ctx *ctx, int metric, const float *q, const float *X, uint64_t n,
+                       uint32_t dim, float *out);
+/* distancer.Normalize of n rows (D/normalize.go:16-32). */
+int wvg_normalize_batch(wvg_ctx *ctx, const float *X, uint64_t n, uint32_t dim, float *out);
+/* BinaryQuantizer.Encode of n rows -> [n][ceil(dim/64)] words (CH/binary_quantization.go:32-45). */
+int wvg_bq_encode(wvg_ctx *ctx, const float *X, uint64_t n, uint32_t dim, uint64_t *out_words);
+/* BinaryQuantizer.DistanceBetweenCompressedVectors of q against n codes (:47-56). */
+int wvg_bq_distance_batch(wvg_ctx *ctx, const uint64_t *q, const uint64_t *codes, uint64_t n,
+                          uint32_t words, float *out);
+/* ProductQuantizer.Encode of n rows (CH/product_quantization.go:420-426,
+ * CH/kmeans.go:103-135; ties to the highest centroid index). */
+int wvg_pq_encode(wvg_ctx *ctx, const float *centers, uint32_t m, uint32_t ks, const float *X,
+                  uint64_t n, uint32_t dim, uint8_t *out_codes);
+/* DistanceLookUpTable for one query (CH/product_quantization.go:62-104): [m][ks]. */
+int wvg_pq_lut(wvg_ctx *ctx, int metric, const float *centers, uint32_t m, uint32_t ks,
+               uint32_t dim, const float *q, float *out_lut);
+/* PQDistancer.Distance of n codes against a LUT (CH/product_quantization.go:352-361). */
+int wvg_pq_adc_batch(wvg_ctx *ctx, int metric, const float *lut, uint32_t m, uint32_t ks,
+                     const uint8_t *codes, uint64_t n, float *out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* WVGPU_H */

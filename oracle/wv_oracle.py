@@ -1,0 +1,266 @@
+"""ctypes wrapper of oracle/wv_oracle.c -- TEST INFRASTRUCTURE ONLY.
+
+Imported only by tests/, __graft_entry__.smoke() (as the checker) and
+bench.py's cpu_baseline leg.  The product (weaviate_amd/) never imports it.
+Parity is pinned against the reference's own compiled C kernels
+(oracle/_ref/libwvref.so, built by `make -C oracle ref` from /root/reference)
+and against the known answers of the reference's Go tests (tests/golden/).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from ctypes import POINTER, c_double, c_float, c_int, c_long, c_uint8, c_uint32, c_uint64, c_void_p
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "_build", "libwvoracle.so")
+REF_SO = os.path.join(HERE, "_ref", "libwvref.so")
+
+L2, DOT, COSINE = 0, 1, 2
+
+_F = POINTER(c_float)
+_U64 = POINTER(c_uint64)
+_U8 = POINTER(c_uint8)
+_REF_FN = ctypes.CFUNCTYPE(None, _F, _F, _F, POINTER(c_long))
+
+_lib = None
+_ref = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_SO):
+            build()
+        l = ctypes.CDLL(ORACLE_SO)
+        for n in ["orc_l2_256", "orc_dot_256", "orc_l2_512", "orc_dot_512", "orc_l2_step", "orc_dot_step"]:
+            getattr(l, n).restype = c_float
+            getattr(l, n).argtypes = [_F, _F, c_long]
+        l.orc_single_dist.restype = c_float
+        l.orc_single_dist.argtypes = [c_int, _F, _F, c_long]
+        l.orc_step.restype = c_float
+        l.orc_step.argtypes = [c_int, _F, _F, c_long]
+        l.orc_normalize.argtypes = [_F, c_long, _F]
+        l.orc_bq_encode.argtypes = [_F, c_long, _U64]
+        l.orc_bq_distance.restype = c_float
+        l.orc_bq_distance.argtypes = [_U64, _U64, c_long]
+        l.orc_pq_lut.argtypes = [c_int, _F, _F, c_long, c_long, c_long, _F]
+        l.orc_pq_adc.restype = c_float
+        l.orc_pq_adc.argtypes = [c_int, _F, _U8, c_long, c_long]
+        l.orc_pq_encode.argtypes = [_F, c_long, c_long, _F, c_long, c_long, _U8]
+        l.orc_kmeans_nearest.restype = c_uint32
+        l.orc_kmeans_nearest.argtypes = [_F, _F, c_long, c_long]
+        l.orc_heap_topk.restype = c_long
+        l.orc_heap_topk.argtypes = [_F, _U64, _U8, c_long, c_long, _U64, _F]
+        l.orc_flat_search.restype = c_long
+        l.orc_flat_search.argtypes = [_F, c_long, c_long, c_long, _U8, _F, c_long, c_int, c_void_p, _U64, _F]
+        l.orc_flat_search_bq.restype = c_long
+        l.orc_flat_search_bq.argtypes = [_F, _U64, c_long, c_long, c_long, _U8, _F, c_long, c_long, c_int, _U64, _F,
+                                         _U64]
+        l.orc_synth_value.restype = c_float
+        l.orc_synth_value.argtypes = [c_uint64, c_uint64, c_uint64, c_int]
+        l.orc_synth_rows.argtypes = [c_uint64, c_uint64, c_long, c_long, c_long, c_int, _F]
+        l.orc_dist_all.argtypes = [c_int, _F, _F, c_long, c_long, _F]
+        l.orc_bq_dist_all.argtypes = [_U64, _U64, c_long, c_long, _F]
+        l.orc_bench_flat.restype = c_double
+        l.orc_bench_flat.argtypes = [_F, c_long, c_long, c_long, _F, c_long, c_long, c_int, c_void_p, c_int, _U64, _F]
+        _lib = l
+    return _lib
+
+
+def ref():
+    """The reference's own l2_256/l2_512/dot_256/dot_512 (None if not built)."""
+    global _ref
+    if _ref is None and os.path.exists(REF_SO):
+        _ref = ctypes.CDLL(REF_SO)
+    return _ref
+
+
+def _f(a):
+    return a.ctypes.data_as(_F)
+
+
+def _u64(a):
+    return a.ctypes.data_as(_U64)
+
+
+def _u8(a):
+    return a.ctypes.data_as(_U8)
+
+
+def f32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def l2_256(a, b):
+    a, b = f32(a), f32(b)
+    return np.float32(lib().orc_l2_256(_f(a), _f(b), len(a)))
+
+
+def dot_256(a, b):
+    a, b = f32(a), f32(b)
+    return np.float32(lib().orc_dot_256(_f(a), _f(b), len(a)))
+
+
+def single_dist(metric, a, b):
+    a, b = f32(a), f32(b)
+    return np.float32(lib().orc_single_dist(metric, _f(a), _f(b), len(a)))
+
+
+def step(metric, a, b):
+    a, b = f32(a), f32(b)
+    return np.float32(lib().orc_step(metric, _f(a), _f(b), len(a)))
+
+
+def dist_all(metric, q, rows):
+    """SingleDist(q, row) for all rows (no normalization applied)."""
+    q, rows = f32(q), f32(rows)
+    out = np.empty(rows.shape[0], dtype=np.float32)
+    lib().orc_dist_all(metric, _f(q), _f(rows), rows.shape[0], rows.shape[1], _f(out))
+    return out
+
+
+def bq_dist_all(qcode, codes):
+    qcode = np.ascontiguousarray(qcode, dtype=np.uint64)
+    codes = np.ascontiguousarray(codes, dtype=np.uint64)
+    out = np.empty(codes.shape[0], dtype=np.float32)
+    lib().orc_bq_dist_all(_u64(qcode), _u64(codes), codes.shape[0], codes.shape[1], _f(out))
+    return out
+
+
+def normalize_rows(X):
+    X = f32(X)
+    return np.stack([normalize(r) for r in X]) if len(X) else X.copy()
+
+
+def normalize(v):
+    v = f32(v)
+    out = np.empty_like(v)
+    lib().orc_normalize(_f(v), len(v), _f(out))
+    return out
+
+
+def bq_encode(v):
+    v = f32(v)
+    out = np.empty((len(v) + 63) // 64, dtype=np.uint64)
+    lib().orc_bq_encode(_f(v), len(v), _u64(out))
+    return out
+
+
+def bq_distance(x, y):
+    x = np.ascontiguousarray(x, dtype=np.uint64)
+    y = np.ascontiguousarray(y, dtype=np.uint64)
+    return np.float32(lib().orc_bq_distance(_u64(x), _u64(y), len(x)))
+
+
+def pq_lut(metric, q, centers):
+    q, centers = f32(q), f32(centers)
+    m, ks, ds = centers.shape
+    out = np.empty((m, ks), dtype=np.float32)
+    lib().orc_pq_lut(metric, _f(q), _f(centers), m, ks, ds, _f(out))
+    return out
+
+
+def pq_adc(metric, lut, code):
+    lut = f32(lut)
+    code = np.ascontiguousarray(code, dtype=np.uint8)
+    m, ks = lut.shape
+    return np.float32(lib().orc_pq_adc(metric, _f(lut), _u8(code), m, ks))
+
+
+def pq_encode(X, centers):
+    X, centers = f32(X), f32(centers)
+    n, d = X.shape
+    m, ks, _ = centers.shape
+    out = np.empty((n, m), dtype=np.uint8)
+    lib().orc_pq_encode(_f(X), n, d, _f(centers), m, ks, _u8(out))
+    return out
+
+
+def heap_topk(dists, ids, k, valid=None):
+    dists = f32(dists)
+    ids = np.ascontiguousarray(ids, dtype=np.uint64)
+    oid = np.empty(max(k, 1), dtype=np.uint64)
+    od = np.empty(max(k, 1), dtype=np.float32)
+    v = None if valid is None else np.ascontiguousarray(valid, dtype=np.uint8)
+    n = lib().orc_heap_topk(_f(dists), _u64(ids), _u8(v) if v is not None else None, len(dists), k, _u64(oid),
+                            _f(od))
+    return oid[:n], od[:n]
+
+
+def flat_search(rows, q, k, metric, valid=None, use_ref_kernel=False):
+    """flat.searchByVector restated over a dense matrix; q must be normalized for cosine."""
+    rows, q = f32(rows), f32(q)
+    n, d = rows.shape
+    oid = np.empty(max(k, 1), dtype=np.uint64)
+    od = np.empty(max(k, 1), dtype=np.float32)
+    fn = None
+    if use_ref_kernel:
+        r = ref()
+        sym = "l2_256" if metric == L2 else "dot_256"
+        fn = ctypes.cast(getattr(r, sym), c_void_p)
+    v = None if valid is None else np.ascontiguousarray(valid, dtype=np.uint8)
+    cnt = lib().orc_flat_search(_f(rows), n, d, d, _u8(v) if v is not None else None, _f(q), k, metric, fn, _u64(oid),
+                                _f(od))
+    return oid[:cnt], od[:cnt]
+
+
+def flat_search_bq(rows, q, k, rescore_limit, metric, valid=None):
+    """flat.searchByVectorBQ restated; q must be normalized for cosine."""
+    rows, q = f32(rows), f32(q)
+    n, d = rows.shape
+    codes = np.stack([bq_encode(r) for r in rows]) if n else np.zeros((0, (d + 63) // 64), np.uint64)
+    codes = np.ascontiguousarray(codes)
+    R = max(rescore_limit, k)
+    oid = np.empty(max(k, 1), dtype=np.uint64)
+    od = np.empty(max(k, 1), dtype=np.float32)
+    cand = np.empty(max(R, 1), dtype=np.uint64)
+    v = None if valid is None else np.ascontiguousarray(valid, dtype=np.uint8)
+    cnt = lib().orc_flat_search_bq(_f(rows), _u64(codes), n, d, d, _u8(v) if v is not None else None, _f(q), k,
+                                   rescore_limit, metric, _u64(oid), _f(od), _u64(cand))
+    return oid[:cnt], od[:cnt]
+
+
+def synth_rows(seed, row0, n, d, dist=0):
+    out = np.empty((n, d), dtype=np.float32)
+    lib().orc_synth_rows(seed, row0, n, d, d, dist, _f(out))
+    return out
+
+
+def bench_flat(rows, qs, k, metric, threads, use_ref_kernel=True):
+    """Times nq flat searches, one query per thread at a time; returns seconds."""
+    rows, qs = f32(rows), f32(qs)
+    n, d = rows.shape
+    nq = qs.shape[0]
+    fn = None
+    if use_ref_kernel and ref() is not None:
+        fn = ctypes.cast(getattr(ref(), "l2_256" if metric == L2 else "dot_256"), c_void_p)
+    oid = np.empty((nq, k), dtype=np.uint64)
+    od = np.empty((nq, k), dtype=np.float32)
+    secs = lib().orc_bench_flat(_f(rows), n, d, d, _f(qs), nq, k, metric, fn, threads, _u64(oid), _f(od))
+    return secs, oid, od, fn is not None
+
+
+def ord_key(dists):
+    """Order-preserving u32 of float32 distances (weaviate_amd/csrc/wvg_common.hpp
+    wvg_ord_f32): NaN -> +NaN (after +Inf); -0 sorts before +0."""
+    u = f32(dists).view(np.uint32).copy()
+    nan = ((u & 0x7F800000) == 0x7F800000) & ((u & 0x007FFFFF) != 0)
+    u[nan] = 0x7FC00000
+    neg = (u & 0x80000000) != 0
+    return np.where(neg, ~u, u | np.uint32(0x80000000)).astype(np.uint32)
+
+
+def lex_topk(dists, ids, k):
+    """Lexicographic (dist, id) top-k -- the GPU's documented tie rule."""
+    dists = f32(dists)
+    ids = np.asarray(ids, dtype=np.uint64)
+    order = np.lexsort((ids, ord_key(dists)))[:k]
+    return ids[order], dists[order]

@@ -1,0 +1,149 @@
+"""CPU tests: the oracle (CPU restatement) pinned against the reference's own
+outputs -- the golden vectors produced by the reference's C kernels and the
+hand-vector known answers of the reference's Go tests."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _bits(x):
+    return np.asarray(x, dtype=np.float32).view(np.uint32)
+
+
+@pytest.fixture(scope="module")
+def golden():
+    return np.load(os.path.join(GOLDEN, "distances.npz"))
+
+
+@pytest.fixture(scope="module")
+def known():
+    with open(os.path.join(GOLDEN, "known_answers.json")) as f:
+        return json.load(f)
+
+
+def _pairs(g):
+    off = 0
+    for i, n in enumerate(g["lens"]):
+        yield i, g["a"][off:off + n], g["b"][off:off + n]
+        off += n
+
+
+@pytest.mark.parametrize("fn,key", [("orc_l2_256", "l2_256"), ("orc_dot_256", "dot_256"),
+                                    ("orc_l2_512", "l2_512"), ("orc_dot_512", "dot_512")])
+def test_oracle_matches_reference_kernels_bitwise(orc, golden, fn, key):
+    """D/c/{l2,dot}_avx{256,512}_amd64.c outputs, all lengths 1..1536."""
+    f = getattr(orc.lib(), fn)
+    got, want = [], golden[key]
+    for i, a, b in _pairs(golden):
+        got.append(f(orc._f(np.ascontiguousarray(a)), orc._f(np.ascontiguousarray(b)), len(a)))
+    assert np.array_equal(_bits(got), _bits(want))
+
+
+def test_l2_known_answers(orc, known):
+    for c in known["l2"]:
+        assert orc.single_dist(orc.L2, c["a"], c["b"]) == np.float32(c["expected"])
+        # Step-by-step equals SingleDist (D/l2_test.go:68-88)
+        s = np.float32(0)
+        for x, y in zip(c["a"], c["b"]):
+            s = np.float32(s + orc.step(orc.L2, [x], [y]))
+        assert s == np.float32(c["expected"])
+
+
+def test_dot_known_answers(orc, known):
+    for c in known["dot"]:
+        assert orc.single_dist(orc.DOT, c["a"], c["b"]) == np.float32(c["expected"])
+
+
+def test_cosine_known_answers(orc, known):
+    for c in known["cosine"]:
+        a, b = orc.normalize(c["a"]), orc.normalize(c["b"])
+        d = orc.single_dist(orc.COSINE, a, b)
+        if c["tol"] == 0.0:
+            assert abs(float(d) - c["expected"]) <= 1e-6
+        else:
+            assert abs(float(d) - c["expected"]) <= c["tol"]
+
+
+def test_normalize_zero_vector(orc):
+    assert np.all(orc.normalize(np.zeros(7)) == 0)
+
+
+def test_bq_known_answers(orc, known):
+    kp = known["bq_pairs"][0]
+    codes = [orc.bq_encode(v) for v in kp["vecs"]]
+    for i, j, want in kp["pairs"]:
+        assert orc.bq_distance(codes[i], codes[j]) == np.float32(want)
+    kq = known["bq_query"]
+    qc = orc.bq_encode(kq["query"])
+    for v, want in zip(kq["vecs"], kq["hamming"]):
+        assert orc.bq_distance(orc.bq_encode(v), qc) == np.float32(want)
+    # DistanceToFloat with the raw query: cosine SingleDist = 1 - dot (CH/quantizer.go:109-115)
+    assert orc.single_dist(orc.COSINE, kq["query"], kq["float_vec"]) == np.float32(kq["distance_to_float"])
+    kf = known["bq_from_id"]
+    base = orc.bq_encode(kf["vecs"][kf["from"]])
+    for v, want in zip(kf["vecs"], kf["hamming"]):
+        assert orc.bq_distance(base, orc.bq_encode(v)) == np.float32(want)
+    assert orc.bq_distance(base, orc.bq_encode(kf["float_vec"])) == np.float32(kf["distance_to_float"])
+
+
+def test_bq_encode_bit_layout(orc):
+    v = np.ones(130, dtype=np.float32)
+    v[[0, 63, 64, 129]] = -1.0
+    v[5] = -0.0  # -0 is not < 0
+    code = orc.bq_encode(v)
+    assert code.tolist() == [1 | (1 << 63), 1, 2]
+
+
+def test_pq_lut_adc_and_encode_tie_rule(orc):
+    rng = np.random.default_rng(3)
+    m, ks, ds = 4, 16, 3
+    centers = rng.integers(-3, 4, (m, ks, ds)).astype(np.float32)
+    centers[:, 7] = centers[:, 2]  # duplicate centroid: ties must go to the higher index (kmeans.go:122-132)
+    X = centers[np.arange(m)[None, :], rng.integers(0, ks, (50, m))].reshape(50, m * ds)
+    codes = orc.pq_encode(X, centers)
+    for s in range(m):
+        assert not np.any(codes[:, s] == 2), "tie must resolve to the later centroid 7"
+    q = rng.uniform(-1, 1, m * ds).astype(np.float32)
+    lut = orc.pq_lut(orc.L2, q, centers)
+    code = codes[0]
+    s = np.float32(0)
+    for i in range(m):
+        s = np.float32(s + lut[i, code[i]])
+    assert orc.pq_adc(orc.L2, lut, code) == s
+
+
+def test_heap_topk_matches_lexicographic_modulo_ties(orc):
+    rng = np.random.default_rng(7)
+    d = rng.integers(0, 20, 2000).astype(np.float32)  # many ties
+    ids = np.arange(2000, dtype=np.uint64)
+    hi, hd = orc.heap_topk(d, ids, 37)
+    li, ld = orc.lex_topk(d, ids, 37)
+    assert np.array_equal(hd, ld)  # distances identical
+    cut = ld[-1]
+    assert set(hi[hd < cut].tolist()) == set(li[ld < cut].tolist())  # ids identical below the boundary tie
+
+
+def test_synthetic_generator_is_stable(orc):
+    # pinned values of the counter-based generator (shared with the device kernel)
+    r = orc.synth_rows(42, 0, 2, 4, 0)
+    assert r.dtype == np.float32 and np.all(r >= -1) and np.all(r < 1)
+    r2 = orc.synth_rows(42, 1, 1, 4, 0)
+    assert np.array_equal(r[1], r2[0])
+    ints = orc.synth_rows(42, 0, 100, 8, 1)
+    assert np.all(ints == np.floor(ints)) and ints.max() <= 255 and ints.min() >= 0
+
+
+def test_flat_search_oracle_with_reference_kernel(orc):
+    """The oracle's flat search gives the same results whether it calls its own
+    restated l2_256 or the reference's compiled l2_256 (when available)."""
+    if orc.ref() is None:
+        pytest.skip("oracle/_ref not built here")
+    rows = orc.synth_rows(5, 0, 3000, 128, 0)
+    q = orc.synth_rows(6, 0, 1, 128, 0)[0]
+    a = orc.flat_search(rows, q, 10, orc.L2)
+    b = orc.flat_search(rows, q, 10, orc.L2, use_ref_kernel=True)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(_bits(a[1]), _bits(b[1]))

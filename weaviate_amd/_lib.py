@@ -1,0 +1,119 @@
+"""ctypes binding of the C ABI in include/wvgpu.h (weaviate_amd/libwvgpu.so).
+
+The library is built in-tree by ``__graft_entry__.build()`` (make -C
+weaviate_amd/csrc).  There is no CPU fallback: if the shared object is
+missing or cannot be loaded, importing the ops raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_float, c_int, c_size_t, c_uint8, c_uint32, c_uint64, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libwvgpu.so")
+
+WVG_OK = 0
+WVG_ERR_INVALID = -1
+WVG_ERR_DIM_MISMATCH = -2
+WVG_ERR_NOMEM = -3
+WVG_ERR_DEVICE = -4
+WVG_ERR_NOT_FOUND = -5
+WVG_ERR_UNSUPPORTED = -6
+WVG_ERR_CAPACITY = -7
+
+KIND_F32, KIND_BQ, KIND_PQ = 0, 1, 2
+METRIC_L2, METRIC_DOT, METRIC_COSINE = 0, 1, 2
+METRIC_BY_NAME = {"l2-squared": METRIC_L2, "dot": METRIC_DOT, "cosine": METRIC_COSINE,
+                  "cosine-dot": METRIC_COSINE}
+
+# name -> (restype, argtypes); every symbol declared in include/wvgpu.h.
+_P = POINTER
+SIGNATURES = {
+    "wvg_abi_version": (c_int, []),
+    "wvg_last_error": (c_char_p, []),
+    "wvg_device_count": (c_int, [_P(c_int)]),
+    "wvg_open": (c_int, [c_int, _P(c_void_p)]),
+    "wvg_close": (c_int, [c_void_p]),
+    "wvg_synchronize": (c_int, [c_void_p]),
+    "wvg_corpus_create": (c_int, [c_void_p, c_int, c_int, c_uint32, c_uint64, c_uint64, _P(c_void_p)]),
+    "wvg_corpus_destroy": (c_int, [c_void_p]),
+    "wvg_corpus_reserve": (c_int, [c_void_p, c_uint64]),
+    "wvg_corpus_info": (c_int, [c_void_p, _P(c_uint64), _P(c_uint64), _P(c_uint64)]),
+    "wvg_corpus_upsert": (c_int, [c_void_p, _P(c_uint64), _P(c_float), c_uint64, c_uint32]),
+    "wvg_corpus_upsert_codes": (c_int, [c_void_p, _P(c_uint64), c_void_p, c_uint64]),
+    "wvg_corpus_delete": (c_int, [c_void_p, _P(c_uint64), c_uint64]),
+    "wvg_corpus_get": (c_int, [c_void_p, c_uint64, c_void_p]),
+    "wvg_corpus_fill_synthetic": (c_int, [c_void_p, c_uint64, c_uint64, c_int]),
+    "wvg_pq_set_codebook": (c_int, [c_void_p, _P(c_float), c_uint32, c_uint32]),
+    "wvg_search": (c_int, [c_void_p, _P(c_float), c_uint32, c_uint32, _P(c_uint64), c_uint64,
+                           _P(c_uint64), _P(c_float), _P(c_uint32)]),
+    "wvg_search_bq_rescore": (c_int, [c_void_p, c_void_p, _P(c_float), c_uint32, c_uint32, c_uint32,
+                                      _P(c_uint64), c_uint64, _P(c_uint64), _P(c_float), _P(c_uint32)]),
+    "wvg_search_workspace_size": (c_size_t, [c_void_p, c_uint32, c_uint32]),
+    "wvg_search_device": (c_int, [c_void_p, c_void_p, c_uint32, c_uint32, c_void_p, c_void_p, c_void_p,
+                                  c_void_p, c_size_t, c_void_p]),
+    "wvg_topk_merge_device": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_uint32, c_uint32, c_uint32,
+                                      c_void_p, c_void_p, c_void_p, c_void_p]),
+    "wvg_profile_start": (c_int, [c_void_p]),
+    "wvg_profile_stop": (c_int, [c_void_p, _P(ctypes.c_double), _P(c_uint64)]),
+    "wvg_distance_batch": (c_int, [c_void_p, c_int, _P(c_float), _P(c_float), c_uint64, c_uint32, _P(c_float)]),
+    "wvg_normalize_batch": (c_int, [c_void_p, _P(c_float), c_uint64, c_uint32, _P(c_float)]),
+    "wvg_bq_encode": (c_int, [c_void_p, _P(c_float), c_uint64, c_uint32, _P(c_uint64)]),
+    "wvg_bq_distance_batch": (c_int, [c_void_p, _P(c_uint64), _P(c_uint64), c_uint64, c_uint32, _P(c_float)]),
+    "wvg_pq_encode": (c_int, [c_void_p, _P(c_float), c_uint32, c_uint32, _P(c_float), c_uint64, c_uint32,
+                              _P(c_uint8)]),
+    "wvg_pq_lut": (c_int, [c_void_p, c_int, _P(c_float), c_uint32, c_uint32, c_uint32, _P(c_float), _P(c_float)]),
+    "wvg_pq_adc_batch": (c_int, [c_void_p, c_int, _P(c_float), c_uint32, c_uint32, _P(c_uint8), c_uint64,
+                                 _P(c_float)]),
+}
+
+
+class WvgError(RuntimeError):
+    """A negative status from the C ABI, carrying wvg_last_error()."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"wvg error {code}: {msg}")
+        self.code = code
+        self.msg = msg
+
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libwvgpu.so (raises if it was not built: no fallback path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: run __graft_entry__.build() (make -C weaviate_amd/csrc)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int) -> None:
+    if rc != WVG_OK:
+        lib = load()
+        raise WvgError(rc, lib.wvg_last_error().decode(errors="replace"))
+
+
+def fptr(a):
+    return a.ctypes.data_as(POINTER(c_float))
+
+
+def u64ptr(a):
+    return a.ctypes.data_as(POINTER(c_uint64))
+
+
+def u32ptr(a):
+    return a.ctypes.data_as(POINTER(c_uint32))
+
+
+def u8ptr(a):
+    return a.ctypes.data_as(POINTER(c_uint8))

@@ -1,0 +1,98 @@
+"""Mirror of Weaviate's ``compressionhelpers`` BQ / PQ quantizers on the GPU.
+
+Reference:
+  BinaryQuantizer      adapters/repos/db/vector/compressionhelpers/binary_quantization.go:24-56
+  ProductQuantizer     .../compressionhelpers/product_quantization.go:155-442
+  KMeans.Encode        .../compressionhelpers/kmeans.go:103-135
+  quantizer[T]         .../compressionhelpers/quantizer.go:21-31
+
+Codebook *training* (KMeans.Fit) is not on the device yet:
+``ProductQuantizer`` takes trained centers ([m][ks][ds] float32, the layout of
+KMeans.ExposeDataForRestore, kmeans.go:85-93).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+from ._lib import METRIC_BY_NAME, check, fptr, u8ptr, u64ptr
+
+
+class BinaryQuantizer:
+    def __init__(self, ctx, distancer=None):
+        self.ctx = ctx
+        self.distancer = distancer
+
+    def Encode(self, vec) -> np.ndarray:
+        return self.EncodeBatch(np.asarray(vec, dtype=np.float32)[None, :])[0]
+
+    def EncodeBatch(self, X) -> np.ndarray:
+        X = np.ascontiguousarray(X, dtype=np.float32)
+        out = np.empty((X.shape[0], (X.shape[1] + 63) // 64), dtype=np.uint64)
+        check(self.ctx.lib.wvg_bq_encode(self.ctx.handle, fptr(X), X.shape[0], X.shape[1], u64ptr(out)))
+        return out
+
+    def DistanceBetweenCompressedVectors(self, x, y):
+        x = np.ascontiguousarray(x, dtype=np.uint64)
+        y = np.ascontiguousarray(y, dtype=np.uint64)
+        if x.shape[0] != y.shape[0]:
+            return 0.0, "BinaryQuantizer.DistanceBetweenCompressedVectors: Both vectors should have the same len"
+        return float(self.DistanceBatch(x, y[None, :])[0]), None
+
+    def DistanceBatch(self, q, codes) -> np.ndarray:
+        q = np.ascontiguousarray(q, dtype=np.uint64)
+        codes = np.ascontiguousarray(codes, dtype=np.uint64)
+        out = np.empty(codes.shape[0], dtype=np.float32)
+        check(self.ctx.lib.wvg_bq_distance_batch(self.ctx.handle, u64ptr(q), u64ptr(codes), codes.shape[0],
+                                                 q.shape[0], fptr(out)))
+        return out
+
+
+class ProductQuantizer:
+    """k-means PQ with given centers [m][ks][ds]."""
+
+    def __init__(self, ctx, centers, distance: str = "l2-squared"):
+        self.ctx = ctx
+        self.centers = np.ascontiguousarray(centers, dtype=np.float32)
+        self.m, self.ks, self.ds = self.centers.shape
+        self.dimensions = self.m * self.ds
+        self.metric = METRIC_BY_NAME[distance]
+
+    def Encode(self, vec) -> np.ndarray:
+        return self.EncodeBatch(np.asarray(vec, dtype=np.float32)[None, :])[0]
+
+    def EncodeBatch(self, X) -> np.ndarray:
+        X = np.ascontiguousarray(X, dtype=np.float32)
+        out = np.empty((X.shape[0], self.m), dtype=np.uint8)
+        check(self.ctx.lib.wvg_pq_encode(self.ctx.handle, fptr(self.centers), self.m, self.ks, fptr(X), X.shape[0],
+                                         X.shape[1], u8ptr(out)))
+        return out
+
+    def CenterAt(self, q) -> np.ndarray:
+        """DistanceLookUpTable for q, fully materialized ([m][ks])."""
+        q = np.ascontiguousarray(q, dtype=np.float32)
+        out = np.empty((self.m, self.ks), dtype=np.float32)
+        check(self.ctx.lib.wvg_pq_lut(self.ctx.handle, self.metric, fptr(self.centers), self.m, self.ks,
+                                      self.dimensions, fptr(q), fptr(out)))
+        return out
+
+    def NewDistancer(self, q):
+        return PQDistancer(self, np.asarray(q, dtype=np.float32), self.CenterAt(q))
+
+
+class PQDistancer:
+    def __init__(self, pq, x, lut):
+        self.pq, self.x, self.lut = pq, x, lut
+
+    def Distance(self, code):
+        code = np.asarray(code, dtype=np.uint8)
+        if code.shape[0] != self.pq.m:
+            return 0.0, False, "inconsistent compressed vector length"  # product_quantization.go:357-358
+        return float(self.DistanceBatch(code[None, :])[0]), True, None
+
+    def DistanceBatch(self, codes) -> np.ndarray:
+        codes = np.ascontiguousarray(codes, dtype=np.uint8)
+        out = np.empty(codes.shape[0], dtype=np.float32)
+        check(self.pq.ctx.lib.wvg_pq_adc_batch(self.pq.ctx.handle, self.pq.metric, fptr(self.lut), self.pq.m,
+                                               self.pq.ks, u8ptr(codes), codes.shape[0], fptr(out)))
+        return out

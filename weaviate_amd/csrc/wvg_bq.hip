@@ -1,0 +1,223 @@
+// wvg_bq.hip -- binary quantization on MI355X.
+//
+// K4 encode: BinaryQuantizer.Encode (CH/binary_quantization.go:32-45): bit j%64
+//   of word j/64 is set iff v[j] < 0 (of the normalized vector for cosine,
+//   V/flat/index.go:258,262-263).
+// K5 scan:   DistanceBetweenCompressedVectors (CH/binary_quantization.go:47-56)
+//   = sum of popcount(x ^ q) over words, fused with the wave top-k (the
+//   findTopVectorsCached heap, V/flat/index.go:456-495).  Roofline: HBM,
+//   N * 8 * ceil(d/64) bytes per query.
+// Tiled layout: [tile][pair c][lane][2 x u64] -- one 16-byte load per lane per
+// word pair, 1 KiB per wave-instruction; the query code is wave-uniform.
+#include "wvg_internal.hpp"
+#include "wvg_topk.hpp"
+
+namespace wvg {
+
+constexpr int BQ_WAVES = 4;
+
+__device__ __forceinline__ uint64_t bq_tile_mask(const ScanArgs &a, uint64_t t)
+{
+    uint64_t m = a.valid[t];
+    if (a.allow) {
+        uint64_t w = (a.id_base >> 6) + t;
+        m &= w < a.allow_words ? a.allow[w] : 0ull;
+    }
+    return m;
+}
+
+template <int E, int NCH>
+__global__ __launch_bounds__(BQ_WAVES * 64) void scan_bq_kernel(ScanArgs a, uint64_t *partials)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t qi = blockIdx.y;
+    const uint64_t *q = reinterpret_cast<const uint64_t *>(a.queries) + (size_t)qi * a.qpitch;
+    const ulonglong2 *data = reinterpret_cast<const ulonglong2 *>(a.data);
+    const uint32_t nch = NCH > 0 ? (uint32_t)NCH : a.nchunks;
+    const uint64_t ntiles = a.tile_end - a.tile_begin;
+    const uint64_t total = (uint64_t)gridDim.x * BQ_WAVES;
+    const uint64_t gw = (uint64_t)blockIdx.x * BQ_WAVES + wave;
+    const uint64_t t0 = a.tile_begin + ntiles * gw / total, t1 = a.tile_begin + ntiles * (gw + 1) / total;
+    WaveTopK<E> tk;
+    tk.init((int)a.k);
+    for (uint64_t t = t0; t < t1; ++t) {
+        const uint64_t m = bq_tile_mask(a, t);
+        if (m == 0ull) continue;
+        const ulonglong2 *rp = data + (size_t)t * nch * 64 + lane;
+        uint32_t tot = 0;
+        if constexpr (NCH > 0) {
+            ulonglong2 xs[NCH];
+#pragma unroll
+            for (int c = 0; c < NCH; c++) xs[c] = rp[(size_t)c * 64];
+#pragma unroll
+            for (int c = 0; c < NCH; c++)
+                tot += (uint32_t)__popcll(xs[c].x ^ q[2 * c]) + (uint32_t)__popcll(xs[c].y ^ q[2 * c + 1]);
+        } else {
+            for (uint32_t c = 0; c < nch; c++) {
+                const ulonglong2 x = rp[(size_t)c * 64];
+                tot += (uint32_t)__popcll(x.x ^ q[2 * c]) + (uint32_t)__popcll(x.y ^ q[2 * c + 1]);
+            }
+        }
+        const float dist = (float)tot;  // exact: sum of float32(popcount) is an integer < 2^24
+        const uint64_t key = ((m >> lane) & 1ull) ? wvg_make_key(dist, (uint32_t)(t * 64 + lane)) : WVG_KEY_NONE;
+        tk.offer(key);
+    }
+    __shared__ uint64_t sh[BQ_WAVES][64 * E];
+#pragma unroll
+    for (int e = 0; e < E; e++) sh[wave][e * 64 + lane] = tk.l[e];
+    __syncthreads();
+    if (wave != 0) return;
+    for (int w = 1; w < BQ_WAVES; w++) {
+        uint64_t o[E];
+#pragma unroll
+        for (int e = 0; e < E; e++) o[e] = sh[w][e * 64 + lane];
+        merge_lists<E>(tk.l, o);
+    }
+    uint64_t *out = partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k;
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const int i = e * 64 + lane;
+        if (i < (int)a.k) out[i] = tk.l[e];
+    }
+}
+
+template <int E>
+static hipError_t launch_bq_e(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
+{
+    dim3 grid(groups, a.nq), block(BQ_WAVES * 64);
+    switch (a.nchunks) {
+    case 1: hipLaunchKernelGGL((scan_bq_kernel<E, 1>), grid, block, 0, s, a, partials); break;   // d <= 128
+    case 6: hipLaunchKernelGGL((scan_bq_kernel<E, 6>), grid, block, 0, s, a, partials); break;   // d = 768
+    case 12: hipLaunchKernelGGL((scan_bq_kernel<E, 12>), grid, block, 0, s, a, partials); break; // d = 1536
+    default: hipLaunchKernelGGL((scan_bq_kernel<E, 0>), grid, block, 0, s, a, partials); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_scan_bq(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
+{
+    if (a.k <= 64) return launch_bq_e<1>(a, partials, groups, s);
+    if (a.k <= 128) return launch_bq_e<2>(a, partials, groups, s);
+    return launch_bq_e<4>(a, partials, groups, s);
+}
+
+// Encode row-major float rows; `normalize` is applied per row first (cosine).
+// One thread per (row, word).  Rows must already be normalized by the caller
+// when normalize == 0 is passed for cosine corpora.
+__global__ void bq_encode_kernel(const float *rows, uint64_t n, uint32_t dim, uint64_t *codes)
+{
+    const uint32_t w = bq_words(dim);
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n * w) return;
+    const uint64_t i = g / w;
+    const uint32_t word = (uint32_t)(g % w);
+    const float *v = rows + i * dim;
+    uint64_t code = 0;
+    const uint32_t j0 = word * 64, j1 = min(dim, j0 + 64);
+    for (uint32_t j = j0; j < j1; j++)
+        if (v[j] < 0.0f) code |= 1ull << (j & 63);
+    codes[g] = code;
+}
+
+hipError_t launch_bq_encode_rows(const float *rows, uint64_t n, uint32_t dim, int normalize, uint64_t *codes,
+                                 hipStream_t s)
+{
+    (void)normalize;
+    const uint64_t total = n * bq_words(dim);
+    if (total == 0) return hipSuccess;
+    hipLaunchKernelGGL(bq_encode_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, rows, n, dim, codes);
+    return hipGetLastError();
+}
+
+__global__ void bq_store_kernel(const uint64_t *codes, const uint64_t *slots, uint64_t n, uint32_t words,
+                                uint32_t nchunks, ulonglong2 *tiled)
+{
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n * nchunks) return;
+    const uint64_t i = g / nchunks;
+    const uint32_t c = (uint32_t)(g % nchunks);
+    const uint64_t slot = slots ? slots[i] : i;
+    const uint64_t *src = codes + i * words;
+    ulonglong2 v;
+    v.x = 2 * c < words ? src[2 * c] : 0ull;
+    v.y = 2 * c + 1 < words ? src[2 * c + 1] : 0ull;
+    tiled[((slot >> 6) * nchunks + c) * 64 + (slot & 63)] = v;
+}
+
+hipError_t launch_bq_store(const uint64_t *codes, const uint64_t *slots, uint64_t n, uint32_t words,
+                           uint32_t nchunks, uint64_t *tiled, hipStream_t s)
+{
+    const uint64_t total = n * nchunks;
+    if (total == 0) return hipSuccess;
+    hipLaunchKernelGGL(bq_store_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, codes, slots, n,
+                       words, nchunks, reinterpret_cast<ulonglong2 *>(tiled));
+    return hipGetLastError();
+}
+
+// Synthetic BQ rows: encode(normalize?(synth row)) generated in place.
+__global__ void bq_synth_kernel(uint64_t seed_mixed, int dist, uint64_t row0, uint64_t n, uint64_t slot0,
+                                uint32_t dim, uint32_t nchunks, int normalize, ulonglong2 *tiled)
+{
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const uint64_t row = row0 + r, slot = slot0 + r;
+    float norm = 1.0f;
+    bool zero = false;
+    if (normalize) {
+        float acc = 0.0f;
+        for (uint32_t i = 0; i < dim; i++) {
+            float v = wvg_synth_value(seed_mixed, row, i, dist);
+            float p = v * v;
+            acc = acc + p;
+        }
+        zero = acc == 0.0f;
+        norm = (float)__builtin_sqrt((double)acc);
+    }
+    ulonglong2 *dst = tiled + ((slot >> 6) * nchunks) * 64 + (slot & 63);
+    for (uint32_t c = 0; c < nchunks; c++) {
+        uint64_t w2[2] = {0ull, 0ull};
+        for (int h = 0; h < 2; h++) {
+            const uint32_t j0 = (2 * c + h) * 64;
+            for (uint32_t j = j0; j < j0 + 64 && j < dim; j++) {
+                float x = wvg_synth_value(seed_mixed, row, j, dist);
+                if (normalize) x = zero ? 0.0f : x / norm;
+                if (x < 0.0f) w2[h] |= 1ull << (j & 63);
+            }
+        }
+        ulonglong2 v;
+        v.x = w2[0];
+        v.y = w2[1];
+        dst[(size_t)c * 64] = v;
+    }
+}
+
+hipError_t launch_bq_synth(uint64_t seed, int dist, uint64_t row0, uint64_t n, uint64_t slot0, uint32_t dim,
+                           uint32_t nchunks, int normalize, uint64_t *tiled, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(bq_synth_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, wvg_mix64(seed), dist,
+                       row0, n, slot0, dim, nchunks, normalize, reinterpret_cast<ulonglong2 *>(tiled));
+    return hipGetLastError();
+}
+
+__global__ void bq_distance_rows_kernel(const uint64_t *q, const uint64_t *codes, uint64_t n, uint32_t words,
+                                        float *out)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t *x = codes + i * words;
+    float total = 0.0f;
+    for (uint32_t w = 0; w < words; w++) total += (float)__popcll(x[w] ^ q[w]);
+    out[i] = total;
+}
+
+hipError_t launch_bq_distance_rows(const uint64_t *q, const uint64_t *codes, uint64_t n, uint32_t words,
+                                   float *out, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(bq_distance_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, q, codes, n,
+                       words, out);
+    return hipGetLastError();
+}
+
+}  // namespace wvg

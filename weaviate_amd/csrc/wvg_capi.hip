@@ -1,0 +1,1190 @@
+// wvg_capi.hip -- the C ABI (include/wvgpu.h): device context, stream pool,
+// device-resident corpora and the search flows of the flat index.
+//
+// Host-side semantics mirrored from the reference:
+//   flat.Add / AddBatch / Delete          V/flat/index.go:197-295
+//   flat.SearchByVector / searchByVector  V/flat/index.go:307-334
+//   flat.searchByVectorBQ (+ rescore)     V/flat/index.go:347-389
+//   flat.normalized / distancer.Normalize V/flat/index.go:522-529, D/normalize.go:16-32
+//   BinaryQuantizer.Encode                CH/binary_quantization.go:32-45
+//   NewProductQuantizer validation        CH/product_quantization.go:187-197
+// Errors are returned as negative codes with a thread-local message; no HIP
+// failure aborts the process (no panics across cgo).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "wvg_internal.hpp"
+
+namespace wvg {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string &msg) { g_last_error = msg; }
+
+int fail(int code, const std::string &msg)
+{
+    g_last_error = msg;
+    return code;
+}
+
+static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+int StreamSlot::device_scratch(size_t bytes, void **out)
+{
+    if (bytes > dscratch_bytes) {
+        if (dscratch) (void)hipFree(dscratch);
+        dscratch = nullptr;
+        dscratch_bytes = 0;
+        size_t want = std::max(bytes, (size_t)1 << 20);
+        hipError_t e = hipMalloc(&dscratch, want);
+        if (e != hipSuccess) return fail(WVG_ERR_NOMEM, std::string("scratch hipMalloc: ") + hipGetErrorString(e));
+        dscratch_bytes = want;
+    }
+    *out = dscratch;
+    return WVG_OK;
+}
+
+int StreamSlot::host_pinned(size_t bytes, void **out)
+{
+    if (bytes > hpinned_bytes) {
+        if (hpinned) (void)hipHostFree(hpinned);
+        hpinned = nullptr;
+        hpinned_bytes = 0;
+        size_t want = std::max(bytes, (size_t)1 << 16);
+        hipError_t e = hipHostMalloc(&hpinned, want, hipHostMallocDefault);
+        if (e != hipSuccess) return fail(WVG_ERR_NOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+        hpinned_bytes = want;
+    }
+    *out = hpinned;
+    return WVG_OK;
+}
+
+// Carves 256-byte aligned regions out of one scratch allocation.
+struct Carver {
+    size_t off = 0;
+    size_t take(size_t bytes)
+    {
+        size_t o = off;
+        off = align_up(off + bytes, 256);
+        return o;
+    }
+};
+
+size_t corpus_row_bytes(int kind, uint32_t dim, uint32_t pq_m)
+{
+    switch (kind) {
+    case WVG_KIND_F32: return (size_t)f32_chunks(dim) * 16;
+    case WVG_KIND_BQ: return (size_t)bq_chunks(dim) * 16;
+    default: return (size_t)pq_chunks(pq_m) * 16;
+    }
+}
+
+static uint32_t corpus_nchunks(const wvg_corpus *c)
+{
+    switch (c->kind) {
+    case WVG_KIND_F32: return f32_chunks(c->dim);
+    case WVG_KIND_BQ: return bq_chunks(c->dim);
+    default: return pq_chunks(c->pq_m);
+    }
+}
+
+// distancer.Normalize (D/normalize.go:16-32) on the host for queries; this
+// translation unit is compiled with -ffp-contract=off.
+static void normalize_host(const float *v, uint32_t n, float *out)
+{
+    float norm = 0.0f;
+    for (uint32_t i = 0; i < n; i++) {
+        float p = v[i] * v[i];
+        norm = norm + p;
+    }
+    if (norm == 0.0f) {
+        for (uint32_t i = 0; i < n; i++) out[i] = 0.0f;
+        return;
+    }
+    norm = (float)std::sqrt((double)norm);
+    for (uint32_t i = 0; i < n; i++) out[i] = v[i] / norm;
+}
+
+// BinaryQuantizer.Encode (CH/binary_quantization.go:32-45).
+static void bq_encode_host(const float *v, uint32_t d, uint64_t *code, uint32_t words)
+{
+    for (uint32_t i = 0; i < words; i++) code[i] = 0;
+    for (uint32_t j = 0; j < d; j++)
+        if (v[j] < 0.0f) code[j / 64] |= 1ull << (j % 64);
+}
+
+struct SlotGuard {
+    wvg_ctx *ctx;
+    StreamSlot *slot = nullptr;
+    explicit SlotGuard(wvg_ctx *c) : ctx(c) {}
+    ~SlotGuard()
+    {
+        if (slot) ctx->release(slot);
+    }
+};
+
+// Allow bitmap -> tile range [tb, te) of slots that can be allowed; false if empty.
+static bool allow_tile_range(const wvg_corpus *c, const uint64_t *allow, uint64_t allow_words, uint64_t &tb,
+                             uint64_t &te)
+{
+    const uint64_t hw_tiles = tiles_of(c->high_water);
+    tb = 0;
+    te = hw_tiles;
+    if (!allow) return hw_tiles > 0;
+    int64_t first = -1, last = -1;
+    for (uint64_t w = 0; w < allow_words; w++)
+        if (allow[w]) {
+            if (first < 0) first = (int64_t)w;
+            last = (int64_t)w;
+        }
+    if (first < 0) return false;  // allow.IsEmpty() -> nothing (V/flat/index.go:425-427)
+    const uint64_t lo_id = (uint64_t)first * 64 + (uint64_t)__builtin_ctzll(allow[first]);
+    const uint64_t hi_id = (uint64_t)last * 64 + 63 - (uint64_t)__builtin_clzll(allow[last]);
+    if (hi_id < c->id_base) return false;
+    const uint64_t lo_slot = lo_id > c->id_base ? lo_id - c->id_base : 0;
+    const uint64_t hi_slot = hi_id - c->id_base;
+    tb = std::min(lo_slot / 64, hw_tiles);
+    te = std::min(hi_slot / 64 + 1, hw_tiles);
+    return te > tb;
+}
+
+static int check_corpus(wvg_corpus *c)
+{
+    if (!c || !c->ctx) return fail(WVG_ERR_INVALID, "null corpus");
+    WVG_HIP(hipSetDevice(c->ctx->device));
+    return WVG_OK;
+}
+
+// Queries -> the device-side representation the scan of this corpus reads.
+// F32: [nq][qpitch] floats (normalized for cosine).  BQ: [nq][qpitch] words.
+// PQ: raw floats are staged at qf and turned into LUTs by the caller.
+static void prepare_queries_host(const wvg_corpus *c, const float *queries, uint32_t nq, std::vector<float> &qf,
+                                 std::vector<uint64_t> &qb, uint32_t &qpitch)
+{
+    const uint32_t d = c->dim;
+    std::vector<float> tmp(d);
+    if (c->kind == WVG_KIND_BQ) {
+        const uint32_t words = bq_words(d);
+        qpitch = bq_chunks(d) * 2;
+        qb.assign((size_t)nq * qpitch, 0ull);
+        for (uint32_t i = 0; i < nq; i++) {
+            const float *q = queries + (size_t)i * d;
+            if (c->metric == WVG_METRIC_COSINE) {
+                normalize_host(q, d, tmp.data());
+                q = tmp.data();
+            }
+            bq_encode_host(q, d, qb.data() + (size_t)i * qpitch, words);
+        }
+        return;
+    }
+    qpitch = c->kind == WVG_KIND_F32 ? f32_chunks(d) * 4 : d;
+    qf.assign((size_t)nq * qpitch, 0.0f);
+    for (uint32_t i = 0; i < nq; i++) {
+        const float *q = queries + (size_t)i * d;
+        float *dst = qf.data() + (size_t)i * qpitch;
+        if (c->metric == WVG_METRIC_COSINE)
+            normalize_host(q, d, dst);
+        else
+            std::memcpy(dst, q, sizeof(float) * d);
+    }
+}
+
+static hipError_t launch_scan(const ScanArgs &a, int kind, uint64_t *partials, int groups, hipStream_t s)
+{
+    switch (kind) {
+    case WVG_KIND_F32: return launch_scan_f32(a, partials, groups, s);
+    case WVG_KIND_BQ: return launch_scan_bq(a, partials, groups, s);
+    default: return launch_scan_pq(a, partials, groups, s);
+    }
+}
+
+static const uint32_t MAX_K = 256;
+
+}  // namespace wvg
+
+using namespace wvg;
+
+// ---------------------------------------------------------------------------
+int wvg_ctx::acquire(StreamSlot **out)
+{
+    {
+        std::lock_guard<std::mutex> g(pool_mu);
+        if (!free_slots.empty()) {
+            *out = free_slots.back();
+            free_slots.pop_back();
+            return WVG_OK;
+        }
+    }
+    StreamSlot *s = new StreamSlot();
+    hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete s;
+        return fail(WVG_ERR_DEVICE, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+    }
+    std::lock_guard<std::mutex> g(pool_mu);
+    all_slots.push_back(s);
+    *out = s;
+    return WVG_OK;
+}
+
+void wvg_ctx::release(StreamSlot *s)
+{
+    std::lock_guard<std::mutex> g(pool_mu);
+    free_slots.push_back(s);
+}
+
+extern "C" {
+
+int wvg_abi_version(void) { return WVG_ABI_VERSION; }
+
+const char *wvg_last_error(void) { return g_last_error.c_str(); }
+
+int wvg_device_count(int *out)
+{
+    if (!out) return fail(WVG_ERR_INVALID, "null out");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        *out = 0;
+        return fail(WVG_ERR_DEVICE, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+    }
+    *out = n;
+    return WVG_OK;
+}
+
+int wvg_open(int device, wvg_ctx **out)
+{
+    if (!out) return fail(WVG_ERR_INVALID, "null out");
+    *out = nullptr;
+    int n = 0;
+    WVG_HIP(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) return fail(WVG_ERR_INVALID, "device index out of range");
+    WVG_HIP(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    WVG_HIP(hipGetDeviceProperties(&prop, device));
+    wvg_ctx *c = new wvg_ctx();
+    c->device = device;
+    c->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    *out = c;
+    return WVG_OK;
+}
+
+int wvg_close(wvg_ctx *ctx)
+{
+    if (!ctx) return WVG_OK;
+    (void)hipSetDevice(ctx->device);
+    for (auto &e : ctx->prof_events) {
+        (void)hipEventDestroy(e.first);
+        (void)hipEventDestroy(e.second);
+    }
+    for (StreamSlot *s : ctx->all_slots) {
+        (void)hipStreamSynchronize(s->stream);
+        if (s->dscratch) (void)hipFree(s->dscratch);
+        if (s->hpinned) (void)hipHostFree(s->hpinned);
+        (void)hipStreamDestroy(s->stream);
+        delete s;
+    }
+    delete ctx;
+    return WVG_OK;
+}
+
+int wvg_synchronize(wvg_ctx *ctx)
+{
+    if (!ctx) return fail(WVG_ERR_INVALID, "null ctx");
+    WVG_HIP(hipSetDevice(ctx->device));
+    WVG_HIP(hipDeviceSynchronize());
+    return WVG_OK;
+}
+
+// ---------------------------------------------------------------------------
+static int corpus_alloc(wvg_corpus *c, uint64_t capacity)
+{
+    const uint64_t tiles = tiles_of(capacity);
+    const size_t row_bytes = corpus_row_bytes(c->kind, c->dim, c->pq_m);
+    void *data = nullptr;
+    uint64_t *valid = nullptr;
+    if (tiles > 0) {
+        if (row_bytes > 0) {
+            hipError_t e = hipMalloc(&data, tiles * 64 * row_bytes);
+            if (e != hipSuccess) return fail(WVG_ERR_NOMEM, std::string("corpus hipMalloc: ") + hipGetErrorString(e));
+            e = hipMemset(data, 0, tiles * 64 * row_bytes);
+            if (e != hipSuccess) {
+                (void)hipFree(data);
+                return fail(WVG_ERR_DEVICE, std::string("corpus hipMemset: ") + hipGetErrorString(e));
+            }
+        }
+        hipError_t e = hipMalloc(&valid, tiles * 8);
+        if (e != hipSuccess) {
+            if (data) (void)hipFree(data);
+            return fail(WVG_ERR_NOMEM, std::string("validity hipMalloc: ") + hipGetErrorString(e));
+        }
+        (void)hipMemset(valid, 0, tiles * 8);
+    }
+    const uint64_t old_tiles = tiles_of(c->capacity);
+    if (c->d_data && data && old_tiles > 0) {
+        WVG_HIP(hipMemcpy(data, c->d_data, std::min(old_tiles, tiles) * 64 * row_bytes, hipMemcpyDeviceToDevice));
+    }
+    if (c->d_valid && valid && old_tiles > 0) {
+        WVG_HIP(hipMemcpy(valid, c->d_valid, std::min(old_tiles, tiles) * 8, hipMemcpyDeviceToDevice));
+    }
+    if (c->d_data) (void)hipFree(c->d_data);
+    if (c->d_valid) (void)hipFree(c->d_valid);
+    c->d_data = data;
+    c->d_valid = valid;
+    c->capacity = tiles * 64;
+    c->h_valid.resize(tiles, 0ull);
+    return WVG_OK;
+}
+
+int wvg_corpus_create(wvg_ctx *ctx, int kind, int metric, uint32_t dim, uint64_t id_base, uint64_t capacity,
+                      wvg_corpus **out)
+{
+    if (!ctx || !out) return fail(WVG_ERR_INVALID, "null ctx/out");
+    *out = nullptr;
+    if (kind < WVG_KIND_F32 || kind > WVG_KIND_PQ) return fail(WVG_ERR_INVALID, "unknown corpus kind");
+    if (metric < WVG_METRIC_L2 || metric > WVG_METRIC_COSINE) return fail(WVG_ERR_INVALID, "unknown metric");
+    if (dim == 0) return fail(WVG_ERR_INVALID, "dim must be > 0");
+    if (id_base % 64 != 0) return fail(WVG_ERR_INVALID, "id_base must be a multiple of 64");
+    if (capacity > (1ull << 32)) return fail(WVG_ERR_INVALID, "capacity above 2^32 rows per corpus");
+    WVG_HIP(hipSetDevice(ctx->device));
+    wvg_corpus *c = new wvg_corpus();
+    c->ctx = ctx;
+    c->kind = kind;
+    c->metric = metric;
+    c->dim = dim;
+    c->id_base = id_base;
+    c->nchunks = kind == WVG_KIND_PQ ? 0 : corpus_nchunks(c);
+    int rc = corpus_alloc(c, capacity);
+    if (rc != WVG_OK) {
+        delete c;
+        return rc;
+    }
+    *out = c;
+    return WVG_OK;
+}
+
+int wvg_corpus_destroy(wvg_corpus *c)
+{
+    if (!c) return WVG_OK;
+    (void)hipSetDevice(c->ctx->device);
+    if (c->d_data) (void)hipFree(c->d_data);
+    if (c->d_valid) (void)hipFree(c->d_valid);
+    if (c->d_centers) (void)hipFree(c->d_centers);
+    delete c;
+    return WVG_OK;
+}
+
+int wvg_corpus_reserve(wvg_corpus *c, uint64_t capacity)
+{
+    int rc = check_corpus(c);
+    if (rc) return rc;
+    std::unique_lock<std::shared_mutex> lk(c->rw);
+    if (capacity <= c->capacity) return WVG_OK;
+    if (capacity > (1ull << 32)) return fail(WVG_ERR_INVALID, "capacity above 2^32 rows per corpus");
+    return corpus_alloc(c, capacity);
+}
+
+int wvg_corpus_info(wvg_corpus *c, uint64_t *count, uint64_t *high_water, uint64_t *capacity)
+{
+    if (!c) return fail(WVG_ERR_INVALID, "null corpus");
+    std::shared_lock<std::shared_mutex> lk(c->rw);
+    if (count) *count = c->count;
+    if (high_water) *high_water = c->high_water;
+    if (capacity) *capacity = c->capacity;
+    return WVG_OK;
+}
+
+// Maps ids to slots, dedups (last occurrence wins, as sequential flat.Add
+// calls would) and updates the host validity mirror.  Returns the row
+// indices to store, in input order.
+static int map_slots(wvg_corpus *c, const uint64_t *ids, uint64_t n, std::vector<uint64_t> &rows,
+                     std::vector<uint64_t> &slots)
+{
+    std::vector<std::pair<uint64_t, uint64_t>> v;
+    v.reserve(n);
+    for (uint64_t i = 0; i < n; i++) {
+        if (ids[i] < c->id_base || ids[i] - c->id_base >= c->capacity)
+            return fail(WVG_ERR_CAPACITY, "id " + std::to_string(ids[i]) + " outside corpus [" +
+                                              std::to_string(c->id_base) + ", " +
+                                              std::to_string(c->id_base + c->capacity) + ")");
+        v.emplace_back(ids[i] - c->id_base, i);
+    }
+    std::stable_sort(v.begin(), v.end(), [](auto &a, auto &b) { return a.first < b.first; });
+    rows.clear();
+    slots.clear();
+    for (size_t j = 0; j < v.size(); j++) {
+        if (j + 1 < v.size() && v[j + 1].first == v[j].first) continue;  // a later duplicate wins
+        rows.push_back(v[j].second);
+        slots.push_back(v[j].first);
+    }
+    return WVG_OK;
+}
+
+static void mark_valid_host(wvg_corpus *c, const std::vector<uint64_t> &slots)
+{
+    for (uint64_t s : slots) {
+        uint64_t &w = c->h_valid[s >> 6];
+        const uint64_t bit = 1ull << (s & 63);
+        if (!(w & bit)) {
+            w |= bit;
+            c->count++;
+        }
+        c->high_water = std::max(c->high_water, s + 1);
+    }
+}
+
+// Stores `nr` rows (host floats, gathered by rows[]) into the corpus.
+static int store_rows(wvg_corpus *c, StreamSlot *sl, const float *vectors, const std::vector<uint64_t> &rows,
+                      const std::vector<uint64_t> &slots, uint64_t r0, uint64_t r1)
+{
+    const uint64_t nr = r1 - r0;
+    const uint32_t d = c->dim;
+    hipStream_t s = sl->stream;
+    Carver cv;
+    const size_t o_rows = cv.take(nr * d * 4);
+    const size_t o_norm = cv.take(nr * d * 4);
+    const size_t o_slots = cv.take(nr * 8);
+    const size_t o_codes = cv.take(nr * std::max<size_t>(bq_words(d) * 8, c->pq_m));
+    const size_t o_tile = cv.take(tiles_of(nr) * 64 * (size_t)f32_chunks(d) * 16);
+    void *base = nullptr;
+    int rc = sl->device_scratch(cv.off, &base);
+    if (rc) return rc;
+    char *b = (char *)base;
+    float *d_rows = (float *)(b + o_rows);
+    float *d_norm = (float *)(b + o_norm);
+    uint64_t *d_slots = (uint64_t *)(b + o_slots);
+    // gather the selected host rows into pinned staging
+    void *pin = nullptr;
+    rc = sl->host_pinned(nr * d * 4 + nr * 8, &pin);
+    if (rc) return rc;
+    float *hrows = (float *)pin;
+    uint64_t *hslots = (uint64_t *)((char *)pin + nr * d * 4);
+    for (uint64_t i = 0; i < nr; i++) {
+        std::memcpy(hrows + i * d, vectors + rows[r0 + i] * d, (size_t)d * 4);
+        hslots[i] = slots[r0 + i];
+    }
+    WVG_HIP(hipMemcpyAsync(d_rows, hrows, nr * d * 4, hipMemcpyHostToDevice, s));
+    WVG_HIP(hipMemcpyAsync(d_slots, hslots, nr * 8, hipMemcpyHostToDevice, s));
+    const float *src = d_rows;
+    if (c->metric == WVG_METRIC_COSINE) {  // flat.Add normalizes (V/flat/index.go:258)
+        WVG_HIP(launch_normalize_rows(d_rows, nr, d, d_norm, s));
+        src = d_norm;
+    }
+    switch (c->kind) {
+    case WVG_KIND_F32:
+        WVG_HIP(launch_f32_store(src, d_slots, nr, d, c->nchunks, 0, (float *)c->d_data, s));
+        break;
+    case WVG_KIND_BQ: {
+        uint64_t *codes = (uint64_t *)(b + o_codes);
+        WVG_HIP(launch_bq_encode_rows(src, nr, d, 0, codes, s));
+        WVG_HIP(launch_bq_store(codes, d_slots, nr, bq_words(d), c->nchunks, (uint64_t *)c->d_data, s));
+        break;
+    }
+    default: {
+        uint8_t *codes = (uint8_t *)(b + o_codes);
+        float *tile = (float *)(b + o_tile);
+        WVG_HIP(launch_f32_store(src, nullptr, nr, d, f32_chunks(d), 0, tile, s));
+        WVG_HIP(launch_pq_encode(tile, nr, d, c->d_centers, c->pq_m, c->pq_ks, codes, s));
+        WVG_HIP(launch_pq_store(codes, d_slots, nr, c->pq_m, c->nchunks, (uint8_t *)c->d_data, s));
+        break;
+    }
+    }
+    WVG_HIP(launch_set_valid(c->d_valid, d_slots, nr, 1, s));
+    WVG_HIP(hipStreamSynchronize(s));
+    return WVG_OK;
+}
+
+static const uint64_t UPSERT_BATCH = 1u << 18;
+
+int wvg_corpus_upsert(wvg_corpus *c, const uint64_t *ids, const float *vectors, uint64_t n, uint32_t dim)
+{
+    int rc = check_corpus(c);
+    if (rc) return rc;
+    if (n == 0) return WVG_OK;
+    if (!ids || !vectors) return fail(WVG_ERR_INVALID, "null ids/vectors");
+    if (dim != c->dim) return fail(WVG_ERR_DIM_MISMATCH, "insert called with a vector of the wrong size");
+    if (c->kind == WVG_KIND_PQ && !c->d_centers) return fail(WVG_ERR_INVALID, "PQ corpus has no codebook");
+    std::unique_lock<std::shared_mutex> lk(c->rw);
+    std::vector<uint64_t> rows, slots;
+    rc = map_slots(c, ids, n, rows, slots);
+    if (rc) return rc;
+    SlotGuard g(c->ctx);
+    rc = c->ctx->acquire(&g.slot);
+    if (rc) return rc;
+    for (uint64_t r0 = 0; r0 < rows.size(); r0 += UPSERT_BATCH) {
+        const uint64_t r1 = std::min<uint64_t>(rows.size(), r0 + UPSERT_BATCH);
+        rc = store_rows(c, g.slot, vectors, rows, slots, r0, r1);
+        if (rc) return rc;
+    }
+    mark_valid_host(c, slots);
+    return WVG_OK;
+}
+
+int wvg_corpus_upsert_codes(wvg_corpus *c, const uint64_t *ids, const void *codes, uint64_t n)
+{
+    int rc = check_corpus(c);
+    if (rc) return rc;
+    if (n == 0) return WVG_OK;
+    if (!ids || !codes) return fail(WVG_ERR_INVALID, "null ids/codes");
+    if (c->kind == WVG_KIND_F32) return fail(WVG_ERR_UNSUPPORTED, "upsert_codes needs a BQ or PQ corpus");
+    if (c->kind == WVG_KIND_PQ && !c->d_centers) return fail(WVG_ERR_INVALID, "PQ corpus has no codebook");
+    std::unique_lock<std::shared_mutex> lk(c->rw);
+    std::vector<uint64_t> rows, slots;
+    rc = map_slots(c, ids, n, rows, slots);
+    if (rc) return rc;
+    SlotGuard g(c->ctx);
+    rc = c->ctx->acquire(&g.slot);
+    if (rc) return rc;
+    const size_t rb = c->kind == WVG_KIND_BQ ? (size_t)bq_words(c->dim) * 8 : c->pq_m;
+    const uint64_t nr = rows.size();
+    Carver cv;
+    const size_t o_codes = cv.take(nr * rb), o_slots = cv.take(nr * 8);
+    void *base = nullptr;
+    rc = g.slot->device_scratch(cv.off, &base);
+    if (rc) return rc;
+    std::vector<unsigned char> hc(nr * rb);
+    for (uint64_t i = 0; i < nr; i++) std::memcpy(hc.data() + i * rb, (const char *)codes + rows[i] * rb, rb);
+    hipStream_t s = g.slot->stream;
+    char *b = (char *)base;
+    WVG_HIP(hipMemcpyAsync(b + o_codes, hc.data(), nr * rb, hipMemcpyHostToDevice, s));
+    WVG_HIP(hipMemcpyAsync(b + o_slots, slots.data(), nr * 8, hipMemcpyHostToDevice, s));
+    if (c->kind == WVG_KIND_BQ)
+        WVG_HIP(launch_bq_store((uint64_t *)(b + o_codes), (uint64_t *)(b + o_slots), nr, bq_words(c->dim), c->nchunks,
+                                (uint64_t *)c->d_data, s));
+    else
+        WVG_HIP(launch_pq_store((uint8_t *)(b + o_codes), (uint64_t *)(b + o_slots), nr, c->pq_m, c->nchunks,
+                                (uint8_t *)c->d_data, s));
+    WVG_HIP(launch_set_valid(c->d_valid, (uint64_t *)(b + o_slots), nr, 1, s));
+    WVG_HIP(hipStreamSynchronize(s));
+    mark_valid_host(c, slots);
+    return WVG_OK;
+}
+
+int wvg_corpus_delete(wvg_corpus *c, const uint64_t *ids, uint64_t n)
+{
+    int rc = check_corpus(c);
+    if (rc) return rc;
+    if (n == 0) return WVG_OK;
+    if (!ids) return fail(WVG_ERR_INVALID, "null ids");
+    std::unique_lock<std::shared_mutex> lk(c->rw);
+    std::vector<uint64_t> slots;
+    for (uint64_t i = 0; i < n; i++) {
+        if (ids[i] < c->id_base || ids[i] - c->id_base >= c->capacity) continue;  // absent: no-op like an LSM delete
+        const uint64_t s = ids[i] - c->id_base;
+        uint64_t &w = c->h_valid[s >> 6];
+        const uint64_t bit = 1ull << (s & 63);
+        if (w & bit) {
+            w &= ~bit;
+            c->count--;
+        }
+        slots.push_back(s);
+    }
+    if (slots.empty()) return WVG_OK;
+    SlotGuard g(c->ctx);
+    rc = c->ctx->acquire(&g.slot);
+    if (rc) return rc;
+    void *base = nullptr;
+    rc = g.slot->device_scratch(slots.size() * 8, &base);
+    if (rc) return rc;
+    WVG_HIP(hipMemcpyAsync(base, slots.data(), slots.size() * 8, hipMemcpyHostToDevice, g.slot->stream));
+    WVG_HIP(launch_set_valid(c->d_valid, (uint64_t *)base, slots.size(), 0, g.slot->stream));
+    WVG_HIP(hipStreamSynchronize(g.slot->stream));
+    return WVG_OK;
+}
+
+int wvg_corpus_get(wvg_corpus *c, uint64_t id, void *out)
+{
+    int rc = check_corpus(c);
+    if (rc) return rc;
+    if (!out) return fail(WVG_ERR_INVALID, "null out");
+    std::shared_lock<std::shared_mutex> lk(c->rw);
+    if (id < c->id_base || id - c->id_base >= c->capacity) return fail(WVG_ERR_NOT_FOUND, "id not found");
+    const uint64_t s = id - c->id_base;
+    if (!((c->h_valid[s >> 6] >> (s & 63)) & 1ull)) return fail(WVG_ERR_NOT_FOUND, "id not found");
+    const uint32_t nch = c->nchunks;
+    std::vector<unsigned char> buf((size_t)nch * 16);
+    const unsigned char *tile = (const unsigned char *)c->d_data + (s >> 6) * (size_t)nch * 64 * 16;
+    WVG_HIP(hipMemcpy2D(buf.data(), 16, tile + (s & 63) * 16, 64 * 16, 16, nch, hipMemcpyDeviceToHost));
+    size_t bytes = c->kind == WVG_KIND_F32 ? (size_t)c->dim * 4
+                   : c->kind == WVG_KIND_BQ ? (size_t)bq_words(c->dim) * 8
+                                            : (size_t)c->pq_m;
+    std::memcpy(out, buf.data(), bytes);
+    return WVG_OK;
+}
+
+int wvg_corpus_fill_synthetic(wvg_corpus *c, uint64_t seed, uint64_t n, int distribution)
+{
+    int rc = check_corpus(c);
+    if (rc) return rc;
+    if (c->kind == WVG_KIND_PQ) return fail(WVG_ERR_UNSUPPORTED, "synthetic fill supports F32 and BQ corpora");
+    if (distribution < 0 || distribution > 1) return fail(WVG_ERR_INVALID, "distribution must be 0 or 1");
+    std::unique_lock<std::shared_mutex> lk(c->rw);
+    if (n > c->capacity) return fail(WVG_ERR_CAPACITY, "n exceeds corpus capacity");
+    SlotGuard g(c->ctx);
+    rc = c->ctx->acquire(&g.slot);
+    if (rc) return rc;
+    hipStream_t s = g.slot->stream;
+    const int norm = c->metric == WVG_METRIC_COSINE;
+    const uint64_t step = 1ull << 24;
+    for (uint64_t r0 = 0; r0 < n; r0 += step) {
+        const uint64_t nr = std::min(step, n - r0);
+        if (c->kind == WVG_KIND_F32)
+            WVG_HIP(launch_f32_synth(seed, distribution, c->id_base + r0, nr, r0, c->dim, c->nchunks, norm,
+                                     (float *)c->d_data, s));
+        else
+            WVG_HIP(launch_bq_synth(seed, distribution, c->id_base + r0, nr, r0, c->dim, c->nchunks, norm,
+                                    (uint64_t *)c->d_data, s));
+    }
+    // validity: full words for [0, n)
+    std::vector<uint64_t> &hv = c->h_valid;
+    for (uint64_t t = 0; t < tiles_of(n); t++) {
+        const uint64_t lo = t * 64, hi = std::min(n, lo + 64);
+        const uint64_t word = hi - lo == 64 ? ~0ull : ((1ull << (hi - lo)) - 1);
+        c->count += (uint64_t)__builtin_popcountll(word & ~hv[t]);
+        hv[t] |= word;
+    }
+    c->high_water = std::max(c->high_water, n);
+    WVG_HIP(hipMemcpyAsync(c->d_valid, hv.data(), tiles_of(n) * 8, hipMemcpyHostToDevice, s));
+    WVG_HIP(hipStreamSynchronize(s));
+    return WVG_OK;
+}
+
+int wvg_pq_set_codebook(wvg_corpus *c, const float *centers, uint32_t m, uint32_t ks)
+{
+    int rc = check_corpus(c);
+    if (rc) return rc;
+    if (c->kind != WVG_KIND_PQ) return fail(WVG_ERR_INVALID, "not a PQ corpus");
+    if (!centers) return fail(WVG_ERR_INVALID, "null centers");
+    // NewProductQuantizer (CH/product_quantization.go:187-197)
+    if (m == 0) return fail(WVG_ERR_INVALID, "segments cannot be 0 nor negative");
+    if (ks > 256)
+        return fail(WVG_ERR_INVALID,
+                    "centroids should not be higher than 256. Attempting to use " + std::to_string(ks));
+    if (ks == 0) return fail(WVG_ERR_INVALID, "centroids must be > 0");
+    if (c->dim % m != 0) return fail(WVG_ERR_INVALID, "segments should be an integer divisor of dimensions");
+    std::unique_lock<std::shared_mutex> lk(c->rw);
+    if (c->count > 0 && m != c->pq_m) return fail(WVG_ERR_INVALID, "cannot change segments of a non-empty PQ corpus");
+    const uint32_t ds = c->dim / m;
+    float *dc = nullptr;
+    WVG_HIP(hipMalloc(&dc, (size_t)m * ks * ds * 4));
+    WVG_HIP(hipMemcpy(dc, centers, (size_t)m * ks * ds * 4, hipMemcpyHostToDevice));
+    if (c->d_centers) (void)hipFree(c->d_centers);
+    c->d_centers = dc;
+    const bool realloc = c->pq_m != m;
+    c->pq_m = m;
+    c->pq_ks = ks;
+    c->pq_ds = ds;
+    c->nchunks = pq_chunks(m);
+    if (realloc) {
+        const uint64_t cap = c->capacity;
+        if (c->d_data) (void)hipFree(c->d_data);
+        if (c->d_valid) (void)hipFree(c->d_valid);
+        c->d_data = nullptr;
+        c->d_valid = nullptr;
+        c->capacity = 0;
+        c->h_valid.clear();
+        return corpus_alloc(c, cap);
+    }
+    return WVG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Search
+// ---------------------------------------------------------------------------
+
+// Next free profiling event pair of the context (grown on demand).
+static int prof_pair(wvg_ctx *ctx, std::pair<hipEvent_t, hipEvent_t> *out)
+{
+    std::lock_guard<std::mutex> g(ctx->prof_mu);
+    if (ctx->prof_used == ctx->prof_events.size()) {
+        hipEvent_t a, b;
+        WVG_HIP(hipEventCreate(&a));
+        WVG_HIP(hipEventCreate(&b));
+        ctx->prof_events.emplace_back(a, b);
+    }
+    *out = ctx->prof_events[ctx->prof_used++];
+    return WVG_OK;
+}
+
+// Runs phase 1 + phase 2 for one corpus with device-resident prepared queries.
+static int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t nq, uint32_t k, const uint64_t *d_allow,
+                      uint64_t allow_words, uint64_t tb, uint64_t te, uint64_t *d_partials, int groups, uint64_t *ids,
+                      float *dists, uint32_t *counts, hipStream_t s)
+{
+    ScanArgs a{};
+    a.data = c->d_data;
+    a.valid = c->d_valid;
+    a.allow = d_allow;
+    a.allow_words = allow_words;
+    a.id_base = c->id_base;
+    a.tile_begin = tb;
+    a.tile_end = te;
+    a.dim = c->dim;
+    a.nchunks = c->nchunks;
+    a.metric = c->metric;
+    a.queries = d_q;
+    a.qpitch = qpitch;
+    a.nq = nq;
+    a.k = k;
+    a.pq_m = c->pq_m;
+    a.pq_ks = c->pq_ks;
+    std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
+    if (c->ctx->profiling.load(std::memory_order_relaxed)) {
+        int rc = prof_pair(c->ctx, &ev);
+        if (rc) return rc;
+        WVG_HIP(hipEventRecord(ev.first, s));
+    }
+    WVG_HIP(launch_scan(a, c->kind, d_partials, groups, s));
+    if (ev.second) WVG_HIP(hipEventRecord(ev.second, s));
+    WVG_HIP(launch_merge_keys(d_partials, nq, (uint32_t)groups * k, k, c->id_base, ids, dists, counts, s));
+    return WVG_OK;
+}
+
+struct SearchPlan {
+    uint64_t tb = 0, te = 0;
+    int groups = 1;
+    bool empty = false;
+};
+
+static SearchPlan plan_search(wvg_corpus *c, uint32_t nq, uint32_t k, const uint64_t *allow, uint64_t allow_words)
+{
+    SearchPlan p;
+    p.empty = !allow_tile_range(c, allow, allow_words, p.tb, p.te) || k == 0 || nq == 0;
+    ScanArgs a{};
+    a.tile_begin = p.tb;
+    a.tile_end = p.te;
+    a.nq = nq;
+    p.groups = scan_groups_for(a, c->ctx->num_cus);
+    return p;
+}
+
+static void write_empty(uint32_t nq, uint32_t k, uint64_t *ids, float *dists, uint32_t *counts)
+{
+    for (uint64_t i = 0; i < (uint64_t)nq * k; i++) {
+        if (ids) ids[i] = WVG_KEY_NONE;
+        if (dists) dists[i] = INFINITY;
+    }
+    if (counts)
+        for (uint32_t i = 0; i < nq; i++) counts[i] = 0;
+}
+
+static int stage_queries(wvg_corpus *c, StreamSlot *sl, const float *queries, uint32_t nq, char *dst, uint32_t &qpitch,
+                         float *d_lut_or_null, char *d_qtmp)
+{
+    std::vector<float> qf;
+    std::vector<uint64_t> qb;
+    prepare_queries_host(c, queries, nq, qf, qb, qpitch);
+    hipStream_t s = sl->stream;
+    if (c->kind == WVG_KIND_BQ) {
+        WVG_HIP(hipMemcpyAsync(dst, qb.data(), qb.size() * 8, hipMemcpyHostToDevice, s));
+        WVG_HIP(hipStreamSynchronize(s));
+        return WVG_OK;
+    }
+    if (c->kind == WVG_KIND_F32) {
+        WVG_HIP(hipMemcpyAsync(dst, qf.data(), qf.size() * 4, hipMemcpyHostToDevice, s));
+        WVG_HIP(hipStreamSynchronize(s));
+        return WVG_OK;
+    }
+    // PQ: queries -> LUTs [nq][m*ks] (CH/product_quantization.go:329-337)
+    WVG_HIP(hipMemcpyAsync(d_qtmp, qf.data(), qf.size() * 4, hipMemcpyHostToDevice, s));
+    WVG_HIP(launch_pq_lut(c->metric, (const float *)d_qtmp, nq, qpitch, c->d_centers, c->pq_m, c->pq_ks, c->pq_ds,
+                          d_lut_or_null, s));
+    WVG_HIP(hipStreamSynchronize(s));
+    qpitch = c->pq_m * c->pq_ks;
+    return WVG_OK;
+}
+
+static size_t query_bytes(const wvg_corpus *c, uint32_t nq)
+{
+    switch (c->kind) {
+    case WVG_KIND_F32: return (size_t)nq * f32_chunks(c->dim) * 16;
+    case WVG_KIND_BQ: return (size_t)nq * bq_chunks(c->dim) * 16;
+    default: return (size_t)nq * c->pq_m * c->pq_ks * 4;
+    }
+}
+
+int wvg_search(wvg_corpus *c, const float *queries, uint32_t nq, uint32_t k, const uint64_t *allow_bits,
+               uint64_t allow_words, uint64_t *out_ids, float *out_dists, uint32_t *out_counts)
+{
+    int rc = check_corpus(c);
+    if (rc) return rc;
+    if (nq > 0 && !queries) return fail(WVG_ERR_INVALID, "null queries");
+    if (k > MAX_K) return fail(WVG_ERR_UNSUPPORTED, "k above 256 is not supported by the fused top-k");
+    if (c->kind == WVG_KIND_PQ && !c->d_centers) return fail(WVG_ERR_INVALID, "PQ corpus has no codebook");
+    std::shared_lock<std::shared_mutex> lk(c->rw);
+    SearchPlan p = plan_search(c, nq, k, allow_bits, allow_words);
+    if (p.empty) {
+        write_empty(nq, k, out_ids, out_dists, out_counts);
+        return WVG_OK;
+    }
+    SlotGuard g(c->ctx);
+    rc = c->ctx->acquire(&g.slot);
+    if (rc) return rc;
+    Carver cv;
+    const size_t o_q = cv.take(query_bytes(c, nq));
+    const size_t o_qtmp = cv.take(c->kind == WVG_KIND_PQ ? (size_t)nq * c->dim * 4 : 0);
+    const size_t o_allow = cv.take(allow_bits ? allow_words * 8 : 0);
+    const size_t o_part = cv.take((size_t)nq * p.groups * k * 8);
+    const size_t o_ids = cv.take((size_t)nq * k * 8);
+    const size_t o_d = cv.take((size_t)nq * k * 4);
+    const size_t o_cnt = cv.take((size_t)nq * 4);
+    void *base = nullptr;
+    rc = g.slot->device_scratch(cv.off, &base);
+    if (rc) return rc;
+    char *b = (char *)base;
+    hipStream_t s = g.slot->stream;
+    uint32_t qpitch = 0;
+    rc = stage_queries(c, g.slot, queries, nq, b + o_q, qpitch, (float *)(b + o_q), b + o_qtmp);
+    if (rc) return rc;
+    const uint64_t *d_allow = nullptr;
+    if (allow_bits) {
+        WVG_HIP(hipMemcpyAsync(b + o_allow, allow_bits, allow_words * 8, hipMemcpyHostToDevice, s));
+        d_allow = (const uint64_t *)(b + o_allow);
+    }
+    rc = run_search(c, b + o_q, qpitch, nq, k, d_allow, allow_words, p.tb, p.te, (uint64_t *)(b + o_part), p.groups,
+                    (uint64_t *)(b + o_ids), (float *)(b + o_d), (uint32_t *)(b + o_cnt), s);
+    if (rc) return rc;
+    if (out_ids) WVG_HIP(hipMemcpyAsync(out_ids, b + o_ids, (size_t)nq * k * 8, hipMemcpyDeviceToHost, s));
+    if (out_dists) WVG_HIP(hipMemcpyAsync(out_dists, b + o_d, (size_t)nq * k * 4, hipMemcpyDeviceToHost, s));
+    if (out_counts) WVG_HIP(hipMemcpyAsync(out_counts, b + o_cnt, (size_t)nq * 4, hipMemcpyDeviceToHost, s));
+    WVG_HIP(hipStreamSynchronize(s));
+    return WVG_OK;
+}
+
+int wvg_search_bq_rescore(wvg_corpus *bq, wvg_corpus *f32, const float *queries, uint32_t nq, uint32_t k,
+                          uint32_t rescore_limit, const uint64_t *allow_bits, uint64_t allow_words, uint64_t *out_ids,
+                          float *out_dists, uint32_t *out_counts)
+{
+    int rc = check_corpus(bq);
+    if (rc) return rc;
+    if (!f32 || bq->kind != WVG_KIND_BQ || f32->kind != WVG_KIND_F32)
+        return fail(WVG_ERR_INVALID, "need a BQ corpus and an F32 corpus");
+    if (bq->dim != f32->dim || bq->id_base != f32->id_base || bq->metric != f32->metric)
+        return fail(WVG_ERR_INVALID, "BQ and F32 corpora disagree on dim/id_base/metric");
+    if (nq > 0 && !queries) return fail(WVG_ERR_INVALID, "null queries");
+    const uint32_t R = std::max(rescore_limit, k);  // searchTimeRescore (V/flat/index.go:297-305)
+    if (R > MAX_K) return fail(WVG_ERR_UNSUPPORTED, "rescore window above 256 is not supported by the fused top-k");
+    std::shared_lock<std::shared_mutex> lk1(bq->rw);
+    std::shared_lock<std::shared_mutex> lk2(f32->rw);
+    SearchPlan p = plan_search(bq, nq, R, allow_bits, allow_words);
+    if (p.empty || k == 0) {
+        write_empty(nq, k, out_ids, out_dists, out_counts);
+        return WVG_OK;
+    }
+    SlotGuard g(bq->ctx);
+    rc = bq->ctx->acquire(&g.slot);
+    if (rc) return rc;
+    const uint32_t d = bq->dim;
+    const uint32_t fpitch = f32_chunks(d) * 4;
+    Carver cv;
+    const size_t o_qb = cv.take(query_bytes(bq, nq));
+    const size_t o_qf = cv.take((size_t)nq * fpitch * 4);
+    const size_t o_allow = cv.take(allow_bits ? allow_words * 8 : 0);
+    const size_t o_part = cv.take((size_t)nq * p.groups * R * 8);
+    const size_t o_cand = cv.take((size_t)nq * R * 8);
+    const size_t o_resc = cv.take((size_t)nq * R * 8);
+    const size_t o_ids = cv.take((size_t)nq * k * 8);
+    const size_t o_d = cv.take((size_t)nq * k * 4);
+    const size_t o_cnt = cv.take((size_t)nq * 4);
+    void *base = nullptr;
+    rc = g.slot->device_scratch(cv.off, &base);
+    if (rc) return rc;
+    char *b = (char *)base;
+    hipStream_t s = g.slot->stream;
+    uint32_t qpb = 0, qpf = 0;
+    rc = stage_queries(bq, g.slot, queries, nq, b + o_qb, qpb, nullptr, nullptr);
+    if (rc) return rc;
+    rc = stage_queries(f32, g.slot, queries, nq, b + o_qf, qpf, nullptr, nullptr);
+    if (rc) return rc;
+    const uint64_t *d_allow = nullptr;
+    if (allow_bits) {
+        WVG_HIP(hipMemcpyAsync(b + o_allow, allow_bits, allow_words * 8, hipMemcpyHostToDevice, s));
+        d_allow = (const uint64_t *)(b + o_allow);
+    }
+    // Hamming top-R keys (slot in the low 32 bits): phase 1 + a keys-only phase 2
+    ScanArgs a{};
+    a.data = bq->d_data;
+    a.valid = bq->d_valid;
+    a.allow = d_allow;
+    a.allow_words = allow_words;
+    a.id_base = bq->id_base;
+    a.tile_begin = p.tb;
+    a.tile_end = p.te;
+    a.dim = d;
+    a.nchunks = bq->nchunks;
+    a.metric = bq->metric;
+    a.queries = b + o_qb;
+    a.qpitch = qpb;
+    a.nq = nq;
+    a.k = R;
+    uint64_t *part = (uint64_t *)(b + o_part);
+    WVG_HIP(launch_scan_bq(a, part, p.groups, s));
+    // merge partials to R candidate ids; ids are id_base + slot, so pass id_base = 0 to keep slots
+    uint64_t *cand_ids = (uint64_t *)(b + o_cand);
+    float *cand_d = (float *)(b + o_ids);  // temporary, overwritten below
+    (void)cand_d;
+    WVG_HIP(launch_merge_keys(part, nq, (uint32_t)p.groups * R, R, 0, cand_ids, (float *)(b + o_resc), nullptr, s));
+    // cand_ids now hold slots (or KEY_NONE); rescore them exactly against the f32 rows
+    WVG_HIP(launch_rescore_keys(f32->metric, (const float *)(b + o_qf), qpf, (const float *)f32->d_data, d,
+                                f32->nchunks, cand_ids, nq, R, R, (uint64_t *)(b + o_resc), s));
+    WVG_HIP(launch_merge_keys((uint64_t *)(b + o_resc), nq, R, k, f32->id_base, (uint64_t *)(b + o_ids),
+                              (float *)(b + o_d), (uint32_t *)(b + o_cnt), s));
+    if (out_ids) WVG_HIP(hipMemcpyAsync(out_ids, b + o_ids, (size_t)nq * k * 8, hipMemcpyDeviceToHost, s));
+    if (out_dists) WVG_HIP(hipMemcpyAsync(out_dists, b + o_d, (size_t)nq * k * 4, hipMemcpyDeviceToHost, s));
+    if (out_counts) WVG_HIP(hipMemcpyAsync(out_counts, b + o_cnt, (size_t)nq * 4, hipMemcpyDeviceToHost, s));
+    WVG_HIP(hipStreamSynchronize(s));
+    return WVG_OK;
+}
+
+size_t wvg_search_workspace_size(wvg_corpus *c, uint32_t nq, uint32_t k)
+{
+    if (!c) return 0;
+    SearchPlan p = plan_search(c, nq, k, nullptr, 0);
+    Carver cv;
+    cv.take((size_t)nq * p.groups * std::max<uint32_t>(k, 1) * 8);
+    cv.take(query_bytes(c, nq));
+    return cv.off;
+}
+
+int wvg_search_device(wvg_corpus *c, const float *d_queries, uint32_t nq, uint32_t k, uint64_t *d_ids, float *d_dists,
+                      uint32_t *d_counts, void *d_workspace, size_t workspace_bytes, void *stream)
+{
+    if (!c) return fail(WVG_ERR_INVALID, "null corpus");
+    if (k > MAX_K) return fail(WVG_ERR_UNSUPPORTED, "k above 256 is not supported by the fused top-k");
+    if (c->kind != WVG_KIND_F32) return fail(WVG_ERR_UNSUPPORTED, "device search supports F32 corpora");
+    if (c->dim % 4 != 0) return fail(WVG_ERR_UNSUPPORTED, "device search needs dim % 4 == 0");
+    hipStream_t s = (hipStream_t)stream;
+    std::shared_lock<std::shared_mutex> lk(c->rw);
+    SearchPlan p = plan_search(c, nq, k, nullptr, 0);
+    if (p.empty) return WVG_OK;
+    Carver cv;
+    const size_t o_part = cv.take((size_t)nq * p.groups * k * 8);
+    if (!d_workspace || workspace_bytes < cv.off) return fail(WVG_ERR_INVALID, "workspace too small");
+    return run_search(c, d_queries, c->dim, nq, k, nullptr, 0, p.tb, p.te,
+                      (uint64_t *)((char *)d_workspace + o_part), p.groups, d_ids, d_dists, d_counts, s);
+}
+
+int wvg_topk_merge_device(wvg_ctx *ctx, const float *d_dists, const uint64_t *d_ids, uint32_t nq, uint32_t nlists,
+                          uint32_t k_in, uint32_t k, uint64_t *d_out_ids, float *d_out_dists, uint32_t *d_out_counts,
+                          void *stream)
+{
+    if (!ctx) return fail(WVG_ERR_INVALID, "null ctx");
+    if ((uint64_t)nlists * k_in > 8192) return fail(WVG_ERR_UNSUPPORTED, "merge input above 8192 pairs per query");
+    if (nq == 0 || k == 0) return WVG_OK;
+    WVG_HIP(launch_merge_pairs(d_dists, d_ids, nq, nlists, k_in, k, d_out_ids, d_out_dists, d_out_counts,
+                               (hipStream_t)stream));
+    return WVG_OK;
+}
+
+int wvg_profile_start(wvg_ctx *ctx)
+{
+    if (!ctx) return fail(WVG_ERR_INVALID, "null ctx");
+    std::lock_guard<std::mutex> g(ctx->prof_mu);
+    ctx->prof_used = 0;
+    ctx->profiling.store(true);
+    return WVG_OK;
+}
+
+int wvg_profile_stop(wvg_ctx *ctx, double *scan_ms_total, uint64_t *scan_launches)
+{
+    if (!ctx) return fail(WVG_ERR_INVALID, "null ctx");
+    WVG_HIP(hipSetDevice(ctx->device));
+    ctx->profiling.store(false);
+    std::lock_guard<std::mutex> g(ctx->prof_mu);
+    double total = 0.0;
+    for (size_t i = 0; i < ctx->prof_used; i++) {
+        WVG_HIP(hipEventSynchronize(ctx->prof_events[i].second));
+        float ms = 0.0f;
+        WVG_HIP(hipEventElapsedTime(&ms, ctx->prof_events[i].first, ctx->prof_events[i].second));
+        total += ms;
+    }
+    if (scan_ms_total) *scan_ms_total = total;
+    if (scan_launches) *scan_launches = ctx->prof_used;
+    ctx->prof_used = 0;
+    return WVG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Bulk primitives
+// ---------------------------------------------------------------------------
+struct Bulk {
+    SlotGuard g;
+    char *b = nullptr;
+    explicit Bulk(wvg_ctx *ctx) : g(ctx) {}
+    int begin(size_t bytes)
+    {
+        int rc = g.ctx->acquire(&g.slot);
+        if (rc) return rc;
+        void *p = nullptr;
+        rc = g.slot->device_scratch(bytes, &p);
+        b = (char *)p;
+        return rc;
+    }
+    hipStream_t s() const { return g.slot->stream; }
+};
+
+int wvg_distance_batch(wvg_ctx *ctx, int metric, const float *q, const float *X, uint64_t n, uint32_t dim, float *out)
+{
+    if (!ctx || !q || (n && (!X || !out))) return fail(WVG_ERR_INVALID, "null argument");
+    if (metric < WVG_METRIC_L2 || metric > WVG_METRIC_COSINE) return fail(WVG_ERR_INVALID, "unknown metric");
+    if (n == 0 || dim == 0) return WVG_OK;
+    WVG_HIP(hipSetDevice(ctx->device));
+    const uint32_t nch = f32_chunks(dim);
+    Carver cv;
+    const size_t o_x = cv.take(n * dim * 4), o_t = cv.take(tiles_of(n) * 64 * (size_t)nch * 16),
+                 o_q = cv.take((size_t)nch * 16), o_o = cv.take(n * 4);
+    Bulk bk(ctx);
+    int rc = bk.begin(cv.off);
+    if (rc) return rc;
+    std::vector<float> qp((size_t)nch * 4, 0.0f);
+    std::memcpy(qp.data(), q, (size_t)dim * 4);
+    WVG_HIP(hipMemcpyAsync(bk.b + o_x, X, n * dim * 4, hipMemcpyHostToDevice, bk.s()));
+    WVG_HIP(hipMemcpyAsync(bk.b + o_q, qp.data(), qp.size() * 4, hipMemcpyHostToDevice, bk.s()));
+    WVG_HIP(launch_f32_store((const float *)(bk.b + o_x), nullptr, n, dim, nch, 0, (float *)(bk.b + o_t), bk.s()));
+    WVG_HIP(launch_distance_rows(metric, (const float *)(bk.b + o_q), (const float *)(bk.b + o_t), n, dim,
+                                 (float *)(bk.b + o_o), bk.s()));
+    WVG_HIP(hipMemcpyAsync(out, bk.b + o_o, n * 4, hipMemcpyDeviceToHost, bk.s()));
+    WVG_HIP(hipStreamSynchronize(bk.s()));
+    return WVG_OK;
+}
+
+int wvg_normalize_batch(wvg_ctx *ctx, const float *X, uint64_t n, uint32_t dim, float *out)
+{
+    if (!ctx || (n && (!X || !out))) return fail(WVG_ERR_INVALID, "null argument");
+    if (n == 0 || dim == 0) return WVG_OK;
+    WVG_HIP(hipSetDevice(ctx->device));
+    Carver cv;
+    const size_t o_x = cv.take(n * dim * 4), o_o = cv.take(n * dim * 4);
+    Bulk bk(ctx);
+    int rc = bk.begin(cv.off);
+    if (rc) return rc;
+    WVG_HIP(hipMemcpyAsync(bk.b + o_x, X, n * dim * 4, hipMemcpyHostToDevice, bk.s()));
+    WVG_HIP(launch_normalize_rows((const float *)(bk.b + o_x), n, dim, (float *)(bk.b + o_o), bk.s()));
+    WVG_HIP(hipMemcpyAsync(out, bk.b + o_o, n * dim * 4, hipMemcpyDeviceToHost, bk.s()));
+    WVG_HIP(hipStreamSynchronize(bk.s()));
+    return WVG_OK;
+}
+
+int wvg_bq_encode(wvg_ctx *ctx, const float *X, uint64_t n, uint32_t dim, uint64_t *out_words)
+{
+    if (!ctx || (n && (!X || !out_words))) return fail(WVG_ERR_INVALID, "null argument");
+    if (n == 0 || dim == 0) return WVG_OK;
+    WVG_HIP(hipSetDevice(ctx->device));
+    const uint32_t w = bq_words(dim);
+    Carver cv;
+    const size_t o_x = cv.take(n * dim * 4), o_o = cv.take(n * w * 8);
+    Bulk bk(ctx);
+    int rc = bk.begin(cv.off);
+    if (rc) return rc;
+    WVG_HIP(hipMemcpyAsync(bk.b + o_x, X, n * dim * 4, hipMemcpyHostToDevice, bk.s()));
+    WVG_HIP(launch_bq_encode_rows((const float *)(bk.b + o_x), n, dim, 0, (uint64_t *)(bk.b + o_o), bk.s()));
+    WVG_HIP(hipMemcpyAsync(out_words, bk.b + o_o, n * w * 8, hipMemcpyDeviceToHost, bk.s()));
+    WVG_HIP(hipStreamSynchronize(bk.s()));
+    return WVG_OK;
+}
+
+int wvg_bq_distance_batch(wvg_ctx *ctx, const uint64_t *q, const uint64_t *codes, uint64_t n, uint32_t words,
+                          float *out)
+{
+    if (!ctx || !q || (n && (!codes || !out))) return fail(WVG_ERR_INVALID, "null argument");
+    if (n == 0) return WVG_OK;
+    WVG_HIP(hipSetDevice(ctx->device));
+    Carver cv;
+    const size_t o_q = cv.take((size_t)words * 8), o_c = cv.take(n * words * 8), o_o = cv.take(n * 4);
+    Bulk bk(ctx);
+    int rc = bk.begin(cv.off);
+    if (rc) return rc;
+    WVG_HIP(hipMemcpyAsync(bk.b + o_q, q, (size_t)words * 8, hipMemcpyHostToDevice, bk.s()));
+    WVG_HIP(hipMemcpyAsync(bk.b + o_c, codes, n * words * 8, hipMemcpyHostToDevice, bk.s()));
+    WVG_HIP(launch_bq_distance_rows((const uint64_t *)(bk.b + o_q), (const uint64_t *)(bk.b + o_c), n, words,
+                                    (float *)(bk.b + o_o), bk.s()));
+    WVG_HIP(hipMemcpyAsync(out, bk.b + o_o, n * 4, hipMemcpyDeviceToHost, bk.s()));
+    WVG_HIP(hipStreamSynchronize(bk.s()));
+    return WVG_OK;
+}
+
+static int pq_validate(uint32_t m, uint32_t ks, uint32_t dim)
+{
+    if (m == 0) return fail(WVG_ERR_INVALID, "segments cannot be 0 nor negative");
+    if (ks > 256)
+        return fail(WVG_ERR_INVALID,
+                    "centroids should not be higher than 256. Attempting to use " + std::to_string(ks));
+    if (ks == 0) return fail(WVG_ERR_INVALID, "centroids must be > 0");
+    if (dim % m != 0) return fail(WVG_ERR_INVALID, "segments should be an integer divisor of dimensions");
+    return WVG_OK;
+}
+
+int wvg_pq_encode(wvg_ctx *ctx, const float *centers, uint32_t m, uint32_t ks, const float *X, uint64_t n,
+                  uint32_t dim, uint8_t *out_codes)
+{
+    if (!ctx || !centers || (n && (!X || !out_codes))) return fail(WVG_ERR_INVALID, "null argument");
+    int rc = pq_validate(m, ks, dim);
+    if (rc) return rc;
+    if (n == 0) return WVG_OK;
+    WVG_HIP(hipSetDevice(ctx->device));
+    const uint32_t nch = f32_chunks(dim), ds = dim / m;
+    Carver cv;
+    const size_t o_x = cv.take(n * dim * 4), o_t = cv.take(tiles_of(n) * 64 * (size_t)nch * 16),
+                 o_c = cv.take((size_t)m * ks * ds * 4), o_o = cv.take(n * m);
+    Bulk bk(ctx);
+    rc = bk.begin(cv.off);
+    if (rc) return rc;
+    WVG_HIP(hipMemcpyAsync(bk.b + o_x, X, n * dim * 4, hipMemcpyHostToDevice, bk.s()));
+    WVG_HIP(hipMemcpyAsync(bk.b + o_c, centers, (size_t)m * ks * ds * 4, hipMemcpyHostToDevice, bk.s()));
+    WVG_HIP(launch_f32_store((const float *)(bk.b + o_x), nullptr, n, dim, nch, 0, (float *)(bk.b + o_t), bk.s()));
+    WVG_HIP(launch_pq_encode((const float *)(bk.b + o_t), n, dim, (const float *)(bk.b + o_c), m, ks,
+                             (uint8_t *)(bk.b + o_o), bk.s()));
+    WVG_HIP(hipMemcpyAsync(out_codes, bk.b + o_o, n * m, hipMemcpyDeviceToHost, bk.s()));
+    WVG_HIP(hipStreamSynchronize(bk.s()));
+    return WVG_OK;
+}
+
+int wvg_pq_lut(wvg_ctx *ctx, int metric, const float *centers, uint32_t m, uint32_t ks, uint32_t dim, const float *q,
+               float *out_lut)
+{
+    if (!ctx || !centers || !q || !out_lut) return fail(WVG_ERR_INVALID, "null argument");
+    int rc = pq_validate(m, ks, dim);
+    if (rc) return rc;
+    WVG_HIP(hipSetDevice(ctx->device));
+    const uint32_t ds = dim / m;
+    Carver cv;
+    const size_t o_q = cv.take((size_t)dim * 4), o_c = cv.take((size_t)m * ks * ds * 4),
+                 o_o = cv.take((size_t)m * ks * 4);
+    Bulk bk(ctx);
+    rc = bk.begin(cv.off);
+    if (rc) return rc;
+    WVG_HIP(hipMemcpyAsync(bk.b + o_q, q, (size_t)dim * 4, hipMemcpyHostToDevice, bk.s()));
+    WVG_HIP(hipMemcpyAsync(bk.b + o_c, centers, (size_t)m * ks * ds * 4, hipMemcpyHostToDevice, bk.s()));
+    WVG_HIP(launch_pq_lut(metric, (const float *)(bk.b + o_q), 1, dim, (const float *)(bk.b + o_c), m, ks, ds,
+                          (float *)(bk.b + o_o), bk.s()));
+    WVG_HIP(hipMemcpyAsync(out_lut, bk.b + o_o, (size_t)m * ks * 4, hipMemcpyDeviceToHost, bk.s()));
+    WVG_HIP(hipStreamSynchronize(bk.s()));
+    return WVG_OK;
+}
+
+int wvg_pq_adc_batch(wvg_ctx *ctx, int metric, const float *lut, uint32_t m, uint32_t ks, const uint8_t *codes,
+                     uint64_t n, float *out)
+{
+    if (!ctx || !lut || (n && (!codes || !out))) return fail(WVG_ERR_INVALID, "null argument");
+    if (n == 0) return WVG_OK;
+    WVG_HIP(hipSetDevice(ctx->device));
+    Carver cv;
+    const size_t o_l = cv.take((size_t)m * ks * 4), o_c = cv.take(n * m), o_o = cv.take(n * 4);
+    Bulk bk(ctx);
+    int rc = bk.begin(cv.off);
+    if (rc) return rc;
+    WVG_HIP(hipMemcpyAsync(bk.b + o_l, lut, (size_t)m * ks * 4, hipMemcpyHostToDevice, bk.s()));
+    WVG_HIP(hipMemcpyAsync(bk.b + o_c, codes, n * m, hipMemcpyHostToDevice, bk.s()));
+    WVG_HIP(launch_pq_adc_rows(metric, (const float *)(bk.b + o_l), m, ks, (const uint8_t *)(bk.b + o_c), n,
+                               (float *)(bk.b + o_o), bk.s()));
+    WVG_HIP(hipMemcpyAsync(out, bk.b + o_o, n * 4, hipMemcpyDeviceToHost, bk.s()));
+    WVG_HIP(hipStreamSynchronize(bk.s()));
+    return WVG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,154 @@
+// wvg_internal.hpp -- host-side internals shared by the HIP translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <mutex>
+#include <shared_mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/wvgpu.h"
+#include "wvg_common.hpp"
+
+namespace wvg {
+
+// thread-local last-error message (wvg_last_error)
+void set_error(const std::string &msg);
+int fail(int code, const std::string &msg);
+
+#define WVG_HIP(expr)                                                                   \
+    do {                                                                                \
+        hipError_t _e = (expr);                                                         \
+        if (_e != hipSuccess)                                                           \
+            return ::wvg::fail(WVG_ERR_DEVICE, std::string(#expr ": ") + hipGetErrorString(_e)); \
+    } while (0)
+
+// A pooled HIP stream with its own grow-only device scratch and pinned host
+// staging, borrowed by one C-ABI call at a time (callers are many goroutines).
+struct StreamSlot {
+    hipStream_t stream = nullptr;
+    void *dscratch = nullptr;
+    size_t dscratch_bytes = 0;
+    void *hpinned = nullptr;
+    size_t hpinned_bytes = 0;
+    int device_scratch(size_t bytes, void **out);
+    int host_pinned(size_t bytes, void **out);
+};
+
+}  // namespace wvg
+
+struct wvg_ctx {
+    int device = 0;
+    int num_cus = 256;
+    std::mutex pool_mu;
+    std::vector<wvg::StreamSlot *> free_slots;
+    std::vector<wvg::StreamSlot *> all_slots;
+    int acquire(wvg::StreamSlot **out);
+    void release(wvg::StreamSlot *s);
+    // profiling (wvg_profile_start/stop): event pairs around scan launches
+    std::atomic<bool> profiling{false};
+    std::mutex prof_mu;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_events;
+    size_t prof_used = 0;
+};
+
+struct wvg_corpus {
+    wvg_ctx *ctx = nullptr;
+    int kind = WVG_KIND_F32;
+    int metric = WVG_METRIC_L2;
+    uint32_t dim = 0;       // vector dimensions
+    uint32_t nchunks = 0;   // 16-byte chunks per row in the tiled layout
+    uint64_t id_base = 0;   // global docID of slot 0 (multiple of 64)
+    uint64_t capacity = 0;  // rows, multiple of 64
+    uint64_t high_water = 0;
+    uint64_t count = 0;
+    void *d_data = nullptr;        // tiled rows
+    uint64_t *d_valid = nullptr;   // one word per tile
+    std::vector<uint64_t> h_valid; // host mirror of d_valid
+    // PQ codebook (kind == PQ)
+    float *d_centers = nullptr;    // [m][ks][ds]
+    uint32_t pq_m = 0, pq_ks = 0, pq_ds = 0;
+    std::shared_mutex rw;          // shared: search; exclusive: upsert/delete/grow
+};
+
+namespace wvg {
+
+__host__ __device__ inline uint64_t tiles_of(uint64_t rows) { return (rows + WVG_TILE - 1) / WVG_TILE; }
+__host__ __device__ inline uint32_t f32_chunks(uint32_t dim) { return (dim + 3) / 4; }
+__host__ __device__ inline uint32_t bq_words(uint32_t dim) { return (dim + 63) / 64; }
+__host__ __device__ inline uint32_t bq_chunks(uint32_t dim) { return (bq_words(dim) + 1) / 2; }
+__host__ __device__ inline uint32_t pq_chunks(uint32_t m) { return (m + 15) / 16; }
+size_t corpus_row_bytes(int kind, uint32_t dim, uint32_t pq_m);
+
+// ---- kernel launchers (wvg_scan.hip / wvg_bq.hip / wvg_pq.hip) -----------
+// Scan phase 1: per (query, workgroup) top-K keys into `partials`
+//   [nq][groups][K].  Returns the number of groups used.
+struct ScanArgs {
+    const void *data;          // tiled corpus
+    const uint64_t *valid;     // one word per tile
+    const uint64_t *allow;     // allow bitmap over global ids, may be null
+    uint64_t allow_words;
+    uint64_t id_base;
+    uint64_t tile_begin, tile_end;
+    uint32_t dim, nchunks;
+    int metric;
+    const void *queries;       // F32: [nq][qpitch] floats; BQ: [nq][2*nchunks] u64; PQ: luts [nq][m*ks]
+    uint32_t qpitch;           // elements per query in `queries`
+    uint32_t nq, k;
+    uint32_t pq_m, pq_ks;
+};
+int scan_groups_for(const ScanArgs &a, int num_cus);
+hipError_t launch_scan_f32(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s);
+hipError_t launch_scan_bq(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s);
+hipError_t launch_scan_pq(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s);
+// Scan phase 2: merge [nq][nlists][K] keys into final (ids, dists, counts).
+hipError_t launch_merge_keys(const uint64_t *partials, uint32_t nq, uint32_t nlists, uint32_t k,
+                             uint64_t id_base, uint64_t *ids, float *dists, uint32_t *counts,
+                             hipStream_t s);
+// Merge (dist, id64) lists: [nq][nlists][k_in] -> [nq][k].
+hipError_t launch_merge_pairs(const float *dists, const uint64_t *ids, uint32_t nq, uint32_t nlists,
+                              uint32_t k_in, uint32_t k, uint64_t *out_ids, float *out_dists,
+                              uint32_t *out_counts, hipStream_t s);
+
+// Row-major -> tiled scatter (with optional normalize for cosine) of F32 rows.
+hipError_t launch_f32_store(const float *rows, const uint64_t *slots, uint64_t n, uint32_t dim,
+                            uint32_t nchunks, int normalize, float *tiled, hipStream_t s);
+hipError_t launch_f32_synth(uint64_t seed, int dist, uint64_t row0, uint64_t n, uint64_t slot0,
+                            uint32_t dim, uint32_t nchunks, int normalize, float *tiled,
+                            hipStream_t s);
+hipError_t launch_f32_gather(const float *tiled, const uint64_t *slots, uint64_t n, uint32_t dim,
+                             uint32_t nchunks, float *rows, hipStream_t s);
+hipError_t launch_normalize_rows(const float *in, uint64_t n, uint32_t dim, float *out,
+                                 hipStream_t s);
+hipError_t launch_distance_rows(int metric, const float *q, const float *rows, uint64_t n,
+                                uint32_t dim, float *out, hipStream_t s);
+hipError_t launch_rescore_keys(int metric, const float *q, uint32_t qpitch, const float *tiled,
+                               uint32_t dim, uint32_t nchunks, const uint64_t *cand_keys,
+                               uint32_t nq, uint32_t ncand, uint32_t cand_stride,
+                               uint64_t *out_keys, hipStream_t s);
+// BQ
+hipError_t launch_bq_encode_rows(const float *rows, uint64_t n, uint32_t dim, int normalize,
+                                 uint64_t *codes, hipStream_t s);
+hipError_t launch_bq_store(const uint64_t *codes, const uint64_t *slots, uint64_t n, uint32_t words,
+                           uint32_t nchunks, uint64_t *tiled, hipStream_t s);
+hipError_t launch_bq_synth(uint64_t seed, int dist, uint64_t row0, uint64_t n, uint64_t slot0,
+                           uint32_t dim, uint32_t nchunks, int normalize, uint64_t *tiled,
+                           hipStream_t s);
+hipError_t launch_bq_distance_rows(const uint64_t *q, const uint64_t *codes, uint64_t n,
+                                   uint32_t words, float *out, hipStream_t s);
+// PQ
+hipError_t launch_pq_lut(int metric, const float *q, uint32_t nq, uint32_t qpitch,
+                         const float *centers, uint32_t m, uint32_t ks, uint32_t ds, float *lut,
+                         hipStream_t s);
+hipError_t launch_pq_encode(const float *rows, uint64_t n, uint32_t dim, const float *centers,
+                            uint32_t m, uint32_t ks, uint8_t *codes, hipStream_t s);
+hipError_t launch_pq_store(const uint8_t *codes, const uint64_t *slots, uint64_t n, uint32_t m,
+                           uint32_t nchunks, uint8_t *tiled, hipStream_t s);
+hipError_t launch_pq_adc_rows(int metric, const float *lut, uint32_t m, uint32_t ks,
+                              const uint8_t *codes, uint64_t n, float *out, hipStream_t s);
+hipError_t launch_set_valid(uint64_t *valid, const uint64_t *slots, uint64_t n, int set,
+                            hipStream_t s);
+
+}  // namespace wvg

@@ -1,0 +1,311 @@
+// wvg_pq.hip -- product quantization on MI355X.
+//
+// K7 LUT:    DistanceLookUpTable entries lut[i][c] = distance.Step(q_i, C_i[c])
+//            (CH/product_quantization.go:85-104; Step is the pure-Go loop,
+//            sequential and unfused on amd64: D/l2.go:79-88, D/dot_product.go:87-94).
+// K8 ADC:    PQDistancer.Distance (CH/product_quantization.go:352-361):
+//            sum += lut[i][code_i] for i = 0..m-1 in order, then Wrap.  The LUT
+//            (m*ks*4 bytes, 32 KiB at m=32, ks=256) lives in LDS; codes stream
+//            from HBM in the tiled layout (16 codes per 16-byte load per lane).
+//            Roofline: HBM, N*m bytes per query (LDS-gather bound when codes
+//            are random: see DESIGN.md).
+// K9 encode: ProductQuantizer.Encode -> KMeans.Nearest (CH/product_quantization.go:420-426,
+//            CH/kmeans.go:103-135): argmin_c l2_256(x_seg, C_s[c]) with the
+//            candidate replacing the best unless best < d (ties -> highest c,
+//            NaN replaces).
+#include "wvg_internal.hpp"
+#include "wvg_rowdist.hpp"
+#include "wvg_topk.hpp"
+
+namespace wvg {
+
+constexpr int PQ_WAVES = 4;
+
+// Step(a, b) in the pure-Go order.
+__device__ __forceinline__ float go_step(int metric, const float *a, const float *b, uint32_t n)
+{
+    float sum = 0.0f;
+    if (metric == WVG_M_L2) {
+        for (uint32_t i = 0; i < n; i++) {
+            float diff = a[i] - b[i];
+            float sq = diff * diff;
+            sum = sum + sq;
+        }
+    } else {
+        for (uint32_t i = 0; i < n; i++) {
+            float p = a[i] * b[i];
+            sum = sum + p;
+        }
+    }
+    return sum;
+}
+
+__global__ void pq_lut_kernel(int metric, const float *q, uint32_t nq, uint32_t qpitch, const float *centers,
+                              uint32_t m, uint32_t ks, uint32_t ds, float *lut)
+{
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t per_q = (uint64_t)m * ks;
+    if (g >= per_q * nq) return;
+    const uint32_t qi = (uint32_t)(g / per_q);
+    const uint32_t r = (uint32_t)(g % per_q);
+    const uint32_t seg = r / ks, c = r % ks;
+    lut[g] = go_step(metric, q + (size_t)qi * qpitch + (size_t)seg * ds, centers + ((size_t)seg * ks + c) * ds, ds);
+}
+
+hipError_t launch_pq_lut(int metric, const float *q, uint32_t nq, uint32_t qpitch, const float *centers, uint32_t m,
+                         uint32_t ks, uint32_t ds, float *lut, hipStream_t s)
+{
+    const uint64_t total = (uint64_t)nq * m * ks;
+    if (total == 0) return hipSuccess;
+    hipLaunchKernelGGL(pq_lut_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, metric, q, nq, qpitch,
+                       centers, m, ks, ds, lut);
+    return hipGetLastError();
+}
+
+// l2_256 (D/c/l2_avx256_amd64.c:14-107) over element accessors.
+template <typename XA, typename CA>
+__device__ __forceinline__ float l2_256_acc(XA x, CA c, int n)
+{
+    float sum = 0.0f;
+    if (n < 8) {
+        for (int i = 0; i < n; i++) scalar_update<WVG_M_L2>(sum, c(i), x(i));
+        return sum;
+    }
+    float acc[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+#pragma unroll
+        for (int l = 0; l < 8; l++) acc[j][l] = 0.0f;
+    int pos = 0, rem = n;
+    while (rem >= 32) {
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+#pragma unroll
+            for (int l = 0; l < 8; l++) acc_update<WVG_M_L2>(acc[j][l], x(pos + 8 * j + l), c(pos + 8 * j + l));
+        pos += 32;
+        rem -= 32;
+    }
+    while (rem >= 8) {
+#pragma unroll
+        for (int l = 0; l < 8; l++) acc_update<WVG_M_L2>(acc[0][l], x(pos + l), c(pos + l));
+        pos += 8;
+        rem -= 8;
+    }
+    while (rem) {
+        scalar_update<WVG_M_L2>(sum, x(pos), c(pos));
+        pos++;
+        rem--;
+    }
+    return avx256_reduce(acc, sum);
+}
+
+// Encode from the tiled float layout; lane = row.  codes: [n][m] row-major.
+// (diff = point - centroid; l2_256(filteredPoint, c) at CH/kmeans.go:120.)
+template <int DS>
+__global__ void pq_encode_kernel(const float4 *tiled, uint64_t n, uint32_t dim, uint32_t nchunks, const float *centers,
+                                 uint32_t m, uint32_t ks, uint32_t ds_rt, uint8_t *codes)
+{
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const uint32_t ds = DS > 0 ? (uint32_t)DS : ds_rt;
+    const float4 *rp = tiled + ((r >> 6) * nchunks) * 64 + (r & 63);
+    for (uint32_t s = 0; s < m; s++) {
+        const float *cs = centers + (size_t)s * ks * ds;
+        uint32_t best = 0;
+        float minD = 3.40282346638528859812e+38f;  // math.MaxFloat32
+        if constexpr (DS == 4) {
+            // segment s is exactly chunk s (dim = 4m): one 16-byte load, scalar unfused path (n < 8)
+            const float4 x = rp[(size_t)s * 64];
+            for (uint32_t c = 0; c < ks; c++) {
+                const float4 cc = *reinterpret_cast<const float4 *>(cs + (size_t)c * 4);
+                float sum = 0.0f;
+                scalar_update<WVG_M_L2>(sum, cc.x, x.x);
+                scalar_update<WVG_M_L2>(sum, cc.y, x.y);
+                scalar_update<WVG_M_L2>(sum, cc.z, x.z);
+                scalar_update<WVG_M_L2>(sum, cc.w, x.w);
+                if (!(minD < sum)) {
+                    minD = sum;
+                    best = c;
+                }
+            }
+        } else {
+            const uint32_t base = s * ds;
+            auto xa = [&](int i) { return elem_at<64>(rp, (int)(base + i)); };
+            for (uint32_t c = 0; c < ks; c++) {
+                const float *cv = cs + (size_t)c * ds;
+                auto ca = [&](int i) { return cv[i]; };
+                const float d = l2_256_acc(xa, ca, (int)ds);
+                if (!(minD < d)) {
+                    minD = d;
+                    best = c;
+                }
+            }
+        }
+        codes[r * m + s] = (uint8_t)best;
+    }
+}
+
+hipError_t launch_pq_encode(const float *tiled, uint64_t n, uint32_t dim, const float *centers, uint32_t m,
+                            uint32_t ks, uint8_t *codes, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    const uint32_t ds = dim / m, nchunks = f32_chunks(dim);
+    dim3 grid((unsigned)((n + 255) / 256)), block(256);
+    if (ds == 4 && dim == 4 * m)
+        hipLaunchKernelGGL((pq_encode_kernel<4>), grid, block, 0, s, reinterpret_cast<const float4 *>(tiled), n, dim,
+                           nchunks, centers, m, ks, ds, codes);
+    else
+        hipLaunchKernelGGL((pq_encode_kernel<0>), grid, block, 0, s, reinterpret_cast<const float4 *>(tiled), n, dim,
+                           nchunks, centers, m, ks, ds, codes);
+    return hipGetLastError();
+}
+
+__global__ void pq_store_kernel(const uint8_t *codes, const uint64_t *slots, uint64_t n, uint32_t m, uint32_t nchunks,
+                                uint4 *tiled)
+{
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n * nchunks) return;
+    const uint64_t i = g / nchunks;
+    const uint32_t c = (uint32_t)(g % nchunks);
+    const uint64_t slot = slots ? slots[i] : i;
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    for (uint32_t b = 0; b < 16; b++) {
+        const uint32_t seg = c * 16 + b;
+        if (seg < m) w[b >> 2] |= (uint32_t)codes[i * m + seg] << (8 * (b & 3));
+    }
+    tiled[((slot >> 6) * nchunks + c) * 64 + (slot & 63)] = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+hipError_t launch_pq_store(const uint8_t *codes, const uint64_t *slots, uint64_t n, uint32_t m, uint32_t nchunks,
+                           uint8_t *tiled, hipStream_t s)
+{
+    const uint64_t total = n * nchunks;
+    if (total == 0) return hipSuccess;
+    hipLaunchKernelGGL(pq_store_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, codes, slots, n, m,
+                       nchunks, reinterpret_cast<uint4 *>(tiled));
+    return hipGetLastError();
+}
+
+__device__ __forceinline__ uint32_t code_at(const uint4 (&cw)[8], int i)
+{
+    const uint4 v = cw[i >> 4];
+    const int w = (i >> 2) & 3;
+    const uint32_t word = w == 0 ? v.x : (w == 1 ? v.y : (w == 2 ? v.z : v.w));
+    return (word >> (8 * (i & 3))) & 0xFFu;
+}
+
+// K8: ADC scan, LUT in LDS.  M = compile-time segments (<= 128) or 0.
+template <int E, int M>
+__global__ __launch_bounds__(PQ_WAVES * 64) void scan_pq_kernel(ScanArgs a, uint64_t *partials)
+{
+    extern __shared__ __attribute__((aligned(16))) float lut[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t qi = blockIdx.y;
+    const uint32_t m = M > 0 ? (uint32_t)M : a.pq_m;
+    const uint32_t ks = a.pq_ks;
+    const float *glut = reinterpret_cast<const float *>(a.queries) + (size_t)qi * a.qpitch;
+    for (uint32_t i = threadIdx.x; i < m * ks; i += blockDim.x) lut[i] = glut[i];
+    __syncthreads();
+    const uint4 *data = reinterpret_cast<const uint4 *>(a.data);
+    const uint32_t nch = a.nchunks;
+    const uint64_t ntiles = a.tile_end - a.tile_begin;
+    const uint64_t total = (uint64_t)gridDim.x * PQ_WAVES;
+    const uint64_t gw = (uint64_t)blockIdx.x * PQ_WAVES + wave;
+    const uint64_t t0 = a.tile_begin + ntiles * gw / total, t1 = a.tile_begin + ntiles * (gw + 1) / total;
+    WaveTopK<E> tk;
+    tk.init((int)a.k);
+    for (uint64_t t = t0; t < t1; ++t) {
+        uint64_t msk = a.valid[t];
+        if (a.allow) {
+            uint64_t w = (a.id_base >> 6) + t;
+            msk &= w < a.allow_words ? a.allow[w] : 0ull;
+        }
+        if (msk == 0ull) continue;
+        const uint4 *rp = data + (size_t)t * nch * 64 + lane;
+        float sum = 0.0f;
+        if constexpr (M > 0) {
+            uint4 cw[8];
+#pragma unroll
+            for (int c = 0; c < (M + 15) / 16; c++) cw[c] = rp[(size_t)c * 64];
+            float v[M];
+#pragma unroll
+            for (int i = 0; i < M; i++) v[i] = lut[i * ks + code_at(cw, i)];
+#pragma unroll
+            for (int i = 0; i < M; i++) sum = sum + v[i];
+        } else {
+            for (uint32_t c = 0; c < nch; c++) {
+                const uint4 x = rp[(size_t)c * 64];
+                const uint32_t ws[4] = {x.x, x.y, x.z, x.w};
+                for (uint32_t b = 0; b < 16; b++) {
+                    const uint32_t i = c * 16 + b;
+                    if (i < m) sum = sum + lut[i * ks + ((ws[b >> 2] >> (8 * (b & 3))) & 0xFFu)];
+                }
+            }
+        }
+        const float dist = wrap_metric(a.metric, sum);
+        const uint64_t key = ((msk >> lane) & 1ull) ? wvg_make_key(dist, (uint32_t)(t * 64 + lane)) : WVG_KEY_NONE;
+        tk.offer(key);
+    }
+    __shared__ uint64_t sh[PQ_WAVES][64 * E];
+#pragma unroll
+    for (int e = 0; e < E; e++) sh[wave][e * 64 + lane] = tk.l[e];
+    __syncthreads();
+    if (wave != 0) return;
+    for (int w = 1; w < PQ_WAVES; w++) {
+        uint64_t o[E];
+#pragma unroll
+        for (int e = 0; e < E; e++) o[e] = sh[w][e * 64 + lane];
+        merge_lists<E>(tk.l, o);
+    }
+    uint64_t *out = partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k;
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const int i = e * 64 + lane;
+        if (i < (int)a.k) out[i] = tk.l[e];
+    }
+}
+
+template <int E>
+static hipError_t launch_pq_e(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
+{
+    dim3 grid(groups, a.nq), block(PQ_WAVES * 64);
+    const size_t lds = (size_t)a.pq_m * a.pq_ks * 4;
+    switch (a.pq_m) {
+    case 8: hipLaunchKernelGGL((scan_pq_kernel<E, 8>), grid, block, lds, s, a, partials); break;
+    case 16: hipLaunchKernelGGL((scan_pq_kernel<E, 16>), grid, block, lds, s, a, partials); break;
+    case 32: hipLaunchKernelGGL((scan_pq_kernel<E, 32>), grid, block, lds, s, a, partials); break;
+    case 64: hipLaunchKernelGGL((scan_pq_kernel<E, 64>), grid, block, lds, s, a, partials); break;
+    default: hipLaunchKernelGGL((scan_pq_kernel<E, 0>), grid, block, lds, s, a, partials); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_scan_pq(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
+{
+    if ((size_t)a.pq_m * a.pq_ks * 4 > 160 * 1024) return hipErrorInvalidValue;
+    if (a.k <= 64) return launch_pq_e<1>(a, partials, groups, s);
+    if (a.k <= 128) return launch_pq_e<2>(a, partials, groups, s);
+    return launch_pq_e<4>(a, partials, groups, s);
+}
+
+__global__ void pq_adc_rows_kernel(int metric, const float *lut, uint32_t m, uint32_t ks, const uint8_t *codes,
+                                   uint64_t n, float *out)
+{
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const uint8_t *c = codes + r * m;
+    float sum = 0.0f;
+    for (uint32_t i = 0; i < m; i++) sum = sum + lut[(size_t)i * ks + c[i]];
+    out[r] = wrap_metric(metric, sum);
+}
+
+hipError_t launch_pq_adc_rows(int metric, const float *lut, uint32_t m, uint32_t ks, const uint8_t *codes, uint64_t n,
+                              float *out, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(pq_adc_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, metric, lut, m, ks,
+                       codes, n, out);
+    return hipGetLastError();
+}
+
+}  // namespace wvg

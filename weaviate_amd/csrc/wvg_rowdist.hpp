@@ -1,0 +1,149 @@
+// wvg_rowdist.hpp -- one lane computes Provider.SingleDist(query, row) for its
+// own row, in exactly the reference's AVX2 reduction order, so the fp32 result
+// is bit-identical to Weaviate's CPU distancer on non-AMX amd64 hosts
+// (dispatch D/l2_amd64.go:19-25, D/dot_product_amd64.go:19-25).
+//
+// Order restated (D/c/l2_avx256_amd64.c:14-107, D/c/dot_avx256_amd64.c:14-104):
+//   n < 8      : sequential scalar loop into `sum` (L2 unfused mul+add,
+//                dot fused vfmadd231ss per the shipped asm)
+//   32-blocks  : acc[j][l] = fma(.., acc[j][l]) for element 32b + 8j + l
+//   8-blocks   : acc[0][l] for element 32nb + 8t + l
+//   tail (<8)  : scalar into `sum`
+//   reduce     : s_l = (acc3+acc2)+(acc1+acc0); ((s0+s1)+(s2+s3)) + ((s4+s5)+(s6+s7)); sum += .
+//
+// The compilation unit must be built with -ffp-contract=off: every fused
+// operation below is an explicit __builtin_fmaf.
+#pragma once
+
+#include "wvg_common.hpp"
+
+namespace wvg {
+
+template <int METRIC>
+__device__ __forceinline__ void acc_update(float &acc, float q, float x)
+{
+    if constexpr (METRIC == WVG_M_L2) {
+        float diff = q - x;
+        acc = __builtin_fmaf(diff, diff, acc);
+    } else {
+        acc = __builtin_fmaf(q, x, acc);
+    }
+}
+
+template <int METRIC>
+__device__ __forceinline__ void scalar_update(float &sum, float q, float x)
+{
+    if constexpr (METRIC == WVG_M_L2) {
+        float diff = q - x;
+        float sq = diff * diff;
+        sum = sum + sq;
+    } else {
+        sum = __builtin_fmaf(q, x, sum);
+    }
+}
+
+__device__ __forceinline__ float avx256_reduce(const float (&acc)[4][8], float sum)
+{
+    float s[8];
+#pragma unroll
+    for (int l = 0; l < 8; l++) {
+        float a01 = acc[1][l] + acc[0][l];
+        float a23 = acc[3][l] + acc[2][l];
+        s[l] = a23 + a01;
+    }
+    float lo = (s[0] + s[1]) + (s[2] + s[3]);
+    float hi = (s[4] + s[5]) + (s[6] + s[7]);
+    return sum + (lo + hi);
+}
+
+template <int METRIC>
+__device__ __forceinline__ void chunk_update(float (&acc)[4][8], int cc, float4 q, float4 x)
+{
+    const int j = cc >> 1, l0 = (cc & 1) * 4;
+    acc_update<METRIC>(acc[j][l0 + 0], q.x, x.x);
+    acc_update<METRIC>(acc[j][l0 + 1], q.y, x.y);
+    acc_update<METRIC>(acc[j][l0 + 2], q.z, x.z);
+    acc_update<METRIC>(acc[j][l0 + 3], q.w, x.w);
+}
+
+// p: chunk 0 of this lane's row; consecutive chunks are CSTRIDE float4 apart
+// (64 in the tiled corpus).  q: the query, 16-byte aligned, padded to 4.
+template <int METRIC, int D, int CSTRIDE>
+__device__ __forceinline__ float row_dot_or_l2_fixed(const float4 *__restrict__ p,
+                                                     const float4 *__restrict__ q)
+{
+    static_assert(D % 32 == 0 && D >= 32, "fixed path needs D % 32 == 0");
+    float acc[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+#pragma unroll
+        for (int l = 0; l < 8; l++) acc[j][l] = 0.0f;
+    constexpr int NB = D / 32;
+    constexpr int UNROLL = NB <= 4 ? NB : 2;
+#pragma unroll UNROLL
+    for (int b = 0; b < NB; b++) {
+        float4 xs[8];
+#pragma unroll
+        for (int cc = 0; cc < 8; cc++) xs[cc] = p[(size_t)(b * 8 + cc) * CSTRIDE];
+#pragma unroll
+        for (int cc = 0; cc < 8; cc++) chunk_update<METRIC>(acc, cc, q[b * 8 + cc], xs[cc]);
+    }
+    return avx256_reduce(acc, 0.0f);
+}
+
+template <int CSTRIDE>
+__device__ __forceinline__ float elem_at(const float4 *__restrict__ p, int pos)
+{
+    const float *c = reinterpret_cast<const float *>(p + (size_t)(pos >> 2) * CSTRIDE);
+    return c[pos & 3];
+}
+
+template <int METRIC, int CSTRIDE>
+__device__ __forceinline__ float row_dot_or_l2_generic(const float4 *__restrict__ p,
+                                                       const float4 *__restrict__ q4, int n)
+{
+    const float *q = reinterpret_cast<const float *>(q4);
+    float sum = 0.0f;
+    if (n < 8) {
+        for (int i = 0; i < n; i++) scalar_update<METRIC>(sum, q[i], elem_at<CSTRIDE>(p, i));
+        return sum;
+    }
+    float acc[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+#pragma unroll
+        for (int l = 0; l < 8; l++) acc[j][l] = 0.0f;
+    const int nb = n >> 5;
+    for (int b = 0; b < nb; b++) {
+        float4 xs[8];
+#pragma unroll
+        for (int cc = 0; cc < 8; cc++) xs[cc] = p[(size_t)(b * 8 + cc) * CSTRIDE];
+#pragma unroll
+        for (int cc = 0; cc < 8; cc++) chunk_update<METRIC>(acc, cc, q4[b * 8 + cc], xs[cc]);
+    }
+    int pos = nb * 32;
+    int rem = n - pos;
+    while (rem >= 8) {
+        const int c = pos >> 2;
+        float4 x0 = p[(size_t)c * CSTRIDE], x1 = p[(size_t)(c + 1) * CSTRIDE];
+        chunk_update<METRIC>(acc, 0, q4[c], x0);  // acc[0][0..3]
+        chunk_update<METRIC>(acc, 1, q4[c + 1], x1);  // acc[0][4..7]
+        pos += 8;
+        rem -= 8;
+    }
+    while (rem) {
+        scalar_update<METRIC>(sum, q[pos], elem_at<CSTRIDE>(p, pos));
+        pos++;
+        rem--;
+    }
+    return avx256_reduce(acc, sum);
+}
+
+// Provider.Wrap of the raw kernel value: L2 identity, dot -x (D/dot_product.go:68-76),
+// cosine-dot 1-x (D/cosine_dist.go:38-45).
+__device__ __forceinline__ float wrap_metric(int metric, float r)
+{
+    return metric == WVG_M_L2 ? r : (metric == WVG_M_DOT ? -r : 1.0f - r);
+}
+
+}  // namespace wvg

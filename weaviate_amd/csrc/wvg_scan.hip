@@ -1,0 +1,477 @@
+// wvg_scan.hip -- K1 fp32 flat scan fused with wave-level top-k (phase 1),
+// K2 top-k merge (phase 2), and the tiled-layout helpers for F32 corpora.
+//
+// Reference path replaced: flat.searchByVector -> findTopVectors
+// (V/flat/index.go:319-334, 411-452): for every live (and allowed) docID in
+// ascending order, SingleDist(query, row) and insertToHeap(k).
+//
+// Phase 1: each wave owns a contiguous range of 64-row tiles.  Lane = row.
+// One global_load_dwordx4 per chunk reads 1 KiB of the tile; the lane folds
+// its row in the AVX2 order (wvg_rowdist.hpp) and offers (dist, slot) to the
+// wave's register top-k.  The workgroup merges its waves' lists in LDS and
+// writes K keys per (query, workgroup).  Phase 2 merges those lists.
+// Roofline: HBM, N*d*4 bytes per query.
+#include "wvg_internal.hpp"
+#include "wvg_rowdist.hpp"
+#include "wvg_topk.hpp"
+
+namespace wvg {
+
+constexpr int SCAN_WAVES = 4;
+
+// Per-tile mask of live, allowed rows (one 64-bit word per tile = one bit per lane).
+__device__ __forceinline__ uint64_t tile_mask(const ScanArgs &a, uint64_t t)
+{
+    uint64_t m = a.valid[t];
+    if (a.allow) {
+        uint64_t w = (a.id_base >> 6) + t;
+        m &= w < a.allow_words ? a.allow[w] : 0ull;
+    }
+    return m;
+}
+
+__device__ __forceinline__ void wave_range(const ScanArgs &a, int waves_per_group, uint64_t &t0,
+                                           uint64_t &t1)
+{
+    const uint64_t ntiles = a.tile_end - a.tile_begin;
+    const uint64_t total = (uint64_t)gridDim.x * waves_per_group;
+    const uint64_t gw = (uint64_t)blockIdx.x * waves_per_group + (threadIdx.x >> 6);
+    t0 = a.tile_begin + ntiles * gw / total;
+    t1 = a.tile_begin + ntiles * (gw + 1) / total;
+}
+
+// Workgroup combine: wave lists -> one sorted list, wave 0 writes K keys.
+template <int E, int WAVES>
+__device__ __forceinline__ void group_combine_store(WaveTopK<E> &tk, uint64_t *out)
+{
+    __shared__ uint64_t sh[WAVES][64 * E];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int e = 0; e < E; e++) sh[wave][e * 64 + lane] = tk.l[e];
+    __syncthreads();
+    if (wave == 0) {
+        for (int w = 1; w < WAVES; w++) {
+            uint64_t o[E];
+#pragma unroll
+            for (int e = 0; e < E; e++) o[e] = sh[w][e * 64 + lane];
+            merge_lists<E>(tk.l, o);
+        }
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            const int i = e * 64 + lane;
+            if (i < tk.k) out[i] = tk.l[e];
+        }
+    }
+}
+
+template <int METRIC, int D, int E>
+__global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_kernel(ScanArgs a, uint64_t *partials)
+{
+    const int lane = threadIdx.x & 63;
+    const uint32_t qi = blockIdx.y;
+    const float4 *q4 = reinterpret_cast<const float4 *>(a.queries) + (size_t)qi * (a.qpitch / 4);
+    const float4 *data = reinterpret_cast<const float4 *>(a.data);
+    uint64_t t0, t1;
+    wave_range(a, SCAN_WAVES, t0, t1);
+    WaveTopK<E> tk;
+    tk.init((int)a.k);
+    for (uint64_t t = t0; t < t1; ++t) {
+        const uint64_t m = tile_mask(a, t);
+        if (m == 0ull) continue;  // wave-uniform: nothing live/allowed in this tile
+        const float4 *rp = data + (size_t)t * a.nchunks * 64 + lane;
+        float r;
+        if constexpr (D > 0)
+            r = row_dot_or_l2_fixed<METRIC, D, 64>(rp, q4);
+        else
+            r = row_dot_or_l2_generic<METRIC, 64>(rp, q4, (int)a.dim);
+        const float dist = wrap_metric(a.metric, r);
+        const uint64_t key = ((m >> lane) & 1ull) ? wvg_make_key(dist, (uint32_t)(t * 64 + lane)) : WVG_KEY_NONE;
+        tk.offer(key);
+    }
+    group_combine_store<E, SCAN_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
+}
+
+int scan_groups_for(const ScanArgs &a, int num_cus)
+{
+    const uint64_t ntiles = a.tile_end > a.tile_begin ? a.tile_end - a.tile_begin : 0;
+    uint64_t g = (ntiles + SCAN_WAVES * 4 - 1) / (SCAN_WAVES * 4);
+    uint64_t cap = (uint64_t)num_cus * 4;
+    if (a.nq > 1) cap = std::max<uint64_t>((uint64_t)num_cus / 4, cap / a.nq);
+    if (g > cap) g = cap;
+    if (g < 1) g = 1;
+    return (int)g;
+}
+
+template <int METRIC, int E>
+static hipError_t launch_f32_e(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
+{
+    dim3 grid(groups, a.nq), block(SCAN_WAVES * 64);
+    switch (a.dim) {
+    case 128: hipLaunchKernelGGL((scan_f32_kernel<METRIC, 128, E>), grid, block, 0, s, a, partials); break;
+    case 768: hipLaunchKernelGGL((scan_f32_kernel<METRIC, 768, E>), grid, block, 0, s, a, partials); break;
+    case 1536: hipLaunchKernelGGL((scan_f32_kernel<METRIC, 1536, E>), grid, block, 0, s, a, partials); break;
+    default: hipLaunchKernelGGL((scan_f32_kernel<METRIC, 0, E>), grid, block, 0, s, a, partials); break;
+    }
+    return hipGetLastError();
+}
+
+template <int METRIC>
+static hipError_t launch_f32_m(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
+{
+    if (a.k <= 64) return launch_f32_e<METRIC, 1>(a, partials, groups, s);
+    if (a.k <= 128) return launch_f32_e<METRIC, 2>(a, partials, groups, s);
+    return launch_f32_e<METRIC, 4>(a, partials, groups, s);
+}
+
+hipError_t launch_scan_f32(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
+{
+    if (a.metric == WVG_M_L2) return launch_f32_m<WVG_M_L2>(a, partials, groups, s);
+    return launch_f32_m<WVG_M_DOT>(a, partials, groups, s);
+}
+
+// ---------------------------------------------------------------------------
+// Phase 2: [nq][n_per_query] keys -> final ids / dists / counts.
+// ---------------------------------------------------------------------------
+template <int E>
+__global__ __launch_bounds__(SCAN_WAVES * 64) void merge_keys_kernel(const uint64_t *partials,
+                                                                     uint32_t n_per_query, uint32_t k,
+                                                                     uint64_t id_base, uint64_t *ids,
+                                                                     float *dists, uint32_t *counts)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t qi = blockIdx.x;
+    const uint64_t *src = partials + (size_t)qi * n_per_query;
+    WaveTopK<E> tk;
+    tk.init((int)k);
+    for (uint32_t base = wave * 64; base < n_per_query; base += SCAN_WAVES * 64) {
+        const uint32_t i = base + lane;
+        tk.offer(i < n_per_query ? src[i] : WVG_KEY_NONE);
+    }
+    __shared__ uint64_t sh[SCAN_WAVES][64 * E];
+#pragma unroll
+    for (int e = 0; e < E; e++) sh[wave][e * 64 + lane] = tk.l[e];
+    __syncthreads();
+    if (wave != 0) return;
+    for (int w = 1; w < SCAN_WAVES; w++) {
+        uint64_t o[E];
+#pragma unroll
+        for (int e = 0; e < E; e++) o[e] = sh[w][e * 64 + lane];
+        merge_lists<E>(tk.l, o);
+    }
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const uint32_t i = e * 64 + lane;
+        const uint64_t key = tk.l[e];
+        const bool live = i < k && key != WVG_KEY_NONE;
+        cnt += (uint32_t)__popcll(__ballot(live));
+        if (i < k) {
+            ids[(size_t)qi * k + i] = live ? id_base + (key & 0xFFFFFFFFull) : WVG_KEY_NONE;
+            dists[(size_t)qi * k + i] = live ? wvg_unord_f32((uint32_t)(key >> 32)) : __builtin_inff();
+        }
+    }
+    if (lane == 0 && counts) counts[qi] = cnt;
+}
+
+hipError_t launch_merge_keys(const uint64_t *partials, uint32_t nq, uint32_t n_per_query, uint32_t k,
+                             uint64_t id_base, uint64_t *ids, float *dists, uint32_t *counts,
+                             hipStream_t s)
+{
+    dim3 grid(nq), block(SCAN_WAVES * 64);
+    if (k <= 64)
+        hipLaunchKernelGGL((merge_keys_kernel<1>), grid, block, 0, s, partials, n_per_query, k, id_base, ids, dists, counts);
+    else if (k <= 128)
+        hipLaunchKernelGGL((merge_keys_kernel<2>), grid, block, 0, s, partials, n_per_query, k, id_base, ids, dists, counts);
+    else
+        hipLaunchKernelGGL((merge_keys_kernel<4>), grid, block, 0, s, partials, n_per_query, k, id_base, ids, dists, counts);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Multi-shard merge of (dist, id64) lists: one workgroup per query, bitonic
+// sort in LDS of all nlists*k_in pairs ordered by (dist, id).  Used after the
+// RCCL all-gather of per-GPU top-k (adapters/repos/db/index.go:1644-1648).
+// ---------------------------------------------------------------------------
+constexpr int MERGE_PAIRS_MAX = 8192;
+
+__global__ __launch_bounds__(1024) void merge_pairs_kernel(const float *dists, const uint64_t *ids,
+                                                           uint32_t nlists, uint32_t k_in, uint32_t k,
+                                                           uint32_t pow2, uint64_t *out_ids,
+                                                           float *out_dists, uint32_t *out_counts)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint64_t *sid = reinterpret_cast<uint64_t *>(smem);
+    uint32_t *sd = reinterpret_cast<uint32_t *>(smem + (size_t)pow2 * 8);
+    const uint32_t qi = blockIdx.x;
+    const uint32_t n = nlists * k_in;
+    for (uint32_t i = threadIdx.x; i < pow2; i += blockDim.x) {
+        if (i < n) {
+            const uint32_t l = i / k_in, j = i % k_in;
+            const size_t src = ((size_t)l * gridDim.x + qi) * k_in + j;  // [nlists][nq][k_in]
+            const uint64_t id = ids[src];
+            sid[i] = id;
+            sd[i] = id == WVG_KEY_NONE ? 0xFFFFFFFFu : wvg_ord_f32(dists[src]);
+        } else {
+            sid[i] = WVG_KEY_NONE;
+            sd[i] = 0xFFFFFFFFu;
+        }
+    }
+    __syncthreads();
+    for (uint32_t size = 2; size <= pow2; size <<= 1) {
+        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+            for (uint32_t i = threadIdx.x; i < pow2; i += blockDim.x) {
+                const uint32_t j = i ^ stride;
+                if (j > i) {
+                    const bool asc = (i & size) == 0;
+                    const bool gt = sd[i] > sd[j] || (sd[i] == sd[j] && sid[i] > sid[j]);
+                    if (gt == asc) {
+                        uint32_t td = sd[i]; sd[i] = sd[j]; sd[j] = td;
+                        uint64_t ti = sid[i]; sid[i] = sid[j]; sid[j] = ti;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    __shared__ uint32_t live_count;
+    if (threadIdx.x == 0) live_count = 0;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < k; i += blockDim.x) {
+        const bool live = i < n && sid[i] != WVG_KEY_NONE;
+        out_ids[(size_t)qi * k + i] = live ? sid[i] : WVG_KEY_NONE;
+        out_dists[(size_t)qi * k + i] = live ? wvg_unord_f32(sd[i]) : __builtin_inff();
+        if (live) atomicAdd(&live_count, 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && out_counts) out_counts[qi] = live_count;
+}
+
+hipError_t launch_merge_pairs(const float *dists, const uint64_t *ids, uint32_t nq, uint32_t nlists,
+                              uint32_t k_in, uint32_t k, uint64_t *out_ids, float *out_dists,
+                              uint32_t *out_counts, hipStream_t s)
+{
+    uint32_t n = nlists * k_in, pow2 = 1;
+    while (pow2 < n) pow2 <<= 1;
+    if (pow2 > (uint32_t)MERGE_PAIRS_MAX) return hipErrorInvalidValue;
+    const size_t lds = (size_t)pow2 * 12;
+    hipLaunchKernelGGL(merge_pairs_kernel, dim3(nq), dim3(1024), lds, s, dists, ids, nlists, k_in, k, pow2,
+                       out_ids, out_dists, out_counts);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Layout helpers
+// ---------------------------------------------------------------------------
+
+// distancer.Normalize (D/normalize.go:16-32), one lane per row: sequential
+// unfused fp32 sum of squares, float32(sqrt(float64)), element-wise divide.
+__global__ void normalize_rows_kernel(const float *in, uint64_t n, uint32_t dim, float *out)
+{
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const float *v = in + r * dim;
+    float *o = out + r * dim;
+    float norm = 0.0f;
+    for (uint32_t i = 0; i < dim; i++) {
+        float p = v[i] * v[i];
+        norm = norm + p;
+    }
+    if (norm == 0.0f) {
+        for (uint32_t i = 0; i < dim; i++) o[i] = 0.0f;
+        return;
+    }
+    norm = (float)__builtin_sqrt((double)norm);
+    for (uint32_t i = 0; i < dim; i++) o[i] = v[i] / norm;
+}
+
+hipError_t launch_normalize_rows(const float *in, uint64_t n, uint32_t dim, float *out, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(normalize_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in, n, dim, out);
+    return hipGetLastError();
+}
+
+// Row-major [n][dim] -> tiled chunks at slots[i] (identity when slots == null).
+__global__ void f32_store_kernel(const float *rows, const uint64_t *slots, uint64_t n, uint32_t dim,
+                                 uint32_t nchunks, float4 *tiled)
+{
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n * nchunks) return;
+    const uint64_t i = g / nchunks;
+    const uint32_t c = (uint32_t)(g % nchunks);
+    const uint64_t slot = slots ? slots[i] : i;
+    const float *src = rows + i * dim;
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        const uint32_t p = c * 4 + e;
+        v[e] = p < dim ? src[p] : 0.0f;
+    }
+    tiled[((slot >> 6) * nchunks + c) * 64 + (slot & 63)] = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+hipError_t launch_f32_store(const float *rows, const uint64_t *slots, uint64_t n, uint32_t dim,
+                            uint32_t nchunks, int normalize, float *tiled, hipStream_t s)
+{
+    (void)normalize;  // rows are normalized by the caller (launch_normalize_rows)
+    const uint64_t total = n * nchunks;
+    if (total == 0) return hipSuccess;
+    hipLaunchKernelGGL(f32_store_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, rows, slots, n,
+                       dim, nchunks, reinterpret_cast<float4 *>(tiled));
+    return hipGetLastError();
+}
+
+// Synthetic rows generated in place; for cosine the row is normalized with
+// the same sequential order as Normalize (two passes over the generator).
+__global__ void f32_synth_kernel(uint64_t seed_mixed, int dist, uint64_t row0, uint64_t n, uint64_t slot0,
+                                 uint32_t dim, uint32_t nchunks, int normalize, float4 *tiled)
+{
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const uint64_t row = row0 + r, slot = slot0 + r;
+    float norm = 1.0f;
+    bool zero = false;
+    if (normalize) {
+        float acc = 0.0f;
+        for (uint32_t i = 0; i < dim; i++) {
+            float v = wvg_synth_value(seed_mixed, row, i, dist);
+            float p = v * v;
+            acc = acc + p;
+        }
+        zero = acc == 0.0f;
+        norm = (float)__builtin_sqrt((double)acc);
+    }
+    float4 *dst = tiled + ((slot >> 6) * nchunks) * 64 + (slot & 63);
+    for (uint32_t c = 0; c < nchunks; c++) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const uint32_t p = c * 4 + e;
+            float x = p < dim ? wvg_synth_value(seed_mixed, row, p, dist) : 0.0f;
+            if (normalize) x = zero ? 0.0f : x / norm;
+            v[e] = x;
+        }
+        dst[(size_t)c * 64] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+}
+
+hipError_t launch_f32_synth(uint64_t seed, int dist, uint64_t row0, uint64_t n, uint64_t slot0, uint32_t dim,
+                            uint32_t nchunks, int normalize, float *tiled, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(f32_synth_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, wvg_mix64(seed), dist,
+                       row0, n, slot0, dim, nchunks, normalize, reinterpret_cast<float4 *>(tiled));
+    return hipGetLastError();
+}
+
+__global__ void f32_gather_kernel(const float4 *tiled, const uint64_t *slots, uint64_t n, uint32_t dim,
+                                  uint32_t nchunks, float *rows)
+{
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n * dim) return;
+    const uint64_t i = g / dim;
+    const uint32_t p = (uint32_t)(g % dim);
+    const uint64_t slot = slots[i];
+    const float4 *row = tiled + ((slot >> 6) * nchunks) * 64 + (slot & 63);
+    rows[g] = elem_at<64>(row, (int)p);
+}
+
+hipError_t launch_f32_gather(const float *tiled, const uint64_t *slots, uint64_t n, uint32_t dim,
+                             uint32_t nchunks, float *rows, hipStream_t s)
+{
+    const uint64_t total = n * dim;
+    if (total == 0) return hipSuccess;
+    hipLaunchKernelGGL(f32_gather_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                       reinterpret_cast<const float4 *>(tiled), slots, n, dim, nchunks, rows);
+    return hipGetLastError();
+}
+
+// Provider.SingleDist(q, X[i]) for a tiled temporary (distancer.BatchProvider).
+template <int METRIC>
+__global__ void distance_tiled_kernel(int metric, const float4 *q4, const float4 *tiled, uint64_t n, uint32_t dim,
+                                      uint32_t nchunks, float *out)
+{
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const float4 *rp = tiled + ((r >> 6) * nchunks) * 64 + (r & 63);
+    out[r] = wrap_metric(metric, row_dot_or_l2_generic<METRIC, 64>(rp, q4, (int)dim));
+}
+
+hipError_t launch_distance_rows(int metric, const float *q, const float *tiled, uint64_t n, uint32_t dim,
+                                float *out, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    const uint32_t nchunks = f32_chunks(dim);
+    dim3 grid((unsigned)((n + 255) / 256)), block(256);
+    if (metric == WVG_M_L2)
+        hipLaunchKernelGGL((distance_tiled_kernel<WVG_M_L2>), grid, block, 0, s, metric,
+                           reinterpret_cast<const float4 *>(q), reinterpret_cast<const float4 *>(tiled), n, dim,
+                           nchunks, out);
+    else
+        hipLaunchKernelGGL((distance_tiled_kernel<WVG_M_DOT>), grid, block, 0, s, metric,
+                           reinterpret_cast<const float4 *>(q), reinterpret_cast<const float4 *>(tiled), n, dim,
+                           nchunks, out);
+    return hipGetLastError();
+}
+
+// Exact rescore of candidate keys (slot in the low 32 bits) against the tiled
+// float rows: the rescore loop of flat.searchByVectorBQ (V/flat/index.go:375-385).
+template <int METRIC>
+__global__ void rescore_keys_kernel(int metric, const float4 *q4, uint32_t qpitch, const float4 *tiled, uint32_t dim,
+                                    uint32_t nchunks, const uint64_t *cand, uint32_t ncand, uint32_t cand_stride,
+                                    uint64_t *out)
+{
+    const uint32_t qi = blockIdx.y;
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= ncand) return;
+    const uint64_t key = cand[(size_t)qi * cand_stride + j];
+    uint64_t res = WVG_KEY_NONE;
+    if (key != WVG_KEY_NONE) {
+        const uint32_t slot = (uint32_t)key;
+        const float4 *rp = tiled + ((size_t)(slot >> 6) * nchunks) * 64 + (slot & 63);
+        const float4 *q = q4 + (size_t)qi * (qpitch / 4);
+        const float d = wrap_metric(metric, row_dot_or_l2_generic<METRIC, 64>(rp, q, (int)dim));
+        res = wvg_make_key(d, slot);
+    }
+    out[(size_t)qi * ncand + j] = res;
+}
+
+hipError_t launch_rescore_keys(int metric, const float *q, uint32_t qpitch, const float *tiled, uint32_t dim,
+                               uint32_t nchunks, const uint64_t *cand_keys, uint32_t nq, uint32_t ncand,
+                               uint32_t cand_stride, uint64_t *out_keys, hipStream_t s)
+{
+    if (nq == 0 || ncand == 0) return hipSuccess;
+    dim3 grid((ncand + 63) / 64, nq), block(64);
+    if (metric == WVG_M_L2)
+        hipLaunchKernelGGL((rescore_keys_kernel<WVG_M_L2>), grid, block, 0, s, metric,
+                           reinterpret_cast<const float4 *>(q), qpitch, reinterpret_cast<const float4 *>(tiled), dim,
+                           nchunks, cand_keys, ncand, cand_stride, out_keys);
+    else
+        hipLaunchKernelGGL((rescore_keys_kernel<WVG_M_DOT>), grid, block, 0, s, metric,
+                           reinterpret_cast<const float4 *>(q), qpitch, reinterpret_cast<const float4 *>(tiled), dim,
+                           nchunks, cand_keys, ncand, cand_stride, out_keys);
+    return hipGetLastError();
+}
+
+// Validity bits (flat.Add sets, flat.Delete clears; V/flat/index.go:247-295).
+__global__ void set_valid_kernel(unsigned long long *valid, const uint64_t *slots, uint64_t n, int set)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t s = slots[i];
+    const unsigned long long bit = 1ull << (s & 63);
+    if (set)
+        atomicOr(valid + (s >> 6), bit);
+    else
+        atomicAnd(valid + (s >> 6), ~bit);
+}
+
+hipError_t launch_set_valid(uint64_t *valid, const uint64_t *slots, uint64_t n, int set, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(set_valid_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                       reinterpret_cast<unsigned long long *>(valid), slots, n, set);
+    return hipGetLastError();
+}
+
+}  // namespace wvg

@@ -1,0 +1,153 @@
+"""Device context and device-resident corpora (handles of the C ABI).
+
+One :class:`Context` per GPU; the multi-GPU deployment runs one process per
+GPU (see weaviate_amd/shard.py).
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import byref, c_int, c_uint64, c_void_p
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, fptr, u32ptr, u64ptr
+
+
+def device_count() -> int:
+    lib = _lib.load()
+    n = c_int(0)
+    check(lib.wvg_device_count(byref(n)))
+    return n.value
+
+
+class Context:
+    """wvg_open / wvg_close."""
+
+    def __init__(self, device: int = 0):
+        self.lib = _lib.load()
+        h = c_void_p()
+        check(self.lib.wvg_open(device, byref(h)))
+        self.handle = h
+        self.device = device
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.wvg_close(self.handle)
+            self.handle = c_void_p()
+
+    def synchronize(self) -> None:
+        check(self.lib.wvg_synchronize(self.handle))
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def allow_bitmap(ids, n_bits: int | None = None) -> np.ndarray:
+    """helpers.AllowList -> bitmap over global docIDs (bit i of word i/64)."""
+    ids = np.asarray(list(ids), dtype=np.uint64)
+    top = int(ids.max()) + 1 if ids.size else 0
+    n_bits = max(n_bits or 0, top)
+    words = np.zeros((n_bits + 63) // 64, dtype=np.uint64)
+    if ids.size:
+        np.bitwise_or.at(words, (ids >> np.uint64(6)).astype(np.int64),
+                         np.left_shift(np.uint64(1), ids & np.uint64(63)))
+    return words
+
+
+class Corpus:
+    """A device-resident corpus (wvg_corpus_*): F32 rows, BQ codes or PQ codes."""
+
+    def __init__(self, ctx: Context, kind: int, metric: int, dim: int, capacity: int, id_base: int = 0):
+        self.ctx = ctx
+        self.lib = ctx.lib
+        self.kind, self.metric, self.dim, self.id_base = kind, metric, dim, id_base
+        h = c_void_p()
+        check(self.lib.wvg_corpus_create(ctx.handle, kind, metric, dim, id_base, capacity, byref(h)))
+        self.handle = h
+
+    def destroy(self) -> None:
+        if self.handle:
+            self.lib.wvg_corpus_destroy(self.handle)
+            self.handle = c_void_p()
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+    def info(self):
+        cnt, hw, cap = c_uint64(), c_uint64(), c_uint64()
+        check(self.lib.wvg_corpus_info(self.handle, byref(cnt), byref(hw), byref(cap)))
+        return cnt.value, hw.value, cap.value
+
+    def reserve(self, capacity: int) -> None:
+        check(self.lib.wvg_corpus_reserve(self.handle, capacity))
+
+    def upsert(self, ids, vectors) -> None:
+        ids = np.ascontiguousarray(ids, dtype=np.uint64)
+        vectors = np.ascontiguousarray(vectors, dtype=np.float32)
+        if vectors.ndim == 1:
+            vectors = vectors[None, :]
+        check(self.lib.wvg_corpus_upsert(self.handle, u64ptr(ids), fptr(vectors), len(ids),
+                                         vectors.shape[1] if vectors.size else self.dim))
+
+    def upsert_codes(self, ids, codes) -> None:
+        ids = np.ascontiguousarray(ids, dtype=np.uint64)
+        codes = np.ascontiguousarray(codes)
+        check(self.lib.wvg_corpus_upsert_codes(self.handle, u64ptr(ids), codes.ctypes.data_as(c_void_p), len(ids)))
+
+    def delete(self, ids) -> None:
+        ids = np.ascontiguousarray(ids, dtype=np.uint64)
+        check(self.lib.wvg_corpus_delete(self.handle, u64ptr(ids), len(ids)))
+
+    def get(self, id_: int, pq_m: int = 0) -> np.ndarray:
+        if self.kind == _lib.KIND_F32:
+            out = np.empty(self.dim, dtype=np.float32)
+        elif self.kind == _lib.KIND_BQ:
+            out = np.empty((self.dim + 63) // 64, dtype=np.uint64)
+        else:
+            out = np.empty(pq_m, dtype=np.uint8)
+        check(self.lib.wvg_corpus_get(self.handle, id_, out.ctypes.data_as(c_void_p)))
+        return out
+
+    def fill_synthetic(self, seed: int, n: int, distribution: int = 0) -> None:
+        check(self.lib.wvg_corpus_fill_synthetic(self.handle, seed, n, distribution))
+
+    def set_codebook(self, centers) -> None:
+        centers = np.ascontiguousarray(centers, dtype=np.float32)
+        m, ks, _ = centers.shape
+        check(self.lib.wvg_pq_set_codebook(self.handle, fptr(centers), m, ks))
+
+    def search(self, queries, k: int, allow=None):
+        """wvg_search: returns (ids [nq][k], dists [nq][k], counts [nq])."""
+        q = np.ascontiguousarray(queries, dtype=np.float32)
+        if q.ndim == 1:
+            q = q[None, :]
+        nq = q.shape[0]
+        ids = np.empty((nq, k), dtype=np.uint64)
+        dists = np.empty((nq, k), dtype=np.float32)
+        counts = np.empty(nq, dtype=np.uint32)
+        aw, an = (None, 0) if allow is None else (np.ascontiguousarray(allow, dtype=np.uint64), len(allow))
+        check(self.lib.wvg_search(self.handle, fptr(q), nq, k, u64ptr(aw) if aw is not None else None, an,
+                                  u64ptr(ids), fptr(dists), u32ptr(counts)))
+        return ids, dists, counts
+
+
+def search_bq_rescore(bq: Corpus, f32: Corpus, queries, k: int, rescore_limit: int, allow=None):
+    q = np.ascontiguousarray(queries, dtype=np.float32)
+    if q.ndim == 1:
+        q = q[None, :]
+    nq = q.shape[0]
+    ids = np.empty((nq, k), dtype=np.uint64)
+    dists = np.empty((nq, k), dtype=np.float32)
+    counts = np.empty(nq, dtype=np.uint32)
+    aw, an = (None, 0) if allow is None else (np.ascontiguousarray(allow, dtype=np.uint64), len(allow))
+    check(bq.lib.wvg_search_bq_rescore(bq.handle, f32.handle, fptr(q), nq, k, rescore_limit,
+                                       u64ptr(aw) if aw is not None else None, an,
+                                       u64ptr(ids), fptr(dists), u32ptr(counts)))
+    return ids, dists, counts

@@ -1,0 +1,137 @@
+"""Mirror of Weaviate's flat vector index (``db.VectorIndex`` implemented by
+``*flat``) with its scans on the GPU.
+
+Reference: adapters/repos/db/vector/flat/index.go
+  Add :247, AddBatch :197, Delete :276, SearchByVector :307,
+  searchByVector :319, searchByVectorBQ :347, searchTimeRescore :297,
+  SearchByVectorDistance :531; interface adapters/repos/db/vector_index.go:24-45.
+
+The device-resident corpus replaces the LSM "vectors" / "vectors_compressed"
+buckets for scoring (the LSM stays the source of truth in Weaviate; here the
+caller owns persistence).  Results are ascending by (distance, docID).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from ._lib import KIND_BQ, KIND_F32, METRIC_BY_NAME, WVG_ERR_DIM_MISMATCH, WvgError
+from .device import Corpus, allow_bitmap, search_bq_rescore
+from .distancer import provider_for
+
+DEFAULT_SEARCH_BY_DIST_INITIAL_LIMIT = 100  # V/common/search_by_dist_params.go:17
+DEFAULT_SEARCH_BY_DIST_LIMIT_MULTIPLIER = 10  # :23
+
+
+class AllowList:
+    """helpers.AllowList (adapters/repos/db/helpers/allow_list.go:19-40) over docIDs."""
+
+    def __init__(self, *ids):
+        self.ids = set(int(i) for i in ids)
+
+    def Insert(self, *ids):
+        self.ids.update(int(i) for i in ids)
+
+    def Contains(self, i):
+        return int(i) in self.ids
+
+    def IsEmpty(self):
+        return not self.ids
+
+    def Len(self):
+        return len(self.ids)
+
+    def bitmap(self):
+        return allow_bitmap(sorted(self.ids))
+
+
+class FlatIndex:
+    def __init__(self, ctx, dims: int, distance: str = "cosine", compression: str | None = None,
+                 rescore_limit: int = -1, capacity: int = 1 << 16, id_base: int = 0):
+        self.ctx = ctx
+        self.dims = dims
+        self.distance = distance
+        self.provider = provider_for(ctx, distance)
+        self.metric = METRIC_BY_NAME[distance]
+        self.compression = compression
+        self.rescore = rescore_limit
+        self.vectors = Corpus(ctx, KIND_F32, self.metric, dims, capacity, id_base)
+        self.bq = Corpus(ctx, KIND_BQ, self.metric, dims, capacity, id_base) if compression == "bq" else None
+
+    # --- writes ------------------------------------------------------------
+    def _grow(self, max_id: int):
+        _, _, cap = self.vectors.info()
+        if max_id - self.vectors.id_base >= cap:
+            new_cap = max(cap * 2, max_id - self.vectors.id_base + 1)
+            self.vectors.reserve(new_cap)
+            if self.bq is not None:
+                self.bq.reserve(new_cap)
+
+    def Add(self, id_: int, vector) -> None:
+        self.AddBatch([id_], [vector])
+
+    def AddBatch(self, ids, vectors) -> None:
+        ids = np.asarray(ids, dtype=np.uint64)
+        if len(ids) == 0:
+            raise ValueError("insertBatch called with empty lists")  # index.go:205-206
+        vectors = np.asarray(vectors, dtype=np.float32)
+        if vectors.ndim != 2 or vectors.shape[0] != len(ids):
+            raise ValueError("ids and vectors sizes does not match")  # index.go:202-203
+        if vectors.shape[1] != self.dims:
+            raise WvgError(WVG_ERR_DIM_MISMATCH, "insert called with a vector of the wrong size")
+        self._grow(int(ids.max()))
+        self.vectors.upsert(ids, vectors)
+        if self.bq is not None:
+            self.bq.upsert(ids, vectors)
+
+    def Delete(self, *ids) -> None:
+        ids = np.asarray(ids, dtype=np.uint64)
+        self.vectors.delete(ids)
+        if self.bq is not None:
+            self.bq.delete(ids)
+
+    # --- reads -------------------------------------------------------------
+    def DistancerProvider(self):
+        return self.provider
+
+    def searchTimeRescore(self, k: int) -> int:
+        return self.rescore if self.rescore > k else k
+
+    def SearchByVector(self, vector, k: int, allow: AllowList | None = None):
+        if k < 0:
+            raise ValueError("k must be >= 0")
+        bm = allow.bitmap() if allow is not None else None
+        if allow is not None and allow.IsEmpty():
+            return np.empty(0, dtype=np.uint64), np.empty(0, dtype=np.float32)
+        if self.bq is not None:
+            ids, dists, counts = search_bq_rescore(self.bq, self.vectors, vector, k, self.searchTimeRescore(k), bm)
+        else:
+            ids, dists, counts = self.vectors.search(vector, k, bm)
+        n = int(counts[0])
+        return ids[0, :n], dists[0, :n]
+
+    def SearchByVectorDistance(self, vector, target: float, max_limit: int, allow: AllowList | None = None):
+        """index.go:531-591: growing limits until a distance above target appears."""
+        offset, limit = 0, DEFAULT_SEARCH_BY_DIST_INITIAL_LIMIT
+        total = offset + limit
+        res_ids, res_d = [], []
+        while True:
+            ids, dist = self.SearchByVector(vector, total, allow)
+            cont = not (len(ids) < total)
+            lo, hi = min(offset, len(ids)), min(total, len(ids))
+            if lo == hi:
+                break
+            for i in range(lo, hi):
+                if dist[i] <= target or abs(float(dist[i]) - float(target)) <= 1e-6:
+                    res_ids.append(int(ids[i]))
+                    res_d.append(float(dist[i]))
+                else:
+                    cont = False
+                    break
+            if not cont:
+                break
+            offset = total
+            limit *= DEFAULT_SEARCH_BY_DIST_LIMIT_MULTIPLIER
+            total = offset + limit
+            if max_limit >= 0 and total > max_limit:
+                break
+        return np.asarray(res_ids, dtype=np.uint64), np.asarray(res_d, dtype=np.float32)
