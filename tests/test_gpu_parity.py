@@ -407,6 +407,9 @@ def test_full_size_1m_x_128_properties(ctx, orc):
         # returned distances are bit-exact recomputations of the returned rows
         got_rows = all_rows[ids[qi].astype(np.int64)]
         assert np.array_equal(bits(orc.dist_all(0, qs[qi], got_rows)), bits(dists[qi]))
-        # nothing in a 20% sample beats the k-th result
+        # no sampled row outside the result beats the k-th result (lexicographic (dist, id))
         sd = orc.dist_all(0, qs[qi], srows)
-        assert np.all(orc.ord_key(sd) >= orc.ord_key(dists[qi][-1:])[0])
+        outside = ~np.isin(sample, ids[qi].astype(np.int64))
+        kth = (int(orc.ord_key(dists[qi][-1:])[0]), int(ids[qi][-1]))
+        sk = orc.ord_key(sd[outside]).astype(np.int64)
+        assert np.all((sk > kth[0]) | ((sk == kth[0]) & (sample[outside] > kth[1])))
