@@ -111,7 +111,7 @@ def main():
     dists = torch.empty((B, k), dtype=torch.float32, device=dev)
     counts = torch.empty(B, dtype=torch.int32, device=dev)
     ws_bytes = lib.wvg_search_workspace_size(corpus.handle, 1, k)
-    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=dev)  # zero-filled once; calls keep it armed
     if world > 1:
         g_d = torch.empty(world * B * k, dtype=torch.float32, device=dev)
         g_i = torch.empty(world * B * k, dtype=torch.int64, device=dev)

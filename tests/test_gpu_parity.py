@@ -216,6 +216,42 @@ def test_multi_query_batch(ctx, orc):
 
 
 # ---------------------------------------------------------------------------
+# K3: batched dot / cosine on fp32 MFMA (nq >= 32 routes there by default)
+@pytest.mark.parametrize("metric", [METRIC_DOT, METRIC_COSINE])
+@pytest.mark.parametrize("d", [32, 96, 128, 160, 768])
+def test_batched_mfma_parity(ctx, orc, metric, d):
+    n, nq = 3000 + 29, 40  # ragged rows; 40 queries = one full and one partial 32-query block
+    rows = orc.synth_rows(500 + d, 0, n, d, 0)
+    qs = orc.synth_rows(501 + d, 0, nq, d, 0)
+    c = Corpus(ctx, KIND_F32, metric, d, n)
+    c.upsert(np.arange(n, dtype=np.uint64), rows)
+    srows = stored_rows(orc, metric, rows)
+    valid = np.ones(n, np.uint8)
+    c.delete(np.array([3, 64, 65, 2000], np.uint64))
+    valid[[3, 64, 65, 2000]] = 0
+    for k in [1, 10, 100]:
+        ids, dists, counts = c.search(qs, k)
+        for qi in range(nq):
+            all_d = orc.dist_all(ORC_METRIC[metric], prep_query(orc, metric, qs[qi]), srows)
+            check_topk(orc, ids[qi], dists[qi], counts[qi], all_d, np.arange(n, dtype=np.uint64), k, valid)
+
+
+def test_batched_mfma_sift_like_ties_and_allow(ctx, orc):
+    n, d, nq, k = 9000, 128, 33, 50
+    rows = (orc.synth_rows(61, 0, n, d, 1) - 128.0).astype(np.float32)  # integers: exact dots, ties
+    qs = (orc.synth_rows(62, 0, nq, d, 1) - 128.0).astype(np.float32)
+    c = Corpus(ctx, KIND_F32, METRIC_DOT, d, n)
+    c.upsert(np.arange(n, dtype=np.uint64), rows)
+    allowed = np.arange(100, 7000, 3, dtype=np.uint64)
+    am = np.zeros(n, np.uint8)
+    am[allowed.astype(np.int64)] = 1
+    ids, dists, counts = c.search(qs, k, allow_bitmap(allowed))
+    for qi in range(nq):
+        all_d = orc.dist_all(1, qs[qi], rows)
+        check_topk(orc, ids[qi], dists[qi], counts[qi], all_d, np.arange(n, dtype=np.uint64), k, am)
+
+
+# ---------------------------------------------------------------------------
 # BQ
 def test_bq_encode_and_distance_bitexact(ctx, orc):
     from weaviate_amd.compressionhelpers import BinaryQuantizer
@@ -367,25 +403,31 @@ def test_topk_merge_device(ctx, orc):
 
 
 def test_search_device_matches_host_api(ctx, orc):
+    """Device API; one zero-filled workspace reused by many calls stays armed."""
     import torch
 
-    n, d, k, nq = 20000, 128, 10, 4
+    n, d, k = 20000, 128, 10
     c = Corpus(ctx, KIND_F32, METRIC_L2, d, n)
     c.fill_synthetic(3, n, 0)
-    qs = orc.synth_rows(4, 0, nq, d, 0)
-    hid, hd, hc = c.search(qs, k)
     lib = _lib.load()
     dev = torch.device("cuda:0")
-    tq = torch.from_numpy(qs).to(dev)
-    ws = torch.empty(lib.wvg_search_workspace_size(c.handle, nq, k), dtype=torch.uint8, device=dev)
-    oi = torch.empty((nq, k), dtype=torch.int64, device=dev)
-    od = torch.empty((nq, k), dtype=torch.float32, device=dev)
-    oc = torch.empty(nq, dtype=torch.int32, device=dev)
-    _lib.check(lib.wvg_search_device(c.handle, tq.data_ptr(), nq, k, oi.data_ptr(), od.data_ptr(), oc.data_ptr(),
-                                     ws.data_ptr(), ws.numel(), torch.cuda.current_stream().cuda_stream))
-    torch.cuda.synchronize()
-    assert np.array_equal(oi.cpu().numpy().view(np.uint64), hid)
-    assert np.array_equal(bits(od.cpu().numpy()), bits(hd))
+    for nq in [4, 1, 3]:
+        ws = torch.zeros(lib.wvg_search_workspace_size(c.handle, nq, k), dtype=torch.uint8, device=dev)
+        for rep in range(3):
+            qs = orc.synth_rows(4 + rep, 0, nq, d, 0)
+            hid, hd, hc = c.search(qs, k)
+            tq = torch.from_numpy(qs).to(dev)
+            oi = torch.empty((nq, k), dtype=torch.int64, device=dev)
+            od = torch.empty((nq, k), dtype=torch.float32, device=dev)
+            oc = torch.empty(nq, dtype=torch.int32, device=dev)
+            _lib.check(lib.wvg_search_device(c.handle, tq.data_ptr(), nq, k, oi.data_ptr(), od.data_ptr(),
+                                             oc.data_ptr(), ws.data_ptr(), ws.numel(),
+                                             torch.cuda.current_stream().cuda_stream))
+            torch.cuda.synchronize()
+            assert np.array_equal(oi.cpu().numpy().view(np.uint64), hid)
+            assert np.array_equal(bits(od.cpu().numpy()), bits(hd))
+            assert np.array_equal(oc.cpu().numpy(), hc.astype(np.int32))
+        assert int(ws[:16 * nq].sum()) == 0  # re-armed
 
 
 # ---------------------------------------------------------------------------

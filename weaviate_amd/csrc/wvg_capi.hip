@@ -194,12 +194,12 @@ static void prepare_queries_host(const wvg_corpus *c, const float *queries, uint
     }
 }
 
-static hipError_t launch_scan(const ScanArgs &a, int kind, uint64_t *partials, int groups, hipStream_t s)
+static hipError_t launch_scan(const ScanArgs &a, int kind, const CandOut &o, int groups, hipStream_t s)
 {
     switch (kind) {
-    case WVG_KIND_F32: return launch_scan_f32(a, partials, groups, s);
-    case WVG_KIND_BQ: return launch_scan_bq(a, partials, groups, s);
-    default: return launch_scan_pq(a, partials, groups, s);
+    case WVG_KIND_F32: return launch_scan_f32(a, o, groups, s);
+    case WVG_KIND_BQ: return launch_scan_bq(a, o, groups, s);
+    default: return launch_scan_pq(a, o, groups, s);
     }
 }
 
@@ -270,6 +270,7 @@ int wvg_open(int device, wvg_ctx **out)
     wvg_ctx *c = new wvg_ctx();
     c->device = device;
     c->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    if (const char *e = getenv("WVG_MFMA_MIN_QUERIES")) c->mfma_min_nq = (uint32_t)strtoul(e, nullptr, 10);
     *out = c;
     return WVG_OK;
 }
@@ -713,8 +714,8 @@ static int prof_pair(wvg_ctx *ctx, std::pair<hipEvent_t, hipEvent_t> *out)
 
 // Runs phase 1 + phase 2 for one corpus with device-resident prepared queries.
 static int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t nq, uint32_t k, const uint64_t *d_allow,
-                      uint64_t allow_words, uint64_t tb, uint64_t te, uint64_t *d_partials, int groups, uint64_t *ids,
-                      float *dists, uint32_t *counts, hipStream_t s)
+                      uint64_t allow_words, uint64_t tb, uint64_t te, const CandOut &co, int groups, bool gemm,
+                      uint64_t *ids, float *dists, uint32_t *counts, hipStream_t s)
 {
     ScanArgs a{};
     a.data = c->d_data;
@@ -739,27 +740,52 @@ static int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t 
         if (rc) return rc;
         WVG_HIP(hipEventRecord(ev.first, s));
     }
-    WVG_HIP(launch_scan(a, c->kind, d_partials, groups, s));
+    if (gemm)
+        WVG_HIP(launch_gemm_topk(a, (uint32_t)groups, co, s));
+    else
+        WVG_HIP(launch_scan(a, c->kind, co, groups, s));
     if (ev.second) WVG_HIP(hipEventRecord(ev.second, s));
-    WVG_HIP(launch_merge_keys(d_partials, nq, (uint32_t)groups * k, k, c->id_base, ids, dists, counts, s));
+    WVG_HIP(launch_merge_cands(co, nq, k, c->id_base, ids, dists, counts, s));
     return WVG_OK;
 }
 
 struct SearchPlan {
     uint64_t tb = 0, te = 0;
-    int groups = 1;
+    int groups = 1;      // scan: workgroups per query; gemm: row ranges
+    bool gemm = false;   // K3 batched MFMA path
     bool empty = false;
+    size_t partial_keys(uint32_t nq, uint32_t k) const { return (size_t)nq * groups * k; }
+    // workspace: [nq] candidate headers (must start zeroed; the merge re-arms them) + [nq][groups*k] keys
+    size_t workspace_bytes(uint32_t nq, uint32_t k) const
+    {
+        return align_up((size_t)nq * CAND_HEADER_BYTES, 256) + partial_keys(nq, k) * 8;
+    }
+    CandOut carve(void *base, uint32_t k) const
+    {
+        CandOut o;
+        o.hdr = base;
+        o.cand = (uint64_t *)((char *)base + align_up((size_t)ncand_q * CAND_HEADER_BYTES, 256));
+        o.cap = (uint32_t)groups * k;
+        return o;
+    }
+    uint32_t ncand_q = 0;
 };
 
 static SearchPlan plan_search(wvg_corpus *c, uint32_t nq, uint32_t k, const uint64_t *allow, uint64_t allow_words)
 {
     SearchPlan p;
+    p.ncand_q = nq;
     p.empty = !allow_tile_range(c, allow, allow_words, p.tb, p.te) || k == 0 || nq == 0;
     ScanArgs a{};
     a.tile_begin = p.tb;
     a.tile_end = p.te;
     a.nq = nq;
-    p.groups = scan_groups_for(a, c->ctx->num_cus);
+    const uint32_t mn = c->ctx->mfma_min_nq;
+    p.gemm = c->kind == WVG_KIND_F32 && mn > 0 && nq >= mn && gemm_supported(c->dim, c->metric);
+    if (p.gemm)
+        p.groups = (int)gemm_row_ranges(nq, std::max<uint64_t>(1, p.te - p.tb), c->ctx->num_cus);
+    else
+        p.groups = scan_groups_for(a, c->ctx->num_cus);
     return p;
 }
 
@@ -829,7 +855,7 @@ int wvg_search(wvg_corpus *c, const float *queries, uint32_t nq, uint32_t k, con
     const size_t o_q = cv.take(query_bytes(c, nq));
     const size_t o_qtmp = cv.take(c->kind == WVG_KIND_PQ ? (size_t)nq * c->dim * 4 : 0);
     const size_t o_allow = cv.take(allow_bits ? allow_words * 8 : 0);
-    const size_t o_part = cv.take((size_t)nq * p.groups * k * 8);
+    const size_t o_part = cv.take(p.workspace_bytes(nq, k));
     const size_t o_ids = cv.take((size_t)nq * k * 8);
     const size_t o_d = cv.take((size_t)nq * k * 4);
     const size_t o_cnt = cv.take((size_t)nq * 4);
@@ -838,6 +864,7 @@ int wvg_search(wvg_corpus *c, const float *queries, uint32_t nq, uint32_t k, con
     if (rc) return rc;
     char *b = (char *)base;
     hipStream_t s = g.slot->stream;
+    WVG_HIP(hipMemsetAsync(b + o_part, 0, (size_t)nq * CAND_HEADER_BYTES, s));  // arm the headers
     uint32_t qpitch = 0;
     rc = stage_queries(c, g.slot, queries, nq, b + o_q, qpitch, (float *)(b + o_q), b + o_qtmp);
     if (rc) return rc;
@@ -846,8 +873,8 @@ int wvg_search(wvg_corpus *c, const float *queries, uint32_t nq, uint32_t k, con
         WVG_HIP(hipMemcpyAsync(b + o_allow, allow_bits, allow_words * 8, hipMemcpyHostToDevice, s));
         d_allow = (const uint64_t *)(b + o_allow);
     }
-    rc = run_search(c, b + o_q, qpitch, nq, k, d_allow, allow_words, p.tb, p.te, (uint64_t *)(b + o_part), p.groups,
-                    (uint64_t *)(b + o_ids), (float *)(b + o_d), (uint32_t *)(b + o_cnt), s);
+    rc = run_search(c, b + o_q, qpitch, nq, k, d_allow, allow_words, p.tb, p.te, p.carve(b + o_part, k), p.groups,
+                    p.gemm, (uint64_t *)(b + o_ids), (float *)(b + o_d), (uint32_t *)(b + o_cnt), s);
     if (rc) return rc;
     if (out_ids) WVG_HIP(hipMemcpyAsync(out_ids, b + o_ids, (size_t)nq * k * 8, hipMemcpyDeviceToHost, s));
     if (out_dists) WVG_HIP(hipMemcpyAsync(out_dists, b + o_d, (size_t)nq * k * 4, hipMemcpyDeviceToHost, s));
@@ -885,7 +912,7 @@ int wvg_search_bq_rescore(wvg_corpus *bq, wvg_corpus *f32, const float *queries,
     const size_t o_qb = cv.take(query_bytes(bq, nq));
     const size_t o_qf = cv.take((size_t)nq * fpitch * 4);
     const size_t o_allow = cv.take(allow_bits ? allow_words * 8 : 0);
-    const size_t o_part = cv.take((size_t)nq * p.groups * R * 8);
+    const size_t o_part = cv.take(p.workspace_bytes(nq, R));
     const size_t o_cand = cv.take((size_t)nq * R * 8);
     const size_t o_resc = cv.take((size_t)nq * R * 8);
     const size_t o_ids = cv.take((size_t)nq * k * 8);
@@ -922,13 +949,12 @@ int wvg_search_bq_rescore(wvg_corpus *bq, wvg_corpus *f32, const float *queries,
     a.qpitch = qpb;
     a.nq = nq;
     a.k = R;
-    uint64_t *part = (uint64_t *)(b + o_part);
-    WVG_HIP(launch_scan_bq(a, part, p.groups, s));
-    // merge partials to R candidate ids; ids are id_base + slot, so pass id_base = 0 to keep slots
+    const CandOut co = p.carve(b + o_part, R);
+    WVG_HIP(hipMemsetAsync(co.hdr, 0, (size_t)nq * CAND_HEADER_BYTES, s));
+    WVG_HIP(launch_scan_bq(a, co, p.groups, s));
+    // Hamming top-R; ids are id_base + slot, so id_base = 0 keeps the slots
     uint64_t *cand_ids = (uint64_t *)(b + o_cand);
-    float *cand_d = (float *)(b + o_ids);  // temporary, overwritten below
-    (void)cand_d;
-    WVG_HIP(launch_merge_keys(part, nq, (uint32_t)p.groups * R, R, 0, cand_ids, (float *)(b + o_resc), nullptr, s));
+    WVG_HIP(launch_merge_cands(co, nq, R, 0, cand_ids, (float *)(b + o_resc), nullptr, s));
     // cand_ids now hold slots (or KEY_NONE); rescore them exactly against the f32 rows
     WVG_HIP(launch_rescore_keys(f32->metric, (const float *)(b + o_qf), qpf, (const float *)f32->d_data, d,
                                 f32->nchunks, cand_ids, nq, R, R, (uint64_t *)(b + o_resc), s));
@@ -946,8 +972,7 @@ size_t wvg_search_workspace_size(wvg_corpus *c, uint32_t nq, uint32_t k)
     if (!c) return 0;
     SearchPlan p = plan_search(c, nq, k, nullptr, 0);
     Carver cv;
-    cv.take((size_t)nq * p.groups * std::max<uint32_t>(k, 1) * 8);
-    cv.take(query_bytes(c, nq));
+    cv.take(p.workspace_bytes(nq, std::max<uint32_t>(k, 1)));
     return cv.off;
 }
 
@@ -962,11 +987,9 @@ int wvg_search_device(wvg_corpus *c, const float *d_queries, uint32_t nq, uint32
     std::shared_lock<std::shared_mutex> lk(c->rw);
     SearchPlan p = plan_search(c, nq, k, nullptr, 0);
     if (p.empty) return WVG_OK;
-    Carver cv;
-    const size_t o_part = cv.take((size_t)nq * p.groups * k * 8);
-    if (!d_workspace || workspace_bytes < cv.off) return fail(WVG_ERR_INVALID, "workspace too small");
-    return run_search(c, d_queries, c->dim, nq, k, nullptr, 0, p.tb, p.te,
-                      (uint64_t *)((char *)d_workspace + o_part), p.groups, d_ids, d_dists, d_counts, s);
+    if (!d_workspace || workspace_bytes < p.workspace_bytes(nq, k)) return fail(WVG_ERR_INVALID, "workspace too small");
+    return run_search(c, d_queries, c->dim, nq, k, nullptr, 0, p.tb, p.te, p.carve(d_workspace, k), p.groups, p.gemm,
+                      d_ids, d_dists, d_counts, s);
 }
 
 int wvg_topk_merge_device(wvg_ctx *ctx, const float *d_dists, const uint64_t *d_ids, uint32_t nq, uint32_t nlists,

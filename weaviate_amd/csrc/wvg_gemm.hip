@@ -11,8 +11,9 @@
 // tree; here every slice gets its own 16x16 accumulator, the MFMA's K = 4
 // steps are 4 consecutive blocks b of that slice, and the epilogue applies the
 // same tree -- so dot products are bit-identical to the CPU distancer.
-// L2 uses ||q||^2-free direct differences? No: L2 is not a contraction; this
-// kernel serves dot and cosine-dot (BASELINE config 2), L2 batches use K1.
+// Squared L2 is not a plain contraction in the reference's order (it squares
+// differences), so this kernel serves dot and cosine-dot (BASELINE config 2);
+// L2 batches use K1.
 //
 // Workgroup: 8 waves, tile = 32 queries x 64 rows (one corpus tile); each
 // wave owns a 16x16 sub-tile with 32 slice accumulators (128 acc VGPRs).
@@ -48,11 +49,10 @@ struct GemmArgs {
 };
 
 template <int E>
-__global__ __launch_bounds__(GWAVES * 64) void gemm_topk_kernel(GemmArgs a, uint64_t *partials)
+__global__ __launch_bounds__(GWAVES * 64) void gemm_topk_kernel(GemmArgs a, CandOut o)
 {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    float *qs[2] = {smem, smem + (GQ + GR) * GSTRIDE};
-    float *rs[2] = {smem + GQ * GSTRIDE, smem + (GQ + GR) * GSTRIDE + GQ * GSTRIDE};
+    // buffer b: queries at smem + b*(GQ+GR)*GSTRIDE, rows right after them
     uint64_t *keys = reinterpret_cast<uint64_t *>(smem + 2 * (GQ + GR) * GSTRIDE);  // [GQ][GR]
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -107,7 +107,7 @@ __global__ __launch_bounds__(GWAVES * 64) void gemm_topk_kernel(GemmArgs a, uint
         for (int i = 0; i < PER; i++) {
             const int idx = tid + i * GWAVES * 64;
             const int row = idx >> 5, c4 = idx & 31;
-            float *dst = row < GQ ? qs[buf] + row * GSTRIDE : rs[buf] + (row - GQ) * GSTRIDE;
+            float *dst = smem + buf * (GQ + GR) * GSTRIDE + row * GSTRIDE;
             *reinterpret_cast<float4 *>(dst + c4 * 4) = pf[i];
         }
     };
@@ -132,8 +132,8 @@ __global__ __launch_bounds__(GWAVES * 64) void gemm_topk_kernel(GemmArgs a, uint
         for (uint32_t kc = 0; kc < nk; kc++) {
             const int cur = kc & 1;
             if (kc + 1 < nk) load_chunk(t, kc + 1);  // prefetch into registers
-            const float *qa = qs[cur] + qrow * GSTRIDE + kk * 32;
-            const float *rb = rs[cur] + rrow * GSTRIDE + kk * 32;
+            const float *qa = smem + cur * (GQ + GR) * GSTRIDE + qrow * GSTRIDE + kk * 32;
+            const float *rb = smem + cur * (GQ + GR) * GSTRIDE + (GQ + rrow) * GSTRIDE + kk * 32;
 #pragma unroll
             for (int g = 0; g < 8; g++) {
                 const float4 av = *reinterpret_cast<const float4 *>(qa + g * 4);
@@ -173,13 +173,7 @@ __global__ __launch_bounds__(GWAVES * 64) void gemm_topk_kernel(GemmArgs a, uint
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const uint32_t q = q0 + wave * 4 + i;
-        if (q >= a.nq) continue;
-        uint64_t *out = partials + ((size_t)q * a.nrr + rr) * a.k;
-#pragma unroll
-        for (int e = 0; e < E; e++) {
-            const int idx = e * 64 + lane;
-            if (idx < (int)a.k) out[idx] = tk[i].l[e];
-        }
+        if (q < a.nq) publish_list<E>(tk[i], reinterpret_cast<CandHeader *>(o.hdr) + q, o.cand + (size_t)q * o.cap);
     }
 }
 
@@ -195,7 +189,7 @@ uint32_t gemm_row_ranges(uint32_t nq, uint64_t ntiles, int num_cus)
     return (uint32_t)want;
 }
 
-hipError_t launch_gemm_topk(const ScanArgs &s, uint32_t nrr, uint64_t *partials, hipStream_t st)
+hipError_t launch_gemm_topk(const ScanArgs &s, uint32_t nrr, const CandOut &o, hipStream_t st)
 {
     GemmArgs a{};
     a.data = reinterpret_cast<const float4 *>(s.data);
@@ -216,11 +210,11 @@ hipError_t launch_gemm_topk(const ScanArgs &s, uint32_t nrr, uint64_t *partials,
     const size_t lds = (size_t)2 * (GQ + GR) * GSTRIDE * 4 + (size_t)GQ * GR * 8;
     dim3 grid(a.nqb * a.nrr), block(GWAVES * 64);
     if (s.k <= 64)
-        hipLaunchKernelGGL((gemm_topk_kernel<1>), grid, block, lds, st, a, partials);
+        hipLaunchKernelGGL((gemm_topk_kernel<1>), grid, block, lds, st, a, o);
     else if (s.k <= 128)
-        hipLaunchKernelGGL((gemm_topk_kernel<2>), grid, block, lds, st, a, partials);
+        hipLaunchKernelGGL((gemm_topk_kernel<2>), grid, block, lds, st, a, o);
     else
-        hipLaunchKernelGGL((gemm_topk_kernel<4>), grid, block, lds, st, a, partials);
+        hipLaunchKernelGGL((gemm_topk_kernel<4>), grid, block, lds, st, a, o);
     return hipGetLastError();
 }
 

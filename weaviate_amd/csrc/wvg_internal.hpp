@@ -42,6 +42,7 @@ struct StreamSlot {
 struct wvg_ctx {
     int device = 0;
     int num_cus = 256;
+    uint32_t mfma_min_nq = 32;  // batches of >= this many dot/cosine queries use K3 (env WVG_MFMA_MIN_QUERIES; 0 = never)
     std::mutex pool_mu;
     std::vector<wvg::StreamSlot *> free_slots;
     std::vector<wvg::StreamSlot *> all_slots;
@@ -99,12 +100,27 @@ struct ScanArgs {
     uint32_t nq, k;
     uint32_t pq_m, pq_ks;
 };
+// Compacted candidates of phase 1 (see wvg_topk.hpp CandHeader): header[nq]
+// (zero = armed) and cand[nq][cap] keys.  The merge re-arms the headers.
+struct CandOut {
+    void *hdr;        // CandHeader[nq]
+    uint64_t *cand;   // [nq][cap]
+    uint32_t cap;     // per-query capacity (workgroups x K)
+};
+constexpr size_t CAND_HEADER_BYTES = 16;
 int scan_groups_for(const ScanArgs &a, int num_cus);
-hipError_t launch_scan_f32(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s);
-hipError_t launch_scan_bq(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s);
-hipError_t launch_scan_pq(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s);
-// Scan phase 2: merge [nq][nlists][K] keys into final (ids, dists, counts).
-hipError_t launch_merge_keys(const uint64_t *partials, uint32_t nq, uint32_t nlists, uint32_t k,
+hipError_t launch_scan_f32(const ScanArgs &a, const CandOut &o, int groups, hipStream_t s);
+hipError_t launch_scan_bq(const ScanArgs &a, const CandOut &o, int groups, hipStream_t s);
+hipError_t launch_scan_pq(const ScanArgs &a, const CandOut &o, int groups, hipStream_t s);
+// K3 batched MFMA scoring (wvg_gemm.hip).
+bool gemm_supported(uint32_t dim, int metric);
+uint32_t gemm_row_ranges(uint32_t nq, uint64_t ntiles, int num_cus);
+hipError_t launch_gemm_topk(const ScanArgs &a, uint32_t nrr, const CandOut &o, hipStream_t s);
+// Phase 2 over compacted candidates -> final (ids = id_base + slot, dists, counts); re-arms headers.
+hipError_t launch_merge_cands(const CandOut &o, uint32_t nq, uint32_t k, uint64_t id_base, uint64_t *ids,
+                              float *dists, uint32_t *counts, hipStream_t s);
+// Dense merge of [nq][n_per_query] keys (BQ rescore).
+hipError_t launch_merge_keys(const uint64_t *partials, uint32_t nq, uint32_t n_per_query, uint32_t k,
                              uint64_t id_base, uint64_t *ids, float *dists, uint32_t *counts,
                              hipStream_t s);
 // Merge (dist, id64) lists: [nq][nlists][k_in] -> [nq][k].

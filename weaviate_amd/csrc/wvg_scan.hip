@@ -19,6 +19,10 @@ namespace wvg {
 
 constexpr int SCAN_WAVES = 4;
 
+// Wave index as a wave-uniform (SGPR) value, so per-wave loops, the tile mask
+// loads and the skip branch are scalar.
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
 // Per-tile mask of live, allowed rows (one 64-bit word per tile = one bit per lane).
 __device__ __forceinline__ uint64_t tile_mask(const ScanArgs &a, uint64_t t)
 {
@@ -35,37 +39,13 @@ __device__ __forceinline__ void wave_range(const ScanArgs &a, int waves_per_grou
 {
     const uint64_t ntiles = a.tile_end - a.tile_begin;
     const uint64_t total = (uint64_t)gridDim.x * waves_per_group;
-    const uint64_t gw = (uint64_t)blockIdx.x * waves_per_group + (threadIdx.x >> 6);
+    const uint64_t gw = (uint64_t)blockIdx.x * waves_per_group + wave_id();
     t0 = a.tile_begin + ntiles * gw / total;
     t1 = a.tile_begin + ntiles * (gw + 1) / total;
 }
 
-// Workgroup combine: wave lists -> one sorted list, wave 0 writes K keys.
-template <int E, int WAVES>
-__device__ __forceinline__ void group_combine_store(WaveTopK<E> &tk, uint64_t *out)
-{
-    __shared__ uint64_t sh[WAVES][64 * E];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-    for (int e = 0; e < E; e++) sh[wave][e * 64 + lane] = tk.l[e];
-    __syncthreads();
-    if (wave == 0) {
-        for (int w = 1; w < WAVES; w++) {
-            uint64_t o[E];
-#pragma unroll
-            for (int e = 0; e < E; e++) o[e] = sh[w][e * 64 + lane];
-            merge_lists<E>(tk.l, o);
-        }
-#pragma unroll
-        for (int e = 0; e < E; e++) {
-            const int i = e * 64 + lane;
-            if (i < tk.k) out[i] = tk.l[e];
-        }
-    }
-}
-
 template <int METRIC, int D, int E>
-__global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_kernel(ScanArgs a, uint64_t *partials)
+__global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_kernel(ScanArgs a, CandOut o)
 {
     const int lane = threadIdx.x & 63;
     const uint32_t qi = blockIdx.y;
@@ -75,8 +55,10 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_kernel(ScanArgs a, u
     wave_range(a, SCAN_WAVES, t0, t1);
     WaveTopK<E> tk;
     tk.init((int)a.k);
+    uint64_t m_next = t0 < t1 ? tile_mask(a, t0) : 0ull;
     for (uint64_t t = t0; t < t1; ++t) {
-        const uint64_t m = tile_mask(a, t);
+        const uint64_t m = m_next;
+        if (t + 1 < t1) m_next = tile_mask(a, t + 1);  // scalar prefetch of the next mask
         if (m == 0ull) continue;  // wave-uniform: nothing live/allowed in this tile
         const float4 *rp = data + (size_t)t * a.nchunks * 64 + lane;
         float r;
@@ -88,14 +70,17 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_kernel(ScanArgs a, u
         const uint64_t key = ((m >> lane) & 1ull) ? wvg_make_key(dist, (uint32_t)(t * 64 + lane)) : WVG_KEY_NONE;
         tk.offer(key);
     }
-    group_combine_store<E, SCAN_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
+    group_publish<E, SCAN_WAVES>(tk, reinterpret_cast<CandHeader *>(o.hdr) + qi, o.cand + (size_t)qi * o.cap);
 }
 
+// Grid: every wave resident at once (3 workgroups of 4 waves per CU at the
+// d=128 kernel's 167 VGPRs), each wave owning a contiguous tile range; at
+// least 2 tiles per wave.  For nq > 1 the queries share the machine.
 int scan_groups_for(const ScanArgs &a, int num_cus)
 {
     const uint64_t ntiles = a.tile_end > a.tile_begin ? a.tile_end - a.tile_begin : 0;
-    uint64_t g = (ntiles + SCAN_WAVES * 4 - 1) / (SCAN_WAVES * 4);
-    uint64_t cap = (uint64_t)num_cus * 4;
+    uint64_t g = (ntiles + SCAN_WAVES * 2 - 1) / (SCAN_WAVES * 2);
+    uint64_t cap = (uint64_t)num_cus * 3;
     if (a.nq > 1) cap = std::max<uint64_t>((uint64_t)num_cus / 4, cap / a.nq);
     if (g > cap) g = cap;
     if (g < 1) g = 1;
@@ -103,30 +88,30 @@ int scan_groups_for(const ScanArgs &a, int num_cus)
 }
 
 template <int METRIC, int E>
-static hipError_t launch_f32_e(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
+static hipError_t launch_f32_e(const ScanArgs &a, const CandOut &o, int groups, hipStream_t s)
 {
     dim3 grid(groups, a.nq), block(SCAN_WAVES * 64);
     switch (a.dim) {
-    case 128: hipLaunchKernelGGL((scan_f32_kernel<METRIC, 128, E>), grid, block, 0, s, a, partials); break;
-    case 768: hipLaunchKernelGGL((scan_f32_kernel<METRIC, 768, E>), grid, block, 0, s, a, partials); break;
-    case 1536: hipLaunchKernelGGL((scan_f32_kernel<METRIC, 1536, E>), grid, block, 0, s, a, partials); break;
-    default: hipLaunchKernelGGL((scan_f32_kernel<METRIC, 0, E>), grid, block, 0, s, a, partials); break;
+    case 128: hipLaunchKernelGGL((scan_f32_kernel<METRIC, 128, E>), grid, block, 0, s, a, o); break;
+    case 768: hipLaunchKernelGGL((scan_f32_kernel<METRIC, 768, E>), grid, block, 0, s, a, o); break;
+    case 1536: hipLaunchKernelGGL((scan_f32_kernel<METRIC, 1536, E>), grid, block, 0, s, a, o); break;
+    default: hipLaunchKernelGGL((scan_f32_kernel<METRIC, 0, E>), grid, block, 0, s, a, o); break;
     }
     return hipGetLastError();
 }
 
 template <int METRIC>
-static hipError_t launch_f32_m(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
+static hipError_t launch_f32_m(const ScanArgs &a, const CandOut &o, int groups, hipStream_t s)
 {
-    if (a.k <= 64) return launch_f32_e<METRIC, 1>(a, partials, groups, s);
-    if (a.k <= 128) return launch_f32_e<METRIC, 2>(a, partials, groups, s);
-    return launch_f32_e<METRIC, 4>(a, partials, groups, s);
+    if (a.k <= 64) return launch_f32_e<METRIC, 1>(a, o, groups, s);
+    if (a.k <= 128) return launch_f32_e<METRIC, 2>(a, o, groups, s);
+    return launch_f32_e<METRIC, 4>(a, o, groups, s);
 }
 
-hipError_t launch_scan_f32(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
+hipError_t launch_scan_f32(const ScanArgs &a, const CandOut &o, int groups, hipStream_t s)
 {
-    if (a.metric == WVG_M_L2) return launch_f32_m<WVG_M_L2>(a, partials, groups, s);
-    return launch_f32_m<WVG_M_DOT>(a, partials, groups, s);
+    if (a.metric == WVG_M_L2) return launch_f32_m<WVG_M_L2>(a, o, groups, s);
+    return launch_f32_m<WVG_M_DOT>(a, o, groups, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -138,7 +123,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void merge_keys_kernel(const uint6
                                                                      uint64_t id_base, uint64_t *ids,
                                                                      float *dists, uint32_t *counts)
 {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wave = wave_id();
     const uint32_t qi = blockIdx.x;
     const uint64_t *src = partials + (size_t)qi * n_per_query;
     WaveTopK<E> tk;
@@ -171,6 +156,67 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void merge_keys_kernel(const uint6
         }
     }
     if (lane == 0 && counts) counts[qi] = cnt;
+}
+
+// Phase 2 over the compacted candidates of one query per workgroup; the
+// candidate count is small (~K log(groups)), so 4 waves offer it in a few
+// batches.  Re-arms the header for the next call (stream order).
+template <int E>
+__global__ __launch_bounds__(SCAN_WAVES * 64) void merge_cands_kernel(CandOut o, uint32_t k, uint64_t id_base,
+                                                                      uint64_t *ids, float *dists, uint32_t *counts)
+{
+    const int lane = threadIdx.x & 63, wave = wave_id();
+    const uint32_t qi = blockIdx.x;
+    CandHeader *hdr = reinterpret_cast<CandHeader *>(o.hdr) + qi;
+    const uint32_t n = min(hdr->count, o.cap);
+    const uint64_t *src = o.cand + (size_t)qi * o.cap;
+    WaveTopK<E> tk;
+    tk.init((int)k);
+    for (uint32_t base = wave * 64; base < n; base += SCAN_WAVES * 64) {
+        const uint32_t i = base + lane;
+        tk.offer(i < n ? src[i] : WVG_KEY_NONE);
+    }
+    __shared__ uint64_t sh[SCAN_WAVES][64 * E];
+#pragma unroll
+    for (int e = 0; e < E; e++) sh[wave][e * 64 + lane] = tk.l[e];
+    __syncthreads();
+    if (wave != 0) return;
+    if (lane == 0) {  // every wave has read `count` (barrier above): re-arm
+        hdr->tau_c = 0ull;
+        hdr->count = 0u;
+    }
+    for (int w = 1; w < SCAN_WAVES; w++) {
+        uint64_t oo[E];
+#pragma unroll
+        for (int e = 0; e < E; e++) oo[e] = sh[w][e * 64 + lane];
+        merge_lists<E>(tk.l, oo);
+    }
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const uint32_t i = e * 64 + lane;
+        const uint64_t key = tk.l[e];
+        const bool live = i < k && key != WVG_KEY_NONE;
+        cnt += (uint32_t)__popcll(__ballot(live));
+        if (i < k) {
+            ids[(size_t)qi * k + i] = live ? id_base + (key & 0xFFFFFFFFull) : WVG_KEY_NONE;
+            dists[(size_t)qi * k + i] = live ? wvg_unord_f32((uint32_t)(key >> 32)) : __builtin_inff();
+        }
+    }
+    if (lane == 0 && counts) counts[qi] = cnt;
+}
+
+hipError_t launch_merge_cands(const CandOut &o, uint32_t nq, uint32_t k, uint64_t id_base, uint64_t *ids, float *dists,
+                              uint32_t *counts, hipStream_t s)
+{
+    dim3 grid(nq), block(SCAN_WAVES * 64);
+    if (k <= 64)
+        hipLaunchKernelGGL((merge_cands_kernel<1>), grid, block, 0, s, o, k, id_base, ids, dists, counts);
+    else if (k <= 128)
+        hipLaunchKernelGGL((merge_cands_kernel<2>), grid, block, 0, s, o, k, id_base, ids, dists, counts);
+    else
+        hipLaunchKernelGGL((merge_cands_kernel<4>), grid, block, 0, s, o, k, id_base, ids, dists, counts);
+    return hipGetLastError();
 }
 
 hipError_t launch_merge_keys(const uint64_t *partials, uint32_t nq, uint32_t n_per_query, uint32_t k,

@@ -62,7 +62,7 @@ class ShardedFlatIndex:
         dists = torch.empty((nq, k), dtype=torch.float32, device=dev)
         counts = torch.empty(nq, dtype=torch.int32, device=dev)
         ws_bytes = self.lib.wvg_search_workspace_size(self.corpus.handle, nq, k)
-        ws = torch.empty(max(1, ws_bytes), dtype=torch.uint8, device=dev)
+        ws = torch.zeros(max(1, ws_bytes), dtype=torch.uint8, device=dev)
         check(self.lib.wvg_search_device(self.corpus.handle, q.data_ptr(), nq, k, ids.data_ptr(), dists.data_ptr(),
                                          counts.data_ptr(), ws.data_ptr(), ws_bytes, stream))
         if not dist.is_initialized() or dist.get_world_size(self.group) == 1:
