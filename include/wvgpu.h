@@ -117,9 +117,8 @@ int wvg_search_bq_rescore(wvg_corpus *bq, wvg_corpus *f32, const float *queries,
  * (a hipStream_t, NULL = default stream); no host synchronization, no
  * allocation (caller supplies a workspace of wvg_search_workspace_size bytes),
  * so a call can be captured in a hipGraph.  Queries must already be
- * normalized for cosine.  The workspace must be ZERO-FILLED before its first
- * use; every call leaves it zero-filled again (the merge re-arms it), so one
- * workspace serves any number of calls on one stream.                      */
+ * normalized for cosine.  One workspace serves any number of calls issued
+ * in order on one stream (no initialization needed).                       */
 size_t wvg_search_workspace_size(wvg_corpus *c, uint32_t nq, uint32_t k);
 int wvg_search_device(wvg_corpus *c, const float *d_queries, uint32_t nq, uint32_t k,
                       uint64_t *d_ids, float *d_dists, uint32_t *d_counts, void *d_workspace,

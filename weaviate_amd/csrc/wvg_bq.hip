@@ -27,7 +27,7 @@ __device__ __forceinline__ uint64_t bq_tile_mask(const ScanArgs &a, uint64_t t)
 }
 
 template <int E, int NCH>
-__global__ __launch_bounds__(BQ_WAVES * 64) void scan_bq_kernel(ScanArgs a, CandOut o)
+__global__ __launch_bounds__(BQ_WAVES * 64) void scan_bq_kernel(ScanArgs a, uint64_t *partials)
 {
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t qi = blockIdx.y;
@@ -62,27 +62,27 @@ __global__ __launch_bounds__(BQ_WAVES * 64) void scan_bq_kernel(ScanArgs a, Cand
         const uint64_t key = ((m >> lane) & 1ull) ? wvg_make_key(dist, (uint32_t)(t * 64 + lane)) : WVG_KEY_NONE;
         tk.offer(key);
     }
-    group_publish<E, BQ_WAVES>(tk, reinterpret_cast<CandHeader *>(o.hdr) + qi, o.cand + (size_t)qi * o.cap);
+    group_combine_store<E, BQ_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
 }
 
 template <int E>
-static hipError_t launch_bq_e(const ScanArgs &a, const CandOut &o, int groups, hipStream_t s)
+static hipError_t launch_bq_e(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
 {
     dim3 grid(groups, a.nq), block(BQ_WAVES * 64);
     switch (a.nchunks) {
-    case 1: hipLaunchKernelGGL((scan_bq_kernel<E, 1>), grid, block, 0, s, a, o); break;   // d <= 128
-    case 6: hipLaunchKernelGGL((scan_bq_kernel<E, 6>), grid, block, 0, s, a, o); break;   // d = 768
-    case 12: hipLaunchKernelGGL((scan_bq_kernel<E, 12>), grid, block, 0, s, a, o); break; // d = 1536
-    default: hipLaunchKernelGGL((scan_bq_kernel<E, 0>), grid, block, 0, s, a, o); break;
+    case 1: hipLaunchKernelGGL((scan_bq_kernel<E, 1>), grid, block, 0, s, a, partials); break;   // d <= 128
+    case 6: hipLaunchKernelGGL((scan_bq_kernel<E, 6>), grid, block, 0, s, a, partials); break;   // d = 768
+    case 12: hipLaunchKernelGGL((scan_bq_kernel<E, 12>), grid, block, 0, s, a, partials); break; // d = 1536
+    default: hipLaunchKernelGGL((scan_bq_kernel<E, 0>), grid, block, 0, s, a, partials); break;
     }
     return hipGetLastError();
 }
 
-hipError_t launch_scan_bq(const ScanArgs &a, const CandOut &o, int groups, hipStream_t s)
+hipError_t launch_scan_bq(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
 {
-    if (a.k <= 64) return launch_bq_e<1>(a, o, groups, s);
-    if (a.k <= 128) return launch_bq_e<2>(a, o, groups, s);
-    return launch_bq_e<4>(a, o, groups, s);
+    if (a.k <= 64) return launch_bq_e<1>(a, partials, groups, s);
+    if (a.k <= 128) return launch_bq_e<2>(a, partials, groups, s);
+    return launch_bq_e<4>(a, partials, groups, s);
 }
 
 // Encode row-major float rows; `normalize` is applied per row first (cosine).

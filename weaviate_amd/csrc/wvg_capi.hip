@@ -194,12 +194,12 @@ static void prepare_queries_host(const wvg_corpus *c, const float *queries, uint
     }
 }
 
-static hipError_t launch_scan(const ScanArgs &a, int kind, const CandOut &o, int groups, hipStream_t s)
+static hipError_t launch_scan(const ScanArgs &a, int kind, uint64_t *partials, int groups, hipStream_t s)
 {
     switch (kind) {
-    case WVG_KIND_F32: return launch_scan_f32(a, o, groups, s);
-    case WVG_KIND_BQ: return launch_scan_bq(a, o, groups, s);
-    default: return launch_scan_pq(a, o, groups, s);
+    case WVG_KIND_F32: return launch_scan_f32(a, partials, groups, s);
+    case WVG_KIND_BQ: return launch_scan_bq(a, partials, groups, s);
+    default: return launch_scan_pq(a, partials, groups, s);
     }
 }
 
@@ -714,7 +714,7 @@ static int prof_pair(wvg_ctx *ctx, std::pair<hipEvent_t, hipEvent_t> *out)
 
 // Runs phase 1 + phase 2 for one corpus with device-resident prepared queries.
 static int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t nq, uint32_t k, const uint64_t *d_allow,
-                      uint64_t allow_words, uint64_t tb, uint64_t te, const CandOut &co, int groups, bool gemm,
+                      uint64_t allow_words, uint64_t tb, uint64_t te, uint64_t *partials, int groups, bool gemm,
                       uint64_t *ids, float *dists, uint32_t *counts, hipStream_t s)
 {
     ScanArgs a{};
@@ -741,11 +741,11 @@ static int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t 
         WVG_HIP(hipEventRecord(ev.first, s));
     }
     if (gemm)
-        WVG_HIP(launch_gemm_topk(a, (uint32_t)groups, co, s));
+        WVG_HIP(launch_gemm_topk(a, (uint32_t)groups, partials, s));
     else
-        WVG_HIP(launch_scan(a, c->kind, co, groups, s));
+        WVG_HIP(launch_scan(a, c->kind, partials, groups, s));
     if (ev.second) WVG_HIP(hipEventRecord(ev.second, s));
-    WVG_HIP(launch_merge_cands(co, nq, k, c->id_base, ids, dists, counts, s));
+    WVG_HIP(launch_merge_keys(partials, nq, (uint32_t)groups * k, k, c->id_base, ids, dists, counts, s));
     return WVG_OK;
 }
 
@@ -755,26 +755,12 @@ struct SearchPlan {
     bool gemm = false;   // K3 batched MFMA path
     bool empty = false;
     size_t partial_keys(uint32_t nq, uint32_t k) const { return (size_t)nq * groups * k; }
-    // workspace: [nq] candidate headers (must start zeroed; the merge re-arms them) + [nq][groups*k] keys
-    size_t workspace_bytes(uint32_t nq, uint32_t k) const
-    {
-        return align_up((size_t)nq * CAND_HEADER_BYTES, 256) + partial_keys(nq, k) * 8;
-    }
-    CandOut carve(void *base, uint32_t k) const
-    {
-        CandOut o;
-        o.hdr = base;
-        o.cand = (uint64_t *)((char *)base + align_up((size_t)ncand_q * CAND_HEADER_BYTES, 256));
-        o.cap = (uint32_t)groups * k;
-        return o;
-    }
-    uint32_t ncand_q = 0;
+    size_t workspace_bytes(uint32_t nq, uint32_t k) const { return partial_keys(nq, k) * 8; }
 };
 
 static SearchPlan plan_search(wvg_corpus *c, uint32_t nq, uint32_t k, const uint64_t *allow, uint64_t allow_words)
 {
     SearchPlan p;
-    p.ncand_q = nq;
     p.empty = !allow_tile_range(c, allow, allow_words, p.tb, p.te) || k == 0 || nq == 0;
     ScanArgs a{};
     a.tile_begin = p.tb;
@@ -864,7 +850,6 @@ int wvg_search(wvg_corpus *c, const float *queries, uint32_t nq, uint32_t k, con
     if (rc) return rc;
     char *b = (char *)base;
     hipStream_t s = g.slot->stream;
-    WVG_HIP(hipMemsetAsync(b + o_part, 0, (size_t)nq * CAND_HEADER_BYTES, s));  // arm the headers
     uint32_t qpitch = 0;
     rc = stage_queries(c, g.slot, queries, nq, b + o_q, qpitch, (float *)(b + o_q), b + o_qtmp);
     if (rc) return rc;
@@ -873,7 +858,7 @@ int wvg_search(wvg_corpus *c, const float *queries, uint32_t nq, uint32_t k, con
         WVG_HIP(hipMemcpyAsync(b + o_allow, allow_bits, allow_words * 8, hipMemcpyHostToDevice, s));
         d_allow = (const uint64_t *)(b + o_allow);
     }
-    rc = run_search(c, b + o_q, qpitch, nq, k, d_allow, allow_words, p.tb, p.te, p.carve(b + o_part, k), p.groups,
+    rc = run_search(c, b + o_q, qpitch, nq, k, d_allow, allow_words, p.tb, p.te, (uint64_t *)(b + o_part), p.groups,
                     p.gemm, (uint64_t *)(b + o_ids), (float *)(b + o_d), (uint32_t *)(b + o_cnt), s);
     if (rc) return rc;
     if (out_ids) WVG_HIP(hipMemcpyAsync(out_ids, b + o_ids, (size_t)nq * k * 8, hipMemcpyDeviceToHost, s));
@@ -949,12 +934,11 @@ int wvg_search_bq_rescore(wvg_corpus *bq, wvg_corpus *f32, const float *queries,
     a.qpitch = qpb;
     a.nq = nq;
     a.k = R;
-    const CandOut co = p.carve(b + o_part, R);
-    WVG_HIP(hipMemsetAsync(co.hdr, 0, (size_t)nq * CAND_HEADER_BYTES, s));
-    WVG_HIP(launch_scan_bq(a, co, p.groups, s));
+    uint64_t *part = (uint64_t *)(b + o_part);
+    WVG_HIP(launch_scan_bq(a, part, p.groups, s));
     // Hamming top-R; ids are id_base + slot, so id_base = 0 keeps the slots
     uint64_t *cand_ids = (uint64_t *)(b + o_cand);
-    WVG_HIP(launch_merge_cands(co, nq, R, 0, cand_ids, (float *)(b + o_resc), nullptr, s));
+    WVG_HIP(launch_merge_keys(part, nq, (uint32_t)p.groups * R, R, 0, cand_ids, (float *)(b + o_resc), nullptr, s));
     // cand_ids now hold slots (or KEY_NONE); rescore them exactly against the f32 rows
     WVG_HIP(launch_rescore_keys(f32->metric, (const float *)(b + o_qf), qpf, (const float *)f32->d_data, d,
                                 f32->nchunks, cand_ids, nq, R, R, (uint64_t *)(b + o_resc), s));
@@ -988,7 +972,7 @@ int wvg_search_device(wvg_corpus *c, const float *d_queries, uint32_t nq, uint32
     SearchPlan p = plan_search(c, nq, k, nullptr, 0);
     if (p.empty) return WVG_OK;
     if (!d_workspace || workspace_bytes < p.workspace_bytes(nq, k)) return fail(WVG_ERR_INVALID, "workspace too small");
-    return run_search(c, d_queries, c->dim, nq, k, nullptr, 0, p.tb, p.te, p.carve(d_workspace, k), p.groups, p.gemm,
+    return run_search(c, d_queries, c->dim, nq, k, nullptr, 0, p.tb, p.te, (uint64_t *)d_workspace, p.groups, p.gemm,
                       d_ids, d_dists, d_counts, s);
 }
 
@@ -1002,6 +986,22 @@ int wvg_topk_merge_device(wvg_ctx *ctx, const float *d_dists, const uint64_t *d_
     WVG_HIP(launch_merge_pairs(d_dists, d_ids, nq, nlists, k_in, k, d_out_ids, d_out_dists, d_out_counts,
                                (hipStream_t)stream));
     return WVG_OK;
+}
+
+// Internal A/B knob (not part of include/wvgpu.h): 0 = K1 scan variant,
+// 1 = K1 resident workgroups per CU.  Returns the previous value.
+int wvgx_set_tuning(int key, int value)
+{
+    Tuning &t = tuning();
+    int old = -1;
+    if (key == 0) {
+        old = t.scan_variant;
+        t.scan_variant = value;
+    } else if (key == 1) {
+        old = t.groups_per_cu;
+        t.groups_per_cu = value;
+    }
+    return old;
 }
 
 int wvg_profile_start(wvg_ctx *ctx)

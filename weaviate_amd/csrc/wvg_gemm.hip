@@ -49,7 +49,7 @@ struct GemmArgs {
 };
 
 template <int E>
-__global__ __launch_bounds__(GWAVES * 64) void gemm_topk_kernel(GemmArgs a, CandOut o)
+__global__ __launch_bounds__(GWAVES * 64) void gemm_topk_kernel(GemmArgs a, uint64_t *partials)
 {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     // buffer b: queries at smem + b*(GQ+GR)*GSTRIDE, rows right after them
@@ -173,7 +173,13 @@ __global__ __launch_bounds__(GWAVES * 64) void gemm_topk_kernel(GemmArgs a, Cand
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const uint32_t q = q0 + wave * 4 + i;
-        if (q < a.nq) publish_list<E>(tk[i], reinterpret_cast<CandHeader *>(o.hdr) + q, o.cand + (size_t)q * o.cap);
+        if (q >= a.nq) continue;
+        uint64_t *out = partials + ((size_t)q * a.nrr + rr) * a.k;
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            const int idx = e * 64 + lane;
+            if (idx < (int)a.k) out[idx] = tk[i].l[e];
+        }
     }
 }
 
@@ -189,7 +195,7 @@ uint32_t gemm_row_ranges(uint32_t nq, uint64_t ntiles, int num_cus)
     return (uint32_t)want;
 }
 
-hipError_t launch_gemm_topk(const ScanArgs &s, uint32_t nrr, const CandOut &o, hipStream_t st)
+hipError_t launch_gemm_topk(const ScanArgs &s, uint32_t nrr, uint64_t *partials, hipStream_t st)
 {
     GemmArgs a{};
     a.data = reinterpret_cast<const float4 *>(s.data);
@@ -210,11 +216,11 @@ hipError_t launch_gemm_topk(const ScanArgs &s, uint32_t nrr, const CandOut &o, h
     const size_t lds = (size_t)2 * (GQ + GR) * GSTRIDE * 4 + (size_t)GQ * GR * 8;
     dim3 grid(a.nqb * a.nrr), block(GWAVES * 64);
     if (s.k <= 64)
-        hipLaunchKernelGGL((gemm_topk_kernel<1>), grid, block, lds, st, a, o);
+        hipLaunchKernelGGL((gemm_topk_kernel<1>), grid, block, lds, st, a, partials);
     else if (s.k <= 128)
-        hipLaunchKernelGGL((gemm_topk_kernel<2>), grid, block, lds, st, a, o);
+        hipLaunchKernelGGL((gemm_topk_kernel<2>), grid, block, lds, st, a, partials);
     else
-        hipLaunchKernelGGL((gemm_topk_kernel<4>), grid, block, lds, st, a, o);
+        hipLaunchKernelGGL((gemm_topk_kernel<4>), grid, block, lds, st, a, partials);
     return hipGetLastError();
 }
 

@@ -100,26 +100,22 @@ struct ScanArgs {
     uint32_t nq, k;
     uint32_t pq_m, pq_ks;
 };
-// Compacted candidates of phase 1 (see wvg_topk.hpp CandHeader): header[nq]
-// (zero = armed) and cand[nq][cap] keys.  The merge re-arms the headers.
-struct CandOut {
-    void *hdr;        // CandHeader[nq]
-    uint64_t *cand;   // [nq][cap]
-    uint32_t cap;     // per-query capacity (workgroups x K)
-};
-constexpr size_t CAND_HEADER_BYTES = 16;
+// Phase 1 writes dense partials [nq][groups][K] (keys, KEY_NONE = empty).
 int scan_groups_for(const ScanArgs &a, int num_cus);
-hipError_t launch_scan_f32(const ScanArgs &a, const CandOut &o, int groups, hipStream_t s);
-hipError_t launch_scan_bq(const ScanArgs &a, const CandOut &o, int groups, hipStream_t s);
-hipError_t launch_scan_pq(const ScanArgs &a, const CandOut &o, int groups, hipStream_t s);
-// K3 batched MFMA scoring (wvg_gemm.hip).
+hipError_t launch_scan_f32(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s);
+hipError_t launch_scan_bq(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s);
+hipError_t launch_scan_pq(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s);
+// K3 batched MFMA scoring (wvg_gemm.hip): partials [nq][nrr][K].
 bool gemm_supported(uint32_t dim, int metric);
 uint32_t gemm_row_ranges(uint32_t nq, uint64_t ntiles, int num_cus);
-hipError_t launch_gemm_topk(const ScanArgs &a, uint32_t nrr, const CandOut &o, hipStream_t s);
-// Phase 2 over compacted candidates -> final (ids = id_base + slot, dists, counts); re-arms headers.
-hipError_t launch_merge_cands(const CandOut &o, uint32_t nq, uint32_t k, uint64_t id_base, uint64_t *ids,
-                              float *dists, uint32_t *counts, hipStream_t s);
-// Dense merge of [nq][n_per_query] keys (BQ rescore).
+hipError_t launch_gemm_topk(const ScanArgs &a, uint32_t nrr, uint64_t *partials, hipStream_t s);
+// Internal tuning knobs (wvgx_set_tuning; A/B experiments, not public ABI).
+struct Tuning {
+    int scan_variant = 0;    // K1 variant (see wvg_scan.hip)
+    int groups_per_cu = 3;   // K1 resident workgroups per CU
+};
+Tuning &tuning();
+// Phase 2: merge [nq][n_per_query] keys into final (ids = id_base + slot, dists, counts).
 hipError_t launch_merge_keys(const uint64_t *partials, uint32_t nq, uint32_t n_per_query, uint32_t k,
                              uint64_t id_base, uint64_t *ids, float *dists, uint32_t *counts,
                              hipStream_t s);

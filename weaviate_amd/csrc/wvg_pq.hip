@@ -196,7 +196,7 @@ __device__ __forceinline__ uint32_t code_at(const uint4 (&cw)[8], int i)
 
 // K8: ADC scan, LUT in LDS.  M = compile-time segments (<= 128) or 0.
 template <int E, int M>
-__global__ __launch_bounds__(PQ_WAVES * 64) void scan_pq_kernel(ScanArgs a, CandOut o)
+__global__ __launch_bounds__(PQ_WAVES * 64) void scan_pq_kernel(ScanArgs a, uint64_t *partials)
 {
     extern __shared__ __attribute__((aligned(16))) float lut[];
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -246,30 +246,30 @@ __global__ __launch_bounds__(PQ_WAVES * 64) void scan_pq_kernel(ScanArgs a, Cand
         const uint64_t key = ((msk >> lane) & 1ull) ? wvg_make_key(dist, (uint32_t)(t * 64 + lane)) : WVG_KEY_NONE;
         tk.offer(key);
     }
-    group_publish<E, PQ_WAVES>(tk, reinterpret_cast<CandHeader *>(o.hdr) + qi, o.cand + (size_t)qi * o.cap);
+    group_combine_store<E, PQ_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
 }
 
 template <int E>
-static hipError_t launch_pq_e(const ScanArgs &a, const CandOut &o, int groups, hipStream_t s)
+static hipError_t launch_pq_e(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
 {
     dim3 grid(groups, a.nq), block(PQ_WAVES * 64);
     const size_t lds = (size_t)a.pq_m * a.pq_ks * 4;
     switch (a.pq_m) {
-    case 8: hipLaunchKernelGGL((scan_pq_kernel<E, 8>), grid, block, lds, s, a, o); break;
-    case 16: hipLaunchKernelGGL((scan_pq_kernel<E, 16>), grid, block, lds, s, a, o); break;
-    case 32: hipLaunchKernelGGL((scan_pq_kernel<E, 32>), grid, block, lds, s, a, o); break;
-    case 64: hipLaunchKernelGGL((scan_pq_kernel<E, 64>), grid, block, lds, s, a, o); break;
-    default: hipLaunchKernelGGL((scan_pq_kernel<E, 0>), grid, block, lds, s, a, o); break;
+    case 8: hipLaunchKernelGGL((scan_pq_kernel<E, 8>), grid, block, lds, s, a, partials); break;
+    case 16: hipLaunchKernelGGL((scan_pq_kernel<E, 16>), grid, block, lds, s, a, partials); break;
+    case 32: hipLaunchKernelGGL((scan_pq_kernel<E, 32>), grid, block, lds, s, a, partials); break;
+    case 64: hipLaunchKernelGGL((scan_pq_kernel<E, 64>), grid, block, lds, s, a, partials); break;
+    default: hipLaunchKernelGGL((scan_pq_kernel<E, 0>), grid, block, lds, s, a, partials); break;
     }
     return hipGetLastError();
 }
 
-hipError_t launch_scan_pq(const ScanArgs &a, const CandOut &o, int groups, hipStream_t s)
+hipError_t launch_scan_pq(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
 {
     if ((size_t)a.pq_m * a.pq_ks * 4 > 160 * 1024) return hipErrorInvalidValue;
-    if (a.k <= 64) return launch_pq_e<1>(a, o, groups, s);
-    if (a.k <= 128) return launch_pq_e<2>(a, o, groups, s);
-    return launch_pq_e<4>(a, o, groups, s);
+    if (a.k <= 64) return launch_pq_e<1>(a, partials, groups, s);
+    if (a.k <= 128) return launch_pq_e<2>(a, partials, groups, s);
+    return launch_pq_e<4>(a, partials, groups, s);
 }
 
 __global__ void pq_adc_rows_kernel(int metric, const float *lut, uint32_t m, uint32_t ks, const uint8_t *codes,

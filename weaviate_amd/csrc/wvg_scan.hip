@@ -19,6 +19,12 @@ namespace wvg {
 
 constexpr int SCAN_WAVES = 4;
 
+Tuning &tuning()
+{
+    static Tuning t;
+    return t;
+}
+
 // Wave index as a wave-uniform (SGPR) value, so per-wave loops, the tile mask
 // loads and the skip branch are scalar.
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
@@ -44,8 +50,15 @@ __device__ __forceinline__ void wave_range(const ScanArgs &a, int waves_per_grou
     t1 = a.tile_begin + ntiles * (gw + 1) / total;
 }
 
+__device__ __forceinline__ uint64_t lane_key(uint64_t m, float dist, uint64_t t, int lane)
+{
+    return ((m >> lane) & 1ull) ? wvg_make_key(dist, (uint32_t)(t * 64 + lane)) : WVG_KEY_NONE;
+}
+
+// Variant 0 (and 2 = plain loads): one tile's loads in flight per wave; tiles
+// with no live/allowed row are skipped without touching their rows.
 template <int METRIC, int D, int E>
-__global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_kernel(ScanArgs a, CandOut o)
+__global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_kernel(ScanArgs a, uint64_t *partials)
 {
     const int lane = threadIdx.x & 63;
     const uint32_t qi = blockIdx.y;
@@ -66,83 +79,192 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_kernel(ScanArgs a, C
             r = row_dot_or_l2_fixed<METRIC, D, 64>(rp, q4);
         else
             r = row_dot_or_l2_generic<METRIC, 64>(rp, q4, (int)a.dim);
-        const float dist = wrap_metric(a.metric, r);
-        const uint64_t key = ((m >> lane) & 1ull) ? wvg_make_key(dist, (uint32_t)(t * 64 + lane)) : WVG_KEY_NONE;
-        tk.offer(key);
+        tk.offer(lane_key(m, wrap_metric(a.metric, r), t, lane));
     }
-    group_publish<E, SCAN_WAVES>(tk, reinterpret_cast<CandHeader *>(o.hdr) + qi, o.cand + (size_t)qi * o.cap);
+    group_combine_store<E, SCAN_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
 }
 
-// Grid: every wave resident at once (3 workgroups of 4 waves per CU at the
-// d=128 kernel's 167 VGPRs), each wave owning a contiguous tile range; at
-// least 2 tiles per wave.  For nq > 1 the queries share the machine.
+// Variant 1: block-granular software pipeline.  The wave's tile range is a
+// flat sequence of 32-float blocks (8 chunks = 8 KiB per wave); the loads of
+// the next two blocks are in flight while a block is folded, across tile
+// boundaries, so a wave never idles the memory system between tiles.  Every
+// tile is loaded (no skip): used when there is no allow list.
+template <int METRIC, int D, int E>
+__global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_pipe_kernel(ScanArgs a, uint64_t *partials)
+{
+    static_assert(D % 32 == 0 && D > 0, "pipelined scan needs a fixed D % 32 == 0");
+    constexpr int NB = D / 32;
+    const int lane = threadIdx.x & 63;
+    const uint32_t qi = blockIdx.y;
+    const float4 *q4 = reinterpret_cast<const float4 *>(a.queries) + (size_t)qi * (a.qpitch / 4);
+    const float4 *data = reinterpret_cast<const float4 *>(a.data) + lane;
+    uint64_t t0, t1;
+    wave_range(a, SCAN_WAVES, t0, t1);
+    WaveTopK<E> tk;
+    tk.init((int)a.k);
+    const uint64_t nunits = (t1 - t0) * NB;
+    float acc[4][8];
+    uint64_t m = 0;
+    float4 b0[8], b1[8], b2[8];
+    auto load_unit = [&](float4 (&buf)[8], uint64_t u) {
+        if (u < nunits) {
+            const uint64_t t = t0 + u / NB;
+            const uint32_t b = (uint32_t)(u % NB);
+            const float4 *p = data + ((size_t)t * (D / 4) + b * 8) * 64;
+#pragma unroll
+            for (int cc = 0; cc < 8; cc++) buf[cc] = ld_stream(p + cc * 64);
+        }
+    };
+    auto consume = [&](const float4 (&buf)[8], uint64_t u) {
+        const uint64_t t = t0 + u / NB;
+        const uint32_t b = (uint32_t)(u % NB);
+        if (b == 0) {
+            m = tile_mask(a, t);
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+#pragma unroll
+                for (int l = 0; l < 8; l++) acc[j][l] = 0.0f;
+        }
+#pragma unroll
+        for (int cc = 0; cc < 8; cc++) chunk_update<METRIC>(acc, cc, q4[b * 8 + cc], buf[cc]);
+        if (b == NB - 1) tk.offer(lane_key(m, wrap_metric(a.metric, avx256_reduce(acc, 0.0f)), t, lane));
+    };
+    load_unit(b0, 0);
+    load_unit(b1, 1);
+    for (uint64_t u = 0; u < nunits; u += 3) {
+        load_unit(b2, u + 2);
+        consume(b0, u);
+        if (u + 1 >= nunits) break;
+        load_unit(b0, u + 3);
+        consume(b1, u + 1);
+        if (u + 2 >= nunits) break;
+        load_unit(b1, u + 4);
+        consume(b2, u + 2);
+    }
+    group_combine_store<E, SCAN_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
+}
+
+// Plain-load twin of variant 0 for A/B (variant 2).
+template <int METRIC, int D, int E>
+__global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_plain_kernel(ScanArgs a, uint64_t *partials)
+{
+    const int lane = threadIdx.x & 63;
+    const uint32_t qi = blockIdx.y;
+    const float4 *q4 = reinterpret_cast<const float4 *>(a.queries) + (size_t)qi * (a.qpitch / 4);
+    const float4 *data = reinterpret_cast<const float4 *>(a.data);
+    uint64_t t0, t1;
+    wave_range(a, SCAN_WAVES, t0, t1);
+    WaveTopK<E> tk;
+    tk.init((int)a.k);
+    for (uint64_t t = t0; t < t1; ++t) {
+        const uint64_t m = tile_mask(a, t);
+        if (m == 0ull) continue;
+        const float4 *rp = data + (size_t)t * a.nchunks * 64 + lane;
+        const float r = row_dot_or_l2_generic<METRIC, 64>(rp, q4, D);
+        tk.offer(lane_key(m, wrap_metric(a.metric, r), t, lane));
+    }
+    group_combine_store<E, SCAN_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
+}
+
+// Grid: `groups_per_cu` resident workgroups of 4 waves per CU (3 at the d=128
+// kernel's 167 VGPRs), each wave owning a contiguous tile range of at least 2
+// tiles.  For nq > 1 the queries share the machine.
 int scan_groups_for(const ScanArgs &a, int num_cus)
 {
     const uint64_t ntiles = a.tile_end > a.tile_begin ? a.tile_end - a.tile_begin : 0;
     uint64_t g = (ntiles + SCAN_WAVES * 2 - 1) / (SCAN_WAVES * 2);
-    uint64_t cap = (uint64_t)num_cus * 3;
+    uint64_t cap = (uint64_t)num_cus * (uint64_t)std::max(1, tuning().groups_per_cu);
     if (a.nq > 1) cap = std::max<uint64_t>((uint64_t)num_cus / 4, cap / a.nq);
     if (g > cap) g = cap;
     if (g < 1) g = 1;
     return (int)g;
 }
 
+template <int METRIC, int D, int E>
+static void launch_fixed(const ScanArgs &a, uint64_t *partials, dim3 grid, dim3 block, hipStream_t s)
+{
+    const int v = tuning().scan_variant;
+    if (v == 1 && !a.allow)
+        hipLaunchKernelGGL((scan_f32_pipe_kernel<METRIC, D, E>), grid, block, 0, s, a, partials);
+    else if (v == 2)
+        hipLaunchKernelGGL((scan_f32_plain_kernel<METRIC, D, E>), grid, block, 0, s, a, partials);
+    else
+        hipLaunchKernelGGL((scan_f32_kernel<METRIC, D, E>), grid, block, 0, s, a, partials);
+}
+
 template <int METRIC, int E>
-static hipError_t launch_f32_e(const ScanArgs &a, const CandOut &o, int groups, hipStream_t s)
+static hipError_t launch_f32_e(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
 {
     dim3 grid(groups, a.nq), block(SCAN_WAVES * 64);
     switch (a.dim) {
-    case 128: hipLaunchKernelGGL((scan_f32_kernel<METRIC, 128, E>), grid, block, 0, s, a, o); break;
-    case 768: hipLaunchKernelGGL((scan_f32_kernel<METRIC, 768, E>), grid, block, 0, s, a, o); break;
-    case 1536: hipLaunchKernelGGL((scan_f32_kernel<METRIC, 1536, E>), grid, block, 0, s, a, o); break;
-    default: hipLaunchKernelGGL((scan_f32_kernel<METRIC, 0, E>), grid, block, 0, s, a, o); break;
+    case 128: launch_fixed<METRIC, 128, E>(a, partials, grid, block, s); break;
+    case 768: launch_fixed<METRIC, 768, E>(a, partials, grid, block, s); break;
+    case 1536: launch_fixed<METRIC, 1536, E>(a, partials, grid, block, s); break;
+    default: hipLaunchKernelGGL((scan_f32_kernel<METRIC, 0, E>), grid, block, 0, s, a, partials); break;
     }
     return hipGetLastError();
 }
 
 template <int METRIC>
-static hipError_t launch_f32_m(const ScanArgs &a, const CandOut &o, int groups, hipStream_t s)
+static hipError_t launch_f32_m(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
 {
-    if (a.k <= 64) return launch_f32_e<METRIC, 1>(a, o, groups, s);
-    if (a.k <= 128) return launch_f32_e<METRIC, 2>(a, o, groups, s);
-    return launch_f32_e<METRIC, 4>(a, o, groups, s);
+    if (a.k <= 64) return launch_f32_e<METRIC, 1>(a, partials, groups, s);
+    if (a.k <= 128) return launch_f32_e<METRIC, 2>(a, partials, groups, s);
+    return launch_f32_e<METRIC, 4>(a, partials, groups, s);
 }
 
-hipError_t launch_scan_f32(const ScanArgs &a, const CandOut &o, int groups, hipStream_t s)
+hipError_t launch_scan_f32(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
 {
-    if (a.metric == WVG_M_L2) return launch_f32_m<WVG_M_L2>(a, o, groups, s);
-    return launch_f32_m<WVG_M_DOT>(a, o, groups, s);
+    if (a.metric == WVG_M_L2) return launch_f32_m<WVG_M_L2>(a, partials, groups, s);
+    return launch_f32_m<WVG_M_DOT>(a, partials, groups, s);
 }
 
 // ---------------------------------------------------------------------------
-// Phase 2: [nq][n_per_query] keys -> final ids / dists / counts.
+// Phase 2: [nq][n_per_query] keys -> final ids / dists / counts.  One
+// workgroup of 16 waves per query; each wave prefetches its whole contiguous
+// share (up to 8 x 64 keys) in one round trip, offers it to its register
+// top-k, then the 16 lists are merged pairwise in LDS (4 levels).
 // ---------------------------------------------------------------------------
+constexpr int MERGE_WAVES = 16;
+constexpr int MERGE_PF = 8;
+
 template <int E>
-__global__ __launch_bounds__(SCAN_WAVES * 64) void merge_keys_kernel(const uint64_t *partials,
-                                                                     uint32_t n_per_query, uint32_t k,
-                                                                     uint64_t id_base, uint64_t *ids,
-                                                                     float *dists, uint32_t *counts)
+__global__ __launch_bounds__(MERGE_WAVES * 64) void merge_keys_kernel(const uint64_t *partials, uint32_t n_per_query,
+                                                                      uint32_t k, uint64_t id_base, uint64_t *ids,
+                                                                      float *dists, uint32_t *counts)
 {
+    __shared__ uint64_t sh[MERGE_WAVES][64 * E];
     const int lane = threadIdx.x & 63, wave = wave_id();
     const uint32_t qi = blockIdx.x;
     const uint64_t *src = partials + (size_t)qi * n_per_query;
+    const uint32_t per = ((n_per_query + MERGE_WAVES * 64 - 1) / (MERGE_WAVES * 64)) * 64;
+    const uint32_t lo = wave * per, hi = min(n_per_query, lo + per);
     WaveTopK<E> tk;
     tk.init((int)k);
-    for (uint32_t base = wave * 64; base < n_per_query; base += SCAN_WAVES * 64) {
-        const uint32_t i = base + lane;
-        tk.offer(i < n_per_query ? src[i] : WVG_KEY_NONE);
+    for (uint32_t base = lo; base < hi; base += MERGE_PF * 64) {
+        uint64_t v[MERGE_PF];
+#pragma unroll
+        for (int p = 0; p < MERGE_PF; p++) {
+            const uint32_t i = base + p * 64 + lane;
+            v[p] = i < hi ? src[i] : WVG_KEY_NONE;
+        }
+#pragma unroll
+        for (int p = 0; p < MERGE_PF; p++) tk.offer(v[p]);
     }
-    __shared__ uint64_t sh[SCAN_WAVES][64 * E];
 #pragma unroll
     for (int e = 0; e < E; e++) sh[wave][e * 64 + lane] = tk.l[e];
-    __syncthreads();
-    if (wave != 0) return;
-    for (int w = 1; w < SCAN_WAVES; w++) {
-        uint64_t o[E];
+    for (int step = 1; step < MERGE_WAVES; step <<= 1) {
+        __syncthreads();
+        if ((wave & (2 * step - 1)) == 0) {
+            uint64_t o[E];
 #pragma unroll
-        for (int e = 0; e < E; e++) o[e] = sh[w][e * 64 + lane];
-        merge_lists<E>(tk.l, o);
+            for (int e = 0; e < E; e++) o[e] = sh[wave + step][e * 64 + lane];
+            merge_lists<E>(tk.l, o);
+#pragma unroll
+            for (int e = 0; e < E; e++) sh[wave][e * 64 + lane] = tk.l[e];
+        }
     }
+    if (wave != 0) return;
     uint32_t cnt = 0;
 #pragma unroll
     for (int e = 0; e < E; e++) {
@@ -156,74 +278,12 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void merge_keys_kernel(const uint6
         }
     }
     if (lane == 0 && counts) counts[qi] = cnt;
-}
-
-// Phase 2 over the compacted candidates of one query per workgroup; the
-// candidate count is small (~K log(groups)), so 4 waves offer it in a few
-// batches.  Re-arms the header for the next call (stream order).
-template <int E>
-__global__ __launch_bounds__(SCAN_WAVES * 64) void merge_cands_kernel(CandOut o, uint32_t k, uint64_t id_base,
-                                                                      uint64_t *ids, float *dists, uint32_t *counts)
-{
-    const int lane = threadIdx.x & 63, wave = wave_id();
-    const uint32_t qi = blockIdx.x;
-    CandHeader *hdr = reinterpret_cast<CandHeader *>(o.hdr) + qi;
-    const uint32_t n = min(hdr->count, o.cap);
-    const uint64_t *src = o.cand + (size_t)qi * o.cap;
-    WaveTopK<E> tk;
-    tk.init((int)k);
-    for (uint32_t base = wave * 64; base < n; base += SCAN_WAVES * 64) {
-        const uint32_t i = base + lane;
-        tk.offer(i < n ? src[i] : WVG_KEY_NONE);
-    }
-    __shared__ uint64_t sh[SCAN_WAVES][64 * E];
-#pragma unroll
-    for (int e = 0; e < E; e++) sh[wave][e * 64 + lane] = tk.l[e];
-    __syncthreads();
-    if (wave != 0) return;
-    if (lane == 0) {  // every wave has read `count` (barrier above): re-arm
-        hdr->tau_c = 0ull;
-        hdr->count = 0u;
-    }
-    for (int w = 1; w < SCAN_WAVES; w++) {
-        uint64_t oo[E];
-#pragma unroll
-        for (int e = 0; e < E; e++) oo[e] = sh[w][e * 64 + lane];
-        merge_lists<E>(tk.l, oo);
-    }
-    uint32_t cnt = 0;
-#pragma unroll
-    for (int e = 0; e < E; e++) {
-        const uint32_t i = e * 64 + lane;
-        const uint64_t key = tk.l[e];
-        const bool live = i < k && key != WVG_KEY_NONE;
-        cnt += (uint32_t)__popcll(__ballot(live));
-        if (i < k) {
-            ids[(size_t)qi * k + i] = live ? id_base + (key & 0xFFFFFFFFull) : WVG_KEY_NONE;
-            dists[(size_t)qi * k + i] = live ? wvg_unord_f32((uint32_t)(key >> 32)) : __builtin_inff();
-        }
-    }
-    if (lane == 0 && counts) counts[qi] = cnt;
-}
-
-hipError_t launch_merge_cands(const CandOut &o, uint32_t nq, uint32_t k, uint64_t id_base, uint64_t *ids, float *dists,
-                              uint32_t *counts, hipStream_t s)
-{
-    dim3 grid(nq), block(SCAN_WAVES * 64);
-    if (k <= 64)
-        hipLaunchKernelGGL((merge_cands_kernel<1>), grid, block, 0, s, o, k, id_base, ids, dists, counts);
-    else if (k <= 128)
-        hipLaunchKernelGGL((merge_cands_kernel<2>), grid, block, 0, s, o, k, id_base, ids, dists, counts);
-    else
-        hipLaunchKernelGGL((merge_cands_kernel<4>), grid, block, 0, s, o, k, id_base, ids, dists, counts);
-    return hipGetLastError();
 }
 
 hipError_t launch_merge_keys(const uint64_t *partials, uint32_t nq, uint32_t n_per_query, uint32_t k,
-                             uint64_t id_base, uint64_t *ids, float *dists, uint32_t *counts,
-                             hipStream_t s)
+                             uint64_t id_base, uint64_t *ids, float *dists, uint32_t *counts, hipStream_t s)
 {
-    dim3 grid(nq), block(SCAN_WAVES * 64);
+    dim3 grid(nq), block(MERGE_WAVES * 64);
     if (k <= 64)
         hipLaunchKernelGGL((merge_keys_kernel<1>), grid, block, 0, s, partials, n_per_query, k, id_base, ids, dists, counts);
     else if (k <= 128)

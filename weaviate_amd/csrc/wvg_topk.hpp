@@ -132,57 +132,11 @@ struct WaveTopK {
     }
 };
 
-// ---------------------------------------------------------------------------
-// Cross-workgroup candidate compaction.  Each (query) owns a header and a
-// candidate buffer.  tau_c holds the COMPLEMENT of the smallest K-th key any
-// workgroup has published so far (so a zero-filled header means "none yet");
-// that key bounds the final K-th key from above, so a workgroup only appends
-// the entries of its list that are <= it.  The merge kernel reads `count`
-// candidates and re-arms the header to zero for the next call.
-// ---------------------------------------------------------------------------
-struct CandHeader {
-    unsigned long long tau_c;
-    unsigned int count;
-    unsigned int pad;
-};
-
-// Wave-level publish of a finished list (all 64 lanes of one wave).
-template <int E>
-__device__ __forceinline__ void publish_list(WaveTopK<E> &tk, CandHeader *hdr, uint64_t *cand)
-{
-    const int lane = threadIdx.x & 63;
-    tk.refresh_tau();  // K-th key of this list (KEY_NONE if fewer than K)
-    unsigned long long thr = 0;
-    if (lane == 0) {
-        const unsigned long long old_c = atomicMax(&hdr->tau_c, ~(unsigned long long)tk.tau);
-        const unsigned long long old = ~old_c;
-        thr = old < tk.tau ? old : tk.tau;
-    }
-    thr = readlane64(thr, 0);
-    bool pred[E];
-    uint32_t tot = 0;
-#pragma unroll
-    for (int e = 0; e < E; e++) {
-        const int i = e * 64 + lane;
-        pred[e] = i < tk.k && tk.l[e] != WVG_KEY_NONE && tk.l[e] <= thr;
-        tot += (uint32_t)__popcll(__ballot(pred[e]));
-    }
-    if (tot == 0) return;
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(&hdr->count, tot);
-    base = __builtin_amdgcn_readfirstlane(base);
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));  // lanes below this one
-#pragma unroll
-    for (int e = 0; e < E; e++) {
-        const uint64_t msk = __ballot(pred[e]);
-        if (pred[e]) cand[base + (uint32_t)__popcll(msk & lt)] = tk.l[e];
-        base += (uint32_t)__popcll(msk);
-    }
-}
-
-// Workgroup combine (WAVES wave lists -> one, in wave 0) + publish.
+// Workgroup combine: WAVES wave lists -> one sorted list in wave 0, which
+// writes its first K keys to `out` (dense per-workgroup partials: no atomics,
+// so the workgroups that all finish together never contend).
 template <int E, int WAVES>
-__device__ __forceinline__ void group_publish(WaveTopK<E> &tk, CandHeader *hdr, uint64_t *cand)
+__device__ __forceinline__ void group_combine_store(WaveTopK<E> &tk, uint64_t *out)
 {
     __shared__ uint64_t sh[WAVES][64 * E];
     const int lane = threadIdx.x & 63;
@@ -199,7 +153,11 @@ __device__ __forceinline__ void group_publish(WaveTopK<E> &tk, CandHeader *hdr, 
         for (int e = 0; e < E; e++) o[e] = sh[w][e * 64 + lane];
         merge_lists<E>(tk.l, o);
     }
-    publish_list<E>(tk, hdr, cand);
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const int i = e * 64 + lane;
+        if (i < tk.k) out[i] = tk.l[e];
+    }
 }
 
 }  // namespace wvg
