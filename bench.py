@@ -5,8 +5,9 @@
 Workload (BASELINE.json configs[0] shape, on the GPU): every GPU holds a
 1,000,000 x 128 fp32 shard (global docIDs rank*1M ..), generated in HBM by a
 counter-based RNG.  A step is a batch of B single-query searches: each query
-is one full scan of the shard (one K1 scan launch + one K2 merge launch per
-query, flat.searchByVector semantics), then -- for N > 1 -- one RCCL
+is one full scan of the shard (one K1 scan launch per query, flat.searchByVector
+semantics; each launch also runs the previous query's top-k merge on one extra
+workgroup -- wvg_search_device_pipelined), then -- for N > 1 -- one RCCL
 all-gather of the B x k (dist, id) candidates and one device merge
 (Index.objectVectorSearch's shard merge).  Weak scaling: value = query
 scans of 1M rows per second over all GPUs = N * B * steps / time.
@@ -110,7 +111,7 @@ def main():
     ids = torch.empty((B, k), dtype=torch.int64, device=dev)
     dists = torch.empty((B, k), dtype=torch.float32, device=dev)
     counts = torch.empty(B, dtype=torch.int32, device=dev)
-    ws_bytes = lib.wvg_search_workspace_size(corpus.handle, 1, k)
+    ws_bytes = lib.wvg_search_workspace_size(corpus.handle, B, k)
     ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=dev)  # zero-filled once; calls keep it armed
     if world > 1:
         g_d = torch.empty(world * B * k, dtype=torch.float32, device=dev)
@@ -120,11 +121,13 @@ def main():
         m_c = torch.empty(B, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
+    assert P % B == 0
+
     def step(s):
-        for j in range(B):
-            qi = (s * B + j) % P
-            check(lib.wvg_search_device(corpus.handle, tq[qi].data_ptr(), 1, k, ids[j].data_ptr(),
-                                        dists[j].data_ptr(), counts[j].data_ptr(), ws.data_ptr(), ws_bytes, stream))
+        # B single-query scans in one call; query i's launch also merges query i-1
+        q0 = (s * B) % P
+        check(lib.wvg_search_device_pipelined(corpus.handle, tq[q0].data_ptr(), B, k, ids.data_ptr(),
+                                              dists.data_ptr(), counts.data_ptr(), ws.data_ptr(), ws_bytes, stream))
         if world > 1:
             dist.all_gather_into_tensor(g_d, dists.view(-1))
             dist.all_gather_into_tensor(g_i, ids.view(-1))

@@ -123,6 +123,14 @@ size_t wvg_search_workspace_size(wvg_corpus *c, uint32_t nq, uint32_t k);
 int wvg_search_device(wvg_corpus *c, const float *d_queries, uint32_t nq, uint32_t k,
                       uint64_t *d_ids, float *d_dists, uint32_t *d_counts, void *d_workspace,
                       size_t workspace_bytes, void *stream);
+/* nq independent single-query searches (each one full scan of the corpus:
+ * flat.SearchByVector per query, as concurrent Weaviate queries issue them)
+ * in ONE call: query i's scan launch also runs query i-1's top-k merge on one
+ * extra workgroup, so the merges cost no launches of their own.  F32
+ * corpora; same workspace size rule; outputs as wvg_search_device.        */
+int wvg_search_device_pipelined(wvg_corpus *c, const float *d_queries, uint32_t nq, uint32_t k,
+                                uint64_t *d_ids, float *d_dists, uint32_t *d_counts,
+                                void *d_workspace, size_t workspace_bytes, void *stream);
 /* Multi-shard merge (Index.objectVectorSearch, adapters/repos/db/index.go:1644-1648):
  * [nlists][nq][k_in] (dist, id) lists (the layout an all-gather of per-GPU
  * [nq][k_in] results produces) -> [nq][k] ascending, ties by id; missing

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--variants", default="0,1,2")
     ap.add_argument("--gpcu", default="2,3,4,6")
     ap.add_argument("--metric", type=int, default=0)
+    ap.add_argument("--pipelined", action="store_true")
     args = ap.parse_args()
     import torch
 
@@ -56,7 +57,15 @@ def main():
                 wsb = lib.wvg_search_workspace_size(c.handle, 1, k)
                 ws = torch.zeros(wsb, dtype=torch.uint8, device=dev)
 
+                wsb = lib.wvg_search_workspace_size(c.handle, Q, k)
+                ws = torch.zeros(wsb, dtype=torch.uint8, device=dev)
+
                 def run():
+                    if args.pipelined:
+                        check(lib.wvg_search_device_pipelined(c.handle, qs.data_ptr(), Q, k, ids.data_ptr(),
+                                                              dists.data_ptr(), cnt.data_ptr(), ws.data_ptr(), wsb,
+                                                              stream))
+                        return
                     for j in range(Q):
                         check(lib.wvg_search_device(c.handle, qs[j].data_ptr(), 1, k, ids[j].data_ptr(),
                                                     dists[j].data_ptr(), cnt[j].data_ptr(), ws.data_ptr(), wsb,

@@ -53,6 +53,8 @@ SIGNATURES = {
     "wvg_search_workspace_size": (c_size_t, [c_void_p, c_uint32, c_uint32]),
     "wvg_search_device": (c_int, [c_void_p, c_void_p, c_uint32, c_uint32, c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_size_t, c_void_p]),
+    "wvg_search_device_pipelined": (c_int, [c_void_p, c_void_p, c_uint32, c_uint32, c_void_p, c_void_p, c_void_p,
+                                            c_void_p, c_size_t, c_void_p]),
     "wvg_topk_merge_device": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_uint32, c_uint32, c_uint32,
                                       c_void_p, c_void_p, c_void_p, c_void_p]),
     "wvg_profile_start": (c_int, [c_void_p]),

@@ -745,7 +745,7 @@ static int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t 
     else
         WVG_HIP(launch_scan(a, c->kind, partials, groups, s));
     if (ev.second) WVG_HIP(hipEventRecord(ev.second, s));
-    WVG_HIP(launch_merge_keys(partials, nq, (uint32_t)groups * k, k, c->id_base, ids, dists, counts, s));
+    WVG_HIP(launch_merge_lists(partials, nq, (uint32_t)groups, k, k, c->id_base, ids, dists, counts, s));
     return WVG_OK;
 }
 
@@ -938,7 +938,7 @@ int wvg_search_bq_rescore(wvg_corpus *bq, wvg_corpus *f32, const float *queries,
     WVG_HIP(launch_scan_bq(a, part, p.groups, s));
     // Hamming top-R; ids are id_base + slot, so id_base = 0 keeps the slots
     uint64_t *cand_ids = (uint64_t *)(b + o_cand);
-    WVG_HIP(launch_merge_keys(part, nq, (uint32_t)p.groups * R, R, 0, cand_ids, (float *)(b + o_resc), nullptr, s));
+    WVG_HIP(launch_merge_lists(part, nq, (uint32_t)p.groups, R, R, 0, cand_ids, (float *)(b + o_resc), nullptr, s));
     // cand_ids now hold slots (or KEY_NONE); rescore them exactly against the f32 rows
     WVG_HIP(launch_rescore_keys(f32->metric, (const float *)(b + o_qf), qpf, (const float *)f32->d_data, d,
                                 f32->nchunks, cand_ids, nq, R, R, (uint64_t *)(b + o_resc), s));
@@ -954,10 +954,60 @@ int wvg_search_bq_rescore(wvg_corpus *bq, wvg_corpus *f32, const float *queries,
 size_t wvg_search_workspace_size(wvg_corpus *c, uint32_t nq, uint32_t k)
 {
     if (!c) return 0;
+    const uint32_t kk = std::max<uint32_t>(k, 1);
     SearchPlan p = plan_search(c, nq, k, nullptr, 0);
-    Carver cv;
-    cv.take(p.workspace_bytes(nq, std::max<uint32_t>(k, 1)));
-    return cv.off;
+    SearchPlan p1 = plan_search(c, 1, k, nullptr, 0);  // pipelined mode: two single-query buffers
+    return std::max(align_up(p.workspace_bytes(nq, kk), 256), 2 * align_up(p1.workspace_bytes(1, kk), 256));
+}
+
+int wvg_search_device_pipelined(wvg_corpus *c, const float *d_queries, uint32_t nq, uint32_t k, uint64_t *d_ids,
+                                float *d_dists, uint32_t *d_counts, void *d_workspace, size_t workspace_bytes,
+                                void *stream)
+{
+    if (!c) return fail(WVG_ERR_INVALID, "null corpus");
+    if (k > MAX_K) return fail(WVG_ERR_UNSUPPORTED, "k above 256 is not supported by the fused top-k");
+    if (c->kind != WVG_KIND_F32) return fail(WVG_ERR_UNSUPPORTED, "pipelined search supports F32 corpora");
+    if (c->dim % 4 != 0) return fail(WVG_ERR_UNSUPPORTED, "device search needs dim % 4 == 0");
+    if (nq == 0 || k == 0) return WVG_OK;
+    hipStream_t s = (hipStream_t)stream;
+    std::shared_lock<std::shared_mutex> lk(c->rw);
+    SearchPlan p = plan_search(c, 1, k, nullptr, 0);
+    if (p.empty) return WVG_OK;
+    const size_t half = align_up(p.workspace_bytes(1, k), 256);
+    if (!d_workspace || workspace_bytes < 2 * half) return fail(WVG_ERR_INVALID, "workspace too small");
+    uint64_t *buf[2] = {(uint64_t *)d_workspace, (uint64_t *)((char *)d_workspace + half)};
+    ScanArgs a{};
+    a.data = c->d_data;
+    a.valid = c->d_valid;
+    a.id_base = c->id_base;
+    a.tile_begin = p.tb;
+    a.tile_end = p.te;
+    a.dim = c->dim;
+    a.nchunks = c->nchunks;
+    a.metric = c->metric;
+    a.qpitch = c->dim;
+    a.nq = 1;
+    a.k = k;
+    for (uint32_t i = 0; i < nq; i++) {
+        a.queries = d_queries + (size_t)i * c->dim;
+        a.side = MergeJob{};
+        if (i > 0) {
+            a.side = MergeJob{buf[(i - 1) & 1], (uint32_t)p.groups, k, k, c->id_base, d_ids + (size_t)(i - 1) * k,
+                              d_dists + (size_t)(i - 1) * k, d_counts ? d_counts + (i - 1) : nullptr, 1};
+        }
+        std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
+        if (c->ctx->profiling.load(std::memory_order_relaxed)) {
+            int rc = prof_pair(c->ctx, &ev);
+            if (rc) return rc;
+            WVG_HIP(hipEventRecord(ev.first, s));
+        }
+        WVG_HIP(launch_scan_f32(a, buf[i & 1], p.groups, s));
+        if (ev.second) WVG_HIP(hipEventRecord(ev.second, s));
+    }
+    const uint32_t last = nq - 1;
+    WVG_HIP(launch_merge_lists(buf[last & 1], 1, (uint32_t)p.groups, k, k, c->id_base, d_ids + (size_t)last * k,
+                               d_dists + (size_t)last * k, d_counts ? d_counts + last : nullptr, s));
+    return WVG_OK;
 }
 
 int wvg_search_device(wvg_corpus *c, const float *d_queries, uint32_t nq, uint32_t k, uint64_t *d_ids, float *d_dists,

@@ -86,6 +86,19 @@ size_t corpus_row_bytes(int kind, uint32_t dim, uint32_t pq_m);
 // ---- kernel launchers (wvg_scan.hip / wvg_bq.hip / wvg_pq.hip) -----------
 // Scan phase 1: per (query, workgroup) top-K keys into `partials`
 //   [nq][groups][K].  Returns the number of groups used.
+// A finished query's phase-2 merge, run by one extra workgroup of the next
+// query's scan launch (inputs complete by stream order): the merge costs no
+// launch of its own and overlaps the scan.
+struct MergeJob {
+    const uint64_t *partials;  // [nlists][list_len] ascending lists
+    uint32_t nlists, list_len, k;
+    uint64_t id_base;
+    uint64_t *ids;
+    float *dists;
+    uint32_t *counts;
+    int active;
+};
+
 struct ScanArgs {
     const void *data;          // tiled corpus
     const uint64_t *valid;     // one word per tile
@@ -99,6 +112,7 @@ struct ScanArgs {
     uint32_t qpitch;           // elements per query in `queries`
     uint32_t nq, k;
     uint32_t pq_m, pq_ks;
+    MergeJob side;             // F32 scan only; gridDim.x includes its workgroup
 };
 // Phase 1 writes dense partials [nq][groups][K] (keys, KEY_NONE = empty).
 int scan_groups_for(const ScanArgs &a, int num_cus);
@@ -115,7 +129,11 @@ struct Tuning {
     int groups_per_cu = 3;   // K1 resident workgroups per CU
 };
 Tuning &tuning();
-// Phase 2: merge [nq][n_per_query] keys into final (ids = id_base + slot, dists, counts).
+// Phase 2: per query `nlists` ascending lists of `list_len` keys -> final
+// (ids = id_base + slot, dists, counts).
+hipError_t launch_merge_lists(const uint64_t *partials, uint32_t nq, uint32_t nlists, uint32_t list_len, uint32_t k,
+                              uint64_t id_base, uint64_t *ids, float *dists, uint32_t *counts, hipStream_t s);
+// Unsorted [nq][n_per_query] keys (list_len = 1).
 hipError_t launch_merge_keys(const uint64_t *partials, uint32_t nq, uint32_t n_per_query, uint32_t k,
                              uint64_t id_base, uint64_t *ids, float *dists, uint32_t *counts,
                              hipStream_t s);

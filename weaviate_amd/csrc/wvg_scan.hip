@@ -44,10 +44,61 @@ __device__ __forceinline__ void wave_range(const ScanArgs &a, int waves_per_grou
                                            uint64_t &t1)
 {
     const uint64_t ntiles = a.tile_end - a.tile_begin;
-    const uint64_t total = (uint64_t)gridDim.x * waves_per_group;
+    const uint64_t groups = gridDim.x - (a.side.active ? 1u : 0u);
+    const uint64_t total = groups * waves_per_group;
     const uint64_t gw = (uint64_t)blockIdx.x * waves_per_group + wave_id();
     t0 = a.tile_begin + ntiles * gw / total;
     t1 = a.tile_begin + ntiles * (gw + 1) / total;
+}
+
+// Phase-2 merge body for one query (see merge_keys_kernel): WAVES waves read
+// `nlists` ascending lists transposed, then tree-merge in LDS; wave 0 writes.
+template <int E, int WAVES>
+__device__ __forceinline__ void merge_lists_body(const uint64_t *src, uint32_t nlists, uint32_t list_len, uint32_t k,
+                                                 uint64_t id_base, uint64_t *ids, float *dists, uint32_t *count)
+{
+    __shared__ uint64_t msh[WAVES][64 * E];
+    const int lane = threadIdx.x & 63, wave = wave_id();
+    WaveTopK<E> tk;
+    tk.init((int)k);
+    for (uint32_t g0 = (uint32_t)wave * 64; g0 < nlists; g0 += WAVES * 64) {
+        const uint32_t list = g0 + lane;
+        const uint64_t *lp = src + (size_t)list * list_len;
+        uint64_t cur = list < nlists ? lp[0] : WVG_KEY_NONE;
+        for (uint32_t r = 0; r < list_len; r++) {
+            const uint64_t nxt = (r + 1 < list_len && list < nlists) ? lp[r + 1] : WVG_KEY_NONE;  // prefetch
+            if (list_len > 1 && r > 0 && __ballot(cur < tk.tau) == 0ull) break;  // sorted lists: done
+            tk.offer(cur);
+            cur = nxt;
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < E; e++) msh[wave][e * 64 + lane] = tk.l[e];
+    for (int step = 1; step < WAVES; step <<= 1) {
+        __syncthreads();
+        if ((wave & (2 * step - 1)) == 0) {
+            uint64_t o[E];
+#pragma unroll
+            for (int e = 0; e < E; e++) o[e] = msh[wave + step][e * 64 + lane];
+            merge_lists<E>(tk.l, o);
+#pragma unroll
+            for (int e = 0; e < E; e++) msh[wave][e * 64 + lane] = tk.l[e];
+        }
+    }
+    if (wave != 0) return;
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const uint32_t i = e * 64 + lane;
+        const uint64_t key = tk.l[e];
+        const bool live = i < k && key != WVG_KEY_NONE;
+        cnt += (uint32_t)__popcll(__ballot(live));
+        if (i < k) {
+            ids[i] = live ? id_base + (key & 0xFFFFFFFFull) : WVG_KEY_NONE;
+            dists[i] = live ? wvg_unord_f32((uint32_t)(key >> 32)) : __builtin_inff();
+        }
+    }
+    if (lane == 0 && count) *count = cnt;
 }
 
 __device__ __forceinline__ uint64_t lane_key(uint64_t m, float dist, uint64_t t, int lane)
@@ -60,6 +111,12 @@ __device__ __forceinline__ uint64_t lane_key(uint64_t m, float dist, uint64_t t,
 template <int METRIC, int D, int E>
 __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_kernel(ScanArgs a, uint64_t *partials)
 {
+    if (a.side.active && blockIdx.x == gridDim.x - 1) {  // the previous query's merge (uniform branch)
+        if (blockIdx.y == 0)
+            merge_lists_body<E, SCAN_WAVES>(a.side.partials, a.side.nlists, a.side.list_len, a.side.k,
+                                            a.side.id_base, a.side.ids, a.side.dists, a.side.counts);
+        return;
+    }
     const int lane = threadIdx.x & 63;
     const uint32_t qi = blockIdx.y;
     const float4 *q4 = reinterpret_cast<const float4 *>(a.queries) + (size_t)qi * (a.qpitch / 4);
@@ -144,6 +201,37 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_pipe_kernel(ScanArgs
     group_combine_store<E, SCAN_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
 }
 
+// Variant 3: as variant 0, but tiles are dealt round-robin to the waves of
+// the whole grid (wave g takes tiles g, g + G, g + 2G, ...), so at any moment
+// all waves read neighbouring tiles: one sweeping front through HBM instead of
+// thousands of separate streams (DRAM row-buffer locality).
+template <int METRIC, int D, int E>
+__global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_sweep_kernel(ScanArgs a, uint64_t *partials)
+{
+    const int lane = threadIdx.x & 63;
+    const uint32_t qi = blockIdx.y;
+    const float4 *q4 = reinterpret_cast<const float4 *>(a.queries) + (size_t)qi * (a.qpitch / 4);
+    const float4 *data = reinterpret_cast<const float4 *>(a.data);
+    const uint64_t G = (uint64_t)gridDim.x * SCAN_WAVES;
+    const uint64_t t0 = a.tile_begin + (uint64_t)blockIdx.x * SCAN_WAVES + wave_id();
+    WaveTopK<E> tk;
+    tk.init((int)a.k);
+    uint64_t m_next = t0 < a.tile_end ? tile_mask(a, t0) : 0ull;
+    for (uint64_t t = t0; t < a.tile_end; t += G) {
+        const uint64_t m = m_next;
+        if (t + G < a.tile_end) m_next = tile_mask(a, t + G);
+        if (m == 0ull) continue;
+        const float4 *rp = data + (size_t)t * a.nchunks * 64 + lane;
+        float r;
+        if constexpr (D > 0)
+            r = row_dot_or_l2_fixed<METRIC, D, 64>(rp, q4);
+        else
+            r = row_dot_or_l2_generic<METRIC, 64>(rp, q4, (int)a.dim);
+        tk.offer(lane_key(m, wrap_metric(a.metric, r), t, lane));
+    }
+    group_combine_store<E, SCAN_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
+}
+
 // Plain-load twin of variant 0 for A/B (variant 2).
 template <int METRIC, int D, int E>
 __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_plain_kernel(ScanArgs a, uint64_t *partials)
@@ -183,11 +271,13 @@ int scan_groups_for(const ScanArgs &a, int num_cus)
 template <int METRIC, int D, int E>
 static void launch_fixed(const ScanArgs &a, uint64_t *partials, dim3 grid, dim3 block, hipStream_t s)
 {
-    const int v = tuning().scan_variant;
+    const int v = a.side.active ? 0 : tuning().scan_variant;
     if (v == 1 && !a.allow)
         hipLaunchKernelGGL((scan_f32_pipe_kernel<METRIC, D, E>), grid, block, 0, s, a, partials);
     else if (v == 2)
         hipLaunchKernelGGL((scan_f32_plain_kernel<METRIC, D, E>), grid, block, 0, s, a, partials);
+    else if (v == 3)
+        hipLaunchKernelGGL((scan_f32_sweep_kernel<METRIC, D, E>), grid, block, 0, s, a, partials);
     else
         hipLaunchKernelGGL((scan_f32_kernel<METRIC, D, E>), grid, block, 0, s, a, partials);
 }
@@ -195,7 +285,7 @@ static void launch_fixed(const ScanArgs &a, uint64_t *partials, dim3 grid, dim3 
 template <int METRIC, int E>
 static hipError_t launch_f32_e(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
 {
-    dim3 grid(groups, a.nq), block(SCAN_WAVES * 64);
+    dim3 grid(groups + (a.side.active ? 1 : 0), a.nq), block(SCAN_WAVES * 64);
     switch (a.dim) {
     case 128: launch_fixed<METRIC, 128, E>(a, partials, grid, block, s); break;
     case 768: launch_fixed<METRIC, 768, E>(a, partials, grid, block, s); break;
@@ -220,77 +310,45 @@ hipError_t launch_scan_f32(const ScanArgs &a, uint64_t *partials, int groups, hi
 }
 
 // ---------------------------------------------------------------------------
-// Phase 2: [nq][n_per_query] keys -> final ids / dists / counts.  One
-// workgroup of 16 waves per query; each wave prefetches its whole contiguous
-// share (up to 8 x 64 keys) in one round trip, offers it to its register
-// top-k, then the 16 lists are merged pairwise in LDS (4 levels).
+// Phase 2: per query, `nlists` ascending lists of `list_len` keys -> final ids
+// / dists / counts.  The lists are read TRANSPOSED: a wave takes 64 lists and
+// offers batch r = the r-th key of each; batch 0 (the 64 list heads) is
+// sorted once, after which almost every lane is rejected by one compare, and
+// the first batch with no key below the threshold ends the group (every later
+// key of those lists is larger).  Unsorted input: list_len = 1.
 // ---------------------------------------------------------------------------
-constexpr int MERGE_WAVES = 16;
-constexpr int MERGE_PF = 8;
+constexpr int MERGE_WAVES = 8;
 
 template <int E>
-__global__ __launch_bounds__(MERGE_WAVES * 64) void merge_keys_kernel(const uint64_t *partials, uint32_t n_per_query,
-                                                                      uint32_t k, uint64_t id_base, uint64_t *ids,
-                                                                      float *dists, uint32_t *counts)
+__global__ __launch_bounds__(MERGE_WAVES * 64) void merge_keys_kernel(const uint64_t *partials, uint32_t nlists,
+                                                                      uint32_t list_len, uint32_t k, uint64_t id_base,
+                                                                      uint64_t *ids, float *dists, uint32_t *counts)
 {
-    __shared__ uint64_t sh[MERGE_WAVES][64 * E];
-    const int lane = threadIdx.x & 63, wave = wave_id();
     const uint32_t qi = blockIdx.x;
-    const uint64_t *src = partials + (size_t)qi * n_per_query;
-    const uint32_t per = ((n_per_query + MERGE_WAVES * 64 - 1) / (MERGE_WAVES * 64)) * 64;
-    const uint32_t lo = wave * per, hi = min(n_per_query, lo + per);
-    WaveTopK<E> tk;
-    tk.init((int)k);
-    for (uint32_t base = lo; base < hi; base += MERGE_PF * 64) {
-        uint64_t v[MERGE_PF];
-#pragma unroll
-        for (int p = 0; p < MERGE_PF; p++) {
-            const uint32_t i = base + p * 64 + lane;
-            v[p] = i < hi ? src[i] : WVG_KEY_NONE;
-        }
-#pragma unroll
-        for (int p = 0; p < MERGE_PF; p++) tk.offer(v[p]);
-    }
-#pragma unroll
-    for (int e = 0; e < E; e++) sh[wave][e * 64 + lane] = tk.l[e];
-    for (int step = 1; step < MERGE_WAVES; step <<= 1) {
-        __syncthreads();
-        if ((wave & (2 * step - 1)) == 0) {
-            uint64_t o[E];
-#pragma unroll
-            for (int e = 0; e < E; e++) o[e] = sh[wave + step][e * 64 + lane];
-            merge_lists<E>(tk.l, o);
-#pragma unroll
-            for (int e = 0; e < E; e++) sh[wave][e * 64 + lane] = tk.l[e];
-        }
-    }
-    if (wave != 0) return;
-    uint32_t cnt = 0;
-#pragma unroll
-    for (int e = 0; e < E; e++) {
-        const uint32_t i = e * 64 + lane;
-        const uint64_t key = tk.l[e];
-        const bool live = i < k && key != WVG_KEY_NONE;
-        cnt += (uint32_t)__popcll(__ballot(live));
-        if (i < k) {
-            ids[(size_t)qi * k + i] = live ? id_base + (key & 0xFFFFFFFFull) : WVG_KEY_NONE;
-            dists[(size_t)qi * k + i] = live ? wvg_unord_f32((uint32_t)(key >> 32)) : __builtin_inff();
-        }
-    }
-    if (lane == 0 && counts) counts[qi] = cnt;
+    merge_lists_body<E, MERGE_WAVES>(partials + (size_t)qi * nlists * list_len, nlists, list_len, k, id_base,
+                                     ids + (size_t)qi * k, dists + (size_t)qi * k, counts ? counts + qi : nullptr);
+}
+
+hipError_t launch_merge_lists(const uint64_t *partials, uint32_t nq, uint32_t nlists, uint32_t list_len, uint32_t k,
+                              uint64_t id_base, uint64_t *ids, float *dists, uint32_t *counts, hipStream_t s)
+{
+    dim3 grid(nq), block(MERGE_WAVES * 64);
+    if (k <= 64)
+        hipLaunchKernelGGL((merge_keys_kernel<1>), grid, block, 0, s, partials, nlists, list_len, k, id_base, ids,
+                           dists, counts);
+    else if (k <= 128)
+        hipLaunchKernelGGL((merge_keys_kernel<2>), grid, block, 0, s, partials, nlists, list_len, k, id_base, ids,
+                           dists, counts);
+    else
+        hipLaunchKernelGGL((merge_keys_kernel<4>), grid, block, 0, s, partials, nlists, list_len, k, id_base, ids,
+                           dists, counts);
+    return hipGetLastError();
 }
 
 hipError_t launch_merge_keys(const uint64_t *partials, uint32_t nq, uint32_t n_per_query, uint32_t k,
                              uint64_t id_base, uint64_t *ids, float *dists, uint32_t *counts, hipStream_t s)
 {
-    dim3 grid(nq), block(MERGE_WAVES * 64);
-    if (k <= 64)
-        hipLaunchKernelGGL((merge_keys_kernel<1>), grid, block, 0, s, partials, n_per_query, k, id_base, ids, dists, counts);
-    else if (k <= 128)
-        hipLaunchKernelGGL((merge_keys_kernel<2>), grid, block, 0, s, partials, n_per_query, k, id_base, ids, dists, counts);
-    else
-        hipLaunchKernelGGL((merge_keys_kernel<4>), grid, block, 0, s, partials, n_per_query, k, id_base, ids, dists, counts);
-    return hipGetLastError();
+    return launch_merge_lists(partials, nq, n_per_query, 1, k, id_base, ids, dists, counts, s);
 }
 
 // ---------------------------------------------------------------------------

@@ -18,9 +18,64 @@
 
 namespace wvg {
 
+// Lane exchange partner = lane ^ M, on the VALU (DPP / gfx950 permlane swaps)
+// instead of the LDS crossbar (ds_bpermute): a bitonic stage becomes a few
+// VALU moves instead of a ~100-cycle LDS round trip.
+//   M = 1, 2, 3 : quad_perm;  4, 8 : row_shl/row_shr by M, selected by lane bit;
+//   16 / 32 : v_permlane16_swap / v_permlane32_swap;  63 : reverse (row_mirror
+//   then the 16- and 32-lane swaps).
+template <int M>
+__device__ __forceinline__ uint32_t xor_lane32(uint32_t v)
+{
+    const int lane = __lane_id();
+    if constexpr (M == 1) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // [1,0,3,2]
+    } else if constexpr (M == 2) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
+    } else if constexpr (M == 4 || M == 8) {
+        const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x100 | M, 0xF, 0xF, false);  // row_shl:M
+        const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x110 | M, 0xF, 0xF, false);  // row_shr:M
+        return (lane & M) ? dn : up;
+    } else if constexpr (M == 16) {
+        auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (lane & 16) ? r[0] : r[1];
+    } else if constexpr (M == 32) {
+        auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (lane & 32) ? r[0] : r[1];
+    } else {
+        static_assert(M == 63, "unsupported lane xor");
+        const uint32_t m15 = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false);  // row_mirror
+        return xor_lane32<32>(xor_lane32<16>(m15));
+    }
+}
+
+template <int M>
+__device__ __forceinline__ uint64_t xor_lane64(uint64_t v)
+{
+    const uint32_t lo = xor_lane32<M>((uint32_t)v), hi = xor_lane32<M>((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
 __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m)
 {
-    return __shfl_xor(v, m, 64);
+    switch (m) {  // m is a compile-time constant at every (unrolled) call site
+    case 1: return xor_lane64<1>(v);
+    case 2: return xor_lane64<2>(v);
+    case 4: return xor_lane64<4>(v);
+    case 8: return xor_lane64<8>(v);
+    case 16: return xor_lane64<16>(v);
+    case 32: return xor_lane64<32>(v);
+    case 63: return xor_lane64<63>(v);
+    default: return __shfl_xor(v, m, 64);
+    }
+}
+
+// lane i receives lane i-1 (lane 0 receives 0): DPP wave_shr:1.
+__device__ __forceinline__ uint64_t shr1_lane64(uint64_t v)
+{
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, 0x138, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), 0x138, 0xF, 0xF, false);
+    return ((uint64_t)hi << 32) | lo;
 }
 
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane)
@@ -98,6 +153,27 @@ __device__ __forceinline__ void merge_lists(uint64_t (&l)[E], const uint64_t (&o
     bitonic_merge<E>(l);
 }
 
+// list <- list with key x inserted in order (elements shift up by one; the
+// last element falls off).  x must be smaller than the list's last element.
+template <int E>
+__device__ __forceinline__ void insert_one(uint64_t (&l)[E], uint64_t x)
+{
+    const int lane = __lane_id();
+    uint64_t prev[E];
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        uint64_t p = shr1_lane64(l[e]);
+        if (lane == 0) p = e == 0 ? 0ull : readlane64(l[e - 1], 63);  // 0 sorts below every key
+        prev[e] = p;
+    }
+#pragma unroll
+    for (int e = 0; e < E; e++) l[e] = l[e] < x ? l[e] : (prev[e] < x ? x : prev[e]);
+}
+
+// Batches with at most this many keys below the threshold are inserted one by
+// one; larger batches are bitonic-sorted and merged.
+constexpr int TOPK_INSERT_MAX = 12;
+
 template <int E>
 struct WaveTopK {
     uint64_t l[E];
@@ -125,10 +201,23 @@ struct WaveTopK {
     // Offer one key per lane (KEY_NONE for an empty lane).
     __device__ __forceinline__ void offer(uint64_t key)
     {
-        if (__ballot(key < tau) == 0ull) return;  // wave-uniform
-        sort64(key);
-        merge_sorted64<E>(l, key);
-        refresh_tau();
+        uint64_t mask = __ballot(key < tau);  // wave-uniform
+        if (mask == 0ull) return;
+        if (__popcll(mask) > TOPK_INSERT_MAX) {
+            sort64(key);
+            merge_sorted64<E>(l, key);
+            refresh_tau();
+            return;
+        }
+        while (mask) {
+            const int c = __builtin_ctzll(mask);
+            mask &= mask - 1;
+            const uint64_t x = readlane64(key, c);
+            if (x < tau) {
+                insert_one<E>(l, x);
+                refresh_tau();
+            }
+        }
     }
 };
 
