@@ -126,7 +126,7 @@ hipError_t launch_gemm_topk(const ScanArgs &a, uint32_t nrr, uint64_t *partials,
 // Internal tuning knobs (wvgx_set_tuning; A/B experiments, not public ABI).
 struct Tuning {
     int scan_variant = 0;    // K1 variant (see wvg_scan.hip)
-    int groups_per_cu = 3;   // K1 resident workgroups per CU
+    int groups_per_cu = 1;   // K1 workgroups per CU (A/B: 1 = fewest partial lists, same scan rate)
 };
 Tuning &tuning();
 // Phase 2: per query `nlists` ascending lists of `list_len` keys -> final
