@@ -139,6 +139,23 @@ int wvg_topk_merge_device(wvg_ctx *ctx, const float *d_dists, const uint64_t *d_
                           uint32_t nlists, uint32_t k_in, uint32_t k, uint64_t *d_out_ids,
                           float *d_out_dists, uint32_t *d_out_counts, void *stream);
 
+/* The rescore loop of flat.searchByVectorBQ (V/flat/index.go:375-385) when
+ * the candidate rows come from the host (LSM point gets): exact SingleDist of
+ * q against rows [n][dim] (q used as given: normalize it first for cosine,
+ * as index.go:352 does) and the top-k of (dist, id).  out_count = min(k, n). */
+int wvg_rescore(wvg_ctx *ctx, int metric, const float *q, const float *rows, const uint64_t *ids,
+                uint64_t n, uint32_t dim, uint32_t k, uint64_t *out_ids, float *out_dists,
+                uint32_t *out_count);
+/* Bulk PQ compression of a resident float corpus (hnsw.compress ->
+ * compressor.Preload per vector, V/hnsw/compress.go:98-104): every live row
+ * of `f32` is encoded with `pq`'s codebook into the same slot of `pq`.  Both
+ * corpora must share dim and id_base. */
+int wvg_pq_encode_corpus(wvg_corpus *pq, wvg_corpus *f32);
+/* Bench / test helper: the synthetic generator of wvg_corpus_fill_synthetic
+ * for arbitrary row ids: out [n][dim] (normalized if `normalize`). */
+int wvg_synthetic_rows(wvg_ctx *ctx, uint64_t seed, const uint64_t *ids, uint64_t n, uint32_t dim,
+                       int distribution, int normalize, float *out);
+
 /* Profiling: while enabled, every scan-kernel launch of this context is
  * bracketed by a pair of HIP events on its stream; stop() synchronizes and
  * returns the summed scan-kernel time and the launch count (feeds the

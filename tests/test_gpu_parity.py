@@ -316,6 +316,43 @@ def test_bq_rescore_flow(ctx, orc, metric):
     assert overlap >= k - 2
 
 
+@pytest.mark.parametrize("metric", [METRIC_L2, METRIC_DOT, METRIC_COSINE])
+def test_rescore_host_rows(ctx, orc, metric):
+    """wvg_rescore == exact SingleDist + top-k over host-fetched candidate rows;
+    ties resolve by input order (the reference inserts in its pop order)."""
+    import ctypes
+
+    lib = _lib.load()
+    n, d, k = 500, 1536, 10
+    rows = orc.synth_rows(71, 0, n, d, 0)
+    q = orc.synth_rows(72, 0, 1, d, 0)[0]
+    if metric == METRIC_COSINE:
+        rows, q = orc.normalize_rows(rows), orc.normalize(q)
+    rows[7] = rows[3]  # an exact tie
+    ids = (1000 + 3 * np.arange(n)[::-1]).astype(np.uint64)
+    oi = np.empty(k, np.uint64)
+    od = np.empty(k, np.float32)
+    cnt = ctypes.c_uint32()
+    _lib.check(lib.wvg_rescore(ctx.handle, metric, _lib.fptr(q), _lib.fptr(rows), _lib.u64ptr(ids), n, d, k,
+                               _lib.u64ptr(oi), _lib.fptr(od), ctypes.byref(cnt)))
+    all_d = orc.dist_all(ORC_METRIC[metric], q, rows)
+    li, ld = orc.lex_topk(all_d, np.arange(n, dtype=np.uint64), k)
+    assert cnt.value == k
+    assert np.array_equal(oi, ids[li.astype(np.int64)]) and np.array_equal(bits(od), bits(ld))
+
+
+def test_synthetic_rows_helper(ctx, orc):
+    lib = _lib.load()
+    ids = np.array([5, 0, 999_999, 123_456_789], np.uint64)
+    for norm in [0, 1]:
+        out = np.empty((len(ids), 96), np.float32)
+        _lib.check(lib.wvg_synthetic_rows(ctx.handle, 42, _lib.u64ptr(ids), len(ids), 96, 0, norm, _lib.fptr(out)))
+        want = np.stack([orc.synth_rows(42, int(i), 1, 96, 0)[0] for i in ids])
+        if norm:
+            want = orc.normalize_rows(want)
+        assert np.array_equal(bits(out), bits(want))
+
+
 # ---------------------------------------------------------------------------
 # PQ
 def _codebook(orc, m, ks, ds, seed):
@@ -364,6 +401,31 @@ def test_pq_scan_parity(ctx, orc, metric):
     ids2, dists2, _ = c2.search(q, 10)
     ids1, dists1, _ = c.search(q, 10)
     assert np.array_equal(ids1, ids2)
+
+
+def test_pq_encode_corpus(ctx, orc):
+    """Bulk compression of a resident float corpus == per-row Encode."""
+    lib = _lib.load()
+    m, ks, d, n = 32, 256, 128, 3000
+    centers = _codebook(orc, m, ks, d // m, 81)
+    f = Corpus(ctx, KIND_F32, METRIC_L2, d, n)
+    f.fill_synthetic(82, n, 0)
+    f.delete(np.array([5, 6], np.uint64))
+    pq = Corpus(ctx, KIND_PQ, METRIC_L2, d, n)
+    pq.set_codebook(centers)
+    _lib.check(lib.wvg_pq_encode_corpus(pq.handle, f.handle))
+    rows = orc.synth_rows(82, 0, n, d, 0)
+    codes = orc.pq_encode(rows, centers)
+    for i in [0, 1, 63, 64, 2999]:
+        assert np.array_equal(pq.get(i, pq_m=m), codes[i])
+    assert pq.info()[0] == n - 2
+    q = orc.synth_rows(83, 0, 1, d, 0)[0]
+    lut = orc.pq_lut(0, q, centers)
+    all_d = np.array([orc.pq_adc(0, lut, cd) for cd in codes], np.float32)
+    valid = np.ones(n, np.uint8)
+    valid[[5, 6]] = 0
+    ids, dists, counts = pq.search(q, 10)
+    check_topk(orc, ids[0], dists[0], counts[0], all_d, np.arange(n, dtype=np.uint64), 10, valid)
 
 
 def test_pq_invalid_config(ctx):

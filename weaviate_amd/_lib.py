@@ -57,6 +57,10 @@ SIGNATURES = {
                                             c_void_p, c_size_t, c_void_p]),
     "wvg_topk_merge_device": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_uint32, c_uint32, c_uint32,
                                       c_void_p, c_void_p, c_void_p, c_void_p]),
+    "wvg_rescore": (c_int, [c_void_p, c_int, _P(c_float), _P(c_float), _P(c_uint64), c_uint64, c_uint32, c_uint32,
+                            _P(c_uint64), _P(c_float), _P(c_uint32)]),
+    "wvg_pq_encode_corpus": (c_int, [c_void_p, c_void_p]),
+    "wvg_synthetic_rows": (c_int, [c_void_p, c_uint64, _P(c_uint64), c_uint64, c_uint32, c_int, c_int, _P(c_float)]),
     "wvg_profile_start": (c_int, [c_void_p]),
     "wvg_profile_stop": (c_int, [c_void_p, _P(ctypes.c_double), _P(c_uint64)]),
     "wvg_distance_batch": (c_int, [c_void_p, c_int, _P(c_float), _P(c_float), c_uint64, c_uint32, _P(c_float)]),

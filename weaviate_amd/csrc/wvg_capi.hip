@@ -128,6 +128,22 @@ struct SlotGuard {
     }
 };
 
+struct Bulk {
+    SlotGuard g;
+    char *b = nullptr;
+    explicit Bulk(wvg_ctx *ctx) : g(ctx) {}
+    int begin(size_t bytes)
+    {
+        int rc = g.ctx->acquire(&g.slot);
+        if (rc) return rc;
+        void *p = nullptr;
+        rc = g.slot->device_scratch(bytes, &p);
+        b = (char *)p;
+        return rc;
+    }
+    hipStream_t s() const { return g.slot->stream; }
+};
+
 // Allow bitmap -> tile range [tb, te) of slots that can be allowed; false if empty.
 static bool allow_tile_range(const wvg_corpus *c, const uint64_t *allow, uint64_t allow_words, uint64_t &tb,
                              uint64_t &te)
@@ -1038,6 +1054,95 @@ int wvg_topk_merge_device(wvg_ctx *ctx, const float *d_dists, const uint64_t *d_
     return WVG_OK;
 }
 
+int wvg_rescore(wvg_ctx *ctx, int metric, const float *q, const float *rows, const uint64_t *ids, uint64_t n,
+                uint32_t dim, uint32_t k, uint64_t *out_ids, float *out_dists, uint32_t *out_count)
+{
+    if (!ctx || !q || (n && (!rows || !ids))) return fail(WVG_ERR_INVALID, "null argument");
+    if (metric < WVG_METRIC_L2 || metric > WVG_METRIC_COSINE) return fail(WVG_ERR_INVALID, "unknown metric");
+    if (k > MAX_K) return fail(WVG_ERR_UNSUPPORTED, "k above 256 is not supported by the fused top-k");
+    if (n > 0xFFFFFFFFull) return fail(WVG_ERR_INVALID, "too many rows");
+    if (out_count) *out_count = 0;
+    if (n == 0 || k == 0 || dim == 0) return WVG_OK;
+    WVG_HIP(hipSetDevice(ctx->device));
+    const uint32_t nch = f32_chunks(dim);
+    Carver cv;
+    const size_t o_x = cv.take(n * dim * 4), o_t = cv.take(tiles_of(n) * 64 * (size_t)nch * 16),
+                 o_q = cv.take((size_t)nch * 16), o_k = cv.take(n * 8), o_i = cv.take((size_t)k * 8),
+                 o_d = cv.take((size_t)k * 4), o_c = cv.take(4);
+    Bulk bk(ctx);
+    int rc = bk.begin(cv.off);
+    if (rc) return rc;
+    std::vector<float> qp((size_t)nch * 4, 0.0f);
+    std::memcpy(qp.data(), q, (size_t)dim * 4);
+    WVG_HIP(hipMemcpyAsync(bk.b + o_x, rows, n * dim * 4, hipMemcpyHostToDevice, bk.s()));
+    WVG_HIP(hipMemcpyAsync(bk.b + o_q, qp.data(), qp.size() * 4, hipMemcpyHostToDevice, bk.s()));
+    WVG_HIP(launch_f32_store((const float *)(bk.b + o_x), nullptr, n, dim, nch, 0, (float *)(bk.b + o_t), bk.s()));
+    WVG_HIP(launch_dist_keys(metric, (const float *)(bk.b + o_q), (const float *)(bk.b + o_t), n, dim,
+                             (uint64_t *)(bk.b + o_k), bk.s()));
+    WVG_HIP(launch_merge_keys((const uint64_t *)(bk.b + o_k), 1, (uint32_t)n, k, 0, (uint64_t *)(bk.b + o_i),
+                              (float *)(bk.b + o_d), (uint32_t *)(bk.b + o_c), bk.s()));
+    std::vector<uint64_t> idx(k);
+    uint32_t cnt = 0;
+    WVG_HIP(hipMemcpyAsync(idx.data(), bk.b + o_i, (size_t)k * 8, hipMemcpyDeviceToHost, bk.s()));
+    if (out_dists) WVG_HIP(hipMemcpyAsync(out_dists, bk.b + o_d, (size_t)k * 4, hipMemcpyDeviceToHost, bk.s()));
+    WVG_HIP(hipMemcpyAsync(&cnt, bk.b + o_c, 4, hipMemcpyDeviceToHost, bk.s()));
+    WVG_HIP(hipStreamSynchronize(bk.s()));
+    for (uint32_t i = 0; i < k; i++)  // row index -> caller's docID
+        if (out_ids) out_ids[i] = i < cnt ? ids[idx[i]] : WVG_KEY_NONE;
+    if (out_count) *out_count = cnt;
+    return WVG_OK;
+}
+
+int wvg_pq_encode_corpus(wvg_corpus *pq, wvg_corpus *f32)
+{
+    int rc = check_corpus(pq);
+    if (rc) return rc;
+    if (!f32 || pq->kind != WVG_KIND_PQ || f32->kind != WVG_KIND_F32)
+        return fail(WVG_ERR_INVALID, "need a PQ corpus and an F32 corpus");
+    if (!pq->d_centers) return fail(WVG_ERR_INVALID, "PQ corpus has no codebook");
+    if (pq->dim != f32->dim || pq->id_base != f32->id_base) return fail(WVG_ERR_INVALID, "dim / id_base mismatch");
+    std::unique_lock<std::shared_mutex> lk1(pq->rw);
+    std::shared_lock<std::shared_mutex> lk2(f32->rw);
+    const uint64_t hw = f32->high_water;
+    if (hw > pq->capacity) return fail(WVG_ERR_CAPACITY, "PQ corpus capacity below the float corpus");
+    if (hw == 0) return WVG_OK;
+    SlotGuard g(pq->ctx);
+    rc = pq->ctx->acquire(&g.slot);
+    if (rc) return rc;
+    hipStream_t s = g.slot->stream;
+    WVG_HIP(launch_pq_encode((const float *)f32->d_data, tiles_of(hw) * 64, pq->dim, pq->d_centers, pq->pq_m,
+                             pq->pq_ks, (uint8_t *)pq->d_data, s, true));
+    const uint64_t tiles = tiles_of(hw);
+    WVG_HIP(hipMemcpyAsync(pq->d_valid, f32->d_valid, tiles * 8, hipMemcpyDeviceToDevice, s));
+    WVG_HIP(hipStreamSynchronize(s));
+    pq->count = 0;
+    for (uint64_t t = 0; t < tiles; t++) {
+        pq->h_valid[t] = f32->h_valid[t];
+        pq->count += (uint64_t)__builtin_popcountll(pq->h_valid[t]);
+    }
+    pq->high_water = std::max(pq->high_water, hw);
+    return WVG_OK;
+}
+
+int wvg_synthetic_rows(wvg_ctx *ctx, uint64_t seed, const uint64_t *ids, uint64_t n, uint32_t dim, int distribution,
+                       int normalize, float *out)
+{
+    if (!ctx || (n && (!ids || !out))) return fail(WVG_ERR_INVALID, "null argument");
+    if (n == 0 || dim == 0) return WVG_OK;
+    WVG_HIP(hipSetDevice(ctx->device));
+    Carver cv;
+    const size_t o_i = cv.take(n * 8), o_o = cv.take(n * dim * 4);
+    Bulk bk(ctx);
+    int rc = bk.begin(cv.off);
+    if (rc) return rc;
+    WVG_HIP(hipMemcpyAsync(bk.b + o_i, ids, n * 8, hipMemcpyHostToDevice, bk.s()));
+    WVG_HIP(launch_synth_rows(seed, distribution, (const uint64_t *)(bk.b + o_i), n, dim, normalize,
+                              (float *)(bk.b + o_o), bk.s()));
+    WVG_HIP(hipMemcpyAsync(out, bk.b + o_o, n * dim * 4, hipMemcpyDeviceToHost, bk.s()));
+    WVG_HIP(hipStreamSynchronize(bk.s()));
+    return WVG_OK;
+}
+
 // Internal A/B knob (not part of include/wvgpu.h): 0 = K1 scan variant,
 // 1 = K1 resident workgroups per CU.  Returns the previous value.
 int wvgx_set_tuning(int key, int value)
@@ -1085,21 +1190,6 @@ int wvg_profile_stop(wvg_ctx *ctx, double *scan_ms_total, uint64_t *scan_launche
 // ---------------------------------------------------------------------------
 // Bulk primitives
 // ---------------------------------------------------------------------------
-struct Bulk {
-    SlotGuard g;
-    char *b = nullptr;
-    explicit Bulk(wvg_ctx *ctx) : g(ctx) {}
-    int begin(size_t bytes)
-    {
-        int rc = g.ctx->acquire(&g.slot);
-        if (rc) return rc;
-        void *p = nullptr;
-        rc = g.slot->device_scratch(bytes, &p);
-        b = (char *)p;
-        return rc;
-    }
-    hipStream_t s() const { return g.slot->stream; }
-};
 
 int wvg_distance_batch(wvg_ctx *ctx, int metric, const float *q, const float *X, uint64_t n, uint32_t dim, float *out)
 {

@@ -154,6 +154,11 @@ hipError_t launch_normalize_rows(const float *in, uint64_t n, uint32_t dim, floa
                                  hipStream_t s);
 hipError_t launch_distance_rows(int metric, const float *q, const float *rows, uint64_t n,
                                 uint32_t dim, float *out, hipStream_t s);
+// keys[i] = (SingleDist(q, row i), i) over a tiled temporary of n rows.
+hipError_t launch_dist_keys(int metric, const float *q, const float *tiled, uint64_t n, uint32_t dim,
+                            uint64_t *keys, hipStream_t s);
+hipError_t launch_synth_rows(uint64_t seed, int dist, const uint64_t *ids, uint64_t n, uint32_t dim,
+                             int normalize, float *out, hipStream_t s);
 hipError_t launch_rescore_keys(int metric, const float *q, uint32_t qpitch, const float *tiled,
                                uint32_t dim, uint32_t nchunks, const uint64_t *cand_keys,
                                uint32_t nq, uint32_t ncand, uint32_t cand_stride,
@@ -172,8 +177,9 @@ hipError_t launch_bq_distance_rows(const uint64_t *q, const uint64_t *codes, uin
 hipError_t launch_pq_lut(int metric, const float *q, uint32_t nq, uint32_t qpitch,
                          const float *centers, uint32_t m, uint32_t ks, uint32_t ds, float *lut,
                          hipStream_t s);
-hipError_t launch_pq_encode(const float *rows, uint64_t n, uint32_t dim, const float *centers,
-                            uint32_t m, uint32_t ks, uint8_t *codes, hipStream_t s);
+// codes: row-major [n][m] bytes, or (tiled_out) the PQ corpus layout at slots 0..n-1.
+hipError_t launch_pq_encode(const float *tiled_rows, uint64_t n, uint32_t dim, const float *centers,
+                            uint32_t m, uint32_t ks, uint8_t *codes, hipStream_t s, bool tiled_out = false);
 hipError_t launch_pq_store(const uint8_t *codes, const uint64_t *slots, uint64_t n, uint32_t m,
                            uint32_t nchunks, uint8_t *tiled, hipStream_t s);
 hipError_t launch_pq_adc_rows(int metric, const float *lut, uint32_t m, uint32_t ks,

@@ -99,9 +99,11 @@ __device__ __forceinline__ float l2_256_acc(XA x, CA c, int n)
     return avx256_reduce(acc, sum);
 }
 
-// Encode from the tiled float layout; lane = row.  codes: [n][m] row-major.
-// (diff = point - centroid; l2_256(filteredPoint, c) at CH/kmeans.go:120.)
-template <int DS>
+// Encode from the tiled float layout; lane = row.  Output either row-major
+// codes [n][m] or, TILED_OUT, the PQ corpus layout (16 codes per 16-byte
+// chunk, stored once per chunk).  (diff = point - centroid; l2_256(filteredPoint, c)
+// at CH/kmeans.go:120.)
+template <int DS, bool TILED_OUT>
 __global__ void pq_encode_kernel(const float4 *tiled, uint64_t n, uint32_t dim, uint32_t nchunks, const float *centers,
                                  uint32_t m, uint32_t ks, uint32_t ds_rt, uint8_t *codes)
 {
@@ -109,54 +111,71 @@ __global__ void pq_encode_kernel(const float4 *tiled, uint64_t n, uint32_t dim, 
     if (r >= n) return;
     const uint32_t ds = DS > 0 ? (uint32_t)DS : ds_rt;
     const float4 *rp = tiled + ((r >> 6) * nchunks) * 64 + (r & 63);
-    for (uint32_t s = 0; s < m; s++) {
-        const float *cs = centers + (size_t)s * ks * ds;
-        uint32_t best = 0;
-        float minD = 3.40282346638528859812e+38f;  // math.MaxFloat32
-        if constexpr (DS == 4) {
-            // segment s is exactly chunk s (dim = 4m): one 16-byte load, scalar unfused path (n < 8)
-            const float4 x = rp[(size_t)s * 64];
-            for (uint32_t c = 0; c < ks; c++) {
-                const float4 cc = *reinterpret_cast<const float4 *>(cs + (size_t)c * 4);
-                float sum = 0.0f;
-                scalar_update<WVG_M_L2>(sum, cc.x, x.x);
-                scalar_update<WVG_M_L2>(sum, cc.y, x.y);
-                scalar_update<WVG_M_L2>(sum, cc.z, x.z);
-                scalar_update<WVG_M_L2>(sum, cc.w, x.w);
-                if (!(minD < sum)) {
-                    minD = sum;
-                    best = c;
+    const uint32_t out_chunks = pq_chunks(m);
+    for (uint32_t oc = 0; oc < out_chunks; oc++) {
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        for (uint32_t bsel = 0; bsel < 16; bsel++) {
+            const uint32_t s = oc * 16 + bsel;
+            if (s >= m) break;
+            const float *cs = centers + (size_t)s * ks * ds;
+            uint32_t best = 0;
+            float minD = 3.40282346638528859812e+38f;  // math.MaxFloat32
+            if constexpr (DS == 4) {
+                // segment s is exactly chunk s (dim = 4m): one 16-byte load, scalar unfused path (n < 8)
+                const float4 x = rp[(size_t)s * 64];
+                for (uint32_t c = 0; c < ks; c++) {
+                    const float4 cc = *reinterpret_cast<const float4 *>(cs + (size_t)c * 4);
+                    float sum = 0.0f;
+                    scalar_update<WVG_M_L2>(sum, cc.x, x.x);
+                    scalar_update<WVG_M_L2>(sum, cc.y, x.y);
+                    scalar_update<WVG_M_L2>(sum, cc.z, x.z);
+                    scalar_update<WVG_M_L2>(sum, cc.w, x.w);
+                    if (!(minD < sum)) {
+                        minD = sum;
+                        best = c;
+                    }
+                }
+            } else {
+                const uint32_t base = s * ds;
+                auto xa = [&](int i) { return elem_at<64>(rp, (int)(base + i)); };
+                for (uint32_t c = 0; c < ks; c++) {
+                    const float *cv = cs + (size_t)c * ds;
+                    auto ca = [&](int i) { return cv[i]; };
+                    const float d = l2_256_acc(xa, ca, (int)ds);
+                    if (!(minD < d)) {
+                        minD = d;
+                        best = c;
+                    }
                 }
             }
-        } else {
-            const uint32_t base = s * ds;
-            auto xa = [&](int i) { return elem_at<64>(rp, (int)(base + i)); };
-            for (uint32_t c = 0; c < ks; c++) {
-                const float *cv = cs + (size_t)c * ds;
-                auto ca = [&](int i) { return cv[i]; };
-                const float d = l2_256_acc(xa, ca, (int)ds);
-                if (!(minD < d)) {
-                    minD = d;
-                    best = c;
-                }
-            }
+            if constexpr (TILED_OUT)
+                w[bsel >> 2] |= best << (8 * (bsel & 3));
+            else
+                codes[r * m + s] = (uint8_t)best;
         }
-        codes[r * m + s] = (uint8_t)best;
+        if constexpr (TILED_OUT)
+            reinterpret_cast<uint4 *>(codes)[((r >> 6) * out_chunks + oc) * 64 + (r & 63)] = make_uint4(w[0], w[1], w[2], w[3]);
     }
 }
 
 hipError_t launch_pq_encode(const float *tiled, uint64_t n, uint32_t dim, const float *centers, uint32_t m,
-                            uint32_t ks, uint8_t *codes, hipStream_t s)
+                            uint32_t ks, uint8_t *codes, hipStream_t s, bool tiled_out)
 {
     if (n == 0) return hipSuccess;
     const uint32_t ds = dim / m, nchunks = f32_chunks(dim);
     dim3 grid((unsigned)((n + 255) / 256)), block(256);
-    if (ds == 4 && dim == 4 * m)
-        hipLaunchKernelGGL((pq_encode_kernel<4>), grid, block, 0, s, reinterpret_cast<const float4 *>(tiled), n, dim,
-                           nchunks, centers, m, ks, ds, codes);
-    else
-        hipLaunchKernelGGL((pq_encode_kernel<0>), grid, block, 0, s, reinterpret_cast<const float4 *>(tiled), n, dim,
-                           nchunks, centers, m, ks, ds, codes);
+    const float4 *t4 = reinterpret_cast<const float4 *>(tiled);
+    if (ds == 4 && dim == 4 * m) {
+        if (tiled_out)
+            hipLaunchKernelGGL((pq_encode_kernel<4, true>), grid, block, 0, s, t4, n, dim, nchunks, centers, m, ks, ds, codes);
+        else
+            hipLaunchKernelGGL((pq_encode_kernel<4, false>), grid, block, 0, s, t4, n, dim, nchunks, centers, m, ks, ds, codes);
+    } else {
+        if (tiled_out)
+            hipLaunchKernelGGL((pq_encode_kernel<0, true>), grid, block, 0, s, t4, n, dim, nchunks, centers, m, ks, ds, codes);
+        else
+            hipLaunchKernelGGL((pq_encode_kernel<0, false>), grid, block, 0, s, t4, n, dim, nchunks, centers, m, ks, ds, codes);
+    }
     return hipGetLastError();
 }
 

@@ -578,6 +578,66 @@ hipError_t launch_distance_rows(int metric, const float *q, const float *tiled, 
     return hipGetLastError();
 }
 
+template <int METRIC>
+__global__ void dist_keys_kernel(int metric, const float4 *q4, const float4 *tiled, uint64_t n, uint32_t dim,
+                                 uint32_t nchunks, uint64_t *keys)
+{
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const float4 *rp = tiled + ((r >> 6) * nchunks) * 64 + (r & 63);
+    keys[r] = wvg_make_key(wrap_metric(metric, row_dot_or_l2_generic<METRIC, 64>(rp, q4, (int)dim)), (uint32_t)r);
+}
+
+hipError_t launch_dist_keys(int metric, const float *q, const float *tiled, uint64_t n, uint32_t dim, uint64_t *keys,
+                            hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    const uint32_t nchunks = f32_chunks(dim);
+    dim3 grid((unsigned)((n + 255) / 256)), block(256);
+    if (metric == WVG_M_L2)
+        hipLaunchKernelGGL((dist_keys_kernel<WVG_M_L2>), grid, block, 0, s, metric, reinterpret_cast<const float4 *>(q),
+                           reinterpret_cast<const float4 *>(tiled), n, dim, nchunks, keys);
+    else
+        hipLaunchKernelGGL((dist_keys_kernel<WVG_M_DOT>), grid, block, 0, s, metric, reinterpret_cast<const float4 *>(q),
+                           reinterpret_cast<const float4 *>(tiled), n, dim, nchunks, keys);
+    return hipGetLastError();
+}
+
+// Synthetic rows for arbitrary ids, row-major (bench / test helper).
+__global__ void synth_rows_kernel(uint64_t seed_mixed, int dist, const uint64_t *ids, uint64_t n, uint32_t dim,
+                                  int normalize, float *out)
+{
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const uint64_t row = ids[r];
+    float norm = 1.0f;
+    bool zero = false;
+    if (normalize) {
+        float acc = 0.0f;
+        for (uint32_t i = 0; i < dim; i++) {
+            float v = wvg_synth_value(seed_mixed, row, i, dist);
+            float p = v * v;
+            acc = acc + p;
+        }
+        zero = acc == 0.0f;
+        norm = (float)__builtin_sqrt((double)acc);
+    }
+    for (uint32_t i = 0; i < dim; i++) {
+        float x = wvg_synth_value(seed_mixed, row, i, dist);
+        if (normalize) x = zero ? 0.0f : x / norm;
+        out[r * dim + i] = x;
+    }
+}
+
+hipError_t launch_synth_rows(uint64_t seed, int dist, const uint64_t *ids, uint64_t n, uint32_t dim, int normalize,
+                             float *out, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(synth_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, wvg_mix64(seed), dist,
+                       ids, n, dim, normalize, out);
+    return hipGetLastError();
+}
+
 // Exact rescore of candidate keys (slot in the low 32 bits) against the tiled
 // float rows: the rescore loop of flat.searchByVectorBQ (V/flat/index.go:375-385).
 template <int METRIC>
