@@ -28,6 +28,11 @@ _ensure_built()
 
 @pytest.fixture(scope="session")
 def ctx():
+    import torch
+
+    # torch ships its own HIP runtime under the same soname: initialise it first
+    # so the process holds ONE runtime that both torch and libwvgpu.so use.
+    torch.cuda.init()
     from weaviate_amd.device import Context
 
     c = Context(0)  # raises on a box without a GPU: GPU tests never silently skip

@@ -491,32 +491,47 @@ def test_search_device_matches_host_api(ctx, orc):
             assert np.array_equal(oc.cpu().numpy(), hc.astype(np.int32))
 
 
-def test_search_device_pipelined_matches_host_api(ctx, orc):
-    """nq single-query scans in one call, merges folded into the next scan launch."""
+@pytest.mark.parametrize("mode", [0, 1])
+def test_search_device_pipelined_matches_host_api(ctx, orc, mode):
+    """nq single-query scans in one call: mode 0 = one launch per query with the
+    merge folded into the next launch; mode 1 = one query-stream launch."""
+    import ctypes
+
     import torch
 
     n, d = 30000 + 7, 128
     lib = _lib.load()
+    lib.wvgx_set_tuning.restype = ctypes.c_int
+    lib.wvgx_set_tuning.argtypes = [ctypes.c_int, ctypes.c_int]
+    old = lib.wvgx_set_tuning(2, mode)
     dev = torch.device("cuda:0")
-    for metric in [METRIC_L2, METRIC_DOT]:
-        c = Corpus(ctx, KIND_F32, metric, d, n)
-        c.fill_synthetic(5, n, 0)
-        c.delete(np.array([0, 1, 77, 30000], np.uint64))
-        for nq, k in [(1, 10), (2, 10), (5, 100), (16, 10), (3, 256)]:
-            qs = orc.synth_rows(9 + nq, 0, nq, d, 0)
-            hid, hd, hc = c.search(qs, k)  # host API (nq concurrent scans in one launch)
-            ws = torch.zeros(lib.wvg_search_workspace_size(c.handle, nq, k), dtype=torch.uint8, device=dev)
-            tq = torch.from_numpy(qs).to(dev)
-            oi = torch.empty((nq, k), dtype=torch.int64, device=dev)
-            od = torch.empty((nq, k), dtype=torch.float32, device=dev)
-            oc = torch.empty(nq, dtype=torch.int32, device=dev)
-            _lib.check(lib.wvg_search_device_pipelined(c.handle, tq.data_ptr(), nq, k, oi.data_ptr(), od.data_ptr(),
-                                                       oc.data_ptr(), ws.data_ptr(), ws.numel(),
-                                                       torch.cuda.current_stream().cuda_stream))
-            torch.cuda.synchronize()
-            assert np.array_equal(oi.cpu().numpy().view(np.uint64), hid)
-            assert np.array_equal(bits(od.cpu().numpy()), bits(hd))
-            assert np.array_equal(oc.cpu().numpy(), hc.astype(np.int32))
+    try:
+        for metric in [METRIC_L2, METRIC_DOT]:
+            c = Corpus(ctx, KIND_F32, metric, d, n)
+            c.fill_synthetic(5, n, 0)
+            c.delete(np.array([0, 1, 77, 30000], np.uint64))
+            for nq, k in [(1, 10), (2, 10), (5, 100), (16, 10), (3, 256)]:
+                ws = torch.zeros(lib.wvg_search_workspace_size(c.handle, nq, k), dtype=torch.uint8, device=dev)
+                outs = []
+                for rep in range(2):  # two calls back to back on one workspace, no sync between them
+                    qs = orc.synth_rows(9 + nq + 100 * rep, 0, nq, d, 0)
+                    tq = torch.from_numpy(qs).to(dev)
+                    oi = torch.empty((nq, k), dtype=torch.int64, device=dev)
+                    od = torch.empty((nq, k), dtype=torch.float32, device=dev)
+                    oc = torch.empty(nq, dtype=torch.int32, device=dev)
+                    _lib.check(lib.wvg_search_device_pipelined(c.handle, tq.data_ptr(), nq, k, oi.data_ptr(),
+                                                               od.data_ptr(), oc.data_ptr(), ws.data_ptr(),
+                                                               ws.numel(), torch.cuda.current_stream().cuda_stream))
+                    outs.append((qs, tq, oi, od, oc))
+                torch.cuda.synchronize()
+                for qs, _, oi, od, oc in outs:
+                    hid, hd, hc = c.search(qs, k)  # host API (nq concurrent scans in one launch)
+                    assert np.array_equal(oi.cpu().numpy().view(np.uint64), hid)
+                    assert np.array_equal(bits(od.cpu().numpy()), bits(hd))
+                    assert np.array_equal(oc.cpu().numpy(), hc.astype(np.int32))
+            c.destroy()
+    finally:
+        lib.wvgx_set_tuning(2, old)
 
 
 # ---------------------------------------------------------------------------

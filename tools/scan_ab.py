@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--gpcu", default="2,3,4,6")
     ap.add_argument("--metric", type=int, default=0)
     ap.add_argument("--pipelined", action="store_true")
+    ap.add_argument("--modes", default="1", help="pipelined: 0 = launch per query, 1 = query-stream launch")
     args = ap.parse_args()
     import torch
 
@@ -48,12 +49,14 @@ def main():
     cnt = torch.empty(Q, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream().cuda_stream
     ref_ids = None
+    ref_d = None
     results = {}
     for rnd in range(args.rounds):
         for v in [int(x) for x in args.variants.split(",")]:
-            for g in [int(x) for x in args.gpcu.split(",")]:
+            for g, mode in [(int(x), int(y)) for x in args.gpcu.split(",") for y in args.modes.split(",")]:
                 lib.wvgx_set_tuning(0, v)
                 lib.wvgx_set_tuning(1, g)
+                lib.wvgx_set_tuning(2, mode)
                 wsb = lib.wvg_search_workspace_size(c.handle, 1, k)
                 ws = torch.zeros(wsb, dtype=torch.uint8, device=dev)
 
@@ -83,15 +86,18 @@ def main():
                 got = ids.cpu().numpy()
                 if ref_ids is None:
                     ref_ids = got.copy()
+                    ref_d = dists.cpu().numpy().copy()
                 ok = bool(np.array_equal(got, ref_ids))
                 scan_us = ms.value * 1e3 / nl.value
-                rec = {"round": rnd, "variant": v, "groups_per_cu": g, "scan_us": round(scan_us, 2),
+                rec = {"round": rnd, "variant": v, "groups_per_cu": g, "mode": mode, "scan_us": round(scan_us, 2),
                        "GBps": round(n * d * 4 / (scan_us * 1e-6) / 1e9, 1),
-                       "wall_us_per_query": round((t1 - t0) / Q * 1e6, 2), "ids_equal": ok}
+                       "wall_us_per_query": round((t1 - t0) / Q * 1e6, 2),
+                       "qps": round(Q / (t1 - t0), 1), "ids_equal": ok,
+                       "dists_equal": bool(np.array_equal(dists.cpu().numpy(), ref_d)) if ref_d is not None else True}
                 print(json.dumps(rec), flush=True)
-                results.setdefault((v, g), []).append(scan_us)
+                results.setdefault((v, g, mode), []).append(scan_us)
     best = min(results.items(), key=lambda kv: np.median(kv[1]))
-    print(json.dumps({"best": {"variant": best[0][0], "groups_per_cu": best[0][1],
+    print(json.dumps({"best": {"variant": best[0][0], "groups_per_cu": best[0][1], "mode": best[0][2],
                                "median_scan_us": round(float(np.median(best[1])), 2)}}))
 
 

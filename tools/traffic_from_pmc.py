@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""HBM bytes per launch from a rocprofv3 `--pmc FETCH_SIZE` pass (tooling only).
+
+FETCH_SIZE is reported in KiB; on gfx950 it counts half the bytes of a wide
+(16 B/lane) streaming read, so it is doubled (MI355X_MICROARCH.md, HBM
+section).  Writes/updates one entry of profiles/traffic.json.
+
+Usage: python tools/traffic_from_pmc.py <counter_collection.csv> <kernel-substring> <entry>
+           --queries-per-launch B --rows N --dim D [--out profiles/traffic.json]
+"""
+import argparse
+import csv
+import json
+import os
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("csv")
+    ap.add_argument("kernel")
+    ap.add_argument("entry")
+    ap.add_argument("--queries-per-launch", type=int, required=True)
+    ap.add_argument("--rows", type=int, required=True)
+    ap.add_argument("--dim", type=int, required=True)
+    ap.add_argument("--bytes-per-row", type=int, default=0, help="algorithmic bytes per row (default dim*4)")
+    ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                  "profiles", "traffic.json"))
+    ap.add_argument("--note", default="")
+    a = ap.parse_args()
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(a.csv))
+            if a.kernel in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE"]
+    if not vals:
+        raise SystemExit(f"no FETCH_SIZE rows for kernel matching {a.kernel!r}")
+    per_launch = sum(vals) / len(vals) * 1024 * 2
+    bpr = a.bytes_per_row or a.dim * 4
+    algo = a.rows * bpr
+    rec = {
+        "kernel_match": a.kernel,
+        "rows": a.rows,
+        "dim": a.dim,
+        "queries_per_launch": a.queries_per_launch,
+        "launches": len(vals),
+        "hbm_bytes_per_launch": int(round(per_launch)),
+        "hbm_bytes_per_query_scan": round(per_launch / a.queries_per_launch, 1),
+        "algorithmic_bytes_per_query_scan": algo,
+        "ratio_to_algorithmic": round(per_launch / a.queries_per_launch / algo, 4),
+        "method": "rocprofv3 --pmc FETCH_SIZE --kernel-trace, separate pass; FETCH_SIZE KiB x 1024 x 2 "
+                  "(gfx950 half-count of 16 B/lane streaming reads); mean over launches",
+    }
+    if a.note:
+        rec["note"] = a.note
+    db = json.load(open(a.out)) if os.path.exists(a.out) else {}
+    db[a.entry] = rec
+    json.dump(db, open(a.out, "w"), indent=1)
+    print(json.dumps({a.entry: rec}))
+
+
+if __name__ == "__main__":
+    main()

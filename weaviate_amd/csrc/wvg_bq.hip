@@ -70,10 +70,10 @@ static hipError_t launch_bq_e(const ScanArgs &a, uint64_t *partials, int groups,
 {
     dim3 grid(groups, a.nq), block(BQ_WAVES * 64);
     switch (a.nchunks) {
-    case 1: hipLaunchKernelGGL((scan_bq_kernel<E, 1>), grid, block, 0, s, a, partials); break;   // d <= 128
-    case 6: hipLaunchKernelGGL((scan_bq_kernel<E, 6>), grid, block, 0, s, a, partials); break;   // d = 768
-    case 12: hipLaunchKernelGGL((scan_bq_kernel<E, 12>), grid, block, 0, s, a, partials); break; // d = 1536
-    default: hipLaunchKernelGGL((scan_bq_kernel<E, 0>), grid, block, 0, s, a, partials); break;
+    case 1: launch_timed((scan_bq_kernel<E, 1>), grid, block, 0, s, a, partials); break;   // d <= 128
+    case 6: launch_timed((scan_bq_kernel<E, 6>), grid, block, 0, s, a, partials); break;   // d = 768
+    case 12: launch_timed((scan_bq_kernel<E, 12>), grid, block, 0, s, a, partials); break; // d = 1536
+    default: launch_timed((scan_bq_kernel<E, 0>), grid, block, 0, s, a, partials); break;
     }
     return hipGetLastError();
 }

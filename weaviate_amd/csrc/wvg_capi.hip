@@ -728,6 +728,32 @@ static int prof_pair(wvg_ctx *ctx, std::pair<hipEvent_t, hipEvent_t> *out)
     return WVG_OK;
 }
 
+// Arms a profiling event pair for the next scan dispatch on this thread
+// (launch_timed binds it to the dispatch); a pair the launch path did not
+// consume is handed back on scope exit.
+struct ProfArm {
+    wvg_ctx *ctx = nullptr;
+    int rc = WVG_OK;
+    explicit ProfArm(wvg_ctx *c)
+    {
+        if (!c->profiling.load(std::memory_order_relaxed)) return;
+        std::pair<hipEvent_t, hipEvent_t> ev;
+        rc = prof_pair(c, &ev);
+        if (rc) return;
+        ctx = c;
+        armed_events() = LaunchEvents{ev.first, ev.second};
+    }
+    ~ProfArm()
+    {
+        if (!ctx) return;
+        if (armed_events().start) {
+            armed_events() = LaunchEvents{};
+            std::lock_guard<std::mutex> g(ctx->prof_mu);
+            if (ctx->prof_used) ctx->prof_used--;
+        }
+    }
+};
+
 // Runs phase 1 + phase 2 for one corpus with device-resident prepared queries.
 static int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t nq, uint32_t k, const uint64_t *d_allow,
                       uint64_t allow_words, uint64_t tb, uint64_t te, uint64_t *partials, int groups, bool gemm,
@@ -750,17 +776,12 @@ static int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t 
     a.k = k;
     a.pq_m = c->pq_m;
     a.pq_ks = c->pq_ks;
-    std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
-    if (c->ctx->profiling.load(std::memory_order_relaxed)) {
-        int rc = prof_pair(c->ctx, &ev);
-        if (rc) return rc;
-        WVG_HIP(hipEventRecord(ev.first, s));
-    }
+    ProfArm arm(c->ctx);
+    if (arm.rc) return arm.rc;
     if (gemm)
         WVG_HIP(launch_gemm_topk(a, (uint32_t)groups, partials, s));
     else
         WVG_HIP(launch_scan(a, c->kind, partials, groups, s));
-    if (ev.second) WVG_HIP(hipEventRecord(ev.second, s));
     WVG_HIP(launch_merge_lists(partials, nq, (uint32_t)groups, k, k, c->id_base, ids, dists, counts, s));
     return WVG_OK;
 }
@@ -967,13 +988,29 @@ int wvg_search_bq_rescore(wvg_corpus *bq, wvg_corpus *f32, const float *queries,
     return WVG_OK;
 }
 
+// Workspace of the query-stream scan: partial lists [nq][groups][k], then the
+// per-query arrival counters and the status word.
+struct StreamLayout {
+    size_t partials = 0, arrivals = 0, total = 0;
+};
+static StreamLayout stream_layout(const SearchPlan &p1, uint32_t nq, uint32_t k)
+{
+    StreamLayout l;
+    l.partials = 0;
+    l.arrivals = align_up((size_t)nq * p1.groups * k * 8, 256);
+    l.total = l.arrivals + align_up(((size_t)nq + 1) * 4, 256);  // memset block: 16-B multiple
+    return l;
+}
+
 size_t wvg_search_workspace_size(wvg_corpus *c, uint32_t nq, uint32_t k)
 {
     if (!c) return 0;
     const uint32_t kk = std::max<uint32_t>(k, 1);
     SearchPlan p = plan_search(c, nq, k, nullptr, 0);
-    SearchPlan p1 = plan_search(c, 1, k, nullptr, 0);  // pipelined mode: two single-query buffers
-    return std::max(align_up(p.workspace_bytes(nq, kk), 256), 2 * align_up(p1.workspace_bytes(1, kk), 256));
+    SearchPlan p1 = plan_search(c, 1, k, nullptr, 0);  // pipelined: two single-query buffers, or the stream layout
+    const size_t chain = 2 * align_up(p1.workspace_bytes(1, kk), 256);
+    const size_t stream = stream_layout(p1, nq, kk).total;
+    return std::max({align_up(p.workspace_bytes(nq, kk), 256), chain, stream});
 }
 
 int wvg_search_device_pipelined(wvg_corpus *c, const float *d_queries, uint32_t nq, uint32_t k, uint64_t *d_ids,
@@ -989,6 +1026,37 @@ int wvg_search_device_pipelined(wvg_corpus *c, const float *d_queries, uint32_t 
     std::shared_lock<std::shared_mutex> lk(c->rw);
     SearchPlan p = plan_search(c, 1, k, nullptr, 0);
     if (p.empty) return WVG_OK;
+    if (tuning().pipeline_mode == 1) {  // query-stream kernel: one launch for all nq queries
+        const StreamLayout l = stream_layout(p, nq, k);
+        if (!d_workspace || workspace_bytes < l.total) return fail(WVG_ERR_INVALID, "workspace too small");
+        char *w = (char *)d_workspace;
+        StreamJob j{};
+        j.partials = (uint64_t *)(w + l.partials);
+        j.arrivals = (uint32_t *)(w + l.arrivals);
+        j.status = j.arrivals + nq;
+        j.groups = (uint32_t)p.groups;
+        j.ids = d_ids;
+        j.dists = d_dists;
+        j.counts = d_counts;
+        ScanArgs a{};
+        a.data = c->d_data;
+        a.valid = c->d_valid;
+        a.id_base = c->id_base;
+        a.tile_begin = p.tb;
+        a.tile_end = p.te;
+        a.dim = c->dim;
+        a.nchunks = c->nchunks;
+        a.metric = c->metric;
+        a.queries = d_queries;
+        a.qpitch = c->dim;
+        a.nq = nq;
+        a.k = k;
+        WVG_HIP(hipMemsetAsync(j.arrivals, 0, align_up(((size_t)nq + 1) * 4, 16), s));
+        ProfArm arm(c->ctx);
+        if (arm.rc) return arm.rc;
+        WVG_HIP(launch_scan_f32_stream(a, j, s));
+        return WVG_OK;
+    }
     const size_t half = align_up(p.workspace_bytes(1, k), 256);
     if (!d_workspace || workspace_bytes < 2 * half) return fail(WVG_ERR_INVALID, "workspace too small");
     uint64_t *buf[2] = {(uint64_t *)d_workspace, (uint64_t *)((char *)d_workspace + half)};
@@ -1011,14 +1079,9 @@ int wvg_search_device_pipelined(wvg_corpus *c, const float *d_queries, uint32_t 
             a.side = MergeJob{buf[(i - 1) & 1], (uint32_t)p.groups, k, k, c->id_base, d_ids + (size_t)(i - 1) * k,
                               d_dists + (size_t)(i - 1) * k, d_counts ? d_counts + (i - 1) : nullptr, 1};
         }
-        std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
-        if (c->ctx->profiling.load(std::memory_order_relaxed)) {
-            int rc = prof_pair(c->ctx, &ev);
-            if (rc) return rc;
-            WVG_HIP(hipEventRecord(ev.first, s));
-        }
+        ProfArm arm(c->ctx);
+        if (arm.rc) return arm.rc;
         WVG_HIP(launch_scan_f32(a, buf[i & 1], p.groups, s));
-        if (ev.second) WVG_HIP(hipEventRecord(ev.second, s));
     }
     const uint32_t last = nq - 1;
     WVG_HIP(launch_merge_lists(buf[last & 1], 1, (uint32_t)p.groups, k, k, c->id_base, d_ids + (size_t)last * k,
@@ -1155,6 +1218,9 @@ int wvgx_set_tuning(int key, int value)
     } else if (key == 1) {
         old = t.groups_per_cu;
         t.groups_per_cu = value;
+    } else if (key == 2) {
+        old = t.pipeline_mode;
+        t.pipeline_mode = value;
     }
     return old;
 }

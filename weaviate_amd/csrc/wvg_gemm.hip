@@ -216,11 +216,11 @@ hipError_t launch_gemm_topk(const ScanArgs &s, uint32_t nrr, uint64_t *partials,
     const size_t lds = (size_t)2 * (GQ + GR) * GSTRIDE * 4 + (size_t)GQ * GR * 8;
     dim3 grid(a.nqb * a.nrr), block(GWAVES * 64);
     if (s.k <= 64)
-        hipLaunchKernelGGL((gemm_topk_kernel<1>), grid, block, lds, st, a, partials);
+        launch_timed((gemm_topk_kernel<1>), grid, block, lds, st, a, partials);
     else if (s.k <= 128)
-        hipLaunchKernelGGL((gemm_topk_kernel<2>), grid, block, lds, st, a, partials);
+        launch_timed((gemm_topk_kernel<2>), grid, block, lds, st, a, partials);
     else
-        hipLaunchKernelGGL((gemm_topk_kernel<4>), grid, block, lds, st, a, partials);
+        launch_timed((gemm_topk_kernel<4>), grid, block, lds, st, a, partials);
     return hipGetLastError();
 }
 

@@ -2,6 +2,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <atomic>
 #include <mutex>
@@ -117,6 +118,21 @@ struct ScanArgs {
 // Phase 1 writes dense partials [nq][groups][K] (keys, KEY_NONE = empty).
 int scan_groups_for(const ScanArgs &a, int num_cus);
 hipError_t launch_scan_f32(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s);
+// Query-stream K1 (wvg_search_device_pipelined): ONE launch scans a.nq queries
+// back to back, every query a full scan of the corpus.  `groups` scan
+// workgroups loop over the queries, publishing each query's partial list with
+// a release + arrival count; one more workgroup waits for each query's
+// `groups` arrivals and merges it while the scan proceeds to the next query.
+struct StreamJob {
+    uint64_t *partials;  // [nq][groups][k]
+    uint32_t *arrivals;  // [nq], zero at launch
+    uint32_t *status;    // bit 0 set if the merge workgroup gave up waiting
+    uint32_t groups;
+    uint64_t *ids;
+    float *dists;
+    uint32_t *counts;
+};
+hipError_t launch_scan_f32_stream(const ScanArgs &a, const StreamJob &j, hipStream_t s);
 hipError_t launch_scan_bq(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s);
 hipError_t launch_scan_pq(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s);
 // K3 batched MFMA scoring (wvg_gemm.hip): partials [nq][nrr][K].
@@ -127,8 +143,29 @@ hipError_t launch_gemm_topk(const ScanArgs &a, uint32_t nrr, uint64_t *partials,
 struct Tuning {
     int scan_variant = 0;    // K1 variant (see wvg_scan.hip)
     int groups_per_cu = 1;   // K1 workgroups per CU (A/B: 1 = fewest partial lists, same scan rate)
+    int pipeline_mode = 1;   // wvg_search_device_pipelined: 0 = one launch per query (merge folded into the
+                             // next launch), 1 = one query-stream launch
 };
 Tuning &tuning();
+// Profiling: events armed by the host runtime (wvg_profile_start) are bound to
+// the next scan-kernel dispatch itself (hipExtLaunchKernel), so timing adds no
+// marker packets -- a hipEventRecord pair around each launch cost ~5 us of idle
+// GPU per record between back-to-back scans.
+struct LaunchEvents {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+LaunchEvents &armed_events();  // thread-local
+template <typename... KArgs, typename... Args>
+inline void launch_timed(void (*kernel)(KArgs...), dim3 grid, dim3 block, uint32_t lds, hipStream_t s, Args... args)
+{
+    LaunchEvents &e = armed_events();
+    if (e.start) {
+        hipExtLaunchKernelGGL(kernel, grid, block, lds, s, e.start, e.stop, 0u, args...);
+        e = LaunchEvents{};
+    } else {
+        hipLaunchKernelGGL(kernel, grid, block, lds, s, args...);
+    }
+}
 // Phase 2: per query `nlists` ascending lists of `list_len` keys -> final
 // (ids = id_base + slot, dists, counts).
 hipError_t launch_merge_lists(const uint64_t *partials, uint32_t nq, uint32_t nlists, uint32_t list_len, uint32_t k,

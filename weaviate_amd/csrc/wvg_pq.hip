@@ -274,11 +274,11 @@ static hipError_t launch_pq_e(const ScanArgs &a, uint64_t *partials, int groups,
     dim3 grid(groups, a.nq), block(PQ_WAVES * 64);
     const size_t lds = (size_t)a.pq_m * a.pq_ks * 4;
     switch (a.pq_m) {
-    case 8: hipLaunchKernelGGL((scan_pq_kernel<E, 8>), grid, block, lds, s, a, partials); break;
-    case 16: hipLaunchKernelGGL((scan_pq_kernel<E, 16>), grid, block, lds, s, a, partials); break;
-    case 32: hipLaunchKernelGGL((scan_pq_kernel<E, 32>), grid, block, lds, s, a, partials); break;
-    case 64: hipLaunchKernelGGL((scan_pq_kernel<E, 64>), grid, block, lds, s, a, partials); break;
-    default: hipLaunchKernelGGL((scan_pq_kernel<E, 0>), grid, block, lds, s, a, partials); break;
+    case 8: launch_timed((scan_pq_kernel<E, 8>), grid, block, lds, s, a, partials); break;
+    case 16: launch_timed((scan_pq_kernel<E, 16>), grid, block, lds, s, a, partials); break;
+    case 32: launch_timed((scan_pq_kernel<E, 32>), grid, block, lds, s, a, partials); break;
+    case 64: launch_timed((scan_pq_kernel<E, 64>), grid, block, lds, s, a, partials); break;
+    default: launch_timed((scan_pq_kernel<E, 0>), grid, block, lds, s, a, partials); break;
     }
     return hipGetLastError();
 }

@@ -25,6 +25,12 @@ Tuning &tuning()
     return t;
 }
 
+LaunchEvents &armed_events()
+{
+    static thread_local LaunchEvents e;
+    return e;
+}
+
 // Wave index as a wave-uniform (SGPR) value, so per-wave loops, the tile mask
 // loads and the skip branch are scalar.
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
@@ -106,25 +112,14 @@ __device__ __forceinline__ uint64_t lane_key(uint64_t m, float dist, uint64_t t,
     return ((m >> lane) & 1ull) ? wvg_make_key(dist, (uint32_t)(t * 64 + lane)) : WVG_KEY_NONE;
 }
 
-// Variant 0 (and 2 = plain loads): one tile's loads in flight per wave; tiles
-// with no live/allowed row are skipped without touching their rows.
+// One wave's tiles [t0, t1) for one query: one tile's loads in flight per
+// wave; tiles with no live/allowed row are skipped without touching their rows.
 template <int METRIC, int D, int E>
-__global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_kernel(ScanArgs a, uint64_t *partials)
+__device__ __forceinline__ void scan_tiles(const ScanArgs &a, const float4 *q4, uint64_t t0, uint64_t t1,
+                                           WaveTopK<E> &tk)
 {
-    if (a.side.active && blockIdx.x == gridDim.x - 1) {  // the previous query's merge (uniform branch)
-        if (blockIdx.y == 0)
-            merge_lists_body<E, SCAN_WAVES>(a.side.partials, a.side.nlists, a.side.list_len, a.side.k,
-                                            a.side.id_base, a.side.ids, a.side.dists, a.side.counts);
-        return;
-    }
     const int lane = threadIdx.x & 63;
-    const uint32_t qi = blockIdx.y;
-    const float4 *q4 = reinterpret_cast<const float4 *>(a.queries) + (size_t)qi * (a.qpitch / 4);
     const float4 *data = reinterpret_cast<const float4 *>(a.data);
-    uint64_t t0, t1;
-    wave_range(a, SCAN_WAVES, t0, t1);
-    WaveTopK<E> tk;
-    tk.init((int)a.k);
     uint64_t m_next = t0 < t1 ? tile_mask(a, t0) : 0ull;
     for (uint64_t t = t0; t < t1; ++t) {
         const uint64_t m = m_next;
@@ -138,7 +133,120 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_kernel(ScanArgs a, u
             r = row_dot_or_l2_generic<METRIC, 64>(rp, q4, (int)a.dim);
         tk.offer(lane_key(m, wrap_metric(a.metric, r), t, lane));
     }
+}
+
+// Variant 0 (and 2 = plain loads).
+template <int METRIC, int D, int E>
+__global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_kernel(ScanArgs a, uint64_t *partials)
+{
+    if (a.side.active && blockIdx.x == gridDim.x - 1) {  // the previous query's merge (uniform branch)
+        if (blockIdx.y == 0)
+            merge_lists_body<E, SCAN_WAVES>(a.side.partials, a.side.nlists, a.side.list_len, a.side.k,
+                                            a.side.id_base, a.side.ids, a.side.dists, a.side.counts);
+        return;
+    }
+    const uint32_t qi = blockIdx.y;
+    const float4 *q4 = reinterpret_cast<const float4 *>(a.queries) + (size_t)qi * (a.qpitch / 4);
+    uint64_t t0, t1;
+    wave_range(a, SCAN_WAVES, t0, t1);
+    WaveTopK<E> tk;
+    tk.init((int)a.k);
+    scan_tiles<METRIC, D, E>(a, q4, t0, t1, tk);
     group_combine_store<E, SCAN_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
+}
+
+// In-launch hand-off (cdna_hip_programming.md §6 Guideline 16, form R1): the
+// producer stores its list write-through (agent-scope relaxed atomic stores =
+// sc1), drains them (s_waitcnt vmcnt(0)) and adds to an arrival counter; no
+// release fence, so no per-query L2 writeback.  The consumer polls the counter
+// relaxed with s_sleep, then ONE agent-scope acquire drops its stale L1 lines.
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(1))) uint64_t gu64;
+
+// Thread 0 polls; false after ~4 s (s_memrealtime is 100 MHz), so a waiting
+// workgroup always exits.
+__device__ __forceinline__ bool wait_arrivals(uint32_t *ctr, uint32_t target)
+{
+    __shared__ int ok;
+    if (threadIdx.x == 0) {
+        const uint64_t start = __builtin_amdgcn_s_memrealtime();
+        int r = 1;
+        while (__hip_atomic_load((gu32 *)ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            if (__builtin_amdgcn_s_memrealtime() - start > 400000000ull) {
+                r = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(4);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        ok = r;
+    }
+    __syncthreads();
+    return ok != 0;
+}
+
+// group_combine_store with write-through stores, then the storing wave drains
+// and publishes one arrival.
+template <int E, int WAVES>
+__device__ __forceinline__ void group_combine_publish(WaveTopK<E> &tk, uint64_t *out, uint32_t *arrivals)
+{
+    __shared__ uint64_t sh[WAVES][64 * E];
+    const int lane = threadIdx.x & 63;
+    const int wave = wave_id();
+#pragma unroll
+    for (int e = 0; e < E; e++) sh[wave][e * 64 + lane] = tk.l[e];
+    __syncthreads();
+    if (wave == 0) {
+        for (int w = 1; w < WAVES; w++) {
+            uint64_t o[E];
+#pragma unroll
+            for (int e = 0; e < E; e++) o[e] = sh[w][e * 64 + lane];
+            merge_lists<E>(tk.l, o);
+        }
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            const int i = e * 64 + lane;
+            if (i < tk.k) __hip_atomic_store((gu64 *)(out + i), tk.l[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_fetch_add((gu32 *)arrivals, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();  // sh is reused by the next query
+}
+
+// Query-stream scan (see StreamJob).  Workgroups 0..groups-1 scan; workgroup
+// `groups` merges.  Scan workgroups never wait on anything, so the merge
+// workgroup's wait always ends.
+template <int METRIC, int D, int E>
+__global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_stream_kernel(ScanArgs a, StreamJob j)
+{
+    const uint32_t G = j.groups;
+    if (blockIdx.x == G) {
+        for (uint32_t q = 0; q < a.nq; q++) {
+            if (!wait_arrivals(j.arrivals + q, G)) {
+                if (threadIdx.x == 0) atomicOr(j.status, 1u);
+                return;
+            }
+            merge_lists_body<E, SCAN_WAVES>(j.partials + (size_t)q * G * a.k, G, a.k, a.k, a.id_base,
+                                            j.ids + (size_t)q * a.k, j.dists + (size_t)q * a.k,
+                                            j.counts ? j.counts + q : nullptr);
+            __syncthreads();  // merge LDS reused by the next query
+        }
+        return;
+    }
+    const uint64_t ntiles = a.tile_end - a.tile_begin;
+    const uint64_t total = (uint64_t)G * SCAN_WAVES;
+    const uint64_t gw = (uint64_t)blockIdx.x * SCAN_WAVES + wave_id();
+    const uint64_t t0 = a.tile_begin + ntiles * gw / total;
+    const uint64_t t1 = a.tile_begin + ntiles * (gw + 1) / total;
+    for (uint32_t q = 0; q < a.nq; q++) {
+        const float4 *q4 = reinterpret_cast<const float4 *>(a.queries) + (size_t)q * (a.qpitch / 4);
+        WaveTopK<E> tk;
+        tk.init((int)a.k);
+        scan_tiles<METRIC, D, E>(a, q4, t0, t1, tk);
+        group_combine_publish<E, SCAN_WAVES>(tk, j.partials + ((size_t)q * G + blockIdx.x) * a.k, j.arrivals + q);
+    }
 }
 
 // Variant 1: block-granular software pipeline.  The wave's tile range is a
@@ -273,13 +381,13 @@ static void launch_fixed(const ScanArgs &a, uint64_t *partials, dim3 grid, dim3 
 {
     const int v = a.side.active ? 0 : tuning().scan_variant;
     if (v == 1 && !a.allow)
-        hipLaunchKernelGGL((scan_f32_pipe_kernel<METRIC, D, E>), grid, block, 0, s, a, partials);
+        launch_timed((scan_f32_pipe_kernel<METRIC, D, E>), grid, block, 0, s, a, partials);
     else if (v == 2)
-        hipLaunchKernelGGL((scan_f32_plain_kernel<METRIC, D, E>), grid, block, 0, s, a, partials);
+        launch_timed((scan_f32_plain_kernel<METRIC, D, E>), grid, block, 0, s, a, partials);
     else if (v == 3)
-        hipLaunchKernelGGL((scan_f32_sweep_kernel<METRIC, D, E>), grid, block, 0, s, a, partials);
+        launch_timed((scan_f32_sweep_kernel<METRIC, D, E>), grid, block, 0, s, a, partials);
     else
-        hipLaunchKernelGGL((scan_f32_kernel<METRIC, D, E>), grid, block, 0, s, a, partials);
+        launch_timed((scan_f32_kernel<METRIC, D, E>), grid, block, 0, s, a, partials);
 }
 
 template <int METRIC, int E>
@@ -290,9 +398,36 @@ static hipError_t launch_f32_e(const ScanArgs &a, uint64_t *partials, int groups
     case 128: launch_fixed<METRIC, 128, E>(a, partials, grid, block, s); break;
     case 768: launch_fixed<METRIC, 768, E>(a, partials, grid, block, s); break;
     case 1536: launch_fixed<METRIC, 1536, E>(a, partials, grid, block, s); break;
-    default: hipLaunchKernelGGL((scan_f32_kernel<METRIC, 0, E>), grid, block, 0, s, a, partials); break;
+    default: launch_timed((scan_f32_kernel<METRIC, 0, E>), grid, block, 0, s, a, partials); break;
     }
     return hipGetLastError();
+}
+
+template <int METRIC, int E>
+static hipError_t launch_stream_e(const ScanArgs &a, const StreamJob &j, hipStream_t s)
+{
+    dim3 grid(j.groups + 1), block(SCAN_WAVES * 64);
+    switch (a.dim) {
+    case 128: launch_timed((scan_f32_stream_kernel<METRIC, 128, E>), grid, block, 0, s, a, j); break;
+    case 768: launch_timed((scan_f32_stream_kernel<METRIC, 768, E>), grid, block, 0, s, a, j); break;
+    case 1536: launch_timed((scan_f32_stream_kernel<METRIC, 1536, E>), grid, block, 0, s, a, j); break;
+    default: launch_timed((scan_f32_stream_kernel<METRIC, 0, E>), grid, block, 0, s, a, j); break;
+    }
+    return hipGetLastError();
+}
+
+template <int METRIC>
+static hipError_t launch_stream_m(const ScanArgs &a, const StreamJob &j, hipStream_t s)
+{
+    if (a.k <= 64) return launch_stream_e<METRIC, 1>(a, j, s);
+    if (a.k <= 128) return launch_stream_e<METRIC, 2>(a, j, s);
+    return launch_stream_e<METRIC, 4>(a, j, s);
+}
+
+hipError_t launch_scan_f32_stream(const ScanArgs &a, const StreamJob &j, hipStream_t s)
+{
+    if (a.metric == WVG_M_L2) return launch_stream_m<WVG_M_L2>(a, j, s);
+    return launch_stream_m<WVG_M_DOT>(a, j, s);
 }
 
 template <int METRIC>
