@@ -26,13 +26,21 @@ __device__ __forceinline__ uint64_t bq_tile_mask(const ScanArgs &a, uint64_t t)
     return m;
 }
 
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ u64x2 ld_codes(const u64x2 *p) { return __builtin_nontemporal_load(p); }
+
+// K5: one wave per 64-row tile at a time (lane = row), XOR + popcount over
+// the tile's 16-byte chunks.  Fixed NCH: the next live tile's chunks are
+// loaded (non-temporal) while the current tile is reduced and offered, so a
+// wave keeps two tiles' codes in flight; tile masks are scalar and prefetched.
 template <int E, int NCH>
 __global__ __launch_bounds__(BQ_WAVES * 64) void scan_bq_kernel(ScanArgs a, uint64_t *partials)
 {
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t qi = blockIdx.y;
     const uint64_t *q = reinterpret_cast<const uint64_t *>(a.queries) + (size_t)qi * a.qpitch;
-    const ulonglong2 *data = reinterpret_cast<const ulonglong2 *>(a.data);
+    const u64x2 *data = reinterpret_cast<const u64x2 *>(a.data);
     const uint32_t nch = NCH > 0 ? (uint32_t)NCH : a.nchunks;
     const uint64_t ntiles = a.tile_end - a.tile_begin;
     const uint64_t total = (uint64_t)gridDim.x * BQ_WAVES;
@@ -40,27 +48,54 @@ __global__ __launch_bounds__(BQ_WAVES * 64) void scan_bq_kernel(ScanArgs a, uint
     const uint64_t t0 = a.tile_begin + ntiles * gw / total, t1 = a.tile_begin + ntiles * (gw + 1) / total;
     WaveTopK<E> tk;
     tk.init((int)a.k);
-    for (uint64_t t = t0; t < t1; ++t) {
-        const uint64_t m = bq_tile_mask(a, t);
-        if (m == 0ull) continue;
-        const ulonglong2 *rp = data + (size_t)t * nch * 64 + lane;
-        uint32_t tot = 0;
-        if constexpr (NCH > 0) {
-            ulonglong2 xs[NCH];
+    if constexpr (NCH > 0) {
+        // next live tile at or after t (wave-uniform), its mask in m
+        auto next_live = [&](uint64_t t, uint64_t &m) {
+            for (; t < t1; ++t) {
+                m = bq_tile_mask(a, t);
+                if (m) break;
+            }
+            return t;
+        };
+        uint64_t m_cur = 0, m_nxt = 0;
+        uint64_t t = next_live(t0, m_cur);
+        u64x2 cur[NCH], nxt[NCH];
+        if (t < t1) {
+            const u64x2 *rp = data + (size_t)t * NCH * 64 + lane;
 #pragma unroll
-            for (int c = 0; c < NCH; c++) xs[c] = rp[(size_t)c * 64];
+            for (int c = 0; c < NCH; c++) cur[c] = ld_codes(rp + (size_t)c * 64);
+        }
+        while (t < t1) {
+            const uint64_t tn = next_live(t + 1, m_nxt);
+            if (tn < t1) {
+                const u64x2 *rp = data + (size_t)tn * NCH * 64 + lane;
+#pragma unroll
+                for (int c = 0; c < NCH; c++) nxt[c] = ld_codes(rp + (size_t)c * 64);
+            }
+            uint32_t tot = 0;
 #pragma unroll
             for (int c = 0; c < NCH; c++)
-                tot += (uint32_t)__popcll(xs[c].x ^ q[2 * c]) + (uint32_t)__popcll(xs[c].y ^ q[2 * c + 1]);
-        } else {
+                tot += (uint32_t)__popcll(cur[c].x ^ q[2 * c]) + (uint32_t)__popcll(cur[c].y ^ q[2 * c + 1]);
+            const float dist = (float)tot;  // exact: sum of float32(popcount) is an integer < 2^24
+            tk.offer(((m_cur >> lane) & 1ull) ? wvg_make_key(dist, (uint32_t)(t * 64 + lane)) : WVG_KEY_NONE);
+#pragma unroll
+            for (int c = 0; c < NCH; c++) cur[c] = nxt[c];
+            t = tn;
+            m_cur = m_nxt;
+        }
+    } else {
+        for (uint64_t t = t0; t < t1; ++t) {
+            const uint64_t m = bq_tile_mask(a, t);
+            if (m == 0ull) continue;
+            const u64x2 *rp = data + (size_t)t * nch * 64 + lane;
+            uint32_t tot = 0;
             for (uint32_t c = 0; c < nch; c++) {
-                const ulonglong2 x = rp[(size_t)c * 64];
+                const u64x2 x = ld_codes(rp + (size_t)c * 64);
                 tot += (uint32_t)__popcll(x.x ^ q[2 * c]) + (uint32_t)__popcll(x.y ^ q[2 * c + 1]);
             }
+            const float dist = (float)tot;
+            tk.offer(((m >> lane) & 1ull) ? wvg_make_key(dist, (uint32_t)(t * 64 + lane)) : WVG_KEY_NONE);
         }
-        const float dist = (float)tot;  // exact: sum of float32(popcount) is an integer < 2^24
-        const uint64_t key = ((m >> lane) & 1ull) ? wvg_make_key(dist, (uint32_t)(t * 64 + lane)) : WVG_KEY_NONE;
-        tk.offer(key);
     }
     group_combine_store<E, BQ_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
 }

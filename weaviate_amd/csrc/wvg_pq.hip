@@ -19,7 +19,7 @@
 
 namespace wvg {
 
-constexpr int PQ_WAVES = 4;
+constexpr int PQ_SCAN_WAVES = 16;  // K8: one workgroup per CU shares the LUT
 
 // Step(a, b) in the pure-Go order.
 __device__ __forceinline__ float go_step(int metric, const float *a, const float *b, uint32_t n)
@@ -205,7 +205,7 @@ hipError_t launch_pq_store(const uint8_t *codes, const uint64_t *slots, uint64_t
     return hipGetLastError();
 }
 
-__device__ __forceinline__ uint32_t code_at(const uint4 (&cw)[8], int i)
+__device__ __forceinline__ uint32_t code_at(const uint4 *cw, int i)
 {
     const uint4 v = cw[i >> 4];
     const int w = (i >> 2) & 3;
@@ -213,45 +213,92 @@ __device__ __forceinline__ uint32_t code_at(const uint4 (&cw)[8], int i)
     return (word >> (8 * (i & 3))) & 0xFFu;
 }
 
-// K8: ADC scan, LUT in LDS.  M = compile-time segments (<= 128) or 0.
-template <int E, int M>
-__global__ __launch_bounds__(PQ_WAVES * 64) void scan_pq_kernel(ScanArgs a, uint64_t *partials)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint4 ld_codes(const uint4 *p)
+{
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ uint64_t pq_tile_mask(const ScanArgs &a, uint64_t t)
+{
+    uint64_t m = a.valid[t];
+    if (a.allow) {
+        uint64_t w = (a.id_base >> 6) + t;
+        m &= w < a.allow_words ? a.allow[w] : 0ull;
+    }
+    return m;
+}
+
+// K8: ADC scan.  One workgroup of PQ_SCAN_WAVES waves per CU shares one copy
+// of the query's LUT (m x ks fp32) in LDS; lane = row, each lane gathers its
+// row's m entries (independent ds_read_b32s) and sums them in segment order
+// (CH/product_quantization.go:85-104).  Fixed M: the next live tile's codes are
+// loaded (non-temporal) while the current tile is looked up, so the HBM
+// latency is covered by 16 waves x 2 tiles in flight per CU.
+template <int E, int M, int KS>
+__global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq_kernel(ScanArgs a, uint64_t *partials)
 {
     extern __shared__ __attribute__((aligned(16))) float lut[];
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t qi = blockIdx.y;
     const uint32_t m = M > 0 ? (uint32_t)M : a.pq_m;
-    const uint32_t ks = a.pq_ks;
+    const uint32_t ks = KS > 0 ? (uint32_t)KS : a.pq_ks;
     const float *glut = reinterpret_cast<const float *>(a.queries) + (size_t)qi * a.qpitch;
     for (uint32_t i = threadIdx.x; i < m * ks; i += blockDim.x) lut[i] = glut[i];
     __syncthreads();
     const uint4 *data = reinterpret_cast<const uint4 *>(a.data);
     const uint32_t nch = a.nchunks;
     const uint64_t ntiles = a.tile_end - a.tile_begin;
-    const uint64_t total = (uint64_t)gridDim.x * PQ_WAVES;
-    const uint64_t gw = (uint64_t)blockIdx.x * PQ_WAVES + wave;
+    const uint64_t total = (uint64_t)gridDim.x * PQ_SCAN_WAVES;
+    const uint64_t gw = (uint64_t)blockIdx.x * PQ_SCAN_WAVES + wave;
     const uint64_t t0 = a.tile_begin + ntiles * gw / total, t1 = a.tile_begin + ntiles * (gw + 1) / total;
     WaveTopK<E> tk;
     tk.init((int)a.k);
-    for (uint64_t t = t0; t < t1; ++t) {
-        uint64_t msk = a.valid[t];
-        if (a.allow) {
-            uint64_t w = (a.id_base >> 6) + t;
-            msk &= w < a.allow_words ? a.allow[w] : 0ull;
-        }
-        if (msk == 0ull) continue;
-        const uint4 *rp = data + (size_t)t * nch * 64 + lane;
-        float sum = 0.0f;
-        if constexpr (M > 0) {
-            uint4 cw[8];
+    if constexpr (M > 0) {
+        constexpr int NC = (M + 15) / 16;
+        auto next_live = [&](uint64_t t, uint64_t &msk) {
+            for (; t < t1; ++t) {
+                msk = pq_tile_mask(a, t);
+                if (msk) break;
+            }
+            return t;
+        };
+        uint64_t m_cur = 0, m_nxt = 0;
+        uint64_t t = next_live(t0, m_cur);
+        uint4 cur[NC], nxt[NC];
+        if (t < t1) {
+            const uint4 *rp = data + (size_t)t * NC * 64 + lane;
 #pragma unroll
-            for (int c = 0; c < (M + 15) / 16; c++) cw[c] = rp[(size_t)c * 64];
+            for (int c = 0; c < NC; c++) cur[c] = ld_codes(rp + (size_t)c * 64);
+        }
+        while (t < t1) {
+            const uint64_t tn = next_live(t + 1, m_nxt);
+            if (tn < t1) {
+                const uint4 *rp = data + (size_t)tn * NC * 64 + lane;
+#pragma unroll
+                for (int c = 0; c < NC; c++) nxt[c] = ld_codes(rp + (size_t)c * 64);
+            }
             float v[M];
 #pragma unroll
-            for (int i = 0; i < M; i++) v[i] = lut[i * ks + code_at(cw, i)];
+            for (int i = 0; i < M; i++) v[i] = lut[i * ks + code_at(cur, i)];
+            float sum = 0.0f;
 #pragma unroll
             for (int i = 0; i < M; i++) sum = sum + v[i];
-        } else {
+            const float dist = wrap_metric(a.metric, sum);
+            tk.offer(((m_cur >> lane) & 1ull) ? wvg_make_key(dist, (uint32_t)(t * 64 + lane)) : WVG_KEY_NONE);
+#pragma unroll
+            for (int c = 0; c < NC; c++) cur[c] = nxt[c];
+            t = tn;
+            m_cur = m_nxt;
+        }
+    } else {
+        for (uint64_t t = t0; t < t1; ++t) {
+            const uint64_t msk = pq_tile_mask(a, t);
+            if (msk == 0ull) continue;
+            const uint4 *rp = data + (size_t)t * nch * 64 + lane;
+            float sum = 0.0f;
             for (uint32_t c = 0; c < nch; c++) {
                 const uint4 x = rp[(size_t)c * 64];
                 const uint32_t ws[4] = {x.x, x.y, x.z, x.w};
@@ -260,26 +307,28 @@ __global__ __launch_bounds__(PQ_WAVES * 64) void scan_pq_kernel(ScanArgs a, uint
                     if (i < m) sum = sum + lut[i * ks + ((ws[b >> 2] >> (8 * (b & 3))) & 0xFFu)];
                 }
             }
+            const float dist = wrap_metric(a.metric, sum);
+            tk.offer(((msk >> lane) & 1ull) ? wvg_make_key(dist, (uint32_t)(t * 64 + lane)) : WVG_KEY_NONE);
         }
-        const float dist = wrap_metric(a.metric, sum);
-        const uint64_t key = ((msk >> lane) & 1ull) ? wvg_make_key(dist, (uint32_t)(t * 64 + lane)) : WVG_KEY_NONE;
-        tk.offer(key);
     }
-    group_combine_store<E, PQ_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
+    group_combine_store<E, PQ_SCAN_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
 }
 
 template <int E>
 static hipError_t launch_pq_e(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
 {
-    dim3 grid(groups, a.nq), block(PQ_WAVES * 64);
+    dim3 grid(groups, a.nq), block(PQ_SCAN_WAVES * 64);
     const size_t lds = (size_t)a.pq_m * a.pq_ks * 4;
-    switch (a.pq_m) {
-    case 8: launch_timed((scan_pq_kernel<E, 8>), grid, block, lds, s, a, partials); break;
-    case 16: launch_timed((scan_pq_kernel<E, 16>), grid, block, lds, s, a, partials); break;
-    case 32: launch_timed((scan_pq_kernel<E, 32>), grid, block, lds, s, a, partials); break;
-    case 64: launch_timed((scan_pq_kernel<E, 64>), grid, block, lds, s, a, partials); break;
-    default: launch_timed((scan_pq_kernel<E, 0>), grid, block, lds, s, a, partials); break;
+    if (a.pq_ks == 256) {
+        switch (a.pq_m) {
+        case 8: launch_timed((scan_pq_kernel<E, 8, 256>), grid, block, lds, s, a, partials); return hipGetLastError();
+        case 16: launch_timed((scan_pq_kernel<E, 16, 256>), grid, block, lds, s, a, partials); return hipGetLastError();
+        case 32: launch_timed((scan_pq_kernel<E, 32, 256>), grid, block, lds, s, a, partials); return hipGetLastError();
+        case 64: launch_timed((scan_pq_kernel<E, 64, 256>), grid, block, lds, s, a, partials); return hipGetLastError();
+        default: break;
+        }
     }
+    launch_timed((scan_pq_kernel<E, 0, 0>), grid, block, lds, s, a, partials);
     return hipGetLastError();
 }
 

@@ -190,12 +190,17 @@ struct WaveTopK {
 
     __device__ __forceinline__ void refresh_tau()
     {
-        const int idx = k - 1;
-        uint64_t v = l[0];
+        // read lane (k-1)&63 of every register, select by (k-1)>>6 on the
+        // scalar side: a select on the vector side is turned into a dynamic
+        // index through scratch, whose vmcnt(0) wait drains in-flight loads.
+        const int idx = k - 1, hi = idx >> 6, lo = idx & 63;
+        uint64_t t = readlane64(l[0], lo);
 #pragma unroll
-        for (int e = 1; e < E; e++)
-            if ((idx >> 6) == e) v = l[e];
-        tau = readlane64(v, idx & 63);
+        for (int e = 1; e < E; e++) {
+            const uint64_t te = readlane64(l[e], lo);
+            t = hi == e ? te : t;
+        }
+        tau = t;
     }
 
     // Offer one key per lane (KEY_NONE for an empty lane).
