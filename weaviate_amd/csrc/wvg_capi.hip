@@ -1221,6 +1221,9 @@ int wvgx_set_tuning(int key, int value)
     } else if (key == 2) {
         old = t.pipeline_mode;
         t.pipeline_mode = value;
+    } else if (key == 3) {
+        old = t.gemm_pf;
+        t.gemm_pf = value;
     }
     return old;
 }

@@ -143,6 +143,7 @@ hipError_t launch_gemm_topk(const ScanArgs &a, uint32_t nrr, uint64_t *partials,
 struct Tuning {
     int scan_variant = 0;    // K1 variant (see wvg_scan.hip)
     int groups_per_cu = 1;   // K1 workgroups per CU (A/B: 1 = fewest partial lists, same scan rate)
+    int gemm_pf = 0;         // K3 register prefetch depth: 0 = by top-k size (2 for k <= 64), 1 = force 1
     int pipeline_mode = 1;   // wvg_search_device_pipelined: 0 = one launch per query (merge folded into the
                              // next launch), 1 = one query-stream launch
 };
