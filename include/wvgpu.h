@@ -101,7 +101,9 @@ int wvg_pq_set_codebook(wvg_corpus *c, const float *centers, uint32_t m, uint32_
  * queries: [nq][dim] float32 (normalized internally for cosine, index.go:323).
  * allow_bits: optional bitmap over global docIDs (helpers.AllowList), bit i of
  * word i/64; an empty allow list yields empty results (index.go:425-427).
- * Outputs: [nq][k] ids/dists, counts[nq] = min(k, live allowed rows).       */
+ * Outputs: [nq][k] ids/dists, counts[nq] = min(k, live allowed rows).
+ * Any k: up to 256 the fused register top-k of the scan; above, a radix
+ * select + sort over per-row distance keys in HBM (the same distances).    */
 int wvg_search(wvg_corpus *c, const float *queries, uint32_t nq, uint32_t k,
                const uint64_t *allow_bits, uint64_t allow_words, uint64_t *out_ids,
                float *out_dists, uint32_t *out_counts);
@@ -112,6 +114,18 @@ int wvg_search_bq_rescore(wvg_corpus *bq, wvg_corpus *f32, const float *queries,
                           uint32_t k, uint32_t rescore_limit, const uint64_t *allow_bits,
                           uint64_t allow_words, uint64_t *out_ids, float *out_dists,
                           uint32_t *out_counts);
+
+/* flat.SearchByVectorDistance (V/flat/index.go:531-591): every row with
+ * dist <= target_distance or |dist - target| <= 1e-6 (floatcomp.InDelta,
+ * usecases/floatcomp/delta.go:16-19), ascending, as far as the growing-limit
+ * loop reaches (limits 100, 1100, 11100, ...; V/common/search_by_dist_params.go:
+ * 14-83): it stops at the first window whose last row is above the target,
+ * and before a limit above max_limit (max_limit < 0: unlimited).  One pass
+ * over the corpus regardless of how many windows the loop takes.
+ * *out_count = number of results; min(count, out_capacity) are written. */
+int wvg_search_by_distance(wvg_corpus *c, const float *query, float target_distance, int64_t max_limit,
+                           const uint64_t *allow_bits, uint64_t allow_words, uint64_t *out_ids,
+                           float *out_dists, uint64_t out_capacity, uint64_t *out_count);
 
 /* Device-pointer variants: inputs/outputs in HBM, asynchronous on `stream`
  * (a hipStream_t, NULL = default stream); no host synchronization, no

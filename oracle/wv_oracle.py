@@ -264,3 +264,40 @@ def lex_topk(dists, ids, k):
     ids = np.asarray(ids, dtype=np.uint64)
     order = np.lexsort((ids, ord_key(dists)))[:k]
     return ids[order], dists[order]
+
+
+def search_by_distance(search_fn, target, max_limit):
+    """SearchByVectorDistance's growing-limit loop, restated from
+    V/hnsw/search.go:85-151 (the loop V/flat/index.go:531-591 intends) with
+    V/common/search_by_dist_params.go:14-83 (limits 100, then offset = total,
+    limit *= 10) and floatcomp.InDelta (usecases/floatcomp/delta.go:16-19).
+    search_fn(total) -> (ids, dists) ascending, as SearchByVector."""
+    target = np.float32(target)
+    offset, limit = 0, 100
+    total = offset + limit
+    res_i, res_d = [], []
+
+    def recursive():
+        ids, dist = search_fn(total)
+        lo, hi = min(offset, len(ids)), min(total, len(ids))
+        ids, dist = ids[lo:hi], dist[lo:hi]
+        if len(ids) == 0:
+            return False
+        cont = bool(np.float32(dist[-1]) <= target)
+        for i in range(len(ids)):
+            if np.float32(dist[i]) <= target or abs(float(dist[i]) - float(target)) <= 1e-6:
+                res_i.append(int(ids[i]))
+                res_d.append(np.float32(dist[i]))
+            else:
+                break
+        return cont
+
+    cont = recursive()
+    while cont:
+        offset = total
+        limit *= 10
+        total = offset + limit
+        if max_limit >= 0 and total > max_limit:
+            break
+        cont = recursive()
+    return np.asarray(res_i, dtype=np.uint64), np.asarray(res_d, dtype=np.float32)

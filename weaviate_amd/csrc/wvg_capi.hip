@@ -857,20 +857,32 @@ static size_t query_bytes(const wvg_corpus *c, uint32_t nq)
     }
 }
 
+}  // extern "C"
+namespace wvg {
+static int search_large_k(wvg_corpus *c, const float *queries, uint32_t nq, uint32_t k, const uint64_t *allow_bits,
+                          uint64_t allow_words, const SearchPlan &p, uint64_t *out_ids, float *out_dists,
+                          uint32_t *out_counts);
+static int bq_rescore_large(wvg_corpus *bq, wvg_corpus *f32, const float *queries, uint32_t nq, uint32_t k,
+                            uint32_t R, const uint64_t *allow_bits, uint64_t allow_words, const SearchPlan &p,
+                            uint64_t *out_ids, float *out_dists, uint32_t *out_counts);
+}  // namespace wvg
+extern "C" {
+
 int wvg_search(wvg_corpus *c, const float *queries, uint32_t nq, uint32_t k, const uint64_t *allow_bits,
                uint64_t allow_words, uint64_t *out_ids, float *out_dists, uint32_t *out_counts)
 {
     int rc = check_corpus(c);
     if (rc) return rc;
     if (nq > 0 && !queries) return fail(WVG_ERR_INVALID, "null queries");
-    if (k > MAX_K) return fail(WVG_ERR_UNSUPPORTED, "k above 256 is not supported by the fused top-k");
     if (c->kind == WVG_KIND_PQ && !c->d_centers) return fail(WVG_ERR_INVALID, "PQ corpus has no codebook");
     std::shared_lock<std::shared_mutex> lk(c->rw);
-    SearchPlan p = plan_search(c, nq, k, allow_bits, allow_words);
+    SearchPlan p = plan_search(c, nq, std::min(k, MAX_K), allow_bits, allow_words);
     if (p.empty) {
         write_empty(nq, k, out_ids, out_dists, out_counts);
         return WVG_OK;
     }
+    if (k > MAX_K)  // beyond the fused register top-k: select + sort in HBM
+        return search_large_k(c, queries, nq, k, allow_bits, allow_words, p, out_ids, out_dists, out_counts);
     SlotGuard g(c->ctx);
     rc = c->ctx->acquire(&g.slot);
     if (rc) return rc;
@@ -905,6 +917,334 @@ int wvg_search(wvg_corpus *c, const float *queries, uint32_t nq, uint32_t k, con
     return WVG_OK;
 }
 
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Unbounded selections (wvg_select.hip): top-k for k > 256 and the range
+// search of SearchByVectorDistance.  One query at a time; every phase in HBM.
+// ---------------------------------------------------------------------------
+namespace wvg {
+
+static ScanArgs scan_args_for(const wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t nq, uint32_t k,
+                              const uint64_t *d_allow, uint64_t allow_words, uint64_t tb, uint64_t te)
+{
+    ScanArgs a{};
+    a.data = c->d_data;
+    a.valid = c->d_valid;
+    a.allow = d_allow;
+    a.allow_words = allow_words;
+    a.id_base = c->id_base;
+    a.tile_begin = tb;
+    a.tile_end = te;
+    a.dim = c->dim;
+    a.nchunks = c->nchunks;
+    a.metric = c->metric;
+    a.queries = d_q;
+    a.qpitch = qpitch;
+    a.nq = nq;
+    a.k = k;
+    a.pq_m = c->pq_m;
+    a.pq_ks = c->pq_ks;
+    return a;
+}
+
+// Device buffers of the selection flow over `nslots` slots.
+struct SelectBufs {
+    uint32_t *keys = nullptr;           // [nslots] ordered distance keys
+    void *st = nullptr;                 // radix-select state
+    uint32_t *hist = nullptr;           // 4096 bins
+    unsigned long long *cnt = nullptr;  // [4] counters
+    uint64_t *cmp = nullptr;            // [nslots] compacted keys
+    uint64_t *sorted = nullptr;         // [nslots] sorted keys
+    void *temp = nullptr;
+    size_t temp_bytes = 0;
+    static void layout(Carver &cv, uint64_t nslots, size_t o[6], size_t &temp_bytes)
+    {
+        temp_bytes = sort_temp_bytes(nslots);
+        o[0] = cv.take(nslots * 4);
+        o[1] = cv.take(select_state_bytes());
+        o[2] = cv.take(4096 * 4);
+        o[3] = cv.take(4 * 8);
+        o[4] = cv.take(nslots * 8);
+        o[5] = cv.take(nslots * 8);
+    }
+    void bind(char *b, const size_t o[6], size_t o_temp, size_t tb)
+    {
+        keys = (uint32_t *)(b + o[0]);
+        st = b + o[1];
+        hist = (uint32_t *)(b + o[2]);
+        cnt = (unsigned long long *)(b + o[3]);
+        cmp = (uint64_t *)(b + o[4]);
+        sorted = (uint64_t *)(b + o[5]);
+        temp = b + o_temp;
+        temp_bytes = tb;
+    }
+};
+
+// Compacts live keys <= threshold (st_dev: the radix-select result, else thr)
+// and sorts them; returns how many there are.
+static int compact_sort(const SelectBufs &sb, uint64_t nslots, const void *st_dev, uint32_t thr, uint32_t slot0,
+                        int num_cus, hipStream_t s, uint64_t *n_out)
+{
+    WVG_HIP(launch_key_compact(sb.keys, nslots, st_dev, thr, slot0, num_cus, sb.cmp, sb.cnt, s));
+    unsigned long long n = 0;
+    WVG_HIP(hipMemcpyAsync(&n, sb.cnt, 8, hipMemcpyDeviceToHost, s));
+    WVG_HIP(hipStreamSynchronize(s));
+    WVG_HIP(sort_keys64(sb.temp, sb.temp_bytes, sb.cmp, sb.sorted, n, s));
+    *n_out = n;
+    return WVG_OK;
+}
+
+// The `want` smallest (distance, slot) keys of one prepared query, ascending,
+// in sb.sorted; *n_out = min(want, live allowed rows).
+static int select_smallest(const wvg_corpus *c, const ScanArgs &a1, uint64_t want, const SelectBufs &sb,
+                           hipStream_t s, uint64_t *n_out)
+{
+    const int cus = c->ctx->num_cus;
+    const uint64_t nslots = (a1.tile_end - a1.tile_begin) * 64;
+    WVG_HIP(launch_ordkeys(a1, c->kind, cus, sb.keys, s));
+    uint64_t n = 0;
+    int rc;
+    if (want >= nslots) {
+        rc = compact_sort(sb, nslots, nullptr, 0xFFFFFFFEu, (uint32_t)(a1.tile_begin * 64), cus, s, &n);
+    } else {
+        WVG_HIP(launch_select_kth(sb.keys, nslots, want, cus, sb.st, sb.hist, s));
+        rc = compact_sort(sb, nslots, sb.st, 0u, (uint32_t)(a1.tile_begin * 64), cus, s, &n);
+    }
+    if (rc) return rc;
+    *n_out = std::min<uint64_t>(n, want);
+    return WVG_OK;
+}
+
+// Element size of one prepared query row (F32 / PQ LUT floats, BQ words).
+static size_t query_elem_bytes(const wvg_corpus *c) { return c->kind == WVG_KIND_BQ ? 8 : 4; }
+
+// wvg_search for k > 256: S1-S4 per query.
+static int search_large_k(wvg_corpus *c, const float *queries, uint32_t nq, uint32_t k, const uint64_t *allow_bits,
+                          uint64_t allow_words, const SearchPlan &p, uint64_t *out_ids, float *out_dists,
+                          uint32_t *out_counts)
+{
+    SlotGuard g(c->ctx);
+    int rc = c->ctx->acquire(&g.slot);
+    if (rc) return rc;
+    const uint64_t nslots = (p.te - p.tb) * 64;
+    Carver cv;
+    const size_t o_q = cv.take(query_bytes(c, nq));
+    const size_t o_qtmp = cv.take(c->kind == WVG_KIND_PQ ? (size_t)nq * c->dim * 4 : 0);
+    const size_t o_allow = cv.take(allow_bits ? allow_words * 8 : 0);
+    size_t o_sel[6], temp_bytes = 0;
+    SelectBufs::layout(cv, nslots, o_sel, temp_bytes);
+    const size_t o_temp = cv.take(temp_bytes);
+    const size_t o_ids = cv.take((size_t)k * 8), o_d = cv.take((size_t)k * 4);
+    void *base = nullptr;
+    rc = g.slot->device_scratch(cv.off, &base);
+    if (rc) return rc;
+    char *b = (char *)base;
+    hipStream_t s = g.slot->stream;
+    uint32_t qpitch = 0;
+    rc = stage_queries(c, g.slot, queries, nq, b + o_q, qpitch, (float *)(b + o_q), b + o_qtmp);
+    if (rc) return rc;
+    const uint64_t *d_allow = nullptr;
+    if (allow_bits) {
+        WVG_HIP(hipMemcpyAsync(b + o_allow, allow_bits, allow_words * 8, hipMemcpyHostToDevice, s));
+        d_allow = (const uint64_t *)(b + o_allow);
+    }
+    SelectBufs sb;
+    sb.bind(b, o_sel, o_temp, temp_bytes);
+    for (uint32_t qi = 0; qi < nq; qi++) {
+        const void *dq = b + o_q + (size_t)qi * qpitch * query_elem_bytes(c);
+        ScanArgs a1 = scan_args_for(c, dq, qpitch, 1, k, d_allow, allow_words, p.tb, p.te);
+        uint64_t n = 0;
+        rc = select_smallest(c, a1, k, sb, s, &n);
+        if (rc) return rc;
+        WVG_HIP(launch_emit_sorted(sb.sorted, n, c->id_base, (uint64_t *)(b + o_ids), (float *)(b + o_d), s));
+        if (out_ids && n) WVG_HIP(hipMemcpyAsync(out_ids + (size_t)qi * k, b + o_ids, n * 8, hipMemcpyDeviceToHost, s));
+        if (out_dists && n)
+            WVG_HIP(hipMemcpyAsync(out_dists + (size_t)qi * k, b + o_d, n * 4, hipMemcpyDeviceToHost, s));
+        WVG_HIP(hipStreamSynchronize(s));
+        for (uint64_t i = n; i < k; i++) {
+            if (out_ids) out_ids[(size_t)qi * k + i] = WVG_KEY_NONE;
+            if (out_dists) out_dists[(size_t)qi * k + i] = INFINITY;
+        }
+        if (out_counts) out_counts[qi] = (uint32_t)n;
+    }
+    return WVG_OK;
+}
+
+// Largest ordered key o in [ord(-inf), ord(+inf)] with pred(unord(o)), for a
+// predicate that is true up to some distance and false above it; 0 (below
+// every real key) if it holds nowhere.
+template <typename Pred>
+static uint32_t max_ord_where(Pred pred)
+{
+    uint32_t lo = wvg_ord_f32(-INFINITY), hi = wvg_ord_f32(INFINITY);
+    if (!pred(wvg_unord_f32(lo))) return 0u;
+    while (lo < hi) {
+        const uint32_t mid = lo + (hi - lo + 1) / 2;
+        if (pred(wvg_unord_f32(mid)))
+            lo = mid;
+        else
+            hi = mid - 1;
+    }
+    return lo;
+}
+
+// flat.searchByVectorBQ with a rescore window above 256: per query the
+// Hamming top-R by S1-S4, the exact rescore of those R rows, a sort, top-k.
+static int bq_rescore_large(wvg_corpus *bq, wvg_corpus *f32, const float *queries, uint32_t nq, uint32_t k,
+                            uint32_t R, const uint64_t *allow_bits, uint64_t allow_words, const SearchPlan &p,
+                            uint64_t *out_ids, float *out_dists, uint32_t *out_counts)
+{
+    SlotGuard g(bq->ctx);
+    int rc = bq->ctx->acquire(&g.slot);
+    if (rc) return rc;
+    const uint32_t fpitch = f32_chunks(bq->dim) * 4;
+    const uint64_t nslots = (p.te - p.tb) * 64;
+    Carver cv;
+    const size_t o_qb = cv.take(query_bytes(bq, nq));
+    const size_t o_qf = cv.take((size_t)nq * fpitch * 4);
+    const size_t o_allow = cv.take(allow_bits ? allow_words * 8 : 0);
+    size_t o_sel[6], temp_bytes = 0;
+    SelectBufs::layout(cv, nslots, o_sel, temp_bytes);
+    const size_t o_temp = cv.take(temp_bytes);
+    const size_t o_resc = cv.take((size_t)R * 8), o_rs = cv.take((size_t)R * 8);
+    const size_t o_ids = cv.take((size_t)k * 8), o_d = cv.take((size_t)k * 4);
+    void *base = nullptr;
+    rc = g.slot->device_scratch(cv.off, &base);
+    if (rc) return rc;
+    char *b = (char *)base;
+    hipStream_t s = g.slot->stream;
+    uint32_t qpb = 0, qpf = 0;
+    rc = stage_queries(bq, g.slot, queries, nq, b + o_qb, qpb, nullptr, nullptr);
+    if (rc) return rc;
+    rc = stage_queries(f32, g.slot, queries, nq, b + o_qf, qpf, nullptr, nullptr);
+    if (rc) return rc;
+    const uint64_t *d_allow = nullptr;
+    if (allow_bits) {
+        WVG_HIP(hipMemcpyAsync(b + o_allow, allow_bits, allow_words * 8, hipMemcpyHostToDevice, s));
+        d_allow = (const uint64_t *)(b + o_allow);
+    }
+    SelectBufs sb;
+    sb.bind(b, o_sel, o_temp, temp_bytes);
+    for (uint32_t qi = 0; qi < nq; qi++) {
+        ScanArgs a1 = scan_args_for(bq, b + o_qb + (size_t)qi * qpb * 8, qpb, 1, R, d_allow, allow_words, p.tb, p.te);
+        uint64_t n = 0;
+        rc = select_smallest(bq, a1, R, sb, s, &n);
+        if (rc) return rc;
+        // sb.sorted[0..n) = Hamming top-R keys (slot in the low 32 bits)
+        WVG_HIP(launch_rescore_keys(f32->metric, (const float *)(b + o_qf) + (size_t)qi * qpf, qpf,
+                                    (const float *)f32->d_data, f32->dim, f32->nchunks, sb.sorted, 1, (uint32_t)n,
+                                    (uint32_t)n, (uint64_t *)(b + o_resc), s));
+        WVG_HIP(sort_keys64(sb.temp, sb.temp_bytes, (uint64_t *)(b + o_resc), (uint64_t *)(b + o_rs), n, s));
+        const uint64_t kk = std::min<uint64_t>(k, n);
+        WVG_HIP(launch_emit_sorted((uint64_t *)(b + o_rs), kk, f32->id_base, (uint64_t *)(b + o_ids),
+                                   (float *)(b + o_d), s));
+        if (out_ids && kk) WVG_HIP(hipMemcpyAsync(out_ids + (size_t)qi * k, b + o_ids, kk * 8, hipMemcpyDeviceToHost, s));
+        if (out_dists && kk)
+            WVG_HIP(hipMemcpyAsync(out_dists + (size_t)qi * k, b + o_d, kk * 4, hipMemcpyDeviceToHost, s));
+        WVG_HIP(hipStreamSynchronize(s));
+        for (uint64_t i = kk; i < k; i++) {
+            if (out_ids) out_ids[(size_t)qi * k + i] = WVG_KEY_NONE;
+            if (out_dists) out_dists[(size_t)qi * k + i] = INFINITY;
+        }
+        if (out_counts) out_counts[qi] = (uint32_t)kk;
+    }
+    return WVG_OK;
+}
+
+// How many of the ascending results SearchByVectorDistance returns, given
+// p_le = #rows with dist <= target, p_q = #rows kept by the threshold test
+// (dist <= target || InDelta 1e-6), live = #rows.  Restates the growing-limit
+// loop: limits 100, 1100, 11100, ... (V/common/search_by_dist_params.go:14-83),
+// continue while the last row of the window is <= target, stop before a
+// limit above max_limit (V/hnsw/search.go:85-151, the loop flat's
+// V/flat/index.go:531-591 intends).
+uint64_t range_result_count(uint64_t p_le, uint64_t p_q, uint64_t live, int64_t max_limit)
+{
+    uint64_t offset = 0, limit = 100, total = 100, searched = 100;
+    for (;;) {
+        const uint64_t hi = std::min(total, live), lo = std::min(offset, live);
+        if (lo == hi) break;                  // empty window
+        if (!(hi - 1 < p_le)) break;          // last found > target
+        offset = total;
+        limit *= 10;
+        total = offset + limit;
+        if (max_limit >= 0 && (int64_t)total > max_limit) break;
+        searched = total;
+    }
+    return std::min(p_q, std::min(searched, live));
+}
+
+}  // namespace wvg
+
+extern "C" {
+
+int wvg_search_by_distance(wvg_corpus *c, const float *query, float target_distance, int64_t max_limit,
+                           const uint64_t *allow_bits, uint64_t allow_words, uint64_t *out_ids, float *out_dists,
+                           uint64_t out_capacity, uint64_t *out_count)
+{
+    int rc = check_corpus(c);
+    if (rc) return rc;
+    if (!query || !out_count) return fail(WVG_ERR_INVALID, "null argument");
+    if (c->kind == WVG_KIND_PQ && !c->d_centers) return fail(WVG_ERR_INVALID, "PQ corpus has no codebook");
+    *out_count = 0;
+    std::shared_lock<std::shared_mutex> lk(c->rw);
+    SearchPlan p = plan_search(c, 1, 1, allow_bits, allow_words);
+    if (p.empty) return WVG_OK;
+    SlotGuard g(c->ctx);
+    rc = c->ctx->acquire(&g.slot);
+    if (rc) return rc;
+    const uint64_t nslots = (p.te - p.tb) * 64;
+    Carver cv;
+    const size_t o_q = cv.take(query_bytes(c, 1));
+    const size_t o_qtmp = cv.take(c->kind == WVG_KIND_PQ ? (size_t)c->dim * 4 : 0);
+    const size_t o_allow = cv.take(allow_bits ? allow_words * 8 : 0);
+    size_t o_sel[6], temp_bytes = 0;
+    SelectBufs::layout(cv, nslots, o_sel, temp_bytes);
+    const size_t o_temp = cv.take(temp_bytes);
+    const size_t o_ids = cv.take(nslots * 8), o_d = cv.take(nslots * 4);
+    void *base = nullptr;
+    rc = g.slot->device_scratch(cv.off, &base);
+    if (rc) return rc;
+    char *b = (char *)base;
+    hipStream_t s = g.slot->stream;
+    uint32_t qpitch = 0;
+    rc = stage_queries(c, g.slot, query, 1, b + o_q, qpitch, (float *)(b + o_q), b + o_qtmp);
+    if (rc) return rc;
+    const uint64_t *d_allow = nullptr;
+    if (allow_bits) {
+        WVG_HIP(hipMemcpyAsync(b + o_allow, allow_bits, allow_words * 8, hipMemcpyHostToDevice, s));
+        d_allow = (const uint64_t *)(b + o_allow);
+    }
+    SelectBufs sb;
+    sb.bind(b, o_sel, o_temp, temp_bytes);
+    const int cus = c->ctx->num_cus;
+    ScanArgs a1 = scan_args_for(c, b + o_q, qpitch, 1, 1, d_allow, allow_words, p.tb, p.te);
+    WVG_HIP(launch_ordkeys(a1, c->kind, cus, sb.keys, s));
+    const float t = target_distance;
+    const uint32_t t_le = max_ord_where([t](float d) { return d <= t; });
+    const uint32_t t_q = max_ord_where([t](float d) {
+        return d <= t || std::fabs((double)d - (double)t) <= 1e-6;  // floatcomp.InDelta
+    });
+    WVG_HIP(launch_key_count(sb.keys, nslots, t_le, t_q, cus, sb.cnt, s));
+    unsigned long long cnt[3] = {0, 0, 0};
+    WVG_HIP(hipMemcpyAsync(cnt, sb.cnt, sizeof(cnt), hipMemcpyDeviceToHost, s));
+    WVG_HIP(hipStreamSynchronize(s));
+    const uint64_t R = range_result_count(cnt[0], cnt[1], cnt[2], max_limit);
+    *out_count = R;
+    if (R == 0) return WVG_OK;
+    uint64_t n = 0;
+    rc = compact_sort(sb, nslots, nullptr, t_q, (uint32_t)(p.tb * 64), cus, s, &n);
+    if (rc) return rc;
+    const uint64_t ncopy = std::min<uint64_t>(R, out_capacity);
+    if (ncopy == 0) return WVG_OK;
+    WVG_HIP(launch_emit_sorted(sb.sorted, ncopy, c->id_base, (uint64_t *)(b + o_ids), (float *)(b + o_d), s));
+    if (out_ids) WVG_HIP(hipMemcpyAsync(out_ids, b + o_ids, ncopy * 8, hipMemcpyDeviceToHost, s));
+    if (out_dists) WVG_HIP(hipMemcpyAsync(out_dists, b + o_d, ncopy * 4, hipMemcpyDeviceToHost, s));
+    WVG_HIP(hipStreamSynchronize(s));
+    return WVG_OK;
+}
+
 int wvg_search_bq_rescore(wvg_corpus *bq, wvg_corpus *f32, const float *queries, uint32_t nq, uint32_t k,
                           uint32_t rescore_limit, const uint64_t *allow_bits, uint64_t allow_words, uint64_t *out_ids,
                           float *out_dists, uint32_t *out_counts)
@@ -917,14 +1257,16 @@ int wvg_search_bq_rescore(wvg_corpus *bq, wvg_corpus *f32, const float *queries,
         return fail(WVG_ERR_INVALID, "BQ and F32 corpora disagree on dim/id_base/metric");
     if (nq > 0 && !queries) return fail(WVG_ERR_INVALID, "null queries");
     const uint32_t R = std::max(rescore_limit, k);  // searchTimeRescore (V/flat/index.go:297-305)
-    if (R > MAX_K) return fail(WVG_ERR_UNSUPPORTED, "rescore window above 256 is not supported by the fused top-k");
     std::shared_lock<std::shared_mutex> lk1(bq->rw);
     std::shared_lock<std::shared_mutex> lk2(f32->rw);
-    SearchPlan p = plan_search(bq, nq, R, allow_bits, allow_words);
+    SearchPlan p = plan_search(bq, nq, std::min(R, MAX_K), allow_bits, allow_words);
     if (p.empty || k == 0) {
         write_empty(nq, k, out_ids, out_dists, out_counts);
         return WVG_OK;
     }
+    if (R > MAX_K)
+        return bq_rescore_large(bq, f32, queries, nq, k, R, allow_bits, allow_words, p, out_ids, out_dists,
+                                out_counts);
     SlotGuard g(bq->ctx);
     rc = bq->ctx->acquire(&g.slot);
     if (rc) return rc;
@@ -1122,7 +1464,6 @@ int wvg_rescore(wvg_ctx *ctx, int metric, const float *q, const float *rows, con
 {
     if (!ctx || !q || (n && (!rows || !ids))) return fail(WVG_ERR_INVALID, "null argument");
     if (metric < WVG_METRIC_L2 || metric > WVG_METRIC_COSINE) return fail(WVG_ERR_INVALID, "unknown metric");
-    if (k > MAX_K) return fail(WVG_ERR_UNSUPPORTED, "k above 256 is not supported by the fused top-k");
     if (n > 0xFFFFFFFFull) return fail(WVG_ERR_INVALID, "too many rows");
     if (out_count) *out_count = 0;
     if (n == 0 || k == 0 || dim == 0) return WVG_OK;
@@ -1132,6 +1473,9 @@ int wvg_rescore(wvg_ctx *ctx, int metric, const float *q, const float *rows, con
     const size_t o_x = cv.take(n * dim * 4), o_t = cv.take(tiles_of(n) * 64 * (size_t)nch * 16),
                  o_q = cv.take((size_t)nch * 16), o_k = cv.take(n * 8), o_i = cv.take((size_t)k * 8),
                  o_d = cv.take((size_t)k * 4), o_c = cv.take(4);
+    const bool large = k > MAX_K;  // beyond the fused top-k: sort the n keys
+    const size_t temp_bytes = large ? sort_temp_bytes(n) : 0;
+    const size_t o_s = cv.take(large ? n * 8 : 0), o_tmp = cv.take(temp_bytes);
     Bulk bk(ctx);
     int rc = bk.begin(cv.off);
     if (rc) return rc;
@@ -1142,8 +1486,24 @@ int wvg_rescore(wvg_ctx *ctx, int metric, const float *q, const float *rows, con
     WVG_HIP(launch_f32_store((const float *)(bk.b + o_x), nullptr, n, dim, nch, 0, (float *)(bk.b + o_t), bk.s()));
     WVG_HIP(launch_dist_keys(metric, (const float *)(bk.b + o_q), (const float *)(bk.b + o_t), n, dim,
                              (uint64_t *)(bk.b + o_k), bk.s()));
-    WVG_HIP(launch_merge_keys((const uint64_t *)(bk.b + o_k), 1, (uint32_t)n, k, 0, (uint64_t *)(bk.b + o_i),
-                              (float *)(bk.b + o_d), (uint32_t *)(bk.b + o_c), bk.s()));
+    if (large) {
+        const uint32_t kk = (uint32_t)std::min<uint64_t>(k, n);
+        WVG_HIP(sort_keys64(bk.b + o_tmp, temp_bytes, (const uint64_t *)(bk.b + o_k), (uint64_t *)(bk.b + o_s), n,
+                            bk.s()));
+        WVG_HIP(launch_emit_sorted((const uint64_t *)(bk.b + o_s), kk, 0, (uint64_t *)(bk.b + o_i),
+                                   (float *)(bk.b + o_d), bk.s()));
+        std::vector<float> inf(k - kk, INFINITY);  // tail: no entry (KEY_NONE id, +inf)
+        WVG_HIP(hipMemcpyAsync(bk.b + o_c, &kk, 4, hipMemcpyHostToDevice, bk.s()));
+        if (kk < k) {
+            WVG_HIP(hipMemsetAsync(bk.b + o_i + (size_t)kk * 8, 0xFF, (size_t)(k - kk) * 8, bk.s()));
+            WVG_HIP(hipMemcpyAsync(bk.b + o_d + (size_t)kk * 4, inf.data(), inf.size() * 4, hipMemcpyHostToDevice,
+                                   bk.s()));
+        }
+        WVG_HIP(hipStreamSynchronize(bk.s()));  // the host sources above are stack buffers
+    } else {
+        WVG_HIP(launch_merge_keys((const uint64_t *)(bk.b + o_k), 1, (uint32_t)n, k, 0, (uint64_t *)(bk.b + o_i),
+                                  (float *)(bk.b + o_d), (uint32_t *)(bk.b + o_c), bk.s()));
+    }
     std::vector<uint64_t> idx(k);
     uint32_t cnt = 0;
     WVG_HIP(hipMemcpyAsync(idx.data(), bk.b + o_i, (size_t)k * 8, hipMemcpyDeviceToHost, bk.s()));

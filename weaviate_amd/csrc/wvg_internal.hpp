@@ -222,6 +222,24 @@ hipError_t launch_pq_store(const uint8_t *codes, const uint64_t *slots, uint64_t
                            uint32_t nchunks, uint8_t *tiled, hipStream_t s);
 hipError_t launch_pq_adc_rows(int metric, const float *lut, uint32_t m, uint32_t ks,
                               const uint8_t *codes, uint64_t n, float *out, hipStream_t s);
+// Unbounded selection (wvg_select.hip): S1 per-row ordered distance keys for
+// one prepared query over [tile_begin, tile_end); S2 radix select of the k-th
+// smallest key; S3 compaction of keys <= threshold into (key << 32 | slot);
+// S4 rocPRIM sort.
+hipError_t launch_ordkeys(const ScanArgs &a, int kind, int num_cus, uint32_t *keys, hipStream_t s);
+size_t select_state_bytes();
+hipError_t launch_select_kth(const uint32_t *keys, uint64_t n, uint64_t k, int num_cus, void *st_dev,
+                             uint32_t *hist, hipStream_t s);
+hipError_t launch_key_count(const uint32_t *keys, uint64_t n, uint32_t t_le, uint32_t t_q, int num_cus,
+                            unsigned long long *counts, hipStream_t s);
+hipError_t launch_key_compact(const uint32_t *keys, uint64_t n, const void *st_dev, uint32_t thr,
+                              uint32_t slot0, int num_cus, uint64_t *out, unsigned long long *count,
+                              hipStream_t s);
+size_t sort_temp_bytes(uint64_t n);
+hipError_t sort_keys64(void *temp, size_t temp_bytes, const uint64_t *in, uint64_t *out, uint64_t n,
+                       hipStream_t s);
+hipError_t launch_emit_sorted(const uint64_t *sorted, uint64_t n, uint64_t id_base, uint64_t *ids,
+                              float *dists, hipStream_t s);
 hipError_t launch_set_valid(uint64_t *valid, const uint64_t *slots, uint64_t n, int set,
                             hipStream_t s);
 

@@ -137,6 +137,23 @@ class Corpus:
                                   u64ptr(ids), fptr(dists), u32ptr(counts)))
         return ids, dists, counts
 
+    def search_by_distance(self, query, target: float, max_limit: int = -1, allow=None, capacity: int | None = None):
+        """wvg_search_by_distance: (ids, dists) of every row within `target`
+        (flat.SearchByVectorDistance, V/flat/index.go:531-591)."""
+        q = np.ascontiguousarray(query, dtype=np.float32).reshape(-1)
+        aw, an = (None, 0) if allow is None else (np.ascontiguousarray(allow, dtype=np.uint64), len(allow))
+        cnt = c_uint64()
+        cap = capacity if capacity is not None else max(1, self.info()[1])
+        while True:
+            ids = np.empty(cap, dtype=np.uint64)
+            dists = np.empty(cap, dtype=np.float32)
+            check(self.lib.wvg_search_by_distance(self.handle, fptr(q), float(target), int(max_limit),
+                                                  u64ptr(aw) if aw is not None else None, an, u64ptr(ids),
+                                                  fptr(dists), cap, byref(cnt)))
+            if cnt.value <= cap:
+                return ids[:cnt.value], dists[:cnt.value]
+            cap = cnt.value
+
 
 def search_bq_rescore(bq: Corpus, f32: Corpus, queries, k: int, rescore_limit: int, allow=None):
     q = np.ascontiguousarray(queries, dtype=np.float32)

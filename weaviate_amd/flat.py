@@ -110,22 +110,30 @@ class FlatIndex:
         return ids[0, :n], dists[0, :n]
 
     def SearchByVectorDistance(self, vector, target: float, max_limit: int, allow: AllowList | None = None):
-        """index.go:531-591: growing limits until a distance above target appears."""
+        """index.go:531-591: the rows the growing-limit loop (limits 100, 1100,
+        11100, ...) keeps -- dist <= target or within 1e-6 -- in one GPU pass
+        (wvg_search_by_distance; DESIGN.md section 4 on the loop's semantics)."""
+        if allow is not None and allow.IsEmpty():
+            return np.empty(0, dtype=np.uint64), np.empty(0, dtype=np.float32)
+        bm = allow.bitmap() if allow is not None else None
+        if self.bq is None:
+            return self.vectors.search_by_distance(vector, target, max_limit, bm)
+        # BQ: every window is a BQ search with rescoring (index.go:539 -> searchByVectorBQ),
+        # so the loop runs as written, each SearchByVector one GPU call (any k).
         offset, limit = 0, DEFAULT_SEARCH_BY_DIST_INITIAL_LIMIT
         total = offset + limit
         res_ids, res_d = [], []
         while True:
             ids, dist = self.SearchByVector(vector, total, allow)
-            cont = not (len(ids) < total)
             lo, hi = min(offset, len(ids)), min(total, len(ids))
             if lo == hi:
                 break
+            cont = bool(dist[hi - 1] <= target)
             for i in range(lo, hi):
                 if dist[i] <= target or abs(float(dist[i]) - float(target)) <= 1e-6:
                     res_ids.append(int(ids[i]))
                     res_d.append(float(dist[i]))
                 else:
-                    cont = False
                     break
             if not cont:
                 break
