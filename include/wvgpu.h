@@ -199,6 +199,29 @@ int wvg_pq_lut(wvg_ctx *ctx, int metric, const float *centers, uint32_t m, uint3
 int wvg_pq_adc_batch(wvg_ctx *ctx, int metric, const float *lut, uint32_t m, uint32_t ks,
                      const uint8_t *codes, uint64_t n, float *out);
 
+/* ProductQuantizer.Fit with the k-means encoder (CH/product_quantization.go:372-418):
+ * the first training_limit rows (0 = all) of X [n][dim]; per segment
+ * KMeans.Fit (CH/kmeans.go:220-250): ks initial centers drawn (with
+ * replacement) from the rows, Lloyd iterations -- nNearest assignment (ties to
+ * the highest index), empty clusters reseeded from a random row of a cluster
+ * with more than one member, centers = sequential fp32 sums / size -- until
+ * fewer than int(float32(n) * 0.01) rows change or after 11 passes.  The
+ * random draws come from a counter RNG keyed by (seed, segment) instead of
+ * Go's unseeded global math/rand.  out_centers: [m][ks][dim/m];
+ * out_iterations (nullable): [m] Lloyd passes per segment.  "not enough data
+ * to fit kmeans" if fewer than ks rows.                                    */
+int wvg_pq_fit(wvg_ctx *ctx, const float *X, uint64_t n, uint32_t dim, uint32_t m, uint32_t ks,
+               uint64_t training_limit, uint64_t seed, float *out_centers, uint32_t *out_iterations);
+/* buildGlobalDistances (CH/product_quantization.go:236-251): [m][ks][ks]
+ * table of Step(C_s[i], C_s[j]) (the symmetric-distance table of HNSW's
+ * node-to-node PQ distances). */
+int wvg_pq_global_distances(wvg_ctx *ctx, int metric, const float *centers, uint32_t m, uint32_t ks, uint32_t dim,
+                            float *out_table);
+/* DistanceBetweenCompressedVectors (CH/product_quantization.go:297-311) of
+ * code x against n codes [n][m], from the table above. */
+int wvg_pq_sdc_batch(wvg_ctx *ctx, int metric, const float *table, uint32_t m, uint32_t ks, const uint8_t *x,
+                     const uint8_t *codes, uint64_t n, float *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -375,6 +375,94 @@ ORC_API void orc_pq_encode(const float *x, long n, long d, const float *centers,
             codes[r * m + s] = (uint8_t)orc_kmeans_nearest(x + r * d + s * ds, centers + s * ks * ds, ks, ds);
 }
 
+/* The random draws of KMeans (rand.Intn(len(data)) at CH/kmeans.go:153,182).
+ * Go's global math/rand is unseeded and shared by the concurrently fitted
+ * segments, so the reference is not reproducible; both sides use this
+ * counter stream keyed by (seed, segment) instead
+ * (weaviate_amd/csrc/wvg_capi.hip kmeans_draw). */
+static uint64_t mix64(uint64_t z);
+static uint64_t orc_kmeans_draw(uint64_t seed, long s, uint64_t *ctr, uint64_t n)
+{
+    uint64_t h = mix64(mix64(seed + 0x632BE59BD9B4E019ull * (uint64_t)(s + 1)) + (*ctr)++);
+    return h % n;
+}
+
+/* KMeans.Fit for one segment: CH/kmeans.go:220-250, with initCenters :146-160,
+ * recluster :162-175, resortOnEmptySets :177-198, recalcCenters :200-213,
+ * stopCondition :215-219.  cc[] is kept as append-only member lists exactly
+ * like m.data.cc (a reseeded row stays in its old cluster's list).
+ * centers: [ks][ds] out.  Returns the number of loop passes. */
+static long orc_kmeans_fit_segment(const float *x, long n, long d, long seg, long ks, long ds, uint64_t seed,
+                                   float *centers)
+{
+    uint64_t ctr = 0;
+    for (long c = 0; c < ks; c++) { /* initCenters */
+        uint64_t r = orc_kmeans_draw(seed, seg, &ctr, (uint64_t)n);
+        memcpy(centers + c * ds, x + r * d + seg * ds, ds * sizeof(float));
+    }
+    uint64_t *points = calloc(n, sizeof(uint64_t));
+    long *cc_len = malloc(ks * sizeof(long));
+    long *cc_cap = malloc(ks * sizeof(long));
+    uint64_t **cc = malloc(ks * sizeof(uint64_t *));
+    for (long c = 0; c < ks; c++) { cc_cap[c] = 16; cc[c] = malloc(16 * sizeof(uint64_t)); }
+#define CC_APPEND(ci, v) do { if (cc_len[ci] == cc_cap[ci]) { cc_cap[ci] *= 2; \
+        cc[ci] = realloc(cc[ci], cc_cap[ci] * sizeof(uint64_t)); } cc[ci][cc_len[ci]++] = (v); } while (0)
+    long changes = 1, passes = 0;
+    for (long i = 0; changes > 0; i++) {
+        passes++;
+        changes = 0;
+        for (long c = 0; c < ks; c++) cc_len[c] = 0;
+        for (long p = 0; p < n; p++) { /* recluster */
+            uint64_t ci = orc_kmeans_nearest(x + p * d + seg * ds, centers, ks, ds);
+            CC_APPEND(ci, (uint64_t)p);
+            if (points[p] != ci) { points[p] = ci; changes++; }
+        }
+        for (long ci = 0; ci < ks; ci++) { /* resortOnEmptySets */
+            if (cc_len[ci] == 0) {
+                uint64_t ri;
+                for (;;) {
+                    ri = orc_kmeans_draw(seed, seg, &ctr, (uint64_t)n);
+                    if (cc_len[points[ri]] > 1) break;
+                }
+                CC_APPEND(ci, ri);
+                points[ri] = (uint64_t)ci;
+                changes = n;
+            }
+        }
+        if (changes > 0) { /* recalcCenters */
+            for (long c = 0; c < ks; c++) {
+                for (long j = 0; j < ds; j++) centers[c * ds + j] = 0.0f;
+                long size = cc_len[c];
+                for (long t = 0; t < size; t++) {
+                    const float *v = x + cc[c][t] * d + seg * ds;
+                    for (long j = 0; j < ds; j++) centers[c * ds + j] += v[j];
+                }
+                for (long j = 0; j < ds; j++) centers[c * ds + j] /= (float)size;
+            }
+        }
+        if (i >= 10 || changes < (long)((float)n * 0.01f)) break; /* stopCondition */
+    }
+#undef CC_APPEND
+    for (long c = 0; c < ks; c++) free(cc[c]);
+    free(cc); free(cc_len); free(cc_cap); free(points);
+    return passes;
+}
+
+/* ProductQuantizer.Fit, k-means encoder: CH/product_quantization.go:372-418
+ * (data truncated to trainingLimit; one KMeans per segment). */
+ORC_API long orc_pq_fit(const float *x, long n, long d, long m, long ks, long training_limit, uint64_t seed,
+                        float *centers, uint32_t *iterations)
+{
+    if (training_limit > 0 && n > training_limit) n = training_limit;
+    if (n < ks) return -1; /* "not enough data to fit kmeans" */
+    long ds = d / m;
+    for (long s = 0; s < m; s++) {
+        long it = orc_kmeans_fit_segment(x, n, d, s, ks, ds, seed, centers + s * ks * ds);
+        if (iterations) iterations[s] = (uint32_t)it;
+    }
+    return 0;
+}
+
 /* ------------------------------------------------------------------------ */
 /* Top-k: the reference's bounded max-heap                                   */
 /* ------------------------------------------------------------------------ */

@@ -55,6 +55,12 @@ def lib():
         l.orc_pq_adc.restype = c_float
         l.orc_pq_adc.argtypes = [c_int, _F, _U8, c_long, c_long]
         l.orc_pq_encode.argtypes = [_F, c_long, c_long, _F, c_long, c_long, _U8]
+        l.orc_pq_fit.restype = c_long
+        l.orc_pq_fit.argtypes = [_F, c_long, c_long, c_long, c_long, c_long, c_uint64, _F,
+                                 ctypes.POINTER(c_uint32)]
+        l.orc_pq_global_distances.argtypes = [c_int, _F, c_long, c_long, c_long, _F]
+        l.orc_pq_sdc.restype = c_float
+        l.orc_pq_sdc.argtypes = [c_int, _F, _U8, _U8, c_long, c_long]
         l.orc_kmeans_nearest.restype = c_uint32
         l.orc_kmeans_nearest.argtypes = [_F, _F, c_long, c_long]
         l.orc_heap_topk.restype = c_long
@@ -182,6 +188,35 @@ def pq_encode(X, centers):
     out = np.empty((n, m), dtype=np.uint8)
     lib().orc_pq_encode(_f(X), n, d, _f(centers), m, ks, _u8(out))
     return out
+
+
+def pq_fit(X, m, ks, training_limit=100_000, seed=0):
+    """ProductQuantizer.Fit (k-means) restated: CH/product_quantization.go:372-418,
+    CH/kmeans.go:146-250; returns (centers [m][ks][ds], passes per segment)."""
+    X = f32(X)
+    n, d = X.shape
+    centers = np.empty((m, ks, d // m), dtype=np.float32)
+    it = np.zeros(m, dtype=np.uint32)
+    rc = lib().orc_pq_fit(_f(X), n, d, m, ks, training_limit, seed, _f(centers),
+                          it.ctypes.data_as(ctypes.POINTER(c_uint32)))
+    if rc != 0:
+        raise ValueError("not enough data to fit kmeans")
+    return centers, it
+
+
+def pq_global_distances(metric, centers):
+    centers = f32(centers)
+    m, ks, ds = centers.shape
+    out = np.empty((m, ks, ks), dtype=np.float32)
+    lib().orc_pq_global_distances(metric, _f(centers), m, ks, ds, _f(out))
+    return out
+
+
+def pq_sdc(metric, table, x, y):
+    table = f32(table)
+    m, ks, _ = table.shape
+    return lib().orc_pq_sdc(metric, _f(table), _u8(np.ascontiguousarray(x, np.uint8)),
+                            _u8(np.ascontiguousarray(y, np.uint8)), m, ks)
 
 
 def heap_topk(dists, ids, k, valid=None):

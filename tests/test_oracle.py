@@ -147,3 +147,40 @@ def test_flat_search_oracle_with_reference_kernel(orc):
     a = orc.flat_search(rows, q, 10, orc.L2)
     b = orc.flat_search(rows, q, 10, orc.L2, use_ref_kernel=True)
     assert np.array_equal(a[0], b[0]) and np.array_equal(_bits(a[1]), _bits(b[1]))
+
+
+def test_oracle_kmeans_fit_properties():
+    """The k-means restatement (CH/kmeans.go:146-250): deterministic for a seed,
+    centers are means of their members (nearest-property pin, kmeans_test.go:26-53)."""
+    from oracle import wv_oracle as orc
+
+    X = np.array([[0, 5], [0.1, 4.9], [0.01, 5.1], [10.1, 7], [5.1, 2], [5.0, 2.1]], np.float32)
+    c1, it1 = orc.pq_fit(X, 1, 3, 0, 5)
+    c2, it2 = orc.pq_fit(X, 1, 3, 0, 5)
+    assert np.array_equal(c1, c2) and np.array_equal(it1, it2)
+    codes = orc.pq_encode(X, c1)[:, 0]
+    for v in range(len(X)):
+        mn = orc.l2_256(X[v], c1[0, codes[v]])
+        assert all(orc.l2_256(X[v], c1[0, c]) >= mn for c in codes)
+    # seed 3 starts in the three separated groups -> each center the mean of its group
+    c3, _ = orc.pq_fit(X, 1, 3, 0, 3)
+    got = np.array(sorted(map(tuple, c3[0].tolist())))
+    assert np.allclose(got, sorted([(0.11 / 3, 5.0), (5.05, 2.05), (10.1, 7.0)]), atol=1e-5)
+    with pytest.raises(ValueError):
+        orc.pq_fit(X, 1, 7, 0, 5)
+
+
+def test_oracle_search_by_distance_loop():
+    """The growing-limit loop restated from V/hnsw/search.go:85-151."""
+    from oracle import wv_oracle as orc
+
+    d = np.arange(5000, dtype=np.float32)
+    ids = np.arange(5000, dtype=np.uint64)
+    fn = lambda tot: (ids[:tot], d[:tot])  # noqa: E731
+    assert len(orc.search_by_distance(fn, 49.0, -1)[0]) == 50
+    assert len(orc.search_by_distance(fn, 99.0, -1)[0]) == 100     # window's last <= target: one more search
+    assert len(orc.search_by_distance(fn, 3000.0, -1)[0]) == 3001
+    assert len(orc.search_by_distance(fn, 3000.0, 1100)[0]) == 1100  # next limit 11100 > max_limit
+    assert len(orc.search_by_distance(fn, 3000.0, 50)[0]) == 100     # the first search always runs
+    assert len(orc.search_by_distance(fn, 1e9, -1)[0]) == 5000
+    assert len(orc.search_by_distance(fn, np.float32(10.0) - np.float32(5e-7), -1)[0]) == 11  # InDelta 1e-6

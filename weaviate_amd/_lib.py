@@ -72,6 +72,11 @@ SIGNATURES = {
     "wvg_pq_encode": (c_int, [c_void_p, _P(c_float), c_uint32, c_uint32, _P(c_float), c_uint64, c_uint32,
                               _P(c_uint8)]),
     "wvg_pq_lut": (c_int, [c_void_p, c_int, _P(c_float), c_uint32, c_uint32, c_uint32, _P(c_float), _P(c_float)]),
+    "wvg_pq_fit": (c_int, [c_void_p, _P(c_float), c_uint64, c_uint32, c_uint32, c_uint32, c_uint64, c_uint64,
+                           _P(c_float), _P(c_uint32)]),
+    "wvg_pq_global_distances": (c_int, [c_void_p, c_int, _P(c_float), c_uint32, c_uint32, c_uint32, _P(c_float)]),
+    "wvg_pq_sdc_batch": (c_int, [c_void_p, c_int, _P(c_float), c_uint32, c_uint32, _P(c_uint8), _P(c_uint8),
+                                 c_uint64, _P(c_float)]),
     "wvg_pq_adc_batch": (c_int, [c_void_p, c_int, _P(c_float), c_uint32, c_uint32, _P(c_uint8), c_uint64,
                                  _P(c_float)]),
 }

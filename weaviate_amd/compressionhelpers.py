@@ -6,16 +6,18 @@ Reference:
   KMeans.Encode        .../compressionhelpers/kmeans.go:103-135
   quantizer[T]         .../compressionhelpers/quantizer.go:21-31
 
-Codebook *training* (KMeans.Fit) is not on the device yet:
-``ProductQuantizer`` takes trained centers ([m][ks][ds] float32, the layout of
-KMeans.ExposeDataForRestore, kmeans.go:85-93).
+``ProductQuantizer`` is built from trained centers ([m][ks][ds] float32, the
+layout of KMeans.ExposeDataForRestore, kmeans.go:85-93) or trained on the GPU
+with :meth:`ProductQuantizer.fit` (KMeans.Fit per segment, kmeans.go:220-250).
 """
 from __future__ import annotations
 
 import numpy as np
 
 from . import _lib
-from ._lib import METRIC_BY_NAME, check, fptr, u8ptr, u64ptr
+from ._lib import METRIC_BY_NAME, check, fptr, u8ptr, u32ptr, u64ptr
+
+DEFAULT_TRAINING_LIMIT = 100_000  # DefaultPQTrainingLimit (entities/vectorindex/hnsw/pq_config.go)
 
 
 class BinaryQuantizer:
@@ -57,6 +59,59 @@ class ProductQuantizer:
         self.m, self.ks, self.ds = self.centers.shape
         self.dimensions = self.m * self.ds
         self.metric = METRIC_BY_NAME[distance]
+        self.fit_passes = None
+        self._global = None
+
+    @classmethod
+    def fit(cls, ctx, data, segments: int, centroids: int = 256, distance: str = "l2-squared",
+            training_limit: int = DEFAULT_TRAINING_LIMIT, seed: int = 0):
+        """NewProductQuantizer + Fit (CH/product_quantization.go:155-229, :372-418)
+        with the k-means encoder, trained on the GPU (wvg_pq_fit)."""
+        X = np.ascontiguousarray(data, dtype=np.float32)
+        n, d = X.shape
+        centers = np.empty((segments, centroids, d // segments if segments else 0), dtype=np.float32)
+        passes = np.zeros(segments, dtype=np.uint32)
+        check(ctx.lib.wvg_pq_fit(ctx.handle, fptr(X), n, d, segments, centroids, training_limit, seed,
+                                 fptr(centers), u32ptr(passes)))
+        pq = cls(ctx, centers, distance)
+        pq.fit_passes = passes
+        return pq
+
+    def globalDistances(self) -> np.ndarray:
+        """buildGlobalDistances (CH/product_quantization.go:236-251), [m][ks][ks]."""
+        if self._global is None:
+            out = np.empty((self.m, self.ks, self.ks), dtype=np.float32)
+            check(self.ctx.lib.wvg_pq_global_distances(self.ctx.handle, self.metric, fptr(self.centers), self.m,
+                                                       self.ks, self.dimensions, fptr(out)))
+            self._global = out
+        return self._global
+
+    def DistanceBetweenCompressedVectors(self, x, y):
+        """:297-311 -- (distance, error)."""
+        x = np.asarray(x, dtype=np.uint8)
+        y = np.asarray(y, dtype=np.uint8)
+        if x.shape[0] != self.m or y.shape[0] != self.m:
+            return 0.0, "inconsistent compressed vectors lengths"
+        return float(self.SDCBatch(x, y[None, :])[0]), None
+
+    def SDCBatch(self, x, codes) -> np.ndarray:
+        tab = self.globalDistances()
+        x = np.ascontiguousarray(x, dtype=np.uint8)
+        codes = np.ascontiguousarray(codes, dtype=np.uint8)
+        out = np.empty(codes.shape[0], dtype=np.float32)
+        check(self.ctx.lib.wvg_pq_sdc_batch(self.ctx.handle, self.metric, fptr(tab), self.m, self.ks, u8ptr(x),
+                                            u8ptr(codes), codes.shape[0], fptr(out)))
+        return out
+
+    def DistanceBetweenCompressedAndUncompressedVectors(self, x, code):
+        """:313-320: sum of Step(x_i, centroid_i[code_i]) in segment order == the
+        ADC lookup of the same code (the LUT holds those Step values)."""
+        return self.NewDistancer(x).Distance(code)[0], None
+
+    def Decode(self, code) -> np.ndarray:
+        """:428-434: concatenated centroids."""
+        code = np.asarray(code, dtype=np.uint8)
+        return np.concatenate([self.centers[i, code[i]] for i in range(self.m)])
 
     def Encode(self, vec) -> np.ndarray:
         return self.EncodeBatch(np.asarray(vec, dtype=np.float32)[None, :])[0]

@@ -361,3 +361,151 @@ hipError_t launch_pq_adc_rows(int metric, const float *lut, uint32_t m, uint32_t
 }
 
 }  // namespace wvg
+
+// ---------------------------------------------------------------------------
+// K10: k-means training (KMeans.Fit, CH/kmeans.go:220-250) -- every segment's
+// Lloyd loop of ProductQuantizer.Fit (CH/product_quantization.go:372-418) in
+// one set of launches per iteration; the host runs the loop control and the
+// rare empty-cluster reseed (kmeans.go:177-198).
+// ---------------------------------------------------------------------------
+namespace wvg {
+
+// recluster (kmeans.go:162-175): points[p][s] = nNearest(x_p, 1) for active
+// segments, counting changes against the previous assignment and cluster
+// sizes.  One thread per (row, segment); l2_256 order, ties -> highest index.
+__global__ void kmeans_assign_kernel(const float *X, uint64_t n, uint32_t dim, const float *centers, uint32_t m,
+                                     uint32_t ks, uint32_t ds, const uint8_t *active, uint8_t *points,
+                                     uint32_t *changes, uint32_t *counts)
+{
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n * m) return;
+    const uint64_t p = g / m;
+    const uint32_t s = (uint32_t)(g % m);
+    if (!active[s]) return;
+    const float *x = X + p * dim + (size_t)s * ds;
+    const float *cs = centers + (size_t)s * ks * ds;
+    uint32_t best = 0;
+    float minD = 3.40282346638528859812e+38f;  // math.MaxFloat32
+    auto xa = [&](int i) { return x[i]; };
+    for (uint32_t c = 0; c < ks; c++) {
+        const float *cv = cs + (size_t)c * ds;
+        auto ca = [&](int i) { return cv[i]; };
+        const float d = l2_256_acc(xa, ca, (int)ds);
+        if (!(minD < d)) {
+            minD = d;
+            best = c;
+        }
+    }
+    if (points[g] != best) {
+        points[g] = (uint8_t)best;
+        atomicAdd(&changes[s], 1u);
+    }
+    atomicAdd(&counts[(size_t)s * ks + best], 1u);
+}
+
+hipError_t launch_kmeans_assign(const float *X, uint64_t n, uint32_t dim, const float *centers, uint32_t m,
+                                uint32_t ks, uint32_t ds, const uint8_t *active, uint8_t *points, uint32_t *changes,
+                                uint32_t *counts, hipStream_t s)
+{
+    const uint64_t total = n * m;
+    if (total == 0) return hipSuccess;
+    hipLaunchKernelGGL(kmeans_assign_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, X, n, dim,
+                       centers, m, ks, ds, active, points, changes, counts);
+    return hipGetLastError();
+}
+
+// recalcCenters (kmeans.go:200-218): centers[s][c][j] = (0 + sum over the
+// members p of cluster c, in ascending p) / float32(size).  A workgroup owns
+// 256 (cluster, dim) outputs of one segment and streams the rows through LDS
+// in chunks of 256, each thread keeping its own sequential fp32 sum.
+// Clusters flagged in `skip` (reseeded on the host) are left untouched.
+constexpr int KM_CHUNK = 256;
+
+__global__ __launch_bounds__(256) void kmeans_recalc_kernel(const float *X, uint64_t n, uint32_t dim,
+                                                             const uint8_t *points, uint32_t m, uint32_t ks,
+                                                             uint32_t ds, const uint8_t *recalc, const uint32_t *counts,
+                                                             const uint8_t *skip, float *centers, uint32_t groups_per_seg,
+                                                             uint32_t chunk)
+{
+    extern __shared__ float xs[];  // [chunk][ds]
+    __shared__ uint8_t ps[KM_CHUNK];
+    const uint32_t s = blockIdx.x / groups_per_seg;
+    if (!recalc[s]) return;
+    const uint32_t o = (blockIdx.x % groups_per_seg) * 256 + threadIdx.x;  // output index within the segment
+    const bool live = o < ks * ds;
+    const uint32_t c = live ? o / ds : 0, j = live ? o % ds : 0;
+    float sum = 0.0f;
+    for (uint64_t p0 = 0; p0 < n; p0 += chunk) {
+        const uint32_t cnt = (uint32_t)min<uint64_t>(chunk, n - p0);
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < cnt; i += 256) ps[i] = points[(p0 + i) * m + s];
+        for (uint32_t i = threadIdx.x; i < cnt * ds; i += 256)
+            xs[i] = X[(p0 + i / ds) * dim + (size_t)s * ds + i % ds];
+        __syncthreads();
+        if (live)
+            for (uint32_t i = 0; i < cnt; i++)
+                if (ps[i] == c) sum = sum + xs[i * ds + j];
+    }
+    if (!live || skip[(size_t)s * ks + c]) return;
+    centers[((size_t)s * ks + c) * ds + j] = sum / (float)counts[(size_t)s * ks + c];
+}
+
+hipError_t launch_kmeans_recalc(const float *X, uint64_t n, uint32_t dim, const uint8_t *points, uint32_t m,
+                                uint32_t ks, uint32_t ds, const uint8_t *recalc, const uint32_t *counts,
+                                const uint8_t *skip, float *centers, hipStream_t s)
+{
+    const uint32_t gps = (ks * ds + 255) / 256;
+    const uint32_t chunk = std::max<uint32_t>(1, std::min<uint32_t>(KM_CHUNK, 16384 / ds));  // <= 64 KiB of rows
+    hipLaunchKernelGGL(kmeans_recalc_kernel, dim3(m * gps), dim3(256), (size_t)chunk * ds * 4, s, X, n, dim,
+                       points, m, ks, ds, recalc, counts, skip, centers, gps, chunk);
+    return hipGetLastError();
+}
+
+// buildGlobalDistances (CH/product_quantization.go:236-251): table[s][i][j] =
+// Step(C_s[i], C_s[j]) for j <= i, mirrored.
+__global__ void pq_sdc_table_kernel(int metric, const float *centers, uint32_t m, uint32_t ks, uint32_t ds,
+                                    float *table)
+{
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= (uint64_t)m * ks * ks) return;
+    const uint32_t s = (uint32_t)(g / ((uint64_t)ks * ks));
+    const uint32_t r = (uint32_t)(g % ((uint64_t)ks * ks));
+    const uint32_t i = r / ks, j = r % ks;
+    const uint32_t hi = i > j ? i : j, lo = i > j ? j : i;
+    const float *cs = centers + (size_t)s * ks * ds;
+    table[g] = go_step(metric, cs + (size_t)hi * ds, cs + (size_t)lo * ds, ds);
+}
+
+hipError_t launch_pq_sdc_table(int metric, const float *centers, uint32_t m, uint32_t ks, uint32_t ds, float *table,
+                               hipStream_t s)
+{
+    const uint64_t total = (uint64_t)m * ks * ks;
+    if (total == 0) return hipSuccess;
+    hipLaunchKernelGGL(pq_sdc_table_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, metric, centers,
+                       m, ks, ds, table);
+    return hipGetLastError();
+}
+
+// DistanceBetweenCompressedVectors (CH/product_quantization.go:297-311):
+// sequential sum of table[i][x_i][y_i], then Wrap.
+__global__ void pq_sdc_rows_kernel(int metric, const float *table, uint32_t m, uint32_t ks, const uint8_t *x,
+                                   const uint8_t *codes, uint64_t n, float *out)
+{
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const uint8_t *y = codes + r * m;
+    float dist = 0.0f;
+    for (uint32_t i = 0; i < m; i++) dist = dist + table[((size_t)i * ks + x[i]) * ks + y[i]];
+    out[r] = wrap_metric(metric, dist);
+}
+
+hipError_t launch_pq_sdc_rows(int metric, const float *table, uint32_t m, uint32_t ks, const uint8_t *x,
+                              const uint8_t *codes, uint64_t n, float *out, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(pq_sdc_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, metric, table, m, ks,
+                       x, codes, n, out);
+    return hipGetLastError();
+}
+
+}  // namespace wvg
