@@ -77,10 +77,25 @@ int wvg_corpus_info(wvg_corpus *c, uint64_t *count, uint64_t *high_water, uint64
  * the codebook (CH/product_quantization.go:420).  vectors: [n][dim] float32. */
 int wvg_corpus_upsert(wvg_corpus *c, const uint64_t *ids, const float *vectors, uint64_t n,
                       uint32_t dim);
-/* Load already-encoded rows (restart from the "vectors_compressed" bucket,
- * V/flat/index.go:640-681): BQ = [n][ceil(dim/64)] uint64 LE words,
+/* Load already-stored rows (restart from the "vectors" / "vectors_compressed"
+ * buckets, V/flat/index.go:640-681): F32 = [n][dim] float32 (already
+ * normalized at Add for cosine), BQ = [n][ceil(dim/64)] uint64 LE words,
  * PQ = [n][m] bytes.  Stored as given (no normalization / encoding). */
 int wvg_corpus_upsert_codes(wvg_corpus *c, const uint64_t *ids, const void *codes, uint64_t n);
+/* Restart / PostStartup bulk load from an LSM cursor (V/flat/index.go:640-681):
+ * keys [n][8] big-endian docIDs, values [n][value_bytes] little-endian rows as
+ * the "vectors" (F32: dim float32) or "vectors_compressed" (BQ: uint64 words)
+ * bucket stores them, or PQ codes (m bytes).  Stored as given; the capacity
+ * grows to the largest id (bqCache.Grow(maxID)).                           */
+int wvg_corpus_load_kv(wvg_corpus *c, const uint8_t *keys, const uint8_t *values, uint64_t n,
+                       uint64_t value_bytes);
+/* Batched Distance / CompressorDistancer.DistanceToNode(id) (CH/compression.go:306-325,
+ * the HNSW rescore loop V/hnsw/search.go:564-581): the query's distance to
+ * the rows with docIDs ids[n] (F32: SingleDist, BQ: Hamming, PQ: ADC);
+ * out_ok[i] = 0 (and out_dists[i] = 0) where the id is not live, like the
+ * reference's ok=false for deleted nodes.                                  */
+int wvg_corpus_distance_by_ids(wvg_corpus *c, const float *query, const uint64_t *ids, uint64_t n,
+                               float *out_dists, uint8_t *out_ok);
 /* flat.Delete (V/flat/index.go:276-295): clears the validity bit. */
 int wvg_corpus_delete(wvg_corpus *c, const uint64_t *ids, uint64_t n);
 /* flat.vectorById (V/flat/index.go:401-407): copies the stored row

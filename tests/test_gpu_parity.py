@@ -163,10 +163,9 @@ def test_delete_allow_list_and_edge_cases(ctx, orc):
     ids, dists, counts = small.search(q, 50)
     assert counts[0] == 7
     check_topk(orc, ids[0], dists[0], counts[0], orc.dist_all(0, q, rows[:7]), np.arange(7, dtype=np.uint64), 50)
-    # k above the fused limit is reported, not silently wrong
-    with pytest.raises(_lib.WvgError) as e:
-        c.search(q, 257)
-    assert e.value.code == _lib.WVG_ERR_UNSUPPORTED
+    # k above the fused register top-k runs the select path with the same result rule
+    ids, dists, counts = c.search(q, 257)
+    check_topk(orc, ids[0], dists[0], counts[0], all_d, all_ids, 257, valid)
     # dimension mismatch on insert
     with pytest.raises(_lib.WvgError) as e:
         c.upsert(np.array([1], np.uint64), np.zeros((1, d + 1), np.float32))

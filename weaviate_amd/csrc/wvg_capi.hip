@@ -84,6 +84,17 @@ size_t corpus_row_bytes(int kind, uint32_t dim, uint32_t pq_m)
     }
 }
 
+// Bytes of one row as the caller hands it over (and as the LSM buckets store
+// it): F32 dim float32, BQ ceil(dim/64) uint64 words, PQ m code bytes.
+static size_t host_row_bytes(const wvg_corpus *c)
+{
+    switch (c->kind) {
+    case WVG_KIND_F32: return (size_t)c->dim * 4;
+    case WVG_KIND_BQ: return (size_t)bq_words(c->dim) * 8;
+    default: return c->pq_m;
+    }
+}
+
 static uint32_t corpus_nchunks(const wvg_corpus *c)
 {
     switch (c->kind) {
@@ -548,7 +559,6 @@ int wvg_corpus_upsert_codes(wvg_corpus *c, const uint64_t *ids, const void *code
     if (rc) return rc;
     if (n == 0) return WVG_OK;
     if (!ids || !codes) return fail(WVG_ERR_INVALID, "null ids/codes");
-    if (c->kind == WVG_KIND_F32) return fail(WVG_ERR_UNSUPPORTED, "upsert_codes needs a BQ or PQ corpus");
     if (c->kind == WVG_KIND_PQ && !c->d_centers) return fail(WVG_ERR_INVALID, "PQ corpus has no codebook");
     std::unique_lock<std::shared_mutex> lk(c->rw);
     std::vector<uint64_t> rows, slots;
@@ -557,7 +567,7 @@ int wvg_corpus_upsert_codes(wvg_corpus *c, const uint64_t *ids, const void *code
     SlotGuard g(c->ctx);
     rc = c->ctx->acquire(&g.slot);
     if (rc) return rc;
-    const size_t rb = c->kind == WVG_KIND_BQ ? (size_t)bq_words(c->dim) * 8 : c->pq_m;
+    const size_t rb = host_row_bytes(c);
     const uint64_t nr = rows.size();
     Carver cv;
     const size_t o_codes = cv.take(nr * rb), o_slots = cv.take(nr * 8);
@@ -570,7 +580,10 @@ int wvg_corpus_upsert_codes(wvg_corpus *c, const uint64_t *ids, const void *code
     char *b = (char *)base;
     WVG_HIP(hipMemcpyAsync(b + o_codes, hc.data(), nr * rb, hipMemcpyHostToDevice, s));
     WVG_HIP(hipMemcpyAsync(b + o_slots, slots.data(), nr * 8, hipMemcpyHostToDevice, s));
-    if (c->kind == WVG_KIND_BQ)
+    if (c->kind == WVG_KIND_F32)  // stored rows: already normalized at Add, kept bit for bit
+        WVG_HIP(launch_f32_store((const float *)(b + o_codes), (uint64_t *)(b + o_slots), nr, c->dim, c->nchunks, 0,
+                                 (float *)c->d_data, s));
+    else if (c->kind == WVG_KIND_BQ)
         WVG_HIP(launch_bq_store((uint64_t *)(b + o_codes), (uint64_t *)(b + o_slots), nr, bq_words(c->dim), c->nchunks,
                                 (uint64_t *)c->d_data, s));
     else
@@ -1938,6 +1951,69 @@ int wvg_pq_sdc_batch(wvg_ctx *ctx, int metric, const float *table, uint32_t m, u
     WVG_HIP(hipMemcpyAsync(out, bk.b + o_o, n * 4, hipMemcpyDeviceToHost, bk.s()));
     WVG_HIP(hipStreamSynchronize(bk.s()));
     return WVG_OK;
+}
+
+int wvg_corpus_distance_by_ids(wvg_corpus *c, const float *query, const uint64_t *ids, uint64_t n, float *out_dists,
+                               uint8_t *out_ok)
+{
+    int rc = check_corpus(c);
+    if (rc) return rc;
+    if (!query || (n && (!ids || !out_dists || !out_ok))) return fail(WVG_ERR_INVALID, "null argument");
+    if (c->kind == WVG_KIND_PQ && !c->d_centers) return fail(WVG_ERR_INVALID, "PQ corpus has no codebook");
+    if (n == 0) return WVG_OK;
+    std::shared_lock<std::shared_mutex> lk(c->rw);
+    SlotGuard g(c->ctx);
+    rc = c->ctx->acquire(&g.slot);
+    if (rc) return rc;
+    Carver cv;
+    const size_t o_q = cv.take(query_bytes(c, 1));
+    const size_t o_qtmp = cv.take(c->kind == WVG_KIND_PQ ? (size_t)c->dim * 4 : 0);
+    const size_t o_ids = cv.take(n * 8), o_d = cv.take(n * 4), o_ok = cv.take(n);
+    void *base = nullptr;
+    rc = g.slot->device_scratch(cv.off, &base);
+    if (rc) return rc;
+    char *b = (char *)base;
+    hipStream_t s = g.slot->stream;
+    uint32_t qpitch = 0;
+    rc = stage_queries(c, g.slot, query, 1, b + o_q, qpitch, (float *)(b + o_q), b + o_qtmp);
+    if (rc) return rc;
+    WVG_HIP(hipMemcpyAsync(b + o_ids, ids, n * 8, hipMemcpyHostToDevice, s));
+    ScanArgs a = scan_args_for(c, b + o_q, qpitch, 1, 1, nullptr, 0, 0, tiles_of(c->high_water));
+    WVG_HIP(launch_dist_by_ids(a, c->kind, c->capacity, (const uint64_t *)(b + o_ids), n, (float *)(b + o_d),
+                               (uint8_t *)(b + o_ok), s));
+    WVG_HIP(hipMemcpyAsync(out_dists, b + o_d, n * 4, hipMemcpyDeviceToHost, s));
+    WVG_HIP(hipMemcpyAsync(out_ok, b + o_ok, n, hipMemcpyDeviceToHost, s));
+    WVG_HIP(hipStreamSynchronize(s));
+    return WVG_OK;
+}
+
+int wvg_corpus_load_kv(wvg_corpus *c, const uint8_t *keys, const uint8_t *values, uint64_t n, uint64_t value_bytes)
+{
+    int rc = check_corpus(c);
+    if (rc) return rc;
+    if (n == 0) return WVG_OK;
+    if (!keys || !values) return fail(WVG_ERR_INVALID, "null keys/values");
+    if (c->kind == WVG_KIND_PQ && !c->d_centers) return fail(WVG_ERR_INVALID, "PQ corpus has no codebook");
+    if (value_bytes != host_row_bytes(c))
+        return fail(WVG_ERR_DIM_MISMATCH, "vector lengths don't match: " + std::to_string(value_bytes) + " vs " +
+                                              std::to_string(host_row_bytes(c)) + " bytes");
+    // keys: 8-byte big-endian docIDs (binary.BigEndian.PutUint64, V/flat/index.go:218-224)
+    std::vector<uint64_t> ids(n);
+    uint64_t max_id = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        uint64_t v = 0;
+        for (int j = 0; j < 8; j++) v = (v << 8) | keys[i * 8 + j];
+        ids[i] = v;
+        max_id = std::max(max_id, v);
+    }
+    if (max_id < c->id_base) return fail(WVG_ERR_CAPACITY, "id below the corpus id_base");
+    if (max_id - c->id_base >= c->capacity) {  // bqCache.Grow(maxID) (V/flat/index.go:671)
+        rc = wvg_corpus_reserve(c, max_id - c->id_base + 1);
+        if (rc) return rc;
+    }
+    // values: little-endian payloads (binary.LittleEndian, index.go:226-245) == the
+    // host layout on little-endian machines, so they load as stored rows
+    return wvg_corpus_upsert_codes(c, ids.data(), values, n);
 }
 
 }  // extern "C"

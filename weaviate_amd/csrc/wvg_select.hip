@@ -344,3 +344,77 @@ hipError_t launch_emit_sorted(const uint64_t *sorted, uint64_t n, uint64_t id_ba
 }
 
 }  // namespace wvg
+
+// ---------------------------------------------------------------------------
+// Distances of one prepared query to corpus rows named by docID: the batched
+// form of distancer.Distance / CompressorDistancer.DistanceToNode(id)
+// (CH/compression.go:306-325) that HNSW's rescore loop
+// (V/hnsw/search.go:564-581) and filtered flat search issue one id at a time.
+// One thread per id (a gather); ok[i] = 0 for ids that are not live.
+// ---------------------------------------------------------------------------
+namespace wvg {
+
+template <int KIND, int METRIC>
+__global__ void dist_by_ids_kernel(ScanArgs a, uint64_t capacity, const uint64_t *ids, uint64_t n, float *out,
+                                   uint8_t *ok)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t id = ids[i];
+    const uint64_t slot = id - a.id_base;
+    const bool live = id >= a.id_base && slot < capacity && ((a.valid[slot >> 6] >> (slot & 63)) & 1ull);
+    float d = 0.0f;
+    if (live) {
+        const uint64_t t = slot >> 6, lane = slot & 63;
+        if constexpr (KIND == WVG_KIND_F32) {
+            const float4 *rp = reinterpret_cast<const float4 *>(a.data) + (size_t)t * a.nchunks * 64 + lane;
+            d = wrap_metric(a.metric, row_dot_or_l2_generic<METRIC, 64>(rp, reinterpret_cast<const float4 *>(a.queries),
+                                                                        (int)a.dim));
+        } else if constexpr (KIND == WVG_KIND_BQ) {
+            const ulonglong2 *rp = reinterpret_cast<const ulonglong2 *>(a.data) + (size_t)t * a.nchunks * 64 + lane;
+            const uint64_t *q = reinterpret_cast<const uint64_t *>(a.queries);
+            uint32_t tot = 0;
+            for (uint32_t c = 0; c < a.nchunks; c++) {
+                const ulonglong2 x = rp[(size_t)c * 64];
+                tot += (uint32_t)__popcll(x.x ^ q[2 * c]) + (uint32_t)__popcll(x.y ^ q[2 * c + 1]);
+            }
+            d = (float)tot;
+        } else {
+            const uint4 *rp = reinterpret_cast<const uint4 *>(a.data) + (size_t)t * a.nchunks * 64 + lane;
+            const float *lut = reinterpret_cast<const float *>(a.queries);
+            float sum = 0.0f;
+            for (uint32_t c = 0; c < a.nchunks; c++) {
+                const uint4 x = rp[(size_t)c * 64];
+                const uint32_t ws[4] = {x.x, x.y, x.z, x.w};
+                for (uint32_t b = 0; b < 16; b++) {
+                    const uint32_t s = c * 16 + b;
+                    if (s < a.pq_m) sum = sum + lut[s * a.pq_ks + ((ws[b >> 2] >> (8 * (b & 3))) & 0xFFu)];
+                }
+            }
+            d = wrap_metric(a.metric, sum);
+        }
+    }
+    out[i] = d;
+    ok[i] = live ? 1 : 0;
+}
+
+hipError_t launch_dist_by_ids(const ScanArgs &a, int kind, uint64_t capacity, const uint64_t *ids, uint64_t n,
+                              float *out, uint8_t *ok, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    dim3 grid((unsigned)((n + 255) / 256)), block(256);
+    if (kind == WVG_KIND_F32) {
+        if (a.metric == WVG_M_L2)
+            hipLaunchKernelGGL((dist_by_ids_kernel<WVG_KIND_F32, WVG_M_L2>), grid, block, 0, s, a, capacity, ids, n, out, ok);
+        else
+            hipLaunchKernelGGL((dist_by_ids_kernel<WVG_KIND_F32, WVG_M_DOT>), grid, block, 0, s, a, capacity, ids, n, out,
+                               ok);
+    } else if (kind == WVG_KIND_BQ) {
+        hipLaunchKernelGGL((dist_by_ids_kernel<WVG_KIND_BQ, 0>), grid, block, 0, s, a, capacity, ids, n, out, ok);
+    } else {
+        hipLaunchKernelGGL((dist_by_ids_kernel<WVG_KIND_PQ, 0>), grid, block, 0, s, a, capacity, ids, n, out, ok);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace wvg

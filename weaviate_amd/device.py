@@ -101,6 +101,24 @@ class Corpus:
         codes = np.ascontiguousarray(codes)
         check(self.lib.wvg_corpus_upsert_codes(self.handle, u64ptr(ids), codes.ctypes.data_as(c_void_p), len(ids)))
 
+    def load_kv(self, keys, values) -> None:
+        """wvg_corpus_load_kv: an LSM cursor's (8-byte big-endian key, LE row) pairs."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1, 8)
+        values = np.ascontiguousarray(values, dtype=np.uint8).reshape(len(keys), -1)
+        check(self.lib.wvg_corpus_load_kv(self.handle, keys.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+                                          values.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), len(keys),
+                                          values.shape[1]))
+
+    def distance_by_ids(self, query, ids):
+        """wvg_corpus_distance_by_ids: (dists, ok) of the query to the rows with these docIDs."""
+        q = np.ascontiguousarray(query, dtype=np.float32).reshape(-1)
+        ids = np.ascontiguousarray(ids, dtype=np.uint64)
+        out = np.empty(len(ids), dtype=np.float32)
+        ok = np.empty(len(ids), dtype=np.uint8)
+        check(self.lib.wvg_corpus_distance_by_ids(self.handle, fptr(q), u64ptr(ids), len(ids), fptr(out),
+                                                  ok.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
+        return out, ok.astype(bool)
+
     def delete(self, ids) -> None:
         ids = np.ascontiguousarray(ids, dtype=np.uint64)
         check(self.lib.wvg_corpus_delete(self.handle, u64ptr(ids), len(ids)))

@@ -83,6 +83,19 @@ class FlatIndex:
         if self.bq is not None:
             self.bq.upsert(ids, vectors)
 
+    def PostStartup(self, vectors_bucket=None, compressed_bucket=None) -> None:
+        """index.go:640-681: rebuild the device corpora from the LSM buckets --
+        iterables of (8-byte big-endian key, little-endian value bytes)."""
+        for corpus, bucket in ((self.vectors, vectors_bucket), (self.bq, compressed_bucket)):
+            if corpus is None or bucket is None:
+                continue
+            kv = list(bucket)
+            if not kv:
+                continue
+            keys = np.frombuffer(b"".join(k for k, _ in kv), dtype=np.uint8)
+            vals = np.frombuffer(b"".join(v for _, v in kv), dtype=np.uint8)
+            corpus.load_kv(keys, vals)
+
     def Delete(self, *ids) -> None:
         ids = np.asarray(ids, dtype=np.uint64)
         self.vectors.delete(ids)
