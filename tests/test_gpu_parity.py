@@ -558,3 +558,42 @@ def test_full_size_1m_x_128_properties(ctx, orc):
         kth = (int(orc.ord_key(dists[qi][-1:])[0]), int(ids[qi][-1]))
         sk = orc.ord_key(sd[outside]).astype(np.int64)
         assert np.all((sk > kth[0]) | ((sk == kth[0]) & (sample[outside] > kth[1])))
+
+
+@pytest.mark.parametrize("variant", [0, 2, 1])
+@pytest.mark.parametrize("metric,d", [(METRIC_COSINE, 768), (METRIC_DOT, 256), (METRIC_COSINE, 1536), (METRIC_DOT, 512)])
+def test_batched_mfma_variants(ctx, orc, variant, metric, d):
+    """K3b (queries resident in LDS, rows streamed into MFMA operands; 0: two
+    query tiles per wave, 2: two waves per SIMD) and K3 (1) against the oracle:
+    ragged rows, deletes, an allow list, partial query blocks, SIFT-like ties."""
+    import ctypes
+
+    lib = _lib.load()
+    lib.wvgx_set_tuning.restype = ctypes.c_int
+    lib.wvgx_set_tuning.argtypes = [ctypes.c_int, ctypes.c_int]
+    old = lib.wvgx_set_tuning(4, variant)
+    try:
+        n, nq = 4000 + 45, 70
+        rows = orc.synth_rows(700 + d, 0, n, d, 0)
+        qs = orc.synth_rows(701 + d, 0, nq, d, 0)
+        if metric == METRIC_DOT:  # integer values: exact dots and many ties
+            rows = np.floor(rows * 3).astype(np.float32)
+            qs = np.floor(qs * 3).astype(np.float32)
+        c = Corpus(ctx, KIND_F32, metric, d, n)
+        c.upsert(np.arange(n, dtype=np.uint64), rows)
+        srows = stored_rows(orc, metric, rows)
+        valid = np.ones(n, np.uint8)
+        dead = [0, 63, 64, 1000, 4044]
+        c.delete(np.array(dead, np.uint64))
+        valid[dead] = 0
+        allowed = np.arange(5, 3900, 2, dtype=np.uint64)
+        am = np.zeros(n, np.uint8)
+        am[allowed.astype(np.int64)] = 1
+        for k, allow in [(1, None), (10, None), (64, None), (10, allowed), (100, None)]:
+            ids, dists, counts = c.search(qs, k, None if allow is None else allow_bitmap(allow))
+            vm = valid if allow is None else valid & am
+            for qi in range(0, nq, 3):
+                all_d = orc.dist_all(ORC_METRIC[metric], prep_query(orc, metric, qs[qi]), srows)
+                check_topk(orc, ids[qi], dists[qi], counts[qi], all_d, np.arange(n, dtype=np.uint64), k, vm)
+    finally:
+        lib.wvgx_set_tuning(4, old)

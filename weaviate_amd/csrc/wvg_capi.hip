@@ -819,7 +819,7 @@ static SearchPlan plan_search(wvg_corpus *c, uint32_t nq, uint32_t k, const uint
     const uint32_t mn = c->ctx->mfma_min_nq;
     p.gemm = c->kind == WVG_KIND_F32 && mn > 0 && nq >= mn && gemm_supported(c->dim, c->metric);
     if (p.gemm)
-        p.groups = (int)gemm_row_ranges(nq, std::max<uint64_t>(1, p.te - p.tb), c->ctx->num_cus);
+        p.groups = (int)gemm_row_ranges(nq, std::max<uint64_t>(1, p.te - p.tb), c->ctx->num_cus, c->dim, k);
     else
         p.groups = scan_groups_for(a, c->ctx->num_cus);
     return p;
@@ -1597,6 +1597,9 @@ int wvgx_set_tuning(int key, int value)
     } else if (key == 3) {
         old = t.gemm_pf;
         t.gemm_pf = value;
+    } else if (key == 4) {
+        old = t.gemm_kernel;
+        t.gemm_kernel = value;
     }
     return old;
 }

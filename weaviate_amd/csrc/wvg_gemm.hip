@@ -286,11 +286,266 @@ __global__ __launch_bounds__(GWAVES * 64) void gemm_topk_kernel(GemmArgs a, uint
     }
 }
 
+// ---------------------------------------------------------------------------
+// K3b: the same contraction with the QUERIES resident and the ROWS streamed
+// straight into MFMA operand registers.  A workgroup = 4 waves (one per SIMD,
+// 512-register budget) and QB = 16*QT queries held in LDS for the whole
+// launch; wave w scores rows 16w..16w+15 of every 64-row tile of the
+// workgroup's row range against all QB queries (QT 16x16 output tiles
+// sharing one B operand).  No workgroup barrier in the main loop: each wave
+// streams its own rows (B: lane (kk, j) loads the 128 contiguous bytes of
+// block 4g+kk of row j, 8 x 16-byte loads per K step, double-buffered in
+// registers one K step ahead), reads the query operands from LDS (XOR-
+// swizzled so every ds_read_b128 is conflict-free) and keeps a per-query
+// top-k list in LDS that a candidate enters only if it beats the list's
+// current k-th key (a rare wave-uniform insertion).  The four waves' lists
+// are merged by rank at the end.  Same slice accumulators and AVX2 reduction
+// tree as K3, so the distances are the same bits.
+// ---------------------------------------------------------------------------
+constexpr int RS_RG = 4;  // row groups of 16 per 64-row tile
+
+// QH query halves x 4 row groups = 4*QH waves; wave (qg, rg) scores rows
+// 16*rg..16*rg+15 of every tile against queries qg*16*QT .. +16*QT.
+template <int D, int QT, int QH, int NBUF>
+__global__ __launch_bounds__(RS_RG * QH * 64, 1) void gemm_rs_kernel(GemmArgs a, uint64_t *partials)
+{
+    constexpr int NW = RS_RG * QH;    // waves per workgroup
+    constexpr int NB = D / 32;        // 32-float blocks per row
+    constexpr int NK = NB / 4;        // K steps of 4 blocks (D % 128 == 0)
+    static_assert(NB % 4 == 0 && NK % NBUF == 0 && NBUF >= 2, "K3b: the B ring must divide the K steps");
+    constexpr int QW = 16 * QT;       // queries per wave
+    constexpr int QB = QW * QH;       // queries per workgroup
+    constexpr int QROW = NB * 8;      // float4 per query row in LDS
+    extern __shared__ __attribute__((aligned(16))) float4 smem4[];
+    float4 *qs = smem4;                                                  // [QB][QROW]
+    const int K = (int)a.k;
+    uint64_t *lists = reinterpret_cast<uint64_t *>(smem4 + QB * QROW);  // [NW][QW][K]
+    uint64_t *thr = lists + NW * QW * K;                                 // [NW][QW]
+    uint64_t *tmp = thr + NW * QW;                                       // [NW][64]
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int rg = wave % RS_RG, qg = wave / RS_RG;
+    const uint32_t b = blockIdx.x;
+    uint32_t qb, rr;
+    if (a.nrr % 8 == 0) {  // the query blocks of one row range share an XCD (blocks b, b+8, ...)
+        const uint32_t xcd = b % 8, w = b / 8;
+        qb = w % a.nqb;
+        rr = (w / a.nqb) * 8 + xcd;
+    } else {
+        qb = b % a.nqb;
+        rr = b / a.nqb;
+    }
+    const uint64_t ntiles = a.tile_end - a.tile_begin;
+    const uint64_t t0 = a.tile_begin + ntiles * rr / a.nrr, t1 = a.tile_begin + ntiles * (rr + 1) / a.nrr;
+    const uint32_t q0 = qb * QB;
+
+    // queries -> LDS: chunk cc of block bk of query i at i*QROW + bk*8 + (cc ^ (i & 7))
+    for (int idx = tid; idx < QB * NB * 8; idx += NW * 64) {
+        const int i = idx / (NB * 8), rem = idx % (NB * 8), bk = rem >> 3, cc = rem & 7;
+        const uint32_t q = q0 + (uint32_t)i;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (q < a.nq) v = *reinterpret_cast<const float4 *>(a.queries + (size_t)q * a.dim + bk * 32 + cc * 4);
+        qs[i * QROW + bk * 8 + (cc ^ (i & 7))] = v;
+    }
+    for (int idx = tid; idx < NW * QW * K; idx += NW * 64) lists[idx] = WVG_KEY_NONE;
+    for (int idx = tid; idx < NW * QW; idx += NW * 64) thr[idx] = WVG_KEY_NONE;
+    __syncthreads();
+
+    const int kk = lane >> 4, j = lane & 15;
+    // A operand: lane (i = j, kk) reads chunk cc of block 4g+kk of query qg*QW + 16*tq + j
+    const float4 *qa = qs + (qg * QW + j) * QROW + kk * 8;
+    const int hsw = j & 7;
+    // B operand: lane (kk, j) reads chunk 8*(4g+kk)+cc of row 16*rg + j
+    const float4 *rbase = reinterpret_cast<const float4 *>(a.data) + (size_t)(8 * kk) * 64 + 16 * rg + j;
+    const uint32_t nch = a.nchunks;
+    uint64_t *wl = lists + (size_t)wave * QW * K;
+    uint64_t *wthr = thr + wave * QW;
+
+    auto tile_live = [&](uint64_t t) -> uint64_t {
+        uint64_t m = sload64(a.valid + t);
+        if (a.allow) {
+            const uint64_t w = (a.id_base >> 6) + t;
+            m &= w < a.allow_words ? sload64(a.allow + w) : 0ull;
+        }
+        return (m >> (16 * rg)) & 0xFFFFull;
+    };
+    auto next_live = [&](uint64_t t, uint64_t &m) {
+        for (; t < t1; ++t) {
+            m = tile_live(t);
+            if (m) break;
+        }
+        return t;
+    };
+    auto load_b = [&](float4 (&bb)[8], uint64_t t, int g) {
+        const float4 *rp = rbase + ((size_t)t * nch + 32 * g) * 64;
+#pragma unroll
+        for (int cc = 0; cc < 8; cc++) bb[cc] = rp[(size_t)cc * 64];
+    };
+    // per-wave top-k list insertion (wave-uniform qi, key)
+    auto insert = [&](int qi, uint64_t key) {
+        uint64_t *L = wl + qi * K;
+        const uint64_t v = lane < K ? L[lane] : WVG_KEY_NONE;
+        const uint64_t last = __shfl(v, K - 1);
+        if (!(key < last)) return;
+        const uint64_t below = __ballot(lane < K && v < key);
+        const int pos = __popcll(below);
+        if (lane < K - 1 && lane >= pos) L[lane + 1] = v;
+        if (lane == pos) L[pos] = key;
+        const uint64_t prev = K >= 2 ? __shfl(v, K - 2) : key;
+        if (lane == 0) wthr[qi] = pos <= K - 2 ? prev : key;
+    };
+
+    floatx4 acc[QT][32];
+    float4 bb[NBUF][8];  // ring of K-step operand buffers: step g lives in bb[g % NBUF]
+    uint64_t m_cur = 0, m_nxt = 0;
+    uint64_t t = next_live(t0, m_cur);
+    if (t < t1) {
+#pragma unroll
+        for (int g = 0; g + 1 < NBUF; g++) load_b(bb[g], t, g);
+    }
+    while (t < t1) {
+        const uint64_t tn = next_live(t + 1, m_nxt);
+#pragma unroll
+        for (int g = 0; g < NK; g++) {
+            // NBUF-1 K steps ahead: a later step of this tile, or an early step of
+            // the next live tile (the last tile re-reads itself into the dead slot)
+            constexpr int AHEAD = NBUF - 1;
+            const int gp = g + AHEAD;
+            if (gp < NK)
+                load_b(bb[gp % NBUF], t, gp);
+            else
+                load_b(bb[gp % NBUF], tn < t1 ? tn : t, gp - NK);
+            // keep the prefetch issued here, ahead of this step's MFMAs (left
+            // alone, the scheduler sinks each load next to its consumer and the
+            // prefetch distance collapses to one MFMA group)
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int cc = 0; cc < 8; cc++) {
+                float4 av[QT];
+#pragma unroll
+                for (int tq = 0; tq < QT; tq++) av[tq] = qa[tq * 16 * QROW + g * 32 + (cc ^ hsw)];
+                const float4 y = bb[g % NBUF][cc];
+#pragma unroll
+                for (int tq = 0; tq < QT; tq++) {
+                    floatx4 *ac = &acc[tq][4 * cc];
+                    const floatx4 z = (floatx4){0.f, 0.f, 0.f, 0.f};
+                    ac[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[tq].x, y.x, g == 0 ? z : ac[0], 0, 0, 0);
+                    ac[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[tq].y, y.y, g == 0 ? z : ac[1], 0, 0, 0);
+                    ac[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[tq].z, y.z, g == 0 ? z : ac[2], 0, 0, 0);
+                    ac[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[tq].w, y.w, g == 0 ? z : ac[3], 0, 0, 0);
+                }
+            }
+        }
+        // epilogue: AVX2 reduction tree (D/c/dot_avx256_amd64.c:94-103) per output
+        // element; C layout: row j = lane & 15, query 4*(lane >> 4) + r.  All
+        // keys first, so the slice accumulators die before the candidate loop.
+        uint64_t keys[QT][4];
+#pragma unroll
+        for (int tq = 0; tq < QT; tq++) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                float sv[8];
+#pragma unroll
+                for (int l = 0; l < 8; l++) {
+                    const float a01 = acc[tq][8 + l][r] + acc[tq][l][r];
+                    const float a23 = acc[tq][24 + l][r] + acc[tq][16 + l][r];
+                    sv[l] = a23 + a01;
+                }
+                const float lo = (sv[0] + sv[1]) + (sv[2] + sv[3]);
+                const float hi = (sv[4] + sv[5]) + (sv[6] + sv[7]);
+                const float dot = 0.0f + (lo + hi);
+                const float dist = a.metric == WVG_M_DOT ? -dot : 1.0f - dot;
+                const int qi = tq * 16 + (lane >> 4) * 4 + r;
+                keys[tq][r] = ((m_cur >> j) & 1ull) && q0 + qg * QW + qi < a.nq
+                                  ? wvg_make_key(dist, (uint32_t)(t * 64 + 16 * rg + j))
+                                  : WVG_KEY_NONE;
+            }
+        }
+#pragma unroll
+        for (int tq = 0; tq < QT; tq++) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const uint64_t key = keys[tq][r];
+                const int qi = tq * 16 + (lane >> 4) * 4 + r;
+                uint64_t pend = __ballot(key < wthr[qi]);
+                while (pend) {  // rare after the first tiles: wave-uniform insertions
+                    const int src = __builtin_ctzll(pend);
+                    pend &= pend - 1;
+                    const int qsrc = tq * 16 + (src >> 4) * 4 + r;
+                    const uint64_t ks = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(key >> 32), src) << 32) |
+                                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key, src);
+                    insert(qsrc, ks);
+                }
+            }
+        }
+        t = tn;
+        m_cur = m_nxt;
+    }
+    __syncthreads();
+    // merge the four row groups' lists by rank: wave w takes queries w, w+NW, ...
+    uint64_t *tw = tmp + wave * 64;
+    for (int qi = wave; qi < QB; qi += NW) {
+        const uint32_t q = q0 + (uint32_t)qi;
+        if (q >= a.nq) break;
+        const int g = qi / QW, ql = qi % QW;
+        uint64_t mine[RS_RG];
+#pragma unroll
+        for (int v = 0; v < RS_RG; v++)
+            mine[v] = lane < K ? lists[((size_t)(g * RS_RG + v) * QW + ql) * K + lane] : WVG_KEY_NONE;
+        int rank[RS_RG] = {0, 0, 0, 0};
+        for (int v = 0; v < RS_RG; v++)
+            for (int p = 0; p < K; p++) {
+                const uint64_t o = lists[((size_t)(g * RS_RG + v) * QW + ql) * K + p];
+#pragma unroll
+                for (int e = 0; e < RS_RG; e++) rank[e] += o < mine[e];
+            }
+        if (lane < K) tw[lane] = WVG_KEY_NONE;
+#pragma unroll
+        for (int e = 0; e < RS_RG; e++)
+            if (mine[e] != WVG_KEY_NONE && rank[e] < K) tw[rank[e]] = mine[e];
+        if (lane < K) partials[((size_t)q * a.nrr + rr) * K + lane] = tw[lane];
+    }
+}
+
+// K3b applies when the queries of a workgroup fit in LDS next to the lists.
+struct RsConfig {
+    int qt = 1, qh = 1;
+    size_t lds = 0;
+};
+static bool rs_config(uint32_t dim, uint32_t k, RsConfig &c)
+{
+    if (k == 0 || k > 64) return false;
+    if (dim != 256 && dim != 512 && dim != 768 && dim != 1024 && dim != 1536) return false;
+    const int mode = tuning().gemm_kernel;  // 0: QT=2 x QH=1 (one wave per SIMD), 2: QT=1 x QH=2
+    c.qt = mode == 2 ? 1 : 2;
+    c.qh = mode == 2 ? 2 : 1;
+    for (;;) {  // shrink the query block until it fits LDS
+        const size_t qw = 16 * (size_t)c.qt, nw = (size_t)RS_RG * c.qh, qb = qw * c.qh;
+        c.lds = qb * dim * 4 + nw * qw * k * 8 + nw * qw * 8 + nw * 64 * 8;
+        if (c.lds <= 160 * 1024) return true;
+        if (c.qh == 2)
+            c.qh = 1;
+        else if (c.qt == 2)
+            c.qt = 1;
+        else
+            return false;
+    }
+}
+
 bool gemm_supported(uint32_t dim, int metric) { return dim % 32 == 0 && dim > 0 && metric != WVG_M_L2; }
 
-uint32_t gemm_row_ranges(uint32_t nq, uint64_t ntiles, int num_cus)
+uint32_t gemm_queries_per_block(uint32_t dim, uint32_t k)
 {
-    const uint32_t nqb = (nq + GQ - 1) / GQ;
+    RsConfig c;
+    if (tuning().gemm_kernel != 1 && rs_config(dim, k, c)) return 16u * (uint32_t)(c.qt * c.qh);
+    return GQ;
+}
+
+uint32_t gemm_row_ranges(uint32_t nq, uint64_t ntiles, int num_cus, uint32_t dim, uint32_t k)
+{
+    const uint32_t qpb = gemm_queries_per_block(dim, k);
+    const uint32_t nqb = (nq + qpb - 1) / qpb;
     uint64_t want = ((uint64_t)num_cus + nqb - 1) / nqb;  // about one workgroup per CU
     want = (want + 7) / 8 * 8;
     if (want > ntiles) want = ntiles;
@@ -314,8 +569,33 @@ hipError_t launch_gemm_topk(const ScanArgs &s, uint32_t nrr, uint64_t *partials,
     a.queries = reinterpret_cast<const float *>(s.queries);
     a.nq = s.nq;
     a.k = s.k;
-    a.nqb = (s.nq + GQ - 1) / GQ;
     a.nrr = nrr;
+    RsConfig rc;
+    if (tuning().gemm_kernel != 1 && rs_config(s.dim, s.k, rc) && s.nchunks == s.dim / 4) {
+        const uint32_t qb = 16u * (uint32_t)(rc.qt * rc.qh);
+        a.nqb = (s.nq + qb - 1) / qb;
+        dim3 grid(a.nqb * a.nrr), block(RS_RG * rc.qh * 64);
+        const uint32_t lds = (uint32_t)rc.lds;
+#define WVG_RS(DD, NBF)                                                                                \
+    case DD:                                                                                           \
+        if (rc.qt == 2)                                                                                \
+            launch_timed((gemm_rs_kernel<DD, 2, 1, NBF>), grid, block, lds, st, a, partials);          \
+        else if (rc.qh == 2)                                                                           \
+            launch_timed((gemm_rs_kernel<DD, 1, 2, 2>), grid, block, lds, st, a, partials);            \
+        else                                                                                           \
+            launch_timed((gemm_rs_kernel<DD, 1, 1, NBF>), grid, block, lds, st, a, partials);          \
+        return hipGetLastError();
+        switch (s.dim) {
+            WVG_RS(256, 2)
+            WVG_RS(512, 2)
+            WVG_RS(768, 3)
+            WVG_RS(1024, 2)
+            WVG_RS(1536, 3)
+        default: break;
+        }
+#undef WVG_RS
+    }
+    a.nqb = (s.nq + GQ - 1) / GQ;
     const size_t lds = (size_t)2 * (GQ + GR) * GSTRIDE * 4 + (size_t)GQ * GR * 8;
     dim3 grid(a.nqb * a.nrr), block(GWAVES * 64);
     if (s.k <= 64)
