@@ -564,7 +564,7 @@ def test_full_size_1m_x_128_properties(ctx, orc):
 @pytest.mark.parametrize("metric,d", [(METRIC_COSINE, 768), (METRIC_DOT, 256), (METRIC_COSINE, 1536), (METRIC_DOT, 512)])
 def test_batched_mfma_variants(ctx, orc, variant, metric, d):
     """K3b (queries resident in LDS, rows streamed into MFMA operands; 0: two
-    query tiles per wave, 2: two waves per SIMD) and K3 (1) against the oracle:
+    waves per SIMD, 2: two query tiles per wave) and K3 (1) against the oracle:
     ragged rows, deletes, an allow list, partial query blocks, SIFT-like ties."""
     import ctypes
 

@@ -1600,6 +1600,9 @@ int wvgx_set_tuning(int key, int value)
     } else if (key == 4) {
         old = t.gemm_kernel;
         t.gemm_kernel = value;
+    } else if (key == 5) {
+        old = t.gemm_skew;
+        t.gemm_skew = value;
     }
     return old;
 }

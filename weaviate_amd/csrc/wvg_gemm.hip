@@ -49,6 +49,7 @@ struct GemmArgs {
     const float *queries;   // [nq][dim] row-major, 16-byte aligned rows (dim % 32 == 0)
     uint32_t nq, k;
     uint32_t nqb, nrr;      // query blocks, row ranges
+    int skew;               // K3b: start delay of query half 1 (units of s_sleep(8))
 };
 
 // PF = chunks of prefetch in registers (2: 48 staging VGPRs; E > 1 top-k
@@ -398,12 +399,102 @@ __global__ __launch_bounds__(RS_RG * QH * 64, 1) void gemm_rs_kernel(GemmArgs a,
 
     floatx4 acc[QT][32];
     float4 bb[NBUF][8];  // ring of K-step operand buffers: step g lives in bb[g % NBUF]
+
+    // MFMAs of one K step for query tile tq: 8 groups of 4 (4 slices each);
+    // the A operand of group cc+2 is read from LDS while group cc issues.
+    auto mfma_half = [&](int tq, int g, const float4 (&bq)[8]) {
+        const float4 *qp = qa + tq * 16 * QROW + g * 32;
+        float4 a0 = qp[0 ^ hsw], a1 = qp[1 ^ hsw];
+#pragma unroll
+        for (int cc = 0; cc < 8; cc++) {
+            float4 a2 = a1;
+            if (cc + 2 < 8) a2 = qp[(cc + 2) ^ hsw];
+            const float4 y = bq[cc];
+            floatx4 *ac = &acc[tq][4 * cc];
+            const floatx4 z = (floatx4){0.f, 0.f, 0.f, 0.f};
+            ac[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, y.x, g == 0 ? z : ac[0], 0, 0, 0);
+            ac[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, y.y, g == 0 ? z : ac[1], 0, 0, 0);
+            ac[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, y.z, g == 0 ? z : ac[2], 0, 0, 0);
+            ac[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, y.w, g == 0 ? z : ac[3], 0, 0, 0);
+            a0 = a1;
+            a1 = a2;
+        }
+    };
+    // Issue order of one half (cdna_hip_programming.md T19; masks: MFMA 0x8,
+    // VALU 0x2, DS read 0x100): A reads two groups ahead of their MFMAs, and
+    // with an epilogue in the region, ~40 of its VALU after each MFMA group.
+    auto pin_plain = [&]() {
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+        for (int cc = 0; cc < 8; cc++) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+            if (cc + 2 < 8) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+    };
+    auto pin_epi = [&]() {
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+        for (int cc = 0; cc < 8; cc++) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+            if (cc + 2 < 8) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 40, 0);
+        }
+    };
+    // Epilogue of query tile tq of row tile (t, m): AVX2 reduction tree
+    // (D/c/dot_avx256_amd64.c:94-103) per output element; C layout: row j =
+    // lane & 15, query 4*(lane >> 4) + r.  Straight-line VALU, so it can run
+    // under the other query tile's MFMAs.
+    auto reduce_keys = [&](int tq, uint64_t t, uint64_t m, uint64_t (&keys)[4]) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            float sv[8];
+#pragma unroll
+            for (int l = 0; l < 8; l++) {
+                const float a01 = acc[tq][8 + l][r] + acc[tq][l][r];
+                const float a23 = acc[tq][24 + l][r] + acc[tq][16 + l][r];
+                sv[l] = a23 + a01;
+            }
+            const float lo = (sv[0] + sv[1]) + (sv[2] + sv[3]);
+            const float hi = (sv[4] + sv[5]) + (sv[6] + sv[7]);
+            const float dot = 0.0f + (lo + hi);
+            const float dist = a.metric == WVG_M_DOT ? -dot : 1.0f - dot;
+            const int qi = tq * 16 + (lane >> 4) * 4 + r;
+            keys[r] = ((m >> j) & 1ull) && q0 + qg * QW + qi < a.nq
+                          ? wvg_make_key(dist, (uint32_t)(t * 64 + 16 * rg + j))
+                          : WVG_KEY_NONE;
+        }
+    };
+    auto candidates = [&](int tq, const uint64_t (&keys)[4]) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const uint64_t key = keys[r];
+            const int qi = tq * 16 + (lane >> 4) * 4 + r;
+            uint64_t pend = __ballot(key < wthr[qi]);
+            while (pend) {  // rare after the first tiles: wave-uniform insertions
+                const int src = __builtin_ctzll(pend);
+                pend &= pend - 1;
+                const int qsrc = tq * 16 + (src >> 4) * 4 + r;
+                const uint64_t ks = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(key >> 32), src) << 32) |
+                                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key, src);
+                insert(qsrc, ks);
+            }
+        }
+    };
+
     uint64_t m_cur = 0, m_nxt = 0;
     uint64_t t = next_live(t0, m_cur);
     if (t < t1) {
 #pragma unroll
         for (int g = 0; g + 1 < NBUF; g++) load_b(bb[g], t, g);
     }
+    // Software pipeline over the two query tiles (QT == 2): tile 0's epilogue
+    // runs under tile 1's last-step MFMAs, tile 1's under the next row tile's
+    // first-step tile-0 MFMAs -- one wave per SIMD, so nothing else would
+    // fill the matrix pipe while a wave reduces.
+    bool have_prev = false;
+    uint64_t t_prev = 0, m_prev = 0;
+    if (QH == 2 && qg == 1)  // A/B knob: de-phase the SIMD partner's epilogues
+        for (int i = 0; i < a.skew; i++) __builtin_amdgcn_s_sleep(8);
     while (t < t1) {
         const uint64_t tn = next_live(t + 1, m_nxt);
 #pragma unroll
@@ -420,67 +511,61 @@ __global__ __launch_bounds__(RS_RG * QH * 64, 1) void gemm_rs_kernel(GemmArgs a,
             // alone, the scheduler sinks each load next to its consumer and the
             // prefetch distance collapses to one MFMA group)
             __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int cc = 0; cc < 8; cc++) {
-                float4 av[QT];
-#pragma unroll
-                for (int tq = 0; tq < QT; tq++) av[tq] = qa[tq * 16 * QROW + g * 32 + (cc ^ hsw)];
-                const float4 y = bb[g % NBUF][cc];
+            const float4 (&bq)[8] = bb[g % NBUF];
+            if constexpr (QT == 2) {
+                if (g == 0 && have_prev) {
+                    uint64_t kp[4];
+                    mfma_half(0, g, bq);
+                    reduce_keys(1, t_prev, m_prev, kp);
+                    pin_epi();
+                    __builtin_amdgcn_sched_barrier(0);
+                    candidates(1, kp);
+                } else {
+                    mfma_half(0, g, bq);
+                    pin_plain();
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                if (g == NK - 1) {
+                    uint64_t k0[4];
+                    mfma_half(1, g, bq);
+                    reduce_keys(0, t, m_cur, k0);
+                    pin_epi();
+                    __builtin_amdgcn_sched_barrier(0);
+                    candidates(0, k0);
+                } else {
+                    mfma_half(1, g, bq);
+                    pin_plain();
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            } else {
 #pragma unroll
                 for (int tq = 0; tq < QT; tq++) {
-                    floatx4 *ac = &acc[tq][4 * cc];
-                    const floatx4 z = (floatx4){0.f, 0.f, 0.f, 0.f};
-                    ac[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[tq].x, y.x, g == 0 ? z : ac[0], 0, 0, 0);
-                    ac[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[tq].y, y.y, g == 0 ? z : ac[1], 0, 0, 0);
-                    ac[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[tq].z, y.z, g == 0 ? z : ac[2], 0, 0, 0);
-                    ac[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[tq].w, y.w, g == 0 ? z : ac[3], 0, 0, 0);
+                    mfma_half(tq, g, bq);
+                    pin_plain();
+                    __builtin_amdgcn_sched_barrier(0);
                 }
             }
         }
-        // epilogue: AVX2 reduction tree (D/c/dot_avx256_amd64.c:94-103) per output
-        // element; C layout: row j = lane & 15, query 4*(lane >> 4) + r.  All
-        // keys first, so the slice accumulators die before the candidate loop.
-        uint64_t keys[QT][4];
+        if constexpr (QT != 2) {
 #pragma unroll
-        for (int tq = 0; tq < QT; tq++) {
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                float sv[8];
-#pragma unroll
-                for (int l = 0; l < 8; l++) {
-                    const float a01 = acc[tq][8 + l][r] + acc[tq][l][r];
-                    const float a23 = acc[tq][24 + l][r] + acc[tq][16 + l][r];
-                    sv[l] = a23 + a01;
-                }
-                const float lo = (sv[0] + sv[1]) + (sv[2] + sv[3]);
-                const float hi = (sv[4] + sv[5]) + (sv[6] + sv[7]);
-                const float dot = 0.0f + (lo + hi);
-                const float dist = a.metric == WVG_M_DOT ? -dot : 1.0f - dot;
-                const int qi = tq * 16 + (lane >> 4) * 4 + r;
-                keys[tq][r] = ((m_cur >> j) & 1ull) && q0 + qg * QW + qi < a.nq
-                                  ? wvg_make_key(dist, (uint32_t)(t * 64 + 16 * rg + j))
-                                  : WVG_KEY_NONE;
+            for (int tq = 0; tq < QT; tq++) {
+                uint64_t kq[4];
+                reduce_keys(tq, t, m_cur, kq);
+                candidates(tq, kq);
             }
         }
-#pragma unroll
-        for (int tq = 0; tq < QT; tq++) {
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const uint64_t key = keys[tq][r];
-                const int qi = tq * 16 + (lane >> 4) * 4 + r;
-                uint64_t pend = __ballot(key < wthr[qi]);
-                while (pend) {  // rare after the first tiles: wave-uniform insertions
-                    const int src = __builtin_ctzll(pend);
-                    pend &= pend - 1;
-                    const int qsrc = tq * 16 + (src >> 4) * 4 + r;
-                    const uint64_t ks = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(key >> 32), src) << 32) |
-                                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key, src);
-                    insert(qsrc, ks);
-                }
-            }
-        }
+        have_prev = true;
+        t_prev = t;
+        m_prev = m_cur;
         t = tn;
         m_cur = m_nxt;
+    }
+    if constexpr (QT == 2) {
+        if (have_prev) {  // the last row tile's query tile 1
+            uint64_t kp[4];
+            reduce_keys(1, t_prev, m_prev, kp);
+            candidates(1, kp);
+        }
     }
     __syncthreads();
     // merge the four row groups' lists by rank: wave w takes queries w, w+NW, ...
@@ -517,9 +602,12 @@ static bool rs_config(uint32_t dim, uint32_t k, RsConfig &c)
 {
     if (k == 0 || k > 64) return false;
     if (dim != 256 && dim != 512 && dim != 768 && dim != 1024 && dim != 1536) return false;
-    const int mode = tuning().gemm_kernel;  // 0: QT=2 x QH=1 (one wave per SIMD), 2: QT=1 x QH=2
-    c.qt = mode == 2 ? 1 : 2;
-    c.qh = mode == 2 ? 2 : 1;
+    // 0: QT=1 x QH=2 (two waves per SIMD: one wave's epilogue runs under the
+    //    other's MFMAs; measured best), 2: QT=2 x QH=1 (one wave per SIMD, the
+    //    two query tiles' epilogues software-pipelined in the wave)
+    const int mode = tuning().gemm_kernel;
+    c.qt = mode == 2 && dim <= 768 ? 2 : 1;  // two query tiles spill registers above d = 768
+    c.qh = mode == 2 ? 1 : 2;
     for (;;) {  // shrink the query block until it fits LDS
         const size_t qw = 16 * (size_t)c.qt, nw = (size_t)RS_RG * c.qh, qb = qw * c.qh;
         c.lds = qb * dim * 4 + nw * qw * k * 8 + nw * qw * 8 + nw * 64 * 8;
@@ -570,6 +658,7 @@ hipError_t launch_gemm_topk(const ScanArgs &s, uint32_t nrr, uint64_t *partials,
     a.nq = s.nq;
     a.k = s.k;
     a.nrr = nrr;
+    a.skew = tuning().gemm_skew;
     RsConfig rc;
     if (tuning().gemm_kernel != 1 && rs_config(s.dim, s.k, rc) && s.nchunks == s.dim / 4) {
         const uint32_t qb = 16u * (uint32_t)(rc.qt * rc.qh);
@@ -588,7 +677,7 @@ hipError_t launch_gemm_topk(const ScanArgs &s, uint32_t nrr, uint64_t *partials,
         switch (s.dim) {
             WVG_RS(256, 2)
             WVG_RS(512, 2)
-            WVG_RS(768, 3)
+            WVG_RS(768, 2)
             WVG_RS(1024, 2)
             WVG_RS(1536, 3)
         default: break;

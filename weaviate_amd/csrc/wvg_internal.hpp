@@ -144,8 +144,9 @@ struct Tuning {
     int scan_variant = 0;    // K1 variant (see wvg_scan.hip)
     int groups_per_cu = 1;   // K1 workgroups per CU (A/B: 1 = fewest partial lists, same scan rate)
     int gemm_pf = 0;         // K3 register prefetch depth: 0 = by top-k size (2 for k <= 64), 1 = force 1
-    int gemm_kernel = 0;     // K3 variant: 0 = K3b (queries resident, rows streamed; 2 query tiles per wave)
-                             // where it applies, 2 = K3b with 2 waves per SIMD, 1 = K3
+    int gemm_kernel = 0;     // K3 variant: 0 = K3b (queries resident, rows streamed; 2 waves per SIMD)
+                             // where it applies, 2 = K3b with 2 query tiles per wave, 1 = K3
+    int gemm_skew = 0;       // K3b two-waves-per-SIMD: start delay of the second query half (x ~512 cycles)
     int pipeline_mode = 1;   // wvg_search_device_pipelined: 0 = one launch per query (merge folded into the
                              // next launch), 1 = one query-stream launch
 };
