@@ -792,7 +792,8 @@ static int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t 
     ProfArm arm(c->ctx);
     if (arm.rc) return arm.rc;
     if (gemm)
-        WVG_HIP(launch_gemm_topk(a, (uint32_t)groups, partials, s));
+        WVG_HIP(launch_gemm_topk(a, (uint32_t)groups, partials,
+                                 reinterpret_cast<uint32_t *>(partials + (size_t)nq * groups * k), c->ctx->num_cus, s));
     else
         WVG_HIP(launch_scan(a, c->kind, partials, groups, s));
     WVG_HIP(launch_merge_lists(partials, nq, (uint32_t)groups, k, k, c->id_base, ids, dists, counts, s));
@@ -805,7 +806,11 @@ struct SearchPlan {
     bool gemm = false;   // K3 batched MFMA path
     bool empty = false;
     size_t partial_keys(uint32_t nq, uint32_t k) const { return (size_t)nq * groups * k; }
-    size_t workspace_bytes(uint32_t nq, uint32_t k) const { return partial_keys(nq, k) * 8; }
+    // K3b's per-row-range progress counters follow the partial lists (gemm only)
+    size_t workspace_bytes(uint32_t nq, uint32_t k) const
+    {
+        return partial_keys(nq, k) * 8 + (gemm ? (size_t)groups * ((nq + 15) / 16) * 4 + 256 : 0);
+    }
 };
 
 static SearchPlan plan_search(wvg_corpus *c, uint32_t nq, uint32_t k, const uint64_t *allow, uint64_t allow_words)
@@ -1603,6 +1608,9 @@ int wvgx_set_tuning(int key, int value)
     } else if (key == 5) {
         old = t.gemm_skew;
         t.gemm_skew = value;
+    } else if (key == 6) {
+        old = t.gemm_lockstep;
+        t.gemm_lockstep = value;
     }
     return old;
 }

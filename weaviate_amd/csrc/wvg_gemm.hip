@@ -50,6 +50,8 @@ struct GemmArgs {
     uint32_t nq, k;
     uint32_t nqb, nrr;      // query blocks, row ranges
     int skew;               // K3b: start delay of query half 1 (units of s_sleep(8))
+    uint32_t *prog;         // K3b: [nrr][nqb] tiles done per workgroup (null: no lockstep)
+    uint32_t lag;           // K3b: allowed lead over the group's slowest workgroup, in tiles
 };
 
 // PF = chunks of prefetch in registers (2: 48 staging VGPRs; E > 1 top-k
@@ -303,7 +305,8 @@ __global__ __launch_bounds__(GWAVES * 64) void gemm_topk_kernel(GemmArgs a, uint
 // are merged by rank at the end.  Same slice accumulators and AVX2 reduction
 // tree as K3, so the distances are the same bits.
 // ---------------------------------------------------------------------------
-constexpr int RS_RG = 4;  // row groups of 16 per 64-row tile
+constexpr int RS_RG = 4;     // row groups of 16 per 64-row tile
+constexpr uint32_t RS_SYNC = 1;  // lockstep check every RS_SYNC tiles
 
 // QH query halves x 4 row groups = 4*QH waves; wave (qg, rg) scores rows
 // 16*rg..16*rg+15 of every tile against queries qg*16*QT .. +16*QT.
@@ -495,6 +498,30 @@ __global__ __launch_bounds__(RS_RG * QH * 64, 1) void gemm_rs_kernel(GemmArgs a,
     uint64_t t_prev = 0, m_prev = 0;
     if (QH == 2 && qg == 1)  // A/B knob: de-phase the SIMD partner's epilogues
         for (int i = 0; i < a.skew; i++) __builtin_amdgcn_s_sleep(8);
+    // Soft lockstep of the nqb workgroups that stream one row range (they share
+    // an XCD and its 4 MiB L2, ~20 row tiles at d = 768): every RS_SYNC tiles a
+    // wave that is more than `lag` tiles ahead of the slowest workgroup of its
+    // group sleeps, so the group's rows come from HBM once and from L2 for the
+    // rest.  Without it the two-waves-per-SIMD variant drifted apart and read
+    // 684 GB from HBM per 1024-query batch (22 x the corpus).  Bounded: a wave
+    // that waits too long (a group member not resident) stops syncing.
+    uint32_t tiles_done = 0;
+    bool lockstep = a.prog != nullptr;
+    uint32_t *grp = a.prog ? a.prog + (size_t)rr * a.nqb : nullptr;
+    auto keep_pace = [&]() {
+        if (wave == 0 && lane == 0)
+            __hip_atomic_store(grp + qb, tiles_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int spin = 0; spin < 2048; spin++) {
+            uint32_t mn = 0xFFFFFFFFu;
+            for (uint32_t i = lane; i < a.nqb; i += 64)
+                mn = min(mn, __hip_atomic_load(grp + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, off));
+            if (tiles_done <= mn + a.lag) return;
+            __builtin_amdgcn_s_sleep(16);
+        }
+        lockstep = false;
+    };
     while (t < t1) {
         const uint64_t tn = next_live(t + 1, m_nxt);
 #pragma unroll
@@ -559,7 +586,10 @@ __global__ __launch_bounds__(RS_RG * QH * 64, 1) void gemm_rs_kernel(GemmArgs a,
         m_prev = m_cur;
         t = tn;
         m_cur = m_nxt;
+        if (lockstep && (++tiles_done % RS_SYNC) == 0) keep_pace();
     }
+    if (a.prog && wave == 0 && lane == 0)  // done: never hold the group back
+        __hip_atomic_store(grp + qb, 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if constexpr (QT == 2) {
         if (have_prev) {  // the last row tile's query tile 1
             uint64_t kp[4];
@@ -641,7 +671,8 @@ uint32_t gemm_row_ranges(uint32_t nq, uint64_t ntiles, int num_cus, uint32_t dim
     return (uint32_t)want;
 }
 
-hipError_t launch_gemm_topk(const ScanArgs &s, uint32_t nrr, uint64_t *partials, hipStream_t st)
+hipError_t launch_gemm_topk(const ScanArgs &s, uint32_t nrr, uint64_t *partials, uint32_t *prog, int num_cus,
+                            hipStream_t st)
 {
     GemmArgs a{};
     a.data = reinterpret_cast<const float4 *>(s.data);
@@ -664,6 +695,13 @@ hipError_t launch_gemm_topk(const ScanArgs &s, uint32_t nrr, uint64_t *partials,
         const uint32_t qb = 16u * (uint32_t)(rc.qt * rc.qh);
         a.nqb = (s.nq + qb - 1) / qb;
         dim3 grid(a.nqb * a.nrr), block(RS_RG * rc.qh * 64);
+        // lockstep only when every workgroup of the grid is resident (one per CU)
+        a.lag = (uint32_t)tuning().gemm_lockstep;
+        a.prog = prog && a.lag && a.nqb * a.nrr <= (uint32_t)num_cus ? prog : nullptr;
+        if (a.prog) {
+            hipError_t e = hipMemsetAsync(a.prog, 0, (size_t)a.nqb * a.nrr * 4, st);
+            if (e != hipSuccess) return e;
+        }
         const uint32_t lds = (uint32_t)rc.lds;
 #define WVG_RS(DD, NBF)                                                                                \
     case DD:                                                                                           \

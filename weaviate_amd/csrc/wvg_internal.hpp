@@ -138,7 +138,9 @@ hipError_t launch_scan_pq(const ScanArgs &a, uint64_t *partials, int groups, hip
 // K3 batched MFMA scoring (wvg_gemm.hip): partials [nq][nrr][K].
 bool gemm_supported(uint32_t dim, int metric);
 uint32_t gemm_row_ranges(uint32_t nq, uint64_t ntiles, int num_cus, uint32_t dim, uint32_t k);
-hipError_t launch_gemm_topk(const ScanArgs &a, uint32_t nrr, uint64_t *partials, hipStream_t s);
+// prog: [nrr][query blocks] u32 workspace (zeroed here) for K3b's soft lockstep.
+hipError_t launch_gemm_topk(const ScanArgs &a, uint32_t nrr, uint64_t *partials, uint32_t *prog, int num_cus,
+                            hipStream_t s);
 // Internal tuning knobs (wvgx_set_tuning; A/B experiments, not public ABI).
 struct Tuning {
     int scan_variant = 0;    // K1 variant (see wvg_scan.hip)
@@ -146,6 +148,8 @@ struct Tuning {
     int gemm_pf = 0;         // K3 register prefetch depth: 0 = by top-k size (2 for k <= 64), 1 = force 1
     int gemm_kernel = 0;     // K3 variant: 0 = K3b (queries resident, rows streamed; 2 waves per SIMD)
                              // where it applies, 2 = K3b with 2 query tiles per wave, 1 = K3
+    int gemm_lockstep = 0;   // K3b soft lockstep of the workgroups sharing a row range:
+                             // allowed lead in tiles, 0 = off (A/B)
     int gemm_skew = 0;       // K3b two-waves-per-SIMD: start delay of the second query half (x ~512 cycles)
     int pipeline_mode = 1;   // wvg_search_device_pipelined: 0 = one launch per query (merge folded into the
                              // next launch), 1 = one query-stream launch
