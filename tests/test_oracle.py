@@ -184,3 +184,23 @@ def test_oracle_search_by_distance_loop():
     assert len(orc.search_by_distance(fn, 3000.0, 50)[0]) == 100     # the first search always runs
     assert len(orc.search_by_distance(fn, 1e9, -1)[0]) == 5000
     assert len(orc.search_by_distance(fn, np.float32(10.0) - np.float32(5e-7), -1)[0]) == 11  # InDelta 1e-6
+
+
+def test_oracle_selftest_under_asan_ubsan():
+    """The checker itself under AddressSanitizer + UBSan (oracle/selftest.c):
+    every entry point over empty, ragged and block-boundary sizes, k = 0 and
+    k > n, deleted rows -- a buffer overrun in the oracle would otherwise show
+    up as a spurious (or hidden) parity difference."""
+    import shutil
+    import subprocess
+
+    here = os.path.join(os.path.dirname(GOLDEN), "..", "oracle")
+    if shutil.which("gcc") is None:
+        pytest.skip("no gcc")
+    b = subprocess.run(["make", "-s", "-C", here, "asan"], capture_output=True, text=True)
+    if b.returncode != 0 and "sanitize" in (b.stderr or ""):
+        pytest.skip("sanitizer runtime unavailable: " + b.stderr[-200:])
+    assert b.returncode == 0, b.stderr
+    r = subprocess.run([os.path.join(here, "_build", "selftest_asan")], capture_output=True, text=True,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1"), timeout=300)
+    assert r.returncode == 0 and "selftest ok" in r.stdout, r.stderr[-2000:]
