@@ -41,7 +41,7 @@ def parse():
     ap.add_argument("--rows", type=int, default=1_000_000, help="rows per GPU")
     ap.add_argument("--dim", type=int, default=128)
     ap.add_argument("--k", type=int, default=10)
-    ap.add_argument("--cpu-queries", type=int, default=1024)
+    ap.add_argument("--cpu-queries", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
 
