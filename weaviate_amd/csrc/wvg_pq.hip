@@ -103,9 +103,14 @@ __device__ __forceinline__ float l2_256_acc(XA x, CA c, int n)
 // codes [n][m] or, TILED_OUT, the PQ corpus layout (16 codes per 16-byte
 // chunk, stored once per chunk).  (diff = point - centroid; l2_256(filteredPoint, c)
 // at CH/kmeans.go:120.)
+// The centroid reads are wave-uniform: read through the constant address
+// space they become s_load_dwordx16 batches whose SGPRs feed the packed
+// subtracts directly -- as generic loads every centroid was a vector load
+// followed by a full-latency wait.
 template <int DS, bool TILED_OUT>
-__global__ void pq_encode_kernel(const float4 *tiled, uint64_t n, uint32_t dim, uint32_t nchunks, const float *centers,
-                                 uint32_t m, uint32_t ks, uint32_t ds_rt, uint8_t *codes)
+__global__ void pq_encode_kernel(const float4 *__restrict__ tiled, uint64_t n, uint32_t dim, uint32_t nchunks,
+                                 const float *__restrict__ centers, uint32_t m, uint32_t ks, uint32_t ds_rt,
+                                 uint8_t *__restrict__ codes)
 {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
@@ -123,13 +128,15 @@ __global__ void pq_encode_kernel(const float4 *tiled, uint64_t n, uint32_t dim, 
             if constexpr (DS == 4) {
                 // segment s is exactly chunk s (dim = 4m): one 16-byte load, scalar unfused path (n < 8)
                 const float4 x = rp[(size_t)s * 64];
+#pragma unroll 8
                 for (uint32_t c = 0; c < ks; c++) {
-                    const float4 cc = *reinterpret_cast<const float4 *>(cs + (size_t)c * 4);
+                    const __attribute__((address_space(4))) float *cc =
+                        (const __attribute__((address_space(4))) float *)(cs + (size_t)c * 4);
                     float sum = 0.0f;
-                    scalar_update<WVG_M_L2>(sum, cc.x, x.x);
-                    scalar_update<WVG_M_L2>(sum, cc.y, x.y);
-                    scalar_update<WVG_M_L2>(sum, cc.z, x.z);
-                    scalar_update<WVG_M_L2>(sum, cc.w, x.w);
+                    scalar_update<WVG_M_L2>(sum, cc[0], x.x);
+                    scalar_update<WVG_M_L2>(sum, cc[1], x.y);
+                    scalar_update<WVG_M_L2>(sum, cc[2], x.z);
+                    scalar_update<WVG_M_L2>(sum, cc[3], x.w);
                     if (!(minD < sum)) {
                         minD = sum;
                         best = c;
@@ -139,7 +146,8 @@ __global__ void pq_encode_kernel(const float4 *tiled, uint64_t n, uint32_t dim, 
                 const uint32_t base = s * ds;
                 auto xa = [&](int i) { return elem_at<64>(rp, (int)(base + i)); };
                 for (uint32_t c = 0; c < ks; c++) {
-                    const float *cv = cs + (size_t)c * ds;
+                    const __attribute__((address_space(4))) float *cv =
+                        (const __attribute__((address_space(4))) float *)(cs + (size_t)c * ds);
                     auto ca = [&](int i) { return cv[i]; };
                     const float d = l2_256_acc(xa, ca, (int)ds);
                     if (!(minD < d)) {
