@@ -1585,7 +1585,7 @@ int wvg_synthetic_rows(wvg_ctx *ctx, uint64_t seed, const uint64_t *ids, uint64_
 }
 
 // Internal A/B knob (not part of include/wvgpu.h): 0 = K1 scan variant,
-// 1 = K1 resident workgroups per CU.  Returns the previous value.
+// 1 = K1 resident workgroups per CU, ... 7 = K8 ADC variant.  Returns the previous value.
 int wvgx_set_tuning(int key, int value)
 {
     Tuning &t = tuning();
@@ -1611,6 +1611,9 @@ int wvgx_set_tuning(int key, int value)
     } else if (key == 6) {
         old = t.gemm_lockstep;
         t.gemm_lockstep = value;
+    } else if (key == 7) {
+        old = t.pq_variant;
+        t.pq_variant = value;
     }
     return old;
 }

@@ -153,6 +153,8 @@ struct Tuning {
     int gemm_skew = 0;       // K3b two-waves-per-SIMD: start delay of the second query half (x ~512 cycles)
     int pipeline_mode = 1;   // wvg_search_device_pipelined: 0 = one launch per query (merge folded into the
                              // next launch), 1 = one query-stream launch
+    int pq_variant = 0;      // K8: 0 = rotated-segment ADC (K8b) where it applies (m = 32, ks = 256),
+                             // 1 = K8 gather in segment order everywhere
 };
 Tuning &tuning();
 // Profiling: events armed by the host runtime (wvg_profile_start) are bound to

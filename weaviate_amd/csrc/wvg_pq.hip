@@ -322,11 +322,195 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq_kernel(ScanArgs a,
     group_combine_store<E, PQ_SCAN_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
 }
 
+// v_cndmask_b32 with a compile-time lane mask held in an SGPR pair: lanes whose
+// bit is set in `mask` take `if_set`, the others `if_clear`.
+__device__ __forceinline__ uint32_t lane_select(uint64_t mask, uint32_t if_clear, uint32_t if_set)
+{
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(if_clear), "v"(if_set), "s"(mask));
+    return r;
+}
+__device__ __forceinline__ float lane_select(uint64_t mask, float if_clear, float if_set)
+{
+    return __uint_as_float(lane_select(mask, __float_as_uint(if_clear), __float_as_uint(if_set)));
+}
+
+// K8b: ADC scan for m = 32, ks = 256 without LDS bank conflicts.
+//
+// K8 gathers lut[i][code_i] with every lane of a wave on the same segment i, so
+// the 32 lanes of a ds_read_b32 group hit 32 random banks (~4-way conflicts,
+// ~8 LDS cycles per read: the scan ran LDS-bound at 57% of HBM).  Here lane l
+// (x = l mod 32) reads segment (x + j) mod 32 at step j, so at every step the
+// 32 lanes of a group read 32 different segments.
+//
+// Each row's sum must still run in segment order (CH/product_quantization.go:85-104).
+// Lane x therefore works on two rows at once: during the pass over tile p it
+// finishes row p (segments x..31, steps 0..31-x) into accumulator A and starts
+// row p+1 (segments 0..x-1, steps 32-x..31) into accumulator B.  The LUT image
+// in LDS makes that routing free: qword c*64 + s' holds (lut[s'][c], +0.0) for
+// s' < 32 and (+0.0, lut[s'-32][c]) for s' >= 32, and step j reads qword
+// c*64 + x + j with ds_read_b64 -- the 32 lanes of a group on 32 distinct bank
+// pairs (2 LDS cycles) -- then one v_pk_add_f32 adds it to (A, B).  Adding
+// +0.0 is exact (a sum that starts at float32(0) never becomes -0.0, and
+// inf/NaN sums stay as they are), so A and B are the reference's sequential
+// sums bit for bit.  At the end of the pass A is row p's distance, B moves to
+// A and B restarts from +0.0.
+//
+// The code of step j is byte x + j of [codes(p) | codes(p+1)]: a 3-stage
+// dword barrel shift by x/4 once per tile, then per step one v_perm with a
+// per-lane selector (x mod 4 + j mod 4) and one v_lshl_or for the address.
+// LDS: the 128 KiB image, one workgroup per CU.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+template <int E, int R, bool IL>
+__global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_rot_kernel(ScanArgs a, uint64_t *partials)
+{
+    extern __shared__ __attribute__((aligned(16))) f32x2 img[];  // [256][64]
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t qi = blockIdx.y;
+    const float *glut = reinterpret_cast<const float *>(a.queries) + (size_t)qi * a.qpitch;
+    for (uint32_t i = threadIdx.x; i < 32u * 256u; i += blockDim.x) {
+        const uint32_t s = i & 31u, c = i >> 5;
+        const float v = glut[s * 256u + c];
+        img[c * 64u + s] = f32x2{v, 0.0f};
+        img[c * 64u + 32u + s] = f32x2{0.0f, v};
+    }
+    __syncthreads();
+    const uint4 *data = reinterpret_cast<const uint4 *>(a.data);
+    const uint64_t ntiles = a.tile_end - a.tile_begin;
+    // IL: the workgroup owns a contiguous tile range and its waves take every
+    // PQ_SCAN_WAVES-th tile of it (the 16 waves stream one 32 KiB block at a
+    // time); otherwise every wave owns a contiguous range.
+    constexpr uint64_t TS = IL ? PQ_SCAN_WAVES : 1;  // tile stride of a wave
+    uint64_t t0, t1;
+    if constexpr (IL) {
+        t0 = a.tile_begin + ntiles * blockIdx.x / gridDim.x + (uint64_t)wave;
+        t1 = a.tile_begin + ntiles * (blockIdx.x + 1) / gridDim.x;
+    } else {
+        const uint64_t total = (uint64_t)gridDim.x * PQ_SCAN_WAVES;
+        const uint64_t gw = (uint64_t)blockIdx.x * PQ_SCAN_WAVES + wave;
+        t0 = a.tile_begin + ntiles * gw / total;
+        t1 = a.tile_begin + ntiles * (gw + 1) / total;
+    }
+    WaveTopK<E> tk;
+    tk.init((int)a.k);
+    if (t0 < t1) {
+        const uint32_t x = (uint32_t)lane & 31u;
+        const uint32_t x8 = x * 8u;
+        uint32_t selv[4];  // v_perm selector: byte (x mod 4) + i of {G[k+1], G[k]} into byte 0
+#pragma unroll
+        for (int i = 0; i < 4; i++) selv[i] = 0x0C0C0C00u | ((x & 3u) + (uint32_t)i);
+        const char *imgb = reinterpret_cast<const char *>(img);
+
+        auto next_live = [&](uint64_t t, uint64_t &msk) {
+            for (; t < t1; t += TS) {
+                msk = pq_tile_mask(a, t);
+                if (msk) break;
+            }
+            return t;
+        };
+        // Loads are unconditional (a finished stream re-reads tile t0, whose
+        // values are never used) so the waits on the ring stay static.
+        auto load = [&](uint64_t t, uint32_t (&w)[8]) {
+            const uint4 *rp = data + (size_t)(t < t1 ? t : t0) * 2 * 64 + lane;
+            const uint4 lo = ld_codes(rp), hi = ld_codes(rp + 64);
+            w[0] = lo.x; w[1] = lo.y; w[2] = lo.z; w[3] = lo.w;
+            w[4] = hi.x; w[5] = hi.y; w[6] = hi.z; w[7] = hi.w;
+        };
+
+        // Ring of R live tiles' codes (R - 2 tiles of HBM latency cover beyond
+        // the pass's own two).  Pass i: cur = slot (i-1) mod R = live tile i-1,
+        // nxt = slot i mod R = live tile i; afterwards slot (i-1) mod R is
+        // refilled with live tile i+R-1.  t1 marks "no tile".
+        uint32_t ring[R][8];
+        uint64_t rt[R], rm[R];
+        rt[R - 1] = t1;
+        rm[R - 1] = 0;
+        {
+            uint64_t t = t0;
+#pragma unroll
+            for (int s = 0; s < R - 1; s++) {
+                uint64_t m = 0;
+                t = next_live(t, m);
+                rt[s] = t;
+                rm[s] = m;
+                load(t, ring[s]);
+                if (t < t1) t += TS;
+            }
+#pragma unroll
+            for (int w = 0; w < 8; w++) ring[R - 1][w] = 0u;
+        }
+        uint64_t t_fill = rt[R - 2] < t1 ? rt[R - 2] + TS : t1;  // where the next refill searches from
+        f32x2 acc = {0.0f, 0.0f};
+        // Passes run in groups of R with no per-pass exit, so every load is
+        // unconditional and the compiler's waits on the ring stay static; the
+        // passes after the last live tile offer nothing (cur slot = t1).
+        do {
+#pragma unroll
+            for (int s = 0; s < R; s++) {
+                const int sc = (s + R - 1) % R;  // cur slot
+                {
+                    // g[i] = dword x/4 + i of [cur | nxt]
+                    uint32_t g[16];
+#pragma unroll
+                    for (int w = 0; w < 8; w++) {
+                        g[w] = ring[sc][w];
+                        g[8 + w] = ring[s][w];
+                    }
+#pragma unroll
+                    for (int i = 0; i < 15; i++) g[i] = lane_select(0xF0F0F0F0F0F0F0F0ull, g[i], g[i + 1]);  // lane bit 2
+#pragma unroll
+                    for (int i = 0; i < 13; i++) g[i] = lane_select(0xFF00FF00FF00FF00ull, g[i], g[i + 2]);  // lane bit 3
+#pragma unroll
+                    for (int i = 0; i < 9; i++) g[i] = lane_select(0xFFFF0000FFFF0000ull, g[i], g[i + 4]);   // lane bit 4
+                    // two halves of 16 reads, each all in flight before its adds
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        f32x2 v[16];
+#pragma unroll
+                        for (int jj = 0; jj < 16; jj++) {
+                            const int j = h * 16 + jj;
+                            const uint32_t code = __builtin_amdgcn_perm(g[(j >> 2) + 1], g[j >> 2], selv[j & 3]);
+                            const uint32_t off = (code << 9) | x8;
+                            v[jj] = *reinterpret_cast<const f32x2 *>(imgb + off + 8 * j);
+                        }
+#pragma unroll
+                        for (int jj = 0; jj < 16; jj++) acc = acc + v[jj];
+                    }
+                    if (rt[sc] < t1) {
+                        const float dist = wrap_metric(a.metric, acc.x);
+                        tk.offer(((rm[sc] >> lane) & 1ull) ? wvg_make_key(dist, (uint32_t)(rt[sc] * 64 + lane))
+                                                           : WVG_KEY_NONE);
+                    }
+                    acc = f32x2{acc.y, 0.0f};
+                    // refill the cur slot with the live tile R-1 passes ahead
+                    uint64_t m = 0;
+                    const uint64_t t = next_live(t_fill, m);
+                    rt[sc] = t;
+                    rm[sc] = m;
+                    load(t, ring[sc]);
+                    t_fill = t < t1 ? t + TS : t1;
+                }
+            }
+        } while (rt[R - 1] < t1);
+    }
+    group_combine_store<E, PQ_SCAN_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
+}
+
 template <int E>
 static hipError_t launch_pq_e(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
 {
     dim3 grid(groups, a.nq), block(PQ_SCAN_WAVES * 64);
     const size_t lds = (size_t)a.pq_m * a.pq_ks * 4;
+    if (a.pq_ks == 256 && a.pq_m == 32 && a.nchunks == 2 && tuning().pq_variant != 1) {
+        // 128 KiB LUT image; variant 0 = ring 4, per-wave ranges (A/B: 2 = ring 6, 3 = ring 4 interleaved)
+        switch (tuning().pq_variant) {
+        case 2: launch_timed((scan_pq32_rot_kernel<E, 6, false>), grid, block, 4 * lds, s, a, partials); break;
+        case 3: launch_timed((scan_pq32_rot_kernel<E, 4, true>), grid, block, 4 * lds, s, a, partials); break;
+        default: launch_timed((scan_pq32_rot_kernel<E, 4, false>), grid, block, 4 * lds, s, a, partials); break;
+        }
+        return hipGetLastError();
+    }
     if (a.pq_ks == 256) {
         switch (a.pq_m) {
         case 8: launch_timed((scan_pq_kernel<E, 8, 256>), grid, block, lds, s, a, partials); return hipGetLastError();
