@@ -643,6 +643,11 @@ int wvg_corpus_get(wvg_corpus *c, uint64_t id, void *out)
     size_t bytes = c->kind == WVG_KIND_F32 ? (size_t)c->dim * 4
                    : c->kind == WVG_KIND_BQ ? (size_t)bq_words(c->dim) * 8
                                             : (size_t)c->pq_m;
+    if (c->kind == WVG_KIND_PQ && pq_rotated(c->pq_m)) {  // stored byte b = code[(b + slot) mod 32]
+        unsigned char *o = (unsigned char *)out;
+        for (uint32_t b = 0; b < 32; b++) o[(b + (uint32_t)(s & 31)) & 31u] = buf[b];
+        return WVG_OK;
+    }
     std::memcpy(out, buf.data(), bytes);
     return WVG_OK;
 }

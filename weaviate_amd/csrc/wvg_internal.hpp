@@ -82,6 +82,56 @@ __host__ __device__ inline uint32_t f32_chunks(uint32_t dim) { return (dim + 3) 
 __host__ __device__ inline uint32_t bq_words(uint32_t dim) { return (dim + 63) / 64; }
 __host__ __device__ inline uint32_t bq_chunks(uint32_t dim) { return (bq_words(dim) + 1) / 2; }
 __host__ __device__ inline uint32_t pq_chunks(uint32_t m) { return (m + 15) / 16; }
+// PQ corpora with m = 32 store each row's 32 codes rotated by its slot:
+// stored byte b = code[(b + slot mod 32) mod 32].  K8b then reads the bytes
+// it needs at step j straight from the stored words (no per-tile barrel
+// shift); every other reader undoes the rotation with pq32_window.
+__host__ __device__ inline bool pq_rotated(uint32_t m) { return m == 32; }
+// out byte i = in byte (off + i) mod 32 (off per lane: v_cndmask stages + v_alignbyte)
+__device__ __forceinline__ void pq32_window(const uint32_t (&in)[8], uint32_t off, uint32_t (&out)[8])
+{
+    uint32_t d[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) d[i] = in[i];
+    const uint32_t q = (off >> 2) & 7u, r = off & 3u;
+#pragma unroll
+    for (int b = 0; b < 3; b++) {
+        const bool sb = (q >> b) & 1u;
+        uint32_t e[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) e[i] = sb ? d[(i + (1 << b)) & 7] : d[i];
+#pragma unroll
+        for (int i = 0; i < 8; i++) d[i] = e[i];
+    }
+#pragma unroll
+    for (int w = 0; w < 8; w++) out[w] = __builtin_amdgcn_alignbyte(d[(w + 1) & 7], d[w], r);
+}
+// One row's ADC sum in segment order (CH/product_quantization.go:85-104) from
+// its tiled code chunks (rp = chunk 0 of the row, chunks 64 uint4 apart), for
+// the non-streaming readers (dist by id, unbounded selection, K8 generic).
+__device__ __forceinline__ float pq_row_sum(const uint4 *rp, uint32_t nch, uint32_t m, uint32_t ks, const float *lut,
+                                            uint64_t slot)
+{
+    float sum = 0.0f;
+    if (pq_rotated(m)) {
+        const uint4 lo = rp[0], hi = rp[64];
+        const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        uint32_t o[8];
+        pq32_window(w, (32u - (uint32_t)(slot & 31)) & 31u, o);
+#pragma unroll
+        for (int i = 0; i < 32; i++) sum = sum + lut[i * ks + ((o[i >> 2] >> (8 * (i & 3))) & 0xFFu)];
+        return sum;
+    }
+    for (uint32_t c = 0; c < nch; c++) {
+        const uint4 x = rp[(size_t)c * 64];
+        const uint32_t ws[4] = {x.x, x.y, x.z, x.w};
+        for (uint32_t b = 0; b < 16; b++) {
+            const uint32_t s = c * 16 + b;
+            if (s < m) sum = sum + lut[s * ks + ((ws[b >> 2] >> (8 * (b & 3))) & 0xFFu)];
+        }
+    }
+    return sum;
+}
 size_t corpus_row_bytes(int kind, uint32_t dim, uint32_t pq_m);
 
 // ---- kernel launchers (wvg_scan.hip / wvg_bq.hip / wvg_pq.hip) -----------

@@ -117,6 +117,7 @@ __global__ void pq_encode_kernel(const float4 *__restrict__ tiled, uint64_t n, u
     const uint32_t ds = DS > 0 ? (uint32_t)DS : ds_rt;
     const float4 *rp = tiled + ((r >> 6) * nchunks) * 64 + (r & 63);
     const uint32_t out_chunks = pq_chunks(m);
+    uint32_t w8[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};  // TILED_OUT, m = 32: all codes, rotated before the store
     for (uint32_t oc = 0; oc < out_chunks; oc++) {
         uint32_t w[4] = {0u, 0u, 0u, 0u};
         for (uint32_t bsel = 0; bsel < 16; bsel++) {
@@ -161,8 +162,27 @@ __global__ void pq_encode_kernel(const float4 *__restrict__ tiled, uint64_t n, u
             else
                 codes[r * m + s] = (uint8_t)best;
         }
-        if constexpr (TILED_OUT)
-            reinterpret_cast<uint4 *>(codes)[((r >> 6) * out_chunks + oc) * 64 + (r & 63)] = make_uint4(w[0], w[1], w[2], w[3]);
+        if constexpr (TILED_OUT) {
+            if (pq_rotated(m)) {
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    if (oc == 0) w8[i] = w[i];
+                    else w8[4 + i] = w[i];
+                }
+            } else {
+                reinterpret_cast<uint4 *>(codes)[((r >> 6) * out_chunks + oc) * 64 + (r & 63)] =
+                    make_uint4(w[0], w[1], w[2], w[3]);
+            }
+        }
+    }
+    if constexpr (TILED_OUT) {
+        if (pq_rotated(m)) {
+            uint32_t st[8];
+            pq32_window(w8, (uint32_t)(r & 31), st);
+            uint4 *o = reinterpret_cast<uint4 *>(codes) + ((r >> 6) * 2) * 64 + (r & 63);
+            o[0] = make_uint4(st[0], st[1], st[2], st[3]);
+            o[64] = make_uint4(st[4], st[5], st[6], st[7]);
+        }
     }
 }
 
@@ -196,8 +216,10 @@ __global__ void pq_store_kernel(const uint8_t *codes, const uint64_t *slots, uin
     const uint32_t c = (uint32_t)(g % nchunks);
     const uint64_t slot = slots ? slots[i] : i;
     uint32_t w[4] = {0u, 0u, 0u, 0u};
+    const uint32_t rot = pq_rotated(m) ? (uint32_t)(slot & 31) : 0u;
     for (uint32_t b = 0; b < 16; b++) {
-        const uint32_t seg = c * 16 + b;
+        const uint32_t pos = c * 16 + b;
+        const uint32_t seg = rot ? (pos + rot) & 31u : pos;
         if (seg < m) w[b >> 2] |= (uint32_t)codes[i * m + seg] << (8 * (b & 3));
     }
     tiled[((slot >> 6) * nchunks + c) * 64 + (slot & 63)] = make_uint4(w[0], w[1], w[2], w[3]);
@@ -288,9 +310,20 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq_kernel(ScanArgs a,
 #pragma unroll
                 for (int c = 0; c < NC; c++) nxt[c] = ld_codes(rp + (size_t)c * 64);
             }
+            uint4 uc[NC];  // codes in segment order (m = 32 rows are stored rotated)
+            if constexpr (M == 32) {
+                const uint32_t w[8] = {cur[0].x, cur[0].y, cur[0].z, cur[0].w, cur[1].x, cur[1].y, cur[1].z, cur[1].w};
+                uint32_t o[8];
+                pq32_window(w, (32u - ((uint32_t)lane & 31u)) & 31u, o);
+                uc[0] = make_uint4(o[0], o[1], o[2], o[3]);
+                uc[1] = make_uint4(o[4], o[5], o[6], o[7]);
+            } else {
+#pragma unroll
+                for (int c = 0; c < NC; c++) uc[c] = cur[c];
+            }
             float v[M];
 #pragma unroll
-            for (int i = 0; i < M; i++) v[i] = lut[i * ks + code_at(cur, i)];
+            for (int i = 0; i < M; i++) v[i] = lut[i * ks + code_at(uc, i)];
             float sum = 0.0f;
 #pragma unroll
             for (int i = 0; i < M; i++) sum = sum + v[i];
@@ -306,33 +339,11 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq_kernel(ScanArgs a,
             const uint64_t msk = pq_tile_mask(a, t);
             if (msk == 0ull) continue;
             const uint4 *rp = data + (size_t)t * nch * 64 + lane;
-            float sum = 0.0f;
-            for (uint32_t c = 0; c < nch; c++) {
-                const uint4 x = rp[(size_t)c * 64];
-                const uint32_t ws[4] = {x.x, x.y, x.z, x.w};
-                for (uint32_t b = 0; b < 16; b++) {
-                    const uint32_t i = c * 16 + b;
-                    if (i < m) sum = sum + lut[i * ks + ((ws[b >> 2] >> (8 * (b & 3))) & 0xFFu)];
-                }
-            }
-            const float dist = wrap_metric(a.metric, sum);
+            const float dist = wrap_metric(a.metric, pq_row_sum(rp, nch, m, ks, lut, (uint64_t)lane));
             tk.offer(((msk >> lane) & 1ull) ? wvg_make_key(dist, (uint32_t)(t * 64 + lane)) : WVG_KEY_NONE);
         }
     }
     group_combine_store<E, PQ_SCAN_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
-}
-
-// v_cndmask_b32 with a compile-time lane mask held in an SGPR pair: lanes whose
-// bit is set in `mask` take `if_set`, the others `if_clear`.
-__device__ __forceinline__ uint32_t lane_select(uint64_t mask, uint32_t if_clear, uint32_t if_set)
-{
-    uint32_t r;
-    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(if_clear), "v"(if_set), "s"(mask));
-    return r;
-}
-__device__ __forceinline__ float lane_select(uint64_t mask, float if_clear, float if_set)
-{
-    return __uint_as_float(lane_select(mask, __float_as_uint(if_clear), __float_as_uint(if_set)));
 }
 
 // K8b: ADC scan for m = 32, ks = 256 without LDS bank conflicts.
@@ -356,9 +367,10 @@ __device__ __forceinline__ float lane_select(uint64_t mask, float if_clear, floa
 // sums bit for bit.  At the end of the pass A is row p's distance, B moves to
 // A and B restarts from +0.0.
 //
-// The code of step j is byte x + j of [codes(p) | codes(p+1)]: a 3-stage
-// dword barrel shift by x/4 once per tile, then per step one v_perm with a
-// per-lane selector (x mod 4 + j mod 4) and one v_lshl_or for the address.
+// Rows of m = 32 corpora are stored rotated by slot mod 32 (pq_rotated), so
+// lane x's code for step j is stored byte j of row p (j < 32 - x) or of row
+// p+1 (j >= 32 - x): one v_bfi per dword with a per-lane byte mask merges the
+// two rows, then a byte extract and one v_lshl_or give the LDS address.
 // LDS: the 128 KiB image, one workgroup per CU.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
@@ -397,9 +409,16 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_rot_kernel(ScanA
     if (t0 < t1) {
         const uint32_t x = (uint32_t)lane & 31u;
         const uint32_t x8 = x * 8u;
-        uint32_t selv[4];  // v_perm selector: byte (x mod 4) + i of {G[k+1], G[k]} into byte 0
+        // the stored rows are rotated by slot mod 32 = x, so step j's code is
+        // stored byte j of row p (j < 32 - x) or of row p+1 (j >= 32 - x)
+        uint32_t nmask[8];  // bytes taken from the next row
 #pragma unroll
-        for (int i = 0; i < 4; i++) selv[i] = 0x0C0C0C00u | ((x & 3u) + (uint32_t)i);
+        for (int w = 0; w < 8; w++) {
+            uint32_t mk = 0u;
+#pragma unroll
+            for (int bb = 0; bb < 4; bb++) mk |= (4u * w + bb + x >= 32u) ? (0xFFu << (8 * bb)) : 0u;
+            nmask[w] = mk;
+        }
         const char *imgb = reinterpret_cast<const char *>(img);
 
         auto next_live = [&](uint64_t t, uint64_t &msk) {
@@ -450,19 +469,10 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_rot_kernel(ScanA
             for (int s = 0; s < R; s++) {
                 const int sc = (s + R - 1) % R;  // cur slot
                 {
-                    // g[i] = dword x/4 + i of [cur | nxt]
-                    uint32_t g[16];
+                    uint32_t win[8];
 #pragma unroll
-                    for (int w = 0; w < 8; w++) {
-                        g[w] = ring[sc][w];
-                        g[8 + w] = ring[s][w];
-                    }
-#pragma unroll
-                    for (int i = 0; i < 15; i++) g[i] = lane_select(0xF0F0F0F0F0F0F0F0ull, g[i], g[i + 1]);  // lane bit 2
-#pragma unroll
-                    for (int i = 0; i < 13; i++) g[i] = lane_select(0xFF00FF00FF00FF00ull, g[i], g[i + 2]);  // lane bit 3
-#pragma unroll
-                    for (int i = 0; i < 9; i++) g[i] = lane_select(0xFFFF0000FFFF0000ull, g[i], g[i + 4]);   // lane bit 4
+                    for (int w = 0; w < 8; w++)
+                        asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(win[w]) : "v"(nmask[w]), "v"(ring[s][w]), "v"(ring[sc][w]));
                     // two halves of 16 reads, each all in flight before its adds
 #pragma unroll
                     for (int h = 0; h < 2; h++) {
@@ -470,8 +480,9 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_rot_kernel(ScanA
 #pragma unroll
                         for (int jj = 0; jj < 16; jj++) {
                             const int j = h * 16 + jj;
-                            const uint32_t code = __builtin_amdgcn_perm(g[(j >> 2) + 1], g[j >> 2], selv[j & 3]);
-                            const uint32_t off = (code << 9) | x8;
+                            // code << 8 by one v_perm (byte j mod 4 into byte 1, zeros elsewhere)
+                            const uint32_t c8 = __builtin_amdgcn_perm(0u, win[j >> 2], 0x0C0C000Cu | ((uint32_t)(j & 3) << 8));
+                            const uint32_t off = (c8 << 1) + x8;
                             v[jj] = *reinterpret_cast<const f32x2 *>(imgb + off + 8 * j);
                         }
 #pragma unroll

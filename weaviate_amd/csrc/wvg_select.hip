@@ -109,15 +109,7 @@ __global__ __launch_bounds__(256) void ordkeys_pq_kernel(ScanArgs a, uint32_t *k
         uint32_t key = ORD_NONE;
         if ((msk >> lane) & 1ull) {
             const uint4 *rp = data + (size_t)t * a.nchunks * 64 + lane;
-            float sum = 0.0f;
-            for (uint32_t c = 0; c < a.nchunks; c++) {
-                const uint4 x = rp[(size_t)c * 64];
-                const uint32_t ws[4] = {x.x, x.y, x.z, x.w};
-                for (uint32_t b = 0; b < 16; b++) {
-                    const uint32_t s = c * 16 + b;
-                    if (s < m) sum = sum + lut[s * ks + ((ws[b >> 2] >> (8 * (b & 3))) & 0xFFu)];
-                }
-            }
+            const float sum = pq_row_sum(rp, a.nchunks, m, ks, lut, (uint64_t)lane);
             key = wvg_ord_f32(wrap_metric(a.metric, sum));
         }
         keys[i * 64 + lane] = key;
@@ -382,16 +374,7 @@ __global__ void dist_by_ids_kernel(ScanArgs a, uint64_t capacity, const uint64_t
         } else {
             const uint4 *rp = reinterpret_cast<const uint4 *>(a.data) + (size_t)t * a.nchunks * 64 + lane;
             const float *lut = reinterpret_cast<const float *>(a.queries);
-            float sum = 0.0f;
-            for (uint32_t c = 0; c < a.nchunks; c++) {
-                const uint4 x = rp[(size_t)c * 64];
-                const uint32_t ws[4] = {x.x, x.y, x.z, x.w};
-                for (uint32_t b = 0; b < 16; b++) {
-                    const uint32_t s = c * 16 + b;
-                    if (s < a.pq_m) sum = sum + lut[s * a.pq_ks + ((ws[b >> 2] >> (8 * (b & 3))) & 0xFFu)];
-                }
-            }
-            d = wrap_metric(a.metric, sum);
+            d = wrap_metric(a.metric, pq_row_sum(rp, a.nchunks, a.pq_m, a.pq_ks, lut, slot));
         }
     }
     out[i] = d;
