@@ -488,11 +488,7 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_rot_kernel(ScanA
 #pragma unroll
                         for (int jj = 0; jj < 16; jj++) acc = acc + v[jj];
                     }
-                    if (rt[sc] < t1) {
-                        const float dist = wrap_metric(a.metric, acc.x);
-                        tk.offer(((rm[sc] >> lane) & 1ull) ? wvg_make_key(dist, (uint32_t)(rt[sc] * 64 + lane))
-                                                           : WVG_KEY_NONE);
-                    }
+                    if (rt[sc] < t1) tk.offer_dist(wrap_metric(a.metric, acc.x), (uint32_t)(rt[sc] * 64 + lane), rm[sc]);
                     acc = f32x2{acc.y, 0.0f};
                     // refill the cur slot with the live tile R-1 passes ahead
                     uint64_t m = 0;
@@ -514,11 +510,11 @@ static hipError_t launch_pq_e(const ScanArgs &a, uint64_t *partials, int groups,
     dim3 grid(groups, a.nq), block(PQ_SCAN_WAVES * 64);
     const size_t lds = (size_t)a.pq_m * a.pq_ks * 4;
     if (a.pq_ks == 256 && a.pq_m == 32 && a.nchunks == 2 && tuning().pq_variant != 1) {
-        // 128 KiB LUT image; variant 0 = ring 4, per-wave ranges (A/B: 2 = ring 6, 3 = ring 4 interleaved)
+        // 128 KiB LUT image; variant 0 = ring 6, per-wave ranges (A/B: 2 = ring 4, 3 = ring 4 interleaved)
         switch (tuning().pq_variant) {
-        case 2: launch_timed((scan_pq32_rot_kernel<E, 6, false>), grid, block, 4 * lds, s, a, partials); break;
+        case 2: launch_timed((scan_pq32_rot_kernel<E, 4, false>), grid, block, 4 * lds, s, a, partials); break;
         case 3: launch_timed((scan_pq32_rot_kernel<E, 4, true>), grid, block, 4 * lds, s, a, partials); break;
-        default: launch_timed((scan_pq32_rot_kernel<E, 4, false>), grid, block, 4 * lds, s, a, partials); break;
+        default: launch_timed((scan_pq32_rot_kernel<E, 6, false>), grid, block, 4 * lds, s, a, partials); break;
         }
         return hipGetLastError();
     }

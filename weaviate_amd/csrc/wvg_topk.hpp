@@ -203,6 +203,17 @@ struct WaveTopK {
         tau = t;
     }
 
+    // Offer (dist, slot) for the lanes set in the wave-uniform `live` mask.  A
+    // batch whose ordered distances all lie above the threshold's is rejected
+    // with one 32-bit compare and a scalar AND, before any 64-bit key is built.
+    __device__ __forceinline__ void offer_dist(float dist, uint32_t slot, uint64_t live)
+    {
+        const uint32_t o = wvg_ord_f32(dist);
+        if ((__ballot(o <= (uint32_t)(tau >> 32)) & live) == 0ull) return;
+        const int lane = threadIdx.x & 63;
+        offer(((live >> lane) & 1ull) ? (((uint64_t)o << 32) | slot) : WVG_KEY_NONE);
+    }
+
     // Offer one key per lane (KEY_NONE for an empty lane).
     __device__ __forceinline__ void offer(uint64_t key)
     {
