@@ -96,6 +96,12 @@ int wvg_corpus_load_kv(wvg_corpus *c, const uint8_t *keys, const uint8_t *values
  * reference's ok=false for deleted nodes.                                  */
 int wvg_corpus_distance_by_ids(wvg_corpus *c, const float *query, const uint64_t *ids, uint64_t n,
                                float *out_dists, uint8_t *out_ok);
+/* The same for many queries in ONE launch (batched HNSW rescore: every
+ * query's ef candidates, V/hnsw/search.go:564-581, for concurrent queries):
+ * queries [nq][dim]; query q's ids are ids[offsets[q] .. offsets[q+1]),
+ * offsets[nq+1] non-decreasing from 0; outputs parallel to ids.            */
+int wvg_corpus_distance_by_ids_batch(wvg_corpus *c, const float *queries, uint32_t nq, const uint64_t *offsets,
+                                     const uint64_t *ids, float *out_dists, uint8_t *out_ok);
 /* flat.Delete (V/flat/index.go:276-295): clears the validity bit. */
 int wvg_corpus_delete(wvg_corpus *c, const uint64_t *ids, uint64_t n);
 /* flat.vectorById (V/flat/index.go:401-407): copies the stored row

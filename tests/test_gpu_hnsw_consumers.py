@@ -145,3 +145,68 @@ def test_index_queue_brute_force(ctx, orc, metric):
         want_i, want_d = orc.lex_topk(cd, cid, len(cid) if k < 0 else k)
         assert np.array_equal(bits(got_d), bits(want_d))
         assert np.array_equal(got_i, want_i)
+
+
+def _corpus_of(ctx, orc, kind, metric, n, d, m=32):
+    rng = np.random.default_rng(29 + kind)
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    c = Corpus(ctx, kind, metric, d, n)
+    if kind == KIND_PQ:
+        c.set_codebook(orc.synth_rows(31, 0, m * 256, d // m, 0).reshape(m, 256, d // m))
+    c.upsert(np.arange(n, dtype=np.uint64), X)
+    return c
+
+
+@pytest.mark.parametrize("kind,metric,m", [(KIND_F32, METRIC_L2, 0), (KIND_F32, METRIC_DOT, 0),
+                                           (KIND_F32, METRIC_COSINE, 0), (KIND_BQ, METRIC_COSINE, 0),
+                                           (KIND_PQ, METRIC_L2, 32), (KIND_PQ, METRIC_DOT, 16)])
+def test_distance_by_ids_batch_equals_per_query(ctx, orc, kind, metric, m):
+    """wvg_corpus_distance_by_ids_batch == one wvg_corpus_distance_by_ids per
+    query, bit for bit, for ragged lists (empty ones included), deleted and
+    unknown ids; rescore_batch == rescore per query."""
+    n, d, nq = 5_000, 128, 7
+    c = _corpus_of(ctx, orc, kind, metric, n, d, m)
+    try:
+        c.delete(np.arange(3, n, 101, dtype=np.uint64))
+        rng = np.random.default_rng(33)
+        qs = rng.standard_normal((nq, d)).astype(np.float32)
+        lists = [rng.choice(n + 40, size=sz, replace=False).astype(np.uint64) for sz in (0, 1, 17, 500, 0, 64, 333)]
+        got = c.distance_by_ids_batch(qs, lists)
+        for q, ids, (dg, okg) in zip(qs, lists, got):
+            if ids.size == 0:
+                assert dg.size == 0 and okg.size == 0
+                continue
+            dw, okw = c.distance_by_ids(q, ids)
+            assert np.array_equal(okg, okw)
+            assert np.array_equal(bits(dg), bits(dw))
+        rb = hnsw.rescore_batch(c, qs, lists, 10, ef=200)
+        for q, ids, (gi, gd) in zip(qs, lists, rb):
+            wi, wd = hnsw.rescore(c, q, ids, 10, ef=200)
+            assert np.array_equal(gi, wi) and np.array_equal(bits(gd), bits(wd))
+    finally:
+        c.destroy()
+
+
+def test_distance_by_ids_batch_errors(ctx, orc):
+    import ctypes
+
+    from weaviate_amd import _lib
+    from weaviate_amd._lib import fptr, u64ptr
+
+    c = _corpus_of(ctx, orc, KIND_F32, METRIC_L2, 100, 16)
+    try:
+        lib = _lib.load()
+        q = np.zeros((2, 16), np.float32)
+        ids = np.arange(4, dtype=np.uint64)
+        out = np.empty(4, np.float32)
+        ok = np.empty(4, np.uint8)
+        okp = ok.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+        bad = np.array([0, 3, 2], np.uint64)  # decreasing
+        assert lib.wvg_corpus_distance_by_ids_batch(c.handle, fptr(q), 2, u64ptr(bad), u64ptr(ids), fptr(out), okp) < 0
+        bad0 = np.array([1, 2, 4], np.uint64)  # offsets[0] != 0
+        assert lib.wvg_corpus_distance_by_ids_batch(c.handle, fptr(q), 2, u64ptr(bad0), u64ptr(ids), fptr(out), okp) < 0
+        good = np.array([0, 1, 4], np.uint64)
+        assert lib.wvg_corpus_distance_by_ids_batch(c.handle, fptr(q), 2, u64ptr(good), u64ptr(ids), fptr(out), okp) == 0
+        assert ok.all()
+    finally:
+        c.destroy()

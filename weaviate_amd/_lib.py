@@ -44,6 +44,8 @@ SIGNATURES = {
     "wvg_corpus_upsert_codes": (c_int, [c_void_p, _P(c_uint64), c_void_p, c_uint64]),
     "wvg_corpus_load_kv": (c_int, [c_void_p, _P(c_uint8), _P(c_uint8), c_uint64, c_uint64]),
     "wvg_corpus_distance_by_ids": (c_int, [c_void_p, _P(c_float), _P(c_uint64), c_uint64, _P(c_float), _P(c_uint8)]),
+    "wvg_corpus_distance_by_ids_batch": (c_int, [c_void_p, _P(c_float), c_uint32, _P(c_uint64), _P(c_uint64),
+                                                 _P(c_float), _P(c_uint8)]),
     "wvg_corpus_delete": (c_int, [c_void_p, _P(c_uint64), c_uint64]),
     "wvg_corpus_get": (c_int, [c_void_p, c_uint64, c_void_p]),
     "wvg_corpus_fill_synthetic": (c_int, [c_void_p, c_uint64, c_uint64, c_int]),

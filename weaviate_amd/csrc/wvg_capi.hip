@@ -2009,6 +2009,50 @@ int wvg_corpus_distance_by_ids(wvg_corpus *c, const float *query, const uint64_t
     return WVG_OK;
 }
 
+int wvg_corpus_distance_by_ids_batch(wvg_corpus *c, const float *queries, uint32_t nq, const uint64_t *offsets,
+                                     const uint64_t *ids, float *out_dists, uint8_t *out_ok)
+{
+    int rc = check_corpus(c);
+    if (rc) return rc;
+    if (nq == 0) return WVG_OK;
+    if (!queries || !offsets) return fail(WVG_ERR_INVALID, "null argument");
+    if (offsets[0] != 0) return fail(WVG_ERR_INVALID, "offsets[0] must be 0");
+    for (uint32_t q = 0; q < nq; q++)
+        if (offsets[q + 1] < offsets[q]) return fail(WVG_ERR_INVALID, "offsets must be non-decreasing");
+    const uint64_t n = offsets[nq];
+    if (n && (!ids || !out_dists || !out_ok)) return fail(WVG_ERR_INVALID, "null argument");
+    if (c->kind == WVG_KIND_PQ && !c->d_centers) return fail(WVG_ERR_INVALID, "PQ corpus has no codebook");
+    if (n == 0) return WVG_OK;
+    std::vector<uint32_t> qidx(n);
+    for (uint32_t q = 0; q < nq; q++)
+        for (uint64_t i = offsets[q]; i < offsets[q + 1]; i++) qidx[i] = q;
+    std::shared_lock<std::shared_mutex> lk(c->rw);
+    SlotGuard g(c->ctx);
+    rc = c->ctx->acquire(&g.slot);
+    if (rc) return rc;
+    Carver cv;
+    const size_t o_q = cv.take(query_bytes(c, nq));
+    const size_t o_qtmp = cv.take(c->kind == WVG_KIND_PQ ? (size_t)nq * c->dim * 4 : 0);
+    const size_t o_ids = cv.take(n * 8), o_qi = cv.take(n * 4), o_d = cv.take(n * 4), o_ok = cv.take(n);
+    void *base = nullptr;
+    rc = g.slot->device_scratch(cv.off, &base);
+    if (rc) return rc;
+    char *b = (char *)base;
+    hipStream_t s = g.slot->stream;
+    uint32_t qpitch = 0;
+    rc = stage_queries(c, g.slot, queries, nq, b + o_q, qpitch, (float *)(b + o_q), b + o_qtmp);
+    if (rc) return rc;
+    WVG_HIP(hipMemcpyAsync(b + o_ids, ids, n * 8, hipMemcpyHostToDevice, s));
+    WVG_HIP(hipMemcpyAsync(b + o_qi, qidx.data(), n * 4, hipMemcpyHostToDevice, s));
+    ScanArgs a = scan_args_for(c, b + o_q, qpitch, nq, 1, nullptr, 0, 0, tiles_of(c->high_water));
+    WVG_HIP(launch_dist_by_ids(a, c->kind, c->capacity, (const uint64_t *)(b + o_ids), n, (float *)(b + o_d),
+                               (uint8_t *)(b + o_ok), s, (const uint32_t *)(b + o_qi)));
+    WVG_HIP(hipMemcpyAsync(out_dists, b + o_d, n * 4, hipMemcpyDeviceToHost, s));
+    WVG_HIP(hipMemcpyAsync(out_ok, b + o_ok, n, hipMemcpyDeviceToHost, s));
+    WVG_HIP(hipStreamSynchronize(s));  // also keeps qidx alive until its copy is done
+    return WVG_OK;
+}
+
 int wvg_corpus_load_kv(wvg_corpus *c, const uint8_t *keys, const uint8_t *values, uint64_t n, uint64_t value_bytes)
 {
     int rc = check_corpus(c);

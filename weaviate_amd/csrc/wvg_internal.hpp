@@ -311,7 +311,8 @@ hipError_t launch_pq_sdc_table(int metric, const float *centers, uint32_t m, uin
 hipError_t launch_pq_sdc_rows(int metric, const float *table, uint32_t m, uint32_t ks, const uint8_t *x,
                               const uint8_t *codes, uint64_t n, float *out, hipStream_t s);
 hipError_t launch_dist_by_ids(const ScanArgs &a, int kind, uint64_t capacity, const uint64_t *ids, uint64_t n,
-                              float *out, uint8_t *ok, hipStream_t s);
+                              float *out, uint8_t *ok, hipStream_t s,
+                              const uint32_t *qidx = nullptr);
 hipError_t launch_set_valid(uint64_t *valid, const uint64_t *slots, uint64_t n, int set,
                             hipStream_t s);
 

@@ -346,12 +346,17 @@ hipError_t launch_emit_sorted(const uint64_t *sorted, uint64_t n, uint64_t id_ba
 // ---------------------------------------------------------------------------
 namespace wvg {
 
+// qidx (nullable): query index of every id -- many queries' candidate lists
+// in one launch (a.queries holds nq prepared queries, a.qpitch elements apart).
 template <int KIND, int METRIC>
 __global__ void dist_by_ids_kernel(ScanArgs a, uint64_t capacity, const uint64_t *ids, uint64_t n, float *out,
-                                   uint8_t *ok)
+                                   uint8_t *ok, const uint32_t *qidx)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    if (qidx)
+        a.queries = reinterpret_cast<const char *>(a.queries) +
+                    (size_t)qidx[i] * a.qpitch * (KIND == WVG_KIND_BQ ? 8u : 4u);
     const uint64_t id = ids[i];
     const uint64_t slot = id - a.id_base;
     const bool live = id >= a.id_base && slot < capacity && ((a.valid[slot >> 6] >> (slot & 63)) & 1ull);
@@ -382,20 +387,20 @@ __global__ void dist_by_ids_kernel(ScanArgs a, uint64_t capacity, const uint64_t
 }
 
 hipError_t launch_dist_by_ids(const ScanArgs &a, int kind, uint64_t capacity, const uint64_t *ids, uint64_t n,
-                              float *out, uint8_t *ok, hipStream_t s)
+                              float *out, uint8_t *ok, hipStream_t s, const uint32_t *qidx)
 {
     if (n == 0) return hipSuccess;
     dim3 grid((unsigned)((n + 255) / 256)), block(256);
     if (kind == WVG_KIND_F32) {
         if (a.metric == WVG_M_L2)
-            hipLaunchKernelGGL((dist_by_ids_kernel<WVG_KIND_F32, WVG_M_L2>), grid, block, 0, s, a, capacity, ids, n, out, ok);
+            hipLaunchKernelGGL((dist_by_ids_kernel<WVG_KIND_F32, WVG_M_L2>), grid, block, 0, s, a, capacity, ids, n, out, ok, qidx);
         else
             hipLaunchKernelGGL((dist_by_ids_kernel<WVG_KIND_F32, WVG_M_DOT>), grid, block, 0, s, a, capacity, ids, n, out,
-                               ok);
+                               ok, qidx);
     } else if (kind == WVG_KIND_BQ) {
-        hipLaunchKernelGGL((dist_by_ids_kernel<WVG_KIND_BQ, 0>), grid, block, 0, s, a, capacity, ids, n, out, ok);
+        hipLaunchKernelGGL((dist_by_ids_kernel<WVG_KIND_BQ, 0>), grid, block, 0, s, a, capacity, ids, n, out, ok, qidx);
     } else {
-        hipLaunchKernelGGL((dist_by_ids_kernel<WVG_KIND_PQ, 0>), grid, block, 0, s, a, capacity, ids, n, out, ok);
+        hipLaunchKernelGGL((dist_by_ids_kernel<WVG_KIND_PQ, 0>), grid, block, 0, s, a, capacity, ids, n, out, ok, qidx);
     }
     return hipGetLastError();
 }

@@ -119,6 +119,25 @@ class Corpus:
                                                   ok.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
         return out, ok.astype(bool)
 
+    def distance_by_ids_batch(self, queries, id_lists):
+        """wvg_corpus_distance_by_ids_batch: one launch for many queries' id lists;
+        returns [(dists, ok)] per query."""
+        q = np.ascontiguousarray(queries, dtype=np.float32).reshape(len(id_lists), -1)
+        lists = [np.ascontiguousarray(x, dtype=np.uint64).reshape(-1) for x in id_lists]
+        offsets = np.zeros(len(lists) + 1, dtype=np.uint64)
+        offsets[1:] = np.cumsum([len(x) for x in lists])
+        ids = np.concatenate(lists) if lists else np.empty(0, np.uint64)
+        ids = np.ascontiguousarray(ids, dtype=np.uint64)
+        out = np.empty(len(ids), dtype=np.float32)
+        ok = np.empty(len(ids), dtype=np.uint8)
+        check(self.lib.wvg_corpus_distance_by_ids_batch(self.handle, fptr(q), len(lists), u64ptr(offsets), u64ptr(ids),
+                                                        fptr(out), ok.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
+        res = []
+        for i in range(len(lists)):
+            a, b = int(offsets[i]), int(offsets[i + 1])
+            res.append((out[a:b], ok[a:b].astype(bool)))
+        return res
+
     def delete(self, ids) -> None:
         ids = np.ascontiguousarray(ids, dtype=np.uint64)
         check(self.lib.wvg_corpus_delete(self.handle, u64ptr(ids), len(ids)))

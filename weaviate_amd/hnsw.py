@@ -11,7 +11,9 @@ loops in it that score many stored vectors against one query:
 * ``rescore`` -- the rescore block of ``searchByVectorDistance`` / ``knnSearchByVector``
   (V/hnsw/search.go:564-597): exact float distances of the ef candidates the
   compressed walk found (``distanceFromBytesToFloatNode``), keep ef, then k.
-  One ``wvg_corpus_distance_by_ids`` over the candidates' device rows.
+  One ``wvg_corpus_distance_by_ids`` over the candidates' device rows;
+  ``rescore_batch`` does the loop for many concurrent queries in one launch
+  (``wvg_corpus_distance_by_ids_batch``).
 
 Both work on a ``Corpus`` that mirrors the HNSW node vectors (F32), or its
 compressed codes (BQ / PQ: ``distBetweenNodeAndVec`` with the compressor's
@@ -60,3 +62,23 @@ def rescore(corpus: Corpus, query, candidate_ids, k: int, ef: int | None = None)
     dists = np.where(ok, dists, np.float32(0.0)).astype(np.float32)
     keep = min(k, ef if ef is not None else cand.size)
     return _lex_smallest(cand, dists, keep)
+
+
+def rescore_batch(corpus: Corpus, queries, candidate_lists, k: int, ef: int | None = None):
+    """``rescore`` for many queries (each with its own candidate list) with ONE
+    device launch: the serving shape, where concurrent HNSW searches reach
+    their rescore step together.  Same per-query semantics as ``rescore``."""
+    lists = [np.asarray(c, dtype=np.uint64).reshape(-1) for c in candidate_lists]
+    q = np.asarray(queries, dtype=np.float32).reshape(len(lists), -1)
+    empty = (np.empty(0, dtype=np.uint64), np.empty(0, dtype=np.float32))
+    if k <= 0:
+        return [empty for _ in lists]
+    out = []
+    for cand, (dists, ok) in zip(lists, corpus.distance_by_ids_batch(q, lists)):
+        if cand.size == 0:
+            out.append(empty)
+            continue
+        dists = np.where(ok, dists, np.float32(0.0)).astype(np.float32)
+        keep = min(k, ef if ef is not None else cand.size)
+        out.append(_lex_smallest(cand, dists, keep))
+    return out
