@@ -105,7 +105,7 @@ def test_rot_equals_gather_variant(ctx, orc, big, metric):
         for k, al in [(10, None), (64, allow), (150, None)]:
             _variant(1)
             b = c.search(qs, k, allow=al)
-            for v in (0, 2, 3):  # K8b: ring 6, ring 4, ring 4 with interleaved waves
+            for v in (0, 2, 3, 4, 5):  # K8b: ring 6, ring 4, interleaved waves, LDS batches 32 / 8
                 _variant(v)
                 a = c.search(qs, k, allow=al)
                 for x, y in zip(a, b):

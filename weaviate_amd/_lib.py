@@ -11,7 +11,8 @@ import os
 from ctypes import POINTER, c_char_p, c_float, c_int, c_size_t, c_uint8, c_uint32, c_uint64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libwvgpu.so")
+# WVG_LIB: an alternative in-tree build of the same library (A/B runs of a kernel change)
+LIB_PATH = os.environ.get("WVG_LIB") or os.path.join(_HERE, "libwvgpu.so")
 
 WVG_OK = 0
 WVG_ERR_INVALID = -1

@@ -374,18 +374,28 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq_kernel(ScanArgs a,
 // LDS: the 128 KiB image, one workgroup per CU.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-template <int E, int R, bool IL>
+template <int E, int R, bool IL, int NB>
 __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_rot_kernel(ScanArgs a, uint64_t *partials)
 {
     extern __shared__ __attribute__((aligned(16))) f32x2 img[];  // [256][64]
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t qi = blockIdx.y;
     const float *glut = reinterpret_cast<const float *>(a.queries) + (size_t)qi * a.qpitch;
-    for (uint32_t i = threadIdx.x; i < 32u * 256u; i += blockDim.x) {
+    // all of a thread's LUT reads in flight at once (a rolled loop paid one L2
+    // round trip per iteration: most of the launch's fixed cost)
+    constexpr int FILL = 32 * 256 / (PQ_SCAN_WAVES * 64);
+    float fv[FILL];
+#pragma unroll
+    for (int it = 0; it < FILL; it++) {
+        const uint32_t i = (uint32_t)it * (PQ_SCAN_WAVES * 64) + threadIdx.x;
+        fv[it] = glut[(i & 31u) * 256u + (i >> 5)];
+    }
+#pragma unroll
+    for (int it = 0; it < FILL; it++) {
+        const uint32_t i = (uint32_t)it * (PQ_SCAN_WAVES * 64) + threadIdx.x;
         const uint32_t s = i & 31u, c = i >> 5;
-        const float v = glut[s * 256u + c];
-        img[c * 64u + s] = f32x2{v, 0.0f};
-        img[c * 64u + 32u + s] = f32x2{0.0f, v};
+        img[c * 64u + s] = f32x2{fv[it], 0.0f};
+        img[c * 64u + 32u + s] = f32x2{0.0f, fv[it]};
     }
     __syncthreads();
     const uint4 *data = reinterpret_cast<const uint4 *>(a.data);
@@ -473,20 +483,20 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_rot_kernel(ScanA
 #pragma unroll
                     for (int w = 0; w < 8; w++)
                         asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(win[w]) : "v"(nmask[w]), "v"(ring[s][w]), "v"(ring[sc][w]));
-                    // two halves of 16 reads, each all in flight before its adds
+                    // batches of NB reads, each all in flight before its adds
 #pragma unroll
-                    for (int h = 0; h < 2; h++) {
-                        f32x2 v[16];
+                    for (int h = 0; h < 32 / NB; h++) {
+                        f32x2 v[NB];
 #pragma unroll
-                        for (int jj = 0; jj < 16; jj++) {
-                            const int j = h * 16 + jj;
+                        for (int jj = 0; jj < NB; jj++) {
+                            const int j = h * NB + jj;
                             // code << 8 by one v_perm (byte j mod 4 into byte 1, zeros elsewhere)
                             const uint32_t c8 = __builtin_amdgcn_perm(0u, win[j >> 2], 0x0C0C000Cu | ((uint32_t)(j & 3) << 8));
                             const uint32_t off = (c8 << 1) + x8;
                             v[jj] = *reinterpret_cast<const f32x2 *>(imgb + off + 8 * j);
                         }
 #pragma unroll
-                        for (int jj = 0; jj < 16; jj++) acc = acc + v[jj];
+                        for (int jj = 0; jj < NB; jj++) acc = acc + v[jj];
                     }
                     if (rt[sc] < t1) tk.offer_dist(wrap_metric(a.metric, acc.x), (uint32_t)(rt[sc] * 64 + lane), rm[sc]);
                     acc = f32x2{acc.y, 0.0f};
@@ -510,11 +520,14 @@ static hipError_t launch_pq_e(const ScanArgs &a, uint64_t *partials, int groups,
     dim3 grid(groups, a.nq), block(PQ_SCAN_WAVES * 64);
     const size_t lds = (size_t)a.pq_m * a.pq_ks * 4;
     if (a.pq_ks == 256 && a.pq_m == 32 && a.nchunks == 2 && tuning().pq_variant != 1) {
-        // 128 KiB LUT image; variant 0 = ring 6, per-wave ranges (A/B: 2 = ring 4, 3 = ring 4 interleaved)
+        // 128 KiB LUT image; variant 0 = ring 6, per-wave ranges, LDS reads in batches of 16
+        // (A/B: 2 = ring 4, 3 = ring 4 interleaved, 4 = batches of 32, 5 = batches of 8)
         switch (tuning().pq_variant) {
-        case 2: launch_timed((scan_pq32_rot_kernel<E, 4, false>), grid, block, 4 * lds, s, a, partials); break;
-        case 3: launch_timed((scan_pq32_rot_kernel<E, 4, true>), grid, block, 4 * lds, s, a, partials); break;
-        default: launch_timed((scan_pq32_rot_kernel<E, 6, false>), grid, block, 4 * lds, s, a, partials); break;
+        case 2: launch_timed((scan_pq32_rot_kernel<E, 4, false, 16>), grid, block, 4 * lds, s, a, partials); break;
+        case 3: launch_timed((scan_pq32_rot_kernel<E, 4, true, 16>), grid, block, 4 * lds, s, a, partials); break;
+        case 4: launch_timed((scan_pq32_rot_kernel<E, 6, false, 32>), grid, block, 4 * lds, s, a, partials); break;
+        case 5: launch_timed((scan_pq32_rot_kernel<E, 6, false, 8>), grid, block, 4 * lds, s, a, partials); break;
+        default: launch_timed((scan_pq32_rot_kernel<E, 6, false, 16>), grid, block, 4 * lds, s, a, partials); break;
         }
         return hipGetLastError();
     }

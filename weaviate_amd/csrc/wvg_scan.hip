@@ -197,11 +197,24 @@ __device__ __forceinline__ void group_combine_publish(WaveTopK<E> &tk, uint64_t 
 #pragma unroll
     for (int e = 0; e < E; e++) sh[wave][e * 64 + lane] = tk.l[e];
     __syncthreads();
-    if (wave == 0) {
-        for (int w = 1; w < WAVES; w++) {
+    // pairwise tree, as group_combine_store
+#pragma unroll
+    for (int half = WAVES / 2; half >= 2; half /= 2) {
+        if (wave < half) {
             uint64_t o[E];
 #pragma unroll
-            for (int e = 0; e < E; e++) o[e] = sh[w][e * 64 + lane];
+            for (int e = 0; e < E; e++) o[e] = sh[wave + half][e * 64 + lane];
+            merge_lists<E>(tk.l, o);
+#pragma unroll
+            for (int e = 0; e < E; e++) sh[wave][e * 64 + lane] = tk.l[e];
+        }
+        __syncthreads();
+    }
+    if (wave == 0) {
+        if (WAVES > 1) {
+            uint64_t o[E];
+#pragma unroll
+            for (int e = 0; e < E; e++) o[e] = sh[1][e * 64 + lane];
             merge_lists<E>(tk.l, o);
         }
 #pragma unroll

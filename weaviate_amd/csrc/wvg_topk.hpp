@@ -239,10 +239,15 @@ struct WaveTopK {
 
 // Workgroup combine: WAVES wave lists -> one sorted list in wave 0, which
 // writes its first K keys to `out` (dense per-workgroup partials: no atomics,
-// so the workgroups that all finish together never contend).
+// so the workgroups that all finish together never contend).  A pairwise tree
+// (log2 WAVES levels of parallel merges) instead of wave 0 merging the other
+// lists one after another: with 16 waves and one workgroup per CU the serial
+// chain of 15 merges was the scan's largest fixed cost.  Keys are unique
+// (slot in the low bits), so the result does not depend on the merge order.
 template <int E, int WAVES>
 __device__ __forceinline__ void group_combine_store(WaveTopK<E> &tk, uint64_t *out)
 {
+    static_assert((WAVES & (WAVES - 1)) == 0, "WAVES must be a power of two");
     __shared__ uint64_t sh[WAVES][64 * E];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -250,14 +255,22 @@ __device__ __forceinline__ void group_combine_store(WaveTopK<E> &tk, uint64_t *o
 #pragma unroll
         for (int e = 0; e < E; e++) sh[wave][e * 64 + lane] = tk.l[e];
         __syncthreads();
+#pragma unroll
+        for (int half = WAVES / 2; half >= 1; half /= 2) {
+            if (wave < half) {
+                uint64_t o[E];
+#pragma unroll
+                for (int e = 0; e < E; e++) o[e] = sh[wave + half][e * 64 + lane];
+                merge_lists<E>(tk.l, o);
+                if (half > 1) {
+#pragma unroll
+                    for (int e = 0; e < E; e++) sh[wave][e * 64 + lane] = tk.l[e];
+                }
+            }
+            if (half > 1) __syncthreads();
+        }
     }
     if (wave != 0) return;
-    for (int w = 1; w < WAVES; w++) {
-        uint64_t o[E];
-#pragma unroll
-        for (int e = 0; e < E; e++) o[e] = sh[w][e * 64 + lane];
-        merge_lists<E>(tk.l, o);
-    }
 #pragma unroll
     for (int e = 0; e < E; e++) {
         const int i = e * 64 + lane;
