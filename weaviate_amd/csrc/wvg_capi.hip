@@ -706,8 +706,13 @@ int wvg_pq_set_codebook(wvg_corpus *c, const float *centers, uint32_t m, uint32_
     if (c->count > 0 && m != c->pq_m) return fail(WVG_ERR_INVALID, "cannot change segments of a non-empty PQ corpus");
     const uint32_t ds = c->dim / m;
     float *dc = nullptr;
-    WVG_HIP(hipMalloc(&dc, (size_t)m * ks * ds * 4));
+    WVG_HIP(hipMalloc(&dc, pq_centers_alloc_bytes(m, ks, ds)));
     WVG_HIP(hipMemcpy(dc, centers, (size_t)m * ks * ds * 4, hipMemcpyHostToDevice));
+    if (pq_has_pairs(ks, ds)) {
+        std::vector<float> pairs((size_t)m * ks * ds);
+        pq_pair_layout(centers, m, ks, pairs.data());
+        WVG_HIP(hipMemcpy(dc + (size_t)m * ks * ds, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice));
+    }
     if (c->d_centers) (void)hipFree(c->d_centers);
     c->d_centers = dc;
     const bool realloc = c->pq_m != m;
@@ -1757,12 +1762,17 @@ int wvg_pq_encode(wvg_ctx *ctx, const float *centers, uint32_t m, uint32_t ks, c
     const uint32_t nch = f32_chunks(dim), ds = dim / m;
     Carver cv;
     const size_t o_x = cv.take(n * dim * 4), o_t = cv.take(tiles_of(n) * 64 * (size_t)nch * 16),
-                 o_c = cv.take((size_t)m * ks * ds * 4), o_o = cv.take(n * m);
+                 o_c = cv.take(pq_centers_alloc_bytes(m, ks, ds)), o_o = cv.take(n * m);
     Bulk bk(ctx);
     rc = bk.begin(cv.off);
     if (rc) return rc;
+    std::vector<float> pairs(pq_has_pairs(ks, ds) ? (size_t)m * ks * ds : 0);
+    if (!pairs.empty()) pq_pair_layout(centers, m, ks, pairs.data());
     WVG_HIP(hipMemcpyAsync(bk.b + o_x, X, n * dim * 4, hipMemcpyHostToDevice, bk.s()));
     WVG_HIP(hipMemcpyAsync(bk.b + o_c, centers, (size_t)m * ks * ds * 4, hipMemcpyHostToDevice, bk.s()));
+    if (!pairs.empty())
+        WVG_HIP(hipMemcpyAsync(bk.b + o_c + (size_t)m * ks * ds * 4, pairs.data(), pairs.size() * 4,
+                               hipMemcpyHostToDevice, bk.s()));
     WVG_HIP(launch_f32_store((const float *)(bk.b + o_x), nullptr, n, dim, nch, 0, (float *)(bk.b + o_t), bk.s()));
     WVG_HIP(launch_pq_encode((const float *)(bk.b + o_t), n, dim, (const float *)(bk.b + o_c), m, ks,
                              (uint8_t *)(bk.b + o_o), bk.s()));

@@ -87,6 +87,22 @@ __host__ __device__ inline uint32_t pq_chunks(uint32_t m) { return (m + 15) / 16
 // it needs at step j straight from the stored words (no per-tile barrel
 // shift); every other reader undoes the rotation with pq32_window.
 __host__ __device__ inline bool pq_rotated(uint32_t m) { return m == 32; }
+// Codebook buffers handed to launch_pq_encode: the [m][ks][ds] table and, for
+// ds == 4 with even ks, the pair-interleaved copy [m][ks/2][4][2] right after
+// it (pq_pair_layout) for the packed two-centroid encoder.
+inline bool pq_has_pairs(uint32_t ks, uint32_t ds) { return ds == 4 && ks % 2 == 0; }
+inline size_t pq_centers_alloc_bytes(uint32_t m, uint32_t ks, uint32_t ds)
+{
+    return (size_t)m * ks * ds * 4 * (pq_has_pairs(ks, ds) ? 2 : 1);
+}
+inline void pq_pair_layout(const float *centers, uint32_t m, uint32_t ks, float *out)
+{
+    for (uint32_t s = 0; s < m; s++)
+        for (uint32_t p = 0; p < ks / 2; p++)
+            for (uint32_t k = 0; k < 4; k++)
+                for (uint32_t h = 0; h < 2; h++)
+                    out[(((size_t)s * (ks / 2) + p) * 4 + k) * 2 + h] = centers[((size_t)s * ks + 2 * p + h) * 4 + k];
+}
 // out byte i = in byte (off + i) mod 32 (off per lane: v_cndmask stages + v_alignbyte)
 __device__ __forceinline__ void pq32_window(const uint32_t (&in)[8], uint32_t off, uint32_t (&out)[8])
 {

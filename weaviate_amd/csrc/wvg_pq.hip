@@ -107,10 +107,15 @@ __device__ __forceinline__ float l2_256_acc(XA x, CA c, int n)
 // space they become s_load_dwordx16 batches whose SGPRs feed the packed
 // subtracts directly -- as generic loads every centroid was a vector load
 // followed by a full-latency wait.
+typedef float f32x2e __attribute__((ext_vector_type(2)));
+
+// pairs (DS == 4, even ks; may be null): the codebook with centroids c and
+// c+1 interleaved per coordinate, [m][ks/2][4][2] (pq_pair_layout), so one
+// scalar register pair feeds a packed op on two centroids at once.
 template <int DS, bool TILED_OUT>
 __global__ void pq_encode_kernel(const float4 *__restrict__ tiled, uint64_t n, uint32_t dim, uint32_t nchunks,
                                  const float *__restrict__ centers, uint32_t m, uint32_t ks, uint32_t ds_rt,
-                                 uint8_t *__restrict__ codes)
+                                 uint8_t *__restrict__ codes, const float *__restrict__ pairs)
 {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
@@ -129,6 +134,31 @@ __global__ void pq_encode_kernel(const float4 *__restrict__ tiled, uint64_t n, u
             if constexpr (DS == 4) {
                 // segment s is exactly chunk s (dim = 4m): one 16-byte load, scalar unfused path (n < 8)
                 const float4 x = rp[(size_t)s * 64];
+                if (pairs) {
+                    // two centroids per packed op: (c_k - x_k)^2 summed in k order,
+                    // exactly the scalar path's sub, mul, add sequence per lane
+                    const f32x2e xx = {x.x, x.x}, xy = {x.y, x.y}, xz = {x.z, x.z}, xw = {x.w, x.w};
+                    const __attribute__((address_space(4))) float *cp =
+                        (const __attribute__((address_space(4))) float *)(pairs + (size_t)s * ks * 4);
+#pragma unroll 4
+                    for (uint32_t p = 0; p < ks / 2; p++) {
+                        const __attribute__((address_space(4))) float *pp = cp + (size_t)p * 8;
+                        const f32x2e d0 = f32x2e{pp[0], pp[1]} - xx, d1 = f32x2e{pp[2], pp[3]} - xy;
+                        const f32x2e d2 = f32x2e{pp[4], pp[5]} - xz, d3 = f32x2e{pp[6], pp[7]} - xw;
+                        f32x2e sum = d0 * d0;
+                        sum = sum + d1 * d1;
+                        sum = sum + d2 * d2;
+                        sum = sum + d3 * d3;
+                        if (!(minD < sum.x)) {
+                            minD = sum.x;
+                            best = 2 * p;
+                        }
+                        if (!(minD < sum.y)) {
+                            minD = sum.y;
+                            best = 2 * p + 1;
+                        }
+                    }
+                } else {
 #pragma unroll 8
                 for (uint32_t c = 0; c < ks; c++) {
                     const __attribute__((address_space(4))) float *cc =
@@ -142,6 +172,7 @@ __global__ void pq_encode_kernel(const float4 *__restrict__ tiled, uint64_t n, u
                         minD = sum;
                         best = c;
                     }
+                }
                 }
             } else {
                 const uint32_t base = s * ds;
@@ -193,16 +224,22 @@ hipError_t launch_pq_encode(const float *tiled, uint64_t n, uint32_t dim, const 
     const uint32_t ds = dim / m, nchunks = f32_chunks(dim);
     dim3 grid((unsigned)((n + 255) / 256)), block(256);
     const float4 *t4 = reinterpret_cast<const float4 *>(tiled);
+    // codebook buffers (pq_centers_alloc_bytes) carry the pair layout after the table
+    const float *pairs = pq_has_pairs(ks, ds) ? centers + (size_t)m * ks * ds : nullptr;
     if (ds == 4 && dim == 4 * m) {
         if (tiled_out)
-            hipLaunchKernelGGL((pq_encode_kernel<4, true>), grid, block, 0, s, t4, n, dim, nchunks, centers, m, ks, ds, codes);
+            hipLaunchKernelGGL((pq_encode_kernel<4, true>), grid, block, 0, s, t4, n, dim, nchunks, centers, m, ks, ds,
+                               codes, pairs);
         else
-            hipLaunchKernelGGL((pq_encode_kernel<4, false>), grid, block, 0, s, t4, n, dim, nchunks, centers, m, ks, ds, codes);
+            hipLaunchKernelGGL((pq_encode_kernel<4, false>), grid, block, 0, s, t4, n, dim, nchunks, centers, m, ks, ds,
+                               codes, pairs);
     } else {
         if (tiled_out)
-            hipLaunchKernelGGL((pq_encode_kernel<0, true>), grid, block, 0, s, t4, n, dim, nchunks, centers, m, ks, ds, codes);
+            hipLaunchKernelGGL((pq_encode_kernel<0, true>), grid, block, 0, s, t4, n, dim, nchunks, centers, m, ks, ds,
+                               codes, nullptr);
         else
-            hipLaunchKernelGGL((pq_encode_kernel<0, false>), grid, block, 0, s, t4, n, dim, nchunks, centers, m, ks, ds, codes);
+            hipLaunchKernelGGL((pq_encode_kernel<0, false>), grid, block, 0, s, t4, n, dim, nchunks, centers, m, ks, ds,
+                               codes, nullptr);
     }
     return hipGetLastError();
 }
