@@ -831,6 +831,8 @@ static SearchPlan plan_search(wvg_corpus *c, uint32_t nq, uint32_t k, const uint
     a.tile_begin = p.tb;
     a.tile_end = p.te;
     a.nq = nq;
+    a.dim = c->kind == WVG_KIND_F32 ? c->dim : 0;  // K1 grid depends on the row size and metric
+    a.metric = c->metric;
     const uint32_t mn = c->ctx->mfma_min_nq;
     p.gemm = c->kind == WVG_KIND_F32 && mn > 0 && nq >= mn && gemm_supported(c->dim, c->metric);
     if (p.gemm)

@@ -210,7 +210,7 @@ hipError_t launch_gemm_topk(const ScanArgs &a, uint32_t nrr, uint64_t *partials,
 // Internal tuning knobs (wvgx_set_tuning; A/B experiments, not public ABI).
 struct Tuning {
     int scan_variant = 0;    // K1 variant (see wvg_scan.hip)
-    int groups_per_cu = 1;   // K1 workgroups per CU (A/B: 1 = fewest partial lists, same scan rate)
+    int groups_per_cu = 0;   // K1 workgroups per CU; 0 = auto by row size (scan_groups_for)
     int gemm_pf = 0;         // K3 register prefetch depth: 0 = by top-k size (2 for k <= 64), 1 = force 1
     int gemm_kernel = 0;     // K3 variant: 0 = K3b (queries resident, rows streamed; 2 waves per SIMD)
                              // where it applies, 2 = K3b with 2 query tiles per wave, 1 = K3

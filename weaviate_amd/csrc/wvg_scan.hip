@@ -382,7 +382,18 @@ int scan_groups_for(const ScanArgs &a, int num_cus)
 {
     const uint64_t ntiles = a.tile_end > a.tile_begin ? a.tile_end - a.tile_begin : 0;
     uint64_t g = (ntiles + SCAN_WAVES * 2 - 1) / (SCAN_WAVES * 2);
-    uint64_t cap = (uint64_t)num_cus * (uint64_t)std::max(1, tuning().groups_per_cu);
+    // groups_per_cu 0 = auto (tools/k1_dim_ab.py, profiles/r01/k1_grid/):
+    // - d <= 128, L2: one per CU (32 KiB of row loads in flight per wave
+    //   already saturate HBM: 7.15 TB/s at 20M x 128; the 1M-row headline
+    //   is 3-6 % slower with two);
+    // - d <= 128, dot / cosine: two (one ran 20M x 128 cosine at 4.2 TB/s,
+    //   two at 6.7);
+    // - d > 128 (F32 only; a.dim is 0 for BQ / PQ): three (a d = 768 row is
+    //   loaded 16 KiB at a time per wave: 4.2 -> 7.15 TB/s at 10M x 768,
+    //   4.2 -> 7.0 at 3M x 1536).
+    int gpc = tuning().groups_per_cu;
+    if (gpc <= 0) gpc = a.dim > 128 ? 3 : (a.dim > 0 && a.metric != WVG_M_L2 ? 2 : 1);
+    uint64_t cap = (uint64_t)num_cus * (uint64_t)gpc;
     if (a.nq > 1) cap = std::max<uint64_t>((uint64_t)num_cus / 4, cap / a.nq);
     if (g > cap) g = cap;
     if (g < 1) g = 1;
