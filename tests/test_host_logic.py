@@ -43,3 +43,40 @@ def test_brute_force_selection_rules(orc):
     assert got_i.tolist() == [77]
     # max_distance <= 0 disables the filter
     assert len(index_queue.brute_force(prov, q, ids, V, -1, max_distance=0.0)[0]) == 10
+
+
+class _OracleCorpus:
+    """Duck-typed stand-in for device.Corpus: distances from the oracle, ids
+    >= n or in `gone` come back ok=False (no GPU needed)."""
+
+    def __init__(self, orc, rows, gone=()):
+        self.orc, self.rows, self.gone = orc, rows, set(int(g) for g in gone)
+
+    def distance_by_ids(self, q, ids):
+        ok = np.array([int(i) < len(self.rows) and int(i) not in self.gone for i in ids], bool)
+        d = np.array([self.orc.l2_256(q, self.rows[int(i)]) if o else 0.0 for i, o in zip(ids, ok)], np.float32)
+        return d, ok
+
+    def distance_by_ids_batch(self, qs, lists):
+        return [self.distance_by_ids(q, ids) for q, ids in zip(qs, lists)]
+
+
+def test_rescore_batch_matches_rescore(orc):
+    """hnsw.rescore_batch keeps rescore's per-query rules (V/hnsw/search.go:564-597):
+    not-ok candidates at distance 0, ef then k, ascending by (distance, docID),
+    empty lists and k <= 0 give empty results."""
+    from weaviate_amd import hnsw
+
+    rng = np.random.default_rng(3)
+    rows = np.floor(rng.uniform(0, 4, (300, 8))).astype(np.float32)  # integer rows: many ties
+    c = _OracleCorpus(orc, rows, gone=[5, 17, 250])
+    qs = np.floor(rng.uniform(0, 4, (5, 8))).astype(np.float32)
+    lists = [rng.choice(320, size=s, replace=False).astype(np.uint64) for s in (40, 0, 1, 120, 7)]
+    for k, ef in [(10, None), (10, 20), (3, 2), (50, 500)]:
+        got = hnsw.rescore_batch(c, qs, lists, k, ef)
+        for q, ids, (gi, gd) in zip(qs, lists, got):
+            wi, wd = hnsw.rescore(c, q, ids, k, ef)
+            assert np.array_equal(gi, wi) and np.array_equal(gd.view(np.uint32), wd.view(np.uint32))
+            if ids.size:
+                assert len(gi) == min(k, ef if ef is not None else ids.size, ids.size)
+    assert all(len(i) == 0 for i, _ in hnsw.rescore_batch(c, qs, lists, 0))
