@@ -96,3 +96,21 @@ def test_sdc_table_and_distance(ctx, orc, metric_name, metric):
     assert pq.DistanceBetweenCompressedVectors(codes[1], codes[2][:3])[1] == "inconsistent compressed vectors lengths"
     # Decode: concatenated centroids (CH/product_quantization.go:428-434)
     assert np.array_equal(pq.Decode(codes[3]), np.concatenate([centers[i, codes[3][i]] for i in range(m)]))
+
+
+def test_pq_codebook_commitlog_restore(ctx, orc):
+    """Fit on the GPU -> ExposeFields -> AddPQ record (V/hnsw/condensor.go:266-285)
+    -> ReadPQ (V/hnsw/deserializer.go:532-590) -> NewProductQuantizerWithEncoders:
+    the restored quantizer encodes and scores bit-identically to the trained one."""
+    from weaviate_amd.compressionhelpers import add_pq_record, read_pq_record
+
+    X = orc.synth_rows(430, 0, 4000, 64, 0)
+    pq = ProductQuantizer.fit(ctx, X, 16, 64, training_limit=0, seed=11)
+    data, used = read_pq_record(add_pq_record(pq.ExposeFields()), 1)
+    back = ProductQuantizer.from_pq_data(ctx, data)
+    codes = pq.EncodeBatch(X[:1000])
+    assert np.array_equal(back.EncodeBatch(X[:1000]), codes)
+    assert np.array_equal(codes, orc.pq_encode(X[:1000], pq.centers))
+    q = X[1234]
+    assert np.array_equal(bits(back.NewDistancer(q).DistanceBatch(codes)), bits(pq.NewDistancer(q).DistanceBatch(codes)))
+    assert np.array_equal(bits(back.SDCBatch(codes[0], codes)), bits(pq.SDCBatch(codes[0], codes)))

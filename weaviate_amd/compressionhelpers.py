@@ -134,6 +134,92 @@ class ProductQuantizer:
     def NewDistancer(self, q):
         return PQDistancer(self, np.asarray(q, dtype=np.float32), self.CenterAt(q))
 
+    def ExposeFields(self) -> "PQData":
+        """:285-295 -- the fields the HNSW commit log persists (compress.go:89)."""
+        return PQData(Ks=self.ks, M=self.m, Dimensions=self.dimensions, EncoderType=USE_KMEANS_ENCODER,
+                      EncoderDistribution=0, Centers=self.centers.copy())
+
+    @classmethod
+    def from_pq_data(cls, ctx, data: "PQData", distance: str = "l2-squared"):
+        """NewProductQuantizerWithEncoders (:224-234) from a restored AddPQ record."""
+        if data.EncoderType != USE_KMEANS_ENCODER:
+            raise ValueError("tile encoder is out of scope: only the k-means encoder runs on the GPU")
+        return cls(ctx, data.Centers, distance)
+
+
+# --- codebook persistence: the HNSW commit log's AddPQ record ------------------
+# Writer: MemoryCondensor.AddPQ (V/hnsw/condensor.go:266-285).  Reader: the
+# AddPQ case of Deserializer.Do (V/hnsw/deserializer.go:143-145) -> ReadPQ
+# (:532-590) -> ReadKMeansEncoder (:509-530).  All integers little-endian; each
+# k-means encoder's payload is KMeans.ExposeDataForRestore (CH/kmeans.go:85-93):
+# ks*ds float32 LE, centroid-major.
+
+ADD_PQ = 11  # HnswCommitType AddPQ (V/hnsw/commit_logger.go:266-280: iota, 12th value)
+USE_TILE_ENCODER = 0  # CH/product_quantization.go:28-31
+USE_KMEANS_ENCODER = 1
+
+
+class PQData:
+    """compressionhelpers.PQData (CH/product_quantization.go:170-179), with the
+    k-means encoders held as one [m][ks][ds] float32 array."""
+
+    def __init__(self, Ks, M, Dimensions, EncoderType=USE_KMEANS_ENCODER, EncoderDistribution=0,
+                 UseBitsEncoding=False, Centers=None):
+        self.Ks, self.M, self.Dimensions = int(Ks), int(M), int(Dimensions)
+        self.EncoderType, self.EncoderDistribution = int(EncoderType), int(EncoderDistribution)
+        self.UseBitsEncoding = bool(UseBitsEncoding)
+        self.Centers = None if Centers is None else np.ascontiguousarray(Centers, dtype=np.float32)
+
+    def __eq__(self, other):
+        return (isinstance(other, PQData)
+                and (self.Ks, self.M, self.Dimensions, self.EncoderType, self.EncoderDistribution,
+                     self.UseBitsEncoding) == (other.Ks, other.M, other.Dimensions, other.EncoderType,
+                                               other.EncoderDistribution, other.UseBitsEncoding)
+                and self.Centers.shape == other.Centers.shape
+                and np.array_equal(self.Centers.view(np.uint32), other.Centers.view(np.uint32)))
+
+
+def add_pq_record(data: PQData) -> bytes:
+    """MemoryCondensor.AddPQ: the full record, commit-type byte included."""
+    if data.EncoderType != USE_KMEANS_ENCODER:
+        raise ValueError("tile encoder is out of scope: only k-means codebooks are written")
+    ds = data.Dimensions // data.M if data.M else 0
+    c = np.ascontiguousarray(data.Centers, dtype="<f4")
+    if c.shape != (data.M, data.Ks, ds):
+        raise ValueError(f"centers shape {c.shape} != (m, ks, ds) = {(data.M, data.Ks, ds)}")
+    head = np.zeros(10, np.uint8)
+    head[0] = ADD_PQ
+    head[1:3] = np.frombuffer(np.uint16(data.Dimensions).astype("<u2").tobytes(), np.uint8)
+    head[3] = data.EncoderType
+    head[4:6] = np.frombuffer(np.uint16(data.Ks).astype("<u2").tobytes(), np.uint8)
+    head[6:8] = np.frombuffer(np.uint16(data.M).astype("<u2").tobytes(), np.uint8)
+    head[8] = data.EncoderDistribution
+    head[9] = 1 if data.UseBitsEncoding else 0
+    return head.tobytes() + c.tobytes()
+
+
+def read_pq_record(buf, offset: int = 0):
+    """Deserializer.ReadPQ on `buf` starting after the commit-type byte.
+    Returns (PQData, bytes consumed); raises ValueError with the reference's
+    messages on a short read or an unknown encoder type."""
+    mv = memoryview(bytes(buf))[offset:]
+    if len(mv) < 9:
+        what = "uint16" if len(mv) < 2 or 3 <= len(mv) < 7 else "byte"
+        raise ValueError(f"failed to read {what}")
+    dims, enc = int.from_bytes(mv[0:2], "little"), mv[2]
+    ks, m = int.from_bytes(mv[3:5], "little"), int.from_bytes(mv[5:7], "little")
+    dist, bits = mv[7], mv[8]
+    if enc == USE_TILE_ENCODER:
+        raise ValueError("tile encoder is out of scope: only k-means codebooks are restored")
+    if enc != USE_KMEANS_ENCODER:
+        raise ValueError("Unsuported encoder type")  # sic, deserializer.go:574
+    ds = dims // m if m else 0
+    need = 4 * m * ks * ds
+    if len(mv) - 9 < need:
+        raise ValueError("failed to read float32")
+    centers = np.frombuffer(mv[9:9 + need], dtype="<f4").astype(np.float32).reshape(m, ks, ds)
+    return PQData(ks, m, dims, enc, dist, bits != 0, centers), 9 + need
+
 
 class PQDistancer:
     def __init__(self, pq, x, lut):
