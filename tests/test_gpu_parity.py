@@ -597,3 +597,41 @@ def test_batched_mfma_variants(ctx, orc, variant, metric, d):
                 check_topk(orc, ids[qi], dists[qi], counts[qi], all_d, np.arange(n, dtype=np.uint64), k, vm)
     finally:
         lib.wvgx_set_tuning(4, old)
+
+
+# Full size (BASELINE config 4): 100M x 128 L2, PQ m=32 ks=256 -- bulk encode on
+# the device, then ADC top-10 over all 100M codes; checked by properties on
+# sampled rows (the oracle cannot encode and scan 100M rows in seconds).
+@pytest.mark.slow
+def test_full_size_pq_100m_properties(ctx, orc):
+    n, d, m, ks, k = 100_000_000, 128, 32, 256, 10
+    f = Corpus(ctx, KIND_F32, METRIC_L2, d, n)
+    f.fill_synthetic(42, n, 0)
+    centers = np.ascontiguousarray(orc.synth_rows(42, 0, ks, d, 0).reshape(ks, m, d // m).transpose(1, 0, 2))
+    pq = Corpus(ctx, KIND_PQ, METRIC_L2, d, n)
+    pq.set_codebook(centers)
+    _lib.check(_lib.load().wvg_pq_encode_corpus(pq.handle, f.handle))
+    f.destroy()
+    # sampled rows at the start, the middle and the end: codes bit-exact vs the oracle
+    starts = [0, n // 2 - 7, n - 20_000]
+    sample_ids = np.concatenate([np.arange(s, s + 20_000, dtype=np.int64) for s in starts])
+    srows = np.concatenate([orc.synth_rows(42, s, 20_000, d, 0) for s in starts])
+    scodes = orc.pq_encode(srows, centers)
+    for j in range(0, len(sample_ids), 997):
+        assert np.array_equal(pq.get(int(sample_ids[j]), pq_m=m), scodes[j]), int(sample_ids[j])
+    qs = orc.synth_rows(43, 0, 3, d, 0)
+    ids, dists, counts = pq.search(qs, k)
+    for qi in range(len(qs)):
+        assert counts[qi] == k
+        assert np.all(np.diff(orc.ord_key(dists[qi]).astype(np.int64)) >= 0)
+        lut = orc.pq_lut(0, qs[qi], centers)
+        # each returned distance is the sequential ADC sum of that row's stored code
+        for i, dv in zip(ids[qi], dists[qi]):
+            assert bits(orc.pq_adc(0, lut, pq.get(int(i), pq_m=m))) == bits(dv)
+        # no sampled row outside the result beats the k-th result (lexicographic (dist, id))
+        sd = np.array([orc.pq_adc(0, lut, c) for c in scodes], np.float32)
+        outside = ~np.isin(sample_ids, ids[qi].astype(np.int64))
+        kth = (int(orc.ord_key(dists[qi][-1:])[0]), int(ids[qi][-1]))
+        sk = orc.ord_key(sd[outside]).astype(np.int64)
+        assert np.all((sk > kth[0]) | ((sk == kth[0]) & (sample_ids[outside] > kth[1])))
+    pq.destroy()
