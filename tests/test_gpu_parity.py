@@ -635,3 +635,33 @@ def test_full_size_pq_100m_properties(ctx, orc):
         sk = orc.ord_key(sd[outside]).astype(np.int64)
         assert np.all((sk > kth[0]) | ((sk == kth[0]) & (sample_ids[outside] > kth[1])))
     pq.destroy()
+
+
+# Full size (BASELINE config 3): 100M x 1536 BQ (W = 24 words) cosine, Hamming
+# top-200 over all 100M device-resident codes (the 614 GB of float rows do not
+# fit, so the rescore stage is covered at small sizes above).
+@pytest.mark.slow
+def test_full_size_bq_100m_x_1536_properties(ctx, orc):
+    n, d, R = 100_000_000, 1536, 200
+    w = (d + 63) // 64
+    c = Corpus(ctx, KIND_BQ, METRIC_COSINE, d, n)
+    c.fill_synthetic(42, n, 0)
+    starts = [0, n // 2 - 13, n - 10_000]
+    sample_ids = np.concatenate([np.arange(s, s + 10_000, dtype=np.int64) for s in starts])
+    scodes = np.stack([orc.bq_encode(orc.normalize(r)) for s in starts for r in orc.synth_rows(42, s, 10_000, d, 0)])
+    for j in range(0, len(sample_ids), 499):
+        assert np.array_equal(c.get(int(sample_ids[j])), scodes[j]), int(sample_ids[j])
+    qs = orc.synth_rows(43, 0, 2, d, 0)
+    ids, dists, counts = c.search(qs, R)
+    for qi in range(len(qs)):
+        assert counts[qi] == R
+        assert np.all(np.diff(dists[qi]) >= 0)
+        qc = orc.bq_encode(orc.normalize(qs[qi]))
+        got = np.stack([c.get(int(i)) for i in ids[qi]])
+        assert got.shape == (R, w)
+        assert np.array_equal(bits(orc.bq_dist_all(qc, got)), bits(dists[qi]))
+        sd = orc.bq_dist_all(qc, scodes)
+        outside = ~np.isin(sample_ids, ids[qi].astype(np.int64))
+        kd, kid = float(dists[qi][-1]), int(ids[qi][-1])
+        assert np.all((sd[outside] > kd) | ((sd[outside] == kd) & (sample_ids[outside] > kid)))
+    c.destroy()
