@@ -665,3 +665,31 @@ def test_full_size_bq_100m_x_1536_properties(ctx, orc):
         kd, kid = float(dists[qi][-1]), int(ids[qi][-1])
         assert np.all((sd[outside] > kd) | ((sd[outside] == kd) & (sample_ids[outside] > kid)))
     c.destroy()
+
+
+# Full size (BASELINE config 2): 10M x 768 fp32 cosine, one 1024-query batch
+# through the batched MFMA path (K3b) -- properties on sampled rows and queries.
+@pytest.mark.slow
+def test_full_size_batched_10m_x_768_cosine_properties(ctx, orc):
+    n, d, nq, k = 10_000_000, 768, 1024, 10
+    c = Corpus(ctx, KIND_F32, METRIC_COSINE, d, n)
+    c.fill_synthetic(42, n, 0)
+    starts = [0, n // 2 - 3, n - 10_000]
+    sample_ids = np.concatenate([np.arange(s, s + 10_000, dtype=np.int64) for s in starts])
+    srows = np.concatenate([orc.normalize_rows(orc.synth_rows(42, s, 10_000, d, 0)) for s in starts])
+    for j in range(0, len(sample_ids), 997):
+        assert np.array_equal(bits(c.get(int(sample_ids[j]))), bits(srows[j])), int(sample_ids[j])
+    qs = orc.synth_rows(43, 0, nq, d, 0)
+    ids, dists, counts = c.search(qs, k)
+    assert np.all(counts == k)
+    for qi in (0, 1, 511, 1023):
+        q = orc.normalize(qs[qi])
+        assert np.all(np.diff(orc.ord_key(dists[qi]).astype(np.int64)) >= 0)
+        got = orc.normalize_rows(np.stack([orc.synth_rows(42, int(i), 1, d, 0)[0] for i in ids[qi]]))
+        assert np.array_equal(bits(orc.dist_all(2, q, got)), bits(dists[qi]))
+        sd = orc.dist_all(2, q, srows)
+        outside = ~np.isin(sample_ids, ids[qi].astype(np.int64))
+        kth = (int(orc.ord_key(dists[qi][-1:])[0]), int(ids[qi][-1]))
+        sk = orc.ord_key(sd[outside]).astype(np.int64)
+        assert np.all((sk > kth[0]) | ((sk == kth[0]) & (sample_ids[outside] > kth[1])))
+    c.destroy()
