@@ -693,3 +693,31 @@ def test_full_size_batched_10m_x_768_cosine_properties(ctx, orc):
         sk = orc.ord_key(sd[outside]).astype(np.int64)
         assert np.all((sk > kth[0]) | ((sk == kth[0]) & (sample_ids[outside] > kth[1])))
     c.destroy()
+
+
+# Full size (BASELINE config 5, one GPU's share): a 125M x 128 fp32 L2 slab
+# holding global docIDs [375M, 500M) (slab 3 of 8), exact 100-NN.
+@pytest.mark.slow
+def test_full_size_slab_125m_global_ids_properties(ctx, orc):
+    n, d, k, base = 125_000_000, 128, 100, 375_000_000
+    c = Corpus(ctx, KIND_F32, METRIC_L2, d, n, id_base=base)
+    c.fill_synthetic(42, n, 0)
+    starts = [base, base + n // 2 - 5, base + n - 20_000]
+    sample_ids = np.concatenate([np.arange(s, s + 20_000, dtype=np.int64) for s in starts])
+    srows = np.concatenate([orc.synth_rows(42, s, 20_000, d, 0) for s in starts])
+    for j in range(0, len(sample_ids), 997):
+        assert np.array_equal(bits(c.get(int(sample_ids[j]))), bits(srows[j])), int(sample_ids[j])
+    qs = orc.synth_rows(43, 0, 2, d, 0)
+    ids, dists, counts = c.search(qs, k)
+    for qi in range(len(qs)):
+        assert counts[qi] == k
+        assert np.all((ids[qi] >= base) & (ids[qi] < base + n))
+        assert np.all(np.diff(orc.ord_key(dists[qi]).astype(np.int64)) >= 0)
+        got = np.stack([orc.synth_rows(42, int(i), 1, d, 0)[0] for i in ids[qi]])
+        assert np.array_equal(bits(orc.dist_all(0, qs[qi], got)), bits(dists[qi]))
+        sd = orc.dist_all(0, qs[qi], srows)
+        outside = ~np.isin(sample_ids, ids[qi].astype(np.int64))
+        kth = (int(orc.ord_key(dists[qi][-1:])[0]), int(ids[qi][-1]))
+        sk = orc.ord_key(sd[outside]).astype(np.int64)
+        assert np.all((sk > kth[0]) | ((sk == kth[0]) & (sample_ids[outside] > kth[1])))
+    c.destroy()
