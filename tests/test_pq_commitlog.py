@@ -64,3 +64,21 @@ def test_read_pq_record_errors():
         read_pq_record(bytes(bad))
     with pytest.raises(ValueError, match="centers shape"):
         add_pq_record(PQData(4, 3, 6, 1, 0, False, CENTERS[:2]))
+
+
+def test_pq_config_errors():
+    """NewProductQuantizer's checks (CH/product_quantization.go:190-207) in the
+    order and with the messages of CH/product_quantization_test.go:132-233."""
+    from weaviate_amd import _lib
+    from weaviate_amd.compressionhelpers import validate_pq_config
+
+    for args, msg in [((4, 256, 128, "kmeans-x", "log-normal"), "invalid encoder type"),
+                      ((4, 256, 128, "kmeans", "normal-x"), "invalid encoder distribution"),
+                      ((0, 256, 128), "segments cannot be 0 nor negative"),
+                      ((-2, 256, 128), "segments cannot be 0 nor negative"),
+                      ((3, 256, 128), "segments should be an integer divisor of dimensions"),
+                      ((4, 512, 128), "centroids should not be higher than 256. Attempting to use 512")]:
+        with pytest.raises(_lib.WvgError, match=msg):
+            validate_pq_config(*args)
+    assert validate_pq_config(4, 256, 128) == (1, 1)  # defaults: kmeans, log-normal
+    assert validate_pq_config(4, 256, 128, "tile", "normal") == (0, 0)

@@ -59,21 +59,27 @@ class ProductQuantizer:
         self.m, self.ks, self.ds = self.centers.shape
         self.dimensions = self.m * self.ds
         self.metric = METRIC_BY_NAME[distance]
+        self.encoder_distribution = LOG_NORMAL_DISTRIBUTION  # DefaultPQEncoderDistribution (pq_config.go:32)
         self.fit_passes = None
         self._global = None
 
     @classmethod
     def fit(cls, ctx, data, segments: int, centroids: int = 256, distance: str = "l2-squared",
-            training_limit: int = DEFAULT_TRAINING_LIMIT, seed: int = 0):
+            training_limit: int = DEFAULT_TRAINING_LIMIT, seed: int = 0, encoder: str = "kmeans",
+            distribution: str = "log-normal"):
         """NewProductQuantizer + Fit (CH/product_quantization.go:155-229, :372-418)
         with the k-means encoder, trained on the GPU (wvg_pq_fit)."""
         X = np.ascontiguousarray(data, dtype=np.float32)
         n, d = X.shape
+        enc, dist = validate_pq_config(segments, centroids, d, encoder, distribution)
+        if enc != USE_KMEANS_ENCODER:
+            raise ValueError("tile encoder is out of scope: only the k-means encoder runs on the GPU")
         centers = np.empty((segments, centroids, d // segments if segments else 0), dtype=np.float32)
         passes = np.zeros(segments, dtype=np.uint32)
         check(ctx.lib.wvg_pq_fit(ctx.handle, fptr(X), n, d, segments, centroids, training_limit, seed,
                                  fptr(centers), u32ptr(passes)))
         pq = cls(ctx, centers, distance)
+        pq.encoder_distribution = dist
         pq.fit_passes = passes
         return pq
 
@@ -137,14 +143,41 @@ class ProductQuantizer:
     def ExposeFields(self) -> "PQData":
         """:285-295 -- the fields the HNSW commit log persists (compress.go:89)."""
         return PQData(Ks=self.ks, M=self.m, Dimensions=self.dimensions, EncoderType=USE_KMEANS_ENCODER,
-                      EncoderDistribution=0, Centers=self.centers.copy())
+                      EncoderDistribution=self.encoder_distribution, Centers=self.centers.copy())
 
     @classmethod
     def from_pq_data(cls, ctx, data: "PQData", distance: str = "l2-squared"):
         """NewProductQuantizerWithEncoders (:224-234) from a restored AddPQ record."""
         if data.EncoderType != USE_KMEANS_ENCODER:
             raise ValueError("tile encoder is out of scope: only the k-means encoder runs on the GPU")
-        return cls(ctx, data.Centers, distance)
+        pq = cls(ctx, data.Centers, distance)
+        pq.encoder_distribution = data.EncoderDistribution
+        return pq
+
+
+NORMAL_DISTRIBUTION, LOG_NORMAL_DISTRIBUTION = 0, 1  # CH/tile_encoder.go:89-90
+
+
+def validate_pq_config(segments: int, centroids: int, dimensions: int, encoder: str = "kmeans",
+                       distribution: str = "log-normal"):
+    """The checks of NewProductQuantizer (CH/product_quantization.go:190-207),
+    in the same order and with the same messages; parseEncoder /
+    parseEncoderDistribution (:257-277; names from entities/vectorindex/hnsw/
+    pq_config.go:21-24).  Returns (encoder type, distribution byte);
+    raises WvgError(WVG_ERR_INVALID), as the C ABI does for the same checks."""
+    if segments <= 0:
+        raise _lib.WvgError(_lib.WVG_ERR_INVALID, "segments cannot be 0 nor negative")
+    if centroids > 256:
+        raise _lib.WvgError(_lib.WVG_ERR_INVALID, f"centroids should not be higher than 256. Attempting to use {centroids}")
+    if dimensions % segments != 0:
+        raise _lib.WvgError(_lib.WVG_ERR_INVALID, "segments should be an integer divisor of dimensions")
+    enc = {"tile": USE_TILE_ENCODER, "kmeans": USE_KMEANS_ENCODER}.get(encoder)
+    if enc is None:
+        raise _lib.WvgError(_lib.WVG_ERR_INVALID, "invalid encoder type")
+    dist = {"log-normal": LOG_NORMAL_DISTRIBUTION, "normal": NORMAL_DISTRIBUTION}.get(distribution)
+    if dist is None:
+        raise _lib.WvgError(_lib.WVG_ERR_INVALID, "invalid encoder distribution")
+    return enc, dist
 
 
 # --- codebook persistence: the HNSW commit log's AddPQ record ------------------
