@@ -2,24 +2,38 @@
 """bench.py -- BASELINE metric: exact 10-NN QPS + achieved HBM GB/s,
 1M x 128 fp32 L2 flat scan, 1/2/4/8-GPU scaling.
 
-Workload (BASELINE.json configs[0] shape, on the GPU): every GPU holds a
-1,000,000 x 128 fp32 shard (global docIDs rank*1M ..), generated in HBM by a
-counter-based RNG.  A step is a batch of B single-query searches: each query
-is one full scan of the shard (one K1 scan launch per query, flat.searchByVector
-semantics; each launch also runs the previous query's top-k merge on one extra
-workgroup -- wvg_search_device_pipelined), then -- for N > 1 -- one RCCL
-all-gather of the B x k (dist, id) candidates and one device merge
-(Index.objectVectorSearch's shard merge).  Weak scaling: value = query
-scans of 1M rows per second over all GPUs = N * B * steps / time.
+Default workload (``--workload flat1m``, BASELINE.json configs[0] shape on
+the GPU): every GPU holds a 1,000,000 x 128 fp32 shard (global docIDs
+rank*1M ..), generated in HBM by a counter-based RNG.  A step is a batch of B
+single-query searches: each query is one full scan of the shard
+(flat.searchByVector semantics; all B in one query-stream launch,
+wvg_search_device_pipelined) written straight into this rank's packed result
+block, then -- for N > 1 -- ONE RCCL all-gather of the blocks and one device
+merge (Index.objectVectorSearch's shard merge, adapters/repos/db/index.go:
+1567-1648).  Weak scaling: value = query scans of 1M rows per second over all
+GPUs = N * B * steps / time.
 
-Run:  python bench.py [--gpus N --steps K --warmup W]
-      (N > 1 via torch.distributed.run, one process per GPU, RCCL)
+``--workload slab1b`` (BASELINE.json configs[4]): the 1B x 128 fp32 L2 corpus
+as 8 slabs of 125M rows, exact 100-NN.  The slabs are dealt to the N GPUs
+(8/N each); a GPU holds one slab in HBM at a time, regenerated in place
+between slabs (generation untimed), scans every step's B queries over it,
+then the per-slab lists are merged on device and -- for N > 1 -- exchanged
+with one all-gather per step.  Strong scaling: value = 1B-row queries per
+second; at N = 1 this is the "8 sequential slabs" QPS_1 of SURVEY.md 8(d).
+
+Run:  python bench.py [--gpus N --steps K --warmup W] [--workload flat1m|slab1b]
+      N > 1: launched by the driver through torch.distributed.run (one
+      process per GPU, RCCL); started directly with --gpus N it re-launches
+      itself that way (before touching any GPU) and exits with its status.
+      --dry-run: CPU-only rehearsal of the launch and the exchange (gloo).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -32,139 +46,209 @@ METRIC = "exact 10-NN QPS + achieved HBM GB/s, 1M×128 L2 flat; 1/2/4/8 GPU scal
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=16, help="single-query searches per step")
-    ap.add_argument("--rows", type=int, default=1_000_000, help="rows per GPU")
+    ap.add_argument("--workload", choices=["flat1m", "slab1b"], default="flat1m")
+    ap.add_argument("--batch", type=int, default=0, help="single-query searches per step (default 16; slab1b 8)")
+    ap.add_argument("--rows", type=int, default=0, help="flat1m: rows per GPU; slab1b: total rows (default 1e9)")
     ap.add_argument("--dim", type=int, default=128)
-    ap.add_argument("--k", type=int, default=10)
-    ap.add_argument("--cpu-queries", type=int, default=4096)
+    ap.add_argument("--k", type=int, default=0, help="neighbours (default 10; slab1b 100)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target wall time of each multi-core CPU leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    return ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true", help="CPU-only rehearsal of the N-rank launch + exchange")
+    a = ap.parse_args(argv)
+    slab = a.workload == "slab1b"
+    a.batch = a.batch or (8 if slab else 16)
+    a.k = a.k or (100 if slab else 10)
+    a.rows = a.rows or (1_000_000_000 if slab else 1_000_000)
+    return a
 
 
-def cpu_baseline(rows_n, d, k, qs, gpu_ids):
-    """Weaviate's CPU flat path on this host: the reference's own l2_256
-    (oracle/_ref, built from /root/reference) when this CPU can run it, else the
-    oracle's bit-identical restatement; bounded max-heap top-k; one query per
-    thread (CH/utils.go:25-42 Concurrently), plus a single-core sample."""
+# ---------------------------------------------------------------------------
+# N-rank launch
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def relaunch(n: int) -> int:
+    """Runs this script under torch.distributed.run with n local ranks (a child
+    process; this process has not touched a GPU) and returns its exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline (rank 0, N = 1): the reference's CPU flat / BQ paths on this host
+def cpu_share() -> tuple[int, int, str]:
+    """(CPUs this process may use, CPUs of the machine, how it was determined):
+    the affinity mask, capped by a cgroup CPU quota (the GPU box gives each
+    job a share of a large host)."""
+    total = os.cpu_count() or 1
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else total
+    how = "sched_getaffinity"
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            q = max(1, int(int(quota) // int(period)))
+            if q < n:
+                n, how = q, "cgroup cpu.max quota"
+    except (OSError, ValueError):
+        pass
+    v = os.environ.get("OMP_NUM_THREADS", "")  # the GPU box's declared per-job CPU share
+    if v.isdigit() and 0 < int(v) < n and "TORCHELASTIC_RUN_ID" not in os.environ:  # (torchrun sets it to 1)
+        n, how = int(v), f"OMP_NUM_THREADS={v} (job CPU share)"
+    return n, total, how
+
+
+def _sized(run_fn, per_query_probe: int, target_s: float, threads: int, cap: int) -> int:
+    """Queries for about target_s seconds of wall time on `threads` threads."""
+    t = run_fn(per_query_probe, 1)
+    per_q = max(t / per_query_probe, 1e-5)
+    return int(max(threads, min(cap, target_s * threads / per_q)))
+
+
+def cpu_baseline(rows_n, d, k, gpu_ids, target_s):
+    """Weaviate's CPU flat path (findTopVectors: l2_256 + bounded max-heap,
+    V/flat/index.go:411-452) and BQ path (findTopVectorsCached Hamming top-200
+    + exact rescore, :347-389, 456-495) over the same 1M x 128 rows, with the
+    reference's own l2_256 (oracle/_ref, built from /root/reference's C) when
+    this CPU runs it, else the oracle's bit-identical restatement; one query
+    per thread (CH/utils.go:25-42 Concurrently) on every CPU of this job's
+    share, plus a single-core sample (Weaviate's flat scan of one query is
+    single-threaded).  Resident float32 matrix: no LSM cursor / decode, so an
+    upper bound on Weaviate's CPU QPS."""
     from oracle import wv_oracle as orc
 
     flags = open("/proc/cpuinfo").read()
-    can_ref = orc.ref() is not None and " avx512f" in flags and " fma" in flags
+    can_ref = orc.ref() is not None and " avx2" in flags and " fma" in flags
+    model = next((ln.split(":", 1)[1].strip() for ln in flags.splitlines() if ln.startswith("model name")), "")
+    threads, total, how = cpu_share()
     rows = orc.synth_rows(42, 0, rows_n, d, 0)
-    threads = max(1, min(16, os.cpu_count() or 1))
-    nq = len(qs)
-    secs, ids, dists, used_ref = orc.bench_flat(rows, qs, k, orc.L2, threads, use_ref_kernel=can_ref)
-    n1 = min(8, nq)
-    secs1, _, _, _ = orc.bench_flat(rows, qs[:n1], k, orc.L2, 1, use_ref_kernel=can_ref)
+    qs = np.random.default_rng(43).uniform(-1, 1, (32768, d)).astype(np.float32)
+
+    def flat(nq, th):
+        return orc.bench_flat(rows, qs[:nq], k, orc.L2, th, use_ref_kernel=can_ref)[0]
+
+    nq = _sized(flat, 4, target_s, threads, len(qs))
+    secs, ids, _, used_ref = orc.bench_flat(rows, qs[:nq], k, orc.L2, threads, use_ref_kernel=can_ref)
+    n1 = min(nq, max(4, int(nq / threads / 4)))
+    secs1 = flat(n1, 1)
     match = bool(np.array_equal(ids[: len(gpu_ids)], gpu_ids))
-    model = ""
-    for line in flags.splitlines():
-        if line.startswith("model name"):
-            model = line.split(":", 1)[1].strip()
-            break
+    # BQ cache flow over the same rows (codes prebuilt, as the cache is at PostStartup)
+    codes = orc.bq_encode_rows(rows)
+    R = 200
+
+    def bq(nqb, th):
+        return orc.bench_flat_bq(rows, codes, qs[:nqb], k, R, orc.L2, th, use_ref_kernel=can_ref)[0]
+
+    nqb = _sized(bq, 8, target_s, threads, len(qs))
+    secs_b = bq(nqb, threads)
+    nb1 = min(nqb, max(8, int(nqb / threads / 4)))
+    secs_b1 = bq(nb1, 1)
+    kernel = "l2_256 compiled from the reference's C source (oracle/_ref)" if used_ref else \
+        "oracle restatement of l2_256"
     return {
         "value": round(nq / secs, 3),
         "unit": "queries/s",
         "cores": threads,
         "kind": "reference" if used_ref else "port",
-        "sample": (f"{nq} queries over the same 1M x 128 rows (resident float32 matrix, no LSM cursor/decode), "
-                   f"one query per thread on {threads} threads, {secs:.1f} s wall; kernel "
-                   + ("l2_256 from the reference's C source (oracle/_ref)" if used_ref else
-                      "oracle restatement of l2_256") + f"; cpu: {model}"),
+        "sample": (f"{nq} exact 10-NN queries over the same {rows_n:,} x {d} rows (resident float32 matrix, "
+                   f"no LSM cursor/decode), one query per thread on {threads} threads ({how}; host has {total} "
+                   f"CPUs), {secs:.1f} s wall; kernel {kernel}; cpu: {model}"),
         "single_core_qps": round(n1 / secs1, 3),
+        "host_cpus": total,
         "ids_match_gpu": match,
+        "bq": {
+            "value": round(nqb / secs_b, 3),
+            "unit": "queries/s",
+            "cores": threads,
+            "single_core_qps": round(nb1 / secs_b1, 3),
+            "sample": (f"{nqb} flat BQ searches (Hamming top-{R} over prebuilt BQ codes with POPCNT, exact "
+                       f"rescore of {R} rows, top-{k}; V/flat/index.go:347-389) over the same rows, "
+                       f"{secs_b:.1f} s wall on {threads} threads"),
+        },
     }
 
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
+# ---------------------------------------------------------------------------
+def _timed(fn, dist, world, dev, torch):
+    """Barrier + synchronize on both sides of fn(); returns the max over ranks."""
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    fn()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el
 
-    from weaviate_amd import _lib
+
+def run_flat1m(args, world, rank, dev, torch, dist):
     from weaviate_amd._lib import KIND_F32, METRIC_L2, check
     from weaviate_amd.device import Context, Corpus
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    from weaviate_amd.shard import all_gather_packed
 
     n, d, k, B = args.rows, args.dim, args.k, args.batch
     cap = (n + 63) // 64 * 64
-    ctx = Context(local)
+    ctx = Context(dev.index)
     lib = ctx.lib
     corpus = Corpus(ctx, KIND_F32, METRIC_L2, d, cap, id_base=rank * cap)
     corpus.fill_synthetic(42, n, 0)
 
     P = 64  # distinct queries cycled through the steps
+    assert P % B == 0
     qs = np.random.default_rng(43).uniform(-1, 1, (P, d)).astype(np.float32)
     tq = torch.from_numpy(qs).to(dev)
-    ids = torch.empty((B, k), dtype=torch.int64, device=dev)
-    dists = torch.empty((B, k), dtype=torch.float32, device=dev)
+    blk = lib.wvg_topk_packed_bytes(B, k)
+    send = torch.empty(blk, dtype=torch.uint8, device=dev)  # ids [B][k] then dists [B][k]
     counts = torch.empty(B, dtype=torch.int32, device=dev)
     ws_bytes = lib.wvg_search_workspace_size(corpus.handle, B, k)
     ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=dev)
-    if world > 1:
-        g_d = torch.empty(world * B * k, dtype=torch.float32, device=dev)
-        g_i = torch.empty(world * B * k, dtype=torch.int64, device=dev)
-        m_ids = torch.empty((B, k), dtype=torch.int64, device=dev)
-        m_d = torch.empty((B, k), dtype=torch.float32, device=dev)
-        m_c = torch.empty(B, dtype=torch.int32, device=dev)
+    recv = torch.empty(world * blk, dtype=torch.uint8, device=dev)
+    m_ids = torch.empty((B, k), dtype=torch.int64, device=dev)
+    m_d = torch.empty((B, k), dtype=torch.float32, device=dev)
+    m_c = torch.empty(B, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
-
-    assert P % B == 0
 
     def step(s):
         # B single-query scans in one call = one query-stream launch (each query a full scan)
         q0 = (s * B) % P
-        check(lib.wvg_search_device_pipelined(corpus.handle, tq[q0].data_ptr(), B, k, ids.data_ptr(),
-                                              dists.data_ptr(), counts.data_ptr(), ws.data_ptr(), ws_bytes, stream))
+        check(lib.wvg_search_device_pipelined(corpus.handle, tq[q0].data_ptr(), B, k, send.data_ptr(),
+                                              send.data_ptr() + B * k * 8, counts.data_ptr(), ws.data_ptr(),
+                                              ws_bytes, stream))
         if world > 1:
-            dist.all_gather_into_tensor(g_d, dists.view(-1))
-            dist.all_gather_into_tensor(g_i, ids.view(-1))
-            check(lib.wvg_topk_merge_device(ctx.handle, g_d.data_ptr(), g_i.data_ptr(), B, world, k, k,
-                                            m_ids.data_ptr(), m_d.data_ptr(), m_c.data_ptr(), stream))
+            all_gather_packed(send, recv)  # ONE collective per step
+            check(lib.wvg_topk_merge_packed(ctx.handle, recv.data_ptr(), B, world, k, k, m_ids.data_ptr(),
+                                            m_d.data_ptr(), m_c.data_ptr(), stream))
 
     for s in range(args.warmup):
         step(s)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    check(lib.wvg_profile_start(ctx.handle))
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for s in range(args.steps):
-        step(args.warmup + s)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
+    check(lib.wvg_search_device_check(ctx.handle, ws.data_ptr(), stream))
     import ctypes
 
+    check(lib.wvg_profile_start(ctx.handle))
+    elapsed = _timed(lambda: [step(args.warmup + s) for s in range(args.steps)], dist, world, dev, torch)
     scan_ms, launches = ctypes.c_double(), ctypes.c_uint64()
     check(lib.wvg_profile_stop(ctx.handle, ctypes.byref(scan_ms), ctypes.byref(launches)))
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    check(lib.wvg_search_device_check(ctx.handle, ws.data_ptr(), stream))  # no merge gave up in the timed run
 
     total_queries = world * B * args.steps  # 1M-row query scans over all GPUs
-    value = total_queries / elapsed
     avg_launch_s = scan_ms.value / 1e3 / max(1, launches.value)
-    # SURVEY.md 8(d): N*d*4 algorithmic bytes per query scan; one launch scans B queries
-    bytes_per_launch = n * d * 4 * B
+    bytes_per_launch = n * d * 4 * B  # SURVEY.md 8(d): N*d*4 algorithmic bytes per query scan
     achieved = bytes_per_launch / avg_launch_s / 1e9
     traffic = None
     tf = os.path.join(ROOT, "profiles", "traffic.json")
@@ -173,56 +257,222 @@ def main():
             rec = json.load(open(tf)).get("scan_f32_stream_l2_128", {})
             if rec.get("rows") == n and rec.get("dim") == d:
                 traffic = int(round(rec["hbm_bytes_per_query_scan"] * B))  # per launch, like `achieved`
-        except Exception:
+        except (OSError, ValueError, KeyError):
             traffic = None
-
-    if rank == 0:
-        out = {
-            "metric": METRIC,
-            "value": round(value, 3),
-            "unit": "queries/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic: uniform[-1,1) rows from a counter RNG (seed 42) generated in HBM; "
-                    "64 uniform[-1,1) queries (seed 43) cycled",
-            "config": {
-                "workload": "flat exact k-NN, 1M x 128 fp32 L2 per GPU, single-query scans "
-                            "(BASELINE configs[0] shape on MI355X)",
-                "rows_per_gpu": n, "dim": d, "k": k, "queries_per_step": B,
-                "parallelism": f"shard rows by docID range over {world} GPU(s); RCCL all-gather of per-GPU top-k",
-            },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": "wvg::scan_f32_stream_kernel<L2,128,1>",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "avg_launch_us": round(avg_launch_s * 1e6, 2),
-                "queries_per_launch": B,
-                "algorithmic_bytes_per_launch": bytes_per_launch,
-                "launches": int(launches.value),
-            },
-            "cpu_baseline": None,
-        }
-        if world == 1 and not args.no_cpu_baseline:
-            nq = args.cpu_queries
-            cq = np.random.default_rng(43).uniform(-1, 1, (nq, d)).astype(np.float32)
-            # GPU results for the first queries (host API) to cross-check at full size
-            gids, _, _ = corpus.search(cq[:16], k)
-            out["cpu_baseline"] = cpu_baseline(n, d, k, cq, gids)
-        print(json.dumps(out), flush=True)
+    out = {
+        "metric": METRIC,
+        "value": round(total_queries / elapsed, 3),
+        "unit": "queries/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: uniform[-1,1) rows from a counter RNG (seed 42) generated in HBM; "
+                "64 uniform[-1,1) queries (seed 43) cycled",
+        "config": {
+            "workload": "flat exact k-NN, 1M x 128 fp32 L2 per GPU, single-query scans "
+                        "(BASELINE configs[0] shape on MI355X)",
+            "rows_per_gpu": n, "dim": d, "k": k, "queries_per_step": B,
+            "parallelism": f"shard rows by docID range over {world} GPU(s); one RCCL all-gather of packed "
+                           f"per-GPU top-k blocks per step + device merge",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": f"wvg::scan_f32_stream_kernel<L2,{d},1>",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "avg_launch_us": round(avg_launch_s * 1e6, 2),
+            "queries_per_launch": B,
+            "algorithmic_bytes_per_launch": bytes_per_launch,
+            "launches": int(launches.value),
+        },
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cq = np.random.default_rng(43).uniform(-1, 1, (16, d)).astype(np.float32)
+        gids, _, _ = corpus.search(cq, k)  # GPU results of the baseline's first queries (full-size cross-check)
+        out["cpu_baseline"] = cpu_baseline(n, d, k, gids, args.cpu_seconds)
     corpus.destroy()
     ctx.close()
+    return out
+
+
+def run_slab1b(args, world, rank, dev, torch, dist):
+    import ctypes
+
+    from weaviate_amd._lib import KIND_F32, METRIC_L2, check
+    from weaviate_amd.device import Context, Corpus
+    from weaviate_amd.shard import all_gather_packed
+
+    total, d, k, B = args.rows, args.dim, args.k, args.batch
+    S = 8  # slabs of the corpus
+    per = (total + S - 1) // S
+    per = (per + 63) // 64 * 64
+    if S % world:
+        raise SystemExit(f"bench.py: slab1b deals {S} slabs evenly, --gpus must divide {S}")
+    mine = [s for s in range(S) if s % world == rank]
+    L = len(mine)
+    ctx = Context(dev.index)
+    lib = ctx.lib
+    steps, W = args.steps, args.warmup
+    qs = torch.from_numpy(np.random.default_rng(43).uniform(-1, 1, (steps * B, d)).astype(np.float32)).to(dev)
+    # per (timed step, local slab) lists; warmup steps write into slot 0
+    ids = torch.empty((steps, L, B, k), dtype=torch.int64, device=dev)
+    dd = torch.empty((steps, L, B, k), dtype=torch.float32, device=dev)
+    cc = torch.empty((steps, L, B), dtype=torch.int32, device=dev)
+    blk = lib.wvg_topk_packed_bytes(B, k)
+    send = torch.empty(blk, dtype=torch.uint8, device=dev)
+    recv = torch.empty(world * blk, dtype=torch.uint8, device=dev)
+    m_ids = torch.empty((steps, B, k), dtype=torch.int64, device=dev)
+    m_d = torch.empty((steps, B, k), dtype=torch.float32, device=dev)
+    m_c = torch.empty((steps, B), dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    elapsed, scan_ms_tot, launches_tot = 0.0, 0.0, 0
+    for j, s in enumerate(mine):
+        n_s = max(0, min(per, total - s * per))
+        c = Corpus(ctx, KIND_F32, METRIC_L2, d, per, id_base=s * per)
+        if n_s:
+            c.fill_synthetic(42, n_s, 0)  # untimed: the slab is (re)generated in place
+        wsb = lib.wvg_search_workspace_size(c.handle, B, k)
+        ws = torch.zeros(wsb, dtype=torch.uint8, device=dev)
+
+        def scan(t, slot):
+            check(lib.wvg_search_device_pipelined(c.handle, qs[(t % steps) * B].data_ptr(), B, k,
+                                                  ids[slot, j].data_ptr(), dd[slot, j].data_ptr(),
+                                                  cc[slot, j].data_ptr(), ws.data_ptr(), wsb, stream))
+
+        for t in range(W):
+            scan(t, 0)
+        check(lib.wvg_profile_start(ctx.handle))
+        elapsed += _timed(lambda: [scan(t, t) for t in range(steps)], dist, world, dev, torch)
+        ms, nl = ctypes.c_double(), ctypes.c_uint64()
+        check(lib.wvg_profile_stop(ctx.handle, ctypes.byref(ms), ctypes.byref(nl)))
+        check(lib.wvg_search_device_check(ctx.handle, ws.data_ptr(), stream))
+        scan_ms_tot += ms.value
+        launches_tot += nl.value
+        c.destroy()
+
+    def merge_all():
+        for t in range(steps):
+            # this GPU's slabs -> one list per query, straight into the packed block
+            check(lib.wvg_topk_merge_device(ctx.handle, dd[t].data_ptr(), ids[t].data_ptr(), B, L, k, k,
+                                            send.data_ptr(), send.data_ptr() + B * k * 8, m_c[t].data_ptr(),
+                                            stream))
+            if world > 1:
+                all_gather_packed(send, recv)
+                check(lib.wvg_topk_merge_packed(ctx.handle, recv.data_ptr(), B, world, k, k, m_ids[t].data_ptr(),
+                                                m_d[t].data_ptr(), m_c[t].data_ptr(), stream))
+
+    elapsed += _timed(merge_all, dist, world, dev, torch)
+    avg_launch_s = scan_ms_tot / 1e3 / max(1, launches_tot)
+    bytes_per_launch = per * d * 4 * B
+    achieved = bytes_per_launch / avg_launch_s / 1e9
+    ctx.close()
+    return {
+        "metric": METRIC,
+        "value": round(B * steps / elapsed, 3),
+        "unit": "queries/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": W,
+        "ms_per_step": round(elapsed / steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: uniform[-1,1) rows from a counter RNG (seed 42) generated in HBM slab by slab "
+                "(generation untimed); uniform[-1,1) queries (seed 43)",
+        "config": {
+            "workload": f"flat exact {k}-NN over {total:,} x {d} fp32 L2 as {S} slabs of {per:,} rows "
+                        f"(BASELINE configs[4]); {L} slab(s) per GPU scanned in sequence",
+            "total_rows": total, "dim": d, "k": k, "queries_per_step": B, "slabs": S, "slabs_per_gpu": L,
+            "parallelism": f"slabs dealt to {world} GPU(s); per step a device merge of the local slabs, one RCCL "
+                           f"all-gather of packed top-{k} blocks and a device merge",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": f"wvg::scan_f32_stream_kernel<L2,{d},2>",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None,
+            "avg_launch_us": round(avg_launch_s * 1e6, 2),
+            "queries_per_launch": B,
+            "algorithmic_bytes_per_launch": bytes_per_launch,
+            "launches": launches_tot,
+        },
+        "cpu_baseline": None,
+    }
+
+
+def dry_run(args, world, rank):
+    """CPU rehearsal: the launch, the packed block and the one all-gather per
+    step over gloo, with a plain numpy brute force standing in for the scan
+    (no GPU, nothing timed against the metric)."""
+    import torch
+    import torch.distributed as dist
+
+    from weaviate_amd.shard import all_gather_packed, pack_block, shard_range, unpack_blocks
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    n, d, k, B = 4096, 16, args.k, args.batch
+    lo, cnt, _ = shard_range(n * world, world, rank)
+    rng = np.random.default_rng(42)
+    X = rng.uniform(-1, 1, (n * world, d)).astype(np.float32)[lo:lo + cnt]
+    Q = np.random.default_rng(43).uniform(-1, 1, (B, d)).astype(np.float32)
+    D = ((Q[:, None, :] - X[None]) ** 2).sum(-1)
+    order = np.argsort(D, axis=1, kind="stable")[:, :k]
+    ids = (order + lo).astype(np.uint64)
+    send = torch.from_numpy(pack_block(ids, np.take_along_axis(D, order, 1).astype(np.float32)))
+    recv = torch.empty(world * send.numel(), dtype=torch.uint8)
+    if world > 1:
+        all_gather_packed(send, recv)
+    else:
+        recv.copy_(send)
+    gi, gd = unpack_blocks(recv.numpy(), world, B, k)
+    assert gi.shape == (world, B, k)
     if world > 1:
         dist.destroy_process_group()
+    return {"metric": METRIC, "value": None, "unit": "queries/s", "n_gpus": world, "steps": 0,
+            "warmup": 0, "ms_per_step": None, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32", "data": "dry run (CPU, gloo): launch + packed all-gather rehearsal only",
+            "config": {"workload": args.workload, "dry_run": True}, "roofline": None, "cpu_baseline": None}
+
+
+def main():
+    args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(relaunch(args.gpus))  # nothing has touched a GPU in this process
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry_run:
+        out = dry_run(args, world, rank)
+    else:
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        if world > 1:
+            dist.init_process_group("nccl", device_id=dev)
+        fn = run_slab1b if args.workload == "slab1b" else run_flat1m
+        out = fn(args, world, rank, dev, torch, dist)
+        if world > 1:
+            dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

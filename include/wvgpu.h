@@ -107,6 +107,10 @@ int wvg_corpus_delete(wvg_corpus *c, const uint64_t *ids, uint64_t n);
 /* flat.vectorById (V/flat/index.go:401-407): copies the stored row
  * (F32: dim floats, BQ: words u64, PQ: m bytes); WVG_ERR_NOT_FOUND if absent. */
 int wvg_corpus_get(wvg_corpus *c, uint64_t id, void *out);
+/* vectorById for many ids in one call (the rescore loop's row fetches,
+ * V/flat/index.go:375-385): out [n][row bytes as wvg_corpus_get];
+ * out_ok[i] = 0 (row zero-filled) where ids[i] is not live.               */
+int wvg_corpus_get_batch(wvg_corpus *c, const uint64_t *ids, uint64_t n, void *out, uint8_t *out_ok);
 /* Bench / test helper: fills slots [0, n) with synthetic rows generated in
  * place from a counter-based RNG keyed by (seed, id_base + slot, column);
  * distribution 0 = uniform [-1,1), 1 = integers 0..255.  F32 and BQ only.  */
@@ -150,10 +154,12 @@ int wvg_search_by_distance(wvg_corpus *c, const float *query, float target_dista
 
 /* Device-pointer variants: inputs/outputs in HBM, asynchronous on `stream`
  * (a hipStream_t, NULL = default stream); no host synchronization, no
- * allocation (caller supplies a workspace of wvg_search_workspace_size bytes),
- * so a call can be captured in a hipGraph.  Queries must already be
- * normalized for cosine.  One workspace serves any number of calls issued
- * in order on one stream (no initialization needed).                       */
+ * allocation (caller supplies a workspace of wvg_search_workspace_size bytes,
+ * zero-filled once before its first use), so a call can be captured in a
+ * hipGraph.  Queries must already be normalized for cosine.  One workspace
+ * serves any number of calls issued in order on one stream.  An empty corpus
+ * (e.g. a rank whose slab holds no rows) yields empty results: ids
+ * UINT64_MAX, dists +inf, counts 0 (as wvg_search).                        */
 size_t wvg_search_workspace_size(wvg_corpus *c, uint32_t nq, uint32_t k);
 int wvg_search_device(wvg_corpus *c, const float *d_queries, uint32_t nq, uint32_t k,
                       uint64_t *d_ids, float *d_dists, uint32_t *d_counts, void *d_workspace,
@@ -166,6 +172,12 @@ int wvg_search_device(wvg_corpus *c, const float *d_queries, uint32_t nq, uint32
 int wvg_search_device_pipelined(wvg_corpus *c, const float *d_queries, uint32_t nq, uint32_t k,
                                 uint64_t *d_ids, float *d_dists, uint32_t *d_counts,
                                 void *d_workspace, size_t workspace_bytes, void *stream);
+/* Synchronizes `stream` and reads (and clears) the workspace's sticky status
+ * word: WVG_ERR_DEVICE if any device search on this workspace since the last
+ * check could not complete -- the query-stream merge workgroup of
+ * wvg_search_device_pipelined gave up waiting for the scan (bounded at 4 s);
+ * the queries it could not merge were given empty results, never stale ones. */
+int wvg_search_device_check(wvg_ctx *ctx, void *d_workspace, void *stream);
 /* Multi-shard merge (Index.objectVectorSearch, adapters/repos/db/index.go:1644-1648):
  * [nlists][nq][k_in] (dist, id) lists (the layout an all-gather of per-GPU
  * [nq][k_in] results produces) -> [nq][k] ascending, ties by id; missing
@@ -173,6 +185,16 @@ int wvg_search_device_pipelined(wvg_corpus *c, const float *d_queries, uint32_t 
 int wvg_topk_merge_device(wvg_ctx *ctx, const float *d_dists, const uint64_t *d_ids, uint32_t nq,
                           uint32_t nlists, uint32_t k_in, uint32_t k, uint64_t *d_out_ids,
                           float *d_out_dists, uint32_t *d_out_counts, void *stream);
+/* The same merge over packed blocks, so one all-gather moves both halves of
+ * every rank's result: a block holds ids [nq][k] uint64 at byte 0 and dists
+ * [nq][k] float32 at byte nq*k*8, and is wvg_topk_packed_bytes(nq, k) bytes
+ * (a multiple of 16); d_packed holds nlists consecutive blocks.  Write a
+ * block directly with wvg_search_device*(..., d_ids = block,
+ * d_dists = block + nq*k*8, ...).                                          */
+size_t wvg_topk_packed_bytes(uint32_t nq, uint32_t k);
+int wvg_topk_merge_packed(wvg_ctx *ctx, const void *d_packed, uint32_t nq, uint32_t nlists, uint32_t k_in,
+                          uint32_t k, uint64_t *d_out_ids, float *d_out_dists, uint32_t *d_out_counts,
+                          void *stream);
 
 /* The rescore loop of flat.searchByVectorBQ (V/flat/index.go:375-385) when
  * the candidate rows come from the host (LSM point gets): exact SingleDist of

@@ -584,11 +584,25 @@ ORC_API long orc_flat_search(const float *rows, long n, long d, long pitch, cons
  * ids, pop all (descending Hamming order), exact distance for each popped id
  * and insertToHeap(k), then extractHeap.  `query` must already be normalized
  * for cosine (index.go:352).  Returns count. */
+static long flat_search_bq_fn(const float *rows, const uint64_t *codes, long n, long d, long pitch,
+                              const uint8_t *valid, const float *query, long k, long rescore_limit, int metric,
+                              orc_dist_fn fn, uint64_t *out_ids, float *out_dists, uint64_t *cand_ids);
+
 ORC_API long orc_flat_search_bq(const float *rows, const uint64_t *codes, long n, long d,
                                 long pitch, const uint8_t *valid, const float *query,
                                 long k, long rescore_limit, int metric,
                                 uint64_t *out_ids, float *out_dists,
                                 uint64_t *cand_ids /* optional, len >= rescore */)
+{
+    return flat_search_bq_fn(rows, codes, n, d, pitch, valid, query, k, rescore_limit, metric, NULL, out_ids,
+                             out_dists, cand_ids);
+}
+
+/* The same with the rescore distance from `fn` (the reference's own l2_256 /
+ * dot_256 from oracle/_ref in the CPU baseline), else the restatement. */
+static long flat_search_bq_fn(const float *rows, const uint64_t *codes, long n, long d, long pitch,
+                              const uint8_t *valid, const float *query, long k, long rescore_limit, int metric,
+                              orc_dist_fn fn, uint64_t *out_ids, float *out_dists, uint64_t *cand_ids)
 {
     long w = (d + 63) / 64;
     long rescore = rescore_limit > k ? rescore_limit : k; /* index.go:297-305 */
@@ -605,7 +619,15 @@ ORC_API long orc_flat_search_bq(const float *rows, const uint64_t *codes, long n
     for (long i = 0; i < nc; i++) ids[i] = heap_pop(&h).id;
     if (cand_ids) memcpy(cand_ids, ids, sizeof(uint64_t) * (size_t)nc);
     for (long i = 0; i < nc; i++) {
-        float dist = orc_single_dist(metric, query, rows + ids[i] * pitch, d);
+        float dist;
+        if (fn) {
+            float r = 0.0f;
+            long len = d;
+            fn((float *)query, (float *)(rows + ids[i] * pitch), &r, &len);
+            dist = (metric == ORC_L2) ? r : (metric == ORC_DOT ? -r : 1.0f - r);
+        } else {
+            dist = orc_single_dist(metric, query, rows + ids[i] * pitch, d);
+        }
         insert_to_heap(&h, k, ids[i], dist);
     }
     long cnt = extract_heap(&h, out_ids, out_dists);
@@ -647,23 +669,26 @@ ORC_API void orc_synth_rows(uint64_t seed, uint64_t row0, long n, long d, long p
 /* Concurrently splits the index range across GOMAXPROCS workers).           */
 /* ------------------------------------------------------------------------ */
 typedef struct {
-    const float *rows; long n, d, pitch; const float *qs; long k; int metric; orc_dist_fn fn;
+    const float *rows; const uint64_t *codes; long n, d, pitch; const float *qs; long k, rescore;
+    int metric; orc_dist_fn fn;
     long q0, q1; uint64_t *out_ids; float *out_dists;
 } orc_job;
 
 static void *orc_worker(void *arg)
 {
     orc_job *j = (orc_job *)arg;
-    for (long q = j->q0; q < j->q1; q++)
-        orc_flat_search(j->rows, j->n, j->d, j->pitch, NULL, j->qs + q * j->d, j->k, j->metric,
-                        j->fn, j->out_ids + q * j->k, j->out_dists + q * j->k);
+    for (long q = j->q0; q < j->q1; q++) {
+        if (j->codes)  /* BQ cache flow: Hamming top-R, exact rescore, top-k */
+            flat_search_bq_fn(j->rows, j->codes, j->n, j->d, j->pitch, NULL, j->qs + q * j->d, j->k, j->rescore,
+                              j->metric, j->fn, j->out_ids + q * j->k, j->out_dists + q * j->k, NULL);
+        else
+            orc_flat_search(j->rows, j->n, j->d, j->pitch, NULL, j->qs + q * j->d, j->k, j->metric,
+                            j->fn, j->out_ids + q * j->k, j->out_dists + q * j->k);
+    }
     return NULL;
 }
 
-/* Runs nq flat searches on `threads` threads; returns wall seconds. */
-ORC_API double orc_bench_flat(const float *rows, long n, long d, long pitch, const float *qs,
-                              long nq, long k, int metric, orc_dist_fn fn, int threads,
-                              uint64_t *out_ids, float *out_dists)
+static double run_jobs(orc_job proto, long nq, int threads)
 {
     if (threads < 1) threads = 1;
     pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)threads);
@@ -675,13 +700,42 @@ ORC_API double orc_bench_flat(const float *rows, long n, long d, long pitch, con
         long q0 = t * split, q1 = q0 + split;
         if (q1 > nq) q1 = nq;
         if (q0 > nq) q0 = nq;
-        jobs[t] = (orc_job){ rows, n, d, pitch, qs, k, metric, fn, q0, q1, out_ids, out_dists };
+        jobs[t] = proto;
+        jobs[t].q0 = q0;
+        jobs[t].q1 = q1;
         pthread_create(&th[t], NULL, orc_worker, &jobs[t]);
     }
     for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
     clock_gettime(CLOCK_MONOTONIC, &t1);
     free(th); free(jobs);
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
+/* Runs nq flat searches on `threads` threads; returns wall seconds. */
+ORC_API double orc_bench_flat(const float *rows, long n, long d, long pitch, const float *qs,
+                              long nq, long k, int metric, orc_dist_fn fn, int threads,
+                              uint64_t *out_ids, float *out_dists)
+{
+    orc_job p = { rows, NULL, n, d, pitch, qs, k, 0, metric, fn, 0, 0, out_ids, out_dists };
+    return run_jobs(p, nq, threads);
+}
+
+/* Runs nq flat BQ searches (findTopVectorsCached + rescore, V/flat/index.go:
+ * 347-389, 456-495) over prebuilt codes [n][ceil(d/64)] (the BQ cache) on
+ * `threads` threads; queries already normalized for cosine.  Wall seconds. */
+ORC_API double orc_bench_flat_bq(const float *rows, const uint64_t *codes, long n, long d, long pitch,
+                                 const float *qs, long nq, long k, long rescore_limit, int metric,
+                                 orc_dist_fn fn, int threads, uint64_t *out_ids, float *out_dists)
+{
+    orc_job p = { rows, codes, n, d, pitch, qs, k, rescore_limit, metric, fn, 0, 0, out_ids, out_dists };
+    return run_jobs(p, nq, threads);
+}
+
+/* BinaryQuantizer.Encode of n rows into codes [n][ceil(d/64)] (test helper). */
+ORC_API void orc_bq_encode_rows(const float *rows, long n, long d, uint64_t *codes)
+{
+    long w = (d + 63) / 64;
+    for (long i = 0; i < n; i++) orc_bq_encode(rows + i * d, d, codes + i * w);
 }
 
 /* Provider.SingleDist(q, rows[i]) for every row (test helper; AVX2-order

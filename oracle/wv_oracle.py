@@ -77,6 +77,10 @@ def lib():
         l.orc_bq_dist_all.argtypes = [_U64, _U64, c_long, c_long, _F]
         l.orc_bench_flat.restype = c_double
         l.orc_bench_flat.argtypes = [_F, c_long, c_long, c_long, _F, c_long, c_long, c_int, c_void_p, c_int, _U64, _F]
+        l.orc_bench_flat_bq.restype = c_double
+        l.orc_bench_flat_bq.argtypes = [_F, _U64, c_long, c_long, c_long, _F, c_long, c_long, c_long, c_int, c_void_p,
+                                        c_int, _U64, _F]
+        l.orc_bq_encode_rows.argtypes = [_F, c_long, c_long, _U64]
         _lib = l
     return _lib
 
@@ -280,6 +284,32 @@ def bench_flat(rows, qs, k, metric, threads, use_ref_kernel=True):
     oid = np.empty((nq, k), dtype=np.uint64)
     od = np.empty((nq, k), dtype=np.float32)
     secs = lib().orc_bench_flat(_f(rows), n, d, d, _f(qs), nq, k, metric, fn, threads, _u64(oid), _f(od))
+    return secs, oid, od, fn is not None
+
+
+def bq_encode_rows(rows):
+    """BinaryQuantizer.Encode of every row -> codes [n][ceil(d/64)]."""
+    rows = f32(rows)
+    n, d = rows.shape
+    codes = np.empty((n, (d + 63) // 64), dtype=np.uint64)
+    lib().orc_bq_encode_rows(_f(rows), n, d, _u64(codes))
+    return codes
+
+
+def bench_flat_bq(rows, codes, qs, k, rescore_limit, metric, threads, use_ref_kernel=True):
+    """Times nq flat BQ searches (Hamming top-R over the codes, exact rescore
+    of R, top-k), one query per thread at a time; returns seconds."""
+    rows, qs = f32(rows), f32(qs)
+    codes = np.ascontiguousarray(codes, dtype=np.uint64)
+    n, d = rows.shape
+    nq = qs.shape[0]
+    fn = None
+    if use_ref_kernel and ref() is not None:
+        fn = ctypes.cast(getattr(ref(), "l2_256" if metric == L2 else "dot_256"), c_void_p)
+    oid = np.empty((nq, k), dtype=np.uint64)
+    od = np.empty((nq, k), dtype=np.float32)
+    secs = lib().orc_bench_flat_bq(_f(rows), _u64(codes), n, d, d, _f(qs), nq, k, rescore_limit, metric, fn, threads,
+                                   _u64(oid), _f(od))
     return secs, oid, od, fn is not None
 
 

@@ -1,8 +1,9 @@
 """CPU tests of the N > 1 path with world_size 2 over gloo: docID-range
-sharding, the all-gather layout [world][nq][k] and the lexicographic merge
-reproduce the single-corpus result (the GPU scan and merge kernels are
-covered by tests/test_gpu_parity.py; here the oracle stands in for the
-per-rank scan, as a checker)."""
+sharding, the packed per-rank block (ids then dists, one all-gather per
+batch) and the lexicographic merge reproduce the single-corpus result.  Here
+the oracle stands in for the per-rank scan and for the merge, as checkers;
+tests/test_gpu_dist.py runs the same exchange with the HIP scan and the
+device merge (wvg_topk_merge_packed) on the GPU."""
 import os
 import socket
 
@@ -11,6 +12,8 @@ import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+
+NONE = np.iinfo(np.uint64).max
 
 
 def _free_port():
@@ -26,7 +29,7 @@ def _worker(rank, world, port, n, d, k, nq, out):
 
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from oracle import wv_oracle as orc
-    from weaviate_amd.shard import all_gather_topk, shard_range
+    from weaviate_amd.shard import all_gather_packed, pack_block, packed_bytes, shard_range, unpack_blocks
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -36,19 +39,24 @@ def _worker(rank, world, port, n, d, k, nq, out):
     rows = orc.synth_rows(42, lo, cnt, d, 0)  # the slab generated from global ids
     qs = orc.synth_rows(43, 0, nq, d, 0)
     ld = np.full((nq, k), np.inf, np.float32)
-    li = np.full((nq, k), np.iinfo(np.uint64).max, np.uint64)
+    li = np.full((nq, k), NONE, np.uint64)
     for qi in range(nq):
+        if cnt == 0:
+            continue
         all_d = orc.dist_all(orc.L2, qs[qi], rows)
         ids, dd = orc.lex_topk(all_d, np.arange(lo, lo + cnt, dtype=np.uint64), k)
         li[qi, :len(ids)] = ids
         ld[qi, :len(ids)] = dd
-    g = all_gather_topk(torch.from_numpy(ld), torch.from_numpy(li.view(np.int64)))
-    assert tuple(g.dists.shape) == (world, nq, k)
-    gd = g.dists.numpy()
-    gi = g.ids.numpy().view(np.uint64)
+    send = torch.from_numpy(pack_block(li, ld))
+    assert send.numel() == packed_bytes(nq, k) and send.numel() % 16 == 0
+    recv = torch.empty(world * send.numel(), dtype=torch.uint8)
+    all_gather_packed(send, recv)  # ONE collective per batch
+    gi, gd = unpack_blocks(recv.numpy(), world, nq, k)
+    assert gi.shape == (world, nq, k)
+    assert np.array_equal(gi[rank], li) and np.array_equal(gd[rank].view(np.uint32), ld.view(np.uint32))
     res = []
     for qi in range(nq):
-        live = gi[:, qi, :] != np.iinfo(np.uint64).max
+        live = gi[:, qi, :] != NONE
         ids, dd = orc.lex_topk(gd[:, qi, :][live], gi[:, qi, :][live], k)
         res.append((ids.tolist(), dd.tolist()))
     if rank == 0:
@@ -57,8 +65,9 @@ def _worker(rank, world, port, n, d, k, nq, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n", [(2, 10_007), (2, 130)])
+@pytest.mark.parametrize("world,n", [(2, 10_007), (2, 130), (2, 63)])
 def test_sharded_search_equals_single_corpus(world, n):
+    """n = 63: rank 1 holds no rows and contributes an all-empty block."""
     from oracle import wv_oracle as orc
 
     d, k, nq = 32, 10, 4
@@ -80,6 +89,30 @@ def test_sharded_search_equals_single_corpus(world, n):
         assert np.array_equal(np.asarray(res[qi][1], np.float32), wd)
 
 
+def test_pack_roundtrip():
+    from weaviate_amd.shard import pack_block, packed_bytes, unpack_blocks
+
+    rng = np.random.default_rng(3)
+    for nq, k in [(1, 1), (3, 10), (16, 10), (5, 7)]:
+        ids = rng.integers(0, 2**63, (nq, k)).astype(np.uint64)
+        ids[0, -1] = NONE
+        dd = rng.standard_normal((nq, k)).astype(np.float32)
+        blocks = np.concatenate([pack_block(ids, dd), pack_block(ids[::-1].copy(), dd[::-1].copy())])
+        assert len(blocks) == 2 * packed_bytes(nq, k)
+        gi, gd = unpack_blocks(blocks, 2, nq, k)
+        assert np.array_equal(gi[0], ids) and np.array_equal(gi[1], ids[::-1])
+        assert np.array_equal(gd[0], dd) and np.array_equal(gd[1], dd[::-1])
+
+
+def test_packed_bytes_matches_library():
+    from weaviate_amd import _lib
+    from weaviate_amd.shard import packed_bytes
+
+    lib = _lib.load()
+    for nq, k in [(1, 1), (16, 10), (8, 100), (3, 7)]:
+        assert lib.wvg_topk_packed_bytes(nq, k) == packed_bytes(nq, k)
+
+
 def test_shard_range_partitions_exactly():
     from weaviate_amd.shard import shard_range
 
@@ -89,7 +122,7 @@ def test_shard_range_partitions_exactly():
             prev_end = 0
             for r in range(world):
                 lo, cnt, _ = shard_range(n, world, r)
-                assert lo % 64 == 0 or cnt == 0
+                assert lo % 64 == 0
                 if cnt:
                     assert lo == prev_end
                     prev_end = lo + cnt

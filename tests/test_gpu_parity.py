@@ -533,33 +533,6 @@ def test_search_device_pipelined_matches_host_api(ctx, orc, mode):
         lib.wvgx_set_tuning(2, old)
 
 
-# ---------------------------------------------------------------------------
-# Full size (BASELINE config 1): 1M x 128 L2 -- size-independent properties
-@pytest.mark.slow
-def test_full_size_1m_x_128_properties(ctx, orc):
-    n, d, k = 1_000_000, 128, 10
-    c = Corpus(ctx, KIND_F32, METRIC_L2, d, n)
-    c.fill_synthetic(42, n, 0)
-    qs = orc.synth_rows(43, 0, 3, d, 0)
-    ids, dists, counts = c.search(qs, k)
-    rng = np.random.default_rng(0)
-    sample = np.sort(rng.choice(n, 200_000, replace=False))
-    all_rows = orc.synth_rows(42, 0, n, d, 0)
-    srows = all_rows[sample]
-    for qi in range(len(qs)):
-        assert counts[qi] == k
-        assert np.all(np.diff(orc.ord_key(dists[qi]).astype(np.int64)) >= 0)  # sorted
-        # returned distances are bit-exact recomputations of the returned rows
-        got_rows = all_rows[ids[qi].astype(np.int64)]
-        assert np.array_equal(bits(orc.dist_all(0, qs[qi], got_rows)), bits(dists[qi]))
-        # no sampled row outside the result beats the k-th result (lexicographic (dist, id))
-        sd = orc.dist_all(0, qs[qi], srows)
-        outside = ~np.isin(sample, ids[qi].astype(np.int64))
-        kth = (int(orc.ord_key(dists[qi][-1:])[0]), int(ids[qi][-1]))
-        sk = orc.ord_key(sd[outside]).astype(np.int64)
-        assert np.all((sk > kth[0]) | ((sk == kth[0]) & (sample[outside] > kth[1])))
-
-
 @pytest.mark.parametrize("variant", [0, 2, 1])
 @pytest.mark.parametrize("metric,d", [(METRIC_COSINE, 768), (METRIC_DOT, 256), (METRIC_COSINE, 1536), (METRIC_DOT, 512)])
 def test_batched_mfma_variants(ctx, orc, variant, metric, d):
@@ -599,125 +572,3 @@ def test_batched_mfma_variants(ctx, orc, variant, metric, d):
         lib.wvgx_set_tuning(4, old)
 
 
-# Full size (BASELINE config 4): 100M x 128 L2, PQ m=32 ks=256 -- bulk encode on
-# the device, then ADC top-10 over all 100M codes; checked by properties on
-# sampled rows (the oracle cannot encode and scan 100M rows in seconds).
-@pytest.mark.slow
-def test_full_size_pq_100m_properties(ctx, orc):
-    n, d, m, ks, k = 100_000_000, 128, 32, 256, 10
-    f = Corpus(ctx, KIND_F32, METRIC_L2, d, n)
-    f.fill_synthetic(42, n, 0)
-    centers = np.ascontiguousarray(orc.synth_rows(42, 0, ks, d, 0).reshape(ks, m, d // m).transpose(1, 0, 2))
-    pq = Corpus(ctx, KIND_PQ, METRIC_L2, d, n)
-    pq.set_codebook(centers)
-    _lib.check(_lib.load().wvg_pq_encode_corpus(pq.handle, f.handle))
-    f.destroy()
-    # sampled rows at the start, the middle and the end: codes bit-exact vs the oracle
-    starts = [0, n // 2 - 7, n - 20_000]
-    sample_ids = np.concatenate([np.arange(s, s + 20_000, dtype=np.int64) for s in starts])
-    srows = np.concatenate([orc.synth_rows(42, s, 20_000, d, 0) for s in starts])
-    scodes = orc.pq_encode(srows, centers)
-    for j in range(0, len(sample_ids), 997):
-        assert np.array_equal(pq.get(int(sample_ids[j]), pq_m=m), scodes[j]), int(sample_ids[j])
-    qs = orc.synth_rows(43, 0, 3, d, 0)
-    ids, dists, counts = pq.search(qs, k)
-    for qi in range(len(qs)):
-        assert counts[qi] == k
-        assert np.all(np.diff(orc.ord_key(dists[qi]).astype(np.int64)) >= 0)
-        lut = orc.pq_lut(0, qs[qi], centers)
-        # each returned distance is the sequential ADC sum of that row's stored code
-        for i, dv in zip(ids[qi], dists[qi]):
-            assert bits(orc.pq_adc(0, lut, pq.get(int(i), pq_m=m))) == bits(dv)
-        # no sampled row outside the result beats the k-th result (lexicographic (dist, id))
-        sd = np.array([orc.pq_adc(0, lut, c) for c in scodes], np.float32)
-        outside = ~np.isin(sample_ids, ids[qi].astype(np.int64))
-        kth = (int(orc.ord_key(dists[qi][-1:])[0]), int(ids[qi][-1]))
-        sk = orc.ord_key(sd[outside]).astype(np.int64)
-        assert np.all((sk > kth[0]) | ((sk == kth[0]) & (sample_ids[outside] > kth[1])))
-    pq.destroy()
-
-
-# Full size (BASELINE config 3): 100M x 1536 BQ (W = 24 words) cosine, Hamming
-# top-200 over all 100M device-resident codes (the 614 GB of float rows do not
-# fit, so the rescore stage is covered at small sizes above).
-@pytest.mark.slow
-def test_full_size_bq_100m_x_1536_properties(ctx, orc):
-    n, d, R = 100_000_000, 1536, 200
-    w = (d + 63) // 64
-    c = Corpus(ctx, KIND_BQ, METRIC_COSINE, d, n)
-    c.fill_synthetic(42, n, 0)
-    starts = [0, n // 2 - 13, n - 10_000]
-    sample_ids = np.concatenate([np.arange(s, s + 10_000, dtype=np.int64) for s in starts])
-    scodes = np.stack([orc.bq_encode(orc.normalize(r)) for s in starts for r in orc.synth_rows(42, s, 10_000, d, 0)])
-    for j in range(0, len(sample_ids), 499):
-        assert np.array_equal(c.get(int(sample_ids[j])), scodes[j]), int(sample_ids[j])
-    qs = orc.synth_rows(43, 0, 2, d, 0)
-    ids, dists, counts = c.search(qs, R)
-    for qi in range(len(qs)):
-        assert counts[qi] == R
-        assert np.all(np.diff(dists[qi]) >= 0)
-        qc = orc.bq_encode(orc.normalize(qs[qi]))
-        got = np.stack([c.get(int(i)) for i in ids[qi]])
-        assert got.shape == (R, w)
-        assert np.array_equal(bits(orc.bq_dist_all(qc, got)), bits(dists[qi]))
-        sd = orc.bq_dist_all(qc, scodes)
-        outside = ~np.isin(sample_ids, ids[qi].astype(np.int64))
-        kd, kid = float(dists[qi][-1]), int(ids[qi][-1])
-        assert np.all((sd[outside] > kd) | ((sd[outside] == kd) & (sample_ids[outside] > kid)))
-    c.destroy()
-
-
-# Full size (BASELINE config 2): 10M x 768 fp32 cosine, one 1024-query batch
-# through the batched MFMA path (K3b) -- properties on sampled rows and queries.
-@pytest.mark.slow
-def test_full_size_batched_10m_x_768_cosine_properties(ctx, orc):
-    n, d, nq, k = 10_000_000, 768, 1024, 10
-    c = Corpus(ctx, KIND_F32, METRIC_COSINE, d, n)
-    c.fill_synthetic(42, n, 0)
-    starts = [0, n // 2 - 3, n - 10_000]
-    sample_ids = np.concatenate([np.arange(s, s + 10_000, dtype=np.int64) for s in starts])
-    srows = np.concatenate([orc.normalize_rows(orc.synth_rows(42, s, 10_000, d, 0)) for s in starts])
-    for j in range(0, len(sample_ids), 997):
-        assert np.array_equal(bits(c.get(int(sample_ids[j]))), bits(srows[j])), int(sample_ids[j])
-    qs = orc.synth_rows(43, 0, nq, d, 0)
-    ids, dists, counts = c.search(qs, k)
-    assert np.all(counts == k)
-    for qi in (0, 1, 511, 1023):
-        q = orc.normalize(qs[qi])
-        assert np.all(np.diff(orc.ord_key(dists[qi]).astype(np.int64)) >= 0)
-        got = orc.normalize_rows(np.stack([orc.synth_rows(42, int(i), 1, d, 0)[0] for i in ids[qi]]))
-        assert np.array_equal(bits(orc.dist_all(2, q, got)), bits(dists[qi]))
-        sd = orc.dist_all(2, q, srows)
-        outside = ~np.isin(sample_ids, ids[qi].astype(np.int64))
-        kth = (int(orc.ord_key(dists[qi][-1:])[0]), int(ids[qi][-1]))
-        sk = orc.ord_key(sd[outside]).astype(np.int64)
-        assert np.all((sk > kth[0]) | ((sk == kth[0]) & (sample_ids[outside] > kth[1])))
-    c.destroy()
-
-
-# Full size (BASELINE config 5, one GPU's share): a 125M x 128 fp32 L2 slab
-# holding global docIDs [375M, 500M) (slab 3 of 8), exact 100-NN.
-@pytest.mark.slow
-def test_full_size_slab_125m_global_ids_properties(ctx, orc):
-    n, d, k, base = 125_000_000, 128, 100, 375_000_000
-    c = Corpus(ctx, KIND_F32, METRIC_L2, d, n, id_base=base)
-    c.fill_synthetic(42, n, 0)
-    starts = [base, base + n // 2 - 5, base + n - 20_000]
-    sample_ids = np.concatenate([np.arange(s, s + 20_000, dtype=np.int64) for s in starts])
-    srows = np.concatenate([orc.synth_rows(42, s, 20_000, d, 0) for s in starts])
-    for j in range(0, len(sample_ids), 997):
-        assert np.array_equal(bits(c.get(int(sample_ids[j]))), bits(srows[j])), int(sample_ids[j])
-    qs = orc.synth_rows(43, 0, 2, d, 0)
-    ids, dists, counts = c.search(qs, k)
-    for qi in range(len(qs)):
-        assert counts[qi] == k
-        assert np.all((ids[qi] >= base) & (ids[qi] < base + n))
-        assert np.all(np.diff(orc.ord_key(dists[qi]).astype(np.int64)) >= 0)
-        got = np.stack([orc.synth_rows(42, int(i), 1, d, 0)[0] for i in ids[qi]])
-        assert np.array_equal(bits(orc.dist_all(0, qs[qi], got)), bits(dists[qi]))
-        sd = orc.dist_all(0, qs[qi], srows)
-        outside = ~np.isin(sample_ids, ids[qi].astype(np.int64))
-        kth = (int(orc.ord_key(dists[qi][-1:])[0]), int(ids[qi][-1]))
-        sk = orc.ord_key(sd[outside]).astype(np.int64)
-        assert np.all((sk > kth[0]) | ((sk == kth[0]) & (sample_ids[outside] > kth[1])))
-    c.destroy()

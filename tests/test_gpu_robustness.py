@@ -1,0 +1,226 @@
+"""GPU tests of the boundary's failure and edge behaviour: stored data right
+after creation, empty corpora on the device path, the query-stream merge
+timeout (surfaced, never stale), allow lists over a docID space far larger
+than the corpus, PQ codebook / code validation, batched row fetch and the
+packed all-gather merge."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from weaviate_amd import _lib
+from weaviate_amd._lib import KIND_BQ, KIND_F32, KIND_PQ, METRIC_COSINE, METRIC_DOT, METRIC_L2
+from weaviate_amd.device import Corpus, allow_bitmap
+
+pytestmark = pytest.mark.gpu
+
+NONE = np.iinfo(np.uint64).max
+
+
+def bits(x):
+    return np.asarray(x, dtype=np.float32).view(np.uint32)
+
+
+def tuning(lib, key, value):
+    lib.wvgx_set_tuning.restype = ctypes.c_int
+    lib.wvgx_set_tuning.argtypes = [ctypes.c_int, ctypes.c_int]
+    return lib.wvgx_set_tuning(key, value)
+
+
+def test_create_then_fill_stored_rows_exact(ctx, orc):
+    """Round 1's fault: the allocation's zero fill (null stream) could land
+    after rows written on a pool stream.  Create + fill + reserve-grow
+    repeatedly and compare chunk 0 of every tile and a stride of all rows."""
+    n, d = 300_000, 128  # 153.6 MB of rows
+    want = orc.synth_rows(42, 0, n, d, 0)
+    for rep in range(3):
+        c = Corpus(ctx, KIND_F32, METRIC_L2, d, n)
+        c.fill_synthetic(42, n, 0)
+        firsts = np.arange(0, n, 64, dtype=np.uint64)  # lane 0 of every tile
+        got, ok = c.get_batch(firsts)
+        assert ok.all() and np.array_equal(bits(got), bits(want[firsts.astype(np.int64)]))
+        strided = np.arange(rep, n, 7, dtype=np.uint64)
+        got, ok = c.get_batch(strided)
+        assert ok.all() and np.array_equal(bits(got), bits(want[strided.astype(np.int64)]))
+        # a grow copies the rows and zero-fills the rest on the same stream
+        c.reserve(2 * n)
+        got, ok = c.get_batch(firsts)
+        assert ok.all() and np.array_equal(bits(got), bits(want[firsts.astype(np.int64)]))
+        c.destroy()
+
+
+@pytest.mark.parametrize("kind", [KIND_F32, KIND_BQ, KIND_PQ])
+def test_get_batch_matches_get(ctx, orc, kind):
+    n, d, m, ks = 1000, 64, 32, 256
+    c = Corpus(ctx, kind, METRIC_L2, d, n, id_base=640)
+    if kind == KIND_PQ:
+        c.set_codebook(orc.synth_rows(5, 0, m * ks, d // m, 0).reshape(m, ks, d // m))
+    c.upsert(np.arange(640, 640 + n, dtype=np.uint64), orc.synth_rows(6, 0, n, d, 0))
+    c.delete(np.array([641, 700], np.uint64))
+    ids = np.array([640, 641, 700, 701, 640 + n - 1, 5, 640 + n + 3, 1000], np.uint64)
+    rows, ok = c.get_batch(ids, pq_m=m)
+    assert ok.tolist() == [True, False, False, True, True, False, False, True]
+    for i, good in zip(ids, ok):
+        if good:
+            assert np.array_equal(rows[list(ids).index(i)], c.get(int(i), pq_m=m))
+    assert not rows[~ok].any()
+
+
+def test_device_search_on_empty_corpus_writes_empty_results(ctx):
+    import torch
+
+    lib = _lib.load()
+    dev = torch.device("cuda:0")
+    for cap in (0, 640):
+        c = Corpus(ctx, KIND_F32, METRIC_L2, 32, cap, id_base=64)
+        nq, k = 3, 10
+        ws = torch.zeros(max(256, lib.wvg_search_workspace_size(c.handle, nq, k)), dtype=torch.uint8, device=dev)
+        q = torch.zeros((nq, 32), dtype=torch.float32, device=dev)
+        for fn in (lib.wvg_search_device, lib.wvg_search_device_pipelined):
+            ids = torch.full((nq, k), 7, dtype=torch.int64, device=dev)  # garbage that must be overwritten
+            dd = torch.full((nq, k), -1.0, dtype=torch.float32, device=dev)
+            cc = torch.full((nq,), 5, dtype=torch.int32, device=dev)
+            _lib.check(fn(c.handle, q.data_ptr(), nq, k, ids.data_ptr(), dd.data_ptr(), cc.data_ptr(),
+                          ws.data_ptr(), ws.numel(), torch.cuda.current_stream().cuda_stream))
+            torch.cuda.synchronize()
+            assert (ids.cpu().numpy().view(np.uint64) == NONE).all()
+            assert np.isinf(dd.cpu().numpy()).all()
+            assert (cc.cpu().numpy() == 0).all()
+        c.destroy()
+
+
+def test_query_stream_merge_timeout_is_reported(ctx, orc):
+    """A merge workgroup that gives up (forced: 1 us wait) makes
+    wvg_search_device_check fail, and the unmerged queries come back empty,
+    never with a previous call's results; the default wait then succeeds."""
+    import torch
+
+    lib = _lib.load()
+    n, d, k, nq = 1_000_000, 128, 10, 4
+    c = Corpus(ctx, KIND_F32, METRIC_L2, d, n)
+    c.fill_synthetic(42, n, 0)
+    dev = torch.device("cuda:0")
+    st = torch.cuda.current_stream().cuda_stream
+    ws = torch.zeros(lib.wvg_search_workspace_size(c.handle, nq, k), dtype=torch.uint8, device=dev)
+    tq = torch.from_numpy(orc.synth_rows(43, 0, nq, d, 0)).to(dev)
+    ids = torch.empty((nq, k), dtype=torch.int64, device=dev)
+    dd = torch.empty((nq, k), dtype=torch.float32, device=dev)
+    cc = torch.empty(nq, dtype=torch.int32, device=dev)
+
+    def run():
+        _lib.check(lib.wvg_search_device_pipelined(c.handle, tq.data_ptr(), nq, k, ids.data_ptr(), dd.data_ptr(),
+                                                   cc.data_ptr(), ws.data_ptr(), ws.numel(), st))
+
+    old_mode = tuning(lib, 2, 1)
+    try:
+        run()
+        _lib.check(lib.wvg_search_device_check(ctx.handle, ws.data_ptr(), st))
+        good = ids.cpu().numpy().copy()
+        assert (cc.cpu().numpy() == k).all()
+        old = tuning(lib, 8, 1)
+        try:
+            run()
+            rc = lib.wvg_search_device_check(ctx.handle, ws.data_ptr(), st)
+        finally:
+            tuning(lib, 8, old)
+        assert rc == _lib.WVG_ERR_DEVICE
+        assert b"timed out" in lib.wvg_last_error()
+        got_c = cc.cpu().numpy()
+        got_i = ids.cpu().numpy()
+        for qi in range(nq):  # each query is either fully merged or empty -- never stale
+            if got_c[qi] == 0:
+                assert (got_i[qi].view(np.uint64) == NONE).all()
+            else:
+                assert np.array_equal(got_i[qi], good[qi])
+        assert (got_c == 0).any()
+        # the check cleared the sticky word; a normal call passes again
+        run()
+        _lib.check(lib.wvg_search_device_check(ctx.handle, ws.data_ptr(), st))
+        assert np.array_equal(ids.cpu().numpy(), good)
+    finally:
+        tuning(lib, 2, old_mode)
+        c.destroy()
+
+
+@pytest.mark.parametrize("kind", [KIND_F32, KIND_BQ])
+def test_allow_list_over_large_docid_space(ctx, orc, kind):
+    """The allow bitmap spans docIDs far beyond this corpus (a 1B-id index
+    whose rank holds [id_base, id_base + n)); only the corpus's window is read."""
+    n, d, k = 5000, 128, 10
+    base = 64 * 1_000_000
+    rows = orc.synth_rows(91, 0, n, d, 0)
+    q = orc.synth_rows(92, 0, 1, d, 0)[0]
+    c = Corpus(ctx, kind, METRIC_L2, d, n, id_base=base)
+    c.upsert(np.arange(base, base + n, dtype=np.uint64), rows)
+    rng = np.random.default_rng(1)
+    inside = np.sort(rng.choice(np.arange(base + 100, base + 4900), 300, replace=False)).astype(np.uint64)
+    outside = np.array([0, 5, base - 1, base + n, base + n + 64, 3 * base], np.uint64)
+    bm = allow_bitmap(np.concatenate([inside, outside]), n_bits=4 * base)
+    ids, dists, counts = c.search(q, k, bm)
+    if kind == KIND_F32:
+        all_d = orc.dist_all(0, q, rows)
+    else:
+        all_d = orc.bq_dist_all(orc.bq_encode(q), np.stack([orc.bq_encode(r) for r in rows]))
+    sl = (inside - base).astype(np.int64)
+    wi, wd = orc.lex_topk(all_d[sl], inside, k)
+    assert counts[0] == k and np.array_equal(ids[0], wi) and np.array_equal(bits(dists[0]), bits(wd))
+    # ids only outside this corpus -> empty; a bitmap that ends before the corpus -> empty
+    for bm2 in (allow_bitmap(outside, n_bits=4 * base), allow_bitmap([3, 64], n_bits=128)):
+        assert c.search(q, k, bm2)[2][0] == 0
+    # k > 256 (select path) with the same window
+    ids, dists, counts = c.search(q, 290, bm)
+    wi, wd = orc.lex_topk(all_d[sl], inside, 290)
+    assert counts[0] == 290 and np.array_equal(ids[0], wi)
+
+
+def test_pq_codebook_shape_and_code_validation(ctx, orc):
+    d, m, ks = 64, 16, 16
+    c = Corpus(ctx, KIND_PQ, METRIC_L2, d, 640)
+    centers = orc.synth_rows(7, 0, m * ks, d // m, 0).reshape(m, ks, d // m)
+    c.set_codebook(centers)
+    codes = (np.arange(10 * m) % ks).astype(np.uint8).reshape(10, m)
+    c.upsert_codes(np.arange(10, dtype=np.uint64), codes)
+    with pytest.raises(_lib.WvgError, match="cannot change centroids"):
+        c.set_codebook(orc.synth_rows(8, 0, m * 8, d // m, 0).reshape(m, 8, d // m))
+    bad = codes.copy()
+    bad[3, 5] = ks  # indexes past the m x ks LUT
+    with pytest.raises(_lib.WvgError, match="not below centroids"):
+        c.upsert_codes(np.arange(20, 30, dtype=np.uint64), bad)
+    assert c.info()[0] == 10  # the rejected call stored nothing
+    c.set_codebook(centers)  # same shape: allowed
+
+
+def test_merge_packed_equals_merge_device(ctx, orc):
+    import torch
+
+    from weaviate_amd.shard import pack_block
+
+    lib = _lib.load()
+    dev = torch.device("cuda:0")
+    G, nq, k = 8, 5, 100
+    rng = np.random.default_rng(11)
+    d = np.floor(rng.uniform(0, 40, (G, nq, k))).astype(np.float32)
+    ids = rng.permutation(G * nq * k).reshape(G, nq, k).astype(np.uint64)
+    ids[2, 1, 50:] = NONE
+    d[2, 1, 50:] = np.inf
+    packed = torch.from_numpy(np.concatenate([pack_block(ids[g], d[g]) for g in range(G)])).to(dev)
+    outs = []
+    for packed_call in (False, True):
+        oi = torch.empty((nq, k), dtype=torch.int64, device=dev)
+        od = torch.empty((nq, k), dtype=torch.float32, device=dev)
+        oc = torch.empty(nq, dtype=torch.int32, device=dev)
+        if packed_call:
+            _lib.check(lib.wvg_topk_merge_packed(ctx.handle, packed.data_ptr(), nq, G, k, k, oi.data_ptr(),
+                                                 od.data_ptr(), oc.data_ptr(), None))
+        else:
+            td = torch.from_numpy(d).to(dev)
+            ti = torch.from_numpy(ids.view(np.int64)).to(dev)
+            _lib.check(lib.wvg_topk_merge_device(ctx.handle, td.data_ptr(), ti.data_ptr(), nq, G, k, k,
+                                                 oi.data_ptr(), od.data_ptr(), oc.data_ptr(), None))
+        torch.cuda.synchronize()
+        outs.append((oi.cpu().numpy().view(np.uint64), od.cpu().numpy(), oc.cpu().numpy()))
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(bits(outs[0][1]), bits(outs[1][1]))
+    for qi in range(nq):
+        live = ids[:, qi, :] != NONE
+        wi, wd = orc.lex_topk(d[:, qi, :][live], ids[:, qi, :][live], k)
+        assert np.array_equal(outs[1][0][qi], wi) and np.array_equal(bits(outs[1][1][qi]), bits(wd))

@@ -49,6 +49,7 @@ SIGNATURES = {
                                                  _P(c_float), _P(c_uint8)]),
     "wvg_corpus_delete": (c_int, [c_void_p, _P(c_uint64), c_uint64]),
     "wvg_corpus_get": (c_int, [c_void_p, c_uint64, c_void_p]),
+    "wvg_corpus_get_batch": (c_int, [c_void_p, _P(c_uint64), c_uint64, c_void_p, _P(c_uint8)]),
     "wvg_corpus_fill_synthetic": (c_int, [c_void_p, c_uint64, c_uint64, c_int]),
     "wvg_pq_set_codebook": (c_int, [c_void_p, _P(c_float), c_uint32, c_uint32]),
     "wvg_search": (c_int, [c_void_p, _P(c_float), c_uint32, c_uint32, _P(c_uint64), c_uint64,
@@ -63,6 +64,10 @@ SIGNATURES = {
     "wvg_search_device_pipelined": (c_int, [c_void_p, c_void_p, c_uint32, c_uint32, c_void_p, c_void_p, c_void_p,
                                             c_void_p, c_size_t, c_void_p]),
     "wvg_topk_merge_device": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_uint32, c_uint32, c_uint32,
+                                      c_void_p, c_void_p, c_void_p, c_void_p]),
+    "wvg_search_device_check": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "wvg_topk_packed_bytes": (c_size_t, [c_uint32, c_uint32]),
+    "wvg_topk_merge_packed": (c_int, [c_void_p, c_void_p, c_uint32, c_uint32, c_uint32, c_uint32,
                                       c_void_p, c_void_p, c_void_p, c_void_p]),
     "wvg_rescore": (c_int, [c_void_p, c_int, _P(c_float), _P(c_float), _P(c_uint64), c_uint64, c_uint32, c_uint32,
                             _P(c_uint64), _P(c_float), _P(c_uint32)]),

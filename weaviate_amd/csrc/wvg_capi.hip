@@ -155,7 +155,11 @@ struct Bulk {
     hipStream_t s() const { return g.slot->stream; }
 };
 
-// Allow bitmap -> tile range [tb, te) of slots that can be allowed; false if empty.
+// Allow bitmap -> tile range [tb, te) of slots that can be allowed; false if
+// empty.  Only the words of this corpus's own docID window are read (the
+// bitmap is over global docIDs and word w covers docIDs 64w..64w+63, so the
+// word of tile t is id_base/64 + t): O(corpus tiles) host work however large
+// the docID space is; the scan then gets the words of [tb, te) only.
 static bool allow_tile_range(const wvg_corpus *c, const uint64_t *allow, uint64_t allow_words, uint64_t &tb,
                              uint64_t &te)
 {
@@ -163,21 +167,18 @@ static bool allow_tile_range(const wvg_corpus *c, const uint64_t *allow, uint64_
     tb = 0;
     te = hw_tiles;
     if (!allow) return hw_tiles > 0;
-    int64_t first = -1, last = -1;
-    for (uint64_t w = 0; w < allow_words; w++)
-        if (allow[w]) {
-            if (first < 0) first = (int64_t)w;
-            last = (int64_t)w;
-        }
-    if (first < 0) return false;  // allow.IsEmpty() -> nothing (V/flat/index.go:425-427)
-    const uint64_t lo_id = (uint64_t)first * 64 + (uint64_t)__builtin_ctzll(allow[first]);
-    const uint64_t hi_id = (uint64_t)last * 64 + 63 - (uint64_t)__builtin_clzll(allow[last]);
-    if (hi_id < c->id_base) return false;
-    const uint64_t lo_slot = lo_id > c->id_base ? lo_id - c->id_base : 0;
-    const uint64_t hi_slot = hi_id - c->id_base;
-    tb = std::min(lo_slot / 64, hw_tiles);
-    te = std::min(hi_slot / 64 + 1, hw_tiles);
-    return te > tb;
+    const uint64_t wb = c->id_base / 64;
+    if (allow_words <= wb) return false;
+    const uint64_t n = std::min(allow_words - wb, hw_tiles);
+    const uint64_t *w = allow + wb;
+    uint64_t first = 0;
+    while (first < n && !w[first]) first++;
+    if (first == n) return false;  // allow.IsEmpty() (here: for this corpus) -> nothing (V/flat/index.go:425-427)
+    uint64_t last = n - 1;
+    while (!w[last]) last--;
+    tb = first;
+    te = last + 1;
+    return true;
 }
 
 static int check_corpus(wvg_corpus *c)
@@ -330,35 +331,54 @@ int wvg_synchronize(wvg_ctx *ctx)
 }
 
 // ---------------------------------------------------------------------------
+// (Re)allocates the row tiles and validity words for `capacity` rows, keeping
+// the rows of the old allocation.  The zero fill and the copy of the old rows
+// run on a pool stream and complete before this returns: every later writer
+// (upsert, synthetic fill, load_kv) runs on a non-blocking pool stream, which
+// does not order against the legacy null stream, so a null-stream memset
+// could land after -- and wipe -- rows written right after creation.  On any
+// failure the new buffers are freed and the corpus keeps its old storage.
 static int corpus_alloc(wvg_corpus *c, uint64_t capacity)
 {
     const uint64_t tiles = tiles_of(capacity);
     const size_t row_bytes = corpus_row_bytes(c->kind, c->dim, c->pq_m);
     void *data = nullptr;
     uint64_t *valid = nullptr;
+    auto drop = [&](int code, const char *what, hipError_t e) {
+        if (data) (void)hipFree(data);
+        if (valid) (void)hipFree(valid);
+        return fail(code, std::string(what) + ": " + hipGetErrorString(e));
+    };
     if (tiles > 0) {
-        if (row_bytes > 0) {
-            hipError_t e = hipMalloc(&data, tiles * 64 * row_bytes);
-            if (e != hipSuccess) return fail(WVG_ERR_NOMEM, std::string("corpus hipMalloc: ") + hipGetErrorString(e));
-            e = hipMemset(data, 0, tiles * 64 * row_bytes);
-            if (e != hipSuccess) {
-                (void)hipFree(data);
-                return fail(WVG_ERR_DEVICE, std::string("corpus hipMemset: ") + hipGetErrorString(e));
-            }
+        hipError_t e;
+        if (row_bytes > 0 && (e = hipMalloc(&data, tiles * 64 * row_bytes)) != hipSuccess) {
+            data = nullptr;
+            return drop(WVG_ERR_NOMEM, "corpus hipMalloc", e);
         }
-        hipError_t e = hipMalloc(&valid, tiles * 8);
-        if (e != hipSuccess) {
+        if ((e = hipMalloc(&valid, tiles * 8)) != hipSuccess) {
+            valid = nullptr;
+            return drop(WVG_ERR_NOMEM, "validity hipMalloc", e);
+        }
+        SlotGuard g(c->ctx);
+        int rc = c->ctx->acquire(&g.slot);
+        if (rc) {
             if (data) (void)hipFree(data);
-            return fail(WVG_ERR_NOMEM, std::string("validity hipMalloc: ") + hipGetErrorString(e));
+            (void)hipFree(valid);
+            return rc;
         }
-        (void)hipMemset(valid, 0, tiles * 8);
-    }
-    const uint64_t old_tiles = tiles_of(c->capacity);
-    if (c->d_data && data && old_tiles > 0) {
-        WVG_HIP(hipMemcpy(data, c->d_data, std::min(old_tiles, tiles) * 64 * row_bytes, hipMemcpyDeviceToDevice));
-    }
-    if (c->d_valid && valid && old_tiles > 0) {
-        WVG_HIP(hipMemcpy(valid, c->d_valid, std::min(old_tiles, tiles) * 8, hipMemcpyDeviceToDevice));
+        const hipStream_t s = g.slot->stream;
+        const uint64_t keep = std::min(tiles_of(c->capacity), tiles);
+        const size_t keep_data = (c->d_data && data) ? keep * 64 * row_bytes : 0;
+        const size_t keep_valid = c->d_valid ? keep * 8 : 0;
+        if (data && keep_data && (e = hipMemcpyAsync(data, c->d_data, keep_data, hipMemcpyDeviceToDevice, s)) != hipSuccess)
+            return drop(WVG_ERR_DEVICE, "corpus row copy", e);
+        if (data && (e = hipMemsetAsync((char *)data + keep_data, 0, tiles * 64 * row_bytes - keep_data, s)) != hipSuccess)
+            return drop(WVG_ERR_DEVICE, "corpus zero fill", e);
+        if (keep_valid && (e = hipMemcpyAsync(valid, c->d_valid, keep_valid, hipMemcpyDeviceToDevice, s)) != hipSuccess)
+            return drop(WVG_ERR_DEVICE, "validity copy", e);
+        if ((e = hipMemsetAsync((char *)valid + keep_valid, 0, tiles * 8 - keep_valid, s)) != hipSuccess)
+            return drop(WVG_ERR_DEVICE, "validity zero fill", e);
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return drop(WVG_ERR_DEVICE, "corpus alloc sync", e);
     }
     if (c->d_data) (void)hipFree(c->d_data);
     if (c->d_valid) (void)hipFree(c->d_valid);
@@ -569,6 +589,14 @@ int wvg_corpus_upsert_codes(wvg_corpus *c, const uint64_t *ids, const void *code
     if (rc) return rc;
     const size_t rb = host_row_bytes(c);
     const uint64_t nr = rows.size();
+    if (c->kind == WVG_KIND_PQ && c->pq_ks < 256) {  // a code indexes the m x ks LUT
+        const unsigned char *cb = (const unsigned char *)codes;
+        for (uint64_t i = 0; i < n * rb; i++)
+            if (cb[i] >= c->pq_ks)
+                return fail(WVG_ERR_INVALID, "PQ code " + std::to_string(cb[i]) + " of row " +
+                                                 std::to_string(i / rb) + " is not below centroids (" +
+                                                 std::to_string(c->pq_ks) + ")");
+    }
     Carver cv;
     const size_t o_codes = cv.take(nr * rb), o_slots = cv.take(nr * 8);
     void *base = nullptr;
@@ -652,6 +680,63 @@ int wvg_corpus_get(wvg_corpus *c, uint64_t id, void *out)
     return WVG_OK;
 }
 
+int wvg_corpus_get_batch(wvg_corpus *c, const uint64_t *ids, uint64_t n, void *out, uint8_t *out_ok)
+{
+    int rc = check_corpus(c);
+    if (rc) return rc;
+    if (n == 0) return WVG_OK;
+    if (!ids || !out || !out_ok) return fail(WVG_ERR_INVALID, "null argument");
+    std::shared_lock<std::shared_mutex> lk(c->rw);
+    const size_t rb = host_row_bytes(c), cb = (size_t)c->nchunks * 16;
+    std::vector<uint64_t> slots, where;  // live rows: slot, output index
+    slots.reserve(n);
+    where.reserve(n);
+    for (uint64_t i = 0; i < n; i++) {
+        const bool in = ids[i] >= c->id_base && ids[i] - c->id_base < c->capacity;
+        const uint64_t s = in ? ids[i] - c->id_base : 0;
+        const bool live = in && ((c->h_valid[s >> 6] >> (s & 63)) & 1ull);
+        out_ok[i] = live ? 1 : 0;
+        if (live) {
+            slots.push_back(s);
+            where.push_back(i);
+        } else {
+            std::memset((char *)out + i * rb, 0, rb);
+        }
+    }
+    if (slots.empty()) return WVG_OK;
+    SlotGuard g(c->ctx);
+    rc = c->ctx->acquire(&g.slot);
+    if (rc) return rc;
+    const hipStream_t st = g.slot->stream;
+    const uint64_t batch = std::max<uint64_t>(1, ((size_t)256 << 20) / (cb + 8));
+    std::vector<unsigned char> buf;
+    for (uint64_t r0 = 0; r0 < slots.size(); r0 += batch) {
+        const uint64_t nr = std::min<uint64_t>(batch, slots.size() - r0);
+        Carver cv;
+        const size_t o_s = cv.take(nr * 8), o_o = cv.take(nr * cb);
+        void *base = nullptr;
+        rc = g.slot->device_scratch(cv.off, &base);
+        if (rc) return rc;
+        char *b = (char *)base;
+        buf.resize(nr * cb);
+        WVG_HIP(hipMemcpyAsync(b + o_s, slots.data() + r0, nr * 8, hipMemcpyHostToDevice, st));
+        WVG_HIP(launch_gather_chunks(c->d_data, (const uint64_t *)(b + o_s), nr, c->nchunks, b + o_o, st));
+        WVG_HIP(hipMemcpyAsync(buf.data(), b + o_o, nr * cb, hipMemcpyDeviceToHost, st));
+        WVG_HIP(hipStreamSynchronize(st));
+        for (uint64_t j = 0; j < nr; j++) {
+            unsigned char *o = (unsigned char *)out + where[r0 + j] * rb;
+            const unsigned char *src = buf.data() + j * cb;
+            if (c->kind == WVG_KIND_PQ && pq_rotated(c->pq_m)) {  // stored byte b = code[(b + slot) mod 32]
+                const uint32_t rot = (uint32_t)(slots[r0 + j] & 31);
+                for (uint32_t q = 0; q < 32; q++) o[(q + rot) & 31u] = src[q];
+            } else {
+                std::memcpy(o, src, rb);
+            }
+        }
+    }
+    return WVG_OK;
+}
+
 int wvg_corpus_fill_synthetic(wvg_corpus *c, uint64_t seed, uint64_t n, int distribution)
 {
     int rc = check_corpus(c);
@@ -703,15 +788,31 @@ int wvg_pq_set_codebook(wvg_corpus *c, const float *centers, uint32_t m, uint32_
     if (ks == 0) return fail(WVG_ERR_INVALID, "centroids must be > 0");
     if (c->dim % m != 0) return fail(WVG_ERR_INVALID, "segments should be an integer divisor of dimensions");
     std::unique_lock<std::shared_mutex> lk(c->rw);
+    // stored codes index the codebook: a non-empty corpus keeps its shape
     if (c->count > 0 && m != c->pq_m) return fail(WVG_ERR_INVALID, "cannot change segments of a non-empty PQ corpus");
+    if (c->count > 0 && ks != c->pq_ks)
+        return fail(WVG_ERR_INVALID, "cannot change centroids of a non-empty PQ corpus");
     const uint32_t ds = c->dim / m;
     float *dc = nullptr;
     WVG_HIP(hipMalloc(&dc, pq_centers_alloc_bytes(m, ks, ds)));
-    WVG_HIP(hipMemcpy(dc, centers, (size_t)m * ks * ds * 4, hipMemcpyHostToDevice));
-    if (pq_has_pairs(ks, ds)) {
-        std::vector<float> pairs((size_t)m * ks * ds);
-        pq_pair_layout(centers, m, ks, pairs.data());
-        WVG_HIP(hipMemcpy(dc + (size_t)m * ks * ds, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice));
+    {
+        std::vector<float> pairs(pq_has_pairs(ks, ds) ? (size_t)m * ks * ds : 0);
+        if (!pairs.empty()) pq_pair_layout(centers, m, ks, pairs.data());
+        SlotGuard g(c->ctx);
+        rc = c->ctx->acquire(&g.slot);
+        hipError_t e = hipSuccess;
+        if (!rc) {
+            const hipStream_t s = g.slot->stream;
+            e = hipMemcpyAsync(dc, centers, (size_t)m * ks * ds * 4, hipMemcpyHostToDevice, s);
+            if (e == hipSuccess && !pairs.empty())
+                e = hipMemcpyAsync(dc + (size_t)m * ks * ds, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice, s);
+            const hipError_t e2 = hipStreamSynchronize(s);  // `pairs` is a host temporary
+            if (e == hipSuccess) e = e2;
+        }
+        if (rc || e != hipSuccess) {
+            (void)hipFree(dc);
+            return rc ? rc : fail(WVG_ERR_DEVICE, std::string("codebook copy: ") + hipGetErrorString(e));
+        }
     }
     if (c->d_centers) (void)hipFree(c->d_centers);
     c->d_centers = dc;
@@ -777,44 +878,13 @@ struct ProfArm {
     }
 };
 
-// Runs phase 1 + phase 2 for one corpus with device-resident prepared queries.
-static int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t nq, uint32_t k, const uint64_t *d_allow,
-                      uint64_t allow_words, uint64_t tb, uint64_t te, uint64_t *partials, int groups, bool gemm,
-                      uint64_t *ids, float *dists, uint32_t *counts, hipStream_t s)
-{
-    ScanArgs a{};
-    a.data = c->d_data;
-    a.valid = c->d_valid;
-    a.allow = d_allow;
-    a.allow_words = allow_words;
-    a.id_base = c->id_base;
-    a.tile_begin = tb;
-    a.tile_end = te;
-    a.dim = c->dim;
-    a.nchunks = c->nchunks;
-    a.metric = c->metric;
-    a.queries = d_q;
-    a.qpitch = qpitch;
-    a.nq = nq;
-    a.k = k;
-    a.pq_m = c->pq_m;
-    a.pq_ks = c->pq_ks;
-    ProfArm arm(c->ctx);
-    if (arm.rc) return arm.rc;
-    if (gemm)
-        WVG_HIP(launch_gemm_topk(a, (uint32_t)groups, partials,
-                                 reinterpret_cast<uint32_t *>(partials + (size_t)nq * groups * k), c->ctx->num_cus, s));
-    else
-        WVG_HIP(launch_scan(a, c->kind, partials, groups, s));
-    WVG_HIP(launch_merge_lists(partials, nq, (uint32_t)groups, k, k, c->id_base, ids, dists, counts, s));
-    return WVG_OK;
-}
-
 struct SearchPlan {
     uint64_t tb = 0, te = 0;
     int groups = 1;      // scan: workgroups per query; gemm: row ranges
     bool gemm = false;   // K3 batched MFMA path
     bool empty = false;
+    const uint64_t *allow_host = nullptr;  // the caller's allow words of tiles [tb, te), or null
+    size_t allow_bytes() const { return allow_host ? (size_t)(te - tb) * 8 : 0; }
     size_t partial_keys(uint32_t nq, uint32_t k) const { return (size_t)nq * groups * k; }
     // K3b's per-row-range progress counters follow the partial lists (gemm only)
     size_t workspace_bytes(uint32_t nq, uint32_t k) const
@@ -827,6 +897,7 @@ static SearchPlan plan_search(wvg_corpus *c, uint32_t nq, uint32_t k, const uint
 {
     SearchPlan p;
     p.empty = !allow_tile_range(c, allow, allow_words, p.tb, p.te) || k == 0 || nq == 0;
+    if (allow && !p.empty) p.allow_host = allow + c->id_base / 64 + p.tb;
     ScanArgs a{};
     a.tile_begin = p.tb;
     a.tile_end = p.te;
@@ -841,6 +912,41 @@ static SearchPlan plan_search(wvg_corpus *c, uint32_t nq, uint32_t k, const uint
         p.groups = scan_groups_for(a, c->ctx->num_cus);
     return p;
 }
+
+// Runs phase 1 + phase 2 for one corpus with device-resident prepared queries.
+static int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t nq, uint32_t k, const uint64_t *d_allow,
+                      const SearchPlan &p, uint64_t *partials, uint64_t *ids, float *dists, uint32_t *counts,
+                      hipStream_t s)
+{
+    ScanArgs a{};
+    a.data = c->d_data;
+    a.valid = c->d_valid;
+    a.allow = d_allow;
+    a.allow_words = d_allow ? p.te - p.tb : 0;
+    a.allow_t0 = p.tb;
+    a.id_base = c->id_base;
+    a.tile_begin = p.tb;
+    a.tile_end = p.te;
+    a.dim = c->dim;
+    a.nchunks = c->nchunks;
+    a.metric = c->metric;
+    a.queries = d_q;
+    a.qpitch = qpitch;
+    a.nq = nq;
+    a.k = k;
+    a.pq_m = c->pq_m;
+    a.pq_ks = c->pq_ks;
+    ProfArm arm(c->ctx);
+    if (arm.rc) return arm.rc;
+    if (p.gemm)
+        WVG_HIP(launch_gemm_topk(a, (uint32_t)p.groups, partials,
+                                 reinterpret_cast<uint32_t *>(partials + (size_t)nq * p.groups * k), c->ctx->num_cus, s));
+    else
+        WVG_HIP(launch_scan(a, c->kind, partials, p.groups, s));
+    WVG_HIP(launch_merge_lists(partials, nq, (uint32_t)p.groups, k, k, c->id_base, ids, dists, counts, s));
+    return WVG_OK;
+}
+
 
 static void write_empty(uint32_t nq, uint32_t k, uint64_t *ids, float *dists, uint32_t *counts)
 {
@@ -919,7 +1025,7 @@ int wvg_search(wvg_corpus *c, const float *queries, uint32_t nq, uint32_t k, con
     Carver cv;
     const size_t o_q = cv.take(query_bytes(c, nq));
     const size_t o_qtmp = cv.take(c->kind == WVG_KIND_PQ ? (size_t)nq * c->dim * 4 : 0);
-    const size_t o_allow = cv.take(allow_bits ? allow_words * 8 : 0);
+    const size_t o_allow = cv.take(p.allow_bytes());
     const size_t o_part = cv.take(p.workspace_bytes(nq, k));
     const size_t o_ids = cv.take((size_t)nq * k * 8);
     const size_t o_d = cv.take((size_t)nq * k * 4);
@@ -933,12 +1039,12 @@ int wvg_search(wvg_corpus *c, const float *queries, uint32_t nq, uint32_t k, con
     rc = stage_queries(c, g.slot, queries, nq, b + o_q, qpitch, (float *)(b + o_q), b + o_qtmp);
     if (rc) return rc;
     const uint64_t *d_allow = nullptr;
-    if (allow_bits) {
-        WVG_HIP(hipMemcpyAsync(b + o_allow, allow_bits, allow_words * 8, hipMemcpyHostToDevice, s));
+    if (p.allow_host) {
+        WVG_HIP(hipMemcpyAsync(b + o_allow, p.allow_host, p.allow_bytes(), hipMemcpyHostToDevice, s));
         d_allow = (const uint64_t *)(b + o_allow);
     }
-    rc = run_search(c, b + o_q, qpitch, nq, k, d_allow, allow_words, p.tb, p.te, (uint64_t *)(b + o_part), p.groups,
-                    p.gemm, (uint64_t *)(b + o_ids), (float *)(b + o_d), (uint32_t *)(b + o_cnt), s);
+    rc = run_search(c, b + o_q, qpitch, nq, k, d_allow, p, (uint64_t *)(b + o_part), (uint64_t *)(b + o_ids),
+                    (float *)(b + o_d), (uint32_t *)(b + o_cnt), s);
     if (rc) return rc;
     if (out_ids) WVG_HIP(hipMemcpyAsync(out_ids, b + o_ids, (size_t)nq * k * 8, hipMemcpyDeviceToHost, s));
     if (out_dists) WVG_HIP(hipMemcpyAsync(out_dists, b + o_d, (size_t)nq * k * 4, hipMemcpyDeviceToHost, s));
@@ -956,13 +1062,14 @@ int wvg_search(wvg_corpus *c, const float *queries, uint32_t nq, uint32_t k, con
 namespace wvg {
 
 static ScanArgs scan_args_for(const wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t nq, uint32_t k,
-                              const uint64_t *d_allow, uint64_t allow_words, uint64_t tb, uint64_t te)
+                              const uint64_t *d_allow, uint64_t tb, uint64_t te)
 {
     ScanArgs a{};
     a.data = c->d_data;
     a.valid = c->d_valid;
     a.allow = d_allow;
-    a.allow_words = allow_words;
+    a.allow_words = d_allow ? te - tb : 0;
+    a.allow_t0 = tb;
     a.id_base = c->id_base;
     a.tile_begin = tb;
     a.tile_end = te;
@@ -1061,7 +1168,7 @@ static int search_large_k(wvg_corpus *c, const float *queries, uint32_t nq, uint
     Carver cv;
     const size_t o_q = cv.take(query_bytes(c, nq));
     const size_t o_qtmp = cv.take(c->kind == WVG_KIND_PQ ? (size_t)nq * c->dim * 4 : 0);
-    const size_t o_allow = cv.take(allow_bits ? allow_words * 8 : 0);
+    const size_t o_allow = cv.take(p.allow_bytes());
     size_t o_sel[6], temp_bytes = 0;
     SelectBufs::layout(cv, nslots, o_sel, temp_bytes);
     const size_t o_temp = cv.take(temp_bytes);
@@ -1075,15 +1182,15 @@ static int search_large_k(wvg_corpus *c, const float *queries, uint32_t nq, uint
     rc = stage_queries(c, g.slot, queries, nq, b + o_q, qpitch, (float *)(b + o_q), b + o_qtmp);
     if (rc) return rc;
     const uint64_t *d_allow = nullptr;
-    if (allow_bits) {
-        WVG_HIP(hipMemcpyAsync(b + o_allow, allow_bits, allow_words * 8, hipMemcpyHostToDevice, s));
+    if (p.allow_host) {
+        WVG_HIP(hipMemcpyAsync(b + o_allow, p.allow_host, p.allow_bytes(), hipMemcpyHostToDevice, s));
         d_allow = (const uint64_t *)(b + o_allow);
     }
     SelectBufs sb;
     sb.bind(b, o_sel, o_temp, temp_bytes);
     for (uint32_t qi = 0; qi < nq; qi++) {
         const void *dq = b + o_q + (size_t)qi * qpitch * query_elem_bytes(c);
-        ScanArgs a1 = scan_args_for(c, dq, qpitch, 1, k, d_allow, allow_words, p.tb, p.te);
+        ScanArgs a1 = scan_args_for(c, dq, qpitch, 1, k, d_allow, p.tb, p.te);
         uint64_t n = 0;
         rc = select_smallest(c, a1, k, sb, s, &n);
         if (rc) return rc;
@@ -1133,7 +1240,7 @@ static int bq_rescore_large(wvg_corpus *bq, wvg_corpus *f32, const float *querie
     Carver cv;
     const size_t o_qb = cv.take(query_bytes(bq, nq));
     const size_t o_qf = cv.take((size_t)nq * fpitch * 4);
-    const size_t o_allow = cv.take(allow_bits ? allow_words * 8 : 0);
+    const size_t o_allow = cv.take(p.allow_bytes());
     size_t o_sel[6], temp_bytes = 0;
     SelectBufs::layout(cv, nslots, o_sel, temp_bytes);
     const size_t o_temp = cv.take(temp_bytes);
@@ -1150,14 +1257,14 @@ static int bq_rescore_large(wvg_corpus *bq, wvg_corpus *f32, const float *querie
     rc = stage_queries(f32, g.slot, queries, nq, b + o_qf, qpf, nullptr, nullptr);
     if (rc) return rc;
     const uint64_t *d_allow = nullptr;
-    if (allow_bits) {
-        WVG_HIP(hipMemcpyAsync(b + o_allow, allow_bits, allow_words * 8, hipMemcpyHostToDevice, s));
+    if (p.allow_host) {
+        WVG_HIP(hipMemcpyAsync(b + o_allow, p.allow_host, p.allow_bytes(), hipMemcpyHostToDevice, s));
         d_allow = (const uint64_t *)(b + o_allow);
     }
     SelectBufs sb;
     sb.bind(b, o_sel, o_temp, temp_bytes);
     for (uint32_t qi = 0; qi < nq; qi++) {
-        ScanArgs a1 = scan_args_for(bq, b + o_qb + (size_t)qi * qpb * 8, qpb, 1, R, d_allow, allow_words, p.tb, p.te);
+        ScanArgs a1 = scan_args_for(bq, b + o_qb + (size_t)qi * qpb * 8, qpb, 1, R, d_allow, p.tb, p.te);
         uint64_t n = 0;
         rc = select_smallest(bq, a1, R, sb, s, &n);
         if (rc) return rc;
@@ -1228,7 +1335,7 @@ int wvg_search_by_distance(wvg_corpus *c, const float *query, float target_dista
     Carver cv;
     const size_t o_q = cv.take(query_bytes(c, 1));
     const size_t o_qtmp = cv.take(c->kind == WVG_KIND_PQ ? (size_t)c->dim * 4 : 0);
-    const size_t o_allow = cv.take(allow_bits ? allow_words * 8 : 0);
+    const size_t o_allow = cv.take(p.allow_bytes());
     size_t o_sel[6], temp_bytes = 0;
     SelectBufs::layout(cv, nslots, o_sel, temp_bytes);
     const size_t o_temp = cv.take(temp_bytes);
@@ -1242,14 +1349,14 @@ int wvg_search_by_distance(wvg_corpus *c, const float *query, float target_dista
     rc = stage_queries(c, g.slot, query, 1, b + o_q, qpitch, (float *)(b + o_q), b + o_qtmp);
     if (rc) return rc;
     const uint64_t *d_allow = nullptr;
-    if (allow_bits) {
-        WVG_HIP(hipMemcpyAsync(b + o_allow, allow_bits, allow_words * 8, hipMemcpyHostToDevice, s));
+    if (p.allow_host) {
+        WVG_HIP(hipMemcpyAsync(b + o_allow, p.allow_host, p.allow_bytes(), hipMemcpyHostToDevice, s));
         d_allow = (const uint64_t *)(b + o_allow);
     }
     SelectBufs sb;
     sb.bind(b, o_sel, o_temp, temp_bytes);
     const int cus = c->ctx->num_cus;
-    ScanArgs a1 = scan_args_for(c, b + o_q, qpitch, 1, 1, d_allow, allow_words, p.tb, p.te);
+    ScanArgs a1 = scan_args_for(c, b + o_q, qpitch, 1, 1, d_allow, p.tb, p.te);
     WVG_HIP(launch_ordkeys(a1, c->kind, cus, sb.keys, s));
     const float t = target_distance;
     const uint32_t t_le = max_ord_where([t](float d) { return d <= t; });
@@ -1305,7 +1412,7 @@ int wvg_search_bq_rescore(wvg_corpus *bq, wvg_corpus *f32, const float *queries,
     Carver cv;
     const size_t o_qb = cv.take(query_bytes(bq, nq));
     const size_t o_qf = cv.take((size_t)nq * fpitch * 4);
-    const size_t o_allow = cv.take(allow_bits ? allow_words * 8 : 0);
+    const size_t o_allow = cv.take(p.allow_bytes());
     const size_t o_part = cv.take(p.workspace_bytes(nq, R));
     const size_t o_cand = cv.take((size_t)nq * R * 8);
     const size_t o_resc = cv.take((size_t)nq * R * 8);
@@ -1323,8 +1430,8 @@ int wvg_search_bq_rescore(wvg_corpus *bq, wvg_corpus *f32, const float *queries,
     rc = stage_queries(f32, g.slot, queries, nq, b + o_qf, qpf, nullptr, nullptr);
     if (rc) return rc;
     const uint64_t *d_allow = nullptr;
-    if (allow_bits) {
-        WVG_HIP(hipMemcpyAsync(b + o_allow, allow_bits, allow_words * 8, hipMemcpyHostToDevice, s));
+    if (p.allow_host) {
+        WVG_HIP(hipMemcpyAsync(b + o_allow, p.allow_host, p.allow_bytes(), hipMemcpyHostToDevice, s));
         d_allow = (const uint64_t *)(b + o_allow);
     }
     // Hamming top-R keys (slot in the low 32 bits): phase 1 + a keys-only phase 2
@@ -1332,7 +1439,8 @@ int wvg_search_bq_rescore(wvg_corpus *bq, wvg_corpus *f32, const float *queries,
     a.data = bq->d_data;
     a.valid = bq->d_valid;
     a.allow = d_allow;
-    a.allow_words = allow_words;
+    a.allow_words = d_allow ? p.te - p.tb : 0;
+    a.allow_t0 = p.tb;
     a.id_base = bq->id_base;
     a.tile_begin = p.tb;
     a.tile_end = p.te;
@@ -1360,17 +1468,21 @@ int wvg_search_bq_rescore(wvg_corpus *bq, wvg_corpus *f32, const float *queries,
     return WVG_OK;
 }
 
-// Workspace of the query-stream scan: partial lists [nq][groups][k], then the
-// per-query arrival counters and the status word.
+// Device-search workspaces start with a 256-byte status block (the sticky
+// status word read by wvg_search_device_check); the scan workspace follows.
+static const size_t WS_STATUS_BYTES = 256;
+
+// Workspace of the query-stream scan (after the status block): partial lists
+// [nq][groups][k], then the per-query arrival counters.
 struct StreamLayout {
     size_t partials = 0, arrivals = 0, total = 0;
 };
 static StreamLayout stream_layout(const SearchPlan &p1, uint32_t nq, uint32_t k)
 {
     StreamLayout l;
-    l.partials = 0;
-    l.arrivals = align_up((size_t)nq * p1.groups * k * 8, 256);
-    l.total = l.arrivals + align_up(((size_t)nq + 1) * 4, 256);  // memset block: 16-B multiple
+    l.partials = WS_STATUS_BYTES;
+    l.arrivals = l.partials + align_up((size_t)nq * p1.groups * k * 8, 256);
+    l.total = l.arrivals + align_up((size_t)nq * 4, 256);  // memset block: 16-B multiple
     return l;
 }
 
@@ -1382,7 +1494,24 @@ size_t wvg_search_workspace_size(wvg_corpus *c, uint32_t nq, uint32_t k)
     SearchPlan p1 = plan_search(c, 1, k, nullptr, 0);  // pipelined: two single-query buffers, or the stream layout
     const size_t chain = 2 * align_up(p1.workspace_bytes(1, kk), 256);
     const size_t stream = stream_layout(p1, nq, kk).total;
-    return std::max({align_up(p.workspace_bytes(nq, kk), 256), chain, stream});
+    return std::max({WS_STATUS_BYTES + align_up(p.workspace_bytes(nq, kk), 256), WS_STATUS_BYTES + chain, stream});
+}
+
+int wvg_search_device_check(wvg_ctx *ctx, void *d_workspace, void *stream)
+{
+    if (!ctx || !d_workspace) return fail(WVG_ERR_INVALID, "null ctx/workspace");
+    WVG_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = (hipStream_t)stream;
+    uint32_t st = 0;
+    WVG_HIP(hipMemcpyAsync(&st, d_workspace, 4, hipMemcpyDeviceToHost, s));
+    WVG_HIP(hipStreamSynchronize(s));
+    if (st == 0) return WVG_OK;
+    WVG_HIP(hipMemsetAsync(d_workspace, 0, 4, s));
+    WVG_HIP(hipStreamSynchronize(s));
+    if (st & WVG_STATUS_MERGE_TIMEOUT)
+        return fail(WVG_ERR_DEVICE, "query-stream merge timed out waiting for the scan workgroups; "
+                                    "the affected queries returned empty results");
+    return fail(WVG_ERR_DEVICE, "device search status " + std::to_string(st));
 }
 
 int wvg_search_device_pipelined(wvg_corpus *c, const float *d_queries, uint32_t nq, uint32_t k, uint64_t *d_ids,
@@ -1397,7 +1526,10 @@ int wvg_search_device_pipelined(wvg_corpus *c, const float *d_queries, uint32_t 
     hipStream_t s = (hipStream_t)stream;
     std::shared_lock<std::shared_mutex> lk(c->rw);
     SearchPlan p = plan_search(c, 1, k, nullptr, 0);
-    if (p.empty) return WVG_OK;
+    if (p.empty) {  // empty corpus / slab: empty results, as wvg_search's write_empty
+        WVG_HIP(launch_fill_empty(d_ids, d_dists, d_counts, nq, k, s));
+        return WVG_OK;
+    }
     if (tuning().pipeline_mode == 1) {  // query-stream kernel: one launch for all nq queries
         const StreamLayout l = stream_layout(p, nq, k);
         if (!d_workspace || workspace_bytes < l.total) return fail(WVG_ERR_INVALID, "workspace too small");
@@ -1405,7 +1537,8 @@ int wvg_search_device_pipelined(wvg_corpus *c, const float *d_queries, uint32_t 
         StreamJob j{};
         j.partials = (uint64_t *)(w + l.partials);
         j.arrivals = (uint32_t *)(w + l.arrivals);
-        j.status = j.arrivals + nq;
+        j.status = (uint32_t *)w;
+        j.wait_limit = tuning().merge_wait_us > 0 ? (uint64_t)tuning().merge_wait_us * 100ull : 400000000ull;
         j.groups = (uint32_t)p.groups;
         j.ids = d_ids;
         j.dists = d_dists;
@@ -1423,15 +1556,16 @@ int wvg_search_device_pipelined(wvg_corpus *c, const float *d_queries, uint32_t 
         a.qpitch = c->dim;
         a.nq = nq;
         a.k = k;
-        WVG_HIP(hipMemsetAsync(j.arrivals, 0, align_up(((size_t)nq + 1) * 4, 16), s));
+        WVG_HIP(hipMemsetAsync(j.arrivals, 0, align_up((size_t)nq * 4, 16), s));
         ProfArm arm(c->ctx);
         if (arm.rc) return arm.rc;
         WVG_HIP(launch_scan_f32_stream(a, j, s));
         return WVG_OK;
     }
     const size_t half = align_up(p.workspace_bytes(1, k), 256);
-    if (!d_workspace || workspace_bytes < 2 * half) return fail(WVG_ERR_INVALID, "workspace too small");
-    uint64_t *buf[2] = {(uint64_t *)d_workspace, (uint64_t *)((char *)d_workspace + half)};
+    if (!d_workspace || workspace_bytes < WS_STATUS_BYTES + 2 * half) return fail(WVG_ERR_INVALID, "workspace too small");
+    char *w0 = (char *)d_workspace + WS_STATUS_BYTES;
+    uint64_t *buf[2] = {(uint64_t *)w0, (uint64_t *)(w0 + half)};
     ScanArgs a{};
     a.data = c->d_data;
     a.valid = c->d_valid;
@@ -1468,12 +1602,17 @@ int wvg_search_device(wvg_corpus *c, const float *d_queries, uint32_t nq, uint32
     if (k > MAX_K) return fail(WVG_ERR_UNSUPPORTED, "k above 256 is not supported by the fused top-k");
     if (c->kind != WVG_KIND_F32) return fail(WVG_ERR_UNSUPPORTED, "device search supports F32 corpora");
     if (c->dim % 4 != 0) return fail(WVG_ERR_UNSUPPORTED, "device search needs dim % 4 == 0");
+    if (nq == 0 || k == 0) return WVG_OK;
     hipStream_t s = (hipStream_t)stream;
     std::shared_lock<std::shared_mutex> lk(c->rw);
     SearchPlan p = plan_search(c, nq, k, nullptr, 0);
-    if (p.empty) return WVG_OK;
-    if (!d_workspace || workspace_bytes < p.workspace_bytes(nq, k)) return fail(WVG_ERR_INVALID, "workspace too small");
-    return run_search(c, d_queries, c->dim, nq, k, nullptr, 0, p.tb, p.te, (uint64_t *)d_workspace, p.groups, p.gemm,
+    if (p.empty) {  // empty corpus / slab (e.g. a rank with no rows): empty results
+        WVG_HIP(launch_fill_empty(d_ids, d_dists, d_counts, nq, k, s));
+        return WVG_OK;
+    }
+    if (!d_workspace || workspace_bytes < WS_STATUS_BYTES + p.workspace_bytes(nq, k))
+        return fail(WVG_ERR_INVALID, "workspace too small");
+    return run_search(c, d_queries, c->dim, nq, k, nullptr, p, (uint64_t *)((char *)d_workspace + WS_STATUS_BYTES),
                       d_ids, d_dists, d_counts, s);
 }
 
@@ -1484,8 +1623,24 @@ int wvg_topk_merge_device(wvg_ctx *ctx, const float *d_dists, const uint64_t *d_
     if (!ctx) return fail(WVG_ERR_INVALID, "null ctx");
     if ((uint64_t)nlists * k_in > 8192) return fail(WVG_ERR_UNSUPPORTED, "merge input above 8192 pairs per query");
     if (nq == 0 || k == 0) return WVG_OK;
-    WVG_HIP(launch_merge_pairs(d_dists, d_ids, nq, nlists, k_in, k, d_out_ids, d_out_dists, d_out_counts,
-                               (hipStream_t)stream));
+    const uint64_t stride = (uint64_t)nq * k_in;
+    WVG_HIP(launch_merge_pairs(d_dists, d_ids, stride, stride, nq, nlists, k_in, k, d_out_ids, d_out_dists,
+                               d_out_counts, (hipStream_t)stream));
+    return WVG_OK;
+}
+
+size_t wvg_topk_packed_bytes(uint32_t nq, uint32_t k) { return align_up((size_t)nq * k * 12, 16); }
+
+int wvg_topk_merge_packed(wvg_ctx *ctx, const void *d_packed, uint32_t nq, uint32_t nlists, uint32_t k_in, uint32_t k,
+                          uint64_t *d_out_ids, float *d_out_dists, uint32_t *d_out_counts, void *stream)
+{
+    if (!ctx || !d_packed) return fail(WVG_ERR_INVALID, "null ctx/input");
+    if ((uint64_t)nlists * k_in > 8192) return fail(WVG_ERR_UNSUPPORTED, "merge input above 8192 pairs per query");
+    if (nq == 0 || k == 0) return WVG_OK;
+    const size_t block = wvg_topk_packed_bytes(nq, k_in);
+    const char *b = (const char *)d_packed;
+    WVG_HIP(launch_merge_pairs((const float *)(b + (size_t)nq * k_in * 8), (const uint64_t *)b, block / 8, block / 4,
+                               nq, nlists, k_in, k, d_out_ids, d_out_dists, d_out_counts, (hipStream_t)stream));
     return WVG_OK;
 }
 
@@ -1597,7 +1752,7 @@ int wvg_synthetic_rows(wvg_ctx *ctx, uint64_t seed, const uint64_t *ids, uint64_
 }
 
 // Internal A/B knob (not part of include/wvgpu.h): 0 = K1 scan variant,
-// 1 = K1 resident workgroups per CU, ... 7 = K8 ADC variant.  Returns the previous value.
+// 1 = K1 resident workgroups per CU, ... 7 = K8 ADC variant, 8 = query-stream merge wait (us).  Returns the previous value.
 int wvgx_set_tuning(int key, int value)
 {
     Tuning &t = tuning();
@@ -1626,6 +1781,9 @@ int wvgx_set_tuning(int key, int value)
     } else if (key == 7) {
         old = t.pq_variant;
         t.pq_variant = value;
+    } else if (key == 8) {
+        old = t.merge_wait_us;
+        t.merge_wait_us = value;
     }
     return old;
 }
@@ -2012,7 +2170,7 @@ int wvg_corpus_distance_by_ids(wvg_corpus *c, const float *query, const uint64_t
     rc = stage_queries(c, g.slot, query, 1, b + o_q, qpitch, (float *)(b + o_q), b + o_qtmp);
     if (rc) return rc;
     WVG_HIP(hipMemcpyAsync(b + o_ids, ids, n * 8, hipMemcpyHostToDevice, s));
-    ScanArgs a = scan_args_for(c, b + o_q, qpitch, 1, 1, nullptr, 0, 0, tiles_of(c->high_water));
+    ScanArgs a = scan_args_for(c, b + o_q, qpitch, 1, 1, nullptr, 0, tiles_of(c->high_water));
     WVG_HIP(launch_dist_by_ids(a, c->kind, c->capacity, (const uint64_t *)(b + o_ids), n, (float *)(b + o_d),
                                (uint8_t *)(b + o_ok), s));
     WVG_HIP(hipMemcpyAsync(out_dists, b + o_d, n * 4, hipMemcpyDeviceToHost, s));
@@ -2056,7 +2214,7 @@ int wvg_corpus_distance_by_ids_batch(wvg_corpus *c, const float *queries, uint32
     if (rc) return rc;
     WVG_HIP(hipMemcpyAsync(b + o_ids, ids, n * 8, hipMemcpyHostToDevice, s));
     WVG_HIP(hipMemcpyAsync(b + o_qi, qidx.data(), n * 4, hipMemcpyHostToDevice, s));
-    ScanArgs a = scan_args_for(c, b + o_q, qpitch, nq, 1, nullptr, 0, 0, tiles_of(c->high_water));
+    ScanArgs a = scan_args_for(c, b + o_q, qpitch, nq, 1, nullptr, 0, tiles_of(c->high_water));
     WVG_HIP(launch_dist_by_ids(a, c->kind, c->capacity, (const uint64_t *)(b + o_ids), n, (float *)(b + o_d),
                                (uint8_t *)(b + o_ok), s, (const uint32_t *)(b + o_qi)));
     WVG_HIP(hipMemcpyAsync(out_dists, b + o_d, n * 4, hipMemcpyDeviceToHost, s));

@@ -42,6 +42,7 @@ struct GemmArgs {
     const uint64_t *valid;  // one word per tile
     const uint64_t *allow;
     uint64_t allow_words;
+    uint64_t allow_t0;      // tile whose validity word allow[0] masks (allow covers tiles [t0, t0 + words))
     uint64_t id_base;
     uint64_t tile_begin, tile_end;
     uint32_t dim, nchunks;  // nchunks: float4 chunks per row in the corpus layout
@@ -146,7 +147,7 @@ __global__ __launch_bounds__(GWAVES * 64) void gemm_topk_kernel(GemmArgs a, uint
     auto tile_live = [&](uint64_t t) {
         uint64_t m = sload64(a.valid + t);
         if (a.allow) {
-            const uint64_t w = (a.id_base >> 6) + t;
+            const uint64_t w = t - a.allow_t0;  // allow[0] is tile allow_t0's word
             m &= w < a.allow_words ? sload64(a.allow + w) : 0ull;
         }
         return m;
@@ -369,7 +370,7 @@ __global__ __launch_bounds__(RS_RG * QH * 64, 1) void gemm_rs_kernel(GemmArgs a,
     auto tile_live = [&](uint64_t t) -> uint64_t {
         uint64_t m = sload64(a.valid + t);
         if (a.allow) {
-            const uint64_t w = (a.id_base >> 6) + t;
+            const uint64_t w = t - a.allow_t0;  // allow[0] is tile allow_t0's word
             m &= w < a.allow_words ? sload64(a.allow + w) : 0ull;
         }
         return (m >> (16 * rg)) & 0xFFFFull;
@@ -679,6 +680,7 @@ hipError_t launch_gemm_topk(const ScanArgs &s, uint32_t nrr, uint64_t *partials,
     a.valid = s.valid;
     a.allow = s.allow;
     a.allow_words = s.allow_words;
+    a.allow_t0 = s.allow_t0;
     a.id_base = s.id_base;
     a.tile_begin = s.tile_begin;
     a.tile_end = s.tile_end;

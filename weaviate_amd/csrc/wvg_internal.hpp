@@ -169,8 +169,9 @@ struct MergeJob {
 struct ScanArgs {
     const void *data;          // tiled corpus
     const uint64_t *valid;     // one word per tile
-    const uint64_t *allow;     // allow bitmap over global ids, may be null
-    uint64_t allow_words;
+    const uint64_t *allow;     // allow bitmap window, may be null: allow[i] masks tile allow_t0 + i
+    uint64_t allow_words;      // tiles covered by the window (tiles outside it are not allowed)
+    uint64_t allow_t0;
     uint64_t id_base;
     uint64_t tile_begin, tile_end;
     uint32_t dim, nchunks;
@@ -189,16 +190,22 @@ hipError_t launch_scan_f32(const ScanArgs &a, uint64_t *partials, int groups, hi
 // workgroups loop over the queries, publishing each query's partial list with
 // a release + arrival count; one more workgroup waits for each query's
 // `groups` arrivals and merges it while the scan proceeds to the next query.
+// Sticky status word of a device-search workspace (its first bytes; read and
+// cleared by wvg_search_device_check).
+constexpr uint32_t WVG_STATUS_MERGE_TIMEOUT = 1u;
 struct StreamJob {
     uint64_t *partials;  // [nq][groups][k]
     uint32_t *arrivals;  // [nq], zero at launch
-    uint32_t *status;    // bit 0 set if the merge workgroup gave up waiting
+    uint32_t *status;    // WVG_STATUS_MERGE_TIMEOUT set if the merge workgroup gave up waiting
+    uint64_t wait_limit; // merge workgroup's wait per query, s_memrealtime ticks (100 MHz)
     uint32_t groups;
     uint64_t *ids;
     float *dists;
     uint32_t *counts;
 };
 hipError_t launch_scan_f32_stream(const ScanArgs &a, const StreamJob &j, hipStream_t s);
+// ids KEY_NONE, dists +inf, counts 0 for nq queries (empty corpus / slab).
+hipError_t launch_fill_empty(uint64_t *ids, float *dists, uint32_t *counts, uint32_t nq, uint32_t k, hipStream_t s);
 hipError_t launch_scan_bq(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s);
 hipError_t launch_scan_pq(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s);
 // K3 batched MFMA scoring (wvg_gemm.hip): partials [nq][nrr][K].
@@ -221,6 +228,7 @@ struct Tuning {
                              // next launch), 1 = one query-stream launch
     int pq_variant = 0;      // K8: 0 = rotated-segment ADC (K8b) where it applies (m = 32, ks = 256),
                              // 1 = K8 gather in segment order everywhere
+    int merge_wait_us = 0;   // query-stream merge workgroup's wait per query in us; 0 = 4 s (test knob)
 };
 Tuning &tuning();
 // Profiling: events armed by the host runtime (wvg_profile_start) are bound to
@@ -250,10 +258,11 @@ hipError_t launch_merge_lists(const uint64_t *partials, uint32_t nq, uint32_t nl
 hipError_t launch_merge_keys(const uint64_t *partials, uint32_t nq, uint32_t n_per_query, uint32_t k,
                              uint64_t id_base, uint64_t *ids, float *dists, uint32_t *counts,
                              hipStream_t s);
-// Merge (dist, id64) lists: [nq][nlists][k_in] -> [nq][k].
-hipError_t launch_merge_pairs(const float *dists, const uint64_t *ids, uint32_t nq, uint32_t nlists,
-                              uint32_t k_in, uint32_t k, uint64_t *out_ids, float *out_dists,
-                              uint32_t *out_counts, hipStream_t s);
+// Merge (dist, id64) lists -> [nq][k]: list l of query q starts at
+// ids + l * ids_stride + q * k_in (dists likewise with d_stride).
+hipError_t launch_merge_pairs(const float *dists, const uint64_t *ids, uint64_t ids_stride, uint64_t d_stride,
+                              uint32_t nq, uint32_t nlists, uint32_t k_in, uint32_t k, uint64_t *out_ids,
+                              float *out_dists, uint32_t *out_counts, hipStream_t s);
 
 // Row-major -> tiled scatter (with optional normalize for cosine) of F32 rows.
 hipError_t launch_f32_store(const float *rows, const uint64_t *slots, uint64_t n, uint32_t dim,
@@ -263,6 +272,9 @@ hipError_t launch_f32_synth(uint64_t seed, int dist, uint64_t row0, uint64_t n, 
                             hipStream_t s);
 hipError_t launch_f32_gather(const float *tiled, const uint64_t *slots, uint64_t n, uint32_t dim,
                              uint32_t nchunks, float *rows, hipStream_t s);
+// out[i] = the raw nchunks 16-byte chunks of slots[i] (any corpus kind).
+hipError_t launch_gather_chunks(const void *tiled, const uint64_t *slots, uint64_t n, uint32_t nchunks, void *out,
+                                hipStream_t s);
 hipError_t launch_normalize_rows(const float *in, uint64_t n, uint32_t dim, float *out,
                                  hipStream_t s);
 hipError_t launch_distance_rows(int metric, const float *q, const float *rows, uint64_t n,

@@ -40,7 +40,7 @@ __device__ __forceinline__ uint64_t tile_mask(const ScanArgs &a, uint64_t t)
 {
     uint64_t m = a.valid[t];
     if (a.allow) {
-        uint64_t w = (a.id_base >> 6) + t;
+        uint64_t w = t - a.allow_t0;  // allow[0] is tile allow_t0's word
         m &= w < a.allow_words ? a.allow[w] : 0ull;
     }
     return m;
@@ -155,6 +155,33 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_kernel(ScanArgs a, u
     group_combine_store<E, SCAN_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
 }
 
+// Empty results for queries [q0, nq): ids KEY_NONE, dists +inf, counts 0
+// (what the host path's write_empty returns for an empty corpus / slab).
+__device__ __forceinline__ void fill_empty_body(uint64_t *ids, float *dists, uint32_t *counts, uint32_t q0,
+                                                uint32_t nq, uint32_t k)
+{
+    const uint64_t n = (uint64_t)(nq - q0) * k, off = (uint64_t)q0 * k;
+    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        if (ids) ids[off + i] = WVG_KEY_NONE;
+        if (dists) dists[off + i] = __builtin_inff();
+    }
+    if (counts)
+        for (uint32_t q = q0 + threadIdx.x; q < nq; q += blockDim.x) counts[q] = 0;
+}
+
+__global__ __launch_bounds__(256) void fill_empty_kernel(uint64_t *ids, float *dists, uint32_t *counts, uint32_t nq,
+                                                         uint32_t k)
+{
+    fill_empty_body(ids, dists, counts, 0, nq, k);
+}
+
+hipError_t launch_fill_empty(uint64_t *ids, float *dists, uint32_t *counts, uint32_t nq, uint32_t k, hipStream_t s)
+{
+    if (nq == 0) return hipSuccess;
+    hipLaunchKernelGGL(fill_empty_kernel, dim3(1), dim3(256), 0, s, ids, dists, counts, nq, k);
+    return hipGetLastError();
+}
+
 // In-launch hand-off (cdna_hip_programming.md §6 Guideline 16, form R1): the
 // producer stores its list write-through (agent-scope relaxed atomic stores =
 // sc1), drains them (s_waitcnt vmcnt(0)) and adds to an arrival counter; no
@@ -163,16 +190,16 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_kernel(ScanArgs a, u
 typedef __attribute__((address_space(1))) uint32_t gu32;
 typedef __attribute__((address_space(1))) uint64_t gu64;
 
-// Thread 0 polls; false after ~4 s (s_memrealtime is 100 MHz), so a waiting
-// workgroup always exits.
-__device__ __forceinline__ bool wait_arrivals(uint32_t *ctr, uint32_t target)
+// Thread 0 polls; false after `limit` ticks of s_memrealtime (100 MHz; 4 s
+// by default), so a waiting workgroup always exits.
+__device__ __forceinline__ bool wait_arrivals(uint32_t *ctr, uint32_t target, uint64_t limit)
 {
     __shared__ int ok;
     if (threadIdx.x == 0) {
         const uint64_t start = __builtin_amdgcn_s_memrealtime();
         int r = 1;
         while (__hip_atomic_load((gu32 *)ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            if (__builtin_amdgcn_s_memrealtime() - start > 400000000ull) {
+            if (__builtin_amdgcn_s_memrealtime() - start > limit) {
                 r = 0;
                 break;
             }
@@ -237,8 +264,11 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_stream_kernel(ScanAr
     const uint32_t G = j.groups;
     if (blockIdx.x == G) {
         for (uint32_t q = 0; q < a.nq; q++) {
-            if (!wait_arrivals(j.arrivals + q, G)) {
-                if (threadIdx.x == 0) atomicOr(j.status, 1u);
+            if (!wait_arrivals(j.arrivals + q, G, j.wait_limit)) {
+                // gave up: queries q.. get empty results (never stale ones) and
+                // the sticky status word tells wvg_search_device_check
+                if (threadIdx.x == 0) atomicOr(j.status, WVG_STATUS_MERGE_TIMEOUT);
+                fill_empty_body(j.ids, j.dists, j.counts, q, a.nq, a.k);
                 return;
             }
             merge_lists_body<E, SCAN_WAVES>(j.partials + (size_t)q * G * a.k, G, a.k, a.k, a.id_base,
@@ -517,7 +547,11 @@ hipError_t launch_merge_keys(const uint64_t *partials, uint32_t nq, uint32_t n_p
 // ---------------------------------------------------------------------------
 constexpr int MERGE_PAIRS_MAX = 8192;
 
+// List l of query qi starts at ids + l * ids_stride + qi * k_in (and likewise
+// for dists): strides of nq * k_in for the plain [nlists][nq][k_in] arrays,
+// the packed block size for all-gathered wvg_topk_packed blocks.
 __global__ __launch_bounds__(1024) void merge_pairs_kernel(const float *dists, const uint64_t *ids,
+                                                           uint64_t ids_stride, uint64_t d_stride,
                                                            uint32_t nlists, uint32_t k_in, uint32_t k,
                                                            uint32_t pow2, uint64_t *out_ids,
                                                            float *out_dists, uint32_t *out_counts)
@@ -530,10 +564,10 @@ __global__ __launch_bounds__(1024) void merge_pairs_kernel(const float *dists, c
     for (uint32_t i = threadIdx.x; i < pow2; i += blockDim.x) {
         if (i < n) {
             const uint32_t l = i / k_in, j = i % k_in;
-            const size_t src = ((size_t)l * gridDim.x + qi) * k_in + j;  // [nlists][nq][k_in]
-            const uint64_t id = ids[src];
+            const size_t q_off = (size_t)qi * k_in + j;
+            const uint64_t id = ids[l * ids_stride + q_off];
             sid[i] = id;
-            sd[i] = id == WVG_KEY_NONE ? 0xFFFFFFFFu : wvg_ord_f32(dists[src]);
+            sd[i] = id == WVG_KEY_NONE ? 0xFFFFFFFFu : wvg_ord_f32(dists[l * d_stride + q_off]);
         } else {
             sid[i] = WVG_KEY_NONE;
             sd[i] = 0xFFFFFFFFu;
@@ -569,16 +603,16 @@ __global__ __launch_bounds__(1024) void merge_pairs_kernel(const float *dists, c
     if (threadIdx.x == 0 && out_counts) out_counts[qi] = live_count;
 }
 
-hipError_t launch_merge_pairs(const float *dists, const uint64_t *ids, uint32_t nq, uint32_t nlists,
-                              uint32_t k_in, uint32_t k, uint64_t *out_ids, float *out_dists,
-                              uint32_t *out_counts, hipStream_t s)
+hipError_t launch_merge_pairs(const float *dists, const uint64_t *ids, uint64_t ids_stride, uint64_t d_stride,
+                              uint32_t nq, uint32_t nlists, uint32_t k_in, uint32_t k, uint64_t *out_ids,
+                              float *out_dists, uint32_t *out_counts, hipStream_t s)
 {
     uint32_t n = nlists * k_in, pow2 = 1;
     while (pow2 < n) pow2 <<= 1;
     if (pow2 > (uint32_t)MERGE_PAIRS_MAX) return hipErrorInvalidValue;
     const size_t lds = (size_t)pow2 * 12;
-    hipLaunchKernelGGL(merge_pairs_kernel, dim3(nq), dim3(1024), lds, s, dists, ids, nlists, k_in, k, pow2,
-                       out_ids, out_dists, out_counts);
+    hipLaunchKernelGGL(merge_pairs_kernel, dim3(nq), dim3(1024), lds, s, dists, ids, ids_stride, d_stride, nlists,
+                       k_in, k, pow2, out_ids, out_dists, out_counts);
     return hipGetLastError();
 }
 
@@ -706,6 +740,29 @@ hipError_t launch_f32_gather(const float *tiled, const uint64_t *slots, uint64_t
     if (total == 0) return hipSuccess;
     hipLaunchKernelGGL(f32_gather_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
                        reinterpret_cast<const float4 *>(tiled), slots, n, dim, nchunks, rows);
+    return hipGetLastError();
+}
+
+// Stored rows by slot, as raw 16-byte chunks: out[i] = the nchunks chunks of
+// slots[i] (any corpus kind; the host trims / un-rotates).
+__global__ void gather_chunks_kernel(const uint4 *tiled, const uint64_t *slots, uint64_t n, uint32_t nchunks,
+                                     uint4 *out)
+{
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n * nchunks) return;
+    const uint64_t i = g / nchunks;
+    const uint32_t c = (uint32_t)(g % nchunks);
+    const uint64_t slot = slots[i];
+    out[g] = tiled[((slot >> 6) * nchunks + c) * 64 + (slot & 63)];
+}
+
+hipError_t launch_gather_chunks(const void *tiled, const uint64_t *slots, uint64_t n, uint32_t nchunks, void *out,
+                                hipStream_t s)
+{
+    const uint64_t total = n * nchunks;
+    if (total == 0) return hipSuccess;
+    hipLaunchKernelGGL(gather_chunks_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                       reinterpret_cast<const uint4 *>(tiled), slots, n, nchunks, reinterpret_cast<uint4 *>(out));
     return hipGetLastError();
 }
 

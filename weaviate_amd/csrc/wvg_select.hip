@@ -36,7 +36,7 @@ __device__ __forceinline__ uint64_t sel_tile_mask(const ScanArgs &a, uint64_t t)
 {
     uint64_t m = a.valid[t];
     if (a.allow) {
-        const uint64_t w = (a.id_base >> 6) + t;
+        const uint64_t w = t - a.allow_t0;  // allow[0] is tile allow_t0's word
         m &= w < a.allow_words ? a.allow[w] : 0ull;
     }
     return m;

@@ -152,6 +152,21 @@ class Corpus:
         check(self.lib.wvg_corpus_get(self.handle, id_, out.ctypes.data_as(c_void_p)))
         return out
 
+    def get_batch(self, ids, pq_m: int = 0):
+        """wvg_corpus_get_batch: (rows [n][...], ok [n]) for many docIDs in one call."""
+        ids = np.ascontiguousarray(ids, dtype=np.uint64).reshape(-1)
+        n = len(ids)
+        if self.kind == _lib.KIND_F32:
+            out = np.empty((n, self.dim), dtype=np.float32)
+        elif self.kind == _lib.KIND_BQ:
+            out = np.empty((n, (self.dim + 63) // 64), dtype=np.uint64)
+        else:
+            out = np.empty((n, pq_m), dtype=np.uint8)
+        ok = np.empty(n, dtype=np.uint8)
+        check(self.lib.wvg_corpus_get_batch(self.handle, u64ptr(ids), n, out.ctypes.data_as(c_void_p),
+                                            ok.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
+        return out, ok.astype(bool)
+
     def fill_synthetic(self, seed: int, n: int, distribution: int = 0) -> None:
         check(self.lib.wvg_corpus_fill_synthetic(self.handle, seed, n, distribution))
 

@@ -1,22 +1,27 @@
 """One-process-per-GPU sharding of a flat index.
 
 Rows are partitioned by contiguous docID range, one slab per GPU; every rank
-scans its slab with the fused K1 scan + top-k, the per-rank (dist, id) lists
-are exchanged with ONE all-gather per query batch (RCCL over xGMI when the
-process group is "nccl"), and every rank merges them on device.  This is the
-device restatement of Index.objectVectorSearch's shard fan-out and merge
-(adapters/repos/db/index.go:1567-1648: per-shard top-limit, concatenate,
-sort by distance, truncate).
+scans its slab with the fused K1 scan + top-k and writes its (id, dist) lists
+straight into ONE packed block (ids [nq][k] uint64, then dists [nq][k]
+float32; ``wvg_topk_packed_bytes``).  A single all-gather per query batch
+(RCCL over xGMI when the process group is "nccl") moves every rank's block,
+and every rank merges the [world] blocks on device (``wvg_topk_merge_packed``).
+This is the device restatement of Index.objectVectorSearch's shard fan-out
+and merge (adapters/repos/db/index.go:1567-1648: per-shard top-limit,
+concatenate, sort by distance, truncate).
 """
 from __future__ import annotations
 
 from dataclasses import dataclass
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
 from . import _lib
 from ._lib import check
+
+KEY_NONE = np.iinfo(np.uint64).max
 
 
 def shard_range(n_total: int, world: int, rank: int, align: int = 64):
@@ -24,25 +29,52 @@ def shard_range(n_total: int, world: int, rank: int, align: int = 64):
     multiple of `align` (the 64-row tile) so bitmaps stay word-aligned."""
     per = (n_total + world - 1) // world
     per = (per + align - 1) // align * align
-    lo = min(n_total, rank * per)
+    lo = rank * per  # aligned even for a rank past the end (count 0)
     hi = min(n_total, lo + per)
-    return lo, hi - lo, per
+    return lo, max(0, hi - lo), per
+
+
+def packed_bytes(nq: int, k: int) -> int:
+    """Size of one rank's packed result block (wvg_topk_packed_bytes)."""
+    return (nq * k * 12 + 15) // 16 * 16
+
+
+def pack_block(ids: np.ndarray, dists: np.ndarray) -> np.ndarray:
+    """Host packing of [nq][k] ids / dists into the block layout (tests, tools)."""
+    nq, k = ids.shape
+    blk = np.zeros(packed_bytes(nq, k), np.uint8)
+    blk[:nq * k * 8] = np.ascontiguousarray(ids, np.uint64).view(np.uint8).reshape(-1)
+    blk[nq * k * 8:nq * k * 12] = np.ascontiguousarray(dists, np.float32).view(np.uint8).reshape(-1)
+    return blk
+
+
+def unpack_blocks(buf: np.ndarray, nlists: int, nq: int, k: int):
+    """[nlists] consecutive packed blocks -> (ids [nlists][nq][k], dists [nlists][nq][k])."""
+    blk = packed_bytes(nq, k)
+    b = np.ascontiguousarray(buf, np.uint8).reshape(nlists, blk)
+    ids = np.ascontiguousarray(b[:, :nq * k * 8]).view(np.uint64).reshape(nlists, nq, k)
+    dists = np.ascontiguousarray(b[:, nq * k * 8:nq * k * 12]).view(np.float32).reshape(nlists, nq, k)
+    return ids, dists
+
+
+def all_gather_packed(send: torch.Tensor, recv: torch.Tensor, group=None) -> None:
+    """One all-gather of the packed blocks: recv[r * len(send):] = rank r's send.
+    With a gloo group and device tensors the exchange is staged through host
+    memory (test rehearsals on one GPU); with nccl it is RCCL over xGMI."""
+    if send.is_cuda and dist.get_backend(group) == "gloo":
+        hr = torch.empty(recv.shape, dtype=recv.dtype)
+        dist.all_gather_into_tensor(hr, send.cpu(), group=group)
+        recv.copy_(hr)
+    else:
+        dist.all_gather_into_tensor(recv, send, group=group)
 
 
 @dataclass
-class GatherBuffers:
-    dists: torch.Tensor
-    ids: torch.Tensor
-
-
-def all_gather_topk(dists: torch.Tensor, ids: torch.Tensor, group=None) -> GatherBuffers:
-    """[nq][k] local lists -> [world][nq][k] (one collective per tensor)."""
-    world = dist.get_world_size(group)
-    gd = torch.empty((world,) + tuple(dists.shape), dtype=dists.dtype, device=dists.device)
-    gi = torch.empty((world,) + tuple(ids.shape), dtype=ids.dtype, device=ids.device)
-    dist.all_gather_into_tensor(gd.view(-1), dists.contiguous().view(-1), group=group)
-    dist.all_gather_into_tensor(gi.view(-1), ids.contiguous().view(-1), group=group)
-    return GatherBuffers(gd, gi)
+class _Buffers:
+    ws: torch.Tensor      # search workspace (zero-filled once)
+    send: torch.Tensor    # this rank's packed block
+    recv: torch.Tensor    # [world] packed blocks
+    counts: torch.Tensor  # local counts
 
 
 class ShardedFlatIndex:
@@ -51,30 +83,56 @@ class ShardedFlatIndex:
     def __init__(self, ctx, corpus, group=None):
         self.ctx, self.corpus, self.group = ctx, corpus, group
         self.lib = ctx.lib
+        self._bufs: dict = {}
 
-    def search_device(self, q: torch.Tensor, k: int, stream=None):
+    def _buffers(self, nq: int, k: int, dev, world: int) -> _Buffers:
+        key = (nq, k, str(dev), world)
+        b = self._bufs.get(key)
+        if b is None:
+            ws_bytes = max(256, self.lib.wvg_search_workspace_size(self.corpus.handle, nq, k))
+            blk = self.lib.wvg_topk_packed_bytes(nq, k)
+            b = _Buffers(ws=torch.zeros(ws_bytes, dtype=torch.uint8, device=dev),
+                         send=torch.empty(blk, dtype=torch.uint8, device=dev),
+                         recv=torch.empty(world * blk, dtype=torch.uint8, device=dev),
+                         counts=torch.empty(nq, dtype=torch.int32, device=dev))
+            self._bufs[key] = b
+        return b
+
+    def search_device(self, q: torch.Tensor, k: int, stream=None, pipelined: bool = False):
         """q: [nq][dim] float32 on this rank's GPU (normalized for cosine).
-        Returns (ids int64 [nq][k] global docIDs, dists [nq][k], counts [nq])."""
+        Returns (ids int64 [nq][k] global docIDs, dists [nq][k], counts [nq]).
+        pipelined: nq independent single-query scans in one launch
+        (wvg_search_device_pipelined) instead of one batched search."""
         nq = q.shape[0]
         dev = q.device
         stream = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
-        ids = torch.empty((nq, k), dtype=torch.int64, device=dev)
-        dists = torch.empty((nq, k), dtype=torch.float32, device=dev)
-        counts = torch.empty(nq, dtype=torch.int32, device=dev)
-        ws_bytes = self.lib.wvg_search_workspace_size(self.corpus.handle, nq, k)
-        ws = torch.zeros(max(1, ws_bytes), dtype=torch.uint8, device=dev)
-        check(self.lib.wvg_search_device(self.corpus.handle, q.data_ptr(), nq, k, ids.data_ptr(), dists.data_ptr(),
-                                         counts.data_ptr(), ws.data_ptr(), ws_bytes, stream))
-        if not dist.is_initialized() or dist.get_world_size(self.group) == 1:
+        world = dist.get_world_size(self.group) if dist.is_initialized() else 1
+        b = self._buffers(nq, k, dev, world)
+        fn = self.lib.wvg_search_device_pipelined if pipelined else self.lib.wvg_search_device
+        if world == 1:
+            ids = torch.empty((nq, k), dtype=torch.int64, device=dev)
+            dists = torch.empty((nq, k), dtype=torch.float32, device=dev)
+            counts = torch.empty(nq, dtype=torch.int32, device=dev)
+            check(fn(self.corpus.handle, q.data_ptr(), nq, k, ids.data_ptr(), dists.data_ptr(), counts.data_ptr(),
+                     b.ws.data_ptr(), b.ws.numel(), stream))
             return ids, dists, counts
-        g = all_gather_topk(dists, ids, self.group)
-        world = g.dists.shape[0]
+        # local lists straight into the packed block: ids at byte 0, dists at nq*k*8
+        check(fn(self.corpus.handle, q.data_ptr(), nq, k, b.send.data_ptr(), b.send.data_ptr() + nq * k * 8,
+                 b.counts.data_ptr(), b.ws.data_ptr(), b.ws.numel(), stream))
+        all_gather_packed(b.send, b.recv, self.group)
         m_ids = torch.empty((nq, k), dtype=torch.int64, device=dev)
         m_d = torch.empty((nq, k), dtype=torch.float32, device=dev)
         m_c = torch.empty(nq, dtype=torch.int32, device=dev)
-        check(self.lib.wvg_topk_merge_device(self.ctx.handle, g.dists.data_ptr(), g.ids.data_ptr(), nq, world, k, k,
-                                             m_ids.data_ptr(), m_d.data_ptr(), m_c.data_ptr(), stream))
+        check(self.lib.wvg_topk_merge_packed(self.ctx.handle, b.recv.data_ptr(), nq, world, k, k, m_ids.data_ptr(),
+                                             m_d.data_ptr(), m_c.data_ptr(), stream))
         return m_ids, m_d, m_c
 
+    def check(self, stream=None) -> None:
+        """wvg_search_device_check over every workspace this index used."""
+        for (nq, k, dev, world), b in self._bufs.items():
+            st = stream if stream is not None else torch.cuda.current_stream(b.ws.device).cuda_stream
+            check(self.lib.wvg_search_device_check(self.ctx.handle, b.ws.data_ptr(), st))
 
-__all__ = ["shard_range", "all_gather_topk", "ShardedFlatIndex", "_lib"]
+
+__all__ = ["shard_range", "packed_bytes", "pack_block", "unpack_blocks", "all_gather_packed", "ShardedFlatIndex",
+           "_lib"]
