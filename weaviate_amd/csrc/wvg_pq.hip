@@ -411,7 +411,14 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq_kernel(ScanArgs a,
 // LDS: the 128 KiB image, one workgroup per CU.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-template <int E, int R, bool IL, int NB>
+// MODE 0: tiles with no live / allowed row are skipped (their codes are never
+// loaded; the scan waits on each refill's tile-mask load).  MODE 1 (dense):
+// every tile of the range is loaded and its validity word rides in the ring
+// as a vector load next to the codes, so no wait sits between refills; used
+// without an allow list on mostly-live corpora.  MODE 2: MODE 1's loads with
+// no lookups (A/B diagnostic: the access pattern's memory ceiling; results
+// are meaningless).
+template <int E, int R, bool IL, int NB, int MODE = 0>
 __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_rot_kernel(ScanArgs a, uint64_t *partials)
 {
     extern __shared__ __attribute__((aligned(16))) f32x2 img[];  // [256][64]
@@ -469,6 +476,10 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_rot_kernel(ScanA
         const char *imgb = reinterpret_cast<const char *>(img);
 
         auto next_live = [&](uint64_t t, uint64_t &msk) {
+            if constexpr (MODE != 0) {
+                msk = 0;  // dense: the tile's mask comes with its codes (vm)
+                return t < t1 ? t : t1;
+            }
             for (; t < t1; t += TS) {
                 msk = pq_tile_mask(a, t);
                 if (msk) break;
@@ -477,11 +488,20 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_rot_kernel(ScanA
         };
         // Loads are unconditional (a finished stream re-reads tile t0, whose
         // values are never used) so the waits on the ring stay static.
-        auto load = [&](uint64_t t, uint32_t (&w)[8]) {
-            const uint4 *rp = data + (size_t)(t < t1 ? t : t0) * 2 * 64 + lane;
+        auto load = [&](uint64_t t, uint32_t (&w)[8], uint64_t &vm) {
+            const uint64_t tt = t < t1 ? t : t0;
+            const uint4 *rp = data + (size_t)tt * 2 * 64 + lane;
             const uint4 lo = ld_codes(rp), hi = ld_codes(rp + 64);
             w[0] = lo.x; w[1] = lo.y; w[2] = lo.z; w[3] = lo.w;
             w[4] = hi.x; w[5] = hi.y; w[6] = hi.z; w[7] = hi.w;
+            if constexpr (MODE != 0) {  // broadcast vector loads (every lane the same word)
+                uint64_t m = t < t1 ? a.valid[tt] : 0ull;
+                if (a.allow) {
+                    const uint64_t w = tt - a.allow_t0;
+                    m &= w < a.allow_words ? a.allow[w] : 0ull;
+                }
+                vm = m;
+            }
         };
 
         // Ring of R live tiles' codes (R - 2 tiles of HBM latency cover beyond
@@ -489,9 +509,10 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_rot_kernel(ScanA
         // nxt = slot i mod R = live tile i; afterwards slot (i-1) mod R is
         // refilled with live tile i+R-1.  t1 marks "no tile".
         uint32_t ring[R][8];
-        uint64_t rt[R], rm[R];
+        uint64_t rt[R], rm[R], rv[R];  // tile, scalar mask (MODE 0), vector-loaded mask (dense)
         rt[R - 1] = t1;
         rm[R - 1] = 0;
+        rv[R - 1] = 0;
         {
             uint64_t t = t0;
 #pragma unroll
@@ -500,7 +521,7 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_rot_kernel(ScanA
                 t = next_live(t, m);
                 rt[s] = t;
                 rm[s] = m;
-                load(t, ring[s]);
+                load(t, ring[s], rv[s]);
                 if (t < t1) t += TS;
             }
 #pragma unroll
@@ -520,6 +541,12 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_rot_kernel(ScanA
 #pragma unroll
                     for (int w = 0; w < 8; w++)
                         asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(win[w]) : "v"(nmask[w]), "v"(ring[s][w]), "v"(ring[sc][w]));
+                    if constexpr (MODE == 2) {
+                        uint32_t x = 0;
+#pragma unroll
+                        for (int w = 0; w < 8; w++) x ^= win[w];
+                        acc = acc + f32x2{(float)(x & 0xFFu), 0.0f};
+                    } else {
                     // batches of NB reads, each all in flight before its adds
 #pragma unroll
                     for (int h = 0; h < 32 / NB; h++) {
@@ -535,14 +562,18 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_rot_kernel(ScanA
 #pragma unroll
                         for (int jj = 0; jj < NB; jj++) acc = acc + v[jj];
                     }
-                    if (rt[sc] < t1) tk.offer_dist(wrap_metric(a.metric, acc.x), (uint32_t)(rt[sc] * 64 + lane), rm[sc]);
+                    }
+                    if (rt[sc] < t1) {
+                        const uint64_t live = MODE != 0 ? __ballot((rv[sc] >> lane) & 1ull) : rm[sc];
+                        tk.offer_dist(wrap_metric(a.metric, acc.x), (uint32_t)(rt[sc] * 64 + lane), live);
+                    }
                     acc = f32x2{acc.y, 0.0f};
                     // refill the cur slot with the live tile R-1 passes ahead
                     uint64_t m = 0;
                     const uint64_t t = next_live(t_fill, m);
                     rt[sc] = t;
                     rm[sc] = m;
-                    load(t, ring[sc]);
+                    load(t, ring[sc], rv[sc]);
                     t_fill = t < t1 ? t + TS : t1;
                 }
             }
@@ -560,6 +591,10 @@ static hipError_t launch_pq_e(const ScanArgs &a, uint64_t *partials, int groups,
         // 128 KiB LUT image; variant 0 = ring 6, per-wave ranges, LDS reads in batches of 16
         // (A/B: 2 = ring 4, 3 = ring 4 interleaved, 4 = batches of 32, 5 = batches of 8)
         switch (tuning().pq_variant) {
+        case 6: launch_timed((scan_pq32_rot_kernel<E, 6, false, 16, 1>), grid, block, 4 * lds, s, a, partials); break;
+        case 7: launch_timed((scan_pq32_rot_kernel<E, 6, false, 16, 2>), grid, block, 4 * lds, s, a, partials); break;
+        case 8: launch_timed((scan_pq32_rot_kernel<E, 4, false, 16, 1>), grid, block, 4 * lds, s, a, partials); break;
+        case 9: launch_timed((scan_pq32_rot_kernel<E, 8, false, 16, 1>), grid, block, 4 * lds, s, a, partials); break;
         case 2: launch_timed((scan_pq32_rot_kernel<E, 4, false, 16>), grid, block, 4 * lds, s, a, partials); break;
         case 3: launch_timed((scan_pq32_rot_kernel<E, 4, true, 16>), grid, block, 4 * lds, s, a, partials); break;
         case 4: launch_timed((scan_pq32_rot_kernel<E, 6, false, 32>), grid, block, 4 * lds, s, a, partials); break;
