@@ -224,3 +224,60 @@ def test_merge_packed_equals_merge_device(ctx, orc):
         live = ids[:, qi, :] != NONE
         wi, wd = orc.lex_topk(d[:, qi, :][live], ids[:, qi, :][live], k)
         assert np.array_equal(outs[1][0][qi], wi) and np.array_equal(bits(outs[1][1][qi]), bits(wd))
+
+
+def test_serpentine_scan_order_does_not_change_results(ctx, orc):
+    """Consecutive scans alternate direction (tuning key 9): the lexicographic
+    top-k does not depend on the order rows are visited, so every call gives
+    the same bits with the alternation on or off -- K1 (host API, query-stream
+    kernel), K8c (PQ m = 32) and the BQ scan."""
+    import torch
+
+    lib = _lib.load()
+    n, d, k = 70_000 + 13, 128, 10
+    qs = orc.synth_rows(77, 0, 5, d, 0)
+    f = Corpus(ctx, KIND_F32, METRIC_L2, d, n)
+    f.fill_synthetic(76, n, 0)
+    f.delete(np.array([3, 64, 69_999], np.uint64))
+    pq = Corpus(ctx, KIND_PQ, METRIC_DOT, d, n)
+    pq.set_codebook(orc.synth_rows(78, 0, 32 * 256, 4, 0).reshape(32, 256, 4))
+    _lib.check(lib.wvg_pq_encode_corpus(pq.handle, f.handle))
+    bq = Corpus(ctx, KIND_BQ, METRIC_COSINE, d, n)
+    bq.fill_synthetic(76, n, 0)
+    dev = torch.device("cuda:0")
+    ws = torch.zeros(lib.wvg_search_workspace_size(f.handle, 5, k), dtype=torch.uint8, device=dev)
+    tq = torch.from_numpy(qs).to(dev)
+
+    def device_stream():
+        oi = torch.empty((5, k), dtype=torch.int64, device=dev)
+        od = torch.empty((5, k), dtype=torch.float32, device=dev)
+        oc = torch.empty(5, dtype=torch.int32, device=dev)
+        _lib.check(lib.wvg_search_device_pipelined(f.handle, tq.data_ptr(), 5, k, oi.data_ptr(), od.data_ptr(),
+                                                   oc.data_ptr(), ws.data_ptr(), ws.numel(),
+                                                   torch.cuda.current_stream().cuda_stream))
+        torch.cuda.synchronize()
+        return oi.cpu().numpy(), od.cpu().numpy()
+
+    def run_all():
+        out = []
+        for rep in range(3):  # consecutive calls: directions alternate between them
+            out.append(f.search(qs, k))
+            out.append(pq.search(qs[rep], 20))
+            out.append(bq.search(qs[rep], 30))
+            out.append(device_stream())
+        return out
+
+    old = tuning(lib, 9, 0)
+    try:
+        want = run_all()
+        tuning(lib, 9, 1)
+        got = run_all()
+        got2 = run_all()
+    finally:
+        tuning(lib, 9, old)
+    for a_, b_, c_ in zip(want, got, got2):
+        for x, y, z in zip(a_, b_, c_):
+            assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8))
+            assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(z).view(np.uint8))
+    for c in (f, pq, bq):
+        c.destroy()

@@ -77,7 +77,9 @@ def test_pq_config_errors():
                       ((0, 256, 128), "segments cannot be 0 nor negative"),
                       ((-2, 256, 128), "segments cannot be 0 nor negative"),
                       ((3, 256, 128), "segments should be an integer divisor of dimensions"),
-                      ((4, 512, 128), "centroids should not be higher than 256. Attempting to use 512")]:
+                      ((4, 512, 128), "centroids should not be higher than 256. Attempting to use 512"),
+                      ((4, 0, 128), "centroids must be > 0"),
+                      ((4, -3, 128), "centroids must be > 0")]:
         with pytest.raises(_lib.WvgError, match=msg):
             validate_pq_config(*args)
     assert validate_pq_config(4, 256, 128) == (1, 1)  # defaults: kmeans, log-normal

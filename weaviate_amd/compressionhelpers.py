@@ -177,6 +177,10 @@ def validate_pq_config(segments: int, centroids: int, dimensions: int, encoder: 
     dist = {"log-normal": LOG_NORMAL_DISTRIBUTION, "normal": NORMAL_DISTRIBUTION}.get(distribution)
     if dist is None:
         raise _lib.WvgError(_lib.WVG_ERR_INVALID, "invalid encoder distribution")
+    # the reference accepts centroids <= 0 here and fails later; the device
+    # path refuses it up front with the C ABI's message (pq_validate)
+    if centroids <= 0:
+        raise _lib.WvgError(_lib.WVG_ERR_INVALID, "centroids must be > 0")
     return enc, dist
 
 

@@ -299,6 +299,7 @@ int wvg_open(int device, wvg_ctx **out)
     c->device = device;
     c->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     if (const char *e = getenv("WVG_MFMA_MIN_QUERIES")) c->mfma_min_nq = (uint32_t)strtoul(e, nullptr, 10);
+    if (const char *e = getenv("WVG_SERPENTINE")) tuning().serpentine = (int)strtol(e, nullptr, 10);  // A/B runs
     *out = c;
     return WVG_OK;
 }
@@ -878,6 +879,23 @@ struct ProfArm {
     }
 };
 
+// Direction of the next scan of `c`: consecutive scans alternate (serpentine),
+// so a scan starts on the rows the previous one read last -- the part of the
+// corpus still in the 256 MiB Infinity Cache.  `nq` scans are reserved (the
+// query-stream kernel alternates per query from the returned start).
+static uint32_t next_direction(wvg_corpus *c, uint32_t nq)
+{
+    if (!tuning().serpentine) return 0u;
+    return (uint32_t)(c->scan_serial.fetch_add(nq, std::memory_order_relaxed) & 1u);
+}
+
+// PQ m = 32 scans without an allow list on a corpus with >= 3/4 of its slots
+// live run K8c, which loads every tile instead of skipping dead ones.
+static int pq_dense(const wvg_corpus *c, const uint64_t *d_allow)
+{
+    return !d_allow && c->count * 4 >= c->high_water * 3;
+}
+
 struct SearchPlan {
     uint64_t tb = 0, te = 0;
     int groups = 1;      // scan: workgroups per query; gemm: row ranges
@@ -936,6 +954,8 @@ static int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t 
     a.k = k;
     a.pq_m = c->pq_m;
     a.pq_ks = c->pq_ks;
+    a.dense = pq_dense(c, d_allow);
+    if (!p.gemm) a.reverse = next_direction(c, 1);
     ProfArm arm(c->ctx);
     if (arm.rc) return arm.rc;
     if (p.gemm)
@@ -1082,6 +1102,7 @@ static ScanArgs scan_args_for(const wvg_corpus *c, const void *d_q, uint32_t qpi
     a.k = k;
     a.pq_m = c->pq_m;
     a.pq_ks = c->pq_ks;
+    a.dense = pq_dense(c, d_allow);
     return a;
 }
 
@@ -1451,6 +1472,7 @@ int wvg_search_bq_rescore(wvg_corpus *bq, wvg_corpus *f32, const float *queries,
     a.qpitch = qpb;
     a.nq = nq;
     a.k = R;
+    a.reverse = next_direction(bq, 1);
     uint64_t *part = (uint64_t *)(b + o_part);
     WVG_HIP(launch_scan_bq(a, part, p.groups, s));
     // Hamming top-R; ids are id_base + slot, so id_base = 0 keeps the slots
@@ -1556,6 +1578,7 @@ int wvg_search_device_pipelined(wvg_corpus *c, const float *d_queries, uint32_t 
         a.qpitch = c->dim;
         a.nq = nq;
         a.k = k;
+        a.reverse = next_direction(c, nq);
         WVG_HIP(hipMemsetAsync(j.arrivals, 0, align_up((size_t)nq * 4, 16), s));
         ProfArm arm(c->ctx);
         if (arm.rc) return arm.rc;
@@ -1578,8 +1601,10 @@ int wvg_search_device_pipelined(wvg_corpus *c, const float *d_queries, uint32_t 
     a.qpitch = c->dim;
     a.nq = 1;
     a.k = k;
+    const uint32_t dir0 = next_direction(c, nq);
     for (uint32_t i = 0; i < nq; i++) {
         a.queries = d_queries + (size_t)i * c->dim;
+        a.reverse = (dir0 + i) & 1u;
         a.side = MergeJob{};
         if (i > 0) {
             a.side = MergeJob{buf[(i - 1) & 1], (uint32_t)p.groups, k, k, c->id_base, d_ids + (size_t)(i - 1) * k,
@@ -1752,7 +1777,8 @@ int wvg_synthetic_rows(wvg_ctx *ctx, uint64_t seed, const uint64_t *ids, uint64_
 }
 
 // Internal A/B knob (not part of include/wvgpu.h): 0 = K1 scan variant,
-// 1 = K1 resident workgroups per CU, ... 7 = K8 ADC variant, 8 = query-stream merge wait (us).  Returns the previous value.
+// 1 = K1 resident workgroups per CU, ... 7 = K8 ADC variant, 8 = query-stream merge wait (us),
+// 9 = serpentine scan order.  Returns the previous value.
 int wvgx_set_tuning(int key, int value)
 {
     Tuning &t = tuning();
@@ -1784,6 +1810,9 @@ int wvgx_set_tuning(int key, int value)
     } else if (key == 8) {
         old = t.merge_wait_us;
         t.merge_wait_us = value;
+    } else if (key == 9) {
+        old = t.serpentine;
+        t.serpentine = value;
     }
     return old;
 }

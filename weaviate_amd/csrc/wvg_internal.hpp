@@ -73,6 +73,7 @@ struct wvg_corpus {
     float *d_centers = nullptr;    // [m][ks][ds]
     uint32_t pq_m = 0, pq_ks = 0, pq_ds = 0;
     std::shared_mutex rw;          // shared: search; exclusive: upsert/delete/grow
+    std::atomic<uint64_t> scan_serial{0};  // query scans issued so far (parity = next scan direction)
 };
 
 namespace wvg {
@@ -181,6 +182,11 @@ struct ScanArgs {
     uint32_t nq, k;
     uint32_t pq_m, pq_ks;
     MergeJob side;             // F32 scan only; gridDim.x includes its workgroup
+    uint32_t reverse;          // scan direction: 1 = every wave walks its tile range downwards.  The
+                               // query-stream kernel alternates per query from this start, and the host
+                               // alternates between calls (wvg_corpus::scan_serial): consecutive scans then
+                               // begin where the previous one ended, on rows still in the Infinity Cache
+    int dense;                 // PQ m = 32: no allow list and mostly-live rows -> K8c (no tile skipping)
 };
 // Phase 1 writes dense partials [nq][groups][K] (keys, KEY_NONE = empty).
 int scan_groups_for(const ScanArgs &a, int num_cus);
@@ -229,6 +235,7 @@ struct Tuning {
     int pq_variant = 0;      // K8: 0 = rotated-segment ADC (K8b) where it applies (m = 32, ks = 256),
                              // 1 = K8 gather in segment order everywhere
     int merge_wait_us = 0;   // query-stream merge workgroup's wait per query in us; 0 = 4 s (test knob)
+    int serpentine = 1;      // alternate the scan direction between consecutive scans (0 = always upwards; A/B)
 };
 Tuning &tuning();
 // Profiling: events armed by the host runtime (wvg_profile_start) are bound to

@@ -582,12 +582,171 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_rot_kernel(ScanA
     group_combine_store<E, PQ_SCAN_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
 }
 
+// K8c: K8b's arithmetic (rotated segments, (A, B) routing in the 128 KiB
+// LUT image, rotated row storage) in its dense form, trimmed for issue: the
+// counters of K8b show every SIMD issuing ~90 % of the time (VALU ~62 %, LDS
+// and SALU the rest) at 73 % of HBM, i.e. the scan is instruction-issue bound,
+// so K8c cuts the per-tile overhead around the 32 lookups:
+//   - codes come through a per-wave buffer resource: the tile's byte offset
+//     is a scalar soffset, the lane's a constant voffset, so a load costs no
+//     address VALU, and loads past the wave's range (the ring's tail) return
+//     zeros instead of needing a clamp;
+//   - tile validity arrives 64 tiles per vector load (lane i = word of tile
+//     i of the block, the allow window ANDed in) and two v_readlane per tile
+//     turn it into the scalar live mask;
+//   - top-k rejection compares the float distance with the K-th distance
+//     (offer_dist_fast) instead of building ordered keys first;
+//   - the metric's Wrap is a template parameter.
+// Every tile of the wave's range is loaded (no skipping of dead tiles): the
+// host runs K8c without an allow list on mostly-live corpora and K8b
+// otherwise.  The A/B sums are K8b's, so results are bit-identical.
+template <int E, int R, int NB, int METRIC>
+__global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_dense_kernel(ScanArgs a, uint64_t *partials)
+{
+    static_assert(64 % R == 0, "the ring length divides the 64-tile mask block");
+    extern __shared__ __attribute__((aligned(16))) f32x2 img[];  // [256][64]
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t qi = blockIdx.y;
+    const float *glut = reinterpret_cast<const float *>(a.queries) + (size_t)qi * a.qpitch;
+    constexpr int FILL = 32 * 256 / (PQ_SCAN_WAVES * 64);
+    float fv[FILL];
+#pragma unroll
+    for (int it = 0; it < FILL; it++) {
+        const uint32_t i = (uint32_t)it * (PQ_SCAN_WAVES * 64) + threadIdx.x;
+        fv[it] = glut[(i & 31u) * 256u + (i >> 5)];
+    }
+#pragma unroll
+    for (int it = 0; it < FILL; it++) {
+        const uint32_t i = (uint32_t)it * (PQ_SCAN_WAVES * 64) + threadIdx.x;
+        const uint32_t s = i & 31u, c = i >> 5;
+        img[c * 64u + s] = f32x2{fv[it], 0.0f};
+        img[c * 64u + 32u + s] = f32x2{0.0f, fv[it]};
+    }
+    __syncthreads();
+    const uint64_t ntiles = a.tile_end - a.tile_begin;
+    const uint64_t total = (uint64_t)gridDim.x * PQ_SCAN_WAVES;
+    const uint64_t gw = (uint64_t)blockIdx.x * PQ_SCAN_WAVES + wave;
+    const uint64_t t0 = a.tile_begin + ntiles * gw / total, t1 = a.tile_begin + ntiles * (gw + 1) / total;
+    WaveTopK<E> tk;
+    tk.init((int)a.k);
+    tk.init_fast();
+    if (t0 < t1) {
+        const uint32_t n = (uint32_t)(t1 - t0);  // tiles of this wave (2 KiB each)
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<char *>(reinterpret_cast<const char *>(a.data)) + t0 * 2048u, (short)0, (int)(n * 2048u),
+            0x00020000);
+        const uint32_t voff = (uint32_t)lane * 16u;
+        const uint32_t x = (uint32_t)lane & 31u, x8 = x * 8u;
+        uint32_t nmask[8];  // bytes of step j taken from the next row (see K8b)
+#pragma unroll
+        for (int w = 0; w < 8; w++) {
+            uint32_t mk = 0u;
+#pragma unroll
+            for (int bb = 0; bb < 4; bb++) mk |= (4u * w + bb + x >= 32u) ? (0xFFu << (8 * bb)) : 0u;
+            nmask[w] = mk;
+        }
+        const char *imgb = reinterpret_cast<const char *>(img);
+        // pass order: tiles t0 + i, or t1 - 1 - i when scanning downwards (rev)
+        const bool rev = a.reverse & 1u;
+        auto tile_of = [&](uint32_t i) -> uint32_t { return rev ? n - 1u - i : i; };
+        auto load = [&](uint32_t i, uint32_t (&w)[8]) {  // the i-th tile of the pass order (zeros past it)
+            const uint32_t so = i < n ? tile_of(i) * 2048u : n * 2048u;
+            const u32x4 lo = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, so, 2);
+            const u32x4 hi = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 1024u, so, 2);
+            w[0] = lo.x; w[1] = lo.y; w[2] = lo.z; w[3] = lo.w;
+            w[4] = hi.x; w[5] = hi.y; w[6] = hi.z; w[7] = hi.w;
+        };
+        auto load_masks = [&](uint32_t b) -> uint64_t {  // lane i: live mask of the (64 b + i)-th tile
+            const uint32_t ii = b * 64u + (uint32_t)lane;
+            const uint64_t t = t0 + (ii < n ? tile_of(ii) : 0u);
+            uint64_t m = 0ull;
+            if (ii < n) {
+                m = a.valid[t];
+                if (a.allow) {
+                    const uint64_t wi = t - a.allow_t0;
+                    m &= wi < a.allow_words ? a.allow[wi] : 0ull;
+                }
+            }
+            return m;
+        };
+        uint64_t mcur = load_masks(0), mnxt = load_masks(1);
+        uint32_t ring[R][8];
+#pragma unroll
+        for (int s = 0; s < R - 1; s++) load((uint32_t)s, ring[s]);
+#pragma unroll
+        for (int w = 0; w < 8; w++) ring[R - 1][w] = 0u;
+        f32x2 acc = {0.0f, 0.0f};
+        // pass i finishes tile i-1 (slot (i-1) mod R) and starts tile i (slot
+        // i mod R); n + 1 passes, in groups of R so the ring slots are static
+        for (uint32_t base = 0; base <= n; base += R) {
+#pragma unroll
+            for (int s = 0; s < R; s++) {
+                const int sc = (s + R - 1) % R;
+                const uint32_t i = base + (uint32_t)s;
+                uint32_t win[8];
+#pragma unroll
+                for (int w = 0; w < 8; w++)
+                    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(win[w]) : "v"(nmask[w]), "v"(ring[s][w]), "v"(ring[sc][w]));
+#pragma unroll
+                for (int h = 0; h < 32 / NB; h++) {
+                    f32x2 v[NB];
+#pragma unroll
+                    for (int jj = 0; jj < NB; jj++) {
+                        const int j = h * NB + jj;
+                        const uint32_t c8 = __builtin_amdgcn_perm(0u, win[j >> 2], 0x0C0C000Cu | ((uint32_t)(j & 3) << 8));
+                        const uint32_t off = (c8 << 1) + x8;
+                        v[jj] = *reinterpret_cast<const f32x2 *>(imgb + off + 8 * j);
+                    }
+#pragma unroll
+                    for (int jj = 0; jj < NB; jj++) acc = acc + v[jj];
+                }
+                if (i >= 1 && i <= n) {  // offer tile i-1
+                    const uint32_t tl = i - 1u;
+                    if (s == 1 && (tl & 63u) == 0u && tl != 0u) {  // (R | 64: block starts land on s == 1)
+                        mcur = mnxt;
+                        mnxt = load_masks((tl >> 6) + 1u);
+                    }
+                    const uint64_t live = readlane64(mcur, (int)(tl & 63u));
+                    const float dist = METRIC == WVG_M_L2 ? acc.x : (METRIC == WVG_M_DOT ? -acc.x : 1.0f - acc.x);
+                    tk.offer_dist_fast(dist, (uint32_t)((t0 + tile_of(tl)) * 64u) + (uint32_t)lane, live);
+                }
+                acc = f32x2{acc.y, 0.0f};
+                load(i + (uint32_t)R - 1u, ring[sc]);  // refill: tile i + R - 1
+            }
+        }
+    }
+    group_combine_store<E, PQ_SCAN_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
+}
+
+template <int E, int R, int NB>
+static void launch_pq_dense(const ScanArgs &a, uint64_t *partials, dim3 grid, dim3 block, size_t lds, hipStream_t s)
+{
+    if (a.metric == WVG_M_L2)
+        launch_timed((scan_pq32_dense_kernel<E, R, NB, WVG_M_L2>), grid, block, lds, s, a, partials);
+    else if (a.metric == WVG_M_DOT)
+        launch_timed((scan_pq32_dense_kernel<E, R, NB, WVG_M_DOT>), grid, block, lds, s, a, partials);
+    else
+        launch_timed((scan_pq32_dense_kernel<E, R, NB, WVG_M_COSINE>), grid, block, lds, s, a, partials);
+}
+
 template <int E>
 static hipError_t launch_pq_e(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
 {
     dim3 grid(groups, a.nq), block(PQ_SCAN_WAVES * 64);
     const size_t lds = (size_t)a.pq_m * a.pq_ks * 4;
-    if (a.pq_ks == 256 && a.pq_m == 32 && a.nchunks == 2 && tuning().pq_variant != 1) {
+    const int v = tuning().pq_variant;
+    const bool m32 = a.pq_ks == 256 && a.pq_m == 32 && a.nchunks == 2;
+    if (m32 && (v == 10 || v == 11 || v == 12 || (v == 0 && a.dense))) {
+        // K8c (dense, issue-trimmed): 0 (auto) / 12 = ring 8 / LDS batches of 16, 10 = ring 8 / 8, 11 = ring 4 / 16
+        if (v == 11)
+            launch_pq_dense<E, 4, 16>(a, partials, grid, block, 4 * lds, s);
+        else if (v == 10)
+            launch_pq_dense<E, 8, 8>(a, partials, grid, block, 4 * lds, s);
+        else
+            launch_pq_dense<E, 8, 16>(a, partials, grid, block, 4 * lds, s);
+        return hipGetLastError();
+    }
+    if (m32 && v != 1) {  // K8b: skips dead / disallowed tiles (0 = auto without K8c's conditions, 13 = forced)
         // 128 KiB LUT image; variant 0 = ring 6, per-wave ranges, LDS reads in batches of 16
         // (A/B: 2 = ring 4, 3 = ring 4 interleaved, 4 = batches of 32, 5 = batches of 8)
         switch (tuning().pq_variant) {

@@ -114,16 +114,20 @@ __device__ __forceinline__ uint64_t lane_key(uint64_t m, float dist, uint64_t t,
 
 // One wave's tiles [t0, t1) for one query: one tile's loads in flight per
 // wave; tiles with no live/allowed row are skipped without touching their rows.
+// rev: walk the range downwards (t1-1 .. t0); the result does not depend on
+// the order (lexicographic keys), only the cache state the next scan finds.
 template <int METRIC, int D, int E>
 __device__ __forceinline__ void scan_tiles(const ScanArgs &a, const float4 *q4, uint64_t t0, uint64_t t1,
-                                           WaveTopK<E> &tk)
+                                           WaveTopK<E> &tk, bool rev = false)
 {
     const int lane = threadIdx.x & 63;
     const float4 *data = reinterpret_cast<const float4 *>(a.data);
-    uint64_t m_next = t0 < t1 ? tile_mask(a, t0) : 0ull;
-    for (uint64_t t = t0; t < t1; ++t) {
+    const uint64_t n = t1 - t0;
+    uint64_t m_next = n ? tile_mask(a, rev ? t1 - 1 : t0) : 0ull;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t t = rev ? t1 - 1 - i : t0 + i;
         const uint64_t m = m_next;
-        if (t + 1 < t1) m_next = tile_mask(a, t + 1);  // scalar prefetch of the next mask
+        if (i + 1 < n) m_next = tile_mask(a, rev ? t - 1 : t + 1);  // scalar prefetch of the next mask
         if (m == 0ull) continue;  // wave-uniform: nothing live/allowed in this tile
         const float4 *rp = data + (size_t)t * a.nchunks * 64 + lane;
         float r;
@@ -151,7 +155,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_kernel(ScanArgs a, u
     wave_range(a, SCAN_WAVES, t0, t1);
     WaveTopK<E> tk;
     tk.init((int)a.k);
-    scan_tiles<METRIC, D, E>(a, q4, t0, t1, tk);
+    scan_tiles<METRIC, D, E>(a, q4, t0, t1, tk, a.reverse & 1u);
     group_combine_store<E, SCAN_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
 }
 
@@ -287,7 +291,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_stream_kernel(ScanAr
         const float4 *q4 = reinterpret_cast<const float4 *>(a.queries) + (size_t)q * (a.qpitch / 4);
         WaveTopK<E> tk;
         tk.init((int)a.k);
-        scan_tiles<METRIC, D, E>(a, q4, t0, t1, tk);
+        scan_tiles<METRIC, D, E>(a, q4, t0, t1, tk, (a.reverse + q) & 1u);  // serpentine over the queries
         group_combine_publish<E, SCAN_WAVES>(tk, j.partials + ((size_t)q * G + blockIdx.x) * a.k, j.arrivals + q);
     }
 }

@@ -214,6 +214,29 @@ struct WaveTopK {
         offer(((live >> lane) & 1ull) ? (((uint64_t)o << 32) | slot) : WVG_KEY_NONE);
     }
 
+    // offer_dist with the rejection on the float distance itself: while the
+    // list is full and its K-th distance tau_f is not NaN, a key below tau
+    // needs dist <= tau_f (ord(-0) < ord(+0) where -0 <= +0 holds; NaN never
+    // passes and never sorts below a non-NaN tau), so the compare is a
+    // superset test; the survivors take the exact path.  tau_f / tau_open
+    // must start from init_fast() and are refreshed after each exact offer.
+    float tau_f;
+    bool tau_open;
+    __device__ __forceinline__ void init_fast()
+    {
+        tau_f = __builtin_inff();
+        tau_open = true;
+    }
+    __device__ __forceinline__ void offer_dist_fast(float dist, uint32_t slot, uint64_t live)
+    {
+        const uint64_t cand = tau_open ? live : (__ballot(dist <= tau_f) & live);
+        if (cand == 0ull) return;
+        const int lane = threadIdx.x & 63;
+        offer(((live >> lane) & 1ull) ? wvg_make_key(dist, slot) : WVG_KEY_NONE);
+        tau_f = wvg_unord_f32((uint32_t)(tau >> 32));
+        tau_open = tau == WVG_KEY_NONE || tau_f != tau_f;
+    }
+
     // Offer one key per lane (KEY_NONE for an empty lane).
     __device__ __forceinline__ void offer(uint64_t key)
     {
