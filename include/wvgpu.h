@@ -151,6 +151,17 @@ int wvg_search_bq_rescore(wvg_corpus *bq, wvg_corpus *f32, const float *queries,
 int wvg_search_by_distance(wvg_corpus *c, const float *query, float target_distance, int64_t max_limit,
                            const uint64_t *allow_bits, uint64_t allow_words, uint64_t *out_ids,
                            float *out_dists, uint64_t out_capacity, uint64_t *out_count);
+/* The flat index's own SearchByVectorDistance result (V/flat/index.go:
+ * 531-591 as written): its loop calls recursiveSearch once -- the post
+ * statement of the `for` is empty, so later iterations only grow the limit
+ * until max_limit stops them (and never stop when max_limit < 0) -- so the
+ * result is the first window: among the `window` (100:
+ * V/common/search_by_dist_params.go:17) nearest rows, those with dist <=
+ * target or within 1e-6 of it, up to the first row beyond.  HNSW callers use
+ * wvg_search_by_distance (V/hnsw/search.go:85-151 re-searches).            */
+int wvg_search_by_distance_window(wvg_corpus *c, const float *query, float target_distance, uint32_t window,
+                                  const uint64_t *allow_bits, uint64_t allow_words, uint64_t *out_ids,
+                                  float *out_dists, uint64_t out_capacity, uint64_t *out_count);
 
 /* Device-pointer variants: inputs/outputs in HBM, asynchronous on `stream`
  * (a hipStream_t, NULL = default stream); no host synchronization, no

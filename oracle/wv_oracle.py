@@ -366,3 +366,48 @@ def search_by_distance(search_fn, target, max_limit):
             break
         cont = recursive()
     return np.asarray(res_i, dtype=np.uint64), np.asarray(res_d, dtype=np.float32)
+
+
+def search_by_distance_flat(search_fn, target, max_limit, max_iterations=1000):
+    """flat.SearchByVectorDistance restated literally from V/flat/index.go:
+    531-591 with V/common/search_by_dist_params.go:14-83.  search_fn(total) ->
+    (ids, dists) ascending, as SearchByVector.  The loop's `for` has no post
+    statement, so recursiveSearch runs once and later iterations only grow the
+    limit (Iterate) until MaxLimitReached -- with max_limit < 0 and a first
+    window that asks to continue, the reference never returns: that case is
+    reported as nonterminating (after max_iterations) with the results so far.
+    Returns (ids, dists, terminated)."""
+    target = np.float32(target)
+    offset, limit = 0, 100
+    total = offset + limit
+    res_i, res_d = [], []
+
+    def recursive():
+        ids, dist = search_fn(total)
+        cont = not (len(ids) < total)
+        lo, hi = min(offset, len(ids)), min(total, len(ids))
+        if lo == hi:
+            return False
+        for i in range(lo, hi):
+            if np.float32(dist[i]) <= target or abs(float(dist[i]) - float(target)) <= 1e-6:
+                res_i.append(int(ids[i]))
+                res_d.append(np.float32(dist[i]))
+            else:
+                cont = False
+                break
+        return cont
+
+    cont = recursive()
+    it = 0
+    terminated = True
+    while cont:
+        offset = total  # searchParams.Iterate()
+        limit *= 10
+        total = offset + limit
+        if max_limit >= 0 and total > max_limit:
+            break
+        it += 1
+        if it >= max_iterations:
+            terminated = False
+            break
+    return np.asarray(res_i, dtype=np.uint64), np.asarray(res_d, dtype=np.float32), terminated

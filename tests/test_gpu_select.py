@@ -191,15 +191,50 @@ def test_flat_index_search_by_distance_and_large_limit(ctx, orc):
     li, ld = orc.lex_topk(all_d, np.arange(n, dtype=np.uint64), 1500)
     assert np.array_equal(ids, li) and np.array_equal(bits(dists), bits(ld))
     t = np.sort(all_d)[400]
-    gi, gd = idx.SearchByVectorDistance(q, t, -1)
+    gi, gd = idx.SearchByVectorDistance(q, t, -1, semantics="hnsw")
     ei, ed = orc.search_by_distance(lambda tot: orc.lex_topk(all_d, np.arange(n, dtype=np.uint64), tot), t, -1)
     assert np.array_equal(gi, ei) and np.array_equal(bits(gd), bits(ed))
-    assert len(idx.SearchByVectorDistance(q, t, -1, AllowList())[0]) == 0
+    assert len(idx.SearchByVectorDistance(q, t, -1, AllowList(), semantics="hnsw")[0]) == 0
     # BQ-compressed index: every window is a rescored BQ search
     bidx = FlatIndex(ctx, d, "l2-squared", compression="bq", rescore_limit=400, capacity=64)
     bidx.AddBatch(np.arange(n), rows)
-    gi, gd = bidx.SearchByVectorDistance(q, t, -1)
+    gi, gd = bidx.SearchByVectorDistance(q, t, -1, semantics="hnsw")
     assert len(gi) > 0 and np.all(gd <= t + 1e-6)
     assert np.array_equal(bits(gd), bits(all_d[gi.astype(np.int64)]))  # rescored = exact distances
     ei, ed = orc.search_by_distance(lambda tot: bidx.SearchByVector(q, tot), t, -1)
     assert np.array_equal(gi, ei) and np.array_equal(bits(gd), bits(ed))
+
+
+@pytest.mark.parametrize("compression", [None, "bq"])
+def test_flat_search_by_distance_reference_semantics(ctx, orc, compression):
+    """FlatIndex.SearchByVectorDistance default = the flat index's own result
+    (V/flat/index.go:531-591 as written: one window of 100), against the
+    literal restatement of that loop (oracle.search_by_distance_flat)."""
+    from weaviate_amd.flat import AllowList, FlatIndex
+
+    n, d = 4000, 48
+    rows = orc.synth_rows(371, 0, n, d, 0)
+    q = orc.synth_rows(372, 0, 1, d, 0)[0]
+    kw = dict(compression="bq", rescore_limit=300) if compression else {}
+    idx = FlatIndex(ctx, d, "l2-squared", capacity=64, **kw)
+    idx.AddBatch(np.arange(n), rows)
+    all_d = orc.dist_all(0, q, rows)
+    srt = np.sort(all_d)
+    for t in [srt[0] - 1, srt[10], srt[99], srt[100], srt[700], np.float32(np.inf),
+              np.nextafter(srt[50], np.float32(-np.inf))]:
+        for max_limit in [-1, 50, 1100, 100_000]:
+            gi, gd = idx.SearchByVectorDistance(q, t, max_limit)
+            ei, ed, done = orc.search_by_distance_flat(lambda tot: idx.SearchByVector(q, tot), t, max_limit)
+            assert np.array_equal(gi, ei) and np.array_equal(bits(gd), bits(ed)), (t, max_limit)
+            assert len(gi) <= 100
+            if compression is None:  # and against the exact lexicographic search
+                xi, xd, _ = orc.search_by_distance_flat(
+                    lambda tot: orc.lex_topk(all_d, np.arange(n, dtype=np.uint64), tot), t, max_limit)
+                assert np.array_equal(gi, xi) and np.array_equal(bits(gd), bits(xd))
+    # a target past the 100th row: the flat result stops at the window, HNSW semantics go on
+    t = srt[700]
+    assert len(idx.SearchByVectorDistance(q, t, -1)[0]) == 100
+    assert len(idx.SearchByVectorDistance(q, t, -1, semantics="hnsw")[0]) > 100
+    allow = AllowList(*range(0, n, 7))
+    gi, gd = idx.SearchByVectorDistance(q, srt[2000], -1, allow)
+    assert len(gi) == 100 and np.all(gi % 7 == 0)

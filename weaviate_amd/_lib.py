@@ -58,6 +58,8 @@ SIGNATURES = {
                                       _P(c_uint64), c_uint64, _P(c_uint64), _P(c_float), _P(c_uint32)]),
     "wvg_search_by_distance": (c_int, [c_void_p, _P(c_float), c_float, ctypes.c_int64, _P(c_uint64), c_uint64,
                                        _P(c_uint64), _P(c_float), c_uint64, _P(c_uint64)]),
+    "wvg_search_by_distance_window": (c_int, [c_void_p, _P(c_float), c_float, c_uint32, _P(c_uint64), c_uint64,
+                                              _P(c_uint64), _P(c_float), c_uint64, _P(c_uint64)]),
     "wvg_search_workspace_size": (c_size_t, [c_void_p, c_uint32, c_uint32]),
     "wvg_search_device": (c_int, [c_void_p, c_void_p, c_uint32, c_uint32, c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_size_t, c_void_p]),

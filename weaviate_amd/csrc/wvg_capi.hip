@@ -1403,6 +1403,34 @@ int wvg_search_by_distance(wvg_corpus *c, const float *query, float target_dista
     return WVG_OK;
 }
 
+int wvg_search_by_distance_window(wvg_corpus *c, const float *query, float target_distance, uint32_t window,
+                                  const uint64_t *allow_bits, uint64_t allow_words, uint64_t *out_ids,
+                                  float *out_dists, uint64_t out_capacity, uint64_t *out_count)
+{
+    if (!c || !query || !out_count) return fail(WVG_ERR_INVALID, "null argument");
+    *out_count = 0;
+    if (window == 0) return WVG_OK;
+    // the first window of flat.SearchByVectorDistance's loop: SearchByVector(q, window)
+    // (V/flat/index.go:539-542), then the rows up to the first beyond the target (:555-567)
+    std::vector<uint64_t> ids(window);
+    std::vector<float> d(window);
+    uint32_t cnt = 0;
+    int rc = wvg_search(c, query, 1, window, allow_bits, allow_words, ids.data(), d.data(), &cnt);
+    if (rc) return rc;
+    uint64_t n = 0;
+    for (uint32_t i = 0; i < cnt; i++) {
+        const bool keep = d[i] <= target_distance || std::fabs((double)d[i] - (double)target_distance) <= 1e-6;
+        if (!keep) break;  // floatcomp.InDelta (usecases/floatcomp/delta.go:16-19)
+        if (n < out_capacity) {
+            if (out_ids) out_ids[n] = ids[i];
+            if (out_dists) out_dists[n] = d[i];
+        }
+        n++;
+    }
+    *out_count = n;
+    return WVG_OK;
+}
+
 int wvg_search_bq_rescore(wvg_corpus *bq, wvg_corpus *f32, const float *queries, uint32_t nq, uint32_t k,
                           uint32_t rescore_limit, const uint64_t *allow_bits, uint64_t allow_words, uint64_t *out_ids,
                           float *out_dists, uint32_t *out_counts)

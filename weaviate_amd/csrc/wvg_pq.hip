@@ -718,6 +718,159 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_dense_kernel(Sca
     group_combine_store<E, PQ_SCAN_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
 }
 
+// K8d: K8c with the R passes of a ring cycle in ONE basic block.  K8c's
+// per-tile offer is a branch, so the compiler schedules every pass on its
+// own and the tail of a pass (its last adds waiting on LDS) cannot overlap
+// the head of the next (its byte merges and first LDS reads).  Here a pass
+// only records its distance and the cheap float filter's verdict (a scalar
+// OR); the exact offers of the cycle's R tiles run after the cycle when any
+// lane passed, in tile order (a stale, larger tau_f only lets more lanes
+// through to the exact test).  Tile masks come R per vector load, one cycle
+// ahead (lane l = the l-th tile offered in the cycle).  GL: codes through
+// global loads with a scalar tile base (saddr) instead of buffer loads.
+template <int E, int R, int NB, int METRIC, bool GL>
+__global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_cycle_kernel(ScanArgs a, uint64_t *partials)
+{
+    extern __shared__ __attribute__((aligned(16))) f32x2 img[];  // [256][64]
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t qi = blockIdx.y;
+    const float *glut = reinterpret_cast<const float *>(a.queries) + (size_t)qi * a.qpitch;
+    constexpr int FILL = 32 * 256 / (PQ_SCAN_WAVES * 64);
+    float fv[FILL];
+#pragma unroll
+    for (int it = 0; it < FILL; it++) {
+        const uint32_t i = (uint32_t)it * (PQ_SCAN_WAVES * 64) + threadIdx.x;
+        fv[it] = glut[(i & 31u) * 256u + (i >> 5)];
+    }
+#pragma unroll
+    for (int it = 0; it < FILL; it++) {
+        const uint32_t i = (uint32_t)it * (PQ_SCAN_WAVES * 64) + threadIdx.x;
+        const uint32_t s = i & 31u, c = i >> 5;
+        img[c * 64u + s] = f32x2{fv[it], 0.0f};
+        img[c * 64u + 32u + s] = f32x2{0.0f, fv[it]};
+    }
+    __syncthreads();
+    const uint64_t ntiles = a.tile_end - a.tile_begin;
+    const uint64_t total = (uint64_t)gridDim.x * PQ_SCAN_WAVES;
+    const uint64_t gw = (uint64_t)blockIdx.x * PQ_SCAN_WAVES + wave;
+    const uint64_t t0 = a.tile_begin + ntiles * gw / total, t1 = a.tile_begin + ntiles * (gw + 1) / total;
+    WaveTopK<E> tk;
+    tk.init((int)a.k);
+    tk.init_fast();
+    if (t0 < t1) {
+        const uint32_t n = (uint32_t)(t1 - t0);
+        const char *wbase = reinterpret_cast<const char *>(a.data) + t0 * 2048u;
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(wbase), (short)0, (int)(n * 2048u), 0x00020000);
+        const uint32_t voff = (uint32_t)lane * 16u;
+        const uint32_t x = (uint32_t)lane & 31u, x8 = x * 8u;
+        uint32_t nmask[8];
+#pragma unroll
+        for (int w = 0; w < 8; w++) {
+            uint32_t mk = 0u;
+#pragma unroll
+            for (int bb = 0; bb < 4; bb++) mk |= (4u * w + bb + x >= 32u) ? (0xFFu << (8 * bb)) : 0u;
+            nmask[w] = mk;
+        }
+        const char *imgb = reinterpret_cast<const char *>(img);
+        const bool rev = a.reverse & 1u;
+        auto tile_of = [&](uint32_t i) -> uint32_t { return rev ? n - 1u - i : i; };
+        auto load = [&](uint32_t i, uint32_t (&w)[8]) {
+            u32x4 lo, hi;
+            if constexpr (GL) {
+                const char *tb = wbase + (size_t)tile_of(i < n ? i : 0u) * 2048u;  // past the range: re-read
+                lo = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(tb + voff));
+                hi = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(tb + voff + 1024u));
+            } else {
+                const uint32_t so = i < n ? tile_of(i) * 2048u : n * 2048u;  // past the range: zeros
+                lo = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, so, 2);
+                hi = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 1024u, so, 2);
+            }
+            w[0] = lo.x; w[1] = lo.y; w[2] = lo.z; w[3] = lo.w;
+            w[4] = hi.x; w[5] = hi.y; w[6] = hi.z; w[7] = hi.w;
+        };
+        // lane l < R: live mask of the tile offered by pass l of the cycle at
+        // `base` (pass order index base - 1 + l; none for index -1 or >= n)
+        auto cycle_masks = [&](uint32_t base) -> uint64_t {
+            const uint32_t ii = base + (uint32_t)lane - 1u;
+            uint64_t m = 0ull;
+            if (lane < R && base + (uint32_t)lane >= 1u && ii < n) {
+                const uint64_t t = t0 + tile_of(ii);
+                m = a.valid[t];
+                if (a.allow) {
+                    const uint64_t wi = t - a.allow_t0;
+                    m &= wi < a.allow_words ? a.allow[wi] : 0ull;
+                }
+            }
+            return m;
+        };
+        uint64_t mg = cycle_masks(0), mgn = cycle_masks(R);
+        uint32_t ring[R][8];
+#pragma unroll
+        for (int s = 0; s < R - 1; s++) load((uint32_t)s, ring[s]);
+#pragma unroll
+        for (int w = 0; w < 8; w++) ring[R - 1][w] = 0u;
+        f32x2 acc = {0.0f, 0.0f};
+        for (uint32_t base = 0; base <= n; base += R) {
+            float dist[R];
+            uint64_t pending = 0ull;
+            const uint64_t open = tk.tau_open ? ~0ull : 0ull;  // list not full yet: every live lane (no branch)
+            const float tf = tk.tau_f;
+#pragma unroll
+            for (int s = 0; s < R; s++) {
+                const int sc = (s + R - 1) % R;
+                const uint32_t i = base + (uint32_t)s;
+                uint32_t win[8];
+#pragma unroll
+                for (int w = 0; w < 8; w++)
+                    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(win[w]) : "v"(nmask[w]), "v"(ring[s][w]), "v"(ring[sc][w]));
+#pragma unroll
+                for (int h = 0; h < 32 / NB; h++) {
+                    f32x2 v[NB];
+#pragma unroll
+                    for (int jj = 0; jj < NB; jj++) {
+                        const int j = h * NB + jj;
+                        const uint32_t c8 = __builtin_amdgcn_perm(0u, win[j >> 2], 0x0C0C000Cu | ((uint32_t)(j & 3) << 8));
+                        const uint32_t off = (c8 << 1) + x8;
+                        v[jj] = *reinterpret_cast<const f32x2 *>(imgb + off + 8 * j);
+                    }
+#pragma unroll
+                    for (int jj = 0; jj < NB; jj++) acc = acc + v[jj];
+                }
+                dist[s] = METRIC == WVG_M_L2 ? acc.x : (METRIC == WVG_M_DOT ? -acc.x : 1.0f - acc.x);
+                const uint64_t live = readlane64(mg, s);
+                pending |= (__ballot(dist[s] <= tf) | open) & live;
+                acc = f32x2{acc.y, 0.0f};
+                load(i + (uint32_t)R - 1u, ring[sc]);
+            }
+            if (pending) {  // exact offers of this cycle's tiles, in order
+#pragma unroll
+                for (int s = 0; s < R; s++) {
+                    const uint64_t live = readlane64(mg, s);
+                    if (live) {
+                        const uint32_t tl = base + (uint32_t)s - 1u;
+                        tk.offer_dist_fast(dist[s], (uint32_t)((t0 + tile_of(tl)) * 64u) + (uint32_t)lane, live);
+                    }
+                }
+            }
+            mg = mgn;
+            mgn = cycle_masks(base + 2u * R);
+        }
+    }
+    group_combine_store<E, PQ_SCAN_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
+}
+
+template <int E, int R, int NB, bool GL>
+static void launch_pq_cycle(const ScanArgs &a, uint64_t *partials, dim3 grid, dim3 block, size_t lds, hipStream_t s)
+{
+    if (a.metric == WVG_M_L2)
+        launch_timed((scan_pq32_cycle_kernel<E, R, NB, WVG_M_L2, GL>), grid, block, lds, s, a, partials);
+    else if (a.metric == WVG_M_DOT)
+        launch_timed((scan_pq32_cycle_kernel<E, R, NB, WVG_M_DOT, GL>), grid, block, lds, s, a, partials);
+    else
+        launch_timed((scan_pq32_cycle_kernel<E, R, NB, WVG_M_COSINE, GL>), grid, block, lds, s, a, partials);
+}
+
 template <int E, int R, int NB>
 static void launch_pq_dense(const ScanArgs &a, uint64_t *partials, dim3 grid, dim3 block, size_t lds, hipStream_t s)
 {
@@ -736,6 +889,15 @@ static hipError_t launch_pq_e(const ScanArgs &a, uint64_t *partials, int groups,
     const size_t lds = (size_t)a.pq_m * a.pq_ks * 4;
     const int v = tuning().pq_variant;
     const bool m32 = a.pq_ks == 256 && a.pq_m == 32 && a.nchunks == 2;
+    if (m32 && v >= 14 && v <= 17) {
+        // K8d (one basic block per ring cycle): 14 = ring 8 / LDS batches of 8, 15 = ring 4 / 16,
+        // 16 = ring 8 / 8 with global loads, 17 = ring 4 / 16 with global loads
+        if (v == 14) launch_pq_cycle<E, 8, 8, false>(a, partials, grid, block, 4 * lds, s);
+        else if (v == 15) launch_pq_cycle<E, 4, 16, false>(a, partials, grid, block, 4 * lds, s);
+        else if (v == 16) launch_pq_cycle<E, 8, 8, true>(a, partials, grid, block, 4 * lds, s);
+        else launch_pq_cycle<E, 4, 16, true>(a, partials, grid, block, 4 * lds, s);
+        return hipGetLastError();
+    }
     if (m32 && (v == 10 || v == 11 || v == 12 || (v == 0 && a.dense))) {
         // K8c (dense, issue-trimmed): 0 (auto) / 12 = ring 8 / LDS batches of 16, 10 = ring 8 / 8, 11 = ring 4 / 16
         if (v == 11)

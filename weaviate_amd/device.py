@@ -206,6 +206,19 @@ class Corpus:
                 return ids[:cnt.value], dists[:cnt.value]
             cap = cnt.value
 
+    def search_by_distance_window(self, query, target: float, window: int = 100, allow=None):
+        """wvg_search_by_distance_window: the flat index's own range-search
+        result (its first window, V/flat/index.go:531-591 as written)."""
+        q = np.ascontiguousarray(query, dtype=np.float32).reshape(-1)
+        aw, an = (None, 0) if allow is None else (np.ascontiguousarray(allow, dtype=np.uint64), len(allow))
+        cnt = c_uint64()
+        ids = np.empty(max(1, window), dtype=np.uint64)
+        dists = np.empty(max(1, window), dtype=np.float32)
+        check(self.lib.wvg_search_by_distance_window(self.handle, fptr(q), float(target), int(window),
+                                                     u64ptr(aw) if aw is not None else None, an, u64ptr(ids),
+                                                     fptr(dists), len(ids), byref(cnt)))
+        return ids[:cnt.value], dists[:cnt.value]
+
 
 def search_bq_rescore(bq: Corpus, f32: Corpus, queries, k: int, rescore_limit: int, allow=None):
     q = np.ascontiguousarray(queries, dtype=np.float32)

@@ -122,13 +122,32 @@ class FlatIndex:
         n = int(counts[0])
         return ids[0, :n], dists[0, :n]
 
-    def SearchByVectorDistance(self, vector, target: float, max_limit: int, allow: AllowList | None = None):
-        """index.go:531-591: the rows the growing-limit loop (limits 100, 1100,
-        11100, ...) keeps -- dist <= target or within 1e-6 -- in one GPU pass
-        (wvg_search_by_distance; DESIGN.md section 4 on the loop's semantics)."""
+    def SearchByVectorDistance(self, vector, target: float, max_limit: int, allow: AllowList | None = None,
+                               semantics: str = "flat"):
+        """index.go:531-591.  semantics="flat" (default): the flat index's own
+        result as the reference computes it -- its loop calls recursiveSearch
+        once (the `for` has no post statement; later iterations only grow the
+        limit until max_limit, and never end for max_limit < 0 when the first
+        window is full), so it returns the rows of the first window of 100
+        (V/common/search_by_dist_params.go:17) up to the first beyond the
+        target: wvg_search_by_distance_window, one fused top-100 scan.  Where
+        the reference would not terminate this returns that window.
+        semantics="hnsw": the re-searching loop HNSW runs
+        (V/hnsw/search.go:85-151; limits 100, 1100, 11100, ...), as one GPU
+        pass (wvg_search_by_distance)."""
+        if semantics not in ("flat", "hnsw"):
+            raise ValueError(f"unknown semantics {semantics!r}")
         if allow is not None and allow.IsEmpty():
             return np.empty(0, dtype=np.uint64), np.empty(0, dtype=np.float32)
         bm = allow.bitmap() if allow is not None else None
+        if semantics == "flat":
+            if self.bq is None:
+                return self.vectors.search_by_distance_window(vector, target, DEFAULT_SEARCH_BY_DIST_INITIAL_LIMIT, bm)
+            ids, dist = self.SearchByVector(vector, DEFAULT_SEARCH_BY_DIST_INITIAL_LIMIT, allow)
+            keep = 0
+            while keep < len(ids) and (dist[keep] <= target or abs(float(dist[keep]) - float(target)) <= 1e-6):
+                keep += 1
+            return np.asarray(ids[:keep], dtype=np.uint64), np.asarray(dist[:keep], dtype=np.float32)
         if self.bq is None:
             return self.vectors.search_by_distance(vector, target, max_limit, bm)
         # BQ: every window is a BQ search with rescoring (index.go:539 -> searchByVectorBQ),
