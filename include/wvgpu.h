@@ -60,6 +60,17 @@ int wvg_device_count(int *out);
 int wvg_open(int device, wvg_ctx **out);
 int wvg_close(wvg_ctx *ctx);
 int wvg_synchronize(wvg_ctx *ctx);
+/* The reduction order of the fp32 distances (l2 / dot / cosine), i.e. which
+ * of the reference's SIMD kernels the results must match bit for bit: its
+ * init() picks l2_512 / dot_512 on hosts with AMX-BF16 and AVX-512, else
+ * l2_256 / dot_256 (D/l2_amd64.go:19-25, D/dot_product_amd64.go:19-25).
+ * Default WVG_ORDER_AVX256 (AMD EPYC hosts, which have no AMX).  Applies to
+ * every fp32 distance of the context (scans, rescoring, DistanceToNode,
+ * wvg_distance_batch); batched dot/cosine then scans with K1 instead of the
+ * MFMA kernel, whose slices are the AVX2 order's chains.                  */
+#define WVG_ORDER_AVX256 0
+#define WVG_ORDER_AVX512 1
+int wvg_set_distance_order(wvg_ctx *ctx, int order);
 
 /* ---- corpus: the device-resident copy of a flat index's rows --------------
  * Replaces the LSM cursor scan of V/flat/index.go:411-452 and the BQ cache of

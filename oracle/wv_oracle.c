@@ -242,6 +242,22 @@ ORC_API float orc_single_dist(int metric, const float *a, const float *b, long n
     }
 }
 
+/* SingleDist as dispatched on AMX + AVX-512 hosts (D/l2_amd64.go:19-25,
+ * D/dot_product_amd64.go:19-25): the 512 kernels, same Wrap. */
+ORC_API float orc_single_dist_512(int metric, const float *a, const float *b, long n)
+{
+    switch (metric) {
+    case ORC_L2: return orc_l2_512(a, b, n);
+    case ORC_DOT: return -orc_dot_512(a, b, n);
+    default: return 1.0f - orc_dot_512(a, b, n);
+    }
+}
+
+ORC_API void orc_dist_all_512(int metric, const float *q, const float *rows, long n, long d, float *out)
+{
+    for (long i = 0; i < n; i++) out[i] = orc_single_dist_512(metric, q, rows + i * d, d);
+}
+
 /* Provider.Wrap: L2 identity (D/l2.go:90-92), dot -x (D/dot_product.go:96-98),
  * cosine 1-x (D/cosine_dist.go:66-68). */
 ORC_API float orc_wrap(int metric, float x)

@@ -74,6 +74,7 @@ def lib():
         l.orc_synth_value.argtypes = [c_uint64, c_uint64, c_uint64, c_int]
         l.orc_synth_rows.argtypes = [c_uint64, c_uint64, c_long, c_long, c_long, c_int, _F]
         l.orc_dist_all.argtypes = [c_int, _F, _F, c_long, c_long, _F]
+        l.orc_dist_all_512.argtypes = [c_int, _F, _F, c_long, c_long, _F]
         l.orc_bq_dist_all.argtypes = [_U64, _U64, c_long, c_long, _F]
         l.orc_bench_flat.restype = c_double
         l.orc_bench_flat.argtypes = [_F, c_long, c_long, c_long, _F, c_long, c_long, c_int, c_void_p, c_int, _U64, _F]
@@ -134,6 +135,14 @@ def dist_all(metric, q, rows):
     q, rows = f32(q), f32(rows)
     out = np.empty(rows.shape[0], dtype=np.float32)
     lib().orc_dist_all(metric, _f(q), _f(rows), rows.shape[0], rows.shape[1], _f(out))
+    return out
+
+
+def dist_all_512(metric, q, rows):
+    """SingleDist(q, row) for all rows with the AVX-512 kernels (AMX hosts)."""
+    q, rows = f32(q), f32(rows)
+    out = np.empty(rows.shape[0], dtype=np.float32)
+    lib().orc_dist_all_512(metric, _f(q), _f(rows), rows.shape[0], rows.shape[1], _f(out))
     return out
 
 

@@ -204,3 +204,18 @@ def test_oracle_selftest_under_asan_ubsan():
     r = subprocess.run([os.path.join(here, "_build", "selftest_asan")], capture_output=True, text=True,
                        env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1"), timeout=300)
     assert r.returncode == 0 and "selftest ok" in r.stdout, r.stderr[-2000:]
+
+
+def test_dist_all_512_matches_reference_kernels(orc):
+    """The oracle's AVX-512-order SingleDist (used by the 512-mode GPU tests)
+    equals the reference's compiled l2_512 / dot_512 outputs, with Wrap."""
+    import os
+
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "distances.npz"))
+    off = 0
+    for n, l5, d5 in zip(g["lens"], g["l2_512"], g["dot_512"]):
+        a, b = g["a"][off:off + n], g["b"][off:off + n]
+        off += n
+        assert orc.dist_all_512(0, a, b[None])[0].view(np.uint32) == np.float32(l5).view(np.uint32)
+        assert orc.dist_all_512(1, a, b[None])[0].view(np.uint32) == np.float32(-d5).view(np.uint32)
+        assert orc.dist_all_512(2, a, b[None])[0].view(np.uint32) == (np.float32(1) - d5).view(np.uint32)

@@ -25,6 +25,7 @@ WVG_ERR_CAPACITY = -7
 
 KIND_F32, KIND_BQ, KIND_PQ = 0, 1, 2
 METRIC_L2, METRIC_DOT, METRIC_COSINE = 0, 1, 2
+ORDER_AVX256, ORDER_AVX512 = 0, 1  # reference SIMD kernel whose reduction order distances follow
 METRIC_BY_NAME = {"l2-squared": METRIC_L2, "dot": METRIC_DOT, "cosine": METRIC_COSINE,
                   "cosine-dot": METRIC_COSINE}
 
@@ -37,6 +38,7 @@ SIGNATURES = {
     "wvg_open": (c_int, [c_int, _P(c_void_p)]),
     "wvg_close": (c_int, [c_void_p]),
     "wvg_synchronize": (c_int, [c_void_p]),
+    "wvg_set_distance_order": (c_int, [c_void_p, c_int]),
     "wvg_corpus_create": (c_int, [c_void_p, c_int, c_int, c_uint32, c_uint64, c_uint64, _P(c_void_p)]),
     "wvg_corpus_destroy": (c_int, [c_void_p]),
     "wvg_corpus_reserve": (c_int, [c_void_p, c_uint64]),

@@ -323,6 +323,14 @@ int wvg_close(wvg_ctx *ctx)
     return WVG_OK;
 }
 
+int wvg_set_distance_order(wvg_ctx *ctx, int order)
+{
+    if (!ctx) return fail(WVG_ERR_INVALID, "null ctx");
+    if (order != WVG_ORDER_AVX256 && order != WVG_ORDER_AVX512) return fail(WVG_ERR_INVALID, "unknown distance order");
+    ctx->order512 = order == WVG_ORDER_AVX512;
+    return WVG_OK;
+}
+
 int wvg_synchronize(wvg_ctx *ctx)
 {
     if (!ctx) return fail(WVG_ERR_INVALID, "null ctx");
@@ -923,7 +931,8 @@ static SearchPlan plan_search(wvg_corpus *c, uint32_t nq, uint32_t k, const uint
     a.dim = c->kind == WVG_KIND_F32 ? c->dim : 0;  // K1 grid depends on the row size and metric
     a.metric = c->metric;
     const uint32_t mn = c->ctx->mfma_min_nq;
-    p.gemm = c->kind == WVG_KIND_F32 && mn > 0 && nq >= mn && gemm_supported(c->dim, c->metric);
+    p.gemm = c->kind == WVG_KIND_F32 && mn > 0 && nq >= mn && gemm_supported(c->dim, c->metric) &&
+             !c->ctx->order512;  // K3's 32 MFMA slices are the AVX2 order's chains
     if (p.gemm)
         p.groups = (int)gemm_row_ranges(nq, std::max<uint64_t>(1, p.te - p.tb), c->ctx->num_cus, c->dim, k);
     else
@@ -955,6 +964,7 @@ static int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t 
     a.pq_m = c->pq_m;
     a.pq_ks = c->pq_ks;
     a.dense = pq_dense(c, d_allow);
+    a.order512 = c->ctx->order512;
     if (!p.gemm) a.reverse = next_direction(c, 1);
     ProfArm arm(c->ctx);
     if (arm.rc) return arm.rc;
@@ -1103,6 +1113,7 @@ static ScanArgs scan_args_for(const wvg_corpus *c, const void *d_q, uint32_t qpi
     a.pq_m = c->pq_m;
     a.pq_ks = c->pq_ks;
     a.dense = pq_dense(c, d_allow);
+    a.order512 = c->ctx->order512;
     return a;
 }
 
@@ -1292,7 +1303,7 @@ static int bq_rescore_large(wvg_corpus *bq, wvg_corpus *f32, const float *querie
         // sb.sorted[0..n) = Hamming top-R keys (slot in the low 32 bits)
         WVG_HIP(launch_rescore_keys(f32->metric, (const float *)(b + o_qf) + (size_t)qi * qpf, qpf,
                                     (const float *)f32->d_data, f32->dim, f32->nchunks, sb.sorted, 1, (uint32_t)n,
-                                    (uint32_t)n, (uint64_t *)(b + o_resc), s));
+                                    (uint32_t)n, (uint64_t *)(b + o_resc), s, f32->ctx->order512));
         WVG_HIP(sort_keys64(sb.temp, sb.temp_bytes, (uint64_t *)(b + o_resc), (uint64_t *)(b + o_rs), n, s));
         const uint64_t kk = std::min<uint64_t>(k, n);
         WVG_HIP(launch_emit_sorted((uint64_t *)(b + o_rs), kk, f32->id_base, (uint64_t *)(b + o_ids),
@@ -1508,7 +1519,7 @@ int wvg_search_bq_rescore(wvg_corpus *bq, wvg_corpus *f32, const float *queries,
     WVG_HIP(launch_merge_lists(part, nq, (uint32_t)p.groups, R, R, 0, cand_ids, (float *)(b + o_resc), nullptr, s));
     // cand_ids now hold slots (or KEY_NONE); rescore them exactly against the f32 rows
     WVG_HIP(launch_rescore_keys(f32->metric, (const float *)(b + o_qf), qpf, (const float *)f32->d_data, d,
-                                f32->nchunks, cand_ids, nq, R, R, (uint64_t *)(b + o_resc), s));
+                                f32->nchunks, cand_ids, nq, R, R, (uint64_t *)(b + o_resc), s, f32->ctx->order512));
     WVG_HIP(launch_merge_keys((uint64_t *)(b + o_resc), nq, R, k, f32->id_base, (uint64_t *)(b + o_ids),
                               (float *)(b + o_d), (uint32_t *)(b + o_cnt), s));
     if (out_ids) WVG_HIP(hipMemcpyAsync(out_ids, b + o_ids, (size_t)nq * k * 8, hipMemcpyDeviceToHost, s));
@@ -1607,6 +1618,7 @@ int wvg_search_device_pipelined(wvg_corpus *c, const float *d_queries, uint32_t 
         a.nq = nq;
         a.k = k;
         a.reverse = next_direction(c, nq);
+        a.order512 = c->ctx->order512;
         WVG_HIP(hipMemsetAsync(j.arrivals, 0, align_up((size_t)nq * 4, 16), s));
         ProfArm arm(c->ctx);
         if (arm.rc) return arm.rc;
@@ -1629,6 +1641,7 @@ int wvg_search_device_pipelined(wvg_corpus *c, const float *d_queries, uint32_t 
     a.qpitch = c->dim;
     a.nq = 1;
     a.k = k;
+    a.order512 = c->ctx->order512;
     const uint32_t dir0 = next_direction(c, nq);
     for (uint32_t i = 0; i < nq; i++) {
         a.queries = d_queries + (size_t)i * c->dim;
@@ -1723,7 +1736,7 @@ int wvg_rescore(wvg_ctx *ctx, int metric, const float *q, const float *rows, con
     WVG_HIP(hipMemcpyAsync(bk.b + o_q, qp.data(), qp.size() * 4, hipMemcpyHostToDevice, bk.s()));
     WVG_HIP(launch_f32_store((const float *)(bk.b + o_x), nullptr, n, dim, nch, 0, (float *)(bk.b + o_t), bk.s()));
     WVG_HIP(launch_dist_keys(metric, (const float *)(bk.b + o_q), (const float *)(bk.b + o_t), n, dim,
-                             (uint64_t *)(bk.b + o_k), bk.s()));
+                             (uint64_t *)(bk.b + o_k), bk.s(), ctx->order512));
     if (large) {
         const uint32_t kk = (uint32_t)std::min<uint64_t>(k, n);
         WVG_HIP(sort_keys64(bk.b + o_tmp, temp_bytes, (const uint64_t *)(bk.b + o_k), (uint64_t *)(bk.b + o_s), n,
@@ -1896,7 +1909,7 @@ int wvg_distance_batch(wvg_ctx *ctx, int metric, const float *q, const float *X,
     WVG_HIP(hipMemcpyAsync(bk.b + o_q, qp.data(), qp.size() * 4, hipMemcpyHostToDevice, bk.s()));
     WVG_HIP(launch_f32_store((const float *)(bk.b + o_x), nullptr, n, dim, nch, 0, (float *)(bk.b + o_t), bk.s()));
     WVG_HIP(launch_distance_rows(metric, (const float *)(bk.b + o_q), (const float *)(bk.b + o_t), n, dim,
-                                 (float *)(bk.b + o_o), bk.s()));
+                                 (float *)(bk.b + o_o), bk.s(), ctx->order512));
     WVG_HIP(hipMemcpyAsync(out, bk.b + o_o, n * 4, hipMemcpyDeviceToHost, bk.s()));
     WVG_HIP(hipStreamSynchronize(bk.s()));
     return WVG_OK;

@@ -44,6 +44,7 @@ struct wvg_ctx {
     int device = 0;
     int num_cus = 256;
     uint32_t mfma_min_nq = 32;  // batches of >= this many dot/cosine queries use K3 (env WVG_MFMA_MIN_QUERIES; 0 = never)
+    int order512 = 0;           // distancer kernels of an AMX + AVX-512 host (wvg_set_distance_order)
     std::mutex pool_mu;
     std::vector<wvg::StreamSlot *> free_slots;
     std::vector<wvg::StreamSlot *> all_slots;
@@ -187,6 +188,7 @@ struct ScanArgs {
                                // alternates between calls (wvg_corpus::scan_serial): consecutive scans then
                                // begin where the previous one ended, on rows still in the Infinity Cache
     int dense;                 // PQ m = 32: no allow list and mostly-live rows -> K8c (no tile skipping)
+    int order512;              // F32 distances in the AVX-512 kernels' order (wvg_set_distance_order)
 };
 // Phase 1 writes dense partials [nq][groups][K] (keys, KEY_NONE = empty).
 int scan_groups_for(const ScanArgs &a, int num_cus);
@@ -285,16 +287,16 @@ hipError_t launch_gather_chunks(const void *tiled, const uint64_t *slots, uint64
 hipError_t launch_normalize_rows(const float *in, uint64_t n, uint32_t dim, float *out,
                                  hipStream_t s);
 hipError_t launch_distance_rows(int metric, const float *q, const float *rows, uint64_t n,
-                                uint32_t dim, float *out, hipStream_t s);
+                                uint32_t dim, float *out, hipStream_t s, int o512 = 0);
 // keys[i] = (SingleDist(q, row i), i) over a tiled temporary of n rows.
 hipError_t launch_dist_keys(int metric, const float *q, const float *tiled, uint64_t n, uint32_t dim,
-                            uint64_t *keys, hipStream_t s);
+                            uint64_t *keys, hipStream_t s, int o512 = 0);
 hipError_t launch_synth_rows(uint64_t seed, int dist, const uint64_t *ids, uint64_t n, uint32_t dim,
                              int normalize, float *out, hipStream_t s);
 hipError_t launch_rescore_keys(int metric, const float *q, uint32_t qpitch, const float *tiled,
                                uint32_t dim, uint32_t nchunks, const uint64_t *cand_keys,
                                uint32_t nq, uint32_t ncand, uint32_t cand_stride,
-                               uint64_t *out_keys, hipStream_t s);
+                               uint64_t *out_keys, hipStream_t s, int o512 = 0);
 // BQ
 hipError_t launch_bq_encode_rows(const float *rows, uint64_t n, uint32_t dim, int normalize,
                                  uint64_t *codes, hipStream_t s);

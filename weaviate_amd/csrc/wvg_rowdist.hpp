@@ -150,6 +150,93 @@ __device__ __forceinline__ float row_dot_or_l2_generic(const float4 *__restrict_
     return avx256_reduce(acc, sum);
 }
 
+// l2_512 / dot_512 (D/c/l2_avx512_amd64.c:14-178, D/c/dot_avx512_amd64.c),
+// the kernels Weaviate dispatches on AMX + AVX-512 hosts (D/l2_amd64.go:19-25,
+// D/dot_product_amd64.go:19-25; wvg_set_distance_order).  Below 128 elements
+// they equal the AVX2 kernels.  Otherwise: 128 chains a5[j][l] (element
+// 128b + 16j + l) over the whole 128-blocks, the tree ((a1+a0) + (a3+a2)) +
+// ((a5+a4) + (a7+a6)) per lane, the low then the high 8 lanes added into
+// acc[0], and the AVX2 loop continues on the rest with that acc[0].
+template <int METRIC, int CSTRIDE>
+__device__ __forceinline__ float row_dist_512(const float4 *__restrict__ p, const float4 *__restrict__ q4, int n)
+{
+    if (n < 128) return row_dot_or_l2_generic<METRIC, CSTRIDE>(p, q4, n);
+    const float *q = reinterpret_cast<const float *>(q4);
+    float a5[8][16];
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+#pragma unroll
+        for (int l = 0; l < 16; l++) a5[j][l] = 0.0f;
+    const int nb = n >> 7;
+    for (int b = 0; b < nb; b++) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            float4 xs[4];
+#pragma unroll
+            for (int c = 0; c < 4; c++) xs[c] = p[(size_t)(b * 32 + j * 4 + c) * CSTRIDE];
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const float4 qq = q4[b * 32 + j * 4 + c];
+                acc_update<METRIC>(a5[j][4 * c + 0], qq.x, xs[c].x);
+                acc_update<METRIC>(a5[j][4 * c + 1], qq.y, xs[c].y);
+                acc_update<METRIC>(a5[j][4 * c + 2], qq.z, xs[c].z);
+                acc_update<METRIC>(a5[j][4 * c + 3], qq.w, xs[c].w);
+            }
+        }
+    }
+    float acc[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+#pragma unroll
+        for (int l = 0; l < 8; l++) acc[j][l] = 0.0f;
+    float r[16];
+#pragma unroll
+    for (int l = 0; l < 16; l++) {
+        float x0 = a5[1][l] + a5[0][l];
+        const float x2 = a5[3][l] + a5[2][l];
+        float x4 = a5[5][l] + a5[4][l];
+        const float x6 = a5[7][l] + a5[6][l];
+        x0 = x2 + x0;
+        x4 = x6 + x4;
+        r[l] = x4 + x0;
+    }
+#pragma unroll
+    for (int l = 0; l < 8; l++) acc[0][l] = r[l] + acc[0][l];
+#pragma unroll
+    for (int l = 0; l < 8; l++) acc[0][l] = r[8 + l] + acc[0][l];
+    float sum = 0.0f;
+    int pos = nb * 128, rem = n - pos;
+    while (rem >= 32) {
+        float4 xs[8];
+#pragma unroll
+        for (int cc = 0; cc < 8; cc++) xs[cc] = p[(size_t)((pos >> 2) + cc) * CSTRIDE];
+#pragma unroll
+        for (int cc = 0; cc < 8; cc++) chunk_update<METRIC>(acc, cc, q4[(pos >> 2) + cc], xs[cc]);
+        pos += 32;
+        rem -= 32;
+    }
+    while (rem >= 8) {
+        const int c = pos >> 2;
+        chunk_update<METRIC>(acc, 0, q4[c], p[(size_t)c * CSTRIDE]);
+        chunk_update<METRIC>(acc, 1, q4[c + 1], p[(size_t)(c + 1) * CSTRIDE]);
+        pos += 8;
+        rem -= 8;
+    }
+    while (rem) {
+        scalar_update<METRIC>(sum, q[pos], elem_at<CSTRIDE>(p, pos));
+        pos++;
+        rem--;
+    }
+    return avx256_reduce(acc, sum);
+}
+
+// The reduction order of the host's distancer: AVX2 (default, EPYC hosts) or AVX-512.
+template <int METRIC, int CSTRIDE>
+__device__ __forceinline__ float row_dist(const float4 *__restrict__ p, const float4 *__restrict__ q4, int n, int o512)
+{
+    return o512 ? row_dist_512<METRIC, CSTRIDE>(p, q4, n) : row_dot_or_l2_generic<METRIC, CSTRIDE>(p, q4, n);
+}
+
 // Provider.Wrap of the raw kernel value: L2 identity, dot -x (D/dot_product.go:68-76),
 // cosine-dot 1-x (D/cosine_dist.go:38-45).
 __device__ __forceinline__ float wrap_metric(int metric, float r)

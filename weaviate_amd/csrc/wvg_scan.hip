@@ -131,7 +131,9 @@ __device__ __forceinline__ void scan_tiles(const ScanArgs &a, const float4 *q4, 
         if (m == 0ull) continue;  // wave-uniform: nothing live/allowed in this tile
         const float4 *rp = data + (size_t)t * a.nchunks * 64 + lane;
         float r;
-        if constexpr (D > 0)
+        if (a.order512)  // wave-uniform: the AVX-512 kernels' order (generic length)
+            r = row_dist_512<METRIC, 64>(rp, q4, (int)a.dim);
+        else if constexpr (D > 0)
             r = row_dot_or_l2_fixed<METRIC, D, 64>(rp, q4);
         else
             r = row_dot_or_l2_generic<METRIC, 64>(rp, q4, (int)a.dim);
@@ -378,7 +380,9 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_sweep_kernel(ScanArg
         if (m == 0ull) continue;
         const float4 *rp = data + (size_t)t * a.nchunks * 64 + lane;
         float r;
-        if constexpr (D > 0)
+        if (a.order512)
+            r = row_dist_512<METRIC, 64>(rp, q4, (int)a.dim);
+        else if constexpr (D > 0)
             r = row_dot_or_l2_fixed<METRIC, D, 64>(rp, q4);
         else
             r = row_dot_or_l2_generic<METRIC, 64>(rp, q4, (int)a.dim);
@@ -403,7 +407,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_plain_kernel(ScanArg
         const uint64_t m = tile_mask(a, t);
         if (m == 0ull) continue;
         const float4 *rp = data + (size_t)t * a.nchunks * 64 + lane;
-        const float r = row_dot_or_l2_generic<METRIC, 64>(rp, q4, D);
+        const float r = row_dist<METRIC, 64>(rp, q4, D, a.order512);
         tk.offer(lane_key(m, wrap_metric(a.metric, r), t, lane));
     }
     group_combine_store<E, SCAN_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
@@ -437,7 +441,7 @@ int scan_groups_for(const ScanArgs &a, int num_cus)
 template <int METRIC, int D, int E>
 static void launch_fixed(const ScanArgs &a, uint64_t *partials, dim3 grid, dim3 block, hipStream_t s)
 {
-    const int v = a.side.active ? 0 : tuning().scan_variant;
+    const int v = a.side.active || a.order512 ? 0 : tuning().scan_variant;  // (variants 1-3: AVX2 order only)
     if (v == 1 && !a.allow)
         launch_timed((scan_f32_pipe_kernel<METRIC, D, E>), grid, block, 0, s, a, partials);
     else if (v == 2)
@@ -773,16 +777,16 @@ hipError_t launch_gather_chunks(const void *tiled, const uint64_t *slots, uint64
 // Provider.SingleDist(q, X[i]) for a tiled temporary (distancer.BatchProvider).
 template <int METRIC>
 __global__ void distance_tiled_kernel(int metric, const float4 *q4, const float4 *tiled, uint64_t n, uint32_t dim,
-                                      uint32_t nchunks, float *out)
+                                      uint32_t nchunks, float *out, int o512)
 {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
     const float4 *rp = tiled + ((r >> 6) * nchunks) * 64 + (r & 63);
-    out[r] = wrap_metric(metric, row_dot_or_l2_generic<METRIC, 64>(rp, q4, (int)dim));
+    out[r] = wrap_metric(metric, row_dist<METRIC, 64>(rp, q4, (int)dim, o512));
 }
 
 hipError_t launch_distance_rows(int metric, const float *q, const float *tiled, uint64_t n, uint32_t dim,
-                                float *out, hipStream_t s)
+                                float *out, hipStream_t s, int o512)
 {
     if (n == 0) return hipSuccess;
     const uint32_t nchunks = f32_chunks(dim);
@@ -790,36 +794,36 @@ hipError_t launch_distance_rows(int metric, const float *q, const float *tiled, 
     if (metric == WVG_M_L2)
         hipLaunchKernelGGL((distance_tiled_kernel<WVG_M_L2>), grid, block, 0, s, metric,
                            reinterpret_cast<const float4 *>(q), reinterpret_cast<const float4 *>(tiled), n, dim,
-                           nchunks, out);
+                           nchunks, out, o512);
     else
         hipLaunchKernelGGL((distance_tiled_kernel<WVG_M_DOT>), grid, block, 0, s, metric,
                            reinterpret_cast<const float4 *>(q), reinterpret_cast<const float4 *>(tiled), n, dim,
-                           nchunks, out);
+                           nchunks, out, o512);
     return hipGetLastError();
 }
 
 template <int METRIC>
 __global__ void dist_keys_kernel(int metric, const float4 *q4, const float4 *tiled, uint64_t n, uint32_t dim,
-                                 uint32_t nchunks, uint64_t *keys)
+                                 uint32_t nchunks, uint64_t *keys, int o512)
 {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
     const float4 *rp = tiled + ((r >> 6) * nchunks) * 64 + (r & 63);
-    keys[r] = wvg_make_key(wrap_metric(metric, row_dot_or_l2_generic<METRIC, 64>(rp, q4, (int)dim)), (uint32_t)r);
+    keys[r] = wvg_make_key(wrap_metric(metric, row_dist<METRIC, 64>(rp, q4, (int)dim, o512)), (uint32_t)r);
 }
 
 hipError_t launch_dist_keys(int metric, const float *q, const float *tiled, uint64_t n, uint32_t dim, uint64_t *keys,
-                            hipStream_t s)
+                            hipStream_t s, int o512)
 {
     if (n == 0) return hipSuccess;
     const uint32_t nchunks = f32_chunks(dim);
     dim3 grid((unsigned)((n + 255) / 256)), block(256);
     if (metric == WVG_M_L2)
         hipLaunchKernelGGL((dist_keys_kernel<WVG_M_L2>), grid, block, 0, s, metric, reinterpret_cast<const float4 *>(q),
-                           reinterpret_cast<const float4 *>(tiled), n, dim, nchunks, keys);
+                           reinterpret_cast<const float4 *>(tiled), n, dim, nchunks, keys, o512);
     else
         hipLaunchKernelGGL((dist_keys_kernel<WVG_M_DOT>), grid, block, 0, s, metric, reinterpret_cast<const float4 *>(q),
-                           reinterpret_cast<const float4 *>(tiled), n, dim, nchunks, keys);
+                           reinterpret_cast<const float4 *>(tiled), n, dim, nchunks, keys, o512);
     return hipGetLastError();
 }
 
@@ -863,7 +867,7 @@ hipError_t launch_synth_rows(uint64_t seed, int dist, const uint64_t *ids, uint6
 template <int METRIC>
 __global__ void rescore_keys_kernel(int metric, const float4 *q4, uint32_t qpitch, const float4 *tiled, uint32_t dim,
                                     uint32_t nchunks, const uint64_t *cand, uint32_t ncand, uint32_t cand_stride,
-                                    uint64_t *out)
+                                    uint64_t *out, int o512)
 {
     const uint32_t qi = blockIdx.y;
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -874,7 +878,7 @@ __global__ void rescore_keys_kernel(int metric, const float4 *q4, uint32_t qpitc
         const uint32_t slot = (uint32_t)key;
         const float4 *rp = tiled + ((size_t)(slot >> 6) * nchunks) * 64 + (slot & 63);
         const float4 *q = q4 + (size_t)qi * (qpitch / 4);
-        const float d = wrap_metric(metric, row_dot_or_l2_generic<METRIC, 64>(rp, q, (int)dim));
+        const float d = wrap_metric(metric, row_dist<METRIC, 64>(rp, q, (int)dim, o512));
         res = wvg_make_key(d, slot);
     }
     out[(size_t)qi * ncand + j] = res;
@@ -882,18 +886,18 @@ __global__ void rescore_keys_kernel(int metric, const float4 *q4, uint32_t qpitc
 
 hipError_t launch_rescore_keys(int metric, const float *q, uint32_t qpitch, const float *tiled, uint32_t dim,
                                uint32_t nchunks, const uint64_t *cand_keys, uint32_t nq, uint32_t ncand,
-                               uint32_t cand_stride, uint64_t *out_keys, hipStream_t s)
+                               uint32_t cand_stride, uint64_t *out_keys, hipStream_t s, int o512)
 {
     if (nq == 0 || ncand == 0) return hipSuccess;
     dim3 grid((ncand + 63) / 64, nq), block(64);
     if (metric == WVG_M_L2)
         hipLaunchKernelGGL((rescore_keys_kernel<WVG_M_L2>), grid, block, 0, s, metric,
                            reinterpret_cast<const float4 *>(q), qpitch, reinterpret_cast<const float4 *>(tiled), dim,
-                           nchunks, cand_keys, ncand, cand_stride, out_keys);
+                           nchunks, cand_keys, ncand, cand_stride, out_keys, o512);
     else
         hipLaunchKernelGGL((rescore_keys_kernel<WVG_M_DOT>), grid, block, 0, s, metric,
                            reinterpret_cast<const float4 *>(q), qpitch, reinterpret_cast<const float4 *>(tiled), dim,
-                           nchunks, cand_keys, ncand, cand_stride, out_keys);
+                           nchunks, cand_keys, ncand, cand_stride, out_keys, o512);
     return hipGetLastError();
 }
 

@@ -58,7 +58,7 @@ __global__ __launch_bounds__(256) void ordkeys_f32_kernel(ScanArgs a, uint32_t *
         uint32_t key = ORD_NONE;
         if ((m >> lane) & 1ull) {
             const float4 *rp = data + (size_t)t * a.nchunks * 64 + lane;
-            key = wvg_ord_f32(wrap_metric(a.metric, row_dot_or_l2_generic<METRIC, 64>(rp, q4, (int)a.dim)));
+            key = wvg_ord_f32(wrap_metric(a.metric, row_dist<METRIC, 64>(rp, q4, (int)a.dim, a.order512)));
         }
         keys[i * 64 + lane] = key;
     }
@@ -365,8 +365,8 @@ __global__ void dist_by_ids_kernel(ScanArgs a, uint64_t capacity, const uint64_t
         const uint64_t t = slot >> 6, lane = slot & 63;
         if constexpr (KIND == WVG_KIND_F32) {
             const float4 *rp = reinterpret_cast<const float4 *>(a.data) + (size_t)t * a.nchunks * 64 + lane;
-            d = wrap_metric(a.metric, row_dot_or_l2_generic<METRIC, 64>(rp, reinterpret_cast<const float4 *>(a.queries),
-                                                                        (int)a.dim));
+            d = wrap_metric(a.metric, row_dist<METRIC, 64>(rp, reinterpret_cast<const float4 *>(a.queries),
+                                                           (int)a.dim, a.order512));
         } else if constexpr (KIND == WVG_KIND_BQ) {
             const ulonglong2 *rp = reinterpret_cast<const ulonglong2 *>(a.data) + (size_t)t * a.nchunks * 64 + lane;
             const uint64_t *q = reinterpret_cast<const uint64_t *>(a.queries);

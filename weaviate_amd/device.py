@@ -39,6 +39,11 @@ class Context:
     def synchronize(self) -> None:
         check(self.lib.wvg_synchronize(self.handle))
 
+    def set_distance_order(self, order: int) -> None:
+        """wvg_set_distance_order: _lib.ORDER_AVX256 (default) or ORDER_AVX512
+        (the kernels Weaviate dispatches on AMX + AVX-512 hosts)."""
+        check(self.lib.wvg_set_distance_order(self.handle, order))
+
     def __enter__(self):
         return self
 
