@@ -181,7 +181,10 @@ int wvg_search_by_distance_window(wvg_corpus *c, const float *query, float targe
  * hipGraph.  Queries must already be normalized for cosine.  One workspace
  * serves any number of calls issued in order on one stream.  An empty corpus
  * (e.g. a rank whose slab holds no rows) yields empty results: ids
- * UINT64_MAX, dists +inf, counts 0 (as wvg_search).                        */
+ * UINT64_MAX, dists +inf, counts 0 (as wvg_search).  wvg_search_device
+ * takes F32, BQ and PQ corpora (d_queries: float [nq][dim]; BQ codes and PQ
+ * LUTs are built on the device -- size the workspace after the PQ codebook
+ * is set); wvg_search_device_pipelined takes F32 corpora.                  */
 size_t wvg_search_workspace_size(wvg_corpus *c, uint32_t nq, uint32_t k);
 int wvg_search_device(wvg_corpus *c, const float *d_queries, uint32_t nq, uint32_t k,
                       uint64_t *d_ids, float *d_dists, uint32_t *d_counts, void *d_workspace,

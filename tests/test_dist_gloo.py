@@ -128,3 +128,37 @@ def test_shard_range_partitions_exactly():
                     prev_end = lo + cnt
                 covered += cnt
             assert covered == n
+
+
+def _bcast_worker(rank, world, port, out):
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from weaviate_amd.shard import broadcast_codebook
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    centers = np.random.default_rng(5).standard_normal((32, 256, 4)).astype(np.float32) if rank == 1 else None
+    cb = broadcast_codebook(centers, src=1)
+    out.put((rank, cb))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_codebook_broadcast():
+    """The PQ codebook of the source rank reaches every rank bit for bit (shape included)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bcast_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    want = np.random.default_rng(5).standard_normal((32, 256, 4)).astype(np.float32)
+    for r in range(world):
+        assert got[r].shape == (32, 256, 4) and np.array_equal(got[r].view(np.uint32), want.view(np.uint32))

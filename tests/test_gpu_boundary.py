@@ -88,3 +88,52 @@ def test_distance_by_ids(ctx, orc, kind):
         want = np.array([orc.pq_adc(1, lut, codes[i]) for i in sl], np.float32)
     assert np.array_equal(bits(dists[ok]), bits(want))
     assert np.all(dists[~ok] == 0)
+
+
+@pytest.mark.parametrize("kind,metric,d", [(KIND_BQ, METRIC_COSINE, 200), (KIND_BQ, METRIC_DOT, 1536),
+                                           (KIND_PQ, METRIC_L2, 128), (KIND_PQ, METRIC_DOT, 96)])
+def test_search_device_bq_pq_equals_host_search(ctx, orc, kind, metric, d):
+    """wvg_search_device on BQ / PQ corpora (codes / LUTs built on the device
+    from float device queries) == wvg_search with the same (normalized)
+    queries, and == the oracle; an empty corpus gives empty results."""
+    import torch
+
+    lib = _lib.load()
+    n, nq, k = 5000 + 3, 6, 10
+    rows = orc.synth_rows(1200 + d, 0, n, d, 0)
+    qs = orc.synth_rows(1201 + d, 0, nq, d, 0)
+    if metric == METRIC_COSINE:
+        qs = np.stack([orc.normalize(q) for q in qs])
+    c = Corpus(ctx, kind, metric, d, n)
+    if kind == KIND_PQ:
+        m = 32 if d % 32 == 0 else 24
+        centers = orc.synth_rows(1202 + d, 0, m * 256, d // m, 0).reshape(m, 256, d // m)
+        c.set_codebook(centers)
+    c.upsert(np.arange(n, dtype=np.uint64), rows)
+    c.delete(np.array([7, 64, 4000], np.uint64))
+    hid, hd, hc = c.search(qs, k)
+    dev = torch.device("cuda:0")
+    ws = torch.zeros(lib.wvg_search_workspace_size(c.handle, nq, k), dtype=torch.uint8, device=dev)
+    tq = torch.from_numpy(qs).to(dev)
+    oi = torch.empty((nq, k), dtype=torch.int64, device=dev)
+    od = torch.empty((nq, k), dtype=torch.float32, device=dev)
+    oc = torch.empty(nq, dtype=torch.int32, device=dev)
+    _lib.check(lib.wvg_search_device(c.handle, tq.data_ptr(), nq, k, oi.data_ptr(), od.data_ptr(), oc.data_ptr(),
+                                     ws.data_ptr(), ws.numel(), torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    assert np.array_equal(oi.cpu().numpy().view(np.uint64), hid)
+    assert np.array_equal(bits(od.cpu().numpy()), bits(hd))
+    assert np.array_equal(oc.cpu().numpy(), hc.astype(np.int32))
+    valid = np.ones(n, bool)
+    valid[[7, 64, 4000]] = False
+    codes = np.stack([orc.bq_encode(r) for r in rows]) if kind == KIND_BQ else orc.pq_encode(rows, centers)
+    for qi in range(nq):
+        if kind == KIND_BQ:
+            all_d = orc.bq_dist_all(orc.bq_encode(qs[qi]), codes)
+        else:
+            om = {METRIC_L2: 0, METRIC_DOT: 1}[metric]
+            lut = orc.pq_lut(om, qs[qi], centers)
+            all_d = np.array([orc.pq_adc(om, lut, cd) for cd in codes], np.float32)
+        wi, wd = orc.lex_topk(all_d[valid], np.arange(n, dtype=np.uint64)[valid], k)
+        assert np.array_equal(hid[qi], wi) and np.array_equal(bits(hd[qi]), bits(wd))
+    c.destroy()

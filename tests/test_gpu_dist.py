@@ -99,3 +99,93 @@ def test_two_ranks_packed_allgather_device_merge(orc, n, pipelined):
             assert np.array_equal(ids[qi][:len(wi)], wi)
             assert np.array_equal(dists[qi][:len(wi)].view(np.uint32), wd.view(np.uint32))
             assert np.all(ids[qi][len(wi):] == np.iinfo(np.uint64).max)
+
+
+def _pq_worker(rank, world, port, n, d, m, ks, k, nq, out):
+    try:
+        _pq_worker_body(rank, world, port, n, d, m, ks, k, nq, out)
+    except BaseException as e:  # report instead of leaving the parent waiting on the queue
+        import traceback
+
+        out.put((rank, "error", traceback.format_exc()))
+        raise
+
+
+def _pq_worker_body(rank, world, port, n, d, m, ks, k, nq, out):
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.init()
+    from weaviate_amd import _lib
+    from weaviate_amd._lib import KIND_F32, KIND_PQ, METRIC_L2
+    from weaviate_amd.device import Context, Corpus
+    from weaviate_amd.shard import ShardedFlatIndex, compress_slab, shard_range
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lo, cnt, per = shard_range(n, world, rank)
+        ctx = Context(0)
+        f = Corpus(ctx, KIND_F32, METRIC_L2, d, cnt, id_base=lo)
+        f.fill_synthetic(52, cnt, 0)
+        centers = None
+        if rank == 0:  # rank 0 trains on its own slab (KMeans.Fit on the device)
+            rows0 = f.get_batch(np.arange(lo, lo + cnt, dtype=np.uint64))[0]
+            centers = np.empty((m, ks, d // m), np.float32)
+            passes = np.zeros(m, np.uint32)  # [m] Lloyd passes per segment
+            _lib.check(ctx.lib.wvg_pq_fit(ctx.handle, _lib.fptr(rows0), cnt, d, m, ks, 0, 7, _lib.fptr(centers),
+                                          _lib.u32ptr(passes)))
+        pq = Corpus(ctx, KIND_PQ, METRIC_L2, d, cnt, id_base=lo)
+        cb = compress_slab(pq, f, centers)
+        rng = np.random.default_rng(53)
+        qs = torch.from_numpy(rng.uniform(-1, 1, (nq, d)).astype(np.float32)).cuda()
+        ids, dists, counts = ShardedFlatIndex(ctx, pq).search_device(qs, k)
+        torch.cuda.synchronize()
+        codes = pq.get_batch(np.arange(lo, lo + cnt, dtype=np.uint64), pq_m=m)[0]
+        out.put((rank, cb, codes, ids.cpu().numpy().view(np.uint64).copy(), dists.cpu().numpy().copy(),
+                 counts.cpu().numpy().copy()))
+        pq.destroy()
+        f.destroy()
+        ctx.close()
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def test_two_ranks_pq_codebook_broadcast_encode_search(orc):
+    """Config 4 sharded: rank 0 fits the codebook, one broadcast,
+    every rank encodes its slab on the GPU, then the sharded ADC search with
+    the packed all-gather + device merge equals the single-corpus oracle."""
+    world, n, d, m, ks, k, nq = 2, 6000 + 17, 32, 8, 32, 10, 4
+    ctxm = mp.get_context("spawn")
+    q = ctxm.Queue()
+    port = _free_port()
+    procs = [ctxm.Process(target=_pq_worker, args=(r, world, port, n, d, m, ks, k, nq, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(world):
+        v = q.get(timeout=240)
+        assert not (len(v) == 3 and v[1] == "error"), v[2]
+        got[v[0]] = v[1:]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    cb = got[0][0]
+    assert np.array_equal(got[1][0].view(np.uint32), cb.view(np.uint32))  # the same codebook on every rank
+    rows = orc.synth_rows(52, 0, n, d, 0)
+    codes = orc.pq_encode(rows, cb)
+    assert np.array_equal(np.concatenate([got[0][1], got[1][1]]), codes)  # each slab encoded on its own GPU
+    qs = np.random.default_rng(53).uniform(-1, 1, (nq, d)).astype(np.float32)
+    for r in range(world):
+        ids, dists, counts = got[r][2:]
+        for qi in range(nq):
+            lut = orc.pq_lut(0, qs[qi], cb)
+            all_d = np.array([orc.pq_adc(0, lut, c) for c in codes], np.float32)
+            wi, wd = orc.lex_topk(all_d, np.arange(n, dtype=np.uint64), k)
+            assert counts[qi] == k and np.array_equal(ids[qi], wi)
+            assert np.array_equal(dists[qi].view(np.uint32), wd.view(np.uint32))

@@ -572,3 +572,55 @@ def test_batched_mfma_variants(ctx, orc, variant, metric, d):
         lib.wvgx_set_tuning(4, old)
 
 
+
+@pytest.mark.parametrize("range_tiles", [-1, 0, 7])
+@pytest.mark.parametrize("variant", [0, 2])
+def test_batched_mfma_nonfinite_zero_and_ranges(ctx, orc, variant, range_tiles):
+    """K3b's float-distance rejection (!(dist > tau) before any key is built)
+    against the oracle on rows that give NaN, +-inf, -0.0 and +0.0 dot
+    products and exact ties; range_tiles 7: many short row ranges per query
+    block (tuning key 10), so lists restart often and the K2 merge sees
+    hundreds of partial lists."""
+    import ctypes
+
+    def check_lex(orc, ids, dists, count, all_d, k, valid):  # NaN sorts last (no heap comparison with NaN rows)
+        sel = valid.astype(bool)
+        li, ld = orc.lex_topk(all_d[sel], np.arange(len(all_d), dtype=np.uint64)[sel], k)
+        assert count == len(li) and np.array_equal(ids[:count], li)
+        assert np.array_equal(bits(dists[:count]), bits(ld))
+
+    lib = _lib.load()
+    lib.wvgx_set_tuning.restype = ctypes.c_int
+    lib.wvgx_set_tuning.argtypes = [ctypes.c_int, ctypes.c_int]
+    old4 = lib.wvgx_set_tuning(4, variant)
+    old10 = lib.wvgx_set_tuning(10, range_tiles)
+    try:
+        n, nq, d = 6000 + 13, 48, 256
+        rows = np.floor(orc.synth_rows(900, 0, n, d, 0) * 2).astype(np.float32)
+        qs = np.floor(orc.synth_rows(901, 0, nq, d, 0) * 2).astype(np.float32)
+        rows[100, 5] = np.nan
+        rows[200, 7] = np.inf
+        rows[300, 9] = -np.inf
+        rows[[400, 401, 5000]] = 0.0        # dot = +0 -> dist -0 under DOT
+        rows[402] = -0.0
+        rows[[403, 404]] = rows[405]        # exact ties
+        qs[3, 5] = 0.0
+        c = Corpus(ctx, KIND_F32, METRIC_DOT, d, n)
+        c.upsert(np.arange(n, dtype=np.uint64), rows)
+        valid = np.ones(n, np.uint8)
+        c.delete(np.array([64, 3000], np.uint64))
+        valid[[64, 3000]] = 0
+        for k in (1, 10, 64):
+            ids, dists, counts = c.search(qs, k)
+            for qi in range(nq):
+                all_d = orc.dist_all(1, qs[qi], rows)
+                check_lex(orc, ids[qi], dists[qi], counts[qi], all_d, k, valid)
+        # large-positive query: NaN / -inf rows rank first and last
+        q = np.full((40, d), 1.0, np.float32)
+        ids, dists, counts = c.search(q, 10)
+        all_d = orc.dist_all(1, q[0], rows)
+        check_lex(orc, ids[0], dists[0], counts[0], all_d, 10, valid)
+        c.destroy()
+    finally:
+        lib.wvgx_set_tuning(4, old4)
+        lib.wvgx_set_tuning(10, old10)

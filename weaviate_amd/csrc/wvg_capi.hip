@@ -912,10 +912,11 @@ struct SearchPlan {
     const uint64_t *allow_host = nullptr;  // the caller's allow words of tiles [tb, te), or null
     size_t allow_bytes() const { return allow_host ? (size_t)(te - tb) * 8 : 0; }
     size_t partial_keys(uint32_t nq, uint32_t k) const { return (size_t)nq * groups * k; }
-    // K3b's per-row-range progress counters follow the partial lists (gemm only)
+    // K3b's per-row-range progress counters, then its per-query distance
+    // bounds, follow the partial lists (gemm only)
     size_t workspace_bytes(uint32_t nq, uint32_t k) const
     {
-        return partial_keys(nq, k) * 8 + (gemm ? (size_t)groups * ((nq + 15) / 16) * 4 + 256 : 0);
+        return partial_keys(nq, k) * 8 + (gemm ? (size_t)groups * ((nq + 15) / 16) * 4 + (size_t)nq * 4 + 256 : 0);
     }
 };
 
@@ -968,9 +969,11 @@ static int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t 
     if (!p.gemm) a.reverse = next_direction(c, 1);
     ProfArm arm(c->ctx);
     if (arm.rc) return arm.rc;
-    if (p.gemm)
-        WVG_HIP(launch_gemm_topk(a, (uint32_t)p.groups, partials,
-                                 reinterpret_cast<uint32_t *>(partials + (size_t)nq * p.groups * k), c->ctx->num_cus, s));
+    if (p.gemm) {
+        uint32_t *prog = reinterpret_cast<uint32_t *>(partials + (size_t)nq * p.groups * k);
+        WVG_HIP(launch_gemm_topk(a, (uint32_t)p.groups, partials, prog, prog + (size_t)p.groups * ((nq + 15) / 16),
+                                 c->ctx->num_cus, s));
+    }
     else
         WVG_HIP(launch_scan(a, c->kind, partials, p.groups, s));
     WVG_HIP(launch_merge_lists(partials, nq, (uint32_t)p.groups, k, k, c->id_base, ids, dists, counts, s));
@@ -1012,6 +1015,18 @@ static int stage_queries(wvg_corpus *c, StreamSlot *sl, const float *queries, ui
     WVG_HIP(hipStreamSynchronize(s));
     qpitch = c->pq_m * c->pq_ks;
     return WVG_OK;
+}
+
+// wvg_search_device's prepared queries after the partial lists: PQ LUTs, or
+// BQ codes at the scan's pitch plus the encoder's dense output.
+static size_t device_query_bytes(const wvg_corpus *c, uint32_t nq)
+{
+    switch (c->kind) {
+    case WVG_KIND_PQ: return align_up((size_t)nq * c->pq_m * c->pq_ks * 4, 256);
+    case WVG_KIND_BQ:
+        return align_up((size_t)nq * bq_chunks(c->dim) * 16, 256) + align_up((size_t)nq * bq_words(c->dim) * 8, 256);
+    default: return 0;
+    }
 }
 
 static size_t query_bytes(const wvg_corpus *c, uint32_t nq)
@@ -1552,10 +1567,12 @@ size_t wvg_search_workspace_size(wvg_corpus *c, uint32_t nq, uint32_t k)
     if (!c) return 0;
     const uint32_t kk = std::max<uint32_t>(k, 1);
     SearchPlan p = plan_search(c, nq, k, nullptr, 0);
+    const size_t dev = WS_STATUS_BYTES + align_up(p.workspace_bytes(nq, kk), 256) + device_query_bytes(c, nq);
+    if (c->kind != WVG_KIND_F32) return dev;  // no pipelined mode
     SearchPlan p1 = plan_search(c, 1, k, nullptr, 0);  // pipelined: two single-query buffers, or the stream layout
     const size_t chain = 2 * align_up(p1.workspace_bytes(1, kk), 256);
     const size_t stream = stream_layout(p1, nq, kk).total;
-    return std::max({WS_STATUS_BYTES + align_up(p.workspace_bytes(nq, kk), 256), WS_STATUS_BYTES + chain, stream});
+    return std::max({dev, WS_STATUS_BYTES + chain, stream});
 }
 
 int wvg_search_device_check(wvg_ctx *ctx, void *d_workspace, void *stream)
@@ -1666,8 +1683,9 @@ int wvg_search_device(wvg_corpus *c, const float *d_queries, uint32_t nq, uint32
 {
     if (!c) return fail(WVG_ERR_INVALID, "null corpus");
     if (k > MAX_K) return fail(WVG_ERR_UNSUPPORTED, "k above 256 is not supported by the fused top-k");
-    if (c->kind != WVG_KIND_F32) return fail(WVG_ERR_UNSUPPORTED, "device search supports F32 corpora");
-    if (c->dim % 4 != 0) return fail(WVG_ERR_UNSUPPORTED, "device search needs dim % 4 == 0");
+    if (c->kind == WVG_KIND_F32 && c->dim % 4 != 0)
+        return fail(WVG_ERR_UNSUPPORTED, "device search needs dim % 4 == 0");
+    if (c->kind == WVG_KIND_PQ && !c->d_centers) return fail(WVG_ERR_INVALID, "PQ corpus has no codebook");
     if (nq == 0 || k == 0) return WVG_OK;
     hipStream_t s = (hipStream_t)stream;
     std::shared_lock<std::shared_mutex> lk(c->rw);
@@ -1676,10 +1694,26 @@ int wvg_search_device(wvg_corpus *c, const float *d_queries, uint32_t nq, uint32
         WVG_HIP(launch_fill_empty(d_ids, d_dists, d_counts, nq, k, s));
         return WVG_OK;
     }
-    if (!d_workspace || workspace_bytes < WS_STATUS_BYTES + p.workspace_bytes(nq, k))
+    const size_t part = align_up(p.workspace_bytes(nq, k), 256);
+    if (!d_workspace || workspace_bytes < WS_STATUS_BYTES + part + device_query_bytes(c, nq))
         return fail(WVG_ERR_INVALID, "workspace too small");
-    return run_search(c, d_queries, c->dim, nq, k, nullptr, p, (uint64_t *)((char *)d_workspace + WS_STATUS_BYTES),
-                      d_ids, d_dists, d_counts, s);
+    uint64_t *partials = (uint64_t *)((char *)d_workspace + WS_STATUS_BYTES);
+    char *qbuf = (char *)d_workspace + WS_STATUS_BYTES + part;
+    if (c->kind == WVG_KIND_PQ) {  // the queries' LUTs on the device (CH/product_quantization.go:329-337)
+        WVG_HIP(launch_pq_lut(c->metric, d_queries, nq, c->dim, c->d_centers, c->pq_m, c->pq_ks, c->pq_ds,
+                              (float *)qbuf, s));
+        return run_search(c, qbuf, c->pq_m * c->pq_ks, nq, k, nullptr, p, partials, d_ids, d_dists, d_counts, s);
+    }
+    if (c->kind == WVG_KIND_BQ) {  // sign bits (CH/binary_quantization.go:32-45) at the scan's query pitch
+        const uint32_t words = bq_words(c->dim), qpitch = bq_chunks(c->dim) * 2;
+        uint64_t *codes = (uint64_t *)(qbuf + align_up((size_t)nq * qpitch * 8, 256));
+        WVG_HIP(launch_bq_encode_rows(d_queries, nq, c->dim, 0, codes, s));
+        WVG_HIP(hipMemsetAsync(qbuf, 0, (size_t)nq * qpitch * 8, s));
+        WVG_HIP(hipMemcpy2DAsync(qbuf, (size_t)qpitch * 8, codes, (size_t)words * 8, (size_t)words * 8, nq,
+                                 hipMemcpyDeviceToDevice, s));
+        return run_search(c, qbuf, qpitch, nq, k, nullptr, p, partials, d_ids, d_dists, d_counts, s);
+    }
+    return run_search(c, d_queries, c->dim, nq, k, nullptr, p, partials, d_ids, d_dists, d_counts, s);
 }
 
 int wvg_topk_merge_device(wvg_ctx *ctx, const float *d_dists, const uint64_t *d_ids, uint32_t nq, uint32_t nlists,
@@ -1819,7 +1853,7 @@ int wvg_synthetic_rows(wvg_ctx *ctx, uint64_t seed, const uint64_t *ids, uint64_
 
 // Internal A/B knob (not part of include/wvgpu.h): 0 = K1 scan variant,
 // 1 = K1 resident workgroups per CU, ... 7 = K8 ADC variant, 8 = query-stream merge wait (us),
-// 9 = serpentine scan order.  Returns the previous value.
+// 9 = serpentine scan order, 10 = K3b row-range length.  Returns the previous value.
 int wvgx_set_tuning(int key, int value)
 {
     Tuning &t = tuning();
@@ -1854,6 +1888,9 @@ int wvgx_set_tuning(int key, int value)
     } else if (key == 9) {
         old = t.serpentine;
         t.serpentine = value;
+    } else if (key == 10) {
+        old = t.gemm_range_tiles;
+        t.gemm_range_tiles = value;
     }
     return old;
 }

@@ -53,6 +53,7 @@ struct GemmArgs {
     int skew;               // K3b: start delay of query half 1 (units of s_sleep(8))
     uint32_t *prog;         // K3b: [nrr][nqb] tiles done per workgroup (null: no lockstep)
     uint32_t lag;           // K3b: allowed lead over the group's slowest workgroup, in tiles
+    uint32_t *gbound;       // K3b: [nq] ordered distance of a finished workgroup's k-th key (min over them)
 };
 
 // PF = chunks of prefetch in registers (2: 48 staging VGPRs; E > 1 top-k
@@ -307,7 +308,7 @@ __global__ __launch_bounds__(GWAVES * 64) void gemm_topk_kernel(GemmArgs a, uint
 // tree as K3, so the distances are the same bits.
 // ---------------------------------------------------------------------------
 constexpr int RS_RG = 4;     // row groups of 16 per 64-row tile
-constexpr uint32_t RS_SYNC = 1;  // lockstep check every RS_SYNC tiles
+constexpr uint32_t RS_SYNC = 1;  // lockstep check at least every RS_SYNC tiles
 
 // QH query halves x 4 row groups = 4*QH waves; wave (qg, rg) scores rows
 // 16*rg..16*rg+15 of every tile against queries qg*16*QT .. +16*QT.
@@ -327,6 +328,8 @@ __global__ __launch_bounds__(RS_RG * QH * 64, 1) void gemm_rs_kernel(GemmArgs a,
     uint64_t *lists = reinterpret_cast<uint64_t *>(smem4 + QB * QROW);  // [NW][QW][K]
     uint64_t *thr = lists + NW * QW * K;                                 // [NW][QW]
     uint64_t *tmp = thr + NW * QW;                                       // [NW][64]
+    float *thrf = reinterpret_cast<float *>(tmp + NW * 64);              // [NW][QW]: rejection distance
+    uint32_t *gord = reinterpret_cast<uint32_t *>(thrf + NW * QW);       // [NW][QW]: bound read at start
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -354,7 +357,17 @@ __global__ __launch_bounds__(RS_RG * QH * 64, 1) void gemm_rs_kernel(GemmArgs a,
         qs[i * QROW + bk * 8 + (cc ^ (i & 7))] = v;
     }
     for (int idx = tid; idx < NW * QW * K; idx += NW * 64) lists[idx] = WVG_KEY_NONE;
-    for (int idx = tid; idx < NW * QW; idx += NW * 64) thr[idx] = WVG_KEY_NONE;
+    // Cross-workgroup bound: a workgroup that finished a row range published,
+    // per query, the ordered distance of its k-th key -- k rows at or below
+    // it exist, so no row above it can be in the final top-k.  Read once at
+    // start (a stale value is a larger, still valid bound); 0xFFFFFFFF = none.
+    for (int idx = tid; idx < NW * QW; idx += NW * 64) {
+        const uint32_t q = q0 + (uint32_t)((idx / QW) / RS_RG * QW + idx % QW);
+        const uint32_t g = a.gbound && q < a.nq ? a.gbound[q] : 0xFFFFFFFFu;
+        thr[idx] = WVG_KEY_NONE;
+        gord[idx] = g;
+        thrf[idx] = wvg_unord_f32(g);  // no bound: a NaN, and !(dist > NaN) admits every row
+    }
     __syncthreads();
 
     const int kk = lane >> 4, j = lane & 15;
@@ -366,6 +379,15 @@ __global__ __launch_bounds__(RS_RG * QH * 64, 1) void gemm_rs_kernel(GemmArgs a,
     const uint32_t nch = a.nchunks;
     uint64_t *wl = lists + (size_t)wave * QW * K;
     uint64_t *wthr = thr + wave * QW;
+    float *wthrf = thrf + wave * QW;
+    const uint32_t *wgord = gord + wave * QW;
+    // lanes of query rows past nq, per (query tile, r): C row i = 4*(lane >> 4) + r
+    uint64_t qlive[QT][4];
+#pragma unroll
+    for (int tq = 0; tq < QT; tq++)
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+            qlive[tq][r] = __ballot(q0 + qg * QW + tq * 16 + (lane >> 4) * 4 + r < a.nq);
 
     auto tile_live = [&](uint64_t t) -> uint64_t {
         uint64_t m = sload64(a.valid + t);
@@ -398,7 +420,11 @@ __global__ __launch_bounds__(RS_RG * QH * 64, 1) void gemm_rs_kernel(GemmArgs a,
         if (lane < K - 1 && lane >= pos) L[lane + 1] = v;
         if (lane == pos) L[pos] = key;
         const uint64_t prev = K >= 2 ? __shfl(v, K - 2) : key;
-        if (lane == 0) wthr[qi] = pos <= K - 2 ? prev : key;
+        if (lane == 0) {
+            const uint64_t th = pos <= K - 2 ? prev : key;
+            wthr[qi] = th;
+            wthrf[qi] = wvg_unord_f32(min((uint32_t)(th >> 32), wgord[qi]));
+        }
     };
 
     floatx4 acc[QT][32];
@@ -448,7 +474,7 @@ __global__ __launch_bounds__(RS_RG * QH * 64, 1) void gemm_rs_kernel(GemmArgs a,
     // (D/c/dot_avx256_amd64.c:94-103) per output element; C layout: row j =
     // lane & 15, query 4*(lane >> 4) + r.  Straight-line VALU, so it can run
     // under the other query tile's MFMAs.
-    auto reduce_keys = [&](int tq, uint64_t t, uint64_t m, uint64_t (&keys)[4]) {
+    auto reduce_keys = [&](int tq, float (&dd)[4]) {
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             float sv[8];
@@ -461,20 +487,22 @@ __global__ __launch_bounds__(RS_RG * QH * 64, 1) void gemm_rs_kernel(GemmArgs a,
             const float lo = (sv[0] + sv[1]) + (sv[2] + sv[3]);
             const float hi = (sv[4] + sv[5]) + (sv[6] + sv[7]);
             const float dot = 0.0f + (lo + hi);
-            const float dist = a.metric == WVG_M_DOT ? -dot : 1.0f - dot;
-            const int qi = tq * 16 + (lane >> 4) * 4 + r;
-            keys[r] = ((m >> j) & 1ull) && q0 + qg * QW + qi < a.nq
-                          ? wvg_make_key(dist, (uint32_t)(t * 64 + 16 * rg + j))
-                          : WVG_KEY_NONE;
+            dd[r] = a.metric == WVG_M_DOT ? -dot : 1.0f - dot;
         }
     };
-    auto candidates = [&](int tq, const uint64_t (&keys)[4]) {
+    // Rejection on the float distance against the list's K-th distance
+    // (a superset test: !(dist > tau) also admits NaN rows, ties and -0 vs
+    // +0, and a NaN tau -- a list not yet full -- admits all); the 64-bit key
+    // is built only for the survivors, and insert() decides exactly.
+    auto candidates = [&](int tq, uint64_t t, uint64_t m, const float (&dd)[4]) {
+        const uint64_t m4 = m * 0x0001000100010001ull;  // the row group's 16 live bits, once per 16-lane group
 #pragma unroll
         for (int r = 0; r < 4; r++) {
-            const uint64_t key = keys[r];
             const int qi = tq * 16 + (lane >> 4) * 4 + r;
-            uint64_t pend = __ballot(key < wthr[qi]);
-            while (pend) {  // rare after the first tiles: wave-uniform insertions
+            uint64_t pend = __ballot(!(dd[r] > wthrf[qi])) & m4 & qlive[tq][r];
+            if (!pend) continue;  // rare after the first tiles: wave-uniform insertions
+            const uint64_t key = wvg_make_key(dd[r], (uint32_t)(t * 64 + 16 * rg + j));
+            while (pend) {
                 const int src = __builtin_ctzll(pend);
                 pend &= pend - 1;
                 const int qsrc = tq * 16 + (src >> 4) * 4 + r;
@@ -508,6 +536,7 @@ __global__ __launch_bounds__(RS_RG * QH * 64, 1) void gemm_rs_kernel(GemmArgs a,
     // that waits too long (a group member not resident) stops syncing.
     uint32_t tiles_done = 0;
     bool lockstep = a.prog != nullptr;
+    const uint32_t sync_every = a.lag / 4 > RS_SYNC ? a.lag / 4 : RS_SYNC;  // check a quarter of the lead
     uint32_t *grp = a.prog ? a.prog + (size_t)rr * a.nqb : nullptr;
     auto keep_pace = [&]() {
         if (wave == 0 && lane == 0)
@@ -542,24 +571,24 @@ __global__ __launch_bounds__(RS_RG * QH * 64, 1) void gemm_rs_kernel(GemmArgs a,
             const float4 (&bq)[8] = bb[g % NBUF];
             if constexpr (QT == 2) {
                 if (g == 0 && have_prev) {
-                    uint64_t kp[4];
+                    float kp[4];
                     mfma_half(0, g, bq);
-                    reduce_keys(1, t_prev, m_prev, kp);
+                    reduce_keys(1, kp);
                     pin_epi();
                     __builtin_amdgcn_sched_barrier(0);
-                    candidates(1, kp);
+                    candidates(1, t_prev, m_prev, kp);
                 } else {
                     mfma_half(0, g, bq);
                     pin_plain();
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 if (g == NK - 1) {
-                    uint64_t k0[4];
+                    float k0[4];
                     mfma_half(1, g, bq);
-                    reduce_keys(0, t, m_cur, k0);
+                    reduce_keys(0, k0);
                     pin_epi();
                     __builtin_amdgcn_sched_barrier(0);
-                    candidates(0, k0);
+                    candidates(0, t, m_cur, k0);
                 } else {
                     mfma_half(1, g, bq);
                     pin_plain();
@@ -577,9 +606,9 @@ __global__ __launch_bounds__(RS_RG * QH * 64, 1) void gemm_rs_kernel(GemmArgs a,
         if constexpr (QT != 2) {
 #pragma unroll
             for (int tq = 0; tq < QT; tq++) {
-                uint64_t kq[4];
-                reduce_keys(tq, t, m_cur, kq);
-                candidates(tq, kq);
+                float kq[4];
+                reduce_keys(tq, kq);
+                candidates(tq, t, m_cur, kq);
             }
         }
         have_prev = true;
@@ -587,15 +616,15 @@ __global__ __launch_bounds__(RS_RG * QH * 64, 1) void gemm_rs_kernel(GemmArgs a,
         m_prev = m_cur;
         t = tn;
         m_cur = m_nxt;
-        if (lockstep && (++tiles_done % RS_SYNC) == 0) keep_pace();
+        if (lockstep && (++tiles_done % sync_every) == 0) keep_pace();
     }
     if (a.prog && wave == 0 && lane == 0)  // done: never hold the group back
         __hip_atomic_store(grp + qb, 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if constexpr (QT == 2) {
         if (have_prev) {  // the last row tile's query tile 1
-            uint64_t kp[4];
-            reduce_keys(1, t_prev, m_prev, kp);
-            candidates(1, kp);
+            float kp[4];
+            reduce_keys(1, kp);
+            candidates(1, t_prev, m_prev, kp);
         }
     }
     __syncthreads();
@@ -621,6 +650,8 @@ __global__ __launch_bounds__(RS_RG * QH * 64, 1) void gemm_rs_kernel(GemmArgs a,
         for (int e = 0; e < RS_RG; e++)
             if (mine[e] != WVG_KEY_NONE && rank[e] < K) tw[rank[e]] = mine[e];
         if (lane < K) partials[((size_t)q * a.nrr + rr) * K + lane] = tw[lane];
+        if (a.gbound && lane == K - 1 && tw[lane] != WVG_KEY_NONE)  // publish this range's k-th distance
+            atomicMin(a.gbound + q, (uint32_t)(tw[lane] >> 32));
     }
 }
 
@@ -641,7 +672,7 @@ static bool rs_config(uint32_t dim, uint32_t k, RsConfig &c)
     c.qh = mode == 2 ? 1 : 2;
     for (;;) {  // shrink the query block until it fits LDS
         const size_t qw = 16 * (size_t)c.qt, nw = (size_t)RS_RG * c.qh, qb = qw * c.qh;
-        c.lds = qb * dim * 4 + nw * qw * k * 8 + nw * qw * 8 + nw * 64 * 8;
+        c.lds = qb * dim * 4 + nw * qw * k * 8 + nw * qw * 8 + nw * 64 * 8 + nw * qw * 8;
         if (c.lds <= 160 * 1024) return true;
         if (c.qh == 2)
             c.qh = 1;
@@ -666,14 +697,22 @@ uint32_t gemm_row_ranges(uint32_t nq, uint64_t ntiles, int num_cus, uint32_t dim
     const uint32_t qpb = gemm_queries_per_block(dim, k);
     const uint32_t nqb = (nq + qpb - 1) / qpb;
     uint64_t want = ((uint64_t)num_cus + nqb - 1) / nqb;  // about one workgroup per CU
+    // Short row ranges dispatched range-major: the nqb workgroups of one range
+    // start together on one XCD and stay within a few tiles of each other, so
+    // each row tile comes from HBM about once per XCD and from L2 for the rest;
+    // a long range per workgroup lets them drift apart (~1.1 TB of fabric reads
+    // per 10M x 768 batch instead of 0.2 TB).  The per-query bounds published by
+    // finished ranges keep the restarted top-k lists cheap.
+    const int rt = tuning().gemm_range_tiles == 0 ? 512 : tuning().gemm_range_tiles;
+    if (rt > 0) want = std::max<uint64_t>(want, (ntiles + rt - 1) / rt);
     want = (want + 7) / 8 * 8;
     if (want > ntiles) want = ntiles;
     if (want < 1) want = 1;
     return (uint32_t)want;
 }
 
-hipError_t launch_gemm_topk(const ScanArgs &s, uint32_t nrr, uint64_t *partials, uint32_t *prog, int num_cus,
-                            hipStream_t st)
+hipError_t launch_gemm_topk(const ScanArgs &s, uint32_t nrr, uint64_t *partials, uint32_t *prog, uint32_t *gbound,
+                            int num_cus, hipStream_t st)
 {
     GemmArgs a{};
     a.data = reinterpret_cast<const float4 *>(s.data);
@@ -702,6 +741,11 @@ hipError_t launch_gemm_topk(const ScanArgs &s, uint32_t nrr, uint64_t *partials,
         a.prog = prog && a.lag && a.nqb * a.nrr <= (uint32_t)num_cus ? prog : nullptr;
         if (a.prog) {
             hipError_t e = hipMemsetAsync(a.prog, 0, (size_t)a.nqb * a.nrr * 4, st);
+            if (e != hipSuccess) return e;
+        }
+        a.gbound = gbound;
+        if (a.gbound) {
+            hipError_t e = hipMemsetAsync(a.gbound, 0xFF, (size_t)s.nq * 4, st);
             if (e != hipSuccess) return e;
         }
         const uint32_t lds = (uint32_t)rc.lds;

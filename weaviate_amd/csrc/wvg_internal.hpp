@@ -219,9 +219,10 @@ hipError_t launch_scan_pq(const ScanArgs &a, uint64_t *partials, int groups, hip
 // K3 batched MFMA scoring (wvg_gemm.hip): partials [nq][nrr][K].
 bool gemm_supported(uint32_t dim, int metric);
 uint32_t gemm_row_ranges(uint32_t nq, uint64_t ntiles, int num_cus, uint32_t dim, uint32_t k);
-// prog: [nrr][query blocks] u32 workspace (zeroed here) for K3b's soft lockstep.
-hipError_t launch_gemm_topk(const ScanArgs &a, uint32_t nrr, uint64_t *partials, uint32_t *prog, int num_cus,
-                            hipStream_t s);
+// prog: [nrr][query blocks] u32 workspace (zeroed here) for K3b's soft lockstep;
+// gbound: [nq] u32 workspace (set to 0xFF.. here) for K3b's per-query distance bounds.
+hipError_t launch_gemm_topk(const ScanArgs &a, uint32_t nrr, uint64_t *partials, uint32_t *prog, uint32_t *gbound,
+                            int num_cus, hipStream_t s);
 // Internal tuning knobs (wvgx_set_tuning; A/B experiments, not public ABI).
 struct Tuning {
     int scan_variant = 0;    // K1 variant (see wvg_scan.hip)
@@ -238,6 +239,8 @@ struct Tuning {
                              // 1 = K8 gather in segment order everywhere
     int merge_wait_us = 0;   // query-stream merge workgroup's wait per query in us; 0 = 4 s (test knob)
     int serpentine = 1;      // alternate the scan direction between consecutive scans (0 = always upwards; A/B)
+    int gemm_range_tiles = 0;  // K3b row-range length in tiles: 0 = auto (512), > 0 = that many,
+                               // -1 = one long range per workgroup (one wave of workgroups; A/B)
 };
 Tuning &tuning();
 // Profiling: events armed by the host runtime (wvg_profile_start) are bound to

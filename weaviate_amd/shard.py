@@ -69,6 +69,40 @@ def all_gather_packed(send: torch.Tensor, recv: torch.Tensor, group=None) -> Non
         dist.all_gather_into_tensor(recv, send, group=group)
 
 
+def broadcast_codebook(centers, src: int = 0, group=None, device=None) -> np.ndarray:
+    """The PQ codebook fitted on rank `src` (ProductQuantizer.Fit,
+    CH/product_quantization.go:372-418) sent once to every rank of the group:
+    a 3-word shape header then the m*ks*ds float32 centres (32 KiB at m = 32,
+    ks = 256, ds = 4) -- two broadcasts per index, RCCL over xGMI with nccl.
+    `centers` [m][ks][ds] is read on `src` only; every rank returns the host
+    copy.  `device`: where the broadcast tensors live (a GPU for nccl; None =
+    host, for gloo)."""
+    rank = dist.get_rank(group)
+    dev = device if device is not None else torch.device("cpu")
+    hdr = torch.zeros(3, dtype=torch.int64, device=dev)
+    if rank == src:
+        c = np.ascontiguousarray(centers, np.float32)
+        if c.ndim != 3:
+            raise ValueError("centers must be [m][ks][ds]")
+        hdr.copy_(torch.tensor(c.shape, dtype=torch.int64))
+    dist.broadcast(hdr, src, group=group)
+    m, ks, ds = (int(v) for v in hdr.cpu().tolist())
+    buf = (torch.from_numpy(c).to(dev) if rank == src else torch.empty((m, ks, ds), dtype=torch.float32, device=dev))
+    dist.broadcast(buf, src, group=group)
+    return buf.cpu().numpy()
+
+
+def compress_slab(pq_corpus, f32_corpus, centers, src: int = 0, group=None, device=None) -> np.ndarray:
+    """Sharded PQ compression: the codebook of rank
+    `src` is broadcast once, then every rank encodes its own docID slab on its
+    GPU (wvg_pq_encode_corpus; V/hnsw/compress.go:98-104 restated per slab) --
+    no collective on the encode itself.  Returns the codebook every rank used."""
+    cb = broadcast_codebook(centers, src, group, device)
+    pq_corpus.set_codebook(cb)
+    check(pq_corpus.ctx.lib.wvg_pq_encode_corpus(pq_corpus.handle, f32_corpus.handle))
+    return cb
+
+
 @dataclass
 class _Buffers:
     ws: torch.Tensor      # search workspace (zero-filled once)
@@ -134,5 +168,5 @@ class ShardedFlatIndex:
             check(self.lib.wvg_search_device_check(self.ctx.handle, b.ws.data_ptr(), st))
 
 
-__all__ = ["shard_range", "packed_bytes", "pack_block", "unpack_blocks", "all_gather_packed", "ShardedFlatIndex",
-           "_lib"]
+__all__ = ["shard_range", "packed_bytes", "pack_block", "unpack_blocks", "all_gather_packed", "broadcast_codebook",
+           "compress_slab", "ShardedFlatIndex", "_lib"]
