@@ -59,6 +59,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target wall time of each multi-core CPU leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dry-run", action="store_true", help="CPU-only rehearsal of the N-rank launch + exchange")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearsal: all ranks on cuda:0 with a gloo exchange (one-GPU boxes; not a measurement)")
     a = ap.parse_args(argv)
     slab = a.workload == "slab1b"
     a.batch = a.batch or (8 if slab else 16)
@@ -214,26 +216,40 @@ def run_flat1m(args, world, rank, dev, torch, dist):
     qs = np.random.default_rng(43).uniform(-1, 1, (P, d)).astype(np.float32)
     tq = torch.from_numpy(qs).to(dev)
     blk = lib.wvg_topk_packed_bytes(B, k)
-    send = torch.empty(blk, dtype=torch.uint8, device=dev)  # ids [B][k] then dists [B][k]
+    # two of each exchange buffer: step s's exchange + merge overlaps step s+1's scan
+    send = [torch.empty(blk, dtype=torch.uint8, device=dev) for _ in range(2)]  # ids [B][k] then dists [B][k]
     counts = torch.empty(B, dtype=torch.int32, device=dev)
     ws_bytes = lib.wvg_search_workspace_size(corpus.handle, B, k)
     ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=dev)
-    recv = torch.empty(world * blk, dtype=torch.uint8, device=dev)
-    m_ids = torch.empty((B, k), dtype=torch.int64, device=dev)
-    m_d = torch.empty((B, k), dtype=torch.float32, device=dev)
-    m_c = torch.empty(B, dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    recv = [torch.empty(world * blk, dtype=torch.uint8, device=dev) for _ in range(2)]
+    m_ids = [torch.empty((B, k), dtype=torch.int64, device=dev) for _ in range(2)]
+    m_d = [torch.empty((B, k), dtype=torch.float32, device=dev) for _ in range(2)]
+    m_c = [torch.empty(B, dtype=torch.int32, device=dev) for _ in range(2)]
+    main_s = torch.cuda.current_stream(dev)
+    stream = main_s.cuda_stream
+    side = torch.cuda.Stream(dev) if world > 1 else None  # the exchange stream
+    scanned = [torch.cuda.Event() for _ in range(2)]
+    exchanged = [torch.cuda.Event() for _ in range(2)]
 
     def step(s):
         # B single-query scans in one call = one query-stream launch (each query a full scan)
         q0 = (s * B) % P
-        check(lib.wvg_search_device_pipelined(corpus.handle, tq[q0].data_ptr(), B, k, send.data_ptr(),
-                                              send.data_ptr() + B * k * 8, counts.data_ptr(), ws.data_ptr(),
+        b = s % 2
+        if world > 1 and s >= 2:
+            main_s.wait_event(exchanged[b])  # send[b] is free once step s-2's all-gather has read it
+        check(lib.wvg_search_device_pipelined(corpus.handle, tq[q0].data_ptr(), B, k, send[b].data_ptr(),
+                                              send[b].data_ptr() + B * k * 8, counts.data_ptr(), ws.data_ptr(),
                                               ws_bytes, stream))
         if world > 1:
-            all_gather_packed(send, recv)  # ONE collective per step
-            check(lib.wvg_topk_merge_packed(ctx.handle, recv.data_ptr(), B, world, k, k, m_ids.data_ptr(),
-                                            m_d.data_ptr(), m_c.data_ptr(), stream))
+            # ONE collective per step, on the exchange stream: RCCL moves step s's blocks and every
+            # rank merges them while this rank's next scan runs on the main stream
+            scanned[b].record(main_s)
+            with torch.cuda.stream(side):
+                side.wait_event(scanned[b])
+                all_gather_packed(send[b], recv[b])
+                check(lib.wvg_topk_merge_packed(ctx.handle, recv[b].data_ptr(), B, world, k, k, m_ids[b].data_ptr(),
+                                                m_d[b].data_ptr(), m_c[b].data_ptr(), side.cuda_stream))
+                exchanged[b].record(side)
 
     for s in range(args.warmup):
         step(s)
@@ -278,7 +294,8 @@ def run_flat1m(args, world, rank, dev, torch, dist):
                         "(BASELINE configs[0] shape on MI355X)",
             "rows_per_gpu": n, "dim": d, "k": k, "queries_per_step": B,
             "parallelism": f"shard rows by docID range over {world} GPU(s); one RCCL all-gather of packed "
-                           f"per-GPU top-k blocks per step + device merge",
+                           f"per-GPU top-k blocks per step + device merge, on a second stream overlapping "
+                           f"the next step's scan",
         },
         "roofline": {
             "bound": "hbm",
@@ -463,10 +480,15 @@ def main():
         import torch
         import torch.distributed as dist
 
+        if args.share_gpu:  # rehearsal on a one-GPU box: every rank on cuda:0, exchange over gloo
+            local = 0
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
         if world > 1:
-            dist.init_process_group("nccl", device_id=dev)
+            if args.share_gpu:
+                dist.init_process_group("gloo")
+            else:
+                dist.init_process_group("nccl", device_id=dev)
         fn = run_slab1b if args.workload == "slab1b" else run_flat1m
         out = fn(args, world, rank, dev, torch, dist)
         if world > 1:
