@@ -624,3 +624,45 @@ def test_batched_mfma_nonfinite_zero_and_ranges(ctx, orc, variant, range_tiles):
     finally:
         lib.wvgx_set_tuning(4, old4)
         lib.wvgx_set_tuning(10, old10)
+
+
+@pytest.mark.parametrize("policy", [1, 2])
+def test_flat_scan_load_policies(ctx, orc, policy):
+    """K1's row loads, non-temporal (1) or default-policy (2; tuning key 11 --
+    the library picks by scanned bytes), through the host search and the
+    query-stream device search: same bits as the oracle."""
+    import ctypes
+
+    import torch
+
+    lib = _lib.load()
+    lib.wvgx_set_tuning.restype = ctypes.c_int
+    lib.wvgx_set_tuning.argtypes = [ctypes.c_int, ctypes.c_int]
+    old = lib.wvgx_set_tuning(11, policy)
+    try:
+        n, d, k, nq = 20_000 + 7, 128, 10, 5
+        c = Corpus(ctx, KIND_F32, METRIC_L2, d, n)
+        c.fill_synthetic(71, n, 0)
+        c.delete(np.array([3, 640], np.uint64))
+        valid = np.ones(n, np.uint8)
+        valid[[3, 640]] = 0
+        rows = orc.synth_rows(71, 0, n, d, 0)
+        qs = orc.synth_rows(72, 0, nq, d, 0)
+        ids, dists, counts = c.search(qs, k)
+        dev = torch.device("cuda:0")
+        ws = torch.zeros(lib.wvg_search_workspace_size(c.handle, nq, k), dtype=torch.uint8, device=dev)
+        tq = torch.from_numpy(qs).to(dev)
+        oi = torch.empty((nq, k), dtype=torch.int64, device=dev)
+        od = torch.empty((nq, k), dtype=torch.float32, device=dev)
+        oc = torch.empty(nq, dtype=torch.int32, device=dev)
+        _lib.check(lib.wvg_search_device_pipelined(c.handle, tq.data_ptr(), nq, k, oi.data_ptr(), od.data_ptr(),
+                                                   oc.data_ptr(), ws.data_ptr(), ws.numel(),
+                                                   torch.cuda.current_stream().cuda_stream))
+        torch.cuda.synchronize()
+        assert np.array_equal(oi.cpu().numpy().view(np.uint64), ids)
+        for qi in range(nq):
+            all_d = orc.dist_all(orc.L2, qs[qi], rows)
+            check_topk(orc, ids[qi], dists[qi], counts[qi], all_d, np.arange(n, dtype=np.uint64), k, valid)
+        c.destroy()
+    finally:
+        lib.wvgx_set_tuning(11, old)

@@ -300,6 +300,7 @@ int wvg_open(int device, wvg_ctx **out)
     c->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     if (const char *e = getenv("WVG_MFMA_MIN_QUERIES")) c->mfma_min_nq = (uint32_t)strtoul(e, nullptr, 10);
     if (const char *e = getenv("WVG_SERPENTINE")) tuning().serpentine = (int)strtol(e, nullptr, 10);  // A/B runs
+    if (const char *e = getenv("WVG_K1_LOADS")) tuning().k1_loads = (int)strtol(e, nullptr, 10);        // A/B runs
     *out = c;
     return WVG_OK;
 }
@@ -904,6 +905,17 @@ static int pq_dense(const wvg_corpus *c, const uint64_t *d_allow)
     return !d_allow && c->count * 4 >= c->high_water * 3;
 }
 
+// K1 row loads: non-temporal for scans far past the 256 MiB Infinity Cache,
+// the default policy up to 800 MiB of scanned rows, where consecutive scans
+// of the same rows find part of them in the cache (1M x 128 = 512 MB: 4 %
+// faster; 2M x 128: 2 % slower; profiles/r02/bench/load_policy_ab.jsonl).
+static int plain_loads(const wvg_corpus *c, uint64_t tb, uint64_t te)
+{
+    const int v = tuning().k1_loads;
+    if (v) return v == 2;
+    return c->kind == WVG_KIND_F32 && (te - tb) * (uint64_t)c->nchunks * 1024ull <= (800ull << 20);
+}
+
 struct SearchPlan {
     uint64_t tb = 0, te = 0;
     int groups = 1;      // scan: workgroups per query; gemm: row ranges
@@ -966,6 +978,7 @@ static int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t 
     a.pq_ks = c->pq_ks;
     a.dense = pq_dense(c, d_allow);
     a.order512 = c->ctx->order512;
+    a.plain = plain_loads(c, p.tb, p.te);
     if (!p.gemm) a.reverse = next_direction(c, 1);
     ProfArm arm(c->ctx);
     if (arm.rc) return arm.rc;
@@ -1636,6 +1649,7 @@ int wvg_search_device_pipelined(wvg_corpus *c, const float *d_queries, uint32_t 
         a.k = k;
         a.reverse = next_direction(c, nq);
         a.order512 = c->ctx->order512;
+        a.plain = plain_loads(c, p.tb, p.te);
         WVG_HIP(hipMemsetAsync(j.arrivals, 0, align_up((size_t)nq * 4, 16), s));
         ProfArm arm(c->ctx);
         if (arm.rc) return arm.rc;
@@ -1659,6 +1673,7 @@ int wvg_search_device_pipelined(wvg_corpus *c, const float *d_queries, uint32_t 
     a.nq = 1;
     a.k = k;
     a.order512 = c->ctx->order512;
+    a.plain = plain_loads(c, p.tb, p.te);
     const uint32_t dir0 = next_direction(c, nq);
     for (uint32_t i = 0; i < nq; i++) {
         a.queries = d_queries + (size_t)i * c->dim;
@@ -1853,7 +1868,7 @@ int wvg_synthetic_rows(wvg_ctx *ctx, uint64_t seed, const uint64_t *ids, uint64_
 
 // Internal A/B knob (not part of include/wvgpu.h): 0 = K1 scan variant,
 // 1 = K1 resident workgroups per CU, ... 7 = K8 ADC variant, 8 = query-stream merge wait (us),
-// 9 = serpentine scan order, 10 = K3b row-range length.  Returns the previous value.
+// 9 = serpentine scan order, 10 = K3b row-range length, 11 = K1 load policy.  Returns the previous value.
 int wvgx_set_tuning(int key, int value)
 {
     Tuning &t = tuning();
@@ -1891,6 +1906,9 @@ int wvgx_set_tuning(int key, int value)
     } else if (key == 10) {
         old = t.gemm_range_tiles;
         t.gemm_range_tiles = value;
+    } else if (key == 11) {
+        old = t.k1_loads;
+        t.k1_loads = value;
     }
     return old;
 }

@@ -189,6 +189,8 @@ struct ScanArgs {
                                // begin where the previous one ended, on rows still in the Infinity Cache
     int dense;                 // PQ m = 32: no allow list and mostly-live rows -> K8c (no tile skipping)
     int order512;              // F32 distances in the AVX-512 kernels' order (wvg_set_distance_order)
+    int plain;                 // F32 K1 row loads with the default cache policy instead of non-temporal
+                               // (scanned bytes within a few x the Infinity Cache: plain_loads())
 };
 // Phase 1 writes dense partials [nq][groups][K] (keys, KEY_NONE = empty).
 int scan_groups_for(const ScanArgs &a, int num_cus);
@@ -239,6 +241,8 @@ struct Tuning {
                              // 1 = K8 gather in segment order everywhere
     int merge_wait_us = 0;   // query-stream merge workgroup's wait per query in us; 0 = 4 s (test knob)
     int serpentine = 1;      // alternate the scan direction between consecutive scans (0 = always upwards; A/B)
+    int k1_loads = 0;        // K1 row-load policy: 0 = by scanned bytes (plain_loads), 1 = non-temporal,
+                             // 2 = default policy (A/B)
     int gemm_range_tiles = 0;  // K3b row-range length in tiles: 0 = auto (512), > 0 = that many,
                                // -1 = one long range per workgroup (one wave of workgroups; A/B)
 };

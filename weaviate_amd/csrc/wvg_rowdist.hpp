@@ -58,13 +58,21 @@ __device__ __forceinline__ float avx256_reduce(const float (&acc)[4][8], float s
 
 typedef float f4v __attribute__((ext_vector_type(4)));
 
-// Streaming (non-temporal) 16-byte load: the corpus is read once per query
-// and is larger than the 256 MiB Infinity Cache at the headline shape
-// (measured: 6.69 vs 5.77 TB/s for a 512 MB read, profiles/r01/hbm_read_ceiling.jsonl).
+// Streaming 16-byte load.  NT: non-temporal -- for a corpus well past the
+// 256 MiB Infinity Cache, read once per query (measured: 6.9 vs 6.2-6.4 TB/s
+// over 3.2 GB, profiles/r02/pq_adc/mall_reuse_policies.jsonl); at or below
+// ~800 MiB the default policy lets consecutive scans of the same rows
+// find part of them there (1M x 128: 1150 vs 1197 us per 16 scans,
+// profiles/r02/bench/load_policy_ab.jsonl).  The host picks (ScanArgs.plain).
+template <bool NT = true>
 __device__ __forceinline__ float4 ld_stream(const float4 *p)
 {
-    const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(p));
-    return make_float4(v.x, v.y, v.z, v.w);
+    if constexpr (NT) {
+        const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(p));
+        return make_float4(v.x, v.y, v.z, v.w);
+    } else {
+        return *p;
+    }
 }
 
 template <int METRIC>
@@ -79,7 +87,7 @@ __device__ __forceinline__ void chunk_update(float (&acc)[4][8], int cc, float4 
 
 // p: chunk 0 of this lane's row; consecutive chunks are CSTRIDE float4 apart
 // (64 in the tiled corpus).  q: the query, 16-byte aligned, padded to 4.
-template <int METRIC, int D, int CSTRIDE>
+template <int METRIC, int D, int CSTRIDE, bool NT = true>
 __device__ __forceinline__ float row_dot_or_l2_fixed(const float4 *__restrict__ p,
                                                      const float4 *__restrict__ q)
 {
@@ -95,7 +103,7 @@ __device__ __forceinline__ float row_dot_or_l2_fixed(const float4 *__restrict__ 
     for (int b = 0; b < NB; b++) {
         float4 xs[8];
 #pragma unroll
-        for (int cc = 0; cc < 8; cc++) xs[cc] = ld_stream(p + (size_t)(b * 8 + cc) * CSTRIDE);
+        for (int cc = 0; cc < 8; cc++) xs[cc] = ld_stream<NT>(p + (size_t)(b * 8 + cc) * CSTRIDE);
 #pragma unroll
         for (int cc = 0; cc < 8; cc++) chunk_update<METRIC>(acc, cc, q[b * 8 + cc], xs[cc]);
     }

@@ -134,7 +134,7 @@ __device__ __forceinline__ void scan_tiles(const ScanArgs &a, const float4 *q4, 
         if (a.order512)  // wave-uniform: the AVX-512 kernels' order (generic length)
             r = row_dist_512<METRIC, 64>(rp, q4, (int)a.dim);
         else if constexpr (D > 0)
-            r = row_dot_or_l2_fixed<METRIC, D, 64>(rp, q4);
+            r = a.plain ? row_dot_or_l2_fixed<METRIC, D, 64, false>(rp, q4) : row_dot_or_l2_fixed<METRIC, D, 64>(rp, q4);
         else
             r = row_dot_or_l2_generic<METRIC, 64>(rp, q4, (int)a.dim);
         tk.offer(lane_key(m, wrap_metric(a.metric, r), t, lane));
