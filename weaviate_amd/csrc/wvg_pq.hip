@@ -600,7 +600,11 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_rot_kernel(ScanA
 // Every tile of the wave's range is loaded (no skipping of dead tiles): the
 // host runs K8c without an allow list on mostly-live corpora and K8b
 // otherwise.  The A/B sums are K8b's, so results are bit-identical.
-template <int E, int R, int NB, int METRIC>
+// W (LDS wait pattern): 0 = the compiler's (one s_waitcnt per lookup, so
+// each add starts as soon as its value lands: 34 waits per tile, 18 % of the
+// tile's instructions); 1 = one wait per batch of NB lookups; 2 = one wait
+// per batch with the next batch's lookups already issued (software pipeline).
+template <int E, int R, int NB, int METRIC, int W = 0>
 __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_dense_kernel(ScanArgs a, uint64_t *partials)
 {
     static_assert(64 % R == 0, "the ring length divides the 64-tile mask block");
@@ -687,18 +691,46 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_dense_kernel(Sca
 #pragma unroll
                 for (int w = 0; w < 8; w++)
                     asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(win[w]) : "v"(nmask[w]), "v"(ring[s][w]), "v"(ring[sc][w]));
+                auto lookup = [&](int j) {
+                    const uint32_t c8 = __builtin_amdgcn_perm(0u, win[j >> 2], 0x0C0C000Cu | ((uint32_t)(j & 3) << 8));
+                    const uint32_t off = (c8 << 1) + x8;
+                    return *reinterpret_cast<const f32x2 *>(imgb + off + 8 * j);
+                };
+                if constexpr (W == 2) {  // batch h+1's lookups in flight while batch h is added
+                    static_assert(NB <= 15, "lgkmcnt holds at most 15 outstanding LDS reads");
+                    constexpr int NH = 32 / NB;
+                    f32x2 v[2][NB];
 #pragma unroll
-                for (int h = 0; h < 32 / NB; h++) {
-                    f32x2 v[NB];
+                    for (int jj = 0; jj < NB; jj++) v[0][jj] = lookup(jj);
 #pragma unroll
-                    for (int jj = 0; jj < NB; jj++) {
-                        const int j = h * NB + jj;
-                        const uint32_t c8 = __builtin_amdgcn_perm(0u, win[j >> 2], 0x0C0C000Cu | ((uint32_t)(j & 3) << 8));
-                        const uint32_t off = (c8 << 1) + x8;
-                        v[jj] = *reinterpret_cast<const f32x2 *>(imgb + off + 8 * j);
+                    for (int h = 0; h < NH; h++) {
+                        if (h + 1 < NH) {
+#pragma unroll
+                            for (int jj = 0; jj < NB; jj++) v[(h + 1) & 1][jj] = lookup((h + 1) * NB + jj);
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+                        if (h + 1 < NH)
+                            __builtin_amdgcn_s_waitcnt(0xC07F | (NB << 8));  // lgkmcnt(NB): batch h landed
+                        else
+                            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int jj = 0; jj < NB; jj++) acc = acc + v[h & 1][jj];
                     }
+                } else {
 #pragma unroll
-                    for (int jj = 0; jj < NB; jj++) acc = acc + v[jj];
+                    for (int h = 0; h < 32 / NB; h++) {
+                        f32x2 v[NB];
+#pragma unroll
+                        for (int jj = 0; jj < NB; jj++) v[jj] = lookup(h * NB + jj);
+                        if constexpr (W == 1) {  // one wait for the whole batch
+                            __builtin_amdgcn_sched_barrier(0);
+                            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+                            __builtin_amdgcn_sched_barrier(0);
+                        }
+#pragma unroll
+                        for (int jj = 0; jj < NB; jj++) acc = acc + v[jj];
+                    }
                 }
                 if (i >= 1 && i <= n) {  // offer tile i-1
                     const uint32_t tl = i - 1u;
@@ -871,15 +903,15 @@ static void launch_pq_cycle(const ScanArgs &a, uint64_t *partials, dim3 grid, di
         launch_timed((scan_pq32_cycle_kernel<E, R, NB, WVG_M_COSINE, GL>), grid, block, lds, s, a, partials);
 }
 
-template <int E, int R, int NB>
+template <int E, int R, int NB, int W = 0>
 static void launch_pq_dense(const ScanArgs &a, uint64_t *partials, dim3 grid, dim3 block, size_t lds, hipStream_t s)
 {
     if (a.metric == WVG_M_L2)
-        launch_timed((scan_pq32_dense_kernel<E, R, NB, WVG_M_L2>), grid, block, lds, s, a, partials);
+        launch_timed((scan_pq32_dense_kernel<E, R, NB, WVG_M_L2, W>), grid, block, lds, s, a, partials);
     else if (a.metric == WVG_M_DOT)
-        launch_timed((scan_pq32_dense_kernel<E, R, NB, WVG_M_DOT>), grid, block, lds, s, a, partials);
+        launch_timed((scan_pq32_dense_kernel<E, R, NB, WVG_M_DOT, W>), grid, block, lds, s, a, partials);
     else
-        launch_timed((scan_pq32_dense_kernel<E, R, NB, WVG_M_COSINE>), grid, block, lds, s, a, partials);
+        launch_timed((scan_pq32_dense_kernel<E, R, NB, WVG_M_COSINE, W>), grid, block, lds, s, a, partials);
 }
 
 template <int E>
@@ -896,6 +928,15 @@ static hipError_t launch_pq_e(const ScanArgs &a, uint64_t *partials, int groups,
         else if (v == 15) launch_pq_cycle<E, 4, 16, false>(a, partials, grid, block, 4 * lds, s);
         else if (v == 16) launch_pq_cycle<E, 8, 8, true>(a, partials, grid, block, 4 * lds, s);
         else launch_pq_cycle<E, 4, 16, true>(a, partials, grid, block, 4 * lds, s);
+        return hipGetLastError();
+    }
+    if (m32 && v >= 18 && v <= 21) {
+        // K8c LDS wait patterns: 18 = one wait per batch of 16, 19 = per batch of 32,
+        // 20 = pipelined batches of 8, 21 = one wait per batch of 8
+        if (v == 18) launch_pq_dense<E, 8, 16, 1>(a, partials, grid, block, 4 * lds, s);
+        else if (v == 19) launch_pq_dense<E, 8, 32, 1>(a, partials, grid, block, 4 * lds, s);
+        else if (v == 20) launch_pq_dense<E, 8, 8, 2>(a, partials, grid, block, 4 * lds, s);
+        else launch_pq_dense<E, 8, 8, 1>(a, partials, grid, block, 4 * lds, s);
         return hipGetLastError();
     }
     if (m32 && (v == 10 || v == 11 || v == 12 || (v == 0 && a.dense))) {
