@@ -49,6 +49,38 @@ class BinaryQuantizer:
                                                  q.shape[0], fptr(out)))
         return out
 
+    def DistanceBetweenCompressedAndUncompressedVectors(self, x, y):
+        """CH/quantizer.go:65-68: Encode(x), then the Hamming distance to y."""
+        return self.DistanceBetweenCompressedVectors(self.Encode(x), y)
+
+    def NewDistancer(self, a) -> "BQDistancer":
+        """CH/quantizer.go:89-95."""
+        a = np.asarray(a, dtype=np.float32)
+        return BQDistancer(self, a, self.Encode(a))
+
+    def NewCompressedQuantizerDistancer(self, code) -> "BQDistancer":
+        """CH/quantizer.go:97-103."""
+        return BQDistancer(self, None, np.asarray(code, dtype=np.uint64))
+
+
+class BQDistancer:
+    """CH/quantizer.go:83-117: Distance(code) = Hamming to the compressed
+    query; DistanceToFloat(x) = the provider's exact SingleDist to the float
+    query when there is one, else the Hamming distance to Encode(x)."""
+
+    def __init__(self, bq, x, compressed):
+        self.bq, self.x, self.compressed = bq, x, compressed
+
+    def Distance(self, code):
+        d, err = self.bq.DistanceBetweenCompressedVectors(self.compressed, code)
+        return d, err is None, err
+
+    def DistanceToFloat(self, x):
+        if self.x is not None and len(self.x) > 0:
+            return self.bq.distancer.SingleDist(self.x, x)
+        d, err = self.bq.DistanceBetweenCompressedVectors(self.compressed, self.bq.Encode(x))
+        return d, err is None, err
+
 
 class ProductQuantizer:
     """k-means PQ with given centers [m][ks][ds]."""
@@ -139,6 +171,10 @@ class ProductQuantizer:
 
     def NewDistancer(self, q):
         return PQDistancer(self, np.asarray(q, dtype=np.float32), self.CenterAt(q))
+
+    def NewCompressedQuantizerDistancer(self, code):
+        """:339-346: no LUT; distances are SDC lookups against this code."""
+        return PQDistancer(self, None, None, np.asarray(code, dtype=np.uint8))
 
     def ExposeFields(self) -> "PQData":
         """:285-295 -- the fields the HNSW commit log persists (compress.go:89)."""
@@ -259,14 +295,29 @@ def read_pq_record(buf, offset: int = 0):
 
 
 class PQDistancer:
-    def __init__(self, pq, x, lut):
-        self.pq, self.x, self.lut = pq, x, lut
+    """CH/product_quantization.go:352-370.  From a float query: ADC through its
+    LUT; from a code (NewCompressedQuantizerDistancer): SDC."""
+
+    def __init__(self, pq, x, lut, compressed=None):
+        self.pq, self.x, self.lut, self.compressed = pq, x, lut, compressed
 
     def Distance(self, code):
         code = np.asarray(code, dtype=np.uint8)
+        if self.lut is None:
+            d, err = self.pq.DistanceBetweenCompressedVectors(self.compressed, code)
+            return d, err is None, err
         if code.shape[0] != self.pq.m:
             return 0.0, False, "inconsistent compressed vector length"  # product_quantization.go:357-358
         return float(self.DistanceBatch(code[None, :])[0]), True, None
+
+    def DistanceToFloat(self, x):
+        """:363-370: the exact distance to the query (the LUT's flatCenter), or SDC to Encode(x)."""
+        if self.lut is not None:
+            from .distancer import provider_for
+
+            return provider_for(self.pq.ctx, _DIST_NAME[self.pq.metric]).SingleDist(x, self.x)
+        d, err = self.pq.DistanceBetweenCompressedVectors(self.compressed, self.pq.Encode(x))
+        return d, err is None, err
 
     def DistanceBatch(self, codes) -> np.ndarray:
         codes = np.ascontiguousarray(codes, dtype=np.uint8)
@@ -274,3 +325,143 @@ class PQDistancer:
         check(self.pq.ctx.lib.wvg_pq_adc_batch(self.pq.ctx.handle, self.pq.metric, fptr(self.lut), self.pq.m,
                                                self.pq.ks, u8ptr(codes), codes.shape[0], fptr(out)))
         return out
+
+
+_DIST_NAME = {_lib.METRIC_L2: "l2-squared", _lib.METRIC_DOT: "dot", _lib.METRIC_COSINE: "cosine-dot"}
+
+
+class QuantizedVectorsCompressor:
+    """compressionhelpers.VectorCompressor (CH/compression.go:37-54, 56-200) with
+    the compressed-vector cache held on the device: one BQ or PQ corpus of codes
+    keyed by docID.  Preload encodes exactly as the reference does (the vector
+    as given -- callers normalize for cosine -- through the quantizer's Encode,
+    :87-94) and stores the code; Delete clears it.  Distances go through the
+    quantizer's distancers, so they are the reference's bits."""
+
+    def __init__(self, ctx, quantizer, capacity: int, dims: int | None = None):
+        from ._lib import KIND_BQ, KIND_PQ
+        from .device import Corpus
+
+        self.ctx, self.quantizer = ctx, quantizer
+        if isinstance(quantizer, BinaryQuantizer):
+            metric = quantizer.distancer.metric if quantizer.distancer is not None else _lib.METRIC_L2
+            self.kind, self.dims = KIND_BQ, int(dims)
+            self.corpus = Corpus(ctx, KIND_BQ, metric, self.dims, capacity)
+        else:
+            self.kind, self.dims = KIND_PQ, quantizer.dimensions
+            self.corpus = Corpus(ctx, KIND_PQ, quantizer.metric, self.dims, capacity)
+            self.corpus.set_codebook(quantizer.centers)
+
+    def Drop(self) -> None:
+        self.corpus.destroy()
+
+    def Preload(self, id_: int, vector) -> None:
+        self.PreloadBatch(np.array([id_], np.uint64), np.asarray(vector, np.float32)[None, :])
+
+    def PreloadBatch(self, ids, vectors) -> None:
+        """Preload of many ids at once (the bulk path of V/hnsw/compress.go:98-104)."""
+        codes = self.quantizer.EncodeBatch(np.ascontiguousarray(vectors, np.float32))
+        self.corpus.upsert_codes(np.ascontiguousarray(ids, np.uint64), codes)
+
+    def Delete(self, id_: int) -> None:
+        self.corpus.delete(np.array([id_], np.uint64))
+
+    def _codes(self, ids):
+        m = self.quantizer.m if self.kind == _lib.KIND_PQ else 0
+        return self.corpus.get_batch(np.ascontiguousarray(ids, np.uint64), pq_m=m)
+
+    def compressedVectorFromID(self, id_: int):
+        """:107-116: (code, error) -- an id never preloaded (or deleted) is an error."""
+        codes, ok = self._codes([id_])
+        if not ok[0]:
+            return None, f"got a nil or zero-length vector at docID {id_}"
+        return codes[0], None
+
+    def DistanceBetweenCompressedVectorsFromIDs(self, x: int, y: int):
+        """:118-131."""
+        cx, err = self.compressedVectorFromID(x)
+        if err:
+            return 0.0, err
+        cy, err = self.compressedVectorFromID(y)
+        if err:
+            return 0.0, err
+        return self.quantizer.DistanceBetweenCompressedVectors(cx, cy)
+
+    def DistanceBetweenCompressedAndUncompressedVectorsFromID(self, id_: int, vector):
+        """:133-140."""
+        c, err = self.compressedVectorFromID(id_)
+        if err:
+            return 0.0, err
+        return self.quantizer.DistanceBetweenCompressedAndUncompressedVectors(np.asarray(vector, np.float32), c)
+
+    def NewDistancer(self, vector):
+        """:158-166: (CompressorDistancer, return function)."""
+        return CompressorDistancer(self, self.quantizer.NewDistancer(vector)), (lambda: None)
+
+    def NewDistancerFromID(self, id_: int):
+        """:168-183: (CompressorDistancer, error)."""
+        c, err = self.compressedVectorFromID(id_)
+        if err:
+            return None, err
+        return CompressorDistancer(self, self.quantizer.NewCompressedQuantizerDistancer(c)), None
+
+    def NewBag(self) -> "QuantizedDistanceBag":
+        """:194-199."""
+        return QuantizedDistanceBag(self)
+
+    def ExposeFields(self):
+        return self.quantizer.ExposeFields() if self.kind == _lib.KIND_PQ else PQData(0, 0, 0)
+
+
+class CompressorDistancer:
+    """quantizedCompressorDistancer (CH/compression.go:306-325): DistanceToNode
+    reads the node's code from the device corpus; DistanceToNodes does a whole
+    candidate list with one gather (the HNSW rescore batch)."""
+
+    def __init__(self, compressor, distancer):
+        self.c, self.d = compressor, distancer
+
+    def DistanceToNode(self, id_: int):
+        code, err = self.c.compressedVectorFromID(id_)
+        if err:
+            return 0.0, False, err
+        return self.d.Distance(code)
+
+    def DistanceToNodes(self, ids):
+        """(dists, ok) for many nodes: one code gather, one batched distance."""
+        codes, ok = self.c._codes(ids)
+        out = np.zeros(len(ok), np.float32)
+        if ok.any():
+            live = codes[ok]
+            if isinstance(self.d, PQDistancer) and self.d.lut is not None:
+                out[ok] = self.d.DistanceBatch(live)
+            elif isinstance(self.d, BQDistancer):
+                out[ok] = self.c.quantizer.DistanceBatch(self.d.compressed, live)
+            else:
+                out[ok] = [self.d.Distance(cd)[0] for cd in live]
+        return out, ok
+
+    def DistanceToFloat(self, vector):
+        return self.d.DistanceToFloat(np.asarray(vector, np.float32))
+
+
+class QuantizedDistanceBag:
+    """CompressionDistanceBag (CH/compression_distance_bag.go:19-45)."""
+
+    def __init__(self, compressor):
+        self.c = compressor
+        self.elements = {}
+
+    def Load(self, id_: int):
+        code, err = self.c.compressedVectorFromID(id_)
+        if err:
+            return err
+        self.elements[id_] = code
+        return None
+
+    def Distance(self, x: int, y: int):
+        if x not in self.elements:
+            return 0.0, f"missing id in bag: {x}"
+        if y not in self.elements:
+            return 0.0, f"missing id in bag: {y}"
+        return self.c.quantizer.DistanceBetweenCompressedVectors(self.elements[x], self.elements[y])
