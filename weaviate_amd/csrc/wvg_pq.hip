@@ -717,6 +717,20 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_dense_kernel(Sca
 #pragma unroll
                         for (int jj = 0; jj < NB; jj++) acc = acc + v[h & 1][jj];
                     }
+                } else if constexpr (W == 3) {  // A and B as two scalar add chains instead of one packed chain
+                    float ax = acc.x, ay = acc.y;
+#pragma unroll
+                    for (int h = 0; h < 32 / NB; h++) {
+                        f32x2 v[NB];
+#pragma unroll
+                        for (int jj = 0; jj < NB; jj++) v[jj] = lookup(h * NB + jj);
+#pragma unroll
+                        for (int jj = 0; jj < NB; jj++) {
+                            asm("v_add_f32 %0, %1, %2" : "=v"(ax) : "v"(ax), "v"(v[jj].x));
+                            asm("v_add_f32 %0, %1, %2" : "=v"(ay) : "v"(ay), "v"(v[jj].y));
+                        }
+                    }
+                    acc = f32x2{ax, ay};
                 } else {
 #pragma unroll
                     for (int h = 0; h < 32 / NB; h++) {
@@ -930,13 +944,16 @@ static hipError_t launch_pq_e(const ScanArgs &a, uint64_t *partials, int groups,
         else launch_pq_cycle<E, 4, 16, true>(a, partials, grid, block, 4 * lds, s);
         return hipGetLastError();
     }
-    if (m32 && v >= 18 && v <= 21) {
+    if (m32 && v >= 18 && v <= 23) {
         // K8c LDS wait patterns: 18 = one wait per batch of 16, 19 = per batch of 32,
-        // 20 = pipelined batches of 8, 21 = one wait per batch of 8
+        // 20 = pipelined batches of 8, 21 = one wait per batch of 8;
+        // 22 / 23 = scalar A and B add chains, batches of 16 / 8
         if (v == 18) launch_pq_dense<E, 8, 16, 1>(a, partials, grid, block, 4 * lds, s);
         else if (v == 19) launch_pq_dense<E, 8, 32, 1>(a, partials, grid, block, 4 * lds, s);
         else if (v == 20) launch_pq_dense<E, 8, 8, 2>(a, partials, grid, block, 4 * lds, s);
-        else launch_pq_dense<E, 8, 8, 1>(a, partials, grid, block, 4 * lds, s);
+        else if (v == 21) launch_pq_dense<E, 8, 8, 1>(a, partials, grid, block, 4 * lds, s);
+        else if (v == 22) launch_pq_dense<E, 8, 16, 3>(a, partials, grid, block, 4 * lds, s);
+        else launch_pq_dense<E, 8, 8, 3>(a, partials, grid, block, 4 * lds, s);
         return hipGetLastError();
     }
     if (m32 && (v == 10 || v == 11 || v == 12 || (v == 0 && a.dense))) {
