@@ -48,6 +48,7 @@ __global__ __launch_bounds__(BQ_WAVES * 64) void scan_bq_kernel(ScanArgs a, uint
     const uint64_t t0 = a.tile_begin + ntiles * gw / total, t1 = a.tile_begin + ntiles * (gw + 1) / total;
     WaveTopK<E> tk;
     tk.init((int)a.k);
+    tk.init_fast();
     if constexpr (NCH > 0) {
         // next live tile at or after t (wave-uniform), its mask in m
         auto next_live = [&](uint64_t t, uint64_t &m) {
@@ -77,7 +78,8 @@ __global__ __launch_bounds__(BQ_WAVES * 64) void scan_bq_kernel(ScanArgs a, uint
             for (int c = 0; c < NCH; c++)
                 tot += (uint32_t)__popcll(cur[c].x ^ q[2 * c]) + (uint32_t)__popcll(cur[c].y ^ q[2 * c + 1]);
             const float dist = (float)tot;  // exact: sum of float32(popcount) is an integer < 2^24
-            tk.offer(((m_cur >> lane) & 1ull) ? wvg_make_key(dist, (uint32_t)(t * 64 + lane)) : WVG_KEY_NONE);
+            // rejection on the float distance first: the key is built only when some lane passes
+            tk.offer_dist_fast(dist, (uint32_t)(t * 64 + lane), m_cur);
 #pragma unroll
             for (int c = 0; c < NCH; c++) cur[c] = nxt[c];
             t = tn;
@@ -94,7 +96,7 @@ __global__ __launch_bounds__(BQ_WAVES * 64) void scan_bq_kernel(ScanArgs a, uint
                 tot += (uint32_t)__popcll(x.x ^ q[2 * c]) + (uint32_t)__popcll(x.y ^ q[2 * c + 1]);
             }
             const float dist = (float)tot;
-            tk.offer(((m >> lane) & 1ull) ? wvg_make_key(dist, (uint32_t)(t * 64 + lane)) : WVG_KEY_NONE);
+            tk.offer_dist_fast(dist, (uint32_t)(t * 64 + lane), m);
         }
     }
     group_combine_store<E, BQ_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
