@@ -680,6 +680,7 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_dense_kernel(Sca
 #pragma unroll
         for (int w = 0; w < 8; w++) ring[R - 1][w] = 0u;
         f32x2 acc = {0.0f, 0.0f};
+        uint32_t dummy = __builtin_amdgcn_readfirstlane(wave);  // W == 5 diagnostic (a scalar register)
         // pass i finishes tile i-1 (slot (i-1) mod R) and starts tile i (slot
         // i mod R); n + 1 passes, in groups of R so the ring slots are static
         for (uint32_t base = 0; base <= n; base += R) {
@@ -716,6 +717,21 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_dense_kernel(Sca
                         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                         for (int jj = 0; jj < NB; jj++) acc = acc + v[h & 1][jj];
+                    }
+                } else if constexpr (W == 4 || W == 5) {  // diagnostics: K8c + 32 extra VALU (4) / SALU (5) per tile
+#pragma unroll
+                    for (int h = 0; h < 32 / NB; h++) {
+                        f32x2 v[NB];
+#pragma unroll
+                        for (int jj = 0; jj < NB; jj++) v[jj] = lookup(h * NB + jj);
+#pragma unroll
+                        for (int jj = 0; jj < NB; jj++) {
+                            acc = acc + v[jj];
+                            if constexpr (W == 4)
+                                asm volatile("v_nop");
+                            else
+                                asm volatile("s_add_u32 %0, %0, 1" : "+s"(dummy));
+                        }
                     }
                 } else if constexpr (W == 3) {  // A and B as two scalar add chains instead of one packed chain
                     float ax = acc.x, ay = acc.y;
@@ -944,16 +960,18 @@ static hipError_t launch_pq_e(const ScanArgs &a, uint64_t *partials, int groups,
         else launch_pq_cycle<E, 4, 16, true>(a, partials, grid, block, 4 * lds, s);
         return hipGetLastError();
     }
-    if (m32 && v >= 18 && v <= 23) {
+    if (m32 && v >= 18 && v <= 25) {
         // K8c LDS wait patterns: 18 = one wait per batch of 16, 19 = per batch of 32,
         // 20 = pipelined batches of 8, 21 = one wait per batch of 8;
-        // 22 / 23 = scalar A and B add chains, batches of 16 / 8
+        // 22 / 23 = scalar A and B add chains, batches of 16 / 8; 24 / 25 = diagnostics (+32 VALU / SALU per tile)
         if (v == 18) launch_pq_dense<E, 8, 16, 1>(a, partials, grid, block, 4 * lds, s);
         else if (v == 19) launch_pq_dense<E, 8, 32, 1>(a, partials, grid, block, 4 * lds, s);
         else if (v == 20) launch_pq_dense<E, 8, 8, 2>(a, partials, grid, block, 4 * lds, s);
         else if (v == 21) launch_pq_dense<E, 8, 8, 1>(a, partials, grid, block, 4 * lds, s);
         else if (v == 22) launch_pq_dense<E, 8, 16, 3>(a, partials, grid, block, 4 * lds, s);
-        else launch_pq_dense<E, 8, 8, 3>(a, partials, grid, block, 4 * lds, s);
+        else if (v == 23) launch_pq_dense<E, 8, 8, 3>(a, partials, grid, block, 4 * lds, s);
+        else if (v == 24) launch_pq_dense<E, 8, 16, 4>(a, partials, grid, block, 4 * lds, s);
+        else launch_pq_dense<E, 8, 16, 5>(a, partials, grid, block, 4 * lds, s);
         return hipGetLastError();
     }
     if (m32 && (v == 10 || v == 11 || v == 12 || (v == 0 && a.dense))) {
