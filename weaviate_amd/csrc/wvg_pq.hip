@@ -718,6 +718,9 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_dense_kernel(Sca
 #pragma unroll
                         for (int jj = 0; jj < NB; jj++) acc = acc + v[h & 1][jj];
                     }
+                } else if constexpr (W == 6) {  // diagnostic: K8c's loads, masks and offers, no lookups
+#pragma unroll
+                    for (int w = 0; w < 8; w++) acc.x = acc.x + __uint_as_float(win[w] & 0x3F800000u);
                 } else if constexpr (W == 4 || W == 5) {  // diagnostics: K8c + 32 extra VALU (4) / SALU (5) per tile
 #pragma unroll
                     for (int h = 0; h < 32 / NB; h++) {
@@ -960,10 +963,11 @@ static hipError_t launch_pq_e(const ScanArgs &a, uint64_t *partials, int groups,
         else launch_pq_cycle<E, 4, 16, true>(a, partials, grid, block, 4 * lds, s);
         return hipGetLastError();
     }
-    if (m32 && v >= 18 && v <= 25) {
+    if (m32 && v >= 18 && v <= 28) {
         // K8c LDS wait patterns: 18 = one wait per batch of 16, 19 = per batch of 32,
         // 20 = pipelined batches of 8, 21 = one wait per batch of 8;
-        // 22 / 23 = scalar A and B add chains, batches of 16 / 8; 24 / 25 = diagnostics (+32 VALU / SALU per tile)
+        // 22 / 23 = scalar A and B add chains, batches of 16 / 8; 24 / 25 = diagnostics (+32 VALU / SALU per
+        // tile); 26 / 27 / 28 = diagnostic: loads, masks and offers only (results are not distances), ring 8 / 4 / 2
         if (v == 18) launch_pq_dense<E, 8, 16, 1>(a, partials, grid, block, 4 * lds, s);
         else if (v == 19) launch_pq_dense<E, 8, 32, 1>(a, partials, grid, block, 4 * lds, s);
         else if (v == 20) launch_pq_dense<E, 8, 8, 2>(a, partials, grid, block, 4 * lds, s);
@@ -971,7 +975,10 @@ static hipError_t launch_pq_e(const ScanArgs &a, uint64_t *partials, int groups,
         else if (v == 22) launch_pq_dense<E, 8, 16, 3>(a, partials, grid, block, 4 * lds, s);
         else if (v == 23) launch_pq_dense<E, 8, 8, 3>(a, partials, grid, block, 4 * lds, s);
         else if (v == 24) launch_pq_dense<E, 8, 16, 4>(a, partials, grid, block, 4 * lds, s);
-        else launch_pq_dense<E, 8, 16, 5>(a, partials, grid, block, 4 * lds, s);
+        else if (v == 25) launch_pq_dense<E, 8, 16, 5>(a, partials, grid, block, 4 * lds, s);
+        else if (v == 26) launch_pq_dense<E, 8, 16, 6>(a, partials, grid, block, 4 * lds, s);
+        else if (v == 27) launch_pq_dense<E, 4, 16, 6>(a, partials, grid, block, 4 * lds, s);
+        else launch_pq_dense<E, 2, 16, 6>(a, partials, grid, block, 4 * lds, s);
         return hipGetLastError();
     }
     if (m32 && (v == 10 || v == 11 || v == 12 || (v == 0 && a.dense))) {
