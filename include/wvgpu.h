@@ -48,6 +48,10 @@ extern "C" {
 #define WVG_METRIC_L2 0     /* "l2-squared" D/l2.go */
 #define WVG_METRIC_DOT 1    /* "dot"        D/dot_product.go */
 #define WVG_METRIC_COSINE 2 /* "cosine-dot" D/cosine_dist.go (rows/queries normalized) */
+#define WVG_METRIC_MANHATTAN 3 /* "manhattan" D/manhattan.go (pure Go on every host) */
+#define WVG_METRIC_HAMMING 4   /* "hamming"   D/hamming.go -> hamming_256 / hamming_512
+                                  (D/hamming_amd64.go:18-24); selected by name in
+                                  adapters/repos/db/shard.go:406-421 like the others */
 
 typedef struct wvg_ctx wvg_ctx;
 typedef struct wvg_corpus wvg_corpus;

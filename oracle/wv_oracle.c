@@ -228,7 +228,53 @@ ORC_API float orc_dot_step(const float *a, const float *b, long n)
     return sum;
 }
 
-enum { ORC_L2 = 0, ORC_DOT = 1, ORC_COSINE = 2 };
+enum { ORC_L2 = 0, ORC_DOT = 1, ORC_COSINE = 2, ORC_MANHATTAN = 3, ORC_HAMMING = 4 };
+
+/* manhattanImpl: D/manhattan.go:20-30 -- pure Go on every host (no SIMD
+ * kernel): sum += float32(math.Abs(float64(a[i] - b[i]))) in element order.
+ * The float64 round trip is exact, so this is fabsf of the fp32 difference.
+ * ManhattanProvider.Step (:68-78) is the same loop. */
+ORC_API float orc_manhattan(const float *a, const float *b, long n)
+{
+    float sum = 0.0f;
+    for (long i = 0; i < n; i++) {
+        float diff = a[i] - b[i];
+        sum += fabsf(diff);
+    }
+    return sum;
+}
+
+/* hamming_256: D/c/hamming_avx256_amd64.c:14-144, dispatched on AVX2 hosts by
+ * D/hamming_amd64.go:18-24 (hamming_512, D/c/hamming_avx512_amd64.c, counts
+ * the same elements with the same comparisons).  An int count, stored as
+ * float.  n < 8 (:20-32): `a[0] != b[0]` per element (C's !=: a NaN counts).
+ * n >= 8: the 32- and 8-blocks (:59-119) compare with _CMP_NEQ_OQ (ordered
+ * not-equal: a NaN does NOT count); the tail (:121-131) with != again.
+ * Note: the reference loops forever for len == 0 (do/while); we return 0. */
+ORC_API float orc_hamming_256(const float *a, const float *b, long len)
+{
+    int n = (int)len;
+    int sum = 0;
+    if (n <= 0) return 0.0f;
+    int nord = n >= 8 ? (n & ~7) : 0;
+    for (int i = 0; i < n; i++) {
+        if (i < nord)
+            sum += (a[i] < b[i] || a[i] > b[i]) ? 1 : 0; /* _CMP_NEQ_OQ */
+        else
+            sum += a[i] != b[i] ? 1 : 0;
+    }
+    return (float)sum;
+}
+
+/* HammingProvider.Step: D/hamming.go:76-86 -- pure Go: sum += float32(1)
+ * where x[i] != y[i] (Go's !=: a NaN counts). */
+ORC_API float orc_hamming_step(const float *a, const float *b, long n)
+{
+    float sum = 0.0f;
+    for (long i = 0; i < n; i++)
+        if (a[i] != b[i]) sum += 1.0f;
+    return sum;
+}
 
 /* Provider.SingleDist on an AVX2 (non-AMX) amd64 host:
  * L2 D/l2.go:46-53 -> l2_256; dot D/dot_product.go:68-76 -> -dot_256;
@@ -238,6 +284,8 @@ ORC_API float orc_single_dist(int metric, const float *a, const float *b, long n
     switch (metric) {
     case ORC_L2: return orc_l2_256(a, b, n);
     case ORC_DOT: return -orc_dot_256(a, b, n);
+    case ORC_MANHATTAN: return orc_manhattan(a, b, n);      /* D/manhattan.go:51-58 */
+    case ORC_HAMMING: return orc_hamming_256(a, b, n);      /* D/hamming.go:59-66 */
     default: return 1.0f - orc_dot_256(a, b, n);
     }
 }
@@ -249,6 +297,8 @@ ORC_API float orc_single_dist_512(int metric, const float *a, const float *b, lo
     switch (metric) {
     case ORC_L2: return orc_l2_512(a, b, n);
     case ORC_DOT: return -orc_dot_512(a, b, n);
+    case ORC_MANHATTAN: return orc_manhattan(a, b, n);
+    case ORC_HAMMING: return orc_hamming_256(a, b, n);  /* hamming_512 counts identically */
     default: return 1.0f - orc_dot_512(a, b, n);
     }
 }
@@ -259,19 +309,25 @@ ORC_API void orc_dist_all_512(int metric, const float *q, const float *rows, lon
 }
 
 /* Provider.Wrap: L2 identity (D/l2.go:90-92), dot -x (D/dot_product.go:96-98),
- * cosine 1-x (D/cosine_dist.go:66-68). */
+ * cosine 1-x (D/cosine_dist.go:66-68), manhattan / hamming identity
+ * (D/manhattan.go:80-82, D/hamming.go:88-90). */
 ORC_API float orc_wrap(int metric, float x)
 {
     switch (metric) {
-    case ORC_L2: return x;
     case ORC_DOT: return -x;
-    default: return 1.0f - x;
+    case ORC_COSINE: return 1.0f - x;
+    default: return x;
     }
 }
 
 ORC_API float orc_step(int metric, const float *a, const float *b, long n)
 {
-    return metric == ORC_L2 ? orc_l2_step(a, b, n) : orc_dot_step(a, b, n);
+    switch (metric) {
+    case ORC_L2: return orc_l2_step(a, b, n);
+    case ORC_MANHATTAN: return orc_manhattan(a, b, n);
+    case ORC_HAMMING: return orc_hamming_step(a, b, n);
+    default: return orc_dot_step(a, b, n);
+    }
 }
 
 /* distancer.Normalize: D/normalize.go:16-32.  Sequential unfused sum of
@@ -569,8 +625,8 @@ typedef void (*orc_dist_fn)(float *, float *, float *, long *);
 /* flat.searchByVector -> findTopVectors (V/flat/index.go:319-334, 411-452)
  * over a dense resident matrix (no LSM cursor / LE decode: favourable to the
  * CPU).  `fn` is the distance kernel (oracle restatement, or the reference's
- * own l2_256 loaded from oracle/_ref).  wrap_neg: 0 = L2 (dist = fn),
- * 1 = dot (dist = -fn), 2 = cosine (dist = 1 - fn). */
+ * own l2_256 / dot_256 / hamming_256 loaded from oracle/_ref); the metric's
+ * Wrap is applied to its result (orc_wrap). */
 ORC_API long orc_flat_search(const float *rows, long n, long d, long pitch, const uint8_t *valid,
                              const float *q, long k, int metric, orc_dist_fn fn,
                              uint64_t *out_ids, float *out_dists)
@@ -584,7 +640,7 @@ ORC_API long orc_flat_search(const float *rows, long n, long d, long pitch, cons
             float r = 0.0f;
             long len = d;
             fn((float *)q, (float *)(rows + i * pitch), &r, &len);
-            dist = (metric == ORC_L2) ? r : (metric == ORC_DOT ? -r : 1.0f - r);
+            dist = orc_wrap(metric, r);
         } else {
             dist = orc_single_dist(metric, q, rows + i * pitch, d);
         }
@@ -640,7 +696,7 @@ static long flat_search_bq_fn(const float *rows, const uint64_t *codes, long n, 
             float r = 0.0f;
             long len = d;
             fn((float *)query, (float *)(rows + ids[i] * pitch), &r, &len);
-            dist = (metric == ORC_L2) ? r : (metric == ORC_DOT ? -r : 1.0f - r);
+            dist = orc_wrap(metric, r);
         } else {
             dist = orc_single_dist(metric, query, rows + ids[i] * pitch, d);
         }

@@ -19,7 +19,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ORACLE_SO = os.path.join(HERE, "_build", "libwvoracle.so")
 REF_SO = os.path.join(HERE, "_ref", "libwvref.so")
 
-L2, DOT, COSINE = 0, 1, 2
+L2, DOT, COSINE, MANHATTAN, HAMMING = 0, 1, 2, 3, 4
 
 _F = POINTER(c_float)
 _U64 = POINTER(c_uint64)
@@ -40,7 +40,8 @@ def lib():
         if not os.path.exists(ORACLE_SO):
             build()
         l = ctypes.CDLL(ORACLE_SO)
-        for n in ["orc_l2_256", "orc_dot_256", "orc_l2_512", "orc_dot_512", "orc_l2_step", "orc_dot_step"]:
+        for n in ["orc_l2_256", "orc_dot_256", "orc_l2_512", "orc_dot_512", "orc_l2_step", "orc_dot_step",
+                  "orc_manhattan", "orc_hamming_256", "orc_hamming_step"]:
             getattr(l, n).restype = c_float
             getattr(l, n).argtypes = [_F, _F, c_long]
         l.orc_single_dist.restype = c_float
@@ -87,7 +88,8 @@ def lib():
 
 
 def ref():
-    """The reference's own l2_256/l2_512/dot_256/dot_512 (None if not built)."""
+    """The reference's own l2_256/l2_512/dot_256/dot_512/hamming_256/hamming_512
+    (None if not built)."""
     global _ref
     if _ref is None and os.path.exists(REF_SO):
         _ref = ctypes.CDLL(REF_SO)
@@ -118,6 +120,22 @@ def l2_256(a, b):
 def dot_256(a, b):
     a, b = f32(a), f32(b)
     return np.float32(lib().orc_dot_256(_f(a), _f(b), len(a)))
+
+
+def ref_symbol(metric):
+    """The reference C kernel behind a metric on an AVX2 host (None for
+    manhattan, which is pure Go)."""
+    return {L2: "l2_256", DOT: "dot_256", COSINE: "dot_256", HAMMING: "hamming_256"}.get(metric)
+
+
+def manhattan(a, b):
+    a, b = f32(a), f32(b)
+    return np.float32(lib().orc_manhattan(_f(a), _f(b), len(a)))
+
+
+def hamming_256(a, b):
+    a, b = f32(a), f32(b)
+    return np.float32(lib().orc_hamming_256(_f(a), _f(b), len(a)))
 
 
 def single_dist(metric, a, b):
@@ -250,10 +268,8 @@ def flat_search(rows, q, k, metric, valid=None, use_ref_kernel=False):
     oid = np.empty(max(k, 1), dtype=np.uint64)
     od = np.empty(max(k, 1), dtype=np.float32)
     fn = None
-    if use_ref_kernel:
-        r = ref()
-        sym = "l2_256" if metric == L2 else "dot_256"
-        fn = ctypes.cast(getattr(r, sym), c_void_p)
+    if use_ref_kernel and ref_symbol(metric):
+        fn = ctypes.cast(getattr(ref(), ref_symbol(metric)), c_void_p)
     v = None if valid is None else np.ascontiguousarray(valid, dtype=np.uint8)
     cnt = lib().orc_flat_search(_f(rows), n, d, d, _u8(v) if v is not None else None, _f(q), k, metric, fn, _u64(oid),
                                 _f(od))
@@ -288,8 +304,8 @@ def bench_flat(rows, qs, k, metric, threads, use_ref_kernel=True):
     n, d = rows.shape
     nq = qs.shape[0]
     fn = None
-    if use_ref_kernel and ref() is not None:
-        fn = ctypes.cast(getattr(ref(), "l2_256" if metric == L2 else "dot_256"), c_void_p)
+    if use_ref_kernel and ref() is not None and ref_symbol(metric):
+        fn = ctypes.cast(getattr(ref(), ref_symbol(metric)), c_void_p)
     oid = np.empty((nq, k), dtype=np.uint64)
     od = np.empty((nq, k), dtype=np.float32)
     secs = lib().orc_bench_flat(_f(rows), n, d, d, _f(qs), nq, k, metric, fn, threads, _u64(oid), _f(od))
@@ -313,8 +329,8 @@ def bench_flat_bq(rows, codes, qs, k, rescore_limit, metric, threads, use_ref_ke
     n, d = rows.shape
     nq = qs.shape[0]
     fn = None
-    if use_ref_kernel and ref() is not None:
-        fn = ctypes.cast(getattr(ref(), "l2_256" if metric == L2 else "dot_256"), c_void_p)
+    if use_ref_kernel and ref() is not None and ref_symbol(metric):
+        fn = ctypes.cast(getattr(ref(), ref_symbol(metric)), c_void_p)
     oid = np.empty((nq, k), dtype=np.uint64)
     od = np.empty((nq, k), dtype=np.float32)
     secs = lib().orc_bench_flat_bq(_f(rows), _u64(codes), n, d, d, _f(qs), nq, k, rescore_limit, metric, fn, threads,

@@ -68,6 +68,45 @@ def test_cosine_known_answers(orc, known):
             assert abs(float(d) - c["expected"]) <= c["tol"]
 
 
+@pytest.mark.parametrize("key", ["hamming_256", "hamming_512"])
+def test_oracle_hamming_matches_reference_kernels(orc, key):
+    """D/c/hamming_avx{256,512}_amd64.c outputs (tests/golden/hamming.npz):
+    equal elements, NaN in the SIMD blocks (_CMP_NEQ_OQ: not counted) and in
+    the scalar tail (!=: counted), -0.0 vs +0.0; lengths 1..1536."""
+    g = np.load(os.path.join(GOLDEN, "hamming.npz"))
+    got = [orc.hamming_256(a, b) for _, a, b in _pairs(g)]
+    assert np.array_equal(_bits(got), _bits(g[key]))
+    # the NaN rule matters: some pairs differ from a plain count of a != b
+    plain = [np.float32(np.count_nonzero(a != b)) for _, a, b in _pairs(g)]
+    assert not np.array_equal(_bits(plain), _bits(g[key]))
+
+
+@pytest.mark.parametrize("metric,key", [("MANHATTAN", "manhattan"), ("HAMMING", "hamming")])
+def test_manhattan_hamming_known_answers(orc, known, metric, key):
+    """D/manhattan_test.go:21-90, D/hamming_test.go:23-103: SingleDist and the
+    step-by-step sum of Step over single elements."""
+    m = getattr(orc, metric)
+    for c in known[key]:
+        assert orc.single_dist(m, c["a"], c["b"]) == np.float32(c["expected"])
+        s = np.float32(0)
+        for x, y in zip(c["a"], c["b"]):
+            s = np.float32(s + orc.step(m, [x], [y]))
+        assert s == np.float32(c["expected"])
+
+
+def test_manhattan_is_the_sequential_go_loop(orc):
+    """manhattanImpl (D/manhattan.go:20-30) adds |a_i - b_i| in element order
+    in fp32: compare with a numpy loop in the same order."""
+    rng = np.random.default_rng(5)
+    for n in [1, 7, 8, 33, 128, 777]:
+        a = rng.uniform(-1, 1, n).astype(np.float32)
+        b = rng.uniform(-1, 1, n).astype(np.float32)
+        s = np.float32(0)
+        for x, y in zip(a, b):
+            s = np.float32(s + np.abs(np.float32(x - y)))
+        assert orc.manhattan(a, b).view(np.uint32) == s.view(np.uint32)
+
+
 def test_normalize_zero_vector(orc):
     assert np.all(orc.normalize(np.zeros(7)) == 0)
 

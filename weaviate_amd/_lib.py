@@ -24,10 +24,10 @@ WVG_ERR_UNSUPPORTED = -6
 WVG_ERR_CAPACITY = -7
 
 KIND_F32, KIND_BQ, KIND_PQ = 0, 1, 2
-METRIC_L2, METRIC_DOT, METRIC_COSINE = 0, 1, 2
+METRIC_L2, METRIC_DOT, METRIC_COSINE, METRIC_MANHATTAN, METRIC_HAMMING = 0, 1, 2, 3, 4
 ORDER_AVX256, ORDER_AVX512 = 0, 1  # reference SIMD kernel whose reduction order distances follow
 METRIC_BY_NAME = {"l2-squared": METRIC_L2, "dot": METRIC_DOT, "cosine": METRIC_COSINE,
-                  "cosine-dot": METRIC_COSINE}
+                  "cosine-dot": METRIC_COSINE, "manhattan": METRIC_MANHATTAN, "hamming": METRIC_HAMMING}
 
 # name -> (restype, argtypes); every symbol declared in include/wvgpu.h.
 _P = POINTER

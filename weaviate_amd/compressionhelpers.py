@@ -327,7 +327,8 @@ class PQDistancer:
         return out
 
 
-_DIST_NAME = {_lib.METRIC_L2: "l2-squared", _lib.METRIC_DOT: "dot", _lib.METRIC_COSINE: "cosine-dot"}
+_DIST_NAME = {_lib.METRIC_L2: "l2-squared", _lib.METRIC_DOT: "dot", _lib.METRIC_COSINE: "cosine-dot",
+              _lib.METRIC_MANHATTAN: "manhattan", _lib.METRIC_HAMMING: "hamming"}
 
 
 class QuantizedVectorsCompressor:

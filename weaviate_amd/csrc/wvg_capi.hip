@@ -405,7 +405,7 @@ int wvg_corpus_create(wvg_ctx *ctx, int kind, int metric, uint32_t dim, uint64_t
     if (!ctx || !out) return fail(WVG_ERR_INVALID, "null ctx/out");
     *out = nullptr;
     if (kind < WVG_KIND_F32 || kind > WVG_KIND_PQ) return fail(WVG_ERR_INVALID, "unknown corpus kind");
-    if (metric < WVG_METRIC_L2 || metric > WVG_METRIC_COSINE) return fail(WVG_ERR_INVALID, "unknown metric");
+    if (metric < WVG_METRIC_L2 || metric > WVG_METRIC_HAMMING) return fail(WVG_ERR_INVALID, "unknown metric");
     if (dim == 0) return fail(WVG_ERR_INVALID, "dim must be > 0");
     if (id_base % 64 != 0) return fail(WVG_ERR_INVALID, "id_base must be a multiple of 64");
     if (capacity > (1ull << 32)) return fail(WVG_ERR_INVALID, "capacity above 2^32 rows per corpus");
@@ -1763,7 +1763,7 @@ int wvg_rescore(wvg_ctx *ctx, int metric, const float *q, const float *rows, con
                 uint32_t dim, uint32_t k, uint64_t *out_ids, float *out_dists, uint32_t *out_count)
 {
     if (!ctx || !q || (n && (!rows || !ids))) return fail(WVG_ERR_INVALID, "null argument");
-    if (metric < WVG_METRIC_L2 || metric > WVG_METRIC_COSINE) return fail(WVG_ERR_INVALID, "unknown metric");
+    if (metric < WVG_METRIC_L2 || metric > WVG_METRIC_HAMMING) return fail(WVG_ERR_INVALID, "unknown metric");
     if (n > 0xFFFFFFFFull) return fail(WVG_ERR_INVALID, "too many rows");
     if (out_count) *out_count = 0;
     if (n == 0 || k == 0 || dim == 0) return WVG_OK;
@@ -1948,7 +1948,7 @@ int wvg_profile_stop(wvg_ctx *ctx, double *scan_ms_total, uint64_t *scan_launche
 int wvg_distance_batch(wvg_ctx *ctx, int metric, const float *q, const float *X, uint64_t n, uint32_t dim, float *out)
 {
     if (!ctx || !q || (n && (!X || !out))) return fail(WVG_ERR_INVALID, "null argument");
-    if (metric < WVG_METRIC_L2 || metric > WVG_METRIC_COSINE) return fail(WVG_ERR_INVALID, "unknown metric");
+    if (metric < WVG_METRIC_L2 || metric > WVG_METRIC_HAMMING) return fail(WVG_ERR_INVALID, "unknown metric");
     if (n == 0 || dim == 0) return WVG_OK;
     WVG_HIP(hipSetDevice(ctx->device));
     const uint32_t nch = f32_chunks(dim);

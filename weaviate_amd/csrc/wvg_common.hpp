@@ -63,8 +63,10 @@ __host__ __device__ inline float wvg_synth_value(uint64_t seed_mixed, uint64_t r
 
 // ---------------------------------------------------------------------------
 // Metrics (entities/vectorindex/common/config.go:22-31 names them
-// "l2-squared", "dot", "cosine"; the provider type of cosine is "cosine-dot").
+// "l2-squared", "dot", "cosine", "manhattan", "hamming"; the provider type of
+// cosine is "cosine-dot").  Kernels templated on a metric instantiate L2, DOT
+// (raw dot product; cosine is DOT with the 1-x Wrap), MANHATTAN and HAMMING.
 // ---------------------------------------------------------------------------
-enum { WVG_M_L2 = 0, WVG_M_DOT = 1, WVG_M_COSINE = 2 };
+enum { WVG_M_L2 = 0, WVG_M_DOT = 1, WVG_M_COSINE = 2, WVG_M_MANHATTAN = 3, WVG_M_HAMMING = 4 };
 
 __device__ __forceinline__ int wvg_lane() { return __lane_id(); }

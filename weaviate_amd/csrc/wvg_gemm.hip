@@ -683,7 +683,10 @@ static bool rs_config(uint32_t dim, uint32_t k, RsConfig &c)
     }
 }
 
-bool gemm_supported(uint32_t dim, int metric) { return dim % 32 == 0 && dim > 0 && metric != WVG_M_L2; }
+bool gemm_supported(uint32_t dim, int metric)
+{
+    return dim % 32 == 0 && dim > 0 && (metric == WVG_M_DOT || metric == WVG_M_COSINE);
+}
 
 uint32_t gemm_queries_per_block(uint32_t dim, uint32_t k)
 {

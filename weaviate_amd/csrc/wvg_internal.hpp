@@ -152,6 +152,24 @@ __device__ __forceinline__ float pq_row_sum(const uint4 *rp, uint32_t nch, uint3
 }
 size_t corpus_row_bytes(int kind, uint32_t dim, uint32_t pq_m);
 
+// f(std::integral_constant<int, M>{}) for the kernel template metric M of a
+// runtime metric: L2, MANHATTAN, HAMMING as themselves; dot and cosine share
+// the raw dot product (DOT), the Wrap (-x / 1-x) is applied at run time.
+template <int M>
+struct MetricTag {
+    static constexpr int value = M;
+};
+template <typename F>
+inline auto with_metric(int metric, F &&f)
+{
+    switch (metric) {
+    case WVG_M_L2: return f(MetricTag<WVG_M_L2>{});
+    case WVG_M_MANHATTAN: return f(MetricTag<WVG_M_MANHATTAN>{});
+    case WVG_M_HAMMING: return f(MetricTag<WVG_M_HAMMING>{});
+    default: return f(MetricTag<WVG_M_DOT>{});
+    }
+}
+
 // ---- kernel launchers (wvg_scan.hip / wvg_bq.hip / wvg_pq.hip) -----------
 // Scan phase 1: per (query, workgroup) top-K keys into `partials`
 //   [nq][groups][K].  Returns the number of groups used.

@@ -21,7 +21,9 @@ namespace wvg {
 
 constexpr int PQ_SCAN_WAVES = 16;  // K8: one workgroup per CU shares the LUT
 
-// Step(a, b) in the pure-Go order.
+// Step(a, b) in the pure-Go order: L2 D/l2.go:79-88, dot / cosine
+// D/dot_product.go:87-94, manhattan D/manhattan.go:68-78 (sum += |a-b|),
+// hamming D/hamming.go:76-86 (sum += 1 where a != b: Go's !=, a NaN counts).
 __device__ __forceinline__ float go_step(int metric, const float *a, const float *b, uint32_t n)
 {
     float sum = 0.0f;
@@ -31,6 +33,11 @@ __device__ __forceinline__ float go_step(int metric, const float *a, const float
             float sq = diff * diff;
             sum = sum + sq;
         }
+    } else if (metric == WVG_M_MANHATTAN) {
+        for (uint32_t i = 0; i < n; i++) sum = sum + __builtin_fabsf(a[i] - b[i]);
+    } else if (metric == WVG_M_HAMMING) {
+        for (uint32_t i = 0; i < n; i++)
+            if (a[i] != b[i]) sum = sum + 1.0f;
     } else {
         for (uint32_t i = 0; i < n; i++) {
             float p = a[i] * b[i];
@@ -928,7 +935,7 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_cycle_kernel(Sca
 template <int E, int R, int NB, bool GL>
 static void launch_pq_cycle(const ScanArgs &a, uint64_t *partials, dim3 grid, dim3 block, size_t lds, hipStream_t s)
 {
-    if (a.metric == WVG_M_L2)
+    if (a.metric == WVG_M_L2 || a.metric == WVG_M_MANHATTAN || a.metric == WVG_M_HAMMING)  // Wrap = identity
         launch_timed((scan_pq32_cycle_kernel<E, R, NB, WVG_M_L2, GL>), grid, block, lds, s, a, partials);
     else if (a.metric == WVG_M_DOT)
         launch_timed((scan_pq32_cycle_kernel<E, R, NB, WVG_M_DOT, GL>), grid, block, lds, s, a, partials);
@@ -939,7 +946,7 @@ static void launch_pq_cycle(const ScanArgs &a, uint64_t *partials, dim3 grid, di
 template <int E, int R, int NB, int W = 0>
 static void launch_pq_dense(const ScanArgs &a, uint64_t *partials, dim3 grid, dim3 block, size_t lds, hipStream_t s)
 {
-    if (a.metric == WVG_M_L2)
+    if (a.metric == WVG_M_L2 || a.metric == WVG_M_MANHATTAN || a.metric == WVG_M_HAMMING)  // Wrap = identity
         launch_timed((scan_pq32_dense_kernel<E, R, NB, WVG_M_L2, W>), grid, block, lds, s, a, partials);
     else if (a.metric == WVG_M_DOT)
         launch_timed((scan_pq32_dense_kernel<E, R, NB, WVG_M_DOT, W>), grid, block, lds, s, a, partials);

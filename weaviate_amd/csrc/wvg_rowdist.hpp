@@ -87,11 +87,82 @@ __device__ __forceinline__ void chunk_update(float (&acc)[4][8], int cc, float4 
 
 // p: chunk 0 of this lane's row; consecutive chunks are CSTRIDE float4 apart
 // (64 in the tiled corpus).  q: the query, 16-byte aligned, padded to 4.
+template <int CSTRIDE>
+__device__ __forceinline__ float elem_at(const float4 *__restrict__ p, int pos)
+{
+    const float *c = reinterpret_cast<const float *>(p + (size_t)(pos >> 2) * CSTRIDE);
+    return c[pos & 3];
+}
+
+// Manhattan and Hamming: the two metrics whose sum is not an AVX2 chain set.
+//  - Manhattan (D/manhattan.go:20-30): pure Go on every host (no SIMD kernel
+//    exists): sum += float32(math.Abs(float64(a_i - b_i))) in element order.
+//    The float64 round trip is exact, so it is |q - x| in fp32 added in order.
+//  - Hamming (D/hamming_amd64.go:18-24 -> D/c/hamming_avx256_amd64.c:14-144;
+//    hamming_512 counts the same elements the same way): an integer count
+//    converted to float once.  n < 8: `a != b` per element (C's unordered !=,
+//    a NaN counts); n >= 8: the first n & ~7 elements by _CMP_NEQ_OQ (ordered:
+//    a NaN does NOT count), the rest by !=.  A count is order-free, so only
+//    which comparison an element gets matters.
+// Whole 16-byte chunks are read 8 at a time (loads in flight), the tail of a
+// dimension that is not a multiple of 4 element by element.
+__device__ __forceinline__ uint32_t neq_oq(float a, float b) { return (a < b) || (a > b) ? 1u : 0u; }
+__device__ __forceinline__ uint32_t neq_uo(float a, float b) { return a != b ? 1u : 0u; }
+
+template <int METRIC>
+constexpr bool is_abs_or_neq = METRIC == WVG_M_MANHATTAN || METRIC == WVG_M_HAMMING;
+
+template <int METRIC, int CSTRIDE, bool NT = false>
+__device__ __forceinline__ float row_abs_or_neq(const float4 *__restrict__ p, const float4 *__restrict__ q4, int n)
+{
+    static_assert(is_abs_or_neq<METRIC>, "manhattan / hamming only");
+    const float *q = reinterpret_cast<const float *>(q4);
+    float sum = 0.0f;
+    uint32_t cnt = 0u;
+    const int nord = METRIC == WVG_M_HAMMING && n >= 8 ? (n & ~7) : 0;  // elements under _CMP_NEQ_OQ
+    auto upd = [&](int c, float4 qq, float4 x) {
+        if constexpr (METRIC == WVG_M_MANHATTAN) {
+            sum = sum + __builtin_fabsf(qq.x - x.x);
+            sum = sum + __builtin_fabsf(qq.y - x.y);
+            sum = sum + __builtin_fabsf(qq.z - x.z);
+            sum = sum + __builtin_fabsf(qq.w - x.w);
+        } else if (4 * c < nord) {  // nord is a multiple of 8: a chunk is wholly inside or outside
+            cnt += neq_oq(qq.x, x.x) + neq_oq(qq.y, x.y) + neq_oq(qq.z, x.z) + neq_oq(qq.w, x.w);
+        } else {
+            cnt += neq_uo(qq.x, x.x) + neq_uo(qq.y, x.y) + neq_uo(qq.z, x.z) + neq_uo(qq.w, x.w);
+        }
+    };
+    const int nc = n >> 2;
+    int c = 0;
+    for (; c + 8 <= nc; c += 8) {
+        float4 xs[8];
+#pragma unroll
+        for (int cc = 0; cc < 8; cc++) xs[cc] = ld_stream<NT>(p + (size_t)(c + cc) * CSTRIDE);
+#pragma unroll
+        for (int cc = 0; cc < 8; cc++) upd(c + cc, q4[c + cc], xs[cc]);
+    }
+    for (; c < nc; c++) upd(c, q4[c], p[(size_t)c * CSTRIDE]);
+    for (int i = nc * 4; i < n; i++) {
+        const float x = elem_at<CSTRIDE>(p, i);
+        if constexpr (METRIC == WVG_M_MANHATTAN)
+            sum = sum + __builtin_fabsf(q[i] - x);
+        else
+            cnt += i < nord ? neq_oq(q[i], x) : neq_uo(q[i], x);
+    }
+    if constexpr (METRIC == WVG_M_HAMMING)
+        return (float)cnt;
+    else
+        return sum;
+}
+
 template <int METRIC, int D, int CSTRIDE, bool NT = true>
 __device__ __forceinline__ float row_dot_or_l2_fixed(const float4 *__restrict__ p,
                                                      const float4 *__restrict__ q)
 {
     static_assert(D % 32 == 0 && D >= 32, "fixed path needs D % 32 == 0");
+    if constexpr (is_abs_or_neq<METRIC>) {
+        return row_abs_or_neq<METRIC, CSTRIDE, NT>(p, q, D);
+    } else {
     float acc[4][8];
 #pragma unroll
     for (int j = 0; j < 4; j++)
@@ -108,19 +179,14 @@ __device__ __forceinline__ float row_dot_or_l2_fixed(const float4 *__restrict__ 
         for (int cc = 0; cc < 8; cc++) chunk_update<METRIC>(acc, cc, q[b * 8 + cc], xs[cc]);
     }
     return avx256_reduce(acc, 0.0f);
-}
-
-template <int CSTRIDE>
-__device__ __forceinline__ float elem_at(const float4 *__restrict__ p, int pos)
-{
-    const float *c = reinterpret_cast<const float *>(p + (size_t)(pos >> 2) * CSTRIDE);
-    return c[pos & 3];
+    }
 }
 
 template <int METRIC, int CSTRIDE>
 __device__ __forceinline__ float row_dot_or_l2_generic(const float4 *__restrict__ p,
                                                        const float4 *__restrict__ q4, int n)
 {
+    if constexpr (is_abs_or_neq<METRIC>) return row_abs_or_neq<METRIC, CSTRIDE>(p, q4, n);
     const float *q = reinterpret_cast<const float *>(q4);
     float sum = 0.0f;
     if (n < 8) {
@@ -168,7 +234,8 @@ __device__ __forceinline__ float row_dot_or_l2_generic(const float4 *__restrict_
 template <int METRIC, int CSTRIDE>
 __device__ __forceinline__ float row_dist_512(const float4 *__restrict__ p, const float4 *__restrict__ q4, int n)
 {
-    if (n < 128) return row_dot_or_l2_generic<METRIC, CSTRIDE>(p, q4, n);
+    // Manhattan has no SIMD kernel; hamming_512 counts like hamming_256
+    if (is_abs_or_neq<METRIC> || n < 128) return row_dot_or_l2_generic<METRIC, CSTRIDE>(p, q4, n);
     const float *q = reinterpret_cast<const float *>(q4);
     float a5[8][16];
 #pragma unroll
@@ -246,10 +313,11 @@ __device__ __forceinline__ float row_dist(const float4 *__restrict__ p, const fl
 }
 
 // Provider.Wrap of the raw kernel value: L2 identity, dot -x (D/dot_product.go:68-76),
-// cosine-dot 1-x (D/cosine_dist.go:38-45).
+// cosine-dot 1-x (D/cosine_dist.go:38-45), manhattan / hamming identity
+// (D/manhattan.go:80-82, D/hamming.go:88-90).
 __device__ __forceinline__ float wrap_metric(int metric, float r)
 {
-    return metric == WVG_M_L2 ? r : (metric == WVG_M_DOT ? -r : 1.0f - r);
+    return metric == WVG_M_DOT ? -r : (metric == WVG_M_COSINE ? 1.0f - r : r);
 }
 
 }  // namespace wvg

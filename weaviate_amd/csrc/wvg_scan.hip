@@ -441,15 +441,15 @@ int scan_groups_for(const ScanArgs &a, int num_cus)
 template <int METRIC, int D, int E>
 static void launch_fixed(const ScanArgs &a, uint64_t *partials, dim3 grid, dim3 block, hipStream_t s)
 {
-    const int v = a.side.active || a.order512 ? 0 : tuning().scan_variant;  // (variants 1-3: AVX2 order only)
-    if (v == 1 && !a.allow)
-        launch_timed((scan_f32_pipe_kernel<METRIC, D, E>), grid, block, 0, s, a, partials);
-    else if (v == 2)
-        launch_timed((scan_f32_plain_kernel<METRIC, D, E>), grid, block, 0, s, a, partials);
-    else if (v == 3)
-        launch_timed((scan_f32_sweep_kernel<METRIC, D, E>), grid, block, 0, s, a, partials);
-    else
-        launch_timed((scan_f32_kernel<METRIC, D, E>), grid, block, 0, s, a, partials);
+    // variants 1-3: AVX2 order only, and L2 / dot (their chain sets)
+    const int v = a.side.active || a.order512 || is_abs_or_neq<METRIC> ? 0 : tuning().scan_variant;
+    if constexpr (!is_abs_or_neq<METRIC>) {
+        if (v == 1 && !a.allow)
+            return launch_timed((scan_f32_pipe_kernel<METRIC, D, E>), grid, block, 0, s, a, partials);
+        if (v == 2) return launch_timed((scan_f32_plain_kernel<METRIC, D, E>), grid, block, 0, s, a, partials);
+        if (v == 3) return launch_timed((scan_f32_sweep_kernel<METRIC, D, E>), grid, block, 0, s, a, partials);
+    }
+    launch_timed((scan_f32_kernel<METRIC, D, E>), grid, block, 0, s, a, partials);
 }
 
 template <int METRIC, int E>
@@ -488,8 +488,7 @@ static hipError_t launch_stream_m(const ScanArgs &a, const StreamJob &j, hipStre
 
 hipError_t launch_scan_f32_stream(const ScanArgs &a, const StreamJob &j, hipStream_t s)
 {
-    if (a.metric == WVG_M_L2) return launch_stream_m<WVG_M_L2>(a, j, s);
-    return launch_stream_m<WVG_M_DOT>(a, j, s);
+    return with_metric(a.metric, [&](auto M) { return launch_stream_m<decltype(M)::value>(a, j, s); });
 }
 
 template <int METRIC>
@@ -502,8 +501,7 @@ static hipError_t launch_f32_m(const ScanArgs &a, uint64_t *partials, int groups
 
 hipError_t launch_scan_f32(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
 {
-    if (a.metric == WVG_M_L2) return launch_f32_m<WVG_M_L2>(a, partials, groups, s);
-    return launch_f32_m<WVG_M_DOT>(a, partials, groups, s);
+    return with_metric(a.metric, [&](auto M) { return launch_f32_m<decltype(M)::value>(a, partials, groups, s); });
 }
 
 // ---------------------------------------------------------------------------
@@ -791,14 +789,11 @@ hipError_t launch_distance_rows(int metric, const float *q, const float *tiled, 
     if (n == 0) return hipSuccess;
     const uint32_t nchunks = f32_chunks(dim);
     dim3 grid((unsigned)((n + 255) / 256)), block(256);
-    if (metric == WVG_M_L2)
-        hipLaunchKernelGGL((distance_tiled_kernel<WVG_M_L2>), grid, block, 0, s, metric,
+    with_metric(metric, [&](auto M) {
+        hipLaunchKernelGGL((distance_tiled_kernel<decltype(M)::value>), grid, block, 0, s, metric,
                            reinterpret_cast<const float4 *>(q), reinterpret_cast<const float4 *>(tiled), n, dim,
                            nchunks, out, o512);
-    else
-        hipLaunchKernelGGL((distance_tiled_kernel<WVG_M_DOT>), grid, block, 0, s, metric,
-                           reinterpret_cast<const float4 *>(q), reinterpret_cast<const float4 *>(tiled), n, dim,
-                           nchunks, out, o512);
+    });
     return hipGetLastError();
 }
 
@@ -818,12 +813,11 @@ hipError_t launch_dist_keys(int metric, const float *q, const float *tiled, uint
     if (n == 0) return hipSuccess;
     const uint32_t nchunks = f32_chunks(dim);
     dim3 grid((unsigned)((n + 255) / 256)), block(256);
-    if (metric == WVG_M_L2)
-        hipLaunchKernelGGL((dist_keys_kernel<WVG_M_L2>), grid, block, 0, s, metric, reinterpret_cast<const float4 *>(q),
-                           reinterpret_cast<const float4 *>(tiled), n, dim, nchunks, keys, o512);
-    else
-        hipLaunchKernelGGL((dist_keys_kernel<WVG_M_DOT>), grid, block, 0, s, metric, reinterpret_cast<const float4 *>(q),
-                           reinterpret_cast<const float4 *>(tiled), n, dim, nchunks, keys, o512);
+    with_metric(metric, [&](auto M) {
+        hipLaunchKernelGGL((dist_keys_kernel<decltype(M)::value>), grid, block, 0, s, metric,
+                           reinterpret_cast<const float4 *>(q), reinterpret_cast<const float4 *>(tiled), n, dim,
+                           nchunks, keys, o512);
+    });
     return hipGetLastError();
 }
 
@@ -890,14 +884,11 @@ hipError_t launch_rescore_keys(int metric, const float *q, uint32_t qpitch, cons
 {
     if (nq == 0 || ncand == 0) return hipSuccess;
     dim3 grid((ncand + 63) / 64, nq), block(64);
-    if (metric == WVG_M_L2)
-        hipLaunchKernelGGL((rescore_keys_kernel<WVG_M_L2>), grid, block, 0, s, metric,
+    with_metric(metric, [&](auto M) {
+        hipLaunchKernelGGL((rescore_keys_kernel<decltype(M)::value>), grid, block, 0, s, metric,
                            reinterpret_cast<const float4 *>(q), qpitch, reinterpret_cast<const float4 *>(tiled), dim,
                            nchunks, cand_keys, ncand, cand_stride, out_keys, o512);
-    else
-        hipLaunchKernelGGL((rescore_keys_kernel<WVG_M_DOT>), grid, block, 0, s, metric,
-                           reinterpret_cast<const float4 *>(q), qpitch, reinterpret_cast<const float4 *>(tiled), dim,
-                           nchunks, cand_keys, ncand, cand_stride, out_keys, o512);
+    });
     return hipGetLastError();
 }
 

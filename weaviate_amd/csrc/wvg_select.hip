@@ -128,10 +128,9 @@ hipError_t launch_ordkeys(const ScanArgs &a, int kind, int num_cus, uint32_t *ke
     if (ntiles == 0) return hipSuccess;
     dim3 grid(sel_grid(ntiles, num_cus)), block(256);
     if (kind == WVG_KIND_F32) {
-        if (a.metric == WVG_M_L2)
-            hipLaunchKernelGGL((ordkeys_f32_kernel<WVG_M_L2>), grid, block, 0, s, a, keys);
-        else
-            hipLaunchKernelGGL((ordkeys_f32_kernel<WVG_M_DOT>), grid, block, 0, s, a, keys);
+        with_metric(a.metric, [&](auto M) {
+            hipLaunchKernelGGL((ordkeys_f32_kernel<decltype(M)::value>), grid, block, 0, s, a, keys);
+        });
     } else if (kind == WVG_KIND_BQ) {
         hipLaunchKernelGGL(ordkeys_bq_kernel, grid, block, 0, s, a, keys);
     } else {
@@ -392,11 +391,10 @@ hipError_t launch_dist_by_ids(const ScanArgs &a, int kind, uint64_t capacity, co
     if (n == 0) return hipSuccess;
     dim3 grid((unsigned)((n + 255) / 256)), block(256);
     if (kind == WVG_KIND_F32) {
-        if (a.metric == WVG_M_L2)
-            hipLaunchKernelGGL((dist_by_ids_kernel<WVG_KIND_F32, WVG_M_L2>), grid, block, 0, s, a, capacity, ids, n, out, ok, qidx);
-        else
-            hipLaunchKernelGGL((dist_by_ids_kernel<WVG_KIND_F32, WVG_M_DOT>), grid, block, 0, s, a, capacity, ids, n, out,
-                               ok, qidx);
+        with_metric(a.metric, [&](auto M) {
+            hipLaunchKernelGGL((dist_by_ids_kernel<WVG_KIND_F32, decltype(M)::value>), grid, block, 0, s, a, capacity,
+                               ids, n, out, ok, qidx);
+        });
     } else if (kind == WVG_KIND_BQ) {
         hipLaunchKernelGGL((dist_by_ids_kernel<WVG_KIND_BQ, 0>), grid, block, 0, s, a, capacity, ids, n, out, ok, qidx);
     } else {

@@ -2,9 +2,10 @@
 
 Reference: adapters/repos/db/vector/hnsw/distancer/provider.go:14-24
 (``New``, ``SingleDist``, ``Step``, ``Wrap``, ``Type``) and the concrete
-providers in l2.go, dot_product.go, cosine_dist.go.  Every distance is
-computed on the GPU in the reference's AVX2 reduction order (bit-identical
-results); ``BatchDist`` is the new bulk entry point (``distancer.BatchProvider``)
+providers in l2.go, dot_product.go, cosine_dist.go, manhattan.go and
+hamming.go.  Every distance is computed on the GPU in the reference's AVX2
+reduction order (bit-identical results; manhattan is the pure-Go loop, hamming
+counts with hamming_256's comparisons); ``BatchDist`` is the new bulk entry point (``distancer.BatchProvider``)
 the flat / HNSW rescore loops use instead of one call per row.
 
 Errors follow the Go convention: ``SingleDist`` returns ``(dist, ok, err)``
@@ -15,7 +16,7 @@ from __future__ import annotations
 import numpy as np
 
 from . import _lib
-from ._lib import METRIC_COSINE, METRIC_DOT, METRIC_L2, check, fptr
+from ._lib import METRIC_COSINE, METRIC_DOT, METRIC_HAMMING, METRIC_L2, METRIC_MANHATTAN, check, fptr
 
 
 class _Provider:
@@ -54,7 +55,8 @@ class _Provider:
         return _Distancer(self, np.asarray(a, dtype=np.float32))
 
     def Step(self, a, b) -> float:
-        """Un-wrapped partial sum in the pure-Go order (l2.go:79-88, dot_product.go:87-94):
+        """Un-wrapped partial sum in the pure-Go order (l2.go:79-88, dot_product.go:87-94,
+        manhattan.go:68-78, hamming.go:76-86):
         a one-segment, one-centroid PQ lookup table is exactly Step(a, b)."""
         a = np.ascontiguousarray(a, dtype=np.float32)
         b = np.ascontiguousarray(b, dtype=np.float32).reshape(1, 1, -1)
@@ -95,10 +97,33 @@ class CosineDistanceProvider(_Provider):
         return np.float32(1.0) - np.float32(x)
 
 
+class ManhattanProvider(_Provider):
+    metric, type_name = METRIC_MANHATTAN, "manhattan"
+
+    def Wrap(self, x):  # manhattan.go:80-82
+        return np.float32(x)
+
+
+class HammingProvider(_Provider):
+    metric, type_name = METRIC_HAMMING, "hamming"
+
+    def Wrap(self, x):  # hamming.go:88-90
+        return np.float32(x)
+
+
+_BY_NAME = {"l2-squared": L2SquaredProvider, "dot": DotProductProvider, "cosine": CosineDistanceProvider,
+            "cosine-dot": CosineDistanceProvider, "manhattan": ManhattanProvider, "hamming": HammingProvider}
+
+
 def provider_for(ctx, name: str) -> _Provider:
-    """Shard.initVectorIndex picks the provider by distance name (adapters/repos/db/shard.go:402-421)."""
-    return {"l2-squared": L2SquaredProvider, "dot": DotProductProvider, "cosine": CosineDistanceProvider,
-            "cosine-dot": CosineDistanceProvider}[name](ctx)
+    """Shard.initVectorIndex picks the provider by distance name (adapters/repos/db/shard.go:406-421);
+    "" means cosine there."""
+    if name == "":
+        name = "cosine"
+    if name not in _BY_NAME:
+        raise ValueError(f'unrecognized distance metric "{name}",choose one of ["cosine", "dot", "l2-squared", '
+                         f'"manhattan","hamming"]')
+    return _BY_NAME[name](ctx)
 
 
 def Normalize(ctx, v) -> np.ndarray:
