@@ -80,3 +80,26 @@ def test_rescore_batch_matches_rescore(orc):
             if ids.size:
                 assert len(gi) == min(k, ef if ef is not None else ids.size, ids.size)
     assert all(len(i) == 0 for i, _ in hnsw.rescore_batch(c, qs, lists, 0))
+
+
+def test_provider_by_distance_name():
+    """Shard.initVectorIndex (adapters/repos/db/shard.go:406-421): the five
+    distance names, "" = cosine, and its error text for anything else; the
+    C-ABI metric codes the providers pass."""
+    import pytest
+
+    from weaviate_amd import _lib
+    from weaviate_amd.distancer import provider_for
+
+    want = {"": ("cosine-dot", _lib.METRIC_COSINE), "cosine": ("cosine-dot", _lib.METRIC_COSINE),
+            "dot": ("dot", _lib.METRIC_DOT), "l2-squared": ("l2-squared", _lib.METRIC_L2),
+            "manhattan": ("manhattan", _lib.METRIC_MANHATTAN), "hamming": ("hamming", _lib.METRIC_HAMMING)}
+    for name, (typ, metric) in want.items():
+        p = provider_for(None, name)
+        assert p.Type() == typ and p.metric == metric
+        assert p.Wrap(2.0) == {_lib.METRIC_DOT: -2.0, _lib.METRIC_COSINE: -1.0}.get(metric, 2.0)
+    with pytest.raises(ValueError) as e:
+        provider_for(None, "euclid")
+    assert str(e.value) == ('unrecognized distance metric "euclid",choose one of ["cosine", "dot", "l2-squared", '
+                            '"manhattan","hamming"]')
+    assert (_lib.METRIC_MANHATTAN, _lib.METRIC_HAMMING) == (3, 4)  # include/wvgpu.h
