@@ -533,18 +533,27 @@ def test_search_device_pipelined_matches_host_api(ctx, orc, mode):
         lib.wvgx_set_tuning(2, old)
 
 
-@pytest.mark.parametrize("variant", [0, 2, 1])
+@pytest.mark.parametrize("variant", [0, 2, 1, "0/pair", "0/pair+prio+skew"])
 @pytest.mark.parametrize("metric,d", [(METRIC_COSINE, 768), (METRIC_DOT, 256), (METRIC_COSINE, 1536), (METRIC_DOT, 512)])
 def test_batched_mfma_variants(ctx, orc, variant, metric, d):
     """K3b (queries resident in LDS, rows streamed into MFMA operands; 0: two
     waves per SIMD, 2: two query tiles per wave) and K3 (1) against the oracle:
-    ragged rows, deletes, an allow list, partial query blocks, SIFT-like ties."""
+    ragged rows, deletes, an allow list, partial query blocks, SIFT-like ties.
+    "0/pair": SIMD partners share queries instead of rows (tuning key 12),
+    "+prio+skew": the second wave per SIMD at priority 1, started late (13, 5)."""
     import ctypes
 
     lib = _lib.load()
     lib.wvgx_set_tuning.restype = ctypes.c_int
     lib.wvgx_set_tuning.argtypes = [ctypes.c_int, ctypes.c_int]
-    old = lib.wvgx_set_tuning(4, variant)
+    knobs = {4: 0}
+    if variant in (0, 1, 2):
+        knobs = {4: variant}
+    if isinstance(variant, str) and "pair" in variant:
+        knobs[12] = 1
+    if isinstance(variant, str) and "prio" in variant:
+        knobs.update({13: 1, 5: 40})
+    prev = {key: lib.wvgx_set_tuning(key, val) for key, val in knobs.items()}
     try:
         n, nq = 4000 + 45, 70
         rows = orc.synth_rows(700 + d, 0, n, d, 0)
@@ -569,7 +578,8 @@ def test_batched_mfma_variants(ctx, orc, variant, metric, d):
                 all_d = orc.dist_all(ORC_METRIC[metric], prep_query(orc, metric, qs[qi]), srows)
                 check_topk(orc, ids[qi], dists[qi], counts[qi], all_d, np.arange(n, dtype=np.uint64), k, vm)
     finally:
-        lib.wvgx_set_tuning(4, old)
+        for key, val in prev.items():
+            lib.wvgx_set_tuning(key, val)
 
 
 

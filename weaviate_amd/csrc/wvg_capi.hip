@@ -1868,7 +1868,8 @@ int wvg_synthetic_rows(wvg_ctx *ctx, uint64_t seed, const uint64_t *ids, uint64_
 
 // Internal A/B knob (not part of include/wvgpu.h): 0 = K1 scan variant,
 // 1 = K1 resident workgroups per CU, ... 7 = K8 ADC variant, 8 = query-stream merge wait (us),
-// 9 = serpentine scan order, 10 = K3b row-range length, 11 = K1 load policy.  Returns the previous value.
+// 9 = serpentine scan order, 10 = K3b row-range length, 11 = K1 load policy, 12 = K3b SIMD pairing,
+// 13 = K3b partner priority.  Returns the previous value.
 int wvgx_set_tuning(int key, int value)
 {
     Tuning &t = tuning();
@@ -1909,6 +1910,12 @@ int wvgx_set_tuning(int key, int value)
     } else if (key == 11) {
         old = t.k1_loads;
         t.k1_loads = value;
+    } else if (key == 12) {
+        old = t.gemm_pairing;
+        t.gemm_pairing = value;
+    } else if (key == 13) {
+        old = t.gemm_prio;
+        t.gemm_prio = value;
     }
     return old;
 }

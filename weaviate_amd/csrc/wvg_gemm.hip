@@ -50,7 +50,9 @@ struct GemmArgs {
     const float *queries;   // [nq][dim] row-major, 16-byte aligned rows (dim % 32 == 0)
     uint32_t nq, k;
     uint32_t nqb, nrr;      // query blocks, row ranges
-    int skew;               // K3b: start delay of query half 1 (units of s_sleep(8))
+    int skew;               // K3b: start delay of waves NW/2.. (units of s_sleep(8))
+    int pairing;            // K3b (QH = 2): 0 = SIMD partners share rows (query halves), 1 = share queries
+    int prio;               // K3b: s_setprio 1 for waves NW/2.. (the second wave on each SIMD)
     uint32_t *prog;         // K3b: [nrr][nqb] tiles done per workgroup (null: no lockstep)
     uint32_t lag;           // K3b: allowed lead over the group's slowest workgroup, in tiles
     uint32_t *gbound;       // K3b: [nq] ordered distance of a finished workgroup's k-th key (min over them)
@@ -333,7 +335,12 @@ __global__ __launch_bounds__(RS_RG * QH * 64, 1) void gemm_rs_kernel(GemmArgs a,
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int rg = wave % RS_RG, qg = wave / RS_RG;
+    // waves w and w + 4 share a SIMD.  pairing 0: they score the same rows
+    // against the two query halves; pairing 1 (QH = 2): the same queries
+    // against different row groups, so their loads are independent.
+    const int rg = QH == 2 && a.pairing ? wave >> 1 : wave % RS_RG;
+    const int qg = QH == 2 && a.pairing ? wave & 1 : wave / RS_RG;
+    const int slot = qg * RS_RG + rg;  // this wave's list / bound slot
     const uint32_t b = blockIdx.x;
     uint32_t qb, rr;
     if (a.nrr % 8 == 0) {  // the query blocks of one row range share an XCD (blocks b, b+8, ...)
@@ -377,10 +384,10 @@ __global__ __launch_bounds__(RS_RG * QH * 64, 1) void gemm_rs_kernel(GemmArgs a,
     // B operand: lane (kk, j) reads chunk 8*(4g+kk)+cc of row 16*rg + j
     const float4 *rbase = reinterpret_cast<const float4 *>(a.data) + (size_t)(8 * kk) * 64 + 16 * rg + j;
     const uint32_t nch = a.nchunks;
-    uint64_t *wl = lists + (size_t)wave * QW * K;
-    uint64_t *wthr = thr + wave * QW;
-    float *wthrf = thrf + wave * QW;
-    const uint32_t *wgord = gord + wave * QW;
+    uint64_t *wl = lists + (size_t)slot * QW * K;
+    uint64_t *wthr = thr + slot * QW;
+    float *wthrf = thrf + slot * QW;
+    const uint32_t *wgord = gord + slot * QW;
     // lanes of query rows past nq, per (query tile, r): C row i = 4*(lane >> 4) + r
     uint64_t qlive[QT][4];
 #pragma unroll
@@ -525,8 +532,10 @@ __global__ __launch_bounds__(RS_RG * QH * 64, 1) void gemm_rs_kernel(GemmArgs a,
     // fill the matrix pipe while a wave reduces.
     bool have_prev = false;
     uint64_t t_prev = 0, m_prev = 0;
-    if (QH == 2 && qg == 1)  // A/B knob: de-phase the SIMD partner's epilogues
+    if (QH == 2 && wave >= NW / 2) {  // A/B knobs: de-phase / prioritise the SIMD partner
+        if (a.prio) __builtin_amdgcn_s_setprio(1);
         for (int i = 0; i < a.skew; i++) __builtin_amdgcn_s_sleep(8);
+    }
     // Soft lockstep of the nqb workgroups that stream one row range (they share
     // an XCD and its 4 MiB L2, ~20 row tiles at d = 768): every RS_SYNC tiles a
     // wave that is more than `lag` tiles ahead of the slowest workgroup of its
@@ -734,6 +743,8 @@ hipError_t launch_gemm_topk(const ScanArgs &s, uint32_t nrr, uint64_t *partials,
     a.k = s.k;
     a.nrr = nrr;
     a.skew = tuning().gemm_skew;
+    a.pairing = tuning().gemm_pairing;
+    a.prio = tuning().gemm_prio;
     RsConfig rc;
     if (tuning().gemm_kernel != 1 && rs_config(s.dim, s.k, rc) && s.nchunks == s.dim / 4) {
         const uint32_t qb = 16u * (uint32_t)(rc.qt * rc.qh);

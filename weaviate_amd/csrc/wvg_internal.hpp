@@ -263,6 +263,8 @@ struct Tuning {
                              // 2 = default policy (A/B)
     int gemm_range_tiles = 0;  // K3b row-range length in tiles: 0 = auto (512), > 0 = that many,
                                // -1 = one long range per workgroup (one wave of workgroups; A/B)
+    int gemm_pairing = 0;    // K3b QH = 2: SIMD partners share rows (0) or queries (1) (A/B)
+    int gemm_prio = 0;       // K3b: s_setprio 1 for the second wave of each SIMD (A/B)
 };
 Tuning &tuning();
 // Profiling: events armed by the host runtime (wvg_profile_start) are bound to
