@@ -189,3 +189,33 @@ def test_concurrent_search_while_writing(ctx, orc):
         assert not errors, errors
     finally:
         corpus.destroy()
+
+
+def test_flat_from_user_config_and_rescore_update(ctx, orc):
+    """flat.New from a parsed user config (BQ, rescoreLimit 20) and
+    UpdateUserConfig raising the rescore limit (V/flat/index.go:67-97,
+    297-305, 593-606): the search-time rescore window follows the update."""
+    from oracle import wv_oracle
+    from weaviate_amd.flat import ParseAndValidateConfig, ValidateUserConfigUpdate
+
+    n, d, k = 5000, 128, 10
+    rows = orc.synth_rows(91, 0, n, d, 0)
+    q = orc.synth_rows(92, 0, 1, d, 0)[0]
+    uc = ParseAndValidateConfig({"distance": "l2-squared", "bq": {"enabled": True, "rescoreLimit": 20}})
+    idx = FlatIndex.from_user_config(ctx, d, uc, capacity=n)
+    assert idx.bq is not None and idx.searchTimeRescore(k) == 20
+    idx.AddBatch(np.arange(n, dtype=np.uint64), rows)
+    codes = orc.bq_encode_rows(rows)
+    ham = orc.bq_dist_all(orc.bq_encode(q), codes)
+    exact = orc.dist_all(wv_oracle.L2, q, rows)
+    for R in (20, 400):
+        if R == 400:
+            upd = ParseAndValidateConfig({"distance": "l2-squared", "bq": {"enabled": True, "rescoreLimit": 400}})
+            ValidateUserConfigUpdate(uc, upd)
+            idx.UpdateUserConfig(upd)
+        assert idx.searchTimeRescore(k) == R
+        ids, dists = idx.SearchByVector(q, k)
+        cand, _ = orc.lex_topk(ham, np.arange(n, dtype=np.uint64), R)
+        li, ld = orc.lex_topk(exact[cand.astype(np.int64)], cand, k)
+        assert np.array_equal(ids, li)
+        assert np.array_equal(dists.view(np.uint32), ld.view(np.uint32))

@@ -103,3 +103,43 @@ def test_provider_by_distance_name():
     assert str(e.value) == ('unrecognized distance metric "euclid",choose one of ["cosine", "dot", "l2-squared", '
                             '"manhattan","hamming"]')
     assert (_lib.METRIC_MANHATTAN, _lib.METRIC_HAMMING) == (3, 4)  # include/wvgpu.h
+
+
+def test_flat_user_config_parse_and_update_rules():
+    """entities/vectorindex/flat/config.go parsing + validation and
+    V/flat/config_update_test.go:24-78's immutable-field cases (messages
+    verbatim); rescore extraction (V/flat/index.go:110-136)."""
+    import pytest
+
+    from weaviate_amd.flat import (CompressionUserConfig as C, ParseAndValidateConfig, UserConfig,
+                                   ValidateUserConfigUpdate, extract_compression, extract_compression_rescore)
+
+    cases = [
+        (UserConfig(PQ=C(Enabled=False)), UserConfig(PQ=C(Enabled=True)),
+         'pq is immutable: attempted change from "false" to "true"'),
+        (UserConfig(BQ=C(Enabled=True)), UserConfig(BQ=C(Enabled=False)),
+         'bq is immutable: attempted change from "true" to "false"'),
+        (UserConfig(Distance="cosine"), UserConfig(Distance="l2-squared"),
+         'distance is immutable: attempted change from "cosine" to "l2-squared"'),
+        (UserConfig(BQ=C(RescoreLimit=10)), UserConfig(BQ=C(RescoreLimit=100)), None),
+    ]
+    for initial, update, err in cases:
+        if err is None:
+            ValidateUserConfigUpdate(initial, update)
+        else:
+            with pytest.raises(ValueError) as e:
+                ValidateUserConfigUpdate(initial, update)
+            assert str(e.value) == err
+    uc = ParseAndValidateConfig({"distance": "manhattan", "bq": {"enabled": True, "rescoreLimit": 250.0},
+                                 "vectorCacheMaxObjects": 7.0})
+    assert uc.Distance == "manhattan" and uc.BQ.Enabled and uc.BQ.RescoreLimit == 250 and uc.VectorCacheMaxObjects == 7
+    assert extract_compression(uc) == "bq" and extract_compression_rescore(uc) == 250
+    d = ParseAndValidateConfig(None)
+    assert d.Distance == "cosine" and d.BQ.RescoreLimit == -1 and extract_compression_rescore(d) == 0
+    for bad, msg in [({"pq": {"enabled": True}}, "PQ is not currently supported for flat indices"),
+                     ({"bq": {"cache": True}}, "not possible to use the cache without compression"),
+                     ("x", "input must be a non-nil map")]:
+        with pytest.raises(ValueError, match=msg):
+            ParseAndValidateConfig(bad)
+    both = UserConfig(PQ=C(Enabled=True, RescoreLimit=5), BQ=C(Enabled=True, RescoreLimit=9))
+    assert extract_compression(both) is None and extract_compression_rescore(both) == 0

@@ -44,7 +44,112 @@ class AllowList:
         return allow_bitmap(sorted(self.ids))
 
 
+# ---------------------------------------------------------------------------
+# The flat index's user config (entities/vectorindex/flat/config.go) and its
+# update rules (V/flat/index.go:593-606, 738-791): what the index is built
+# from and what a schema update may change (only the rescore limit).
+# ---------------------------------------------------------------------------
+DEFAULT_VECTOR_CACHE_MAX_OBJECTS = int(1e12)  # config.go:24
+DEFAULT_COMPRESSION_RESCORE = -1  # config.go:26 ("let Weaviate pick")
+
+
+class CompressionUserConfig:
+    def __init__(self, Enabled: bool = False, RescoreLimit: int = DEFAULT_COMPRESSION_RESCORE, Cache: bool = False):
+        self.Enabled, self.RescoreLimit, self.Cache = Enabled, RescoreLimit, Cache
+
+
+class UserConfig:
+    """flatent.UserConfig with SetDefaults (config.go:53-62)."""
+
+    def __init__(self, Distance: str = "cosine", PQ: CompressionUserConfig | None = None,
+                 BQ: CompressionUserConfig | None = None,
+                 VectorCacheMaxObjects: int = DEFAULT_VECTOR_CACHE_MAX_OBJECTS):
+        self.Distance = Distance
+        self.VectorCacheMaxObjects = VectorCacheMaxObjects
+        self.PQ = PQ if PQ is not None else CompressionUserConfig()
+        self.BQ = BQ if BQ is not None else CompressionUserConfig()
+
+    def IndexType(self) -> str:
+        return "flat"
+
+    def DistanceName(self) -> str:
+        return self.Distance
+
+
+def _opt_int(m, name, set_fn):  # entities/vectorindex/common OptionalIntFromMap: json numbers arrive as float
+    v = m.get(name)
+    if isinstance(v, float) or (isinstance(v, int) and not isinstance(v, bool)):
+        set_fn(int(v))
+
+
+def _opt_typed(m, name, typ, set_fn):  # OptionalBoolFromMap / OptionalStringFromMap: other types are ignored
+    v = m.get(name)
+    if isinstance(v, typ):
+        set_fn(v)
+
+
+def ParseAndValidateConfig(input_) -> UserConfig:
+    """config.go:64-148 then validate (:150-166).  Raises ValueError with the
+    reference's messages."""
+    uc = UserConfig()
+    if input_ is None:
+        return uc
+    if not isinstance(input_, dict):
+        raise ValueError("input must be a non-nil map")
+    _opt_typed(input_, "distance", str, lambda v: setattr(uc, "Distance", v))
+    _opt_int(input_, "vectorCacheMaxObjects", lambda v: setattr(uc, "VectorCacheMaxObjects", v))
+    for key, cfg in (("pq", uc.PQ), ("bq", uc.BQ)):
+        sub = input_.get(key)
+        if isinstance(sub, dict):
+            _opt_typed(sub, "enabled", bool, lambda v, c=cfg: setattr(c, "Enabled", v))
+            _opt_typed(sub, "cache", bool, lambda v, c=cfg: setattr(c, "Cache", v))
+            _opt_int(sub, "rescoreLimit", lambda v, c=cfg: setattr(c, "RescoreLimit", v))
+    if uc.PQ.Enabled:
+        raise ValueError("PQ is not currently supported for flat indices")
+    if (uc.PQ.Cache and not uc.PQ.Enabled) or (uc.BQ.Cache and not uc.BQ.Enabled):
+        raise ValueError("not possible to use the cache without compression")
+    return uc
+
+
+def extract_compression(uc: UserConfig) -> str | None:
+    """V/flat/index.go:110-124 (both enabled = none)."""
+    if uc.BQ.Enabled and uc.PQ.Enabled:
+        return None
+    return "bq" if uc.BQ.Enabled else ("pq" if uc.PQ.Enabled else None)
+
+
+def extract_compression_rescore(uc: UserConfig) -> int:
+    """V/flat/index.go:126-136."""
+    c = extract_compression(uc)
+    return uc.PQ.RescoreLimit if c == "pq" else (uc.BQ.RescoreLimit if c == "bq" else 0)
+
+
+def ValidateUserConfigUpdate(initial: UserConfig, updated: UserConfig) -> None:
+    """V/flat/index.go:751-791: distance, pq.cache, pq and bq are immutable."""
+    for name, get in (("distance", lambda c: c.Distance), ("pq.cache", lambda c: c.PQ.Cache),
+                      ("pq", lambda c: c.PQ.Enabled), ("bq", lambda c: c.BQ.Enabled)):
+        old, new = get(initial), get(updated)
+        if old != new:
+            fmt = lambda v: str(v).lower() if isinstance(v, bool) else str(v)  # Go's %v of a bool
+            raise ValueError(f'{name} is immutable: attempted change from "{fmt(old)}" to "{fmt(new)}"')
+
+
 class FlatIndex:
+    @classmethod
+    def from_user_config(cls, ctx, dims: int, uc: UserConfig, capacity: int = 1 << 16, id_base: int = 0):
+        """flat.New (V/flat/index.go:67-97): compression and rescore from the
+        user config; PQ searches uncompressed (:311-313), so it keeps no code
+        corpus here."""
+        comp = extract_compression(uc)
+        return cls(ctx, dims, uc.Distance or "cosine", "bq" if comp == "bq" else None,
+                   extract_compression_rescore(uc), capacity, id_base)
+
+    def UpdateUserConfig(self, updated: UserConfig, callback=None) -> None:
+        """V/flat/index.go:593-606: only the rescore limit takes effect."""
+        self.rescore = extract_compression_rescore(updated)
+        if callback is not None:
+            callback()
+
     def __init__(self, ctx, dims: int, distance: str = "cosine", compression: str | None = None,
                  rescore_limit: int = -1, capacity: int = 1 << 16, id_base: int = 0):
         self.ctx = ctx
