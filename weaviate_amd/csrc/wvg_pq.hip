@@ -611,11 +611,34 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_rot_kernel(ScanA
 // each add starts as soon as its value lands: 34 waits per tile, 18 % of the
 // tile's instructions); 1 = one wait per batch of NB lookups; 2 = one wait
 // per batch with the next batch's lookups already issued (software pipeline).
-template <int E, int R, int NB, int METRIC, int W = 0>
+// W = 7: one-instruction lookup addresses (PQ32_IMG7_BYTES image, below).
+//
+// The one-v_perm address (W = 7).  K8c's address of step j is
+// (code << 9) + 8x + 8j: a v_perm for code << 8 and a v_lshl_add.  Here the
+// image is split by form instead of interleaved: region A holds (lut[s][c],
+// +0.0) at byte c*256 + 8s, region B holds (+0.0, lut[s][c]) at byte
+// PQ32_IMG7_B + c*256 + 8s.  Lane x's address of step j is then
+//   8x | code << 8 | (x + j >= 32) << 16,   plus the immediate 8j:
+// an A step (x + j < 32) lands on (code, s = x + j) in region A; a B step
+// lands on 65536 + code*256 + 8(x + j) = PQ32_IMG7_B + code*256 + 8(x+j-32).
+// The three bytes come from ONE v_perm of the merged code word and a per-lane
+// constant F[j / 3] = 8x | flag(3k) << 8 | flag(3k+1) << 16 | flag(3k+2) << 24.
+// Banks (ds_read_b64, (a/4) mod 64 per 32-lane group): 2(x+j) for A lanes,
+// 2(x+j-32) for B lanes -- distinct, as in K8b.  Same sums, same results.
+constexpr uint32_t PQ32_IMG7_B = 65536u + 256u;
+constexpr uint32_t PQ32_IMG7_BYTES = PQ32_IMG7_B + 65536u;
+// LDS address of the dynamic image: the kernel's only static LDS is the
+// workgroup top-k buffer (group_combine_store: 16 waves x 64E keys x 8 B)
+template <int E>
+constexpr uint32_t PQ32_IMG7_BASE = (uint32_t)PQ_SCAN_WAVES * 64u * E * 8u;
+
+// ACT < 16 (diagnostic): only the first ACT waves of the workgroup scan (the
+// occupancy the scan needs: ACT / 4 waves per SIMD).
+template <int E, int R, int NB, int METRIC, int W = 0, int ACT = PQ_SCAN_WAVES>
 __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_dense_kernel(ScanArgs a, uint64_t *partials)
 {
     static_assert(64 % R == 0, "the ring length divides the 64-tile mask block");
-    extern __shared__ __attribute__((aligned(16))) f32x2 img[];  // [256][64]
+    extern __shared__ __attribute__((aligned(16))) f32x2 img[];  // [256][64] (W = 7: regions A and B)
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t qi = blockIdx.y;
     const float *glut = reinterpret_cast<const float *>(a.queries) + (size_t)qi * a.qpitch;
@@ -630,14 +653,20 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_dense_kernel(Sca
     for (int it = 0; it < FILL; it++) {
         const uint32_t i = (uint32_t)it * (PQ_SCAN_WAVES * 64) + threadIdx.x;
         const uint32_t s = i & 31u, c = i >> 5;
-        img[c * 64u + s] = f32x2{fv[it], 0.0f};
-        img[c * 64u + 32u + s] = f32x2{0.0f, fv[it]};
+        if constexpr (W == 7) {
+            img[c * 32u + s] = f32x2{fv[it], 0.0f};
+            img[PQ32_IMG7_B / 8u + c * 32u + s] = f32x2{0.0f, fv[it]};
+        } else {
+            img[c * 64u + s] = f32x2{fv[it], 0.0f};
+            img[c * 64u + 32u + s] = f32x2{0.0f, fv[it]};
+        }
     }
     __syncthreads();
     const uint64_t ntiles = a.tile_end - a.tile_begin;
-    const uint64_t total = (uint64_t)gridDim.x * PQ_SCAN_WAVES;
-    const uint64_t gw = (uint64_t)blockIdx.x * PQ_SCAN_WAVES + wave;
-    const uint64_t t0 = a.tile_begin + ntiles * gw / total, t1 = a.tile_begin + ntiles * (gw + 1) / total;
+    const uint64_t total = (uint64_t)gridDim.x * ACT;
+    const uint64_t gw = (uint64_t)blockIdx.x * ACT + (wave < ACT ? wave : 0);
+    uint64_t t0 = a.tile_begin + ntiles * gw / total, t1 = a.tile_begin + ntiles * (gw + 1) / total;
+    if (wave >= ACT) t1 = t0;
     WaveTopK<E> tk;
     tk.init((int)a.k);
     tk.init_fast();
@@ -655,6 +684,17 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_dense_kernel(Sca
 #pragma unroll
             for (int bb = 0; bb < 4; bb++) mk |= (4u * w + bb + x >= 32u) ? (0xFFu << (8 * bb)) : 0u;
             nmask[w] = mk;
+        }
+        uint32_t F[W == 7 ? 11 : 1];  // W = 7: 8x and the B flags of steps 3k..3k+2
+#pragma unroll
+        for (int k = 0; k < (W == 7 ? 11 : 1); k++) {
+            uint32_t f = x8;
+#pragma unroll
+            for (int b = 0; b < 3; b++) {
+                const uint32_t j = 3u * k + b;
+                f |= (j < 32u && x + j >= 32u) ? (1u << (8 * (b + 1))) : 0u;
+            }
+            F[k] = f;
         }
         const char *imgb = reinterpret_cast<const char *>(img);
         // pass order: tiles t0 + i, or t1 - 1 - i when scanning downwards (rev)
@@ -700,6 +740,19 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_dense_kernel(Sca
                 for (int w = 0; w < 8; w++)
                     asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(win[w]) : "v"(nmask[w]), "v"(ring[s][w]), "v"(ring[sc][w]));
                 auto lookup = [&](int j) {
+                    if constexpr (W == 7) {  // byte0 = 8x (F), byte1 = code, byte2 = B flag of step j (F)
+                        const uint32_t sel =
+                            0x0C000004u | ((5u + (uint32_t)(j % 3)) << 16) | ((uint32_t)(j & 3) << 8);
+                        const uint32_t off = __builtin_amdgcn_perm(F[j / 3], win[j >> 2], sel);
+                        // the image's LDS address is a compile-time constant (after the static
+                        // top-k buffer, PQ32_IMG7_BASE; the host checks it), so base + 8j is the
+                        // instruction's immediate and the address costs the v_perm only
+                        typedef const f32x2 __attribute__((address_space(3))) lds_f32x2;
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wint-to-pointer-cast"  // LDS pointers are 32-bit
+                        return *(lds_f32x2 *)(off + (PQ32_IMG7_BASE<E> + 8u * (uint32_t)j));
+#pragma clang diagnostic pop
+                    }
                     const uint32_t c8 = __builtin_amdgcn_perm(0u, win[j >> 2], 0x0C0C000Cu | ((uint32_t)(j & 3) << 8));
                     const uint32_t off = (c8 << 1) + x8;
                     return *reinterpret_cast<const f32x2 *>(imgb + off + 8 * j);
@@ -788,6 +841,191 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_dense_kernel(Sca
         }
     }
     group_combine_store<E, PQ_SCAN_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
+}
+
+// K8e: K8c's sums and the one-v_perm image (W = 7) with fewer, wider waves.
+// A/B on MI355X (profiles/r02/pq_adc/k8e_*.jsonl): letting only 8 or 12 of
+// K8c's 16 waves scan made it FASTER (0.526 -> 0.506-0.516 ms per 100M-row
+// scan) while the loads-only skeleton did not change with the wave count --
+// 16 streams per CU contend, occupancy is not what is missing.  So a
+// workgroup here has WV waves (WV = 8: two per SIMD, up to 256 VGPRs each) and
+// each wave runs TP independent tile streams (contiguous halves of its range):
+// every pass does the lookups of TP tiles in one basic block, so the adds of
+// one stream's chain fill the LDS latency of the other's.  Per stream: its own
+// buffer resource (loads past its range return zeros), ring of R tiles and
+// 64-tile mask blocks; one register top-k per wave.
+template <int E, int WV>
+constexpr uint32_t PQ32_WIDE_BASE = (uint32_t)WV * 64u * E * 8u;  // LDS address of the image (after sh[WV][64E])
+
+template <int E, int WV, int R, int NB, int TP, int METRIC>
+__global__ __launch_bounds__(WV * 64) void scan_pq32_wide_kernel(ScanArgs a, uint64_t *partials)
+{
+    static_assert(64 % R == 0, "the ring length divides the 64-tile mask block");
+    static_assert(32 % NB == 0, "LDS batches divide the 32 steps");
+    extern __shared__ __attribute__((aligned(16))) f32x2 img[];  // regions A and B (PQ32_IMG7_*)
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t qi = blockIdx.y;
+    const float *glut = reinterpret_cast<const float *>(a.queries) + (size_t)qi * a.qpitch;
+    constexpr int FILL = 32 * 256 / (WV * 64);
+    float fv[FILL];
+#pragma unroll
+    for (int it = 0; it < FILL; it++) {
+        const uint32_t i = (uint32_t)it * (WV * 64) + threadIdx.x;
+        fv[it] = glut[(i & 31u) * 256u + (i >> 5)];
+    }
+    const uint64_t ntiles = a.tile_end - a.tile_begin;
+    const uint64_t total = (uint64_t)gridDim.x * WV * TP;  // streams of the launch
+    const uint64_t g0 = ((uint64_t)blockIdx.x * WV + wave) * TP;
+    uint64_t s0[TP];
+    uint32_t n[TP];
+    uint32_t nmax = 0;
+#pragma unroll
+    for (int p = 0; p < TP; p++) {
+        s0[p] = a.tile_begin + ntiles * (g0 + p) / total;
+        n[p] = (uint32_t)(a.tile_begin + ntiles * (g0 + p + 1) / total - s0[p]);
+        nmax = n[p] > nmax ? n[p] : nmax;
+    }
+    WaveTopK<E> tk;
+    tk.init((int)a.k);
+    tk.init_fast();
+    {  // (every wave sets up and issues its first loads, so they overlap the image fill)
+        __amdgpu_buffer_rsrc_t rs[TP];
+#pragma unroll
+        for (int p = 0; p < TP; p++)
+            rs[p] = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<char *>(reinterpret_cast<const char *>(a.data)) + s0[p] * 2048u, (short)0,
+                (int)(n[p] * 2048u), 0x00020000);
+        const uint32_t voff = (uint32_t)lane * 16u;
+        const uint32_t x = (uint32_t)lane & 31u, x8 = x * 8u;
+        uint32_t nmask[8];  // bytes of step j taken from the next row (see K8b)
+#pragma unroll
+        for (int w = 0; w < 8; w++) {
+            uint32_t mk = 0u;
+#pragma unroll
+            for (int bb = 0; bb < 4; bb++) mk |= (4u * w + bb + x >= 32u) ? (0xFFu << (8 * bb)) : 0u;
+            nmask[w] = mk;
+        }
+        uint32_t F[11];  // 8x and the B flags of steps 3k..3k+2 (see PQ32_IMG7_B)
+#pragma unroll
+        for (int k = 0; k < 11; k++) {
+            uint32_t f = x8;
+#pragma unroll
+            for (int b = 0; b < 3; b++) {
+                const uint32_t j = 3u * k + b;
+                f |= (j < 32u && x + j >= 32u) ? (1u << (8 * (b + 1))) : 0u;
+            }
+            F[k] = f;
+        }
+        const bool rev = a.reverse & 1u;  // pass order: tiles s0 + i, or the stream's last - i
+        auto tile_of = [&](int p, uint32_t i) -> uint32_t { return rev ? n[p] - 1u - i : i; };
+        auto load = [&](int p, uint32_t i, uint32_t (&w)[8]) {  // the i-th tile of stream p (zeros past it)
+            const uint32_t so = i < n[p] ? tile_of(p, i) * 2048u : n[p] * 2048u;
+            const u32x4 lo = __builtin_amdgcn_raw_buffer_load_b128(rs[p], voff, so, 2);
+            const u32x4 hi = __builtin_amdgcn_raw_buffer_load_b128(rs[p], voff + 1024u, so, 2);
+            w[0] = lo.x; w[1] = lo.y; w[2] = lo.z; w[3] = lo.w;
+            w[4] = hi.x; w[5] = hi.y; w[6] = hi.z; w[7] = hi.w;
+        };
+        auto load_masks = [&](int p, uint32_t b) -> uint64_t {  // lane i: live mask of stream p's (64 b + i)-th tile
+            const uint32_t ii = b * 64u + (uint32_t)lane;
+            const uint64_t t = s0[p] + (ii < n[p] ? tile_of(p, ii) : 0u);
+            uint64_t m = 0ull;
+            if (ii < n[p]) {
+                m = a.valid[t];
+                if (a.allow) {
+                    const uint64_t wi = t - a.allow_t0;
+                    m &= wi < a.allow_words ? a.allow[wi] : 0ull;
+                }
+            }
+            return m;
+        };
+        uint64_t mcur[TP], mnxt[TP];
+        uint32_t ring[TP][R][8];
+        f32x2 acc[TP];
+#pragma unroll
+        for (int p = 0; p < TP; p++) {
+            mcur[p] = load_masks(p, 0);
+            mnxt[p] = load_masks(p, 1);
+#pragma unroll
+            for (int s = 0; s < R - 1; s++) load(p, (uint32_t)s, ring[p][s]);
+#pragma unroll
+            for (int w = 0; w < 8; w++) ring[p][R - 1][w] = 0u;
+            acc[p] = f32x2{0.0f, 0.0f};
+        }
+#pragma unroll
+        for (int it = 0; it < FILL; it++) {
+            const uint32_t i = (uint32_t)it * (WV * 64) + threadIdx.x;
+            const uint32_t s = i & 31u, c = i >> 5;
+            img[c * 32u + s] = f32x2{fv[it], 0.0f};
+            img[PQ32_IMG7_B / 8u + c * 32u + s] = f32x2{0.0f, fv[it]};
+        }
+        __syncthreads();
+        typedef const f32x2 __attribute__((address_space(3))) lds_f32x2;
+        // pass i finishes tile i-1 and starts tile i of every stream; nmax + 1 passes in groups of R
+        if (nmax > 0)
+        for (uint32_t base = 0; base <= nmax; base += R) {
+#pragma unroll
+            for (int s = 0; s < R; s++) {
+                const int sc = (s + R - 1) % R;
+                const uint32_t i = base + (uint32_t)s;
+                uint32_t win[TP][8];
+#pragma unroll
+                for (int p = 0; p < TP; p++)
+#pragma unroll
+                    for (int w = 0; w < 8; w++)
+                        asm("v_bfi_b32 %0, %1, %2, %3"
+                            : "=v"(win[p][w])
+                            : "v"(nmask[w]), "v"(ring[p][s][w]), "v"(ring[p][sc][w]));
+#pragma unroll
+                for (int h = 0; h < 32 / NB; h++) {
+                    f32x2 v[TP][NB];
+#pragma unroll
+                    for (int jj = 0; jj < NB; jj++) {
+                        const int j = h * NB + jj;
+                        const uint32_t sel =
+                            0x0C000004u | ((5u + (uint32_t)(j % 3)) << 16) | ((uint32_t)(j & 3) << 8);
+#pragma unroll
+                        for (int p = 0; p < TP; p++) {
+                            const uint32_t off = __builtin_amdgcn_perm(F[j / 3], win[p][j >> 2], sel);
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wint-to-pointer-cast"  // LDS pointers are 32-bit
+                            v[p][jj] = *(lds_f32x2 *)(off + (PQ32_WIDE_BASE<E, WV> + 8u * (uint32_t)j));
+#pragma clang diagnostic pop
+                        }
+                    }
+#pragma unroll
+                    for (int jj = 0; jj < NB; jj++)
+#pragma unroll
+                        for (int p = 0; p < TP; p++) acc[p] = acc[p] + v[p][jj];
+                }
+                if (i >= 1 && i <= nmax) {  // offer tile i-1 of every stream that has it
+                    const uint32_t tl = i - 1u;
+                    if (s == 1 && (tl & 63u) == 0u && tl != 0u) {  // (R | 64: block starts land on s == 1)
+#pragma unroll
+                        for (int p = 0; p < TP; p++) {
+                            mcur[p] = mnxt[p];
+                            mnxt[p] = load_masks(p, (tl >> 6) + 1u);
+                        }
+                    }
+#pragma unroll
+                    for (int p = 0; p < TP; p++) {
+                        if (tl < n[p]) {
+                            const uint64_t live = readlane64(mcur[p], (int)(tl & 63u));
+                            const float dist = METRIC == WVG_M_L2 ? acc[p].x
+                                               : (METRIC == WVG_M_DOT ? -acc[p].x : 1.0f - acc[p].x);
+                            tk.offer_dist_fast(dist, (uint32_t)((s0[p] + tile_of(p, tl)) * 64u) + (uint32_t)lane,
+                                               live);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int p = 0; p < TP; p++) {
+                    acc[p] = f32x2{acc[p].y, 0.0f};
+                    load(p, i + (uint32_t)R - 1u, ring[p][sc]);  // refill: tile i + R - 1
+                }
+            }
+        }
+    }
+    group_combine_store<E, WV>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
 }
 
 // K8d: K8c with the R passes of a ring cycle in ONE basic block.  K8c's
@@ -943,15 +1181,63 @@ static void launch_pq_cycle(const ScanArgs &a, uint64_t *partials, dim3 grid, di
         launch_timed((scan_pq32_cycle_kernel<E, R, NB, WVG_M_COSINE, GL>), grid, block, lds, s, a, partials);
 }
 
-template <int E, int R, int NB, int W = 0>
+template <int E, int R, int NB, int W = 0, int ACT = PQ_SCAN_WAVES>
 static void launch_pq_dense(const ScanArgs &a, uint64_t *partials, dim3 grid, dim3 block, size_t lds, hipStream_t s)
 {
     if (a.metric == WVG_M_L2 || a.metric == WVG_M_MANHATTAN || a.metric == WVG_M_HAMMING)  // Wrap = identity
-        launch_timed((scan_pq32_dense_kernel<E, R, NB, WVG_M_L2, W>), grid, block, lds, s, a, partials);
+        launch_timed((scan_pq32_dense_kernel<E, R, NB, WVG_M_L2, W, ACT>), grid, block, lds, s, a, partials);
     else if (a.metric == WVG_M_DOT)
-        launch_timed((scan_pq32_dense_kernel<E, R, NB, WVG_M_DOT, W>), grid, block, lds, s, a, partials);
+        launch_timed((scan_pq32_dense_kernel<E, R, NB, WVG_M_DOT, W, ACT>), grid, block, lds, s, a, partials);
     else
-        launch_timed((scan_pq32_dense_kernel<E, R, NB, WVG_M_COSINE, W>), grid, block, lds, s, a, partials);
+        launch_timed((scan_pq32_dense_kernel<E, R, NB, WVG_M_COSINE, W, ACT>), grid, block, lds, s, a, partials);
+}
+
+// W = 7 reads its image at the compile-time LDS address PQ32_IMG7_BASE<E>: use
+// it only where the static LDS really ends there and image + top-k buffer fit
+// the CU's 160 KiB (not for E = 4); otherwise variants 29-31 fall through to K8b
+template <int E>
+static bool img7_ok()
+{
+    static const bool ok = [] {
+        if (PQ32_IMG7_BASE<E> + PQ32_IMG7_BYTES > 160u * 1024u) return false;
+        hipFuncAttributes fa{};
+        if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(&scan_pq32_dense_kernel<E, 8, 16, WVG_M_L2, 7>)) !=
+            hipSuccess)
+            return false;
+        return fa.sharedSizeBytes == PQ32_IMG7_BASE<E>;
+    }();
+    return ok;
+}
+
+// K8e reads its image at the compile-time LDS address PQ32_WIDE_BASE: the
+// host launches an instantiation only where the static LDS really ends there
+template <int E, int WV, int R, int NB, int TP>
+static bool wide_ok()
+{
+    static const bool ok = [] {
+        if (PQ32_WIDE_BASE<E, WV> + PQ32_IMG7_BYTES > 160u * 1024u) return false;
+        hipFuncAttributes fa{};
+        if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(
+                                          &scan_pq32_wide_kernel<E, WV, R, NB, TP, WVG_M_L2>)) != hipSuccess)
+            return false;
+        return fa.sharedSizeBytes == PQ32_WIDE_BASE<E, WV>;
+    }();
+    return ok;
+}
+
+template <int E, int WV, int R, int NB, int TP>
+static bool launch_pq_wide(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
+{
+    if (!wide_ok<E, WV, R, NB, TP>()) return false;
+    const dim3 grid(groups, a.nq), block(WV * 64);
+    const uint32_t lds = PQ32_IMG7_BYTES;
+    if (a.metric == WVG_M_L2 || a.metric == WVG_M_MANHATTAN || a.metric == WVG_M_HAMMING)  // Wrap = identity
+        launch_timed((scan_pq32_wide_kernel<E, WV, R, NB, TP, WVG_M_L2>), grid, block, lds, s, a, partials);
+    else if (a.metric == WVG_M_DOT)
+        launch_timed((scan_pq32_wide_kernel<E, WV, R, NB, TP, WVG_M_DOT>), grid, block, lds, s, a, partials);
+    else
+        launch_timed((scan_pq32_wide_kernel<E, WV, R, NB, TP, WVG_M_COSINE>), grid, block, lds, s, a, partials);
+    return true;
 }
 
 template <int E>
@@ -988,6 +1274,44 @@ static hipError_t launch_pq_e(const ScanArgs &a, uint64_t *partials, int groups,
         else launch_pq_dense<E, 2, 16, 6>(a, partials, grid, block, 4 * lds, s);
         return hipGetLastError();
     }
+    if (m32 && v >= 40 && v <= 43) {
+        // K8e: 40 = 8 waves, 1 stream, ring 4 / 16; 41 = 8 waves, 1 stream, ring 2 / 16;
+        // 42 = 8 waves, 2 streams, ring 2 / 16; 43 = 8 waves, 2 streams, ring 2 / 8
+        bool ok;
+        if (v == 40) ok = launch_pq_wide<E, 8, 4, 16, 1>(a, partials, groups, s);
+        else if (v == 41) ok = launch_pq_wide<E, 8, 2, 16, 1>(a, partials, groups, s);
+        else if (v == 42) ok = launch_pq_wide<E, 8, 2, 16, 2>(a, partials, groups, s);
+        else ok = launch_pq_wide<E, 8, 2, 8, 2>(a, partials, groups, s);
+        if (ok) return hipGetLastError();
+    }
+    if (m32 && v >= 35 && v <= 39) {
+        // K8e (WV waves, TP streams per wave): 35 = 8 waves, 1 stream, ring 8 / LDS batches of 16;
+        // 36 = 8 waves, 2 streams, ring 4 / 8; 37 = 8 waves, 2 streams, ring 4 / 16;
+        // 38 = 4 waves, 2 streams, ring 8 / 16; 39 = 8 waves, 1 stream, ring 16 / 16
+        bool ok;
+        if (v == 35) ok = launch_pq_wide<E, 8, 8, 16, 1>(a, partials, groups, s);
+        else if (v == 36) ok = launch_pq_wide<E, 8, 4, 8, 2>(a, partials, groups, s);
+        else if (v == 37) ok = launch_pq_wide<E, 8, 4, 16, 2>(a, partials, groups, s);
+        else if (v == 38) ok = launch_pq_wide<E, 4, 8, 16, 2>(a, partials, groups, s);
+        else ok = launch_pq_wide<E, 8, 16, 16, 1>(a, partials, groups, s);
+        if (ok) return hipGetLastError();
+    }
+    if (m32 && v == 34) {  // diagnostic: the K8c skeleton (variant 26) with 8 of the 16 waves scanning
+        launch_pq_dense<E, 8, 16, 6, 8>(a, partials, grid, block, 4 * lds, s);
+        return hipGetLastError();
+    }
+    if (m32 && v >= 29 && v <= 33 && img7_ok<E>()) {
+        // K8c with one-v_perm lookup addresses (W = 7): 29 = ring 8 / LDS batches of 16, 30 = 8 / 8, 31 = 4 / 16;
+        // 32 / 33 = 31 with 8 / 12 of the 16 waves scanning (diagnostic: 2 / 3 waves per SIMD)
+        if (v == 29) launch_pq_dense<E, 8, 16, 7>(a, partials, grid, block, PQ32_IMG7_BYTES, s);
+        else if (v == 30) launch_pq_dense<E, 8, 8, 7>(a, partials, grid, block, PQ32_IMG7_BYTES, s);
+        else if (v == 32) launch_pq_dense<E, 4, 16, 7, 8>(a, partials, grid, block, PQ32_IMG7_BYTES, s);
+        else if (v == 33) launch_pq_dense<E, 4, 16, 7, 12>(a, partials, grid, block, PQ32_IMG7_BYTES, s);
+        else launch_pq_dense<E, 4, 16, 7>(a, partials, grid, block, PQ32_IMG7_BYTES, s);
+        return hipGetLastError();
+    }
+    // the default for m = 32, ks = 256 on mostly-live corpora without an allow list: K8e (8 waves, 2 streams)
+    if (m32 && v == 0 && a.dense && launch_pq_wide<E, 8, 4, 16, 2>(a, partials, groups, s)) return hipGetLastError();
     if (m32 && (v == 10 || v == 11 || v == 12 || (v == 0 && a.dense))) {
         // K8c (dense, issue-trimmed): 0 (auto) / 12 = ring 8 / LDS batches of 16, 10 = ring 8 / 8, 11 = ring 4 / 16
         if (v == 11)
