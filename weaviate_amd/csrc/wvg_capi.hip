@@ -1779,10 +1779,20 @@ int wvg_rescore(wvg_ctx *ctx, int metric, const float *q, const float *rows, con
     Bulk bk(ctx);
     int rc = bk.begin(cv.off);
     if (rc) return rc;
-    std::vector<float> qp((size_t)nch * 4, 0.0f);
-    std::memcpy(qp.data(), q, (size_t)dim * 4);
-    WVG_HIP(hipMemcpyAsync(bk.b + o_x, rows, n * dim * 4, hipMemcpyHostToDevice, bk.s()));
-    WVG_HIP(hipMemcpyAsync(bk.b + o_q, qp.data(), qp.size() * 4, hipMemcpyHostToDevice, bk.s()));
+    // host rows, query and results go through the slot's pinned staging: a
+    // pageable hipMemcpyAsync is a staged, blocking copy (the caller's R rows
+    // are the rescore's only sizeable transfer)
+    const size_t rows_b = n * dim * 4, q_b = (size_t)nch * 16, out_b = o_c + 4 - o_i;
+    const size_t p_q = align_up(rows_b, 256), p_out = p_q + align_up(q_b, 256);
+    void *pinv = nullptr;
+    rc = bk.g.slot->host_pinned(p_out + out_b, &pinv);
+    if (rc) return rc;
+    char *pin = (char *)pinv;
+    std::memcpy(pin, rows, rows_b);
+    std::memset(pin + p_q, 0, q_b);
+    std::memcpy(pin + p_q, q, (size_t)dim * 4);
+    WVG_HIP(hipMemcpyAsync(bk.b + o_x, pin, rows_b, hipMemcpyHostToDevice, bk.s()));
+    WVG_HIP(hipMemcpyAsync(bk.b + o_q, pin + p_q, q_b, hipMemcpyHostToDevice, bk.s()));
     WVG_HIP(launch_f32_store((const float *)(bk.b + o_x), nullptr, n, dim, nch, 0, (float *)(bk.b + o_t), bk.s()));
     WVG_HIP(launch_dist_keys(metric, (const float *)(bk.b + o_q), (const float *)(bk.b + o_t), n, dim,
                              (uint64_t *)(bk.b + o_k), bk.s(), ctx->order512));
@@ -1804,12 +1814,13 @@ int wvg_rescore(wvg_ctx *ctx, int metric, const float *q, const float *rows, con
         WVG_HIP(launch_merge_keys((const uint64_t *)(bk.b + o_k), 1, (uint32_t)n, k, 0, (uint64_t *)(bk.b + o_i),
                                   (float *)(bk.b + o_d), (uint32_t *)(bk.b + o_c), bk.s()));
     }
-    std::vector<uint64_t> idx(k);
-    uint32_t cnt = 0;
-    WVG_HIP(hipMemcpyAsync(idx.data(), bk.b + o_i, (size_t)k * 8, hipMemcpyDeviceToHost, bk.s()));
-    if (out_dists) WVG_HIP(hipMemcpyAsync(out_dists, bk.b + o_d, (size_t)k * 4, hipMemcpyDeviceToHost, bk.s()));
-    WVG_HIP(hipMemcpyAsync(&cnt, bk.b + o_c, 4, hipMemcpyDeviceToHost, bk.s()));
+    // one copy of the [ids | dists | count] span back through the staging
+    WVG_HIP(hipMemcpyAsync(pin + p_out, bk.b + o_i, out_b, hipMemcpyDeviceToHost, bk.s()));
     WVG_HIP(hipStreamSynchronize(bk.s()));
+    const uint64_t *idx = (const uint64_t *)(pin + p_out);
+    uint32_t cnt = 0;
+    std::memcpy(&cnt, pin + p_out + (o_c - o_i), 4);
+    if (out_dists) std::memcpy(out_dists, pin + p_out + (o_d - o_i), (size_t)k * 4);
     for (uint32_t i = 0; i < k; i++)  // row index -> caller's docID
         if (out_ids) out_ids[i] = i < cnt ? ids[idx[i]] : WVG_KEY_NONE;
     if (out_count) *out_count = cnt;
@@ -1987,10 +1998,16 @@ int wvg_normalize_batch(wvg_ctx *ctx, const float *X, uint64_t n, uint32_t dim, 
     Bulk bk(ctx);
     int rc = bk.begin(cv.off);
     if (rc) return rc;
-    WVG_HIP(hipMemcpyAsync(bk.b + o_x, X, n * dim * 4, hipMemcpyHostToDevice, bk.s()));
+    const size_t bytes = n * dim * 4;  // in and out through the slot's pinned staging (see wvg_rescore)
+    void *pin = nullptr;
+    rc = bk.g.slot->host_pinned(bytes, &pin);
+    if (rc) return rc;
+    std::memcpy(pin, X, bytes);
+    WVG_HIP(hipMemcpyAsync(bk.b + o_x, pin, bytes, hipMemcpyHostToDevice, bk.s()));
     WVG_HIP(launch_normalize_rows((const float *)(bk.b + o_x), n, dim, (float *)(bk.b + o_o), bk.s()));
-    WVG_HIP(hipMemcpyAsync(out, bk.b + o_o, n * dim * 4, hipMemcpyDeviceToHost, bk.s()));
+    WVG_HIP(hipMemcpyAsync(pin, bk.b + o_o, bytes, hipMemcpyDeviceToHost, bk.s()));
     WVG_HIP(hipStreamSynchronize(bk.s()));
+    std::memcpy(out, pin, bytes);
     return WVG_OK;
 }
 

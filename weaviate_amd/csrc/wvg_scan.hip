@@ -628,29 +628,43 @@ hipError_t launch_merge_pairs(const float *dists, const uint64_t *ids, uint64_t 
 
 // distancer.Normalize (D/normalize.go:16-32), one lane per row: sequential
 // unfused fp32 sum of squares, float32(sqrt(float64)), element-wise divide.
-__global__ void normalize_rows_kernel(const float *in, uint64_t n, uint32_t dim, float *out)
+// The sequential fp32 sum of Normalize (D/normalize.go:16-32) over 64 values
+// a wave holds at once (lane l: element b + l): the wave folds them in element
+// order through v_readlane, so every lane ends with the same, in-order sum.
+// One wave per row: the loads are coalesced and the 1536-long dependent add
+// chain runs on registers (one thread per row waited on a load per element).
+__device__ __forceinline__ float wave_seq_sum(float acc, float p, uint32_t cnt)
 {
-    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint32_t l = 0; l < cnt; l++) acc = acc + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p), (int)l));
+    return acc;
+}
+
+__global__ __launch_bounds__(256) void normalize_rows_kernel(const float *in, uint64_t n, uint32_t dim, float *out)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t r = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // one row per wave
     if (r >= n) return;
     const float *v = in + r * dim;
     float *o = out + r * dim;
     float norm = 0.0f;
-    for (uint32_t i = 0; i < dim; i++) {
-        float p = v[i] * v[i];
-        norm = norm + p;
+    for (uint32_t b = 0; b < dim; b += 64) {
+        const uint32_t i = b + lane;
+        const float x = i < dim ? v[i] : 0.0f;
+        const float p = x * x;
+        norm = wave_seq_sum(norm, p, dim - b < 64u ? dim - b : 64u);
     }
     if (norm == 0.0f) {
-        for (uint32_t i = 0; i < dim; i++) o[i] = 0.0f;
+        for (uint32_t i = lane; i < dim; i += 64) o[i] = 0.0f;
         return;
     }
     norm = (float)__builtin_sqrt((double)norm);
-    for (uint32_t i = 0; i < dim; i++) o[i] = v[i] / norm;
+    for (uint32_t i = lane; i < dim; i += 64) o[i] = v[i] / norm;
 }
 
 hipError_t launch_normalize_rows(const float *in, uint64_t n, uint32_t dim, float *out, hipStream_t s)
 {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(normalize_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in, n, dim, out);
+    hipLaunchKernelGGL(normalize_rows_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, in, n, dim, out);
     return hipGetLastError();
 }
 
@@ -821,26 +835,29 @@ hipError_t launch_dist_keys(int metric, const float *q, const float *tiled, uint
     return hipGetLastError();
 }
 
-// Synthetic rows for arbitrary ids, row-major (bench / test helper).
-__global__ void synth_rows_kernel(uint64_t seed_mixed, int dist, const uint64_t *ids, uint64_t n, uint32_t dim,
-                                  int normalize, float *out)
+// Synthetic rows for arbitrary ids, row-major (bench / test helper); one
+// wave per row, the normalize sum as in normalize_rows_kernel.
+__global__ __launch_bounds__(256) void synth_rows_kernel(uint64_t seed_mixed, int dist, const uint64_t *ids,
+                                                         uint64_t n, uint32_t dim, int normalize, float *out)
 {
-    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t r = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= n) return;
     const uint64_t row = ids[r];
     float norm = 1.0f;
     bool zero = false;
     if (normalize) {
         float acc = 0.0f;
-        for (uint32_t i = 0; i < dim; i++) {
-            float v = wvg_synth_value(seed_mixed, row, i, dist);
-            float p = v * v;
-            acc = acc + p;
+        for (uint32_t b = 0; b < dim; b += 64) {
+            const uint32_t i = b + lane;
+            const float v = i < dim ? wvg_synth_value(seed_mixed, row, i, dist) : 0.0f;
+            const float p = v * v;
+            acc = wave_seq_sum(acc, p, dim - b < 64u ? dim - b : 64u);
         }
         zero = acc == 0.0f;
         norm = (float)__builtin_sqrt((double)acc);
     }
-    for (uint32_t i = 0; i < dim; i++) {
+    for (uint32_t i = lane; i < dim; i += 64) {
         float x = wvg_synth_value(seed_mixed, row, i, dist);
         if (normalize) x = zero ? 0.0f : x / norm;
         out[r * dim + i] = x;
@@ -851,7 +868,7 @@ hipError_t launch_synth_rows(uint64_t seed, int dist, const uint64_t *ids, uint6
                              float *out, hipStream_t s)
 {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(synth_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, wvg_mix64(seed), dist,
+    hipLaunchKernelGGL(synth_rows_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, wvg_mix64(seed), dist,
                        ids, n, dim, normalize, out);
     return hipGetLastError();
 }
