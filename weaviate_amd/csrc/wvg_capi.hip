@@ -1010,22 +1010,22 @@ static int stage_queries(wvg_corpus *c, StreamSlot *sl, const float *queries, ui
     std::vector<float> qf;
     std::vector<uint64_t> qb;
     prepare_queries_host(c, queries, nq, qf, qb, qpitch);
+    // A copy from pageable memory returns once the source has been staged, so
+    // qf / qb may go out of scope without a stream sync (which would put a host
+    // round trip between the PQ LUT kernel and the scan).
     hipStream_t s = sl->stream;
     if (c->kind == WVG_KIND_BQ) {
         WVG_HIP(hipMemcpyAsync(dst, qb.data(), qb.size() * 8, hipMemcpyHostToDevice, s));
-        WVG_HIP(hipStreamSynchronize(s));
         return WVG_OK;
     }
     if (c->kind == WVG_KIND_F32) {
         WVG_HIP(hipMemcpyAsync(dst, qf.data(), qf.size() * 4, hipMemcpyHostToDevice, s));
-        WVG_HIP(hipStreamSynchronize(s));
         return WVG_OK;
     }
     // PQ: queries -> LUTs [nq][m*ks] (CH/product_quantization.go:329-337)
     WVG_HIP(hipMemcpyAsync(d_qtmp, qf.data(), qf.size() * 4, hipMemcpyHostToDevice, s));
     WVG_HIP(launch_pq_lut(c->metric, (const float *)d_qtmp, nq, qpitch, c->d_centers, c->pq_m, c->pq_ks, c->pq_ds,
                           d_lut_or_null, s));
-    WVG_HIP(hipStreamSynchronize(s));
     qpitch = c->pq_m * c->pq_ks;
     return WVG_OK;
 }
@@ -1104,10 +1104,18 @@ int wvg_search(wvg_corpus *c, const float *queries, uint32_t nq, uint32_t k, con
     rc = run_search(c, b + o_q, qpitch, nq, k, d_allow, p, (uint64_t *)(b + o_part), (uint64_t *)(b + o_ids),
                     (float *)(b + o_d), (uint32_t *)(b + o_cnt), s);
     if (rc) return rc;
-    if (out_ids) WVG_HIP(hipMemcpyAsync(out_ids, b + o_ids, (size_t)nq * k * 8, hipMemcpyDeviceToHost, s));
-    if (out_dists) WVG_HIP(hipMemcpyAsync(out_dists, b + o_d, (size_t)nq * k * 4, hipMemcpyDeviceToHost, s));
-    if (out_counts) WVG_HIP(hipMemcpyAsync(out_counts, b + o_cnt, (size_t)nq * 4, hipMemcpyDeviceToHost, s));
+    // results: ONE copy of the [ids | dists | counts] span into the slot's
+    // pinned staging (three pageable copies were three blocking round trips)
+    const size_t out_b = o_cnt + (size_t)nq * 4 - o_ids;
+    void *pinv = nullptr;
+    rc = g.slot->host_pinned(out_b, &pinv);
+    if (rc) return rc;
+    const char *pin = (const char *)pinv;
+    WVG_HIP(hipMemcpyAsync(pinv, b + o_ids, out_b, hipMemcpyDeviceToHost, s));
     WVG_HIP(hipStreamSynchronize(s));
+    if (out_ids) std::memcpy(out_ids, pin, (size_t)nq * k * 8);
+    if (out_dists) std::memcpy(out_dists, pin + (o_d - o_ids), (size_t)nq * k * 4);
+    if (out_counts) std::memcpy(out_counts, pin + (o_cnt - o_ids), (size_t)nq * 4);
     return WVG_OK;
 }
 
