@@ -85,11 +85,18 @@ def test_known_answers_on_gpu(ctx):
     assert s == 12.5
 
 
-def test_normalize_bitexact(ctx, orc):
+@pytest.mark.parametrize("d", [1, 63, 64, 65, 77, 128, 1536])
+def test_normalize_bitexact(ctx, orc, d):
+    """normalize_rows_kernel (one wave per row, the sum folded in element order
+    through v_readlane) = Normalize's sequential fp32 sum (D/normalize.go:16-32),
+    for dims around the 64-element block, zero rows and non-finite elements."""
     from weaviate_amd.distancer import Normalize
 
-    X = orc.synth_rows(11, 0, 300, 77, 0)
+    X = orc.synth_rows(11 + d, 0, 300, d, 0) * np.float32(3e3)
     X[3] = 0
+    X[5, d // 2] = np.inf
+    X[7, d - 1] = np.nan
+    X[9] = np.float32(1e-30)  # squares underflow: a zero norm
     assert np.array_equal(bits(Normalize(ctx, X)), bits(orc.normalize_rows(X)))
 
 
@@ -340,13 +347,14 @@ def test_rescore_host_rows(ctx, orc, metric):
     assert np.array_equal(oi, ids[li.astype(np.int64)]) and np.array_equal(bits(od), bits(ld))
 
 
-def test_synthetic_rows_helper(ctx, orc):
+@pytest.mark.parametrize("d", [96, 1, 65, 1536])
+def test_synthetic_rows_helper(ctx, orc, d):
     lib = _lib.load()
-    ids = np.array([5, 0, 999_999, 123_456_789], np.uint64)
+    ids = np.array([5, 0, 999_999, 123_456_789, 7, 8, 9], np.uint64)  # 7 rows: two workgroups of 4 waves
     for norm in [0, 1]:
-        out = np.empty((len(ids), 96), np.float32)
-        _lib.check(lib.wvg_synthetic_rows(ctx.handle, 42, _lib.u64ptr(ids), len(ids), 96, 0, norm, _lib.fptr(out)))
-        want = np.stack([orc.synth_rows(42, int(i), 1, 96, 0)[0] for i in ids])
+        out = np.empty((len(ids), d), np.float32)
+        _lib.check(lib.wvg_synthetic_rows(ctx.handle, 42, _lib.u64ptr(ids), len(ids), d, 0, norm, _lib.fptr(out)))
+        want = np.stack([orc.synth_rows(42, int(i), 1, d, 0)[0] for i in ids])
         if norm:
             want = orc.normalize_rows(want)
         assert np.array_equal(bits(out), bits(want))
