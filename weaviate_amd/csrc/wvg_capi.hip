@@ -139,6 +139,42 @@ struct SlotGuard {
     }
 };
 
+// Host bytes of one call in the slot's pinned buffer.  A copy from pageable
+// memory is a staged, blocking round trip (~16 us each for a few hundred
+// bytes on MI355X: tools/latency_probe.py), so a call's small inputs and its
+// results go through here.  The call reserves every piece up front (the
+// buffer may only move before the first copy is queued) and the region is
+// not reused before the call's closing stream sync.  Pieces above
+// STAGE_MAX stay pageable (their fixed cost is noise; pinned memory is not).
+constexpr size_t STAGE_MAX = (size_t)8 << 20;
+static size_t stage_bytes(size_t bytes) { return bytes <= STAGE_MAX ? align_up(bytes, 64) : 0; }
+struct Staging {
+    char *p = nullptr;
+    size_t off = 0, cap = 0;
+    int reserve(StreamSlot *sl, size_t bytes)
+    {
+        void *v = nullptr;
+        const int rc = sl->host_pinned(std::max<size_t>(bytes, 64), &v);
+        p = (char *)v;
+        cap = bytes;
+        off = 0;
+        return rc;
+    }
+    char *take(size_t bytes)  // a reserved piece (stage_bytes(bytes) of it)
+    {
+        char *r = p + off;
+        off += align_up(bytes, 64);
+        return r;
+    }
+    hipError_t h2d(void *dst, const void *src, size_t bytes, hipStream_t s)
+    {
+        if (bytes > STAGE_MAX) return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
+        char *r = take(bytes);
+        std::memcpy(r, src, bytes);
+        return hipMemcpyAsync(dst, r, bytes, hipMemcpyHostToDevice, s);
+    }
+};
+
 struct Bulk {
     SlotGuard g;
     char *b = nullptr;
@@ -1005,7 +1041,7 @@ static void write_empty(uint32_t nq, uint32_t k, uint64_t *ids, float *dists, ui
 }
 
 static int stage_queries(wvg_corpus *c, StreamSlot *sl, const float *queries, uint32_t nq, char *dst, uint32_t &qpitch,
-                         float *d_lut_or_null, char *d_qtmp)
+                         float *d_lut_or_null, char *d_qtmp, Staging *st = nullptr)
 {
     std::vector<float> qf;
     std::vector<uint64_t> qb;
@@ -1014,16 +1050,19 @@ static int stage_queries(wvg_corpus *c, StreamSlot *sl, const float *queries, ui
     // qf / qb may go out of scope without a stream sync (which would put a host
     // round trip between the PQ LUT kernel and the scan).
     hipStream_t s = sl->stream;
+    auto h2d = [&](void *d, const void *h, size_t bytes) {
+        return st ? st->h2d(d, h, bytes, s) : hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s);
+    };
     if (c->kind == WVG_KIND_BQ) {
-        WVG_HIP(hipMemcpyAsync(dst, qb.data(), qb.size() * 8, hipMemcpyHostToDevice, s));
+        WVG_HIP(h2d(dst, qb.data(), qb.size() * 8));
         return WVG_OK;
     }
     if (c->kind == WVG_KIND_F32) {
-        WVG_HIP(hipMemcpyAsync(dst, qf.data(), qf.size() * 4, hipMemcpyHostToDevice, s));
+        WVG_HIP(h2d(dst, qf.data(), qf.size() * 4));
         return WVG_OK;
     }
     // PQ: queries -> LUTs [nq][m*ks] (CH/product_quantization.go:329-337)
-    WVG_HIP(hipMemcpyAsync(d_qtmp, qf.data(), qf.size() * 4, hipMemcpyHostToDevice, s));
+    WVG_HIP(h2d(d_qtmp, qf.data(), qf.size() * 4));
     WVG_HIP(launch_pq_lut(c->metric, (const float *)d_qtmp, nq, qpitch, c->d_centers, c->pq_m, c->pq_ks, c->pq_ds,
                           d_lut_or_null, s));
     qpitch = c->pq_m * c->pq_ks;
@@ -1049,6 +1088,12 @@ static size_t query_bytes(const wvg_corpus *c, uint32_t nq)
     case WVG_KIND_BQ: return (size_t)nq * bq_chunks(c->dim) * 16;
     default: return (size_t)nq * c->pq_m * c->pq_ks * 4;
     }
+}
+
+// Upper bound of the host bytes stage_queries copies (a Staging reservation).
+static size_t staged_query_bytes(const wvg_corpus *c, uint32_t nq)
+{
+    return std::max(query_bytes(c, nq), (size_t)nq * c->dim * 4);
 }
 
 }  // extern "C"
@@ -1093,25 +1138,28 @@ int wvg_search(wvg_corpus *c, const float *queries, uint32_t nq, uint32_t k, con
     if (rc) return rc;
     char *b = (char *)base;
     hipStream_t s = g.slot->stream;
+    // queries, allow words and the [ids | dists | counts] result span through
+    // the slot's pinned staging: one copy each way, no pageable round trips
+    const size_t out_b = o_cnt + (size_t)nq * 4 - o_ids;
+    Staging st;
+    rc = st.reserve(g.slot, stage_bytes(staged_query_bytes(c, nq)) +
+                                (p.allow_host ? stage_bytes(p.allow_bytes()) : 0) + stage_bytes(out_b));
+    if (rc) return rc;
     uint32_t qpitch = 0;
-    rc = stage_queries(c, g.slot, queries, nq, b + o_q, qpitch, (float *)(b + o_q), b + o_qtmp);
+    rc = stage_queries(c, g.slot, queries, nq, b + o_q, qpitch, (float *)(b + o_q), b + o_qtmp, &st);
     if (rc) return rc;
     const uint64_t *d_allow = nullptr;
     if (p.allow_host) {
-        WVG_HIP(hipMemcpyAsync(b + o_allow, p.allow_host, p.allow_bytes(), hipMemcpyHostToDevice, s));
+        WVG_HIP(st.h2d(b + o_allow, p.allow_host, p.allow_bytes(), s));
         d_allow = (const uint64_t *)(b + o_allow);
     }
     rc = run_search(c, b + o_q, qpitch, nq, k, d_allow, p, (uint64_t *)(b + o_part), (uint64_t *)(b + o_ids),
                     (float *)(b + o_d), (uint32_t *)(b + o_cnt), s);
     if (rc) return rc;
-    // results: ONE copy of the [ids | dists | counts] span into the slot's
-    // pinned staging (three pageable copies were three blocking round trips)
-    const size_t out_b = o_cnt + (size_t)nq * 4 - o_ids;
-    void *pinv = nullptr;
-    rc = g.slot->host_pinned(out_b, &pinv);
-    if (rc) return rc;
-    const char *pin = (const char *)pinv;
-    WVG_HIP(hipMemcpyAsync(pinv, b + o_ids, out_b, hipMemcpyDeviceToHost, s));
+    const char *pin = out_b <= STAGE_MAX ? st.take(out_b) : nullptr;
+    std::vector<char> big(pin ? 0 : out_b);
+    if (!pin) pin = big.data();
+    WVG_HIP(hipMemcpyAsync((void *)pin, b + o_ids, out_b, hipMemcpyDeviceToHost, s));
     WVG_HIP(hipStreamSynchronize(s));
     if (out_ids) std::memcpy(out_ids, pin, (size_t)nq * k * 8);
     if (out_dists) std::memcpy(out_dists, pin + (o_d - o_ids), (size_t)nq * k * 4);
@@ -1986,13 +2034,18 @@ int wvg_distance_batch(wvg_ctx *ctx, int metric, const float *q, const float *X,
     if (rc) return rc;
     std::vector<float> qp((size_t)nch * 4, 0.0f);
     std::memcpy(qp.data(), q, (size_t)dim * 4);
-    WVG_HIP(hipMemcpyAsync(bk.b + o_x, X, n * dim * 4, hipMemcpyHostToDevice, bk.s()));
-    WVG_HIP(hipMemcpyAsync(bk.b + o_q, qp.data(), qp.size() * 4, hipMemcpyHostToDevice, bk.s()));
+    Staging st;  // rows (up to STAGE_MAX), query and distances through the slot's pinned staging
+    rc = st.reserve(bk.g.slot, stage_bytes(n * dim * 4) + stage_bytes(qp.size() * 4) + stage_bytes(n * 4));
+    if (rc) return rc;
+    WVG_HIP(st.h2d(bk.b + o_x, X, n * dim * 4, bk.s()));
+    WVG_HIP(st.h2d(bk.b + o_q, qp.data(), qp.size() * 4, bk.s()));
     WVG_HIP(launch_f32_store((const float *)(bk.b + o_x), nullptr, n, dim, nch, 0, (float *)(bk.b + o_t), bk.s()));
     WVG_HIP(launch_distance_rows(metric, (const float *)(bk.b + o_q), (const float *)(bk.b + o_t), n, dim,
                                  (float *)(bk.b + o_o), bk.s(), ctx->order512));
-    WVG_HIP(hipMemcpyAsync(out, bk.b + o_o, n * 4, hipMemcpyDeviceToHost, bk.s()));
+    char *pin = n * 4 <= STAGE_MAX ? st.take(n * 4) : nullptr;
+    WVG_HIP(hipMemcpyAsync(pin ? (void *)pin : (void *)out, bk.b + o_o, n * 4, hipMemcpyDeviceToHost, bk.s()));
     WVG_HIP(hipStreamSynchronize(bk.s()));
+    if (pin) std::memcpy(out, pin, n * 4);
     return WVG_OK;
 }
 
@@ -2323,13 +2376,25 @@ int wvg_corpus_distance_by_ids(wvg_corpus *c, const float *query, const uint64_t
     if (rc) return rc;
     char *b = (char *)base;
     hipStream_t s = g.slot->stream;
-    uint32_t qpitch = 0;
-    rc = stage_queries(c, g.slot, query, 1, b + o_q, qpitch, (float *)(b + o_q), b + o_qtmp);
+    const size_t out_b = o_ok + n - o_d;  // [dists | ok]
+    Staging st;
+    rc = st.reserve(g.slot, stage_bytes(staged_query_bytes(c, 1)) + stage_bytes(n * 8) + stage_bytes(out_b));
     if (rc) return rc;
-    WVG_HIP(hipMemcpyAsync(b + o_ids, ids, n * 8, hipMemcpyHostToDevice, s));
+    uint32_t qpitch = 0;
+    rc = stage_queries(c, g.slot, query, 1, b + o_q, qpitch, (float *)(b + o_q), b + o_qtmp, &st);
+    if (rc) return rc;
+    WVG_HIP(st.h2d(b + o_ids, ids, n * 8, s));
     ScanArgs a = scan_args_for(c, b + o_q, qpitch, 1, 1, nullptr, 0, tiles_of(c->high_water));
     WVG_HIP(launch_dist_by_ids(a, c->kind, c->capacity, (const uint64_t *)(b + o_ids), n, (float *)(b + o_d),
                                (uint8_t *)(b + o_ok), s));
+    if (out_b <= STAGE_MAX) {
+        char *pin = st.take(out_b);
+        WVG_HIP(hipMemcpyAsync(pin, b + o_d, out_b, hipMemcpyDeviceToHost, s));
+        WVG_HIP(hipStreamSynchronize(s));
+        std::memcpy(out_dists, pin, n * 4);
+        std::memcpy(out_ok, pin + (o_ok - o_d), n);
+        return WVG_OK;
+    }
     WVG_HIP(hipMemcpyAsync(out_dists, b + o_d, n * 4, hipMemcpyDeviceToHost, s));
     WVG_HIP(hipMemcpyAsync(out_ok, b + o_ok, n, hipMemcpyDeviceToHost, s));
     WVG_HIP(hipStreamSynchronize(s));
