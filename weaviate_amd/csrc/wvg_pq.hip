@@ -857,7 +857,7 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_dense_kernel(Sca
 template <int E, int WV>
 constexpr uint32_t PQ32_WIDE_BASE = (uint32_t)WV * 64u * E * 8u;  // LDS address of the image (after sh[WV][64E])
 
-template <int E, int WV, int R, int NB, int TP, int METRIC>
+template <int E, int WV, int R, int NB, int TP, int METRIC, bool IL = false>
 __global__ __launch_bounds__(WV * 64) void scan_pq32_wide_kernel(ScanArgs a, uint64_t *partials)
 {
     static_assert(64 % R == 0, "the ring length divides the 64-tile mask block");
@@ -874,17 +874,30 @@ __global__ __launch_bounds__(WV * 64) void scan_pq32_wide_kernel(ScanArgs a, uin
         fv[it] = glut[(i & 31u) * 256u + (i >> 5)];
     }
     const uint64_t ntiles = a.tile_end - a.tile_begin;
-    const uint64_t total = (uint64_t)gridDim.x * WV * TP;  // streams of the launch
-    const uint64_t g0 = ((uint64_t)blockIdx.x * WV + wave) * TP;
+    // IL (A/B, TP = 1): the workgroup owns one contiguous range and its waves
+    // take every WV-th tile of it (the CU streams one 16 KiB block at a time)
+    static_assert(!IL || TP == 1, "interleaved waves run one stream");
+    constexpr uint32_t STRIDE = IL ? WV : 1;  // tiles between a stream's consecutive tiles
     uint64_t s0[TP];
     uint32_t n[TP];
     uint32_t nmax = 0;
+    if constexpr (IL) {
+        const uint64_t w0 = a.tile_begin + ntiles * blockIdx.x / gridDim.x;
+        const uint64_t w1 = a.tile_begin + ntiles * (blockIdx.x + 1) / gridDim.x;
+        s0[0] = w0 + wave;
+        n[0] = s0[0] < w1 ? (uint32_t)((w1 - s0[0] + WV - 1) / WV) : 0u;
+        nmax = n[0];
+    } else {
+        const uint64_t total = (uint64_t)gridDim.x * WV * TP;  // streams of the launch
+        const uint64_t g0 = ((uint64_t)blockIdx.x * WV + wave) * TP;
 #pragma unroll
-    for (int p = 0; p < TP; p++) {
-        s0[p] = a.tile_begin + ntiles * (g0 + p) / total;
-        n[p] = (uint32_t)(a.tile_begin + ntiles * (g0 + p + 1) / total - s0[p]);
-        nmax = n[p] > nmax ? n[p] : nmax;
+        for (int p = 0; p < TP; p++) {
+            s0[p] = a.tile_begin + ntiles * (g0 + p) / total;
+            n[p] = (uint32_t)(a.tile_begin + ntiles * (g0 + p + 1) / total - s0[p]);
+            nmax = n[p] > nmax ? n[p] : nmax;
+        }
     }
+    auto span = [&](int p) -> uint32_t { return n[p] ? ((n[p] - 1u) * STRIDE + 1u) * 2048u : 0u; };  // bytes
     WaveTopK<E> tk;
     tk.init((int)a.k);
     tk.init_fast();
@@ -894,7 +907,7 @@ __global__ __launch_bounds__(WV * 64) void scan_pq32_wide_kernel(ScanArgs a, uin
         for (int p = 0; p < TP; p++)
             rs[p] = __builtin_amdgcn_make_buffer_rsrc(
                 const_cast<char *>(reinterpret_cast<const char *>(a.data)) + s0[p] * 2048u, (short)0,
-                (int)(n[p] * 2048u), 0x00020000);
+                (int)span(p), 0x00020000);
         const uint32_t voff = (uint32_t)lane * 16u;
         const uint32_t x = (uint32_t)lane & 31u, x8 = x * 8u;
         uint32_t nmask[8];  // bytes of step j taken from the next row (see K8b)
@@ -919,7 +932,7 @@ __global__ __launch_bounds__(WV * 64) void scan_pq32_wide_kernel(ScanArgs a, uin
         const bool rev = a.reverse & 1u;  // pass order: tiles s0 + i, or the stream's last - i
         auto tile_of = [&](int p, uint32_t i) -> uint32_t { return rev ? n[p] - 1u - i : i; };
         auto load = [&](int p, uint32_t i, uint32_t (&w)[8]) {  // the i-th tile of stream p (zeros past it)
-            const uint32_t so = i < n[p] ? tile_of(p, i) * 2048u : n[p] * 2048u;
+            const uint32_t so = i < n[p] ? tile_of(p, i) * (STRIDE * 2048u) : span(p);
             const u32x4 lo = __builtin_amdgcn_raw_buffer_load_b128(rs[p], voff, so, 2);
             const u32x4 hi = __builtin_amdgcn_raw_buffer_load_b128(rs[p], voff + 1024u, so, 2);
             w[0] = lo.x; w[1] = lo.y; w[2] = lo.z; w[3] = lo.w;
@@ -927,7 +940,7 @@ __global__ __launch_bounds__(WV * 64) void scan_pq32_wide_kernel(ScanArgs a, uin
         };
         auto load_masks = [&](int p, uint32_t b) -> uint64_t {  // lane i: live mask of stream p's (64 b + i)-th tile
             const uint32_t ii = b * 64u + (uint32_t)lane;
-            const uint64_t t = s0[p] + (ii < n[p] ? tile_of(p, ii) : 0u);
+            const uint64_t t = s0[p] + (uint64_t)(ii < n[p] ? tile_of(p, ii) : 0u) * STRIDE;
             uint64_t m = 0ull;
             if (ii < n[p]) {
                 m = a.valid[t];
@@ -1012,8 +1025,9 @@ __global__ __launch_bounds__(WV * 64) void scan_pq32_wide_kernel(ScanArgs a, uin
                             const uint64_t live = readlane64(mcur[p], (int)(tl & 63u));
                             const float dist = METRIC == WVG_M_L2 ? acc[p].x
                                                : (METRIC == WVG_M_DOT ? -acc[p].x : 1.0f - acc[p].x);
-                            tk.offer_dist_fast(dist, (uint32_t)((s0[p] + tile_of(p, tl)) * 64u) + (uint32_t)lane,
-                                               live);
+                            tk.offer_dist_fast(
+                                dist, (uint32_t)((s0[p] + (uint64_t)tile_of(p, tl) * STRIDE) * 64u) + (uint32_t)lane,
+                                live);
                         }
                     }
                 }
@@ -1211,32 +1225,32 @@ static bool img7_ok()
 
 // K8e reads its image at the compile-time LDS address PQ32_WIDE_BASE: the
 // host launches an instantiation only where the static LDS really ends there
-template <int E, int WV, int R, int NB, int TP>
+template <int E, int WV, int R, int NB, int TP, bool IL = false>
 static bool wide_ok()
 {
     static const bool ok = [] {
         if (PQ32_WIDE_BASE<E, WV> + PQ32_IMG7_BYTES > 160u * 1024u) return false;
         hipFuncAttributes fa{};
         if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(
-                                          &scan_pq32_wide_kernel<E, WV, R, NB, TP, WVG_M_L2>)) != hipSuccess)
+                                          &scan_pq32_wide_kernel<E, WV, R, NB, TP, WVG_M_L2, IL>)) != hipSuccess)
             return false;
         return fa.sharedSizeBytes == PQ32_WIDE_BASE<E, WV>;
     }();
     return ok;
 }
 
-template <int E, int WV, int R, int NB, int TP>
+template <int E, int WV, int R, int NB, int TP, bool IL = false>
 static bool launch_pq_wide(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
 {
-    if (!wide_ok<E, WV, R, NB, TP>()) return false;
+    if (!wide_ok<E, WV, R, NB, TP, IL>()) return false;
     const dim3 grid(groups, a.nq), block(WV * 64);
     const uint32_t lds = PQ32_IMG7_BYTES;
     if (a.metric == WVG_M_L2 || a.metric == WVG_M_MANHATTAN || a.metric == WVG_M_HAMMING)  // Wrap = identity
-        launch_timed((scan_pq32_wide_kernel<E, WV, R, NB, TP, WVG_M_L2>), grid, block, lds, s, a, partials);
+        launch_timed((scan_pq32_wide_kernel<E, WV, R, NB, TP, WVG_M_L2, IL>), grid, block, lds, s, a, partials);
     else if (a.metric == WVG_M_DOT)
-        launch_timed((scan_pq32_wide_kernel<E, WV, R, NB, TP, WVG_M_DOT>), grid, block, lds, s, a, partials);
+        launch_timed((scan_pq32_wide_kernel<E, WV, R, NB, TP, WVG_M_DOT, IL>), grid, block, lds, s, a, partials);
     else
-        launch_timed((scan_pq32_wide_kernel<E, WV, R, NB, TP, WVG_M_COSINE>), grid, block, lds, s, a, partials);
+        launch_timed((scan_pq32_wide_kernel<E, WV, R, NB, TP, WVG_M_COSINE, IL>), grid, block, lds, s, a, partials);
     return true;
 }
 
@@ -1274,6 +1288,16 @@ static hipError_t launch_pq_e(const ScanArgs &a, uint64_t *partials, int groups,
         else launch_pq_dense<E, 2, 16, 6>(a, partials, grid, block, 4 * lds, s);
         return hipGetLastError();
     }
+    if (m32 && (v == 46 || v == 47)) {  // K8e with interleaved waves (IL): 46 = 8 waves, ring 4 / 16; 47 = ring 8 / 16
+        if (v == 46 ? launch_pq_wide<E, 8, 4, 16, 1, true>(a, partials, groups, s)
+                    : launch_pq_wide<E, 8, 8, 16, 1, true>(a, partials, groups, s))
+            return hipGetLastError();
+    }
+    if (m32 && (v == 44 || v == 45)) {  // K8e 8 waves, 1 stream, ring 4, LDS batches of 8 / 32
+        if (v == 44 ? launch_pq_wide<E, 8, 4, 8, 1>(a, partials, groups, s)
+                    : launch_pq_wide<E, 8, 4, 32, 1>(a, partials, groups, s))
+            return hipGetLastError();
+    }
     if (m32 && v >= 40 && v <= 43) {
         // K8e: 40 = 8 waves, 1 stream, ring 4 / 16; 41 = 8 waves, 1 stream, ring 2 / 16;
         // 42 = 8 waves, 2 streams, ring 2 / 16; 43 = 8 waves, 2 streams, ring 2 / 8
@@ -1310,8 +1334,8 @@ static hipError_t launch_pq_e(const ScanArgs &a, uint64_t *partials, int groups,
         else launch_pq_dense<E, 4, 16, 7>(a, partials, grid, block, PQ32_IMG7_BYTES, s);
         return hipGetLastError();
     }
-    // the default for m = 32, ks = 256 on mostly-live corpora without an allow list: K8e (8 waves, 2 streams)
-    if (m32 && v == 0 && a.dense && launch_pq_wide<E, 8, 4, 16, 2>(a, partials, groups, s)) return hipGetLastError();
+    // the default for m = 32, ks = 256 on mostly-live corpora without an allow list: K8e (8 waves, ring 4)
+    if (m32 && v == 0 && a.dense && launch_pq_wide<E, 8, 4, 16, 1>(a, partials, groups, s)) return hipGetLastError();
     if (m32 && (v == 10 || v == 11 || v == 12 || (v == 0 && a.dense))) {
         // K8c (dense, issue-trimmed): 0 (auto) / 12 = ring 8 / LDS batches of 16, 10 = ring 8 / 8, 11 = ring 4 / 16
         if (v == 11)
