@@ -1,3 +1,4 @@
+import ctypes
 """GPU parity tests: the HIP path (through the C ABI) against the oracle on the
 same seeded inputs, bit-exact for distances / codes / ids.
 
@@ -408,6 +409,54 @@ def test_pq_scan_parity(ctx, orc, metric):
     ids2, dists2, _ = c2.search(q, 10)
     ids1, dists1, _ = c.search(q, 10)
     assert np.array_equal(ids1, ids2)
+
+
+def _tuning(key, value):
+    lib = _lib.load()
+    lib.wvgx_set_tuning.restype = ctypes.c_int
+    lib.wvgx_set_tuning.argtypes = [ctypes.c_int, ctypes.c_int]
+    return lib.wvgx_set_tuning(key, value)
+
+
+@pytest.mark.parametrize("min3", [1, 0])
+def test_pq_encode_argmin_ties_and_nonfinite(ctx, orc, min3):
+    """nNearest's rule (CH/kmeans.go:126-130: replace on !(minD < d)) under the
+    encoder's min3 pair argmin (tuning key 14 = 1) and the plain loop (0):
+    exact ties inside a centroid pair and across pairs go to the highest
+    index, rows with NaN take the reference loop, rows whose every distance
+    overflows to +inf keep centroid 0, and a codebook holding a NaN disables
+    the min3 path."""
+    from weaviate_amd.compressionhelpers import ProductQuantizer
+
+    m, ks, d = 32, 256, 128
+    centers = _codebook(orc, m, ks, d // m, 910)
+    centers[:, 9] = centers[:, 8]      # a tie inside pair 4
+    centers[:, 201] = centers[:, 8]    # ... and with a later pair
+    centers[:, 130] = centers[:, 131]  # a tie inside pair 65 only
+    X = orc.synth_rows(911, 0, 700, d, 0)
+    X[:4] = centers[np.arange(m)[None, :], np.array([[8] * m] * 4)].reshape(4, d)   # d = 0 at 8, 9, 201
+    X[4:8] = centers[np.arange(m)[None, :], np.array([[131] * m] * 4)].reshape(4, d)  # d = 0 at 130, 131
+    X[8, 5] = np.nan                   # segment 1 of row 8: NaN distances
+    X[70, 127] = np.nan                # a NaN in the second wave of the batch
+    X[9, 12:16] = np.float32(3e38)     # segment 3: every distance overflows to +inf
+    X[10, 0:4] = np.inf                # segment 0: +inf distances
+    old = _tuning(14, min3)
+    try:
+        for cb in (centers, None):
+            if cb is None:  # NaN in the codebook: the pair path must not use min3
+                cb = centers.copy()
+                cb[2, 17, 1] = np.nan
+            want = orc.pq_encode(X, cb)
+            pq = ProductQuantizer(ctx, cb)
+            assert np.array_equal(pq.EncodeBatch(X), want)
+            c = Corpus(ctx, KIND_PQ, METRIC_L2, d, len(X))
+            c.set_codebook(cb)
+            c.upsert(np.arange(len(X), dtype=np.uint64), X)
+            got = c.get_batch(np.arange(len(X), dtype=np.uint64), pq_m=m)[0]
+            assert np.array_equal(got, want)
+            c.destroy()
+    finally:
+        _tuning(14, old)
 
 
 def test_pq_encode_corpus(ctx, orc):

@@ -583,7 +583,7 @@ static int store_rows(wvg_corpus *c, StreamSlot *sl, const float *vectors, const
         uint8_t *codes = (uint8_t *)(b + o_codes);
         float *tile = (float *)(b + o_tile);
         WVG_HIP(launch_f32_store(src, nullptr, nr, d, f32_chunks(d), 0, tile, s));
-        WVG_HIP(launch_pq_encode(tile, nr, d, c->d_centers, c->pq_m, c->pq_ks, codes, s));
+        WVG_HIP(launch_pq_encode(tile, nr, d, c->d_centers, c->pq_m, c->pq_ks, codes, s, false, c->pq_nan_free));
         WVG_HIP(launch_pq_store(codes, d_slots, nr, c->pq_m, c->nchunks, (uint8_t *)c->d_data, s));
         break;
     }
@@ -866,6 +866,7 @@ int wvg_pq_set_codebook(wvg_corpus *c, const float *centers, uint32_t m, uint32_
     c->pq_m = m;
     c->pq_ks = ks;
     c->pq_ds = ds;
+    c->pq_nan_free = pq_nan_free(centers, (size_t)m * ks * ds);
     c->nchunks = pq_chunks(m);
     if (realloc) {
         const uint64_t cap = c->capacity;
@@ -1901,7 +1902,7 @@ int wvg_pq_encode_corpus(wvg_corpus *pq, wvg_corpus *f32)
     if (rc) return rc;
     hipStream_t s = g.slot->stream;
     WVG_HIP(launch_pq_encode((const float *)f32->d_data, tiles_of(hw) * 64, pq->dim, pq->d_centers, pq->pq_m,
-                             pq->pq_ks, (uint8_t *)pq->d_data, s, true));
+                             pq->pq_ks, (uint8_t *)pq->d_data, s, true, pq->pq_nan_free));
     const uint64_t tiles = tiles_of(hw);
     WVG_HIP(hipMemcpyAsync(pq->d_valid, f32->d_valid, tiles * 8, hipMemcpyDeviceToDevice, s));
     WVG_HIP(hipStreamSynchronize(s));
@@ -1936,7 +1937,7 @@ int wvg_synthetic_rows(wvg_ctx *ctx, uint64_t seed, const uint64_t *ids, uint64_
 // Internal A/B knob (not part of include/wvgpu.h): 0 = K1 scan variant,
 // 1 = K1 resident workgroups per CU, ... 7 = K8 ADC variant, 8 = query-stream merge wait (us),
 // 9 = serpentine scan order, 10 = K3b row-range length, 11 = K1 load policy, 12 = K3b SIMD pairing,
-// 13 = K3b partner priority.  Returns the previous value.
+// 13 = K3b partner priority, 14 = PQ encode min3 argmin.  Returns the previous value.
 int wvgx_set_tuning(int key, int value)
 {
     Tuning &t = tuning();
@@ -1983,6 +1984,9 @@ int wvgx_set_tuning(int key, int value)
     } else if (key == 13) {
         old = t.gemm_prio;
         t.gemm_prio = value;
+    } else if (key == 14) {
+        old = t.pq_encode_min3;
+        t.pq_encode_min3 = value;
     }
     return old;
 }
@@ -2145,7 +2149,7 @@ int wvg_pq_encode(wvg_ctx *ctx, const float *centers, uint32_t m, uint32_t ks, c
                                hipMemcpyHostToDevice, bk.s()));
     WVG_HIP(launch_f32_store((const float *)(bk.b + o_x), nullptr, n, dim, nch, 0, (float *)(bk.b + o_t), bk.s()));
     WVG_HIP(launch_pq_encode((const float *)(bk.b + o_t), n, dim, (const float *)(bk.b + o_c), m, ks,
-                             (uint8_t *)(bk.b + o_o), bk.s()));
+                             (uint8_t *)(bk.b + o_o), bk.s(), false, pq_nan_free(centers, (size_t)m * ks * ds)));
     WVG_HIP(hipMemcpyAsync(out_codes, bk.b + o_o, n * m, hipMemcpyDeviceToHost, bk.s()));
     WVG_HIP(hipStreamSynchronize(bk.s()));
     return WVG_OK;

@@ -73,6 +73,7 @@ struct wvg_corpus {
     // PQ codebook (kind == PQ)
     float *d_centers = nullptr;    // [m][ks][ds]
     uint32_t pq_m = 0, pq_ks = 0, pq_ds = 0;
+    bool pq_nan_free = false;      // the codebook has no NaN (launch_pq_encode)
     std::shared_mutex rw;          // shared: search; exclusive: upsert/delete/grow
     std::atomic<uint64_t> scan_serial{0};  // query scans issued so far (parity = next scan direction)
 };
@@ -265,6 +266,8 @@ struct Tuning {
                                // -1 = one long range per workgroup (one wave of workgroups; A/B)
     int gemm_pairing = 0;    // K3b QH = 2: SIMD partners share rows (0) or queries (1) (A/B)
     int gemm_prio = 0;       // K3b: s_setprio 1 for the second wave of each SIMD (A/B)
+    int pq_encode_min3 = 1;  // PQ encode pair path: min3 argmin on NaN-free codebooks (1) or the
+                             // reference's compare-and-select loop everywhere (0; A/B and parity)
 };
 Tuning &tuning();
 // Profiling: events armed by the host runtime (wvg_profile_start) are bound to
@@ -339,8 +342,16 @@ hipError_t launch_pq_lut(int metric, const float *q, uint32_t nq, uint32_t qpitc
                          const float *centers, uint32_t m, uint32_t ks, uint32_t ds, float *lut,
                          hipStream_t s);
 // codes: row-major [n][m] bytes, or (tiled_out) the PQ corpus layout at slots 0..n-1.
+// nan_free: the codebook holds no NaN (enables the pair path's min3 argmin, pq_encode_kernel).
 hipError_t launch_pq_encode(const float *tiled_rows, uint64_t n, uint32_t dim, const float *centers,
-                            uint32_t m, uint32_t ks, uint8_t *codes, hipStream_t s, bool tiled_out = false);
+                            uint32_t m, uint32_t ks, uint8_t *codes, hipStream_t s, bool tiled_out = false,
+                            bool nan_free = false);
+inline bool pq_nan_free(const float *centers, size_t count)
+{
+    for (size_t i = 0; i < count; i++)
+        if (centers[i] != centers[i]) return false;
+    return true;
+}
 hipError_t launch_pq_store(const uint8_t *codes, const uint64_t *slots, uint64_t n, uint32_t m,
                            uint32_t nchunks, uint8_t *tiled, hipStream_t s);
 hipError_t launch_pq_adc_rows(int metric, const float *lut, uint32_t m, uint32_t ks,

@@ -119,10 +119,21 @@ typedef float f32x2e __attribute__((ext_vector_type(2)));
 // pairs (DS == 4, even ks; may be null): the codebook with centroids c and
 // c+1 interleaved per coordinate, [m][ks/2][4][2] (pq_pair_layout), so one
 // scalar register pair feeds a packed op on two centroids at once.
+// Argmin in the pair path.  The reference keeps a centroid when
+// !(minD < d) (CH/kmeans.go:126-130): without NaN distances the result is the
+// LAST index at the global minimum, so the loop only tracks the running
+// minimum (one v_min3_f32 per pair) and the last PAIR that holds it (two
+// compares and one select), and the winner inside that pair is decided once
+// at the end by recomputing its two distances (the same ops, the same bits):
+// 5 VALU per pair for the argmin instead of 8 (two compares, four selects and
+// two index moves).  NaN distances need a NaN in the row's segment or in a
+// centroid (centroid - row with finite centroids is never NaN: x = +-inf gives
+// +inf); `nan_free` says the codebook has none, and a wave whose segment has a
+// NaN takes the reference loop.
 template <int DS, bool TILED_OUT>
 __global__ void pq_encode_kernel(const float4 *__restrict__ tiled, uint64_t n, uint32_t dim, uint32_t nchunks,
                                  const float *__restrict__ centers, uint32_t m, uint32_t ks, uint32_t ds_rt,
-                                 uint8_t *__restrict__ codes, const float *__restrict__ pairs)
+                                 uint8_t *__restrict__ codes, const float *__restrict__ pairs, int nan_free)
 {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
@@ -141,7 +152,39 @@ __global__ void pq_encode_kernel(const float4 *__restrict__ tiled, uint64_t n, u
             if constexpr (DS == 4) {
                 // segment s is exactly chunk s (dim = 4m): one 16-byte load, scalar unfused path (n < 8)
                 const float4 x = rp[(size_t)s * 64];
-                if (pairs) {
+                const bool row_nan = !(x.x == x.x && x.y == x.y && x.z == x.z && x.w == x.w);
+                if (pairs && nan_free && __ballot(row_nan) == 0ull) {  // (see the argmin note above)
+                    const f32x2e xx = {x.x, x.x}, xy = {x.y, x.y}, xz = {x.z, x.z}, xw = {x.w, x.w};
+                    const __attribute__((address_space(4))) float *cp =
+                        (const __attribute__((address_space(4))) float *)(pairs + (size_t)s * ks * 4);
+                    auto pair_sum = [&](const float *pp) {  // (c - x)^2 summed in k order for centroids 2p, 2p+1
+                        const f32x2e d0 = f32x2e{pp[0], pp[1]} - xx, d1 = f32x2e{pp[2], pp[3]} - xy;
+                        const f32x2e d2 = f32x2e{pp[4], pp[5]} - xz, d3 = f32x2e{pp[6], pp[7]} - xw;
+                        f32x2e sum = d0 * d0;
+                        sum = sum + d1 * d1;
+                        sum = sum + d2 * d2;
+                        sum = sum + d3 * d3;
+                        return sum;
+                    };
+                    float mn = minD;
+                    uint32_t bp = 0;
+#pragma unroll 4
+                    for (uint32_t p = 0; p < ks / 2; p++) {
+                        const __attribute__((address_space(4))) float *pp = cp + (size_t)p * 8;
+                        const f32x2e d0 = f32x2e{pp[0], pp[1]} - xx, d1 = f32x2e{pp[2], pp[3]} - xy;
+                        const f32x2e d2 = f32x2e{pp[4], pp[5]} - xz, d3 = f32x2e{pp[6], pp[7]} - xw;
+                        f32x2e sum = d0 * d0;
+                        sum = sum + d1 * d1;
+                        sum = sum + d2 * d2;
+                        sum = sum + d3 * d3;
+                        const float m2 = __builtin_fminf(__builtin_fminf(mn, sum.x), sum.y);
+                        if ((sum.x == m2) | (sum.y == m2)) bp = p;
+                        mn = m2;
+                    }
+                    const f32x2e sb = pair_sum(pairs + ((size_t)s * ks + 2 * bp) * 4);
+                    best = sb.y == mn ? 2 * bp + 1 : 2 * bp;  // 0 when nothing beat math.MaxFloat32
+                    minD = mn;
+                } else if (pairs) {
                     // two centroids per packed op: (c_k - x_k)^2 summed in k order,
                     // exactly the scalar path's sub, mul, add sequence per lane
                     const f32x2e xx = {x.x, x.x}, xy = {x.y, x.y}, xz = {x.z, x.z}, xw = {x.w, x.w};
@@ -225,7 +268,7 @@ __global__ void pq_encode_kernel(const float4 *__restrict__ tiled, uint64_t n, u
 }
 
 hipError_t launch_pq_encode(const float *tiled, uint64_t n, uint32_t dim, const float *centers, uint32_t m,
-                            uint32_t ks, uint8_t *codes, hipStream_t s, bool tiled_out)
+                            uint32_t ks, uint8_t *codes, hipStream_t s, bool tiled_out, bool nan_free)
 {
     if (n == 0) return hipSuccess;
     const uint32_t ds = dim / m, nchunks = f32_chunks(dim);
@@ -233,20 +276,21 @@ hipError_t launch_pq_encode(const float *tiled, uint64_t n, uint32_t dim, const 
     const float4 *t4 = reinterpret_cast<const float4 *>(tiled);
     // codebook buffers (pq_centers_alloc_bytes) carry the pair layout after the table
     const float *pairs = pq_has_pairs(ks, ds) ? centers + (size_t)m * ks * ds : nullptr;
+    nan_free = nan_free && tuning().pq_encode_min3 != 0;
     if (ds == 4 && dim == 4 * m) {
         if (tiled_out)
             hipLaunchKernelGGL((pq_encode_kernel<4, true>), grid, block, 0, s, t4, n, dim, nchunks, centers, m, ks, ds,
-                               codes, pairs);
+                               codes, pairs, (int)nan_free);
         else
             hipLaunchKernelGGL((pq_encode_kernel<4, false>), grid, block, 0, s, t4, n, dim, nchunks, centers, m, ks, ds,
-                               codes, pairs);
+                               codes, pairs, (int)nan_free);
     } else {
         if (tiled_out)
             hipLaunchKernelGGL((pq_encode_kernel<0, true>), grid, block, 0, s, t4, n, dim, nchunks, centers, m, ks, ds,
-                               codes, nullptr);
+                               codes, nullptr, 0);
         else
             hipLaunchKernelGGL((pq_encode_kernel<0, false>), grid, block, 0, s, t4, n, dim, nchunks, centers, m, ks, ds,
-                               codes, nullptr);
+                               codes, nullptr, 0);
     }
     return hipGetLastError();
 }
