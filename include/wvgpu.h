@@ -64,6 +64,13 @@ int wvg_device_count(int *out);
 int wvg_open(int device, wvg_ctx **out);
 int wvg_close(wvg_ctx *ctx);
 int wvg_synchronize(wvg_ctx *ctx);
+/* Page-locked host memory for a caller's reusable staging buffers (e.g. the
+ * R rows flat.searchByVectorBQ gathers for its rescore, V/flat/index.go:375-385):
+ * every entry point copies from / to such a buffer directly, without its own
+ * staging copy.  Any other host pointer keeps working (copied through the
+ * call's staging).  Free with wvg_host_free on the same context. */
+int wvg_host_alloc(wvg_ctx *ctx, uint64_t bytes, void **out);
+int wvg_host_free(wvg_ctx *ctx, void *p);
 /* The reduction order of the fp32 distances (l2 / dot / cosine), i.e. which
  * of the reference's SIMD kernels the results must match bit for bit: its
  * init() picks l2_512 / dot_512 on hosts with AMX-BF16 and AVX-512, else

@@ -281,3 +281,41 @@ def test_serpentine_scan_order_does_not_change_results(ctx, orc):
             assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(z).view(np.uint8))
     for c in (f, pq, bq):
         c.destroy()
+
+
+def test_pinned_host_buffers(ctx, orc):
+    """wvg_host_alloc buffers go straight to the copies (no staging copy); the
+    results equal those from ordinary (pageable) host memory."""
+    import ctypes as ct
+
+    from weaviate_amd._lib import METRIC_COSINE, METRIC_L2, check, fptr, u32ptr, u64ptr
+
+    lib = ctx.lib
+    R, d, k = 200, 1536, 10
+    ids = np.arange(7000, 7000 + R, dtype=np.uint64)
+    rows = np.empty((R, d), np.float32)
+    check(lib.wvg_synthetic_rows(ctx.handle, 42, u64ptr(ids), R, d, 0, 1, fptr(rows)))
+    pinned = ctx.host_array((R, d), np.float32)
+    try:
+        check(lib.wvg_synthetic_rows(ctx.handle, 42, u64ptr(ids), R, d, 0, 1, fptr(pinned)))  # D2H into it
+        assert np.array_equal(pinned.view(np.uint32), rows.view(np.uint32))
+        q = orc.normalize(orc.synth_rows(43, 0, 1, d, 0)[0])
+        outs = []
+        for src in (rows, pinned):
+            oi, od, oc = np.empty(k, np.uint64), np.empty(k, np.float32), np.zeros(1, np.uint32)
+            check(lib.wvg_rescore(ctx.handle, METRIC_COSINE, fptr(q), fptr(src), u64ptr(ids), R, d, k, u64ptr(oi),
+                                  fptr(od), u32ptr(oc)))
+            outs.append((oi.copy(), od.view(np.uint32).copy(), int(oc[0])))
+        assert outs[0][2] == k and np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+        d1, d2 = np.empty(R, np.float32), np.empty(R, np.float32)
+        check(lib.wvg_distance_batch(ctx.handle, METRIC_L2, fptr(q), fptr(rows), R, d, fptr(d1)))
+        check(lib.wvg_distance_batch(ctx.handle, METRIC_L2, fptr(q), fptr(pinned), R, d, fptr(d2)))
+        assert np.array_equal(d1.view(np.uint32), d2.view(np.uint32))
+        want = orc.dist_all(orc.L2, q, rows)
+        assert np.array_equal(d1.view(np.uint32), np.asarray(want, np.float32).view(np.uint32))
+    finally:
+        ctx.free_host_array(pinned)
+    check(lib.wvg_host_free(ctx.handle, None))  # null is a no-op
+    p = ct.c_void_p()
+    check(lib.wvg_host_alloc(ctx.handle, 0, ct.byref(p)))
+    assert not p.value

@@ -38,6 +38,8 @@ SIGNATURES = {
     "wvg_open": (c_int, [c_int, _P(c_void_p)]),
     "wvg_close": (c_int, [c_void_p]),
     "wvg_synchronize": (c_int, [c_void_p]),
+    "wvg_host_alloc": (c_int, [c_void_p, c_uint64, POINTER(c_void_p)]),
+    "wvg_host_free": (c_int, [c_void_p, c_void_p]),
     "wvg_set_distance_order": (c_int, [c_void_p, c_int]),
     "wvg_corpus_create": (c_int, [c_void_p, c_int, c_int, c_uint32, c_uint64, c_uint64, _P(c_void_p)]),
     "wvg_corpus_destroy": (c_int, [c_void_p]),

@@ -148,6 +148,18 @@ struct SlotGuard {
 // STAGE_MAX stay pageable (their fixed cost is noise; pinned memory is not).
 constexpr size_t STAGE_MAX = (size_t)8 << 20;
 static size_t stage_bytes(size_t bytes) { return bytes <= STAGE_MAX ? align_up(bytes, 64) : 0; }
+// True for page-locked host memory (wvg_host_alloc / hipHostMalloc): a copy
+// from it needs no staging.
+static bool host_pinned_ptr(const void *p)
+{
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();  // an unregistered pointer reports an error: clear it
+        return false;
+    }
+    return at.type == hipMemoryTypeHost;
+}
+
 struct Staging {
     char *p = nullptr;
     size_t off = 0, cap = 0;
@@ -168,7 +180,7 @@ struct Staging {
     }
     hipError_t h2d(void *dst, const void *src, size_t bytes, hipStream_t s)
     {
-        if (bytes > STAGE_MAX) return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
+        if (bytes > STAGE_MAX || host_pinned_ptr(src)) return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
         char *r = take(bytes);
         std::memcpy(r, src, bytes);
         return hipMemcpyAsync(dst, r, bytes, hipMemcpyHostToDevice, s);
@@ -373,6 +385,29 @@ int wvg_synchronize(wvg_ctx *ctx)
     if (!ctx) return fail(WVG_ERR_INVALID, "null ctx");
     WVG_HIP(hipSetDevice(ctx->device));
     WVG_HIP(hipDeviceSynchronize());
+    return WVG_OK;
+}
+
+int wvg_host_alloc(wvg_ctx *ctx, uint64_t bytes, void **out)
+{
+    if (!ctx || !out) return fail(WVG_ERR_INVALID, "null argument");
+    *out = nullptr;
+    if (bytes == 0) return WVG_OK;
+    WVG_HIP(hipSetDevice(ctx->device));
+    hipError_t e = hipHostMalloc(out, bytes, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        *out = nullptr;
+        return fail(WVG_ERR_NOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+    }
+    return WVG_OK;
+}
+
+int wvg_host_free(wvg_ctx *ctx, void *p)
+{
+    if (!ctx) return fail(WVG_ERR_INVALID, "null context");
+    if (!p) return WVG_OK;
+    WVG_HIP(hipSetDevice(ctx->device));
+    WVG_HIP(hipHostFree(p));
     return WVG_OK;
 }
 
@@ -1840,16 +1875,14 @@ int wvg_rescore(wvg_ctx *ctx, int metric, const float *q, const float *rows, con
     // pageable hipMemcpyAsync is a staged, blocking copy (the caller's R rows
     // are the rescore's only sizeable transfer)
     const size_t rows_b = n * dim * 4, q_b = (size_t)nch * 16, out_b = o_c + 4 - o_i;
-    const size_t p_q = align_up(rows_b, 256), p_out = p_q + align_up(q_b, 256);
-    void *pinv = nullptr;
-    rc = bk.g.slot->host_pinned(p_out + out_b, &pinv);
+    const bool rows_pinned = host_pinned_ptr(rows);  // a wvg_host_alloc buffer: copied from directly
+    Staging st;
+    rc = st.reserve(bk.g.slot, (rows_pinned ? 0 : stage_bytes(rows_b)) + stage_bytes(q_b) + stage_bytes(out_b));
     if (rc) return rc;
-    char *pin = (char *)pinv;
-    std::memcpy(pin, rows, rows_b);
-    std::memset(pin + p_q, 0, q_b);
-    std::memcpy(pin + p_q, q, (size_t)dim * 4);
-    WVG_HIP(hipMemcpyAsync(bk.b + o_x, pin, rows_b, hipMemcpyHostToDevice, bk.s()));
-    WVG_HIP(hipMemcpyAsync(bk.b + o_q, pin + p_q, q_b, hipMemcpyHostToDevice, bk.s()));
+    WVG_HIP(st.h2d(bk.b + o_x, rows, rows_b, bk.s()));
+    std::vector<float> qp((size_t)nch * 4, 0.0f);
+    std::memcpy(qp.data(), q, (size_t)dim * 4);
+    WVG_HIP(st.h2d(bk.b + o_q, qp.data(), q_b, bk.s()));
     WVG_HIP(launch_f32_store((const float *)(bk.b + o_x), nullptr, n, dim, nch, 0, (float *)(bk.b + o_t), bk.s()));
     WVG_HIP(launch_dist_keys(metric, (const float *)(bk.b + o_q), (const float *)(bk.b + o_t), n, dim,
                              (uint64_t *)(bk.b + o_k), bk.s(), ctx->order512));
@@ -1872,12 +1905,13 @@ int wvg_rescore(wvg_ctx *ctx, int metric, const float *q, const float *rows, con
                                   (float *)(bk.b + o_d), (uint32_t *)(bk.b + o_c), bk.s()));
     }
     // one copy of the [ids | dists | count] span back through the staging
-    WVG_HIP(hipMemcpyAsync(pin + p_out, bk.b + o_i, out_b, hipMemcpyDeviceToHost, bk.s()));
+    char *pin = st.take(out_b);
+    WVG_HIP(hipMemcpyAsync(pin, bk.b + o_i, out_b, hipMemcpyDeviceToHost, bk.s()));
     WVG_HIP(hipStreamSynchronize(bk.s()));
-    const uint64_t *idx = (const uint64_t *)(pin + p_out);
+    const uint64_t *idx = (const uint64_t *)pin;
     uint32_t cnt = 0;
-    std::memcpy(&cnt, pin + p_out + (o_c - o_i), 4);
-    if (out_dists) std::memcpy(out_dists, pin + p_out + (o_d - o_i), (size_t)k * 4);
+    std::memcpy(&cnt, pin + (o_c - o_i), 4);
+    if (out_dists) std::memcpy(out_dists, pin + (o_d - o_i), (size_t)k * 4);
     for (uint32_t i = 0; i < k; i++)  // row index -> caller's docID
         if (out_ids) out_ids[i] = i < cnt ? ids[idx[i]] : WVG_KEY_NONE;
     if (out_count) *out_count = cnt;
@@ -1926,7 +1960,10 @@ int wvg_synthetic_rows(wvg_ctx *ctx, uint64_t seed, const uint64_t *ids, uint64_
     Bulk bk(ctx);
     int rc = bk.begin(cv.off);
     if (rc) return rc;
-    WVG_HIP(hipMemcpyAsync(bk.b + o_i, ids, n * 8, hipMemcpyHostToDevice, bk.s()));
+    Staging st;
+    rc = st.reserve(bk.g.slot, stage_bytes(n * 8));
+    if (rc) return rc;
+    WVG_HIP(st.h2d(bk.b + o_i, ids, n * 8, bk.s()));
     WVG_HIP(launch_synth_rows(seed, distribution, (const uint64_t *)(bk.b + o_i), n, dim, normalize,
                               (float *)(bk.b + o_o), bk.s()));
     WVG_HIP(hipMemcpyAsync(out, bk.b + o_o, n * dim * 4, hipMemcpyDeviceToHost, bk.s()));

@@ -39,6 +39,24 @@ class Context:
     def synchronize(self) -> None:
         check(self.lib.wvg_synchronize(self.handle))
 
+    def host_array(self, shape, dtype=np.float32):
+        """wvg_host_alloc: a numpy array over page-locked host memory, which the
+        entry points copy from / to without a staging copy; freed with
+        free_host_array (the array must not be used afterwards)."""
+        dt = np.dtype(dtype)
+        n = int(np.prod(shape)) * dt.itemsize
+        p = c_void_p()
+        check(self.lib.wvg_host_alloc(self.handle, max(n, 1), byref(p)))
+        buf = (ctypes.c_uint8 * max(n, 1)).from_address(p.value)
+        arr = np.frombuffer(buf, dtype=np.uint8, count=n).view(dt).reshape(shape)
+        self._pinned = getattr(self, "_pinned", {})
+        self._pinned[arr.ctypes.data] = p
+        return arr
+
+    def free_host_array(self, arr) -> None:
+        p = self._pinned.pop(arr.ctypes.data)
+        check(self.lib.wvg_host_free(self.handle, p))
+
     def set_distance_order(self, order: int) -> None:
         """wvg_set_distance_order: _lib.ORDER_AVX256 (default) or ORDER_AVX512
         (the kernels Weaviate dispatches on AMX + AVX-512 hosts)."""
