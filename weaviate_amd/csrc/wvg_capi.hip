@@ -348,6 +348,7 @@ int wvg_open(int device, wvg_ctx **out)
     c->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     if (const char *e = getenv("WVG_MFMA_MIN_QUERIES")) c->mfma_min_nq = (uint32_t)strtoul(e, nullptr, 10);
     if (const char *e = getenv("WVG_SERPENTINE")) tuning().serpentine = (int)strtol(e, nullptr, 10);  // A/B runs
+    if (const char *e = getenv("WVG_K1_TAIL")) tuning().k1_tail = (int)strtol(e, nullptr, 10);        // A/B runs
     if (const char *e = getenv("WVG_K1_LOADS")) tuning().k1_loads = (int)strtol(e, nullptr, 10);        // A/B runs
     *out = c;
     return WVG_OK;
@@ -988,6 +989,28 @@ static int plain_loads(const wvg_corpus *c, uint64_t tb, uint64_t te)
     return c->kind == WVG_KIND_F32 && (te - tb) * (uint64_t)c->nchunks * 1024ull <= (800ull << 20);
 }
 
+// K1 cache tail: with serpentine scans (consecutive scans alternate
+// direction) the next scan starts on the rows this one read last, so each
+// wave reads the last ~320 MB worth of its pass with the default policy (the
+// 256 MiB Infinity Cache plus the L2s keep them) and the rest non-temporal
+// (which does not evict them).  1M x 128 (512 MB): tail 160/256 -> 13.95k ->
+// 14.80k QPS; 128/256: 14.74k; all default-policy: 13.95k
+// (profiles/r02/bench/k1_cache_tail_ab.txt).  Scans that fit are all default
+// policy (plain_loads).
+constexpr uint64_t K1_CACHE_BYTES = 320000000ull;
+static uint32_t k1_cache_tail(const wvg_corpus *c, uint64_t tb, uint64_t te)
+{
+    const int v = tuning().k1_tail;
+    // F32 scans only: the same split in K8e's PQ code loads (tail 25/256 at 100M
+    // codes) measured no gain -- that scan is not purely memory-bound
+    if (c->kind != WVG_KIND_F32 || v < 0) return 0u;
+    if (v > 0) return (uint32_t)std::min(v, 256);
+    if (!tuning().serpentine || tuning().k1_loads) return 0u;  // no reversal / a forced policy (A/B)
+    const uint64_t bytes = (te - tb) * (uint64_t)c->nchunks * 1024ull;
+    if (bytes <= K1_CACHE_BYTES) return 0u;
+    return (uint32_t)std::max<uint64_t>(1, (256ull * K1_CACHE_BYTES) / bytes);
+}
+
 struct SearchPlan {
     uint64_t tb = 0, te = 0;
     int groups = 1;      // scan: workgroups per query; gemm: row ranges
@@ -1051,6 +1074,7 @@ static int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t 
     a.dense = pq_dense(c, d_allow);
     a.order512 = c->ctx->order512;
     a.plain = plain_loads(c, p.tb, p.te);
+    a.cache_tail256 = k1_cache_tail(c, p.tb, p.te);
     if (!p.gemm) a.reverse = next_direction(c, 1);
     ProfArm arm(c->ctx);
     if (arm.rc) return arm.rc;
@@ -1742,6 +1766,7 @@ int wvg_search_device_pipelined(wvg_corpus *c, const float *d_queries, uint32_t 
         a.reverse = next_direction(c, nq);
         a.order512 = c->ctx->order512;
         a.plain = plain_loads(c, p.tb, p.te);
+    a.cache_tail256 = k1_cache_tail(c, p.tb, p.te);
         WVG_HIP(hipMemsetAsync(j.arrivals, 0, align_up((size_t)nq * 4, 16), s));
         ProfArm arm(c->ctx);
         if (arm.rc) return arm.rc;
@@ -1766,6 +1791,7 @@ int wvg_search_device_pipelined(wvg_corpus *c, const float *d_queries, uint32_t 
     a.k = k;
     a.order512 = c->ctx->order512;
     a.plain = plain_loads(c, p.tb, p.te);
+    a.cache_tail256 = k1_cache_tail(c, p.tb, p.te);
     const uint32_t dir0 = next_direction(c, nq);
     for (uint32_t i = 0; i < nq; i++) {
         a.queries = d_queries + (size_t)i * c->dim;

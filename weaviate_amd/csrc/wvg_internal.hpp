@@ -210,6 +210,9 @@ struct ScanArgs {
     int order512;              // F32 distances in the AVX-512 kernels' order (wvg_set_distance_order)
     int plain;                 // F32 K1 row loads with the default cache policy instead of non-temporal
                                // (scanned bytes within a few x the Infinity Cache: plain_loads())
+    uint32_t cache_tail256;    // K1 (A/B): if > 0, each wave reads the last cache_tail256/256 of its pass
+                               // with the default policy and the rest non-temporal -- the serpentine's
+                               // next pass starts on exactly those rows
 };
 // Phase 1 writes dense partials [nq][groups][K] (keys, KEY_NONE = empty).
 int scan_groups_for(const ScanArgs &a, int num_cus);
@@ -266,6 +269,8 @@ struct Tuning {
                                // -1 = one long range per workgroup (one wave of workgroups; A/B)
     int gemm_pairing = 0;    // K3b QH = 2: SIMD partners share rows (0) or queries (1) (A/B)
     int gemm_prio = 0;       // K3b: s_setprio 1 for the second wave of each SIMD (A/B)
+    int k1_tail = 0;         // K1 cache_tail256: 0 = auto (k1_cache_tail), -1 = off (plain_loads() policy
+                             // for the whole pass), 1..256 = forced (A/B; env WVG_K1_TAIL)
     int pq_encode_min3 = 1;  // PQ encode pair path: min3 argmin on NaN-free codebooks (1) or the
                              // reference's compare-and-select loop everywhere (0; A/B and parity)
 };

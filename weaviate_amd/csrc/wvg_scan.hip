@@ -123,6 +123,8 @@ __device__ __forceinline__ void scan_tiles(const ScanArgs &a, const float4 *q4, 
     const int lane = threadIdx.x & 63;
     const float4 *data = reinterpret_cast<const float4 *>(a.data);
     const uint64_t n = t1 - t0;
+    // passes i >= split load with the default policy (cache_tail256: only the tail of the pass)
+    const uint64_t split = a.cache_tail256 ? n - ((n * a.cache_tail256) >> 8) : (a.plain ? 0 : n);
     uint64_t m_next = n ? tile_mask(a, rev ? t1 - 1 : t0) : 0ull;
     for (uint64_t i = 0; i < n; ++i) {
         const uint64_t t = rev ? t1 - 1 - i : t0 + i;
@@ -134,7 +136,7 @@ __device__ __forceinline__ void scan_tiles(const ScanArgs &a, const float4 *q4, 
         if (a.order512)  // wave-uniform: the AVX-512 kernels' order (generic length)
             r = row_dist_512<METRIC, 64>(rp, q4, (int)a.dim);
         else if constexpr (D > 0)
-            r = a.plain ? row_dot_or_l2_fixed<METRIC, D, 64, false>(rp, q4) : row_dot_or_l2_fixed<METRIC, D, 64>(rp, q4);
+            r = i >= split ? row_dot_or_l2_fixed<METRIC, D, 64, false>(rp, q4) : row_dot_or_l2_fixed<METRIC, D, 64>(rp, q4);
         else
             r = row_dot_or_l2_generic<METRIC, 64>(rp, q4, (int)a.dim);
         tk.offer(lane_key(m, wrap_metric(a.metric, r), t, lane));
