@@ -309,6 +309,10 @@ def run_flat1m(args, world, rank, dev, torch, dist):
             "queries_per_launch": B,
             "algorithmic_bytes_per_launch": bytes_per_launch,
             "launches": int(launches.value),
+            "note": ("every query is a full scan (N*d*4 algorithmic bytes); consecutive scans alternate "
+                     "direction and each reads the last ~320 MB of its pass with the default cache policy "
+                     "(k1_cache_tail), so the next scan starts on rows held by the 256 MiB Infinity Cache + "
+                     "L2s -- FETCH_SIZE (`traffic`) counts those Infinity-Cache hits as fetched bytes"),
         },
         "cpu_baseline": None,
     }
