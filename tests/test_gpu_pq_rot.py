@@ -105,7 +105,7 @@ def test_rot_equals_gather_variant(ctx, orc, big, metric):
         for k, al in [(10, None), (64, allow), (150, None)]:
             _variant(1)
             b = c.search(qs, k, allow=al)
-            for v in (0, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 29, 30, 31, 32, 33, 35, 36, 37, 38, 39, 40, 41, 42, 43, 44, 45, 46, 47):
+            for v in (0, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 29, 30, 31, 32, 33, 35, 36, 37, 38, 39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 49):
                 # K8b: ring 6, ring 4, interleaved waves, LDS batches 32 / 8, dense (no tile skip) rings 6 / 4 / 8;
                 # K8c rings 8 / 4 / 8; K8b forced; K8d (buffer / global loads); K8c one-v_perm addresses; K8e
                 _variant(v)

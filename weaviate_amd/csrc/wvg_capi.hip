@@ -1015,6 +1015,7 @@ struct SearchPlan {
     uint64_t tb = 0, te = 0;
     int groups = 1;      // scan: workgroups per query; gemm: row ranges
     bool gemm = false;   // K3 batched MFMA path
+    bool cosched = false; // PQ batch: co-scheduled K8e (ScanArgs::cosched)
     bool empty = false;
     const uint64_t *allow_host = nullptr;  // the caller's allow words of tiles [tb, te), or null
     size_t allow_bytes() const { return allow_host ? (size_t)(te - tb) * 8 : 0; }
@@ -1045,6 +1046,11 @@ static SearchPlan plan_search(wvg_corpus *c, uint32_t nq, uint32_t k, const uint
         p.groups = (int)gemm_row_ranges(nq, std::max<uint64_t>(1, p.te - p.tb), c->ctx->num_cus, c->dim, k);
     else
         p.groups = scan_groups_for(a, c->ctx->num_cus);
+    // PQ batches: the nq queries of one row range run side by side on one XCD and share its L2
+    p.cosched = c->kind == WVG_KIND_PQ && c->pq_m == 32 && c->pq_ks == 256 && nq > 1 && !allow &&
+                pq_dense(c, nullptr) && tuning().pq_cosched != 0 &&
+                (tuning().pq_variant == 0 || tuning().pq_variant == 48 || tuning().pq_variant == 49);
+    if (p.cosched) p.groups = pq_cosched_groups(nq, c->ctx->num_cus);
     return p;
 }
 
@@ -1072,6 +1078,7 @@ static int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t 
     a.pq_m = c->pq_m;
     a.pq_ks = c->pq_ks;
     a.dense = pq_dense(c, d_allow);
+    a.cosched = p.cosched;
     a.order512 = c->ctx->order512;
     a.plain = plain_loads(c, p.tb, p.te);
     a.cache_tail256 = k1_cache_tail(c, p.tb, p.te);
@@ -2000,7 +2007,7 @@ int wvg_synthetic_rows(wvg_ctx *ctx, uint64_t seed, const uint64_t *ids, uint64_
 // Internal A/B knob (not part of include/wvgpu.h): 0 = K1 scan variant,
 // 1 = K1 resident workgroups per CU, ... 7 = K8 ADC variant, 8 = query-stream merge wait (us),
 // 9 = serpentine scan order, 10 = K3b row-range length, 11 = K1 load policy, 12 = K3b SIMD pairing,
-// 13 = K3b partner priority, 14 = PQ encode min3 argmin.  Returns the previous value.
+// 13 = K3b partner priority, 14 = PQ encode min3 argmin, 15 = co-scheduled PQ batches.  Returns the previous value.
 int wvgx_set_tuning(int key, int value)
 {
     Tuning &t = tuning();
@@ -2050,6 +2057,9 @@ int wvgx_set_tuning(int key, int value)
     } else if (key == 14) {
         old = t.pq_encode_min3;
         t.pq_encode_min3 = value;
+    } else if (key == 15) {
+        old = t.pq_cosched;
+        t.pq_cosched = value;
     }
     return old;
 }

@@ -207,6 +207,8 @@ struct ScanArgs {
                                // alternates between calls (wvg_corpus::scan_serial): consecutive scans then
                                // begin where the previous one ended, on rows still in the Infinity Cache
     int dense;                 // PQ m = 32: no allow list and mostly-live rows -> K8c (no tile skipping)
+    int cosched;               // PQ m = 32 dense, nq > 1: K8e with a 1D grid whose consecutive workgroups
+                               // on one XCD are the nq queries of one row range (pq_cosched_groups)
     int order512;              // F32 distances in the AVX-512 kernels' order (wvg_set_distance_order)
     int plain;                 // F32 K1 row loads with the default cache policy instead of non-temporal
                                // (scanned bytes within a few x the Infinity Cache: plain_loads())
@@ -216,6 +218,13 @@ struct ScanArgs {
 };
 // Phase 1 writes dense partials [nq][groups][K] (keys, KEY_NONE = empty).
 int scan_groups_for(const ScanArgs &a, int num_cus);
+// Row ranges per query of a co-scheduled PQ batch: a multiple of 8 (XCDs) with
+// ranges x nq ~ one workgroup per CU.
+inline int pq_cosched_groups(uint32_t nq, int num_cus)
+{
+    const int g = num_cus / (int)(nq ? nq : 1) / 8;
+    return 8 * (g > 0 ? g : 1);
+}
 hipError_t launch_scan_f32(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s);
 // Query-stream K1 (wvg_search_device_pipelined): ONE launch scans a.nq queries
 // back to back, every query a full scan of the corpus.  `groups` scan
@@ -269,6 +278,7 @@ struct Tuning {
                                // -1 = one long range per workgroup (one wave of workgroups; A/B)
     int gemm_pairing = 0;    // K3b QH = 2: SIMD partners share rows (0) or queries (1) (A/B)
     int gemm_prio = 0;       // K3b: s_setprio 1 for the second wave of each SIMD (A/B)
+    int pq_cosched = 1;      // PQ batches (nq > 1): co-scheduled K8e (1) or one range set per query (0; A/B)
     int k1_tail = 0;         // K1 cache_tail256: 0 = auto (k1_cache_tail), -1 = off (plain_loads() policy
                              // for the whole pass), 1..256 = forced (A/B; env WVG_K1_TAIL)
     int pq_encode_min3 = 1;  // PQ encode pair path: min3 argmin on NaN-free codebooks (1) or the

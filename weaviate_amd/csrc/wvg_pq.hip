@@ -901,14 +901,24 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_dense_kernel(Sca
 template <int E, int WV>
 constexpr uint32_t PQ32_WIDE_BASE = (uint32_t)WV * 64u * E * 8u;  // LDS address of the image (after sh[WV][64E])
 
-template <int E, int WV, int R, int NB, int TP, int METRIC, bool IL = false>
+template <int E, int WV, int R, int NB, int TP, int METRIC, bool IL = false, bool COS = false>
 __global__ __launch_bounds__(WV * 64) void scan_pq32_wide_kernel(ScanArgs a, uint64_t *partials)
 {
     static_assert(64 % R == 0, "the ring length divides the 64-tile mask block");
     static_assert(32 % NB == 0, "LDS batches divide the 32 steps");
     extern __shared__ __attribute__((aligned(16))) f32x2 img[];  // regions A and B (PQ32_IMG7_*)
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t qi = blockIdx.y;
+    // COS (co-scheduled PQ batch, a.cosched): a 1D grid of G ranges x nq queries.  Workgroup id ->
+    // (range, query) so that the nq queries of one range are consecutive ids on one XCD (ids
+    // with equal id % 8): they are resident together and read the same rows side by side, so all
+    // but the first read of a line hit the XCD's L2 (the loads keep the default policy).
+    uint32_t qi = blockIdx.y, rng = blockIdx.x, G = gridDim.x;
+    if constexpr (COS) {
+        G = gridDim.x / a.nq;
+        const uint32_t kk = blockIdx.x >> 3;
+        rng = (kk / a.nq) * 8u + (blockIdx.x & 7u);
+        qi = kk % a.nq;
+    }
     const float *glut = reinterpret_cast<const float *>(a.queries) + (size_t)qi * a.qpitch;
     constexpr int FILL = 32 * 256 / (WV * 64);
     float fv[FILL];
@@ -926,14 +936,14 @@ __global__ __launch_bounds__(WV * 64) void scan_pq32_wide_kernel(ScanArgs a, uin
     uint32_t n[TP];
     uint32_t nmax = 0;
     if constexpr (IL) {
-        const uint64_t w0 = a.tile_begin + ntiles * blockIdx.x / gridDim.x;
-        const uint64_t w1 = a.tile_begin + ntiles * (blockIdx.x + 1) / gridDim.x;
+        const uint64_t w0 = a.tile_begin + ntiles * rng / G;
+        const uint64_t w1 = a.tile_begin + ntiles * (rng + 1) / G;
         s0[0] = w0 + wave;
         n[0] = s0[0] < w1 ? (uint32_t)((w1 - s0[0] + WV - 1) / WV) : 0u;
         nmax = n[0];
     } else {
-        const uint64_t total = (uint64_t)gridDim.x * WV * TP;  // streams of the launch
-        const uint64_t g0 = ((uint64_t)blockIdx.x * WV + wave) * TP;
+        const uint64_t total = (uint64_t)G * WV * TP;  // streams of one query
+        const uint64_t g0 = ((uint64_t)rng * WV + wave) * TP;
 #pragma unroll
         for (int p = 0; p < TP; p++) {
             s0[p] = a.tile_begin + ntiles * (g0 + p) / total;
@@ -977,8 +987,9 @@ __global__ __launch_bounds__(WV * 64) void scan_pq32_wide_kernel(ScanArgs a, uin
         auto tile_of = [&](int p, uint32_t i) -> uint32_t { return rev ? n[p] - 1u - i : i; };
         auto load = [&](int p, uint32_t i, uint32_t (&w)[8]) {  // the i-th tile of stream p (zeros past it)
             const uint32_t so = i < n[p] ? tile_of(p, i) * (STRIDE * 2048u) : span(p);
-            const u32x4 lo = __builtin_amdgcn_raw_buffer_load_b128(rs[p], voff, so, 2);
-            const u32x4 hi = __builtin_amdgcn_raw_buffer_load_b128(rs[p], voff + 1024u, so, 2);
+            constexpr int POL = COS ? 0 : 2;  // co-scheduled: keep the lines in L2 for the other queries
+            const u32x4 lo = __builtin_amdgcn_raw_buffer_load_b128(rs[p], voff, so, POL);
+            const u32x4 hi = __builtin_amdgcn_raw_buffer_load_b128(rs[p], voff + 1024u, so, POL);
             w[0] = lo.x; w[1] = lo.y; w[2] = lo.z; w[3] = lo.w;
             w[4] = hi.x; w[5] = hi.y; w[6] = hi.z; w[7] = hi.w;
         };
@@ -1083,7 +1094,7 @@ __global__ __launch_bounds__(WV * 64) void scan_pq32_wide_kernel(ScanArgs a, uin
             }
         }
     }
-    group_combine_store<E, WV>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
+    group_combine_store<E, WV>(tk, partials + ((size_t)qi * G + rng) * a.k);
 }
 
 // K8d: K8c with the R passes of a ring cycle in ONE basic block.  K8c's
@@ -1269,32 +1280,32 @@ static bool img7_ok()
 
 // K8e reads its image at the compile-time LDS address PQ32_WIDE_BASE: the
 // host launches an instantiation only where the static LDS really ends there
-template <int E, int WV, int R, int NB, int TP, bool IL = false>
+template <int E, int WV, int R, int NB, int TP, bool IL = false, bool COS = false>
 static bool wide_ok()
 {
     static const bool ok = [] {
         if (PQ32_WIDE_BASE<E, WV> + PQ32_IMG7_BYTES > 160u * 1024u) return false;
         hipFuncAttributes fa{};
         if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(
-                                          &scan_pq32_wide_kernel<E, WV, R, NB, TP, WVG_M_L2, IL>)) != hipSuccess)
+                                          &scan_pq32_wide_kernel<E, WV, R, NB, TP, WVG_M_L2, IL, COS>)) != hipSuccess)
             return false;
         return fa.sharedSizeBytes == PQ32_WIDE_BASE<E, WV>;
     }();
     return ok;
 }
 
-template <int E, int WV, int R, int NB, int TP, bool IL = false>
+template <int E, int WV, int R, int NB, int TP, bool IL = false, bool COS = false>
 static bool launch_pq_wide(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
 {
-    if (!wide_ok<E, WV, R, NB, TP, IL>()) return false;
-    const dim3 grid(groups, a.nq), block(WV * 64);
+    if (!wide_ok<E, WV, R, NB, TP, IL, COS>()) return false;
+    const dim3 grid = COS ? dim3((unsigned)groups * a.nq) : dim3(groups, a.nq), block(WV * 64);
     const uint32_t lds = PQ32_IMG7_BYTES;
     if (a.metric == WVG_M_L2 || a.metric == WVG_M_MANHATTAN || a.metric == WVG_M_HAMMING)  // Wrap = identity
-        launch_timed((scan_pq32_wide_kernel<E, WV, R, NB, TP, WVG_M_L2, IL>), grid, block, lds, s, a, partials);
+        launch_timed((scan_pq32_wide_kernel<E, WV, R, NB, TP, WVG_M_L2, IL, COS>), grid, block, lds, s, a, partials);
     else if (a.metric == WVG_M_DOT)
-        launch_timed((scan_pq32_wide_kernel<E, WV, R, NB, TP, WVG_M_DOT, IL>), grid, block, lds, s, a, partials);
+        launch_timed((scan_pq32_wide_kernel<E, WV, R, NB, TP, WVG_M_DOT, IL, COS>), grid, block, lds, s, a, partials);
     else
-        launch_timed((scan_pq32_wide_kernel<E, WV, R, NB, TP, WVG_M_COSINE, IL>), grid, block, lds, s, a, partials);
+        launch_timed((scan_pq32_wide_kernel<E, WV, R, NB, TP, WVG_M_COSINE, IL, COS>), grid, block, lds, s, a, partials);
     return true;
 }
 
@@ -1378,8 +1389,22 @@ static hipError_t launch_pq_e(const ScanArgs &a, uint64_t *partials, int groups,
         else launch_pq_dense<E, 4, 16, 7>(a, partials, grid, block, PQ32_IMG7_BYTES, s);
         return hipGetLastError();
     }
-    // the default for m = 32, ks = 256 on mostly-live corpora without an allow list: K8e (8 waves, ring 4)
+    // the default for m = 32, ks = 256 on mostly-live corpora without an allow list: K8e (8 waves, ring 4);
+    // batches (a.cosched, groups % 8 == 0): co-scheduled over one range per XCD, 16 waves per CU
+    // (0.338 ms per query of a 16-query batch at 100M codes vs 0.375 with 8 waves; 8 when the 16-wave
+    // top-k buffer and the image exceed the LDS, E = 4)
+    if (m32 && v == 0 && a.dense && a.cosched && groups % 8 == 0 &&
+        (launch_pq_wide<E, 16, 4, 16, 1, false, true>(a, partials, groups, s) ||
+         launch_pq_wide<E, 8, 4, 16, 1, false, true>(a, partials, groups, s)))
+        return hipGetLastError();
     if (m32 && v == 0 && a.dense && launch_pq_wide<E, 8, 4, 16, 1>(a, partials, groups, s)) return hipGetLastError();
+    if (m32 && (v == 48 || v == 49) && a.dense && a.cosched && groups % 8 == 0) {
+        // A/B: co-scheduled batches with 16 waves per CU (the L2 serves most reads, so the
+        // 16-wave contention of K8c may no longer bind): 48 = ring 4, 49 = ring 8
+        if (v == 48 ? launch_pq_wide<E, 16, 4, 16, 1, false, true>(a, partials, groups, s)
+                    : launch_pq_wide<E, 16, 8, 16, 1, false, true>(a, partials, groups, s))
+            return hipGetLastError();
+    }
     if (m32 && (v == 10 || v == 11 || v == 12 || (v == 0 && a.dense))) {
         // K8c (dense, issue-trimmed): 0 (auto) / 12 = ring 8 / LDS batches of 16, 10 = ring 8 / 8, 11 = ring 4 / 16
         if (v == 11)
