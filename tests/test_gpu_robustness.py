@@ -319,3 +319,32 @@ def test_pinned_host_buffers(ctx, orc):
     p = ct.c_void_p()
     check(lib.wvg_host_alloc(ctx.handle, 0, ct.byref(p)))
     assert not p.value
+
+
+@pytest.mark.parametrize("kind", [KIND_BQ, KIND_PQ])
+def test_cosched_batches_equal_single_queries(ctx, orc, kind):
+    """Co-scheduled batches (K5 / K8e COS: the nq queries of a row range on one
+    XCD) return exactly what one query per call returns, with it on or off."""
+    n, d = 50_000 + 37, 128
+    rows = orc.synth_rows(600, 0, n, d, 0)
+    c = Corpus(ctx, kind, METRIC_L2, d, n)
+    if kind == KIND_PQ:
+        centers = orc.synth_rows(601, 0, 32 * 256, d // 32, 0).reshape(32, 256, d // 32)
+        c.set_codebook(centers)
+    c.upsert(np.arange(n, dtype=np.uint64), rows)
+    c.delete(np.arange(5, n, 97, dtype=np.uint64))
+    qs = orc.synth_rows(602, 0, 12, d, 0)
+    try:
+        for k in (10, 100, 200):
+            singles = [c.search(qs[i], k) for i in range(len(qs))]
+            for cos in (1, 0):
+                old = tuning(_lib.load(), 15, cos)
+                try:
+                    ids, dists, counts = c.search(qs, k)
+                finally:
+                    tuning(_lib.load(), 15, old)
+                for i, (si, sd, sc) in enumerate(singles):
+                    assert counts[i] == sc[0]
+                    assert np.array_equal(ids[i], si[0]) and np.array_equal(dists[i].view(np.uint32), sd[0].view(np.uint32))
+    finally:
+        c.destroy()

@@ -34,17 +34,32 @@ __device__ __forceinline__ u64x2 ld_codes(const u64x2 *p) { return __builtin_non
 // the tile's 16-byte chunks.  Fixed NCH: the next live tile's chunks are
 // loaded (non-temporal) while the current tile is reduced and offered, so a
 // wave keeps two tiles' codes in flight; tile masks are scalar and prefetched.
-template <int E, int NCH>
+// COS (a batch, ScanArgs::cosched): the 1D grid's consecutive ids on one XCD
+// are the nq queries of one row range, which read the same codes side by side
+// from that XCD's L2 (default-policy loads; K8e COS in wvg_pq.hip).
+template <int E, int NCH, bool COS = false>
 __global__ __launch_bounds__(BQ_WAVES * 64) void scan_bq_kernel(ScanArgs a, uint64_t *partials)
 {
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t qi = blockIdx.y;
+    uint32_t qi = blockIdx.y, rng = blockIdx.x, G = gridDim.x;
+    if constexpr (COS) {
+        G = gridDim.x / a.nq;
+        const uint32_t kk = blockIdx.x >> 3;
+        rng = (kk / a.nq) * 8u + (blockIdx.x & 7u);
+        qi = kk % a.nq;
+    }
+    auto ld = [](const u64x2 *p) -> u64x2 {
+        if constexpr (COS)
+            return *p;
+        else
+            return ld_codes(p);
+    };
     const uint64_t *q = reinterpret_cast<const uint64_t *>(a.queries) + (size_t)qi * a.qpitch;
     const u64x2 *data = reinterpret_cast<const u64x2 *>(a.data);
     const uint32_t nch = NCH > 0 ? (uint32_t)NCH : a.nchunks;
     const uint64_t ntiles = a.tile_end - a.tile_begin;
-    const uint64_t total = (uint64_t)gridDim.x * BQ_WAVES;
-    const uint64_t gw = (uint64_t)blockIdx.x * BQ_WAVES + wave;
+    const uint64_t total = (uint64_t)G * BQ_WAVES;
+    const uint64_t gw = (uint64_t)rng * BQ_WAVES + wave;
     const uint64_t t0 = a.tile_begin + ntiles * gw / total, t1 = a.tile_begin + ntiles * (gw + 1) / total;
     WaveTopK<E> tk;
     tk.init((int)a.k);
@@ -64,14 +79,14 @@ __global__ __launch_bounds__(BQ_WAVES * 64) void scan_bq_kernel(ScanArgs a, uint
         if (t < t1) {
             const u64x2 *rp = data + (size_t)t * NCH * 64 + lane;
 #pragma unroll
-            for (int c = 0; c < NCH; c++) cur[c] = ld_codes(rp + (size_t)c * 64);
+            for (int c = 0; c < NCH; c++) cur[c] = ld(rp + (size_t)c * 64);
         }
         while (t < t1) {
             const uint64_t tn = next_live(t + 1, m_nxt);
             if (tn < t1) {
                 const u64x2 *rp = data + (size_t)tn * NCH * 64 + lane;
 #pragma unroll
-                for (int c = 0; c < NCH; c++) nxt[c] = ld_codes(rp + (size_t)c * 64);
+                for (int c = 0; c < NCH; c++) nxt[c] = ld(rp + (size_t)c * 64);
             }
             uint32_t tot = 0;
 #pragma unroll
@@ -92,27 +107,34 @@ __global__ __launch_bounds__(BQ_WAVES * 64) void scan_bq_kernel(ScanArgs a, uint
             const u64x2 *rp = data + (size_t)t * nch * 64 + lane;
             uint32_t tot = 0;
             for (uint32_t c = 0; c < nch; c++) {
-                const u64x2 x = ld_codes(rp + (size_t)c * 64);
+                const u64x2 x = ld(rp + (size_t)c * 64);
                 tot += (uint32_t)__popcll(x.x ^ q[2 * c]) + (uint32_t)__popcll(x.y ^ q[2 * c + 1]);
             }
             const float dist = (float)tot;
             tk.offer_dist_fast(dist, (uint32_t)(t * 64 + lane), m);
         }
     }
-    group_combine_store<E, BQ_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
+    group_combine_store<E, BQ_WAVES>(tk, partials + ((size_t)qi * G + rng) * a.k);
+}
+
+template <int E, bool COS>
+static hipError_t launch_bq_ec(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
+{
+    const dim3 grid = COS ? dim3((unsigned)groups * a.nq) : dim3(groups, a.nq), block(BQ_WAVES * 64);
+    switch (a.nchunks) {
+    case 1: launch_timed((scan_bq_kernel<E, 1, COS>), grid, block, 0, s, a, partials); break;   // d <= 128
+    case 6: launch_timed((scan_bq_kernel<E, 6, COS>), grid, block, 0, s, a, partials); break;   // d = 768
+    case 12: launch_timed((scan_bq_kernel<E, 12, COS>), grid, block, 0, s, a, partials); break; // d = 1536
+    default: launch_timed((scan_bq_kernel<E, 0, COS>), grid, block, 0, s, a, partials); break;
+    }
+    return hipGetLastError();
 }
 
 template <int E>
 static hipError_t launch_bq_e(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
 {
-    dim3 grid(groups, a.nq), block(BQ_WAVES * 64);
-    switch (a.nchunks) {
-    case 1: launch_timed((scan_bq_kernel<E, 1>), grid, block, 0, s, a, partials); break;   // d <= 128
-    case 6: launch_timed((scan_bq_kernel<E, 6>), grid, block, 0, s, a, partials); break;   // d = 768
-    case 12: launch_timed((scan_bq_kernel<E, 12>), grid, block, 0, s, a, partials); break; // d = 1536
-    default: launch_timed((scan_bq_kernel<E, 0>), grid, block, 0, s, a, partials); break;
-    }
-    return hipGetLastError();
+    if (a.cosched && a.nq > 1 && groups % 8 == 0) return launch_bq_ec<E, true>(a, partials, groups, s);
+    return launch_bq_ec<E, false>(a, partials, groups, s);
 }
 
 hipError_t launch_scan_bq(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)

@@ -1047,10 +1047,12 @@ static SearchPlan plan_search(wvg_corpus *c, uint32_t nq, uint32_t k, const uint
     else
         p.groups = scan_groups_for(a, c->ctx->num_cus);
     // PQ batches: the nq queries of one row range run side by side on one XCD and share its L2
-    p.cosched = c->kind == WVG_KIND_PQ && c->pq_m == 32 && c->pq_ks == 256 && nq > 1 && !allow &&
-                pq_dense(c, nullptr) && tuning().pq_cosched != 0 &&
-                (tuning().pq_variant == 0 || tuning().pq_variant == 48 || tuning().pq_variant == 49);
-    if (p.cosched) p.groups = pq_cosched_groups(nq, c->ctx->num_cus);
+    const bool pq_cos = c->kind == WVG_KIND_PQ && c->pq_m == 32 && c->pq_ks == 256 && pq_dense(c, nullptr) &&
+                        (tuning().pq_variant == 0 || tuning().pq_variant == 48 || tuning().pq_variant == 49);
+    const bool bq_cos = c->kind == WVG_KIND_BQ;  // K5 COS (wvg_bq.hip)
+    p.cosched = nq > 1 && !allow && tuning().pq_cosched != 0 && (pq_cos || bq_cos);
+    if (p.cosched)  // BQ: K5 workgroups are 4 waves, so bq_cos_gpc of them per CU
+        p.groups = pq_cosched_groups(nq, c->ctx->num_cus * (bq_cos ? std::max(1, tuning().bq_cos_gpc) : 1));
     return p;
 }
 
@@ -2007,7 +2009,7 @@ int wvg_synthetic_rows(wvg_ctx *ctx, uint64_t seed, const uint64_t *ids, uint64_
 // Internal A/B knob (not part of include/wvgpu.h): 0 = K1 scan variant,
 // 1 = K1 resident workgroups per CU, ... 7 = K8 ADC variant, 8 = query-stream merge wait (us),
 // 9 = serpentine scan order, 10 = K3b row-range length, 11 = K1 load policy, 12 = K3b SIMD pairing,
-// 13 = K3b partner priority, 14 = PQ encode min3 argmin, 15 = co-scheduled PQ batches.  Returns the previous value.
+// 13 = K3b partner priority, 14 = PQ encode min3 argmin, 15 = co-scheduled PQ / BQ batches, 16 = co-scheduled BQ workgroups per CU.  Returns the previous value.
 int wvgx_set_tuning(int key, int value)
 {
     Tuning &t = tuning();
@@ -2060,6 +2062,9 @@ int wvgx_set_tuning(int key, int value)
     } else if (key == 15) {
         old = t.pq_cosched;
         t.pq_cosched = value;
+    } else if (key == 16) {
+        old = t.bq_cos_gpc;
+        t.bq_cos_gpc = value;
     }
     return old;
 }

@@ -278,7 +278,9 @@ struct Tuning {
                                // -1 = one long range per workgroup (one wave of workgroups; A/B)
     int gemm_pairing = 0;    // K3b QH = 2: SIMD partners share rows (0) or queries (1) (A/B)
     int gemm_prio = 0;       // K3b: s_setprio 1 for the second wave of each SIMD (A/B)
-    int pq_cosched = 1;      // PQ batches (nq > 1): co-scheduled K8e (1) or one range set per query (0; A/B)
+    int pq_cosched = 1;      // PQ / BQ batches (nq > 1): co-scheduled K8e / K5 (1) or one range set per
+                             // query (0; A/B)
+    int bq_cos_gpc = 1;      // co-scheduled K5: 4-wave workgroups per CU (A/B)
     int k1_tail = 0;         // K1 cache_tail256: 0 = auto (k1_cache_tail), -1 = off (plain_loads() policy
                              // for the whole pass), 1..256 = forced (A/B; env WVG_K1_TAIL)
     int pq_encode_min3 = 1;  // PQ encode pair path: min3 argmin on NaN-free codebooks (1) or the
