@@ -280,7 +280,8 @@ struct Tuning {
     int gemm_prio = 0;       // K3b: s_setprio 1 for the second wave of each SIMD (A/B)
     int pq_cosched = 1;      // PQ / BQ batches (nq > 1): co-scheduled K8e / K5 (1) or one range set per
                              // query (0; A/B)
-    int bq_cos_gpc = 1;      // co-scheduled K5: 4-wave workgroups per CU (A/B)
+    int bq_cos_gpc = 2;      // co-scheduled K5: 4-wave workgroups per CU (2: 1.01 ms per query of an 8-query
+                             // 100M x 1536 batch; 1: 1.49, 4: 1.34; A/B)
     int k1_tail = 0;         // K1 cache_tail256: 0 = auto (k1_cache_tail), -1 = off (plain_loads() policy
                              // for the whole pass), 1..256 = forced (A/B; env WVG_K1_TAIL)
     int pq_encode_min3 = 1;  // PQ encode pair path: min3 argmin on NaN-free codebooks (1) or the
