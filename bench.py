@@ -199,6 +199,68 @@ def _timed(fn, dist, world, dev, torch):
     return el
 
 
+def stored_traffic(n, d, B):
+    """HBM-side bytes per launch from the last rocprofv3 PMC pass over this
+    exact workload (profiles/traffic.json, written by tools/traffic_from_pmc.py):
+    FETCH_SIZE (x2, gfx950 half-count) counts Infinity-Cache hits as fetched,
+    so it is the L2 -> fabric traffic, not DRAM traffic.  Not measured in this
+    process (rocprofv3 cannot run inside the bench); labelled as stored."""
+    tf = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        rec = json.load(open(tf)).get("scan_f32_stream_l2_128", {})
+    except (OSError, ValueError):
+        return None, None
+    if rec.get("rows") != n or rec.get("dim") != d or "hbm_bytes_per_query_scan" not in rec:
+        return None, None
+    src = (f"stored, not measured in this run: profiles/traffic.json['scan_f32_stream_l2_128'] "
+           f"({rec.get('source', '')}; {rec.get('method', '')})")
+    return int(round(rec["hbm_bytes_per_query_scan"] * B)), src
+
+
+def no_reuse_leg(args, dev, torch, n, d, k, B, tq, P, launches):
+    """The headline kernel with nothing reused between scans: a context with
+    wvg_options.cache_reuse = 0 (every scan walks upwards, every row load
+    non-temporal) over a fresh copy of the same rows, same launch shape (B
+    query scans per launch).  Returns the average launch time (s) from HIP
+    events bound to each dispatch, and the context's HBM read ceiling
+    (wvg_measure_hbm_read over 2 GiB: 8x the Infinity Cache)."""
+    import ctypes
+
+    from weaviate_amd._lib import KIND_F32, METRIC_L2, check
+    from weaviate_amd.device import Context, Corpus
+
+    cap = (n + 63) // 64 * 64
+    ctx = Context(dev.index, cache_reuse=0)
+    lib = ctx.lib
+    c = Corpus(ctx, KIND_F32, METRIC_L2, d, cap)
+    c.fill_synthetic(42, n, 0)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    wsb = lib.wvg_search_workspace_size(c.handle, B, k)
+    ws = torch.zeros(wsb, dtype=torch.uint8, device=dev)
+    oi = torch.empty((B, k), dtype=torch.int64, device=dev)
+    od = torch.empty((B, k), dtype=torch.float32, device=dev)
+    oc = torch.empty(B, dtype=torch.int32, device=dev)
+
+    def launch(s):
+        check(lib.wvg_search_device_pipelined(c.handle, tq[(s * B) % P].data_ptr(), B, k, oi.data_ptr(),
+                                              od.data_ptr(), oc.data_ptr(), ws.data_ptr(), wsb, stream))
+
+    for s in range(2):
+        launch(s)
+    torch.cuda.synchronize(dev)
+    check(lib.wvg_profile_start(ctx.handle))
+    for s in range(launches):
+        launch(s)
+    ms, nl = ctypes.c_double(), ctypes.c_uint64()
+    check(lib.wvg_profile_stop(ctx.handle, ctypes.byref(ms), ctypes.byref(nl)))
+    check(lib.wvg_search_device_check(ctx.handle, ws.data_ptr(), stream))
+    gbps = ctypes.c_double()
+    check(lib.wvg_measure_hbm_read(ctx.handle, 2 << 30, 5, ctypes.byref(gbps)))
+    c.destroy()
+    ctx.close()
+    return ms.value / 1e3 / max(1, nl.value), gbps.value
+
+
 def run_flat1m(args, world, rank, dev, torch, dist):
     from weaviate_amd._lib import KIND_F32, METRIC_L2, check
     from weaviate_amd.device import Context, Corpus
@@ -266,15 +328,10 @@ def run_flat1m(args, world, rank, dev, torch, dist):
     avg_launch_s = scan_ms.value / 1e3 / max(1, launches.value)
     bytes_per_launch = n * d * 4 * B  # N*d*4 algorithmic bytes per query scan
     achieved = bytes_per_launch / avg_launch_s / 1e9
-    traffic = None
-    tf = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tf):
-        try:
-            rec = json.load(open(tf)).get("scan_f32_stream_l2_128", {})
-            if rec.get("rows") == n and rec.get("dim") == d:
-                traffic = int(round(rec["hbm_bytes_per_query_scan"] * B))  # per launch, like `achieved`
-        except (OSError, ValueError, KeyError):
-            traffic = None
+    traffic, traffic_src = stored_traffic(n, d, B)  # per launch, like `achieved`
+    # untimed: the same kernel with no reuse between scans, and the HBM read ceiling
+    nr_launch_s, ceiling = no_reuse_leg(args, dev, torch, n, d, k, B, tq, P, max(5, min(args.steps, 20)))
+    achieved_nr = bytes_per_launch / nr_launch_s / 1e9
     out = {
         "metric": METRIC,
         "value": round(total_queries / elapsed, 3),
@@ -305,14 +362,25 @@ def run_flat1m(args, world, rank, dev, torch, dist):
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
+            "traffic_source": traffic_src,
             "avg_launch_us": round(avg_launch_s * 1e6, 2),
             "queries_per_launch": B,
             "algorithmic_bytes_per_launch": bytes_per_launch,
             "launches": int(launches.value),
-            "note": ("every query is a full scan (N*d*4 algorithmic bytes); consecutive scans alternate "
-                     "direction and each reads the last ~320 MB of its pass with the default cache policy "
-                     "(k1_cache_tail), so the next scan starts on rows held by the 256 MiB Infinity Cache + "
-                     "L2s -- FETCH_SIZE (`traffic`) counts those Infinity-Cache hits as fetched bytes"),
+            "achieved_no_reuse": round(achieved_nr, 1),
+            "frac_no_reuse": round(achieved_nr / HBM_PEAK_GBS, 4),
+            "avg_launch_us_no_reuse": round(nr_launch_s * 1e6, 2),
+            "ceiling_GBps": round(ceiling, 1),
+            "frac_of_ceiling_no_reuse": round(achieved_nr / ceiling, 4) if ceiling > 0 else None,
+            "note": ("`achieved` = ALGORITHMIC bytes (N*d*4 per query scan, every query a full scan) / the "
+                     "kernel's average launch time, Infinity-Cache reuse included: consecutive scans alternate "
+                     "direction and read the last ~320 MB of each pass with the default cache policy "
+                     "(k1_cache_tail), so each scan starts on rows the previous one left in the 256 MiB "
+                     "Infinity Cache -- it is not a DRAM rate and can exceed the DRAM read ceiling.  "
+                     "`achieved_no_reuse` / `frac_no_reuse`: the same kernel and launch shape in a context with "
+                     "wvg_options.cache_reuse = 0 (one direction, all loads non-temporal) over a fresh copy of "
+                     "the rows, measured in this run.  `ceiling_GBps`: wvg_measure_hbm_read (2 GiB non-temporal "
+                     "streaming read) in this run.  `traffic`: see traffic_source"),
         },
         "cpu_baseline": None,
     }

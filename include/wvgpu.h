@@ -62,6 +62,27 @@ const char *wvg_last_error(void);
 int wvg_device_count(int *out);
 /* One context per GPU (one process per GPU in the multi-GPU deployment). */
 int wvg_open(int device, wvg_ctx **out);
+/* Context options, fixed for the life of the context (wvg_open uses the
+ * defaults).  Fill with wvg_options_default, change fields, then open.     */
+typedef struct wvg_options {
+    uint32_t size;             /* sizeof(wvg_options) (ABI guard; set by wvg_options_default) */
+    uint32_t mfma_min_queries; /* dot / cosine batches of at least this many queries are scored on the
+                                  matrix cores (bf16 screen + exact fp32 rescore, or exact fp32 MFMA);
+                                  smaller ones run one HBM-bound scan per query.  0 = never.  Default 32. */
+    int32_t cache_reuse;       /* 1 (default): consecutive scans of a corpus alternate direction and read
+                                  the last ~320 MB of each pass with the default cache policy, so the next
+                                  scan starts on rows still in the 256 MiB Infinity Cache.  0: streaming --
+                                  one direction, non-temporal loads, no reuse between scans (e.g. next to
+                                  other memory-heavy work, or to measure the DRAM-bound rate). */
+    uint32_t merge_wait_us;    /* bound on the in-launch merge's wait for one query's scan workgroups
+                                  (wvg_search_device_pipelined); 0 = the default, 4 s.  On expiry the
+                                  query gets empty results and wvg_search_device_check fails. */
+    int32_t batch_screen;      /* 1 (default): batched dot / cosine searches screen every row with bf16
+                                  MFMA and a per-row error bound, then rescore the candidates exactly in
+                                  fp32 (results identical to the exact path); 0: exact fp32 MFMA only. */
+} wvg_options;
+void wvg_options_default(wvg_options *opts);
+int wvg_open_ex(int device, const wvg_options *opts, wvg_ctx **out);
 int wvg_close(wvg_ctx *ctx);
 int wvg_synchronize(wvg_ctx *ctx);
 /* Page-locked host memory for a caller's reusable staging buffers (e.g. the
@@ -202,9 +223,10 @@ int wvg_search_device(wvg_corpus *c, const float *d_queries, uint32_t nq, uint32
                       size_t workspace_bytes, void *stream);
 /* nq independent single-query searches (each one full scan of the corpus:
  * flat.SearchByVector per query, as concurrent Weaviate queries issue them)
- * in ONE call: query i's scan launch also runs query i-1's top-k merge on one
- * extra workgroup, so the merges cost no launches of their own.  F32
- * corpora; same workspace size rule; outputs as wvg_search_device.        */
+ * in ONE launch: the scan workgroups walk the queries back to back and one
+ * extra workgroup merges each query's partial lists while the scan moves
+ * on, so the merges cost no launches of their own.  F32 corpora; same
+ * workspace size rule; outputs as wvg_search_device.                       */
 int wvg_search_device_pipelined(wvg_corpus *c, const float *d_queries, uint32_t nq, uint32_t k,
                                 uint64_t *d_ids, float *d_dists, uint32_t *d_counts,
                                 void *d_workspace, size_t workspace_bytes, void *stream);
@@ -255,6 +277,11 @@ int wvg_synthetic_rows(wvg_ctx *ctx, uint64_t seed, const uint64_t *ids, uint64_
  * vector_index_durations_ms metric, usecases/monitoring/prometheus.go:292). */
 int wvg_profile_start(wvg_ctx *ctx);
 int wvg_profile_stop(wvg_ctx *ctx, double *scan_ms_total, uint64_t *scan_launches);
+/* Measurement helper: the HBM streaming-read rate of this GPU, in GB/s -- the
+ * best of grid-stride 16-byte non-temporal reads of a `bytes` buffer (its
+ * own allocation, freed again) over 1024..8192 workgroups, `reps` passes
+ * each.  The ceiling the HBM-bound scans are compared with (roofline).    */
+int wvg_measure_hbm_read(wvg_ctx *ctx, uint64_t bytes, uint32_t reps, double *out_gbps);
 
 /* ---- bulk primitives (distancer.BatchProvider / compressionhelpers bulk) --- */
 /* Provider.SingleDist of q against n rows X [n][dim] (D/provider.go:14-20). */

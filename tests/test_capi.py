@@ -60,3 +60,34 @@ def test_open_without_device_fails_cleanly():
     rc = lib.wvg_open(0, ctypes.byref(h))
     assert rc in (_lib.WVG_ERR_DEVICE, _lib.WVG_ERR_INVALID)
     assert not h.value
+
+
+def test_exports_equal_header():
+    """The product library exports exactly the header's entry points: no
+    tuning setter (wvgx_*), no A/B knobs -- those live in the tools build."""
+    import subprocess
+
+    from weaviate_amd import _lib
+
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], check=True, capture_output=True,
+                         text=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if ln.split() and ln.split()[-1].startswith("wvg")}
+    assert exported == set(header_symbols())
+
+
+def test_options_struct_matches_library():
+    import ctypes as ct
+
+    from weaviate_amd import _lib
+
+    lib = _lib.load()
+    o = _lib.Options()
+    lib.wvg_options_default(ct.byref(o))
+    assert o.size == ct.sizeof(_lib.Options)
+    assert (o.mfma_min_queries, o.cache_reuse, o.merge_wait_us, o.batch_screen) == (32, 1, 0, 1)
+    bad = _lib.Options()
+    lib.wvg_options_default(ct.byref(bad))
+    bad.size = 3
+    h = ct.c_void_p()
+    assert lib.wvg_open_ex(0, ct.byref(bad), ct.byref(h)) == _lib.WVG_ERR_INVALID
+    assert not h.value

@@ -23,7 +23,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n, d, k, nq, dead, pipelined, out):
+def _worker(rank, world, port, n, d, k, nq, dead, pipelined, side, out):
     import sys
 
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -51,8 +51,15 @@ def _worker(rank, world, port, n, d, k, nq, dead, pipelined, out):
         qs = torch.from_numpy(rng.uniform(-1, 1, (nq, d)).astype(np.float32)).cuda()
         idx = ShardedFlatIndex(ctx, c)
         res = []
+        st = torch.cuda.Stream() if side else None
         for rep in range(2):  # the cached workspace / send / recv buffers are reused
-            ids, dists, counts = idx.search_device(qs, k, pipelined=pipelined)
+            # side: every step on the caller's own stream -- a raw hipStream_t,
+            # then the torch.cuda.Stream -- while torch's current stream stays
+            # the default one (the all-gather and merge must order on it too)
+            s_arg = None if st is None else (st.cuda_stream if rep == 0 else st)
+            ids, dists, counts = idx.search_device(qs, k, stream=s_arg, pipelined=pipelined)
+            if st is not None:
+                st.synchronize()
             torch.cuda.synchronize()
             res.append((ids.cpu().numpy().view(np.uint64).copy(), dists.cpu().numpy().copy(),
                         counts.cpu().numpy().copy()))
@@ -66,15 +73,16 @@ def _worker(rank, world, port, n, d, k, nq, dead, pipelined, out):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n,pipelined", [(20_000 + 37, False), (20_000 + 37, True), (50, False), (50, True)])
-def test_two_ranks_packed_allgather_device_merge(orc, n, pipelined):
+@pytest.mark.parametrize("n,pipelined,side", [(20_000 + 37, False, False), (20_000 + 37, True, False), (50, False, False),
+                                             (50, True, False), (20_000 + 37, False, True), (20_000 + 37, True, True)])
+def test_two_ranks_packed_allgather_device_merge(orc, n, pipelined, side):
     """n = 50: rank 1's slab is empty (empty results from the device path)."""
     world, d, k, nq = 2, 64, 10, 5
     dead = [0, 3, 777, 10_111, 20_036]
     ctxm = mp.get_context("spawn")
     q = ctxm.Queue()
     port = _free_port()
-    procs = [ctxm.Process(target=_worker, args=(r, world, port, n, d, k, nq, dead, pipelined, q))
+    procs = [ctxm.Process(target=_worker, args=(r, world, port, n, d, k, nq, dead, pipelined, side, q))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -189,3 +197,39 @@ def test_two_ranks_pq_codebook_broadcast_encode_search(orc):
             wi, wd = orc.lex_topk(all_d, np.arange(n, dtype=np.uint64), k)
             assert counts[qi] == k and np.array_equal(ids[qi], wi)
             assert np.array_equal(dists[qi].view(np.uint32), wd.view(np.uint32))
+
+
+def test_sharded_workspace_follows_slab_growth(ctx, orc):
+    """ShardedFlatIndex asks for the workspace size on every call: a batch
+    (nq >= the MFMA threshold) on a small slab, then the slab grows by 30x,
+    then the same batch again -- the grown plan (more K3b row ranges) must
+    get a grown workspace, not 'workspace too small'."""
+    import torch
+
+    from weaviate_amd._lib import KIND_F32, METRIC_DOT
+    from weaviate_amd.device import Corpus
+    from weaviate_amd.shard import ShardedFlatIndex
+
+    d, k, nq = 128, 10, 40
+    c = Corpus(ctx, KIND_F32, METRIC_DOT, d, 2048)
+    try:
+        c.fill_synthetic(61, 2048, 0)
+        qs = np.random.default_rng(62).uniform(-1, 1, (nq, d)).astype(np.float32)
+        idx = ShardedFlatIndex(ctx, c)
+        tq = torch.from_numpy(qs).cuda()
+        for n in (2048, 60_000):
+            if n > 2048:
+                c.reserve(n)
+                c.fill_synthetic(61, n, 0)
+            ids, dists, counts = idx.search_device(tq, k)
+            torch.cuda.synchronize()
+            ids = ids.cpu().numpy().view(np.uint64)
+            dists = dists.cpu().numpy()
+            rows = orc.synth_rows(61, 0, n, d, 0)
+            for qi in (0, nq - 1):
+                wi, wd = orc.lex_topk(orc.dist_all(orc.DOT, qs[qi], rows), np.arange(n, dtype=np.uint64), k)
+                assert np.array_equal(ids[qi], wi)
+                assert np.array_equal(dists[qi].view(np.uint32), wd.view(np.uint32))
+        idx.check()
+    finally:
+        c.destroy()

@@ -411,21 +411,13 @@ def test_pq_scan_parity(ctx, orc, metric):
     assert np.array_equal(ids1, ids2)
 
 
-def _tuning(key, value):
-    lib = _lib.load()
-    lib.wvgx_set_tuning.restype = ctypes.c_int
-    lib.wvgx_set_tuning.argtypes = [ctypes.c_int, ctypes.c_int]
-    return lib.wvgx_set_tuning(key, value)
-
-
-@pytest.mark.parametrize("min3", [1, 0])
-def test_pq_encode_argmin_ties_and_nonfinite(ctx, orc, min3):
-    """nNearest's rule (CH/kmeans.go:126-130: replace on !(minD < d)) under the
-    encoder's min3 pair argmin (tuning key 14 = 1) and the plain loop (0):
-    exact ties inside a centroid pair and across pairs go to the highest
-    index, rows with NaN take the reference loop, rows whose every distance
-    overflows to +inf keep centroid 0, and a codebook holding a NaN disables
-    the min3 path."""
+def test_pq_encode_argmin_ties_and_nonfinite(ctx, orc):
+    """nNearest's rule (CH/kmeans.go:126-130: replace on !(minD < d)) on both
+    encoder paths -- the min3 pair argmin (NaN-free codebooks) and the
+    reference's compare-and-select loop (a codebook holding a NaN, or a row
+    with NaN in the segment): exact ties inside a centroid pair and across
+    pairs go to the highest index, rows with NaN take the reference loop, rows
+    whose every distance overflows to +inf keep centroid 0."""
     from weaviate_amd.compressionhelpers import ProductQuantizer
 
     m, ks, d = 32, 256, 128
@@ -440,23 +432,19 @@ def test_pq_encode_argmin_ties_and_nonfinite(ctx, orc, min3):
     X[70, 127] = np.nan                # a NaN in the second wave of the batch
     X[9, 12:16] = np.float32(3e38)     # segment 3: every distance overflows to +inf
     X[10, 0:4] = np.inf                # segment 0: +inf distances
-    old = _tuning(14, min3)
-    try:
-        for cb in (centers, None):
-            if cb is None:  # NaN in the codebook: the pair path must not use min3
-                cb = centers.copy()
-                cb[2, 17, 1] = np.nan
-            want = orc.pq_encode(X, cb)
-            pq = ProductQuantizer(ctx, cb)
-            assert np.array_equal(pq.EncodeBatch(X), want)
-            c = Corpus(ctx, KIND_PQ, METRIC_L2, d, len(X))
-            c.set_codebook(cb)
-            c.upsert(np.arange(len(X), dtype=np.uint64), X)
-            got = c.get_batch(np.arange(len(X), dtype=np.uint64), pq_m=m)[0]
-            assert np.array_equal(got, want)
-            c.destroy()
-    finally:
-        _tuning(14, old)
+    for cb in (centers, None):
+        if cb is None:  # NaN in the codebook: the pair path must not use min3 (the loop sees the same ties)
+            cb = centers.copy()
+            cb[2, 17, 1] = np.nan
+        want = orc.pq_encode(X, cb)
+        pq = ProductQuantizer(ctx, cb)
+        assert np.array_equal(pq.EncodeBatch(X), want)
+        c = Corpus(ctx, KIND_PQ, METRIC_L2, d, len(X))
+        c.set_codebook(cb)
+        c.upsert(np.arange(len(X), dtype=np.uint64), X)
+        got = c.get_batch(np.arange(len(X), dtype=np.uint64), pq_m=m)[0]
+        assert np.array_equal(got, want)
+        c.destroy()
 
 
 def test_pq_encode_corpus(ctx, orc):
@@ -547,70 +535,53 @@ def test_search_device_matches_host_api(ctx, orc):
             assert np.array_equal(oc.cpu().numpy(), hc.astype(np.int32))
 
 
-@pytest.mark.parametrize("mode", [0, 1])
-def test_search_device_pipelined_matches_host_api(ctx, orc, mode):
-    """nq single-query scans in one call: mode 0 = one launch per query with the
-    merge folded into the next launch; mode 1 = one query-stream launch."""
-    import ctypes
-
+def test_search_device_pipelined_matches_host_api(ctx, orc):
+    """nq single-query scans in one query-stream launch (the merge workgroup
+    merges each query while the scan moves on) == the host API."""
     import torch
 
     n, d = 30000 + 7, 128
     lib = _lib.load()
-    lib.wvgx_set_tuning.restype = ctypes.c_int
-    lib.wvgx_set_tuning.argtypes = [ctypes.c_int, ctypes.c_int]
-    old = lib.wvgx_set_tuning(2, mode)
     dev = torch.device("cuda:0")
-    try:
-        for metric in [METRIC_L2, METRIC_DOT]:
-            c = Corpus(ctx, KIND_F32, metric, d, n)
-            c.fill_synthetic(5, n, 0)
-            c.delete(np.array([0, 1, 77, 30000], np.uint64))
-            for nq, k in [(1, 10), (2, 10), (5, 100), (16, 10), (3, 256)]:
-                ws = torch.zeros(lib.wvg_search_workspace_size(c.handle, nq, k), dtype=torch.uint8, device=dev)
-                outs = []
-                for rep in range(2):  # two calls back to back on one workspace, no sync between them
-                    qs = orc.synth_rows(9 + nq + 100 * rep, 0, nq, d, 0)
-                    tq = torch.from_numpy(qs).to(dev)
-                    oi = torch.empty((nq, k), dtype=torch.int64, device=dev)
-                    od = torch.empty((nq, k), dtype=torch.float32, device=dev)
-                    oc = torch.empty(nq, dtype=torch.int32, device=dev)
-                    _lib.check(lib.wvg_search_device_pipelined(c.handle, tq.data_ptr(), nq, k, oi.data_ptr(),
-                                                               od.data_ptr(), oc.data_ptr(), ws.data_ptr(),
-                                                               ws.numel(), torch.cuda.current_stream().cuda_stream))
-                    outs.append((qs, tq, oi, od, oc))
-                torch.cuda.synchronize()
-                for qs, _, oi, od, oc in outs:
-                    hid, hd, hc = c.search(qs, k)  # host API (nq concurrent scans in one launch)
-                    assert np.array_equal(oi.cpu().numpy().view(np.uint64), hid)
-                    assert np.array_equal(bits(od.cpu().numpy()), bits(hd))
-                    assert np.array_equal(oc.cpu().numpy(), hc.astype(np.int32))
-            c.destroy()
-    finally:
-        lib.wvgx_set_tuning(2, old)
+    for metric in [METRIC_L2, METRIC_DOT]:
+        c = Corpus(ctx, KIND_F32, metric, d, n)
+        c.fill_synthetic(5, n, 0)
+        c.delete(np.array([0, 1, 77, 30000], np.uint64))
+        for nq, k in [(1, 10), (2, 10), (5, 100), (16, 10), (3, 256)]:
+            ws = torch.zeros(lib.wvg_search_workspace_size(c.handle, nq, k), dtype=torch.uint8, device=dev)
+            outs = []
+            for rep in range(2):  # two calls back to back on one workspace, no sync between them
+                qs = orc.synth_rows(9 + nq + 100 * rep, 0, nq, d, 0)
+                tq = torch.from_numpy(qs).to(dev)
+                oi = torch.empty((nq, k), dtype=torch.int64, device=dev)
+                od = torch.empty((nq, k), dtype=torch.float32, device=dev)
+                oc = torch.empty(nq, dtype=torch.int32, device=dev)
+                _lib.check(lib.wvg_search_device_pipelined(c.handle, tq.data_ptr(), nq, k, oi.data_ptr(),
+                                                           od.data_ptr(), oc.data_ptr(), ws.data_ptr(),
+                                                           ws.numel(), torch.cuda.current_stream().cuda_stream))
+                outs.append((qs, tq, oi, od, oc))
+            torch.cuda.synchronize()
+            for qs, _, oi, od, oc in outs:
+                hid, hd, hc = c.search(qs, k)  # host API (nq concurrent scans in one launch)
+                assert np.array_equal(oi.cpu().numpy().view(np.uint64), hid)
+                assert np.array_equal(bits(od.cpu().numpy()), bits(hd))
+                assert np.array_equal(oc.cpu().numpy(), hc.astype(np.int32))
+        c.destroy()
 
 
-@pytest.mark.parametrize("variant", [0, 2, 1, "0/pair", "0/pair+prio+skew"])
-@pytest.mark.parametrize("metric,d", [(METRIC_COSINE, 768), (METRIC_DOT, 256), (METRIC_COSINE, 1536), (METRIC_DOT, 512)])
-def test_batched_mfma_variants(ctx, orc, variant, metric, d):
-    """K3b (queries resident in LDS, rows streamed into MFMA operands; 0: two
-    waves per SIMD, 2: two query tiles per wave) and K3 (1) against the oracle:
-    ragged rows, deletes, an allow list, partial query blocks, SIFT-like ties.
-    "0/pair": SIMD partners share queries instead of rows (tuning key 12),
-    "+prio+skew": the second wave per SIMD at priority 1, started late (13, 5)."""
-    import ctypes
+@pytest.mark.parametrize("screen", [0, 1])
+@pytest.mark.parametrize("metric,d", [(METRIC_COSINE, 768), (METRIC_DOT, 256), (METRIC_COSINE, 1536), (METRIC_DOT, 512),
+                                      (METRIC_DOT, 128), (METRIC_COSINE, 96)])
+def test_batched_mfma_variants(ctx, orc, screen, metric, d):
+    """Batched dot / cosine on the matrix cores against the oracle: ragged
+    rows, deletes, an allow list, partial query blocks, SIFT-like ties.
+    screen 0: the exact fp32 MFMA kernels -- K3b (queries resident in LDS,
+    rows streamed into MFMA operands) for k <= 64 and d in {256 .. 1536}, K3
+    otherwise (k = 100, d = 128 / 96); screen 1: the context default, where
+    the bf16 screen + exact rescore takes the batches it applies to."""
+    from weaviate_amd.device import Context
 
-    lib = _lib.load()
-    lib.wvgx_set_tuning.restype = ctypes.c_int
-    lib.wvgx_set_tuning.argtypes = [ctypes.c_int, ctypes.c_int]
-    knobs = {4: 0}
-    if variant in (0, 1, 2):
-        knobs = {4: variant}
-    if isinstance(variant, str) and "pair" in variant:
-        knobs[12] = 1
-    if isinstance(variant, str) and "prio" in variant:
-        knobs.update({13: 1, 5: 40})
-    prev = {key: lib.wvgx_set_tuning(key, val) for key, val in knobs.items()}
+    cx = ctx if screen else Context(0, batch_screen=0)
     try:
         n, nq = 4000 + 45, 70
         rows = orc.synth_rows(700 + d, 0, n, d, 0)
@@ -618,7 +589,7 @@ def test_batched_mfma_variants(ctx, orc, variant, metric, d):
         if metric == METRIC_DOT:  # integer values: exact dots and many ties
             rows = np.floor(rows * 3).astype(np.float32)
             qs = np.floor(qs * 3).astype(np.float32)
-        c = Corpus(ctx, KIND_F32, metric, d, n)
+        c = Corpus(cx, KIND_F32, metric, d, n)
         c.upsert(np.arange(n, dtype=np.uint64), rows)
         srows = stored_rows(orc, metric, rows)
         valid = np.ones(n, np.uint8)
@@ -634,21 +605,22 @@ def test_batched_mfma_variants(ctx, orc, variant, metric, d):
             for qi in range(0, nq, 3):
                 all_d = orc.dist_all(ORC_METRIC[metric], prep_query(orc, metric, qs[qi]), srows)
                 check_topk(orc, ids[qi], dists[qi], counts[qi], all_d, np.arange(n, dtype=np.uint64), k, vm)
+        c.destroy()
     finally:
-        for key, val in prev.items():
-            lib.wvgx_set_tuning(key, val)
+        if cx is not ctx:
+            cx.close()
 
 
 
-@pytest.mark.parametrize("range_tiles", [-1, 0, 7])
-@pytest.mark.parametrize("variant", [0, 2])
-def test_batched_mfma_nonfinite_zero_and_ranges(ctx, orc, variant, range_tiles):
-    """K3b's float-distance rejection (!(dist > tau) before any key is built)
-    against the oracle on rows that give NaN, +-inf, -0.0 and +0.0 dot
-    products and exact ties; range_tiles 7: many short row ranges per query
-    block (tuning key 10), so lists restart often and the K2 merge sees
-    hundreds of partial lists."""
-    import ctypes
+@pytest.mark.parametrize("screen", [0, 1])
+def test_batched_mfma_nonfinite_zero_and_ranges(ctx, orc, screen):
+    """The batched kernels' float-distance rejection (!(dist > tau) before any
+    key is built) against the oracle on rows that give NaN, +-inf, -0.0 and
+    +0.0 dot products and exact ties; 94 tiles over 94 row ranges, so lists
+    restart often and the K2 merge sees many partial lists.  screen 0: exact
+    fp32 MFMA only; 1: the bf16 screen, whose error bound is infinite for the
+    non-finite rows (always rescored exactly)."""
+    from weaviate_amd.device import Context
 
     def check_lex(orc, ids, dists, count, all_d, k, valid):  # NaN sorts last (no heap comparison with NaN rows)
         sel = valid.astype(bool)
@@ -656,11 +628,7 @@ def test_batched_mfma_nonfinite_zero_and_ranges(ctx, orc, variant, range_tiles):
         assert count == len(li) and np.array_equal(ids[:count], li)
         assert np.array_equal(bits(dists[:count]), bits(ld))
 
-    lib = _lib.load()
-    lib.wvgx_set_tuning.restype = ctypes.c_int
-    lib.wvgx_set_tuning.argtypes = [ctypes.c_int, ctypes.c_int]
-    old4 = lib.wvgx_set_tuning(4, variant)
-    old10 = lib.wvgx_set_tuning(10, range_tiles)
+    cx = ctx if screen else Context(0, batch_screen=0)
     try:
         n, nq, d = 6000 + 13, 48, 256
         rows = np.floor(orc.synth_rows(900, 0, n, d, 0) * 2).astype(np.float32)
@@ -672,7 +640,7 @@ def test_batched_mfma_nonfinite_zero_and_ranges(ctx, orc, variant, range_tiles):
         rows[402] = -0.0
         rows[[403, 404]] = rows[405]        # exact ties
         qs[3, 5] = 0.0
-        c = Corpus(ctx, KIND_F32, METRIC_DOT, d, n)
+        c = Corpus(cx, KIND_F32, METRIC_DOT, d, n)
         c.upsert(np.arange(n, dtype=np.uint64), rows)
         valid = np.ones(n, np.uint8)
         c.delete(np.array([64, 3000], np.uint64))
@@ -689,26 +657,26 @@ def test_batched_mfma_nonfinite_zero_and_ranges(ctx, orc, variant, range_tiles):
         check_lex(orc, ids[0], dists[0], counts[0], all_d, 10, valid)
         c.destroy()
     finally:
-        lib.wvgx_set_tuning(4, old4)
-        lib.wvgx_set_tuning(10, old10)
+        if cx is not ctx:
+            cx.close()
 
 
-@pytest.mark.parametrize("policy", [1, 2])
-def test_flat_scan_load_policies(ctx, orc, policy):
-    """K1's row loads, non-temporal (1) or default-policy (2; tuning key 11 --
-    the library picks by scanned bytes), through the host search and the
-    query-stream device search: same bits as the oracle."""
-    import ctypes
-
+@pytest.mark.parametrize("reuse", [0, 1])
+def test_flat_scan_load_policies(ctx, orc, reuse):
+    """K1's row loads: the default context (reuse 1: default-policy loads at
+    this size, alternating directions) and a streaming context
+    (wvg_options.cache_reuse = 0: non-temporal loads, one direction), through
+    the host search and the query-stream device search: same bits as the
+    oracle."""
     import torch
 
+    from weaviate_amd.device import Context
+
     lib = _lib.load()
-    lib.wvgx_set_tuning.restype = ctypes.c_int
-    lib.wvgx_set_tuning.argtypes = [ctypes.c_int, ctypes.c_int]
-    old = lib.wvgx_set_tuning(11, policy)
+    cx = ctx if reuse else Context(0, cache_reuse=0)
     try:
         n, d, k, nq = 20_000 + 7, 128, 10, 5
-        c = Corpus(ctx, KIND_F32, METRIC_L2, d, n)
+        c = Corpus(cx, KIND_F32, METRIC_L2, d, n)
         c.fill_synthetic(71, n, 0)
         c.delete(np.array([3, 640], np.uint64))
         valid = np.ones(n, np.uint8)
@@ -732,4 +700,5 @@ def test_flat_scan_load_policies(ctx, orc, policy):
             check_topk(orc, ids[qi], dists[qi], counts[qi], all_d, np.arange(n, dtype=np.uint64), k, valid)
         c.destroy()
     finally:
-        lib.wvgx_set_tuning(11, old)
+        if cx is not ctx:
+            cx.close()

@@ -1,5 +1,9 @@
-"""K8b (rotated-segment ADC scan, m = 32, ks = 256) against the oracle and
-against K8 (segment-order gather), bit for bit.
+"""The m = 32, ks = 256 ADC scans against the oracle and against each other,
+bit for bit: K8e (dense corpora, no allow list; one query per call), K8e COS
+(co-scheduled batches), K8b (the rotated-segment scan that skips dead /
+disallowed tiles: allow lists, thin corpora) and K8 (segment-order gather,
+any m: here m = 16 on the same rows' codes' first half is not comparable, so
+K8 is pinned to the oracle in test_gpu_parity).
 
 K8b reads a different segment on every lane and keeps two rows in flight per
 lane, so these cases aim at its pipeline: many tiles per wave, fully deleted
@@ -7,8 +11,6 @@ tiles between live ones, ragged tails, allow lists, several queries per
 launch, every top-k width (E = 1, 2, 4) and non-finite LUT entries.
 PQDistancer.Distance: CH/product_quantization.go:352-361 (LookUp :85-104).
 """
-import ctypes
-
 import numpy as np
 import pytest
 
@@ -23,11 +25,22 @@ pytestmark = pytest.mark.gpu
 M, KS, D = 32, 256, 128
 
 
-def _variant(v):
-    lib = _lib.load()
-    lib.wvgx_set_tuning.restype = ctypes.c_int
-    lib.wvgx_set_tuning.argtypes = [ctypes.c_int, ctypes.c_int]
-    return lib.wvgx_set_tuning(7, v)
+def _paths(c, qs, k, allow=None):
+    """The same searches through every product path: one batch call (K8e COS
+    when dense and no allow list), one call per query (K8e), and with an
+    allow list admitting every row (K8b, which skips dead tiles)."""
+    n = c.info()[1]
+    batch = c.search(qs, k, allow=allow)
+    singles = [c.search(qs[i], k, allow=allow) for i in range(len(qs))]
+    single = tuple(np.concatenate([x[j] for x in singles]) for j in range(3))
+    every = allow if allow is not None else allow_bitmap(np.arange(n, dtype=np.uint64))
+    k8b = c.search(qs, k, allow=every)
+    return batch, single, k8b
+
+
+def _same(a, b):
+    for x, y in zip(a, b):
+        assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8))
 
 
 def adc_all(metric, lut, codes):
@@ -81,63 +94,57 @@ def test_rot_scan_vs_oracle(ctx, orc, big, metric):
     n, codes, centers, _, valid = big
     c = _corpus(ctx, metric, big)
     qs = orc.synth_rows(63, 0, 3, D, 0)
-    old = _variant(0)
     try:
         for k in (10, 100, 200):
-            ids, dists, counts = c.search(qs, k)
+            paths = _paths(c, qs, k)
+            for p in paths[1:]:
+                _same(paths[0], p)
+            ids, dists, counts = paths[0]
             for qi in range(len(qs)):
                 lut = orc.pq_lut(ORC_METRIC[metric], qs[qi], centers)
                 all_d = adc_all(ORC_METRIC[metric], lut, codes)
                 check_topk(orc, ids[qi], dists[qi], counts[qi], all_d, np.arange(n, dtype=np.uint64), k, valid)
     finally:
-        _variant(old)
         c.destroy()
 
 
 @pytest.mark.parametrize("metric", [METRIC_L2, METRIC_DOT, METRIC_COSINE])
-def test_rot_equals_gather_variant(ctx, orc, big, metric):
+def test_rot_paths_agree(ctx, orc, big, metric):
+    """K8e, K8e COS and K8b give the same bits, with and without a real allow
+    list (an allow list sends every call to K8b, so then the three calls
+    differ only in batching)."""
     n = big[0]
     c = _corpus(ctx, metric, big)
     qs = orc.synth_rows(64, 0, 2, D, 0)
     allow = allow_bitmap(np.arange(0, n, 3, dtype=np.uint64))
-    old = _variant(0)
     try:
-        for k, al in [(10, None), (64, allow), (150, None)]:
-            _variant(1)
-            b = c.search(qs, k, allow=al)
-            for v in (0, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 29, 30, 31, 32, 33, 35, 36, 37, 38, 39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 49):
-                # K8b: ring 6, ring 4, interleaved waves, LDS batches 32 / 8, dense (no tile skip) rings 6 / 4 / 8;
-                # K8c rings 8 / 4 / 8; K8b forced; K8d (buffer / global loads); K8c one-v_perm addresses; K8e
-                _variant(v)
-                a = c.search(qs, k, allow=al)
-                for x, y in zip(a, b):
-                    assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8)), v
+        for k, al in [(10, None), (64, allow), (150, None), (256, None)]:
+            paths = _paths(c, qs, k, al)
+            for p in paths[1:]:
+                _same(paths[0], p)
     finally:
-        _variant(old)
         c.destroy()
 
 
 def test_rot_nonfinite_lut(ctx, orc, big):
     """Queries far outside the codebook overflow LUT entries to +inf; rows that
-    hit them must tie at inf in both variants, the others stay exact."""
-    n = big[0]
+    hit them must tie at inf on every path, the others stay exact."""
+    n, codes, centers, _, valid = big
     c = _corpus(ctx, METRIC_L2, big)
     q = orc.synth_rows(65, 0, 1, D, 0)[0].copy()
     q[:4] = 3e19  # segment 0: (3e19 - c)^2 -> inf for every centroid
     q2 = orc.synth_rows(66, 0, 1, D, 0)[0].copy()
     q2[64:66] = 2e19  # one segment: inf once the squares are summed
-    old = _variant(0)
+    qs = np.stack([q, q2])
     try:
-        for qq in (q, q2):
-            _variant(1)
-            b = c.search(qq, 20)
-            for v in (0, 6, 10, 14, 17, 18, 20, 22, 29, 31, 35, 36, 38, 41, 42, 46):
-                _variant(v)
-                a = c.search(qq, 20)
-                for x, y in zip(a, b):
-                    assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8))
+        paths = _paths(c, qs, 20)
+        for p in paths[1:]:
+            _same(paths[0], p)
+        ids, dists, counts = paths[0]
+        for qi in range(2):
+            all_d = adc_all(0, orc.pq_lut(0, qs[qi], centers), codes)
+            check_topk(orc, ids[qi], dists[qi], counts[qi], all_d, np.arange(n, dtype=np.uint64), 20, valid)
     finally:
-        _variant(old)
         c.destroy()
 
 

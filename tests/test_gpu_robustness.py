@@ -21,12 +21,6 @@ def bits(x):
     return np.asarray(x, dtype=np.float32).view(np.uint32)
 
 
-def tuning(lib, key, value):
-    lib.wvgx_set_tuning.restype = ctypes.c_int
-    lib.wvgx_set_tuning.argtypes = [ctypes.c_int, ctypes.c_int]
-    return lib.wvgx_set_tuning(key, value)
-
-
 def test_create_then_fill_stored_rows_exact(ctx, orc):
     """Round 1's fault: the allocation's zero fill (null stream) could land
     after rows written on a pool stream.  Create + fill + reserve-grow
@@ -90,14 +84,21 @@ def test_device_search_on_empty_corpus_writes_empty_results(ctx):
 
 
 def test_query_stream_merge_timeout_is_reported(ctx, orc):
-    """A merge workgroup that gives up (forced: 1 us wait) makes
-    wvg_search_device_check fail, and the unmerged queries come back empty,
-    never with a previous call's results; the default wait then succeeds."""
+    """A merge workgroup that gives up (a context with a 1 us merge wait,
+    wvg_options.merge_wait_us) makes wvg_search_device_check fail, and the
+    unmerged queries come back empty, never with a previous call's results;
+    the default wait then succeeds."""
     import torch
+
+    from weaviate_amd.device import Context
 
     lib = _lib.load()
     n, d, k, nq = 1_000_000, 128, 10, 4
+    short = Context(0, merge_wait_us=1)
+    assert short.options["merge_wait_us"] == 1
     c = Corpus(ctx, KIND_F32, METRIC_L2, d, n)
+    cs = Corpus(short, KIND_F32, METRIC_L2, d, n)
+    cs.fill_synthetic(42, n, 0)
     c.fill_synthetic(42, n, 0)
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream().cuda_stream
@@ -107,22 +108,17 @@ def test_query_stream_merge_timeout_is_reported(ctx, orc):
     dd = torch.empty((nq, k), dtype=torch.float32, device=dev)
     cc = torch.empty(nq, dtype=torch.int32, device=dev)
 
-    def run():
-        _lib.check(lib.wvg_search_device_pipelined(c.handle, tq.data_ptr(), nq, k, ids.data_ptr(), dd.data_ptr(),
-                                                   cc.data_ptr(), ws.data_ptr(), ws.numel(), st))
+    def run(corpus):
+        _lib.check(lib.wvg_search_device_pipelined(corpus.handle, tq.data_ptr(), nq, k, ids.data_ptr(),
+                                                   dd.data_ptr(), cc.data_ptr(), ws.data_ptr(), ws.numel(), st))
 
-    old_mode = tuning(lib, 2, 1)
     try:
-        run()
+        run(c)
         _lib.check(lib.wvg_search_device_check(ctx.handle, ws.data_ptr(), st))
         good = ids.cpu().numpy().copy()
         assert (cc.cpu().numpy() == k).all()
-        old = tuning(lib, 8, 1)
-        try:
-            run()
-            rc = lib.wvg_search_device_check(ctx.handle, ws.data_ptr(), st)
-        finally:
-            tuning(lib, 8, old)
+        run(cs)  # the same rows and workspace, the 1 us merge bound
+        rc = lib.wvg_search_device_check(short.handle, ws.data_ptr(), st)
         assert rc == _lib.WVG_ERR_DEVICE
         assert b"timed out" in lib.wvg_last_error()
         got_c = cc.cpu().numpy()
@@ -134,12 +130,13 @@ def test_query_stream_merge_timeout_is_reported(ctx, orc):
                 assert np.array_equal(got_i[qi], good[qi])
         assert (got_c == 0).any()
         # the check cleared the sticky word; a normal call passes again
-        run()
+        run(c)
         _lib.check(lib.wvg_search_device_check(ctx.handle, ws.data_ptr(), st))
         assert np.array_equal(ids.cpu().numpy(), good)
     finally:
-        tuning(lib, 2, old_mode)
         c.destroy()
+        cs.destroy()
+        short.close()
 
 
 @pytest.mark.parametrize("kind", [KIND_F32, KIND_BQ])
@@ -226,39 +223,47 @@ def test_merge_packed_equals_merge_device(ctx, orc):
         assert np.array_equal(outs[1][0][qi], wi) and np.array_equal(bits(outs[1][1][qi]), bits(wd))
 
 
-def test_serpentine_scan_order_does_not_change_results(ctx, orc):
-    """Consecutive scans alternate direction (tuning key 9): the lexicographic
-    top-k does not depend on the order rows are visited, so every call gives
-    the same bits with the alternation on or off -- K1 (host API, query-stream
-    kernel), K8c (PQ m = 32) and the BQ scan."""
+def test_cache_reuse_scan_order_does_not_change_results(ctx, orc):
+    """With wvg_options.cache_reuse (the default) consecutive scans alternate
+    direction and read their tail with the default cache policy; with it off
+    every scan walks upwards with non-temporal loads.  The lexicographic top-k
+    does not depend on the order rows are visited, so every call gives the
+    same bits in both contexts -- K1 (host API, query-stream kernel), K8e
+    (PQ m = 32) and the BQ scan, three calls in a row each."""
     import torch
+
+    from weaviate_amd.device import Context
 
     lib = _lib.load()
     n, d, k = 70_000 + 13, 128, 10
     qs = orc.synth_rows(77, 0, 5, d, 0)
-    f = Corpus(ctx, KIND_F32, METRIC_L2, d, n)
-    f.fill_synthetic(76, n, 0)
-    f.delete(np.array([3, 64, 69_999], np.uint64))
-    pq = Corpus(ctx, KIND_PQ, METRIC_DOT, d, n)
-    pq.set_codebook(orc.synth_rows(78, 0, 32 * 256, 4, 0).reshape(32, 256, 4))
-    _lib.check(lib.wvg_pq_encode_corpus(pq.handle, f.handle))
-    bq = Corpus(ctx, KIND_BQ, METRIC_COSINE, d, n)
-    bq.fill_synthetic(76, n, 0)
     dev = torch.device("cuda:0")
-    ws = torch.zeros(lib.wvg_search_workspace_size(f.handle, 5, k), dtype=torch.uint8, device=dev)
     tq = torch.from_numpy(qs).to(dev)
 
-    def device_stream():
-        oi = torch.empty((5, k), dtype=torch.int64, device=dev)
-        od = torch.empty((5, k), dtype=torch.float32, device=dev)
-        oc = torch.empty(5, dtype=torch.int32, device=dev)
-        _lib.check(lib.wvg_search_device_pipelined(f.handle, tq.data_ptr(), 5, k, oi.data_ptr(), od.data_ptr(),
-                                                   oc.data_ptr(), ws.data_ptr(), ws.numel(),
-                                                   torch.cuda.current_stream().cuda_stream))
-        torch.cuda.synchronize()
-        return oi.cpu().numpy(), od.cpu().numpy()
+    def build(cx):
+        f = Corpus(cx, KIND_F32, METRIC_L2, d, n)
+        f.fill_synthetic(76, n, 0)
+        f.delete(np.array([3, 64, 69_999], np.uint64))
+        pq = Corpus(cx, KIND_PQ, METRIC_DOT, d, n)
+        pq.set_codebook(orc.synth_rows(78, 0, 32 * 256, 4, 0).reshape(32, 256, 4))
+        _lib.check(lib.wvg_pq_encode_corpus(pq.handle, f.handle))
+        bq = Corpus(cx, KIND_BQ, METRIC_COSINE, d, n)
+        bq.fill_synthetic(76, n, 0)
+        return f, pq, bq
 
-    def run_all():
+    def run_all(f, pq, bq):
+        ws = torch.zeros(lib.wvg_search_workspace_size(f.handle, 5, k), dtype=torch.uint8, device=dev)
+
+        def device_stream():
+            oi = torch.empty((5, k), dtype=torch.int64, device=dev)
+            od = torch.empty((5, k), dtype=torch.float32, device=dev)
+            oc = torch.empty(5, dtype=torch.int32, device=dev)
+            _lib.check(lib.wvg_search_device_pipelined(f.handle, tq.data_ptr(), 5, k, oi.data_ptr(),
+                                                       od.data_ptr(), oc.data_ptr(), ws.data_ptr(), ws.numel(),
+                                                       torch.cuda.current_stream().cuda_stream))
+            torch.cuda.synchronize()
+            return oi.cpu().numpy(), od.cpu().numpy()
+
         out = []
         for rep in range(3):  # consecutive calls: directions alternate between them
             out.append(f.search(qs, k))
@@ -267,20 +272,23 @@ def test_serpentine_scan_order_does_not_change_results(ctx, orc):
             out.append(device_stream())
         return out
 
-    old = tuning(lib, 9, 0)
+    streaming = Context(0, cache_reuse=0)
     try:
-        want = run_all()
-        tuning(lib, 9, 1)
-        got = run_all()
-        got2 = run_all()
+        cs = build(streaming)
+        want = run_all(*cs)
+        for c in cs:
+            c.destroy()
+        cr = build(ctx)
+        got = run_all(*cr)
+        got2 = run_all(*cr)
+        for c in cr:
+            c.destroy()
     finally:
-        tuning(lib, 9, old)
+        streaming.close()
     for a_, b_, c_ in zip(want, got, got2):
         for x, y, z in zip(a_, b_, c_):
             assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8))
             assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(z).view(np.uint8))
-    for c in (f, pq, bq):
-        c.destroy()
 
 
 def test_pinned_host_buffers(ctx, orc):
@@ -324,27 +332,45 @@ def test_pinned_host_buffers(ctx, orc):
 @pytest.mark.parametrize("kind", [KIND_BQ, KIND_PQ])
 def test_cosched_batches_equal_single_queries(ctx, orc, kind):
     """Co-scheduled batches (K5 / K8e COS: the nq queries of a row range on one
-    XCD) return exactly what one query per call returns, with it on or off."""
+    XCD, workgroup id -> (range, query)) return exactly what one query per
+    call returns.  nq = 2 .. 300 covers the range-count floor of
+    pq_cosched_groups (8 ranges once nq >= num_cus / 8, where the queries of
+    a range are no longer all resident together), k = 256 the E = 4 top-k
+    (where the 16-wave PQ image does not fit and 8 waves run), and the BQ
+    batch also goes through searchByVectorBQ's rescore flow."""
+    from weaviate_amd.device import search_bq_rescore
+
     n, d = 50_000 + 37, 128
     rows = orc.synth_rows(600, 0, n, d, 0)
     c = Corpus(ctx, kind, METRIC_L2, d, n)
+    f = None
     if kind == KIND_PQ:
         centers = orc.synth_rows(601, 0, 32 * 256, d // 32, 0).reshape(32, 256, d // 32)
         c.set_codebook(centers)
+    else:
+        f = Corpus(ctx, KIND_F32, METRIC_L2, d, n)
+        f.upsert(np.arange(n, dtype=np.uint64), rows)
     c.upsert(np.arange(n, dtype=np.uint64), rows)
-    c.delete(np.arange(5, n, 97, dtype=np.uint64))
-    qs = orc.synth_rows(602, 0, 12, d, 0)
+    dead = np.arange(5, n, 97, dtype=np.uint64)
+    c.delete(dead)
+    if f is not None:
+        f.delete(dead)
+    qs_all = orc.synth_rows(602, 0, 300, d, 0)
     try:
-        for k in (10, 100, 200):
-            singles = [c.search(qs[i], k) for i in range(len(qs))]
-            for cos in (1, 0):
-                old = tuning(_lib.load(), 15, cos)
-                try:
-                    ids, dists, counts = c.search(qs, k)
-                finally:
-                    tuning(_lib.load(), 15, old)
+        for nq, ks in [(2, (10, 256)), (12, (10, 100, 200)), (40, (10, 256)), (300, (10,))]:
+            qs = qs_all[:nq]
+            for k in ks:
+                singles = [c.search(qs[i], k) for i in range(nq)]
+                ids, dists, counts = c.search(qs, k)
                 for i, (si, sd, sc) in enumerate(singles):
                     assert counts[i] == sc[0]
-                    assert np.array_equal(ids[i], si[0]) and np.array_equal(dists[i].view(np.uint32), sd[0].view(np.uint32))
+                    assert np.array_equal(ids[i], si[0]) and np.array_equal(bits(dists[i]), bits(sd[0]))
+            if f is not None and nq <= 40:
+                single = [search_bq_rescore(c, f, qs[i], 10, 200) for i in range(nq)]
+                bi, bd, bc = search_bq_rescore(c, f, qs, 10, 200)
+                for i, (si, sd, sc) in enumerate(single):
+                    assert bc[i] == sc[0] and np.array_equal(bi[i], si[0]) and np.array_equal(bits(bd[i]), bits(sd[0]))
     finally:
         c.destroy()
+        if f is not None:
+            f.destroy()

@@ -15,6 +15,8 @@ import time
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# A/B knobs (wvgx_set_tuning) exist only in the tools build: make -C weaviate_amd/csrc tools
+os.environ.setdefault("WVG_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "libwvgpu_tools.so"))
 
 
 def main():

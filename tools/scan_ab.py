@@ -15,6 +15,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+# A/B knobs (wvgx_set_tuning) exist only in the tools build: make -C weaviate_amd/csrc tools
+os.environ.setdefault("WVG_LIB", os.path.join(ROOT, "tools", "libwvgpu_tools.so"))
 
 
 def main():

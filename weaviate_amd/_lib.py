@@ -29,6 +29,14 @@ ORDER_AVX256, ORDER_AVX512 = 0, 1  # reference SIMD kernel whose reduction order
 METRIC_BY_NAME = {"l2-squared": METRIC_L2, "dot": METRIC_DOT, "cosine": METRIC_COSINE,
                   "cosine-dot": METRIC_COSINE, "manhattan": METRIC_MANHATTAN, "hamming": METRIC_HAMMING}
 
+
+
+class Options(ctypes.Structure):
+    """struct wvg_options (include/wvgpu.h): context options fixed at wvg_open_ex."""
+    _fields_ = [("size", c_uint32), ("mfma_min_queries", c_uint32), ("cache_reuse", ctypes.c_int32),
+                ("merge_wait_us", c_uint32), ("batch_screen", ctypes.c_int32)]
+
+
 # name -> (restype, argtypes); every symbol declared in include/wvgpu.h.
 _P = POINTER
 SIGNATURES = {
@@ -36,6 +44,8 @@ SIGNATURES = {
     "wvg_last_error": (c_char_p, []),
     "wvg_device_count": (c_int, [_P(c_int)]),
     "wvg_open": (c_int, [c_int, _P(c_void_p)]),
+    "wvg_options_default": (None, [_P(Options)]),
+    "wvg_open_ex": (c_int, [c_int, _P(Options), _P(c_void_p)]),
     "wvg_close": (c_int, [c_void_p]),
     "wvg_synchronize": (c_int, [c_void_p]),
     "wvg_host_alloc": (c_int, [c_void_p, c_uint64, POINTER(c_void_p)]),
@@ -81,6 +91,7 @@ SIGNATURES = {
     "wvg_synthetic_rows": (c_int, [c_void_p, c_uint64, _P(c_uint64), c_uint64, c_uint32, c_int, c_int, _P(c_float)]),
     "wvg_profile_start": (c_int, [c_void_p]),
     "wvg_profile_stop": (c_int, [c_void_p, _P(ctypes.c_double), _P(c_uint64)]),
+    "wvg_measure_hbm_read": (c_int, [c_void_p, c_uint64, c_uint32, _P(ctypes.c_double)]),
     "wvg_distance_batch": (c_int, [c_void_p, c_int, _P(c_float), _P(c_float), c_uint64, c_uint32, _P(c_float)]),
     "wvg_normalize_batch": (c_int, [c_void_p, _P(c_float), c_uint64, c_uint32, _P(c_float)]),
     "wvg_bq_encode": (c_int, [c_void_p, _P(c_float), c_uint64, c_uint32, _P(c_uint64)]),

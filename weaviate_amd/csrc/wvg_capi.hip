@@ -333,10 +333,29 @@ int wvg_device_count(int *out)
     return WVG_OK;
 }
 
-int wvg_open(int device, wvg_ctx **out)
+void wvg_options_default(wvg_options *o)
+{
+    if (!o) return;
+    *o = wvg_options{};
+    o->size = (uint32_t)sizeof(wvg_options);
+    o->mfma_min_queries = 32;
+    o->cache_reuse = 1;
+    o->merge_wait_us = 0;
+    o->batch_screen = 1;
+}
+
+int wvg_open(int device, wvg_ctx **out) { return wvg_open_ex(device, nullptr, out); }
+
+int wvg_open_ex(int device, const wvg_options *opts, wvg_ctx **out)
 {
     if (!out) return fail(WVG_ERR_INVALID, "null out");
     *out = nullptr;
+    wvg_options o;
+    wvg_options_default(&o);
+    if (opts) {
+        if (opts->size != sizeof(wvg_options)) return fail(WVG_ERR_INVALID, "wvg_options.size mismatch");
+        o = *opts;
+    }
     int n = 0;
     WVG_HIP(hipGetDeviceCount(&n));
     if (device < 0 || device >= n) return fail(WVG_ERR_INVALID, "device index out of range");
@@ -346,10 +365,13 @@ int wvg_open(int device, wvg_ctx **out)
     wvg_ctx *c = new wvg_ctx();
     c->device = device;
     c->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-    if (const char *e = getenv("WVG_MFMA_MIN_QUERIES")) c->mfma_min_nq = (uint32_t)strtoul(e, nullptr, 10);
+    c->opt = o;
+#ifdef WVG_TOOLS
+    if (const char *e = getenv("WVG_MFMA_MIN_QUERIES")) c->opt.mfma_min_queries = (uint32_t)strtoul(e, nullptr, 10);
     if (const char *e = getenv("WVG_SERPENTINE")) tuning().serpentine = (int)strtol(e, nullptr, 10);  // A/B runs
     if (const char *e = getenv("WVG_K1_TAIL")) tuning().k1_tail = (int)strtol(e, nullptr, 10);        // A/B runs
     if (const char *e = getenv("WVG_K1_LOADS")) tuning().k1_loads = (int)strtol(e, nullptr, 10);        // A/B runs
+#endif
     *out = c;
     return WVG_OK;
 }
@@ -967,7 +989,7 @@ struct ProfArm {
 // query-stream kernel alternates per query from the returned start).
 static uint32_t next_direction(wvg_corpus *c, uint32_t nq)
 {
-    if (!tuning().serpentine) return 0u;
+    if (!c->ctx->opt.cache_reuse || !tuning().serpentine) return 0u;
     return (uint32_t)(c->scan_serial.fetch_add(nq, std::memory_order_relaxed) & 1u);
 }
 
@@ -986,6 +1008,7 @@ static int plain_loads(const wvg_corpus *c, uint64_t tb, uint64_t te)
 {
     const int v = tuning().k1_loads;
     if (v) return v == 2;
+    if (!c->ctx->opt.cache_reuse) return 0;  // streaming: every row load non-temporal
     return c->kind == WVG_KIND_F32 && (te - tb) * (uint64_t)c->nchunks * 1024ull <= (800ull << 20);
 }
 
@@ -1003,7 +1026,7 @@ static uint32_t k1_cache_tail(const wvg_corpus *c, uint64_t tb, uint64_t te)
     const int v = tuning().k1_tail;
     // F32 scans only: the same split in K8e's PQ code loads (tail 25/256 at 100M
     // codes) measured no gain -- that scan is not purely memory-bound
-    if (c->kind != WVG_KIND_F32 || v < 0) return 0u;
+    if (c->kind != WVG_KIND_F32 || v < 0 || !c->ctx->opt.cache_reuse) return 0u;
     if (v > 0) return (uint32_t)std::min(v, 256);
     if (!tuning().serpentine || tuning().k1_loads) return 0u;  // no reversal / a forced policy (A/B)
     const uint64_t bytes = (te - tb) * (uint64_t)c->nchunks * 1024ull;
@@ -1039,7 +1062,7 @@ static SearchPlan plan_search(wvg_corpus *c, uint32_t nq, uint32_t k, const uint
     a.nq = nq;
     a.dim = c->kind == WVG_KIND_F32 ? c->dim : 0;  // K1 grid depends on the row size and metric
     a.metric = c->metric;
-    const uint32_t mn = c->ctx->mfma_min_nq;
+    const uint32_t mn = c->ctx->opt.mfma_min_queries;
     p.gemm = c->kind == WVG_KIND_F32 && mn > 0 && nq >= mn && gemm_supported(c->dim, c->metric) &&
              !c->ctx->order512;  // K3's 32 MFMA slices are the AVX2 order's chains
     if (p.gemm)
@@ -1664,6 +1687,7 @@ int wvg_search_bq_rescore(wvg_corpus *bq, wvg_corpus *f32, const float *queries,
     a.qpitch = qpb;
     a.nq = nq;
     a.k = R;
+    a.cosched = p.cosched;  // the plan's group count assumes the co-scheduled K5 grid (nq > 1)
     a.reverse = next_direction(bq, 1);
     uint64_t *part = (uint64_t *)(b + o_part);
     WVG_HIP(launch_scan_bq(a, part, p.groups, s));
@@ -1746,7 +1770,7 @@ int wvg_search_device_pipelined(wvg_corpus *c, const float *d_queries, uint32_t 
         WVG_HIP(launch_fill_empty(d_ids, d_dists, d_counts, nq, k, s));
         return WVG_OK;
     }
-    if (tuning().pipeline_mode == 1) {  // query-stream kernel: one launch for all nq queries
+    if (tuning().pipeline_mode == 1) {  // query-stream kernel: one launch for all nq queries (the product path)
         const StreamLayout l = stream_layout(p, nq, k);
         if (!d_workspace || workspace_bytes < l.total) return fail(WVG_ERR_INVALID, "workspace too small");
         char *w = (char *)d_workspace;
@@ -1754,7 +1778,8 @@ int wvg_search_device_pipelined(wvg_corpus *c, const float *d_queries, uint32_t 
         j.partials = (uint64_t *)(w + l.partials);
         j.arrivals = (uint32_t *)(w + l.arrivals);
         j.status = (uint32_t *)w;
-        j.wait_limit = tuning().merge_wait_us > 0 ? (uint64_t)tuning().merge_wait_us * 100ull : 400000000ull;
+        const uint32_t wait_us = tuning().merge_wait_us > 0 ? (uint32_t)tuning().merge_wait_us : c->ctx->opt.merge_wait_us;
+        j.wait_limit = wait_us > 0 ? (uint64_t)wait_us * 100ull : 400000000ull;
         j.groups = (uint32_t)p.groups;
         j.ids = d_ids;
         j.dists = d_dists;
@@ -1782,6 +1807,8 @@ int wvg_search_device_pipelined(wvg_corpus *c, const float *d_queries, uint32_t 
         WVG_HIP(launch_scan_f32_stream(a, j, s));
         return WVG_OK;
     }
+#ifdef WVG_TOOLS
+    // A/B (pipeline_mode 0): one scan launch per query, query i's launch merging query i-1
     const size_t half = align_up(p.workspace_bytes(1, k), 256);
     if (!d_workspace || workspace_bytes < WS_STATUS_BYTES + 2 * half) return fail(WVG_ERR_INVALID, "workspace too small");
     char *w0 = (char *)d_workspace + WS_STATUS_BYTES;
@@ -1818,6 +1845,9 @@ int wvg_search_device_pipelined(wvg_corpus *c, const float *d_queries, uint32_t 
     WVG_HIP(launch_merge_lists(buf[last & 1], 1, (uint32_t)p.groups, k, k, c->id_base, d_ids + (size_t)last * k,
                                d_dists + (size_t)last * k, d_counts ? d_counts + last : nullptr, s));
     return WVG_OK;
+#else
+    return fail(WVG_ERR_UNSUPPORTED, "pipeline mode");
+#endif
 }
 
 int wvg_search_device(wvg_corpus *c, const float *d_queries, uint32_t nq, uint32_t k, uint64_t *d_ids, float *d_dists,
@@ -2006,7 +2036,8 @@ int wvg_synthetic_rows(wvg_ctx *ctx, uint64_t seed, const uint64_t *ids, uint64_
     return WVG_OK;
 }
 
-// Internal A/B knob (not part of include/wvgpu.h): 0 = K1 scan variant,
+#ifdef WVG_TOOLS
+// A/B knob of the tools build (not part of include/wvgpu.h): 0 = K1 scan variant,
 // 1 = K1 resident workgroups per CU, ... 7 = K8 ADC variant, 8 = query-stream merge wait (us),
 // 9 = serpentine scan order, 10 = K3b row-range length, 11 = K1 load policy, 12 = K3b SIMD pairing,
 // 13 = K3b partner priority, 14 = PQ encode min3 argmin, 15 = co-scheduled PQ / BQ batches, 16 = co-scheduled BQ workgroups per CU.  Returns the previous value.
@@ -2067,6 +2098,49 @@ int wvgx_set_tuning(int key, int value)
         t.bq_cos_gpc = value;
     }
     return old;
+}
+#endif
+
+int wvg_measure_hbm_read(wvg_ctx *ctx, uint64_t bytes, uint32_t reps, double *out_gbps)
+{
+    if (!ctx || !out_gbps) return fail(WVG_ERR_INVALID, "null argument");
+    *out_gbps = 0.0;
+    bytes = bytes / 4096 * 4096;
+    if (bytes == 0 || reps == 0) return fail(WVG_ERR_INVALID, "bytes and reps must be > 0");
+    WVG_HIP(hipSetDevice(ctx->device));
+    void *buf = nullptr;
+    if (hipMalloc(&buf, bytes + 256) != hipSuccess) return fail(WVG_ERR_NOMEM, "probe buffer hipMalloc");
+    SlotGuard g(ctx);
+    hipEvent_t a = nullptr, b = nullptr;
+    auto done = [&](int rc) {
+        if (g.slot) (void)hipStreamSynchronize(g.slot->stream);
+        if (a) (void)hipEventDestroy(a);
+        if (b) (void)hipEventDestroy(b);
+        (void)hipFree(buf);
+        return rc;
+    };
+    int rc = ctx->acquire(&g.slot);
+    if (rc) return done(rc);
+    const hipStream_t s = g.slot->stream;
+    float *sink = (float *)((char *)buf + bytes);
+    if (hipMemsetAsync(buf, 0, bytes + 256, s) != hipSuccess || hipEventCreate(&a) != hipSuccess ||
+        hipEventCreate(&b) != hipSuccess)
+        return done(fail(WVG_ERR_DEVICE, "probe setup"));
+    double best = 0.0;
+    for (int blocks : {1024, 2048, 4096, 8192}) {
+        for (int w = 0; w < 2; w++)
+            if (launch_hbm_read(buf, bytes, blocks, sink, s) != hipSuccess) return done(fail(WVG_ERR_DEVICE, "probe"));
+        (void)hipEventRecord(a, s);
+        for (uint32_t r = 0; r < reps; r++)
+            if (launch_hbm_read(buf, bytes, blocks, sink, s) != hipSuccess) return done(fail(WVG_ERR_DEVICE, "probe"));
+        (void)hipEventRecord(b, s);
+        float ms = 0.f;
+        if (hipEventSynchronize(b) != hipSuccess || hipEventElapsedTime(&ms, a, b) != hipSuccess || ms <= 0.f)
+            return done(fail(WVG_ERR_DEVICE, "probe timing"));
+        best = std::max(best, (double)bytes * reps / (ms * 1e-3) / 1e9);
+    }
+    *out_gbps = best;
+    return done(WVG_OK);
 }
 
 int wvg_profile_start(wvg_ctx *ctx)
@@ -2141,13 +2215,23 @@ int wvg_normalize_batch(wvg_ctx *ctx, const float *X, uint64_t n, uint32_t dim, 
     Bulk bk(ctx);
     int rc = bk.begin(cv.off);
     if (rc) return rc;
-    const size_t bytes = n * dim * 4;  // in and out through the slot's pinned staging (see wvg_rescore)
-    void *pin = nullptr;
-    rc = bk.g.slot->host_pinned(bytes, &pin);
+    // in and out through the slot's pinned staging (see wvg_rescore) up to
+    // STAGE_MAX; larger inputs are copied straight from / to the caller's
+    // buffers (pageable copies), so a bulk normalize never pins its whole
+    // input for the life of the context
+    const size_t bytes = n * dim * 4;
+    const bool direct = stage_bytes(bytes) == 0 || host_pinned_ptr(X);
+    Staging st;
+    rc = st.reserve(bk.g.slot, direct ? 0 : stage_bytes(bytes));
     if (rc) return rc;
-    std::memcpy(pin, X, bytes);
-    WVG_HIP(hipMemcpyAsync(bk.b + o_x, pin, bytes, hipMemcpyHostToDevice, bk.s()));
+    WVG_HIP(st.h2d(bk.b + o_x, X, bytes, bk.s()));
     WVG_HIP(launch_normalize_rows((const float *)(bk.b + o_x), n, dim, (float *)(bk.b + o_o), bk.s()));
+    if (direct || host_pinned_ptr(out)) {
+        WVG_HIP(hipMemcpyAsync(out, bk.b + o_o, bytes, hipMemcpyDeviceToHost, bk.s()));
+        WVG_HIP(hipStreamSynchronize(bk.s()));
+        return WVG_OK;
+    }
+    char *pin = st.p;  // the input's staging piece, free again once the input copy has run
     WVG_HIP(hipMemcpyAsync(pin, bk.b + o_o, bytes, hipMemcpyDeviceToHost, bk.s()));
     WVG_HIP(hipStreamSynchronize(bk.s()));
     std::memcpy(out, pin, bytes);

@@ -763,11 +763,19 @@ hipError_t launch_gemm_topk(const ScanArgs &s, uint32_t nrr, uint64_t *partials,
             if (e != hipSuccess) return e;
         }
         const uint32_t lds = (uint32_t)rc.lds;
+#ifdef WVG_TOOLS
+#define WVG_RS_QT2(DD, NBF)                                                                            \
+        if (rc.qt == 2) {                                                                              \
+            launch_timed((gemm_rs_kernel<DD, 2, 1, NBF>), grid, block, lds, st, a, partials);          \
+            return hipGetLastError();                                                                  \
+        }
+#else
+#define WVG_RS_QT2(DD, NBF)
+#endif
 #define WVG_RS(DD, NBF)                                                                                \
     case DD:                                                                                           \
-        if (rc.qt == 2)                                                                                \
-            launch_timed((gemm_rs_kernel<DD, 2, 1, NBF>), grid, block, lds, st, a, partials);          \
-        else if (rc.qh == 2)                                                                           \
+        WVG_RS_QT2(DD, NBF)                                                                            \
+        if (rc.qh == 2)                                                                                \
             launch_timed((gemm_rs_kernel<DD, 1, 2, 2>), grid, block, lds, st, a, partials);            \
         else                                                                                           \
             launch_timed((gemm_rs_kernel<DD, 1, 1, NBF>), grid, block, lds, st, a, partials);          \
@@ -781,14 +789,17 @@ hipError_t launch_gemm_topk(const ScanArgs &s, uint32_t nrr, uint64_t *partials,
         default: break;
         }
 #undef WVG_RS
+#undef WVG_RS_QT2
     }
     a.nqb = (s.nq + GQ - 1) / GQ;
     const size_t lds = (size_t)2 * (GQ + GR) * GSTRIDE * 4 + (size_t)GQ * GR * 8;
     dim3 grid(a.nqb * a.nrr), block(GWAVES * 64);
     if (s.k <= 64)
+#ifdef WVG_TOOLS
         if (tuning().gemm_pf == 1)
             launch_timed((gemm_topk_kernel<1, 1>), grid, block, lds, st, a, partials);
         else
+#endif
             launch_timed((gemm_topk_kernel<1, 2>), grid, block, lds, st, a, partials);
     else if (s.k <= 128)
         launch_timed((gemm_topk_kernel<2, 1>), grid, block, lds, st, a, partials);

@@ -43,7 +43,7 @@ struct StreamSlot {
 struct wvg_ctx {
     int device = 0;
     int num_cus = 256;
-    uint32_t mfma_min_nq = 32;  // batches of >= this many dot/cosine queries use K3 (env WVG_MFMA_MIN_QUERIES; 0 = never)
+    wvg_options opt{};          // fixed at wvg_open / wvg_open_ex
     int order512 = 0;           // distancer kernels of an AMX + AVX-512 host (wvg_set_distance_order)
     std::mutex pool_mu;
     std::vector<wvg::StreamSlot *> free_slots;
@@ -256,7 +256,11 @@ uint32_t gemm_row_ranges(uint32_t nq, uint64_t ntiles, int num_cus, uint32_t dim
 // gbound: [nq] u32 workspace (set to 0xFF.. here) for K3b's per-query distance bounds.
 hipError_t launch_gemm_topk(const ScanArgs &a, uint32_t nrr, uint64_t *partials, uint32_t *prog, uint32_t *gbound,
                             int num_cus, hipStream_t s);
-// Internal tuning knobs (wvgx_set_tuning; A/B experiments, not public ABI).
+// A/B knobs of the tools build (make -C weaviate_amd/csrc tools ->
+// tools/libwvgpu_tools.so, -DWVG_TOOLS, which exports wvgx_set_tuning and
+// compiles the tuning / diagnostic kernel variants).  In the product library
+// tuning() is a constant holding these defaults: nothing here can change at
+// run time, and every per-deployment choice is a context option (wvg_options).
 struct Tuning {
     int scan_variant = 0;    // K1 variant (see wvg_scan.hip)
     int groups_per_cu = 0;   // K1 workgroups per CU; 0 = auto by row size (scan_groups_for)
@@ -287,7 +291,11 @@ struct Tuning {
     int pq_encode_min3 = 1;  // PQ encode pair path: min3 argmin on NaN-free codebooks (1) or the
                              // reference's compare-and-select loop everywhere (0; A/B and parity)
 };
+#ifdef WVG_TOOLS
 Tuning &tuning();
+#else
+const Tuning &tuning();
+#endif
 // Profiling: events armed by the host runtime (wvg_profile_start) are bound to
 // the next scan-kernel dispatch itself (hipExtLaunchKernel), so timing adds no
 // marker packets -- a hipEventRecord pair around each launch cost ~5 us of idle
@@ -406,6 +414,7 @@ hipError_t launch_pq_sdc_rows(int metric, const float *table, uint32_t m, uint32
 hipError_t launch_dist_by_ids(const ScanArgs &a, int kind, uint64_t capacity, const uint64_t *ids, uint64_t n,
                               float *out, uint8_t *ok, hipStream_t s,
                               const uint32_t *qidx = nullptr);
+hipError_t launch_hbm_read(const void *p, uint64_t bytes, int blocks, float *out, hipStream_t s);
 hipError_t launch_set_valid(uint64_t *valid, const uint64_t *slots, uint64_t n, int set,
                             hipStream_t s);
 

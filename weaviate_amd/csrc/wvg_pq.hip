@@ -676,6 +676,9 @@ constexpr uint32_t PQ32_IMG7_BYTES = PQ32_IMG7_B + 65536u;
 template <int E>
 constexpr uint32_t PQ32_IMG7_BASE = (uint32_t)PQ_SCAN_WAVES * 64u * E * 8u;
 
+#ifdef WVG_TOOLS
+// K8c is a tools-build kernel: K8e (below) replaced it as the dense path, and
+// K8b serves the product wherever K8e's LDS layout check fails.
 // ACT < 16 (diagnostic): only the first ACT waves of the workgroup scan (the
 // occupancy the scan needs: ACT / 4 waves per SIMD).
 template <int E, int R, int NB, int METRIC, int W = 0, int ACT = PQ_SCAN_WAVES>
@@ -886,6 +889,7 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_dense_kernel(Sca
     }
     group_combine_store<E, PQ_SCAN_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
 }
+#endif  // WVG_TOOLS
 
 // K8e: K8c's sums and the one-v_perm image (W = 7) with fewer, wider waves.
 // A/B on MI355X (profiles/r02/pq_adc/k8e_*.jsonl): letting only 8 or 12 of
@@ -1097,7 +1101,8 @@ __global__ __launch_bounds__(WV * 64) void scan_pq32_wide_kernel(ScanArgs a, uin
     group_combine_store<E, WV>(tk, partials + ((size_t)qi * G + rng) * a.k);
 }
 
-// K8d: K8c with the R passes of a ring cycle in ONE basic block.  K8c's
+#ifdef WVG_TOOLS
+// K8d (tools build): K8c with the R passes of a ring cycle in ONE basic block.  K8c's
 // per-tile offer is a branch, so the compiler schedules every pass on its
 // own and the tail of a pass (its last adds waiting on LDS) cannot overlap
 // the head of the next (its byte merges and first LDS reads).  Here a pass
@@ -1277,6 +1282,7 @@ static bool img7_ok()
     }();
     return ok;
 }
+#endif  // WVG_TOOLS
 
 // K8e reads its image at the compile-time LDS address PQ32_WIDE_BASE: the
 // host launches an instantiation only where the static LDS really ends there
@@ -1310,7 +1316,13 @@ static bool launch_pq_wide(const ScanArgs &a, uint64_t *partials, int groups, hi
 }
 
 template <int E>
-static hipError_t launch_pq_e(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
+static hipError_t launch_pq_e(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s);
+
+#ifdef WVG_TOOLS
+// Tools build: every A/B and diagnostic variant (tuning key 7; variants 24-28
+// and 34 are diagnostics whose results are NOT distances).
+template <int E>
+static hipError_t launch_pq_e_variant(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
 {
     dim3 grid(groups, a.nq), block(PQ_SCAN_WAVES * 64);
     const size_t lds = (size_t)a.pq_m * a.pq_ks * 4;
@@ -1429,6 +1441,45 @@ static hipError_t launch_pq_e(const ScanArgs &a, uint64_t *partials, int groups,
         case 5: launch_timed((scan_pq32_rot_kernel<E, 6, false, 8>), grid, block, 4 * lds, s, a, partials); break;
         default: launch_timed((scan_pq32_rot_kernel<E, 6, false, 16>), grid, block, 4 * lds, s, a, partials); break;
         }
+        return hipGetLastError();
+    }
+    if (a.pq_ks == 256) {
+        switch (a.pq_m) {
+        case 8: launch_timed((scan_pq_kernel<E, 8, 256>), grid, block, lds, s, a, partials); return hipGetLastError();
+        case 16: launch_timed((scan_pq_kernel<E, 16, 256>), grid, block, lds, s, a, partials); return hipGetLastError();
+        case 32: launch_timed((scan_pq_kernel<E, 32, 256>), grid, block, lds, s, a, partials); return hipGetLastError();
+        case 64: launch_timed((scan_pq_kernel<E, 64, 256>), grid, block, lds, s, a, partials); return hipGetLastError();
+        default: break;
+        }
+    }
+    launch_timed((scan_pq_kernel<E, 0, 0>), grid, block, lds, s, a, partials);
+    return hipGetLastError();
+}
+#endif  // WVG_TOOLS
+
+// The product's ADC scan choice.  m = 32, ks = 256 (the rotated layout):
+//   - a co-scheduled batch (a.cosched: nq > 1, dense, no allow list): K8e COS,
+//     16 waves per CU (8 when the image and the E = 4 top-k buffer exceed the LDS);
+//   - a dense corpus (>= 3/4 of the slots live, no allow list): K8e, 8 waves;
+//   - otherwise (allow lists, many deletes -- dead tiles are skipped), and
+//     wherever K8e's compile-time LDS layout check fails: K8b;
+// any other (m, ks): K8, the LUT in LDS in segment order.
+template <int E>
+static hipError_t launch_pq_e(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
+{
+#ifdef WVG_TOOLS
+    if (tuning().pq_variant != 0) return launch_pq_e_variant<E>(a, partials, groups, s);
+#endif
+    dim3 grid(groups, a.nq), block(PQ_SCAN_WAVES * 64);
+    const size_t lds = (size_t)a.pq_m * a.pq_ks * 4;
+    const bool m32 = a.pq_ks == 256 && a.pq_m == 32 && a.nchunks == 2;
+    if (m32 && a.dense && a.cosched && groups % 8 == 0 &&
+        (launch_pq_wide<E, 16, 4, 16, 1, false, true>(a, partials, groups, s) ||
+         launch_pq_wide<E, 8, 4, 16, 1, false, true>(a, partials, groups, s)))
+        return hipGetLastError();
+    if (m32 && a.dense && launch_pq_wide<E, 8, 4, 16, 1>(a, partials, groups, s)) return hipGetLastError();
+    if (m32) {
+        launch_timed((scan_pq32_rot_kernel<E, 6, false, 16>), grid, block, 4 * lds, s, a, partials);
         return hipGetLastError();
     }
     if (a.pq_ks == 256) {

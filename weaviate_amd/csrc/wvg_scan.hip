@@ -19,11 +19,19 @@ namespace wvg {
 
 constexpr int SCAN_WAVES = 4;
 
+#ifdef WVG_TOOLS
 Tuning &tuning()
 {
     static Tuning t;
     return t;
 }
+#else
+const Tuning &tuning()
+{
+    static const Tuning t;
+    return t;
+}
+#endif
 
 LaunchEvents &armed_events()
 {
@@ -300,6 +308,9 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_stream_kernel(ScanAr
     }
 }
 
+#ifdef WVG_TOOLS
+// Tools-build A/B variants of K1 (tuning key 0; profiles/r01/scan_ab_*.jsonl):
+// none beat scan_f32_kernel, so the product library does not carry them.
 // Variant 1: block-granular software pipeline.  The wave's tile range is a
 // flat sequence of 32-float blocks (8 chunks = 8 KiB per wave); the loads of
 // the next two blocks are in flight while a block is folded, across tile
@@ -414,6 +425,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_plain_kernel(ScanArg
     }
     group_combine_store<E, SCAN_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
 }
+#endif  // WVG_TOOLS
 
 // Grid: `groups_per_cu` resident workgroups of 4 waves per CU (3 at the d=128
 // kernel's 167 VGPRs), each wave owning a contiguous tile range of at least 2
@@ -443,6 +455,7 @@ int scan_groups_for(const ScanArgs &a, int num_cus)
 template <int METRIC, int D, int E>
 static void launch_fixed(const ScanArgs &a, uint64_t *partials, dim3 grid, dim3 block, hipStream_t s)
 {
+#ifdef WVG_TOOLS
     // variants 1-3: AVX2 order only, and L2 / dot (their chain sets)
     const int v = a.side.active || a.order512 || is_abs_or_neq<METRIC> ? 0 : tuning().scan_variant;
     if constexpr (!is_abs_or_neq<METRIC>) {
@@ -451,6 +464,7 @@ static void launch_fixed(const ScanArgs &a, uint64_t *partials, dim3 grid, dim3 
         if (v == 2) return launch_timed((scan_f32_plain_kernel<METRIC, D, E>), grid, block, 0, s, a, partials);
         if (v == 3) return launch_timed((scan_f32_sweep_kernel<METRIC, D, E>), grid, block, 0, s, a, partials);
     }
+#endif
     launch_timed((scan_f32_kernel<METRIC, D, E>), grid, block, 0, s, a, partials);
 }
 
@@ -908,6 +922,34 @@ hipError_t launch_rescore_keys(int metric, const float *q, uint32_t qpitch, cons
                            reinterpret_cast<const float4 *>(q), qpitch, reinterpret_cast<const float4 *>(tiled), dim,
                            nchunks, cand_keys, ncand, cand_stride, out_keys, o512);
     });
+    return hipGetLastError();
+}
+
+// Streaming-read probe behind wvg_measure_hbm_read: the HBM read ceiling the
+// scans are judged against, measured in-process (tools/hbm_read.hip's best
+// form: grid-stride 16-byte non-temporal loads, 8 in flight per lane).
+__global__ __launch_bounds__(256) void hbm_read_kernel(const float4 *__restrict__ p, uint64_t n4, float *out)
+{
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const f4v *q = reinterpret_cast<const f4v *>(p);
+    float acc = 0.f;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 7 * stride < n4; i += 8 * stride) {
+        f4v v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = __builtin_nontemporal_load(q + i + u * stride);
+#pragma unroll
+        for (int u = 0; u < 8; u++) acc += v[u].x + v[u].y + v[u].z + v[u].w;
+    }
+    for (; i < n4; i += stride) acc += q[i].x;
+    if (acc == 12345.678f) out[0] = acc;  // keeps the loads live; never true for the zero-filled buffer
+}
+
+hipError_t launch_hbm_read(const void *p, uint64_t bytes, int blocks, float *out, hipStream_t s)
+{
+    hipLaunchKernelGGL(hbm_read_kernel, dim3(blocks), dim3(256), 0, s, reinterpret_cast<const float4 *>(p), bytes / 16,
+                       out);
     return hipGetLastError();
 }
 

@@ -22,14 +22,23 @@ def device_count() -> int:
 
 
 class Context:
-    """wvg_open / wvg_close."""
+    """wvg_open_ex / wvg_close.  Keyword options set the fields of
+    wvg_options (mfma_min_queries, cache_reuse, merge_wait_us, batch_screen);
+    the others keep wvg_options_default's values."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, **options):
         self.lib = _lib.load()
+        opts = _lib.Options()
+        self.lib.wvg_options_default(byref(opts))
+        for name, value in options.items():
+            if name == "size" or name not in dict(_lib.Options._fields_):
+                raise TypeError(f"unknown context option {name!r}")
+            setattr(opts, name, int(value))
         h = c_void_p()
-        check(self.lib.wvg_open(device, byref(h)))
+        check(self.lib.wvg_open_ex(device, byref(opts), byref(h)))
         self.handle = h
         self.device = device
+        self.options = {name: getattr(opts, name) for name, _ in _lib.Options._fields_ if name != "size"}
 
     def close(self) -> None:
         if self.handle:

@@ -105,10 +105,22 @@ def compress_slab(pq_corpus, f32_corpus, centers, src: int = 0, group=None, devi
 
 @dataclass
 class _Buffers:
-    ws: torch.Tensor      # search workspace (zero-filled once)
+    ws: torch.Tensor      # search workspace (zero-filled when allocated)
     send: torch.Tensor    # this rank's packed block
     recv: torch.Tensor    # [world] packed blocks
     counts: torch.Tensor  # local counts
+
+
+def _stream_obj(stream, dev):
+    """(torch stream object, raw hipStream_t) of the caller's stream: torch's
+    current stream when `stream` is None, else the raw handle wrapped so torch
+    ops (the all-gather, its staging copies, allocations) can run on it."""
+    if stream is None:
+        s = torch.cuda.current_stream(dev)
+        return s, s.cuda_stream
+    if isinstance(stream, torch.cuda.Stream):
+        return stream, stream.cuda_stream
+    return torch.cuda.ExternalStream(int(stream), device=dev), int(stream)
 
 
 class ShardedFlatIndex:
@@ -120,46 +132,58 @@ class ShardedFlatIndex:
         self._bufs: dict = {}
 
     def _buffers(self, nq: int, k: int, dev, world: int) -> _Buffers:
+        # The workspace size depends on the corpus's current state (its tile
+        # count, how many rows are live), so it is asked for on every call --
+        # a host-only computation -- and the cached workspace grows when a
+        # grown (or thinned) slab needs more.
+        ws_bytes = max(256, self.lib.wvg_search_workspace_size(self.corpus.handle, nq, k))
         key = (nq, k, str(dev), world)
         b = self._bufs.get(key)
         if b is None:
-            ws_bytes = max(256, self.lib.wvg_search_workspace_size(self.corpus.handle, nq, k))
             blk = self.lib.wvg_topk_packed_bytes(nq, k)
             b = _Buffers(ws=torch.zeros(ws_bytes, dtype=torch.uint8, device=dev),
                          send=torch.empty(blk, dtype=torch.uint8, device=dev),
                          recv=torch.empty(world * blk, dtype=torch.uint8, device=dev),
                          counts=torch.empty(nq, dtype=torch.int32, device=dev))
             self._bufs[key] = b
+        elif b.ws.numel() < ws_bytes:
+            b.ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=dev)
         return b
 
     def search_device(self, q: torch.Tensor, k: int, stream=None, pipelined: bool = False):
         """q: [nq][dim] float32 on this rank's GPU (normalized for cosine).
         Returns (ids int64 [nq][k] global docIDs, dists [nq][k], counts [nq]).
-        pipelined: nq independent single-query scans in one launch
-        (wvg_search_device_pipelined) instead of one batched search."""
+        stream: the stream every step runs on (a torch.cuda.Stream or a raw
+        hipStream_t; None = torch's current stream): the scan, the all-gather
+        (and, over gloo, its host staging copies), the merge and the result
+        allocations are all ordered on it, so a caller's side stream needs no
+        extra synchronisation.  pipelined: nq independent single-query scans
+        in one launch (wvg_search_device_pipelined) instead of one batched
+        search."""
         nq = q.shape[0]
         dev = q.device
-        stream = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+        s_obj, s_raw = _stream_obj(stream, dev)
         world = dist.get_world_size(self.group) if dist.is_initialized() else 1
-        b = self._buffers(nq, k, dev, world)
         fn = self.lib.wvg_search_device_pipelined if pipelined else self.lib.wvg_search_device
-        if world == 1:
-            ids = torch.empty((nq, k), dtype=torch.int64, device=dev)
-            dists = torch.empty((nq, k), dtype=torch.float32, device=dev)
-            counts = torch.empty(nq, dtype=torch.int32, device=dev)
-            check(fn(self.corpus.handle, q.data_ptr(), nq, k, ids.data_ptr(), dists.data_ptr(), counts.data_ptr(),
-                     b.ws.data_ptr(), b.ws.numel(), stream))
-            return ids, dists, counts
-        # local lists straight into the packed block: ids at byte 0, dists at nq*k*8
-        check(fn(self.corpus.handle, q.data_ptr(), nq, k, b.send.data_ptr(), b.send.data_ptr() + nq * k * 8,
-                 b.counts.data_ptr(), b.ws.data_ptr(), b.ws.numel(), stream))
-        all_gather_packed(b.send, b.recv, self.group)
-        m_ids = torch.empty((nq, k), dtype=torch.int64, device=dev)
-        m_d = torch.empty((nq, k), dtype=torch.float32, device=dev)
-        m_c = torch.empty(nq, dtype=torch.int32, device=dev)
-        check(self.lib.wvg_topk_merge_packed(self.ctx.handle, b.recv.data_ptr(), nq, world, k, k, m_ids.data_ptr(),
-                                             m_d.data_ptr(), m_c.data_ptr(), stream))
-        return m_ids, m_d, m_c
+        with torch.cuda.stream(s_obj):
+            b = self._buffers(nq, k, dev, world)
+            if world == 1:
+                ids = torch.empty((nq, k), dtype=torch.int64, device=dev)
+                dists = torch.empty((nq, k), dtype=torch.float32, device=dev)
+                counts = torch.empty(nq, dtype=torch.int32, device=dev)
+                check(fn(self.corpus.handle, q.data_ptr(), nq, k, ids.data_ptr(), dists.data_ptr(),
+                         counts.data_ptr(), b.ws.data_ptr(), b.ws.numel(), s_raw))
+                return ids, dists, counts
+            # local lists straight into the packed block: ids at byte 0, dists at nq*k*8
+            check(fn(self.corpus.handle, q.data_ptr(), nq, k, b.send.data_ptr(), b.send.data_ptr() + nq * k * 8,
+                     b.counts.data_ptr(), b.ws.data_ptr(), b.ws.numel(), s_raw))
+            all_gather_packed(b.send, b.recv, self.group)  # ordered after the scan on s_obj
+            m_ids = torch.empty((nq, k), dtype=torch.int64, device=dev)
+            m_d = torch.empty((nq, k), dtype=torch.float32, device=dev)
+            m_c = torch.empty(nq, dtype=torch.int32, device=dev)
+            check(self.lib.wvg_topk_merge_packed(self.ctx.handle, b.recv.data_ptr(), nq, world, k, k,
+                                                 m_ids.data_ptr(), m_d.data_ptr(), m_c.data_ptr(), s_raw))
+            return m_ids, m_d, m_c
 
     def check(self, stream=None) -> None:
         """wvg_search_device_check over every workspace this index used."""
