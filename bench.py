@@ -57,6 +57,8 @@ def parse(argv=None):
     ap.add_argument("--dim", type=int, default=128)
     ap.add_argument("--k", type=int, default=0, help="neighbours (default 10; slab1b 100)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target wall time of each multi-core CPU leg")
+    ap.add_argument("--no-reuse-rows", type=int, default=4_000_000,
+                    help="rows of the untimed no-reuse leg (frac_no_reuse); 8x the Infinity Cache at d = 128")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dry-run", action="store_true", help="CPU-only rehearsal of the N-rank launch + exchange")
     ap.add_argument("--share-gpu", action="store_true",
@@ -220,10 +222,12 @@ def stored_traffic(n, d, B):
 def no_reuse_leg(args, dev, torch, n, d, k, B, tq, P, launches):
     """The headline kernel with nothing reused between scans: a context with
     wvg_options.cache_reuse = 0 (every scan walks upwards, every row load
-    non-temporal) over a fresh copy of the same rows, same launch shape (B
-    query scans per launch).  Returns the average launch time (s) from HIP
-    events bound to each dispatch, and the context's HBM read ceiling
-    (wvg_measure_hbm_read over 2 GiB: 8x the Infinity Cache)."""
+    non-temporal) over n synthetic rows of the same shape -- n = 4M by default
+    (2 GB, 8x the 256 MiB Infinity Cache; at 1M rows = 512 MB, about twice
+    the cache, part of a streaming scan's rows may still be served on-die) -- same
+    launch shape (B query scans per launch).  Returns the average launch time
+    (s) from HIP events bound to each dispatch, and the context's HBM read
+    ceiling (wvg_measure_hbm_read over 2 GiB)."""
     import ctypes
 
     from weaviate_amd._lib import KIND_F32, METRIC_L2, check
@@ -330,8 +334,9 @@ def run_flat1m(args, world, rank, dev, torch, dist):
     achieved = bytes_per_launch / avg_launch_s / 1e9
     traffic, traffic_src = stored_traffic(n, d, B)  # per launch, like `achieved`
     # untimed: the same kernel with no reuse between scans, and the HBM read ceiling
-    nr_launch_s, ceiling = no_reuse_leg(args, dev, torch, n, d, k, B, tq, P, max(5, min(args.steps, 20)))
-    achieved_nr = bytes_per_launch / nr_launch_s / 1e9
+    nr_rows = max(n, args.no_reuse_rows)
+    nr_launch_s, ceiling = no_reuse_leg(args, dev, torch, nr_rows, d, k, B, tq, P, max(4, min(args.steps, 10)))
+    achieved_nr = nr_rows * d * 4 * B / nr_launch_s / 1e9
     out = {
         "metric": METRIC,
         "value": round(total_queries / elapsed, 3),
@@ -370,6 +375,7 @@ def run_flat1m(args, world, rank, dev, torch, dist):
             "achieved_no_reuse": round(achieved_nr, 1),
             "frac_no_reuse": round(achieved_nr / HBM_PEAK_GBS, 4),
             "avg_launch_us_no_reuse": round(nr_launch_s * 1e6, 2),
+            "rows_no_reuse": nr_rows,
             "ceiling_GBps": round(ceiling, 1),
             "frac_of_ceiling_no_reuse": round(achieved_nr / ceiling, 4) if ceiling > 0 else None,
             "note": ("`achieved` = ALGORITHMIC bytes (N*d*4 per query scan, every query a full scan) / the "
@@ -378,8 +384,8 @@ def run_flat1m(args, world, rank, dev, torch, dist):
                      "(k1_cache_tail), so each scan starts on rows the previous one left in the 256 MiB "
                      "Infinity Cache -- it is not a DRAM rate and can exceed the DRAM read ceiling.  "
                      "`achieved_no_reuse` / `frac_no_reuse`: the same kernel and launch shape in a context with "
-                     "wvg_options.cache_reuse = 0 (one direction, all loads non-temporal) over a fresh copy of "
-                     "the rows, measured in this run.  `ceiling_GBps`: wvg_measure_hbm_read (2 GiB non-temporal "
+                     "wvg_options.cache_reuse = 0 (one direction, all loads non-temporal) over rows_no_reuse rows "
+                     "(8x the Infinity Cache), measured in this run.  `ceiling_GBps`: wvg_measure_hbm_read (2 GiB non-temporal "
                      "streaming read) in this run.  `traffic`: see traffic_source"),
         },
         "cpu_baseline": None,
