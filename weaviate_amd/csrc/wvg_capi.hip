@@ -229,6 +229,31 @@ static bool allow_tile_range(const wvg_corpus *c, const uint64_t *allow, uint64_
     return true;
 }
 
+// Rows of tiles [t0, t1) were (re)written: the shadow rebuilds them at the
+// next screened search.  Callers hold the corpus lock exclusively.
+static void shadow_mark(wvg_corpus *c, uint64_t t0, uint64_t t1)
+{
+    if (!c->d_shadow || t1 <= t0) return;
+    if (c->sh_dirty_lo >= c->sh_dirty_hi) {
+        c->sh_dirty_lo = t0;
+        c->sh_dirty_hi = t1;
+    } else {
+        c->sh_dirty_lo = std::min(c->sh_dirty_lo, t0);
+        c->sh_dirty_hi = std::max(c->sh_dirty_hi, t1);
+    }
+}
+
+static void shadow_free(wvg_corpus *c)
+{
+    if (c->d_shadow) (void)hipFree(c->d_shadow);
+    if (c->d_norms) (void)hipFree(c->d_norms);
+    if (c->d_nmax) (void)hipFree(c->d_nmax);
+    c->d_shadow = nullptr;
+    c->d_norms = nullptr;
+    c->d_nmax = nullptr;
+    c->sh_dirty_lo = c->sh_dirty_hi = 0;
+}
+
 static int check_corpus(wvg_corpus *c)
 {
     if (!c || !c->ctx) return fail(WVG_ERR_INVALID, "null corpus");
@@ -489,6 +514,7 @@ static int corpus_alloc(wvg_corpus *c, uint64_t capacity)
     c->d_data = data;
     c->d_valid = valid;
     c->capacity = tiles * 64;
+    shadow_free(c);  // sized by the capacity: rebuilt at the next screened search
     c->h_valid.resize(tiles, 0ull);
     return WVG_OK;
 }
@@ -527,6 +553,8 @@ int wvg_corpus_destroy(wvg_corpus *c)
     if (c->d_data) (void)hipFree(c->d_data);
     if (c->d_valid) (void)hipFree(c->d_valid);
     if (c->d_centers) (void)hipFree(c->d_centers);
+    shadow_free(c);
+    if (c->sh_ready) (void)hipEventDestroy(c->sh_ready);
     delete c;
     return WVG_OK;
 }
@@ -668,6 +696,7 @@ int wvg_corpus_upsert(wvg_corpus *c, const uint64_t *ids, const float *vectors, 
     SlotGuard g(c->ctx);
     rc = c->ctx->acquire(&g.slot);
     if (rc) return rc;
+    if (!slots.empty()) shadow_mark(c, slots.front() >> 6, (slots.back() >> 6) + 1);  // slots ascend
     for (uint64_t r0 = 0; r0 < rows.size(); r0 += UPSERT_BATCH) {
         const uint64_t r1 = std::min<uint64_t>(rows.size(), r0 + UPSERT_BATCH);
         rc = store_rows(c, g.slot, vectors, rows, slots, r0, r1);
@@ -723,6 +752,7 @@ int wvg_corpus_upsert_codes(wvg_corpus *c, const uint64_t *ids, const void *code
                                 (uint8_t *)c->d_data, s));
     WVG_HIP(launch_set_valid(c->d_valid, (uint64_t *)(b + o_slots), nr, 1, s));
     WVG_HIP(hipStreamSynchronize(s));
+    if (!slots.empty()) shadow_mark(c, slots.front() >> 6, (slots.back() >> 6) + 1);
     mark_valid_host(c, slots);
     return WVG_OK;
 }
@@ -873,6 +903,7 @@ int wvg_corpus_fill_synthetic(wvg_corpus *c, uint64_t seed, uint64_t n, int dist
         hv[t] |= word;
     }
     c->high_water = std::max(c->high_water, n);
+    shadow_mark(c, 0, tiles_of(n));
     WVG_HIP(hipMemcpyAsync(c->d_valid, hv.data(), tiles_of(n) * 8, hipMemcpyHostToDevice, s));
     WVG_HIP(hipStreamSynchronize(s));
     return WVG_OK;
@@ -1034,10 +1065,40 @@ static uint32_t k1_cache_tail(const wvg_corpus *c, uint64_t tb, uint64_t te)
     return (uint32_t)std::max<uint64_t>(1, (256ull * K1_CACHE_BYTES) / bytes);
 }
 
+// Workspace of a K3c screen (wvg_screen.hip): range lists, candidates,
+// rescored keys, per-query bounds, query fragments and constants, the
+// flagged-query list and the rescan's partial lists.
+struct ScreenWs {
+    size_t part = 0, cand = 0, keys = 0, gb = 0, qf = 0, k1 = 0, k2 = 0, em = 0, fl = 0, nf = 0, fbp = 0, total = 0;
+};
+static ScreenWs screen_ws(uint32_t nq, uint32_t k, uint32_t nrr, uint32_t kbn, uint32_t fb_groups)
+{
+    ScreenWs w;
+    Carver cv;
+    const size_t nq_pad = (size_t)(nq + 127) / 128 * 128, ncand = (size_t)nrr * SCREEN_M;
+    w.part = cv.take(nq * ncand * 8);
+    w.cand = cv.take(nq * ncand * 8);
+    w.keys = cv.take(nq * ncand * 8);
+    w.gb = cv.take((size_t)nq * 4);
+    w.qf = cv.take(nq_pad / 16 * kbn * 1024);
+    w.k1 = cv.take(nq_pad * 4);
+    w.k2 = cv.take(nq_pad * 4);
+    w.em = cv.take(nq_pad * 4);
+    w.fl = cv.take((size_t)nq * 4);
+    w.nf = cv.take(4);
+    w.fbp = cv.take((size_t)nq * fb_groups * k * 8);
+    w.total = cv.off;
+    return w;
+}
+
 struct SearchPlan {
     uint64_t tb = 0, te = 0;
-    int groups = 1;      // scan: workgroups per query; gemm: row ranges
+    int groups = 1;      // scan: workgroups per query; gemm: row ranges (screen: K3c row ranges)
     bool gemm = false;   // K3 batched MFMA path
+    bool screen = false; // gemm via the K3c bf16 screen + exact rescore
+    int exact_groups = 1;   // screen: K3b's row ranges, if the shadow cannot be built
+    uint32_t fb_groups = 0; // screen: K1 workgroups per flagged query's rescan
+    uint32_t kbn = 0;       // screen: 32-element K blocks
     bool cosched = false; // PQ batch: co-scheduled K8e (ScanArgs::cosched)
     bool empty = false;
     const uint64_t *allow_host = nullptr;  // the caller's allow words of tiles [tb, te), or null
@@ -1045,9 +1106,14 @@ struct SearchPlan {
     size_t partial_keys(uint32_t nq, uint32_t k) const { return (size_t)nq * groups * k; }
     // K3b's per-row-range progress counters, then its per-query distance
     // bounds, follow the partial lists (gemm only)
+    static size_t gemm_bytes(uint32_t nq, uint32_t k, int groups, bool gemm)
+    {
+        return (size_t)nq * groups * k * 8 + (gemm ? (size_t)groups * ((nq + 15) / 16) * 4 + (size_t)nq * 4 + 256 : 0);
+    }
     size_t workspace_bytes(uint32_t nq, uint32_t k) const
     {
-        return partial_keys(nq, k) * 8 + (gemm ? (size_t)groups * ((nq + 15) / 16) * 4 + (size_t)nq * 4 + 256 : 0);
+        if (screen) return std::max(screen_ws(nq, k, (uint32_t)groups, kbn, fb_groups).total, gemm_bytes(nq, k, exact_groups, true));
+        return gemm_bytes(nq, k, groups, gemm);
     }
 };
 
@@ -1069,6 +1135,17 @@ static SearchPlan plan_search(wvg_corpus *c, uint32_t nq, uint32_t k, const uint
         p.groups = (int)gemm_row_ranges(nq, std::max<uint64_t>(1, p.te - p.tb), c->ctx->num_cus, c->dim, k);
     else
         p.groups = scan_groups_for(a, c->ctx->num_cus);
+    // bf16 screen + exact rescore for the batches it applies to (results identical to K3b)
+    if (p.gemm && c->ctx->opt.batch_screen && screen_supported(c->dim, c->metric, k) && c->dim % 4 == 0 &&
+        !c->sh_failed) {
+        p.screen = true;
+        p.exact_groups = p.groups;
+        p.groups = (int)screen_row_ranges(nq, std::max<uint64_t>(1, p.te - p.tb), c->ctx->num_cus);
+        ScanArgs a1 = a;
+        a1.nq = 1;
+        p.fb_groups = (uint32_t)std::min(scan_groups_for(a1, c->ctx->num_cus), c->ctx->num_cus);
+        p.kbn = screen_kblocks(c->dim);
+    }
     // PQ batches: the nq queries of one row range run side by side on one XCD and share its L2
     const bool pq_cos = c->kind == WVG_KIND_PQ && c->pq_m == 32 && c->pq_ks == 256 && pq_dense(c, nullptr) &&
                         (tuning().pq_variant == 0 || tuning().pq_variant == 48 || tuning().pq_variant == 49);
@@ -1077,6 +1154,96 @@ static SearchPlan plan_search(wvg_corpus *c, uint32_t nq, uint32_t k, const uint
     if (p.cosched)  // BQ: K5 workgroups are 4 waves, so bq_cos_gpc of them per CU
         p.groups = pq_cosched_groups(nq, c->ctx->num_cus * (bq_cos ? std::max(1, tuning().bq_cos_gpc) : 1));
     return p;
+}
+
+// The bf16 shadow (fragments + row norms) of an F32 dot / cosine corpus,
+// allocated on first use and rebuilt over the tiles written since the last
+// build; ordered before the caller's screen on stream s.  False when it
+// cannot be allocated (the batch then runs the exact path).
+static bool ensure_shadow(wvg_corpus *c, hipStream_t s)
+{
+    std::lock_guard<std::mutex> g(c->sh_mu);
+    if (c->sh_failed) return false;
+    const uint64_t tiles = tiles_of(c->capacity);
+    const uint32_t kbn = screen_kblocks(c->dim);
+    if (!c->d_shadow) {
+        const size_t sbytes = (size_t)(tiles + 4) * kbn * 4 * 1024, nbytes = (size_t)(tiles + 4) * 64 * 4;
+        void *sh = nullptr, *nr = nullptr, *mx = nullptr;
+        if (hipMalloc(&sh, sbytes) != hipSuccess || hipMalloc(&nr, nbytes) != hipSuccess ||
+            hipMalloc(&mx, 256) != hipSuccess || hipMemsetAsync(sh, 0, sbytes, s) != hipSuccess ||
+            hipMemsetAsync(nr, 0, nbytes, s) != hipSuccess || hipMemsetAsync(mx, 0, 256, s) != hipSuccess ||
+            (!c->sh_ready && hipEventCreateWithFlags(&c->sh_ready, hipEventDisableTiming) != hipSuccess)) {
+            (void)hipGetLastError();
+            (void)hipStreamSynchronize(s);
+            if (sh) (void)hipFree(sh);
+            if (nr) (void)hipFree(nr);
+            if (mx) (void)hipFree(mx);
+            c->sh_failed = true;
+            return false;
+        }
+        c->d_shadow = sh;
+        c->d_norms = (float *)nr;
+        c->d_nmax = (uint32_t *)mx;
+        c->sh_dirty_lo = 0;
+        c->sh_dirty_hi = tiles_of(c->high_water);
+    }
+    if (c->sh_dirty_lo < c->sh_dirty_hi) {
+        if (launch_shadow_build((const float *)c->d_data, c->dim, c->sh_dirty_lo, c->sh_dirty_hi, c->d_shadow,
+                                c->d_norms, c->d_nmax, s) != hipSuccess ||
+            hipEventRecord(c->sh_ready, s) != hipSuccess)
+            return false;
+        c->sh_dirty_lo = c->sh_dirty_hi = 0;
+        return true;
+    }
+    return hipStreamWaitEvent(s, c->sh_ready, 0) == hipSuccess;
+}
+
+// K3c: screen, exact rescore of the candidates, top-k; the flagged queries
+// (a range list overflowed below tau) are rescanned exactly with K1.
+static int run_screen(wvg_corpus *c, const ScanArgs &a, const SearchPlan &p, char *ws, uint64_t *ids, float *dists,
+                      uint32_t *counts, hipStream_t s)
+{
+    const uint32_t nq = a.nq, k = a.k, nrr = (uint32_t)p.groups, ncand = nrr * SCREEN_M;
+    const ScreenWs w = screen_ws(nq, k, nrr, p.kbn, p.fb_groups);
+    ScreenLaunch L{};
+    L.shadow = c->d_shadow;
+    L.norms = c->d_norms;
+    L.nmax = c->d_nmax;
+    L.valid = a.valid;
+    L.allow = a.allow;
+    L.allow_words = a.allow_words;
+    L.allow_t0 = a.allow_t0;
+    L.tile_begin = a.tile_begin;
+    L.tile_end = a.tile_end;
+    L.dim = c->dim;
+    L.queries = (const float *)a.queries;
+    L.qpitch = a.qpitch;
+    L.nq = nq;
+    L.k = k;
+    L.nrr = nrr;
+    L.cosine = c->metric == WVG_METRIC_COSINE;
+    L.qfrag = ws + w.qf;
+    L.k1 = (float *)(ws + w.k1);
+    L.k2 = (float *)(ws + w.k2);
+    L.emax = (float *)(ws + w.em);
+    L.gbound = (uint32_t *)(ws + w.gb);
+    L.partials = (uint64_t *)(ws + w.part);
+    L.cand = (uint64_t *)(ws + w.cand);
+    L.flist = (uint32_t *)(ws + w.fl);
+    L.nflag = (uint32_t *)(ws + w.nf);
+    WVG_HIP(launch_screen(L, s));
+    uint64_t *keys = (uint64_t *)(ws + w.keys);
+    WVG_HIP(launch_rescore_keys(c->metric, (const float *)a.queries, a.qpitch, (const float *)c->d_data, c->dim,
+                                c->nchunks, L.cand, nq, ncand, ncand, keys, s, 0));
+    WVG_HIP(launch_merge_keys(keys, nq, ncand, k, c->id_base, ids, dists, counts, s));
+    ScanArgs f = a;
+    f.nq = 1;
+    f.cosched = 0;
+    f.reverse = 0;
+    uint64_t *fbp = (uint64_t *)(ws + w.fbp);
+    WVG_HIP(launch_scan_f32_qlist(f, fbp, (int)p.fb_groups, L.flist, L.nflag, std::min<uint32_t>(nq, 8), s));
+    WVG_HIP(launch_merge_lists_qlist(fbp, nq, p.fb_groups, k, k, c->id_base, ids, dists, counts, L.flist, L.nflag, s));
+    return WVG_OK;
 }
 
 // Runs phase 1 + phase 2 for one corpus with device-resident prepared queries.
@@ -1108,6 +1275,17 @@ static int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t 
     a.plain = plain_loads(c, p.tb, p.te);
     a.cache_tail256 = k1_cache_tail(c, p.tb, p.te);
     if (!p.gemm) a.reverse = next_direction(c, 1);
+    if (p.screen) {
+        if (ensure_shadow(c, s)) {
+            ProfArm arm(c->ctx);
+            if (arm.rc) return arm.rc;
+            return run_screen(c, a, p, reinterpret_cast<char *>(partials), ids, dists, counts, s);
+        }
+        SearchPlan pe = p;  // no shadow: the exact MFMA path over the same workspace
+        pe.screen = false;
+        pe.groups = p.exact_groups;
+        return run_search(c, d_q, qpitch, nq, k, d_allow, pe, partials, ids, dists, counts, s);
+    }
     ProfArm arm(c->ctx);
     if (arm.rc) return arm.rc;
     if (p.gemm) {

@@ -74,6 +74,15 @@ struct wvg_corpus {
     float *d_centers = nullptr;    // [m][ks][ds]
     uint32_t pq_m = 0, pq_ks = 0, pq_ds = 0;
     bool pq_nan_free = false;      // the codebook has no NaN (launch_pq_encode)
+    // K3c's bf16 shadow of an F32 dot / cosine corpus (wvg_screen.hip), built on
+    // the first batched search that uses it and kept in step with later writes
+    void *d_shadow = nullptr;      // [tiles + 4][screen_kblocks][4][64] 16-B bf16 fragments
+    float *d_norms = nullptr;      // [(tiles + 4) * 64] row-norm upper bounds
+    uint32_t *d_nmax = nullptr;    // max of d_norms (float bits)
+    uint64_t sh_dirty_lo = 0, sh_dirty_hi = 0;  // tiles written since the last build
+    bool sh_failed = false;        // the shadow could not be allocated: batches stay on the exact path
+    std::mutex sh_mu;              // builds (searches hold rw shared)
+    hipEvent_t sh_ready = nullptr; // the last build, for searches on other streams
     std::shared_mutex rw;          // shared: search; exclusive: upsert/delete/grow
     std::atomic<uint64_t> scan_serial{0};  // query scans issued so far (parity = next scan direction)
 };
@@ -249,6 +258,42 @@ hipError_t launch_scan_f32_stream(const ScanArgs &a, const StreamJob &j, hipStre
 hipError_t launch_fill_empty(uint64_t *ids, float *dists, uint32_t *counts, uint32_t nq, uint32_t k, hipStream_t s);
 hipError_t launch_scan_bq(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s);
 hipError_t launch_scan_pq(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s);
+// The exact K1 rescan of a device-resident query list (qlist[0 .. *nlist)),
+// `slots` queries in flight: partials [f][groups][k]; and its merge.
+hipError_t launch_scan_f32_qlist(const ScanArgs &a, uint64_t *partials, int groups, const uint32_t *qlist,
+                                 const uint32_t *nlist, uint32_t slots, hipStream_t s);
+hipError_t launch_merge_lists_qlist(const uint64_t *partials, uint32_t nq, uint32_t nlists, uint32_t list_len,
+                                    uint32_t k, uint64_t id_base, uint64_t *ids, float *dists, uint32_t *counts,
+                                    const uint32_t *qlist, const uint32_t *nlist, hipStream_t s);
+// K3c bf16 MFMA screen + exact rescore (wvg_screen.hip).
+constexpr int SCREEN_M = 16;  // lower bounds kept per (wave, query) and per (row range, query)
+inline uint32_t screen_kblocks(uint32_t dim) { return (dim + 63) / 64 * 2; }
+bool screen_supported(uint32_t dim, int metric, uint32_t k);
+uint32_t screen_row_ranges(uint32_t nq, uint64_t ntiles, int num_cus);
+hipError_t launch_shadow_build(const float *tiled, uint32_t dim, uint64_t t0, uint64_t t1, void *shadow, float *norms,
+                               uint32_t *nmax, hipStream_t s);
+struct ScreenLaunch {
+    const void *shadow;
+    const float *norms;
+    const uint32_t *nmax;
+    const uint64_t *valid;
+    const uint64_t *allow;
+    uint64_t allow_words, allow_t0;
+    uint64_t tile_begin, tile_end;
+    uint32_t dim;
+    const float *queries;  // [nq][qpitch] (normalized for cosine)
+    uint32_t qpitch, nq, k, nrr;
+    int cosine;
+    void *qfrag;           // [nq_pad / 16][kblocks][64] x 16 B
+    float *k1, *k2, *emax; // [nq_pad]
+    uint32_t *gbound;      // [nq]
+    uint64_t *partials;    // [nq][nrr][SCREEN_M]
+    uint64_t *cand;        // [nq][nrr * SCREEN_M]
+    uint32_t *flist;       // [nq] flagged queries
+    uint32_t *nflag;       // count
+};
+// screen + collect (the rescore, merge and rescan are launched by the host)
+hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s);
 // K3 batched MFMA scoring (wvg_gemm.hip): partials [nq][nrr][K].
 bool gemm_supported(uint32_t dim, int metric);
 uint32_t gemm_row_ranges(uint32_t nq, uint64_t ntiles, int num_cus, uint32_t dim, uint32_t k);

@@ -171,6 +171,27 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_kernel(ScanArgs a, u
     group_combine_store<E, SCAN_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
 }
 
+// The exact rescan of a query list (the K3c screen's flagged queries, whose
+// candidate lists overflowed): block (g, f) scans slice g for the listed
+// queries f, f + gridDim.y, ... < *nlist; partials [f][groups][k].
+template <int METRIC, int D, int E>
+__global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_qlist_kernel(ScanArgs a, uint64_t *partials,
+                                                                          const uint32_t *qlist, const uint32_t *nlist)
+{
+    const uint32_t nl = *nlist;
+    uint64_t t0, t1;
+    wave_range(a, SCAN_WAVES, t0, t1);
+    for (uint32_t f = blockIdx.y; f < nl; f += gridDim.y) {
+        const uint32_t qi = qlist[f];
+        const float4 *q4 = reinterpret_cast<const float4 *>(a.queries) + (size_t)qi * (a.qpitch / 4);
+        WaveTopK<E> tk;
+        tk.init((int)a.k);
+        scan_tiles<METRIC, D, E>(a, q4, t0, t1, tk);
+        group_combine_store<E, SCAN_WAVES>(tk, partials + ((size_t)f * gridDim.x + blockIdx.x) * a.k);
+        __syncthreads();  // the combine's LDS is reused by the next listed query
+    }
+}
+
 // Empty results for queries [q0, nq): ids KEY_NONE, dists +inf, counts 0
 // (what the host path's write_empty returns for an empty corpus / slab).
 __device__ __forceinline__ void fill_empty_body(uint64_t *ids, float *dists, uint32_t *counts, uint32_t q0,
@@ -515,6 +536,30 @@ static hipError_t launch_f32_m(const ScanArgs &a, uint64_t *partials, int groups
     return launch_f32_e<METRIC, 4>(a, partials, groups, s);
 }
 
+template <int METRIC, int E>
+static hipError_t launch_qlist_e(const ScanArgs &a, uint64_t *partials, int groups, const uint32_t *qlist,
+                                 const uint32_t *nlist, uint32_t slots, hipStream_t s)
+{
+    dim3 grid(groups, slots), block(SCAN_WAVES * 64);
+    switch (a.dim) {
+    case 128: hipLaunchKernelGGL((scan_f32_qlist_kernel<METRIC, 128, E>), grid, block, 0, s, a, partials, qlist, nlist); break;
+    case 768: hipLaunchKernelGGL((scan_f32_qlist_kernel<METRIC, 768, E>), grid, block, 0, s, a, partials, qlist, nlist); break;
+    default: hipLaunchKernelGGL((scan_f32_qlist_kernel<METRIC, 0, E>), grid, block, 0, s, a, partials, qlist, nlist); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_scan_f32_qlist(const ScanArgs &a, uint64_t *partials, int groups, const uint32_t *qlist,
+                                 const uint32_t *nlist, uint32_t slots, hipStream_t s)
+{
+    return with_metric(a.metric, [&](auto M) -> hipError_t {
+        constexpr int MM = decltype(M)::value;
+        if (a.k <= 64) return launch_qlist_e<MM, 1>(a, partials, groups, qlist, nlist, slots, s);
+        if (a.k <= 128) return launch_qlist_e<MM, 2>(a, partials, groups, qlist, nlist, slots, s);
+        return launch_qlist_e<MM, 4>(a, partials, groups, qlist, nlist, slots, s);
+    });
+}
+
 hipError_t launch_scan_f32(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
 {
     return with_metric(a.metric, [&](auto M) { return launch_f32_m<decltype(M)::value>(a, partials, groups, s); });
@@ -553,6 +598,40 @@ hipError_t launch_merge_lists(const uint64_t *partials, uint32_t nq, uint32_t nl
     else
         hipLaunchKernelGGL((merge_keys_kernel<4>), grid, block, 0, s, partials, nlists, list_len, k, id_base, ids,
                            dists, counts);
+    return hipGetLastError();
+}
+
+// Phase 2 for a query list: block f merges listed query qlist[f]'s lists
+// (partials [f][nlists][list_len]) into that query's outputs.
+template <int E>
+__global__ __launch_bounds__(MERGE_WAVES * 64) void merge_keys_qlist_kernel(const uint64_t *partials, uint32_t nlists,
+                                                                            uint32_t list_len, uint32_t k,
+                                                                            uint64_t id_base, uint64_t *ids,
+                                                                            float *dists, uint32_t *counts,
+                                                                            const uint32_t *qlist,
+                                                                            const uint32_t *nlist)
+{
+    const uint32_t f = blockIdx.x;
+    if (f >= *nlist) return;
+    const uint32_t qi = qlist[f];
+    merge_lists_body<E, MERGE_WAVES>(partials + (size_t)f * nlists * list_len, nlists, list_len, k, id_base,
+                                     ids + (size_t)qi * k, dists + (size_t)qi * k, counts ? counts + qi : nullptr);
+}
+
+hipError_t launch_merge_lists_qlist(const uint64_t *partials, uint32_t nq, uint32_t nlists, uint32_t list_len,
+                                    uint32_t k, uint64_t id_base, uint64_t *ids, float *dists, uint32_t *counts,
+                                    const uint32_t *qlist, const uint32_t *nlist, hipStream_t s)
+{
+    dim3 grid(nq), block(MERGE_WAVES * 64);
+    if (k <= 64)
+        hipLaunchKernelGGL((merge_keys_qlist_kernel<1>), grid, block, 0, s, partials, nlists, list_len, k, id_base, ids,
+                           dists, counts, qlist, nlist);
+    else if (k <= 128)
+        hipLaunchKernelGGL((merge_keys_qlist_kernel<2>), grid, block, 0, s, partials, nlists, list_len, k, id_base, ids,
+                           dists, counts, qlist, nlist);
+    else
+        hipLaunchKernelGGL((merge_keys_qlist_kernel<4>), grid, block, 0, s, partials, nlists, list_len, k, id_base, ids,
+                           dists, counts, qlist, nlist);
     return hipGetLastError();
 }
 

@@ -1,0 +1,600 @@
+// wvg_screen.hip -- K3c: batched dot / cosine scoring as a bf16 MFMA screen
+// with a rigorous per-(query, row) error bound, followed by the exact fp32
+// rescore of every row the bound cannot rule out.  Results are bit-identical
+// to the exact path (K3b / K1, the reference's AVX2-order dot_256):
+//
+//   Reference: Q independent flat.searchByVector calls (V/flat/index.go:319)
+//   over the same rows, SingleDist = dot_256 (D/dot_product.go:68-98,
+//   D/c/dot_avx256_amd64.c) or its cosine Wrap (D/cosine_dist.go:38-68).
+//
+// The bound.  r = the exact fp32 dot of (q, x) in the AVX2 order; s = the
+// bf16 MFMA dot of (bf16(q), bf16(x)) (round to nearest: |x - bf16(x)| <=
+// 2^-8 |x|, products exact in fp32, fp32 accumulation).  Then
+//   |r - s| <= (2^-7 + 2^-16 + 3 d 2^-24) sum |q_i x_i| + (denormal terms)
+//           <= c Nq Nx + 2^-120 (Nq + Nx) + 2^-110,
+// Nq, Nx upper bounds of the L2 norms (Cauchy-Schwarz), c = 2^-7 + 2^-15 +
+// d 2^-21 (the extra terms absorb the fp32 roundings of the bound itself).
+// Cosine adds 2^-19 for the 1 - r roundings.  Per element: E = fma(Nx, K1q,
+// K2q), u = s + E >= r, so lower = -u (dot) / 1 - u (cosine) <= the exact
+// distance.  A row can be in the top-k only if lower <= tau, for any tau
+// with k rows at or below it: tau = (k-th smallest lower) + 2 Emax_q, taken
+// per wave from its lists and across workgroups from finished row ranges.
+//
+// K3c.  A workgroup owns 128 queries x one range of 256-row blocks; per
+// 64-deep K stage it stages 16 KiB of query fragments and 32 KiB of row
+// fragments into LDS with global_load_lds (both pre-laid out in HBM in MFMA
+// operand order: 1 KiB = one 16 x 32 bf16 fragment, lane l = item l & 15,
+// k 8 (l >> 4) .. +7), double-buffered, one barrier per stage; 8 waves as
+// 4 (queries) x 2 (rows), each wave a 32 x 128 tile of 16x16x32 bf16 MFMAs.
+// After a row block: u per element, one compare with the query's threshold;
+// the rare survivors enter the wave's per-query list of the SC_M smallest
+// lower bounds (LDS).  A finished range merges its two waves' lists per query
+// into partials and publishes tau (atomicMin); collect keeps the entries with
+// lower <= the final tau -- a superset of the exact top-k and its ties -- and
+// flags a query whose range list was full below tau (rows may have been
+// dropped): it is rescanned exactly (K1).
+// Roofline: bf16 MFMA, 2 Q N d FLOP per batch (2.5 PFLOP/s dense).
+#include "wvg_internal.hpp"
+
+namespace wvg {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int SC_BQ = 128;                 // queries per workgroup
+constexpr int SC_WAVES = 8;                // 4 (query quarters) x 2 (row halves)
+constexpr int SC_AFR = 16;                 // query fragments per stage (8 groups of 16 x 2 K blocks)
+constexpr int SC_BFR = 32;                 // row fragments per stage (16 groups of 16 x 2 K blocks)
+constexpr int SC_STAGE = (SC_AFR + SC_BFR) * 1024;  // bytes per stage buffer
+constexpr int SC_LISTS = SC_WAVES * 32 * SCREEN_M * 8;
+constexpr int SC_LDS = 2 * SC_STAGE + SC_LISTS + SC_WAVES * 32 * 4 * 2 + SC_BQ * 4 * 3;
+
+__device__ __forceinline__ uint64_t sc_sload64(const uint64_t *p)
+{
+    uint64_t v;
+    asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+    return v;
+}
+
+// ---------------------------------------------------------------------------
+// Shadow build: bf16 fragments + row-norm upper bounds of tiles [t0, t1).
+// One thread per (fragment, lane): fragment (t, kb, rg), lane l -> row
+// 16 rg + (l & 15) of tile t, elements 32 kb + 8 (l >> 4) .. + 7.
+__global__ __launch_bounds__(256) void shadow_frag_kernel(const float4 *__restrict__ tiled, uint32_t nchunks,
+                                                          uint32_t kbn, uint64_t t0, uint64_t nfrag, uint4 *shadow)
+{
+    const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= nfrag * 64) return;
+    const uint32_t lane = (uint32_t)(g & 63);
+    const uint64_t f = g >> 6;                 // fragment index relative to tile t0
+    const uint32_t rg = (uint32_t)(f & 3);
+    const uint64_t tk = f >> 2;
+    const uint32_t kb = (uint32_t)(tk % kbn);
+    const uint64_t t = t0 + tk / kbn;
+    const uint32_t row = 16 * rg + (lane & 15);
+    const uint32_t c0 = (32 * kb + 8 * (lane >> 4)) / 4;  // first float4 chunk
+    float v[8];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const uint32_t c = c0 + h;
+        const float4 x = c < nchunks ? tiled[((size_t)t * nchunks + c) * 64 + row] : make_float4(0.f, 0.f, 0.f, 0.f);
+        v[4 * h + 0] = x.x;
+        v[4 * h + 1] = x.y;
+        v[4 * h + 2] = x.z;
+        v[4 * h + 3] = x.w;
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; e++) o[e] = (__bf16)v[e];  // v_cvt_pk_bf16_f32: round to nearest even
+    shadow[((t * kbn + kb) * 4 + rg) * 64 + lane] = *reinterpret_cast<const uint4 *>(&o);
+}
+
+// An upper bound of the L2 norm from the exact square sum in double:
+// rounded up past the float cast; +inf for a non-finite row.
+__device__ __forceinline__ float norm_upper(double ss)
+{
+    if (!(ss < 1e300)) return __builtin_inff();  // inf / NaN components
+    return (float)(__builtin_sqrt(ss) * (1.0 + 1e-6));
+}
+
+__global__ __launch_bounds__(256) void shadow_norm_kernel(const float4 *__restrict__ tiled, uint32_t nchunks,
+                                                          uint64_t slot0, uint64_t n, float *norms, uint32_t *nmax)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    float nv = 0.f;
+    if (i < n) {
+        const uint64_t slot = slot0 + i;
+        const float4 *rp = tiled + (slot >> 6) * nchunks * 64 + (slot & 63);
+        double ss = 0.0;
+        for (uint32_t c = 0; c < nchunks; c++) {
+            const float4 x = rp[(size_t)c * 64];
+            ss += (double)x.x * x.x + (double)x.y * x.y + (double)x.z * x.z + (double)x.w * x.w;
+        }
+        nv = norm_upper(ss);
+        norms[slot] = nv;
+    }
+    // the block's maximum, then one atomic (non-negative floats order as their bits)
+    uint32_t b = __float_as_uint(nv);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) b = max(b, (uint32_t)__shfl_xor((int)b, off));
+    if ((threadIdx.x & 63) == 0) atomicMax(nmax, b);
+}
+
+hipError_t launch_shadow_build(const float *tiled, uint32_t dim, uint64_t t0, uint64_t t1, void *shadow, float *norms,
+                               uint32_t *nmax, hipStream_t s)
+{
+    if (t1 <= t0) return hipSuccess;
+    const uint32_t nch = f32_chunks(dim), kbn = screen_kblocks(dim);
+    const uint64_t nfrag = (t1 - t0) * kbn * 4;
+    hipLaunchKernelGGL(shadow_frag_kernel, dim3((unsigned)((nfrag * 64 + 255) / 256)), dim3(256), 0, s,
+                       reinterpret_cast<const float4 *>(tiled), nch, kbn, t0, nfrag, reinterpret_cast<uint4 *>(shadow));
+    const uint64_t n = (t1 - t0) * 64;
+    hipLaunchKernelGGL(shadow_norm_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                       reinterpret_cast<const float4 *>(tiled), nch, t0 * 64, n, norms, nmax);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Query preparation: fragments [nq16][kbn][64] and the bound constants.
+__global__ __launch_bounds__(256) void screen_qfrag_kernel(const float *q, uint32_t nq, uint32_t qpitch, uint32_t dim,
+                                                           uint32_t kbn, uint32_t nq16, uint4 *qfrag)
+{
+    const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= (uint64_t)nq16 * kbn * 64) return;
+    const uint32_t lane = (uint32_t)(g & 63);
+    const uint32_t kb = (uint32_t)((g >> 6) % kbn);
+    const uint32_t qg = (uint32_t)((g >> 6) / kbn);
+    const uint32_t qi = 16 * qg + (lane & 15);
+    const uint32_t e0 = 32 * kb + 8 * (lane >> 4);
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+        const uint32_t p = e0 + e;
+        o[e] = (__bf16)(qi < nq && p < dim ? q[(size_t)qi * qpitch + p] : 0.0f);
+    }
+    qfrag[g] = *reinterpret_cast<const uint4 *>(&o);
+}
+
+__global__ __launch_bounds__(256) void screen_qconst_kernel(const float *q, uint32_t nq, uint32_t qpitch,
+                                                            uint32_t dim, uint32_t nq_pad, int cosine,
+                                                            const uint32_t *nmax, float *k1, float *k2, float *emax)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t qi = blockIdx.x * 4 + (threadIdx.x >> 6);  // one wave per query
+    if (qi >= nq_pad) return;
+    double ss = 0.0;
+    if (qi < nq)
+        for (uint32_t i = lane; i < dim; i += 64) {
+            const double x = q[(size_t)qi * qpitch + i];
+            ss += x * x;
+        }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off);
+    if (lane) return;
+    const float nq_up = norm_upper(ss);
+    const float c = 0x1p-7f + 0x1p-15f + (float)dim * 0x1p-21f;
+    const float a = cosine ? 0x1p-19f : 0x1p-110f;
+    float K1 = c * nq_up + 0x1p-120f, K2 = 0x1p-120f * nq_up + a;
+    if (qi >= nq) K1 = K2 = 0.f;
+    k1[qi] = K1;
+    k2[qi] = K2;
+    emax[qi] = __builtin_fmaf(__uint_as_float(*nmax), K1, K2);
+}
+
+// ---------------------------------------------------------------------------
+// K3c
+struct ScreenArgs {
+    const uint4 *shadow;      // [tiles][kbn][4][64]
+    const float *norms;       // [slots]
+    const uint64_t *valid;
+    const uint64_t *allow;
+    uint64_t allow_words, allow_t0;
+    uint64_t tile_begin, tile_end;
+    uint32_t kbn;             // 32-element K blocks (even)
+    const uint4 *qfrag;       // [nq16][kbn][64]
+    const float *k1, *k2, *emax;  // [nq_pad]
+    uint32_t nq, k, nqb, nrr;
+    int cosine;
+    uint32_t *gbound;         // [nq] ordered tau; 0xFFFFFFFF = none yet
+    uint64_t *partials;       // [nq][nrr][SCREEN_M]
+};
+
+// lower bound (distance space) of a survivor's u; NaN u (a non-finite row or
+// query) -> -inf: always a candidate, rescored exactly
+__device__ __forceinline__ float sc_lower(float u, int cosine)
+{
+    if (u != u) return -__builtin_inff();
+    return cosine ? 1.0f - u : -u;
+}
+
+// u-space threshold of a distance threshold tau (a superset for cosine)
+__device__ __forceinline__ float sc_sigma(float tau, int cosine)
+{
+    if (!(tau < __builtin_inff())) return -__builtin_inff();
+    return cosine ? (1.0f - tau) - 0x1p-20f : -tau;
+}
+
+// tau from the k-th smallest lower bound of a list: every one of those k rows
+// has its exact distance <= lower + 2 E <= lower_k + 2 Emax.  Not a number
+// (-inf + inf: a non-finite query) means no bound: +inf.
+__device__ __forceinline__ float sc_tau_k(float lower_k, float emax, int cosine)
+{
+    const float t = lower_k + 2.0f * emax * (1.0f + 0x1p-10f) + (cosine ? 0x1p-20f : 0.0f);
+    return t == t ? t : __builtin_inff();
+}
+
+__device__ __forceinline__ float key_lower(uint64_t key) { return wvg_unord_f32((uint32_t)(key >> 32)); }
+
+__global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint64_t *lists = reinterpret_cast<uint64_t *>(smem + 2 * SC_STAGE);  // [8][32][M]
+    float *tau = reinterpret_cast<float *>(smem + 2 * SC_STAGE + SC_LISTS);  // [8][32] distance-space threshold
+    float *sig = tau + SC_WAVES * 32;                                      // [8][32] u-space threshold
+    float *ck1 = sig + SC_WAVES * 32;                                      // [128]
+    float *ck2 = ck1 + SC_BQ;
+    float *cem = ck2 + SC_BQ;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wq = w & 3, wr = w >> 2;
+    const int K = (int)a.k, M = SCREEN_M;
+    const int cosine = a.cosine;
+    // the nqb query blocks of one row range share an XCD (blocks b, b+8, ...)
+    const uint32_t b = blockIdx.x;
+    uint32_t qb, rr;
+    if (a.nrr % 8 == 0) {
+        const uint32_t xcd = b % 8, wv = b / 8;
+        qb = wv % a.nqb;
+        rr = (wv / a.nqb) * 8 + xcd;
+    } else {
+        qb = b % a.nqb;
+        rr = b / a.nqb;
+    }
+    const uint64_t ntiles = a.tile_end - a.tile_begin;
+    const uint64_t nblk = (ntiles + 3) / 4;  // 256-row blocks
+    const uint64_t blk0 = nblk * rr / a.nrr, blk1 = nblk * (rr + 1) / a.nrr;
+    const uint32_t q0 = qb * SC_BQ;
+    const uint32_t NK = a.kbn / 2;  // 64-deep stages per row block
+
+    // per-query constants and thresholds
+    for (int i = tid; i < SC_BQ; i += SC_WAVES * 64) {
+        const uint32_t q = q0 + (uint32_t)i;
+        ck1[i] = a.k1[q];
+        ck2[i] = a.k2[q];
+        cem[i] = a.emax[q];
+    }
+    for (int i = tid; i < SC_WAVES * 32; i += SC_WAVES * 64) {
+        const int ww = i / 32, ql = i % 32;
+        const uint32_t q = q0 + (uint32_t)((ww & 3) * 32 + ql);
+        const uint32_t g = q < a.nq ? a.gbound[q] : 0u;
+        const float t = q >= a.nq ? -__builtin_inff() : (g == 0xFFFFFFFFu ? __builtin_inff() : wvg_unord_f32(g));
+        tau[i] = t;
+        sig[i] = q >= a.nq ? __builtin_inff() : sc_sigma(t, cosine);
+    }
+    for (int i = tid; i < SC_WAVES * 32 * M; i += SC_WAVES * 64) lists[i] = WVG_KEY_NONE;
+    __syncthreads();
+    if (blk0 >= blk1) goto publish;
+    {
+        // stage loader: wave w moves fragments 6w .. 6w+5 of a stage (A 0..15, B 16..47)
+        auto load_stage = [&](unsigned char *dst, uint64_t blk, uint32_t ks) {
+#pragma unroll
+            for (int j = 0; j < 6; j++) {
+                const int f = 6 * w + j;
+                const uint4 *src;
+                if (f < SC_AFR) {
+                    const int kb2 = f >> 3, g = f & 7;
+                    src = a.qfrag + ((size_t)(qb * 8 + g) * a.kbn + 2 * ks + kb2) * 64;
+                } else {
+                    const int fb = f - SC_AFR, kb2 = fb >> 4, r16 = fb & 15, tt = r16 >> 2, rg = r16 & 3;
+                    const uint64_t t = a.tile_begin + blk * 4 + tt;  // the shadow is padded by 4 tiles
+                    src = a.shadow + (((size_t)t * a.kbn + 2 * ks + kb2) * 4 + rg) * 64;
+                }
+                __builtin_amdgcn_global_load_lds(src + lane, reinterpret_cast<uint4 *>(dst + f * 1024), 16, 0, 0);
+            }
+        };
+        const int qlane = 4 * (lane >> 4);
+        uint64_t qlive[2][4];
+#pragma unroll
+        for (int mq = 0; mq < 2; mq++)
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+                qlive[mq][r] = __ballot(q0 + 32 * wq + 16 * mq + qlane + r < a.nq);
+        uint64_t *WL = lists + (size_t)w * 32 * M;
+        float *WT = tau + w * 32, *WS = sig + w * 32;
+
+        // exact list insertion of one survivor (wave-uniform ql, u, slot)
+        auto insert = [&](int ql, float u, uint32_t slot) {
+            const float lower = sc_lower(u, cosine);
+            if (!(lower <= WT[ql])) return;
+            const uint64_t key = ((uint64_t)wvg_ord_f32(lower) << 32) | slot;
+            uint64_t *L = WL + ql * M;
+            const uint64_t v = lane < M ? L[lane] : WVG_KEY_NONE;
+            const uint64_t last = __shfl(v, M - 1);
+            if (!(key < last)) return;
+            const int pos = __popcll(__ballot(lane < M && v < key));
+            if (lane >= pos && lane < M - 1) L[lane + 1] = v;
+            if (lane == pos) L[pos] = key;
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            const uint64_t nk = L[K - 1], nm = L[M - 1];
+            if (lane == 0) {
+                float t = WT[ql];
+                if (nk != WVG_KEY_NONE) t = fminf(t, sc_tau_k(key_lower(nk), cem[32 * wq + ql], cosine));
+                if (nm != WVG_KEY_NONE) t = fminf(t, key_lower(nm));
+                WT[ql] = t;
+                WS[ql] = sc_sigma(t, cosine);
+            }
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        };
+
+        floatx4 acc[2][8];
+#pragma unroll
+        for (int mq = 0; mq < 2; mq++)
+#pragma unroll
+            for (int nr = 0; nr < 8; nr++) acc[mq][nr] = (floatx4){0.f, 0.f, 0.f, 0.f};
+        float nrm[8];
+        uint64_t blk = blk0;
+        uint32_t ks = 0;
+        int cur = 0;
+        load_stage(smem, blk, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        for (;;) {
+            // next stage in flight while this one is computed
+            uint64_t nblk_ = blk;
+            uint32_t nks = ks + 1;
+            if (nks == NK) {
+                nks = 0;
+                nblk_ = blk + 1;
+            }
+            const bool more = nblk_ < blk1;
+            if (more) load_stage(smem + (cur ^ 1) * SC_STAGE, nblk_, nks);
+            if (ks == 0) {
+#pragma unroll
+                for (int nr = 0; nr < 8; nr++) {
+                    const uint64_t slot = (a.tile_begin + blk * 4 + 2 * wr + (nr >> 2)) * 64 + 16 * (nr & 3) + (lane & 15);
+                    nrm[nr] = a.norms[slot];
+                }
+            }
+            const unsigned char *sb = smem + cur * SC_STAGE;
+#pragma unroll
+            for (int kb2 = 0; kb2 < 2; kb2++) {
+                bf16x8 av[2], bv[8];
+#pragma unroll
+                for (int mq = 0; mq < 2; mq++)
+                    av[mq] = *reinterpret_cast<const bf16x8 *>(sb + (kb2 * 8 + 2 * wq + mq) * 1024 + lane * 16);
+#pragma unroll
+                for (int nr = 0; nr < 8; nr++)
+                    bv[nr] = *reinterpret_cast<const bf16x8 *>(sb + (SC_AFR + kb2 * 16 + 8 * wr + nr) * 1024 + lane * 16);
+#pragma unroll
+                for (int mq = 0; mq < 2; mq++)
+#pragma unroll
+                    for (int nr = 0; nr < 8; nr++)
+                        acc[mq][nr] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[mq], bv[nr], acc[mq][nr], 0, 0, 0);
+            }
+            if (ks == NK - 1) {
+                // epilogue of row block blk: C layout row (query) qlane + r, column (row) lane & 15
+                uint64_t vm[2];
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const uint64_t t = a.tile_begin + blk * 4 + 2 * wr + h;
+                    uint64_t m = t < a.tile_end ? sc_sload64(a.valid + t) : 0ull;
+                    if (a.allow && m) {
+                        const uint64_t aw = t - a.allow_t0;
+                        m &= aw < a.allow_words ? sc_sload64(a.allow + aw) : 0ull;
+                    }
+                    vm[h] = m;
+                }
+#pragma unroll
+                for (int mq = 0; mq < 2; mq++) {
+                    const float4 k1v = *reinterpret_cast<const float4 *>(ck1 + 32 * wq + 16 * mq + qlane);
+                    const float4 k2v = *reinterpret_cast<const float4 *>(ck2 + 32 * wq + 16 * mq + qlane);
+                    const float4 sv = *reinterpret_cast<const float4 *>(WS + 16 * mq + qlane);
+                    const float k1r[4] = {k1v.x, k1v.y, k1v.z, k1v.w};
+                    const float k2r[4] = {k2v.x, k2v.y, k2v.z, k2v.w};
+                    const float svr[4] = {sv.x, sv.y, sv.z, sv.w};
+#pragma unroll
+                    for (int nr = 0; nr < 8; nr++) {
+                        const uint64_t m16 = (vm[nr >> 2] >> (16 * (nr & 3))) & 0xFFFFull;
+                        const uint64_t m64 = m16 * 0x0001000100010001ull;
+#pragma unroll
+                        for (int r = 0; r < 4; r++) {
+                            const float u = acc[mq][nr][r] + __builtin_fmaf(nrm[nr], k1r[r], k2r[r]);
+                            uint64_t pass = __ballot(!(u < svr[r])) & m64 & qlive[mq][r];
+                            while (pass) {  // rare after the first row blocks of a range
+                                const int src = __builtin_ctzll(pass);
+                                pass &= pass - 1;
+                                const int ql = 16 * mq + 4 * (src >> 4) + r;
+                                const float us = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(u), src));
+                                const uint32_t slot = (uint32_t)((a.tile_begin + blk * 4) * 64 + 128 * wr + 16 * nr +
+                                                                 (src & 15));
+                                insert(ql, us, slot);
+                            }
+                        }
+                    }
+                }
+#pragma unroll
+                for (int mq = 0; mq < 2; mq++)
+#pragma unroll
+                    for (int nr = 0; nr < 8; nr++) acc[mq][nr] = (floatx4){0.f, 0.f, 0.f, 0.f};
+            }
+            if (!more) break;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            blk = nblk_;
+            ks = nks;
+            cur ^= 1;
+        }
+    }
+publish:
+    __syncthreads();
+    // merge the two row halves' lists per query (waves wq and wq + 4), by rank:
+    // wave w takes queries w, w + 8, ... of the workgroup
+    for (int qw = w; qw < SC_BQ; qw += SC_WAVES) {
+        const uint32_t q = q0 + (uint32_t)qw;
+        if (q >= a.nq) break;
+        const int qq = qw >> 5, ql = qw & 31;
+        const uint64_t x = lane < M ? lists[((size_t)qq * 32 + ql) * M + lane]
+                                    : (lane < 2 * M ? lists[((size_t)(qq + 4) * 32 + ql) * M + lane - M] : WVG_KEY_NONE);
+        int rank = 0;
+        for (int j = 0; j < 2 * M; j++) {
+            const uint64_t y = __shfl(x, j);
+            rank += (y < x) || (y == x && j < lane);
+        }
+        uint64_t *out = a.partials + ((size_t)q * a.nrr + rr) * M;
+        if (lane < 2 * M && rank < M) out[rank] = x;
+        if (lane < 2 * M && rank == K - 1 && x != WVG_KEY_NONE) {
+            const float t = sc_tau_k(key_lower(x), cem[qw], cosine);
+            atomicMin(a.gbound + q, wvg_ord_f32(t));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Collect, per query.  Every range list holds its range's SCREEN_M smallest
+// lower bounds, so their union holds the global k smallest: tau* = the k-th
+// smallest lower of the union + 2 Emax is a valid bound (k rows at or below
+// it) and the tightest the lists give -- far below the per-range bounds the
+// screen published.  Entries with lower <= tau* become the rescore
+// candidates (KEY_NONE elsewhere); a range list that is full with its last
+// entry <= tau* may have dropped a row below tau*: the query is flagged for
+// the exact rescan.  The k-th smallest is a 4-pass radix select (8-bit
+// digits) over the entries' ordered lower bounds in LDS.
+constexpr uint32_t SC_COLLECT_MAX = 8192;  // nrr * SCREEN_M (screen_row_ranges caps nrr at 512)
+
+__global__ __launch_bounds__(256) void screen_collect_kernel(const uint64_t *partials, uint32_t nrr, uint32_t k,
+                                                             const float *emax, int cosine, uint64_t *cand,
+                                                             uint32_t *flist, uint32_t *nflag)
+{
+    __shared__ uint32_t hv[SC_COLLECT_MAX];
+    __shared__ uint32_t hist[256];
+    __shared__ uint32_t sh_prefix, sh_need, sh_total;
+    __shared__ int ovf;
+    const uint32_t q = blockIdx.x, n = nrr * SCREEN_M;
+    const uint64_t *src = partials + (size_t)q * n;
+    uint64_t *dst = cand + (size_t)q * n;
+    if (threadIdx.x == 0) {
+        ovf = 0;
+        sh_prefix = 0;
+        sh_need = k;
+        sh_total = 0;
+    }
+    __syncthreads();
+    uint32_t live = 0;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint64_t e = src[i];
+        hv[i] = (uint32_t)(e >> 32);  // KEY_NONE -> 0xFFFFFFFF, above every real ordered distance
+        live += e != WVG_KEY_NONE;
+    }
+    atomicAdd(&sh_total, live);
+    __syncthreads();
+    float t = __builtin_inff();
+    if (sh_total >= k) {
+        for (int shift = 24; shift >= 0; shift -= 8) {
+            for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) hist[i] = 0;
+            __syncthreads();
+            const uint32_t hi_mask = shift == 24 ? 0u : (0xFFFFFFFFu << (shift + 8));
+            const uint32_t pre = sh_prefix;
+            for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+                const uint32_t v = hv[i];
+                if (v != 0xFFFFFFFFu && (v & hi_mask) == (pre & hi_mask)) atomicAdd(&hist[(v >> shift) & 255u], 1u);
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                uint32_t need = sh_need, cum = 0, dg = 255;
+                for (uint32_t d = 0; d < 256; d++) {
+                    if (cum + hist[d] >= need) {
+                        dg = d;
+                        break;
+                    }
+                    cum += hist[d];
+                }
+                sh_need = need - cum;
+                sh_prefix = pre | (dg << shift);
+            }
+            __syncthreads();
+        }
+        t = sc_tau_k(wvg_unord_f32(sh_prefix), emax[q], cosine);
+    }
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint64_t e = src[i];
+        const bool keep = e != WVG_KEY_NONE && key_lower(e) <= t;
+        dst[i] = keep ? e : WVG_KEY_NONE;
+        if (keep && (i % SCREEN_M) == SCREEN_M - 1) ovf = 1;  // full list, last entry within tau*
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && ovf) flist[atomicAdd(nflag, 1u)] = q;
+}
+
+// Whether K3c applies (the bound needs dim % 32 == 0 only for the fragment
+// layout; k <= SCREEN_M for the list to hold the k-th key).
+bool screen_supported(uint32_t dim, int metric, uint32_t k)
+{
+    return dim % 32 == 0 && dim > 0 && k > 0 && k <= (uint32_t)SCREEN_M &&
+           (metric == WVG_M_DOT || metric == WVG_M_COSINE);
+}
+
+uint32_t screen_row_ranges(uint32_t nq, uint64_t ntiles, int num_cus)
+{
+    const uint32_t nqb = (nq + SC_BQ - 1) / SC_BQ;
+    const uint64_t nblk = (ntiles + 3) / 4;
+    // ranges of ~128 row blocks dispatched range-major (the nqb workgroups of a
+    // range start together on one XCD and share its L2 for the row fragments),
+    // at least one workgroup per CU
+    uint64_t want = std::max<uint64_t>(((uint64_t)num_cus + nqb - 1) / nqb, (nblk + 127) / 128);
+    want = std::min<uint64_t>((want + 7) / 8 * 8, SC_COLLECT_MAX / SCREEN_M);
+    if (want > nblk) want = nblk;
+    if (want < 1) want = 1;
+    return (uint32_t)want;
+}
+
+hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
+{
+    const uint32_t kbn = screen_kblocks(L.dim);
+    const uint32_t nq16 = (L.nq + 15) / 16, nq_pad = (L.nq + SC_BQ - 1) / SC_BQ * SC_BQ;
+    const uint32_t nqb = nq_pad / SC_BQ;
+    hipError_t e;
+    // query fragments for every 16-query group of the padded batch
+    hipLaunchKernelGGL(screen_qfrag_kernel, dim3((unsigned)(((uint64_t)nq_pad / 16 * kbn * 64 + 255) / 256)), dim3(256),
+                       0, s, L.queries, L.nq, L.qpitch, L.dim, kbn, nq_pad / 16, reinterpret_cast<uint4 *>(L.qfrag));
+    (void)nq16;
+    hipLaunchKernelGGL(screen_qconst_kernel, dim3(nq_pad / 4), dim3(256), 0, s, L.queries, L.nq, L.qpitch, L.dim,
+                       nq_pad, L.cosine, L.nmax, L.k1, L.k2, L.emax);
+    if ((e = hipMemsetAsync(L.gbound, 0xFF, (size_t)L.nq * 4, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(L.nflag, 0, 4, s)) != hipSuccess) return e;
+    ScreenArgs a{};
+    a.shadow = reinterpret_cast<const uint4 *>(L.shadow);
+    a.norms = L.norms;
+    a.valid = L.valid;
+    a.allow = L.allow;
+    a.allow_words = L.allow_words;
+    a.allow_t0 = L.allow_t0;
+    a.tile_begin = L.tile_begin;
+    a.tile_end = L.tile_end;
+    a.kbn = kbn;
+    a.qfrag = reinterpret_cast<const uint4 *>(L.qfrag);
+    a.k1 = L.k1;
+    a.k2 = L.k2;
+    a.emax = L.emax;
+    a.nq = L.nq;
+    a.k = L.k;
+    a.nqb = nqb;
+    a.nrr = L.nrr;
+    a.cosine = L.cosine;
+    a.gbound = L.gbound;
+    a.partials = L.partials;
+    static bool attr = [] {
+        return hipFuncSetAttribute(reinterpret_cast<const void *>(&screen_kernel),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, SC_LDS) == hipSuccess;
+    }();
+    (void)attr;
+    launch_timed(screen_kernel, dim3(nqb * L.nrr), dim3(SC_WAVES * 64), (uint32_t)SC_LDS, s, a);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(screen_collect_kernel, dim3(L.nq), dim3(256), 0, s, L.partials, L.nrr, L.k, L.emax, L.cosine,
+                       L.cand, L.flist, L.nflag);
+    return hipGetLastError();
+}
+
+}  // namespace wvg
