@@ -329,9 +329,9 @@ def test_pinned_host_buffers(ctx, orc):
     assert not p.value
 
 
-@pytest.mark.parametrize("kind", [KIND_BQ, KIND_PQ])
+@pytest.mark.parametrize("kind", [KIND_F32, KIND_BQ, KIND_PQ])
 def test_cosched_batches_equal_single_queries(ctx, orc, kind):
-    """Co-scheduled batches (K5 / K8e COS: the nq queries of a row range on one
+    """Co-scheduled batches (K1 / K5 / K8e COS: the nq queries of a row range on one
     XCD, workgroup id -> (range, query)) return exactly what one query per
     call returns.  nq = 2 .. 300 covers the range-count floor of
     pq_cosched_groups (8 ranges once nq >= num_cus / 8, where the queries of
@@ -356,15 +356,17 @@ def test_cosched_batches_equal_single_queries(ctx, orc, kind):
     if f is not None:
         f.delete(dead)
     qs_all = orc.synth_rows(602, 0, 300, d, 0)
+    allow = allow_bitmap(np.arange(3, n, 5, dtype=np.uint64)) if kind == KIND_F32 else None
     try:
         for nq, ks in [(2, (10, 256)), (12, (10, 100, 200)), (40, (10, 256)), (300, (10,))]:
             qs = qs_all[:nq]
             for k in ks:
-                singles = [c.search(qs[i], k) for i in range(nq)]
-                ids, dists, counts = c.search(qs, k)
-                for i, (si, sd, sc) in enumerate(singles):
-                    assert counts[i] == sc[0]
-                    assert np.array_equal(ids[i], si[0]) and np.array_equal(bits(dists[i]), bits(sd[0]))
+                for al in ((None, allow) if allow is not None and nq <= 12 else (None,)):
+                    singles = [c.search(qs[i], k, al) for i in range(nq)]
+                    ids, dists, counts = c.search(qs, k, al)
+                    for i, (si, sd, sc) in enumerate(singles):
+                        assert counts[i] == sc[0]
+                        assert np.array_equal(ids[i], si[0]) and np.array_equal(bits(dists[i]), bits(sd[0]))
             if f is not None and nq <= 40:
                 single = [search_bq_rescore(c, f, qs[i], 10, 200) for i in range(nq)]
                 bi, bd, bc = search_bq_rescore(c, f, qs, 10, 200)

@@ -181,7 +181,9 @@ def test_screen_device_path(ctx, exact_ctx, orc):
     rows = orc.synth_rows(1500, 0, n, d, 0)
     a, b = _pair(ctx, exact_ctx, METRIC_COSINE, d, rows)
     try:
-        qs = np.stack([orc.normalize(q) for q in orc.synth_rows(1501, 0, nq, d, 0)]).astype(np.float32)
+        raw = orc.synth_rows(1501, 0, nq, d, 0)
+        # the device API takes normalized queries; the host API normalizes raw ones (Normalize, the same bits)
+        qs = np.stack([orc.normalize(q) for q in raw]).astype(np.float32)
         lib = ctx.lib
         dev = torch.device("cuda:0")
         ws = torch.zeros(lib.wvg_search_workspace_size(a.handle, nq, k), dtype=torch.uint8, device=dev)
@@ -195,7 +197,7 @@ def test_screen_device_path(ctx, exact_ctx, orc):
                                              torch.cuda.current_stream().cuda_stream))
             torch.cuda.synchronize()
             _same((oi.cpu().numpy().view(np.uint64), od.cpu().numpy(), oc.cpu().numpy().astype(np.uint32)),
-                  b.search(qs, k))
+                  b.search(raw, k))
     finally:
         a.destroy()
         b.destroy()

@@ -1153,6 +1153,14 @@ static SearchPlan plan_search(wvg_corpus *c, uint32_t nq, uint32_t k, const uint
     p.cosched = nq > 1 && !allow && tuning().pq_cosched != 0 && (pq_cos || bq_cos);
     if (p.cosched)  // BQ: K5 workgroups are 4 waves, so bq_cos_gpc of them per CU
         p.groups = pq_cosched_groups(nq, c->ctx->num_cus * (bq_cos ? std::max(1, tuning().bq_cos_gpc) : 1));
+    // flat batches below the MFMA threshold: K1 COS, the nq queries of one row
+    // range side by side on one XCD (K1's workgroups per CU as for one query)
+    if (c->kind == WVG_KIND_F32 && nq > 1 && !p.gemm && tuning().pq_cosched != 0) {
+        ScanArgs a1 = a;
+        a1.nq = 1;
+        p.cosched = true;
+        p.groups = pq_cosched_groups(nq, std::max(scan_groups_for(a1, c->ctx->num_cus), 8));
+    }
     return p;
 }
 
@@ -1275,6 +1283,10 @@ static int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t 
     a.plain = plain_loads(c, p.tb, p.te);
     a.cache_tail256 = k1_cache_tail(c, p.tb, p.te);
     if (!p.gemm) a.reverse = next_direction(c, 1);
+    if (p.cosched && c->kind == WVG_KIND_F32) {  // K1 COS: partners read the rows from L2
+        a.plain = 1;
+        a.cache_tail256 = 0;
+    }
     if (p.screen) {
         if (ensure_shadow(c, s)) {
             ProfArm arm(c->ctx);
@@ -2558,21 +2570,31 @@ int wvg_pq_fit(wvg_ctx *ctx, const float *X, uint64_t n, uint32_t dim, uint32_t 
     if (n < ks) return fail(WVG_ERR_INVALID, "not enough data to fit kmeans");  // kmeans.go:222-224
     if (n > 0xFFFFFFFFull) return fail(WVG_ERR_INVALID, "too many training rows");
     WVG_HIP(hipSetDevice(ctx->device));
-    const uint32_t ds = dim / m;
+    const uint32_t ds = dim / m, nch = f32_chunks(dim);
     const size_t nc = (size_t)m * ks * ds;
     Carver cv;
-    const size_t o_x = cv.take(n * dim * 4), o_c = cv.take(nc * 4), o_p = cv.take(n * m),
+    const size_t o_x = cv.take(n * dim * 4), o_xt = cv.take(tiles_of(n) * 64 * (size_t)nch * 16),
+                 o_c = cv.take(pq_centers_alloc_bytes(m, ks, ds)), o_p = cv.take(n * m), o_code = cv.take(n * m),
+                 o_mem = cv.take(n * m * 4), o_off = cv.take((size_t)m * ks * 4),
                  o_cnt = cv.take((size_t)m * ks * 4), o_chg = cv.take((size_t)m * 4), o_act = cv.take(m),
                  o_rec = cv.take(m), o_skip = cv.take((size_t)m * ks);
     Bulk bk(ctx);
     rc = bk.begin(cv.off);
     if (rc) return rc;
     hipStream_t s = bk.s();
-    float *dX = (float *)(bk.b + o_x), *dC = (float *)(bk.b + o_c);
-    uint8_t *dP = (uint8_t *)(bk.b + o_p);
+    float *dX = (float *)(bk.b + o_x), *dXt = (float *)(bk.b + o_xt), *dC = (float *)(bk.b + o_c);
+    uint8_t *dP = (uint8_t *)(bk.b + o_p), *dCode = (uint8_t *)(bk.b + o_code);
+    uint32_t *dMem = (uint32_t *)(bk.b + o_mem), *dOff = (uint32_t *)(bk.b + o_off);
     uint32_t *dCnt = (uint32_t *)(bk.b + o_cnt), *dChg = (uint32_t *)(bk.b + o_chg);
     uint8_t *dAct = (uint8_t *)(bk.b + o_act), *dRec = (uint8_t *)(bk.b + o_rec), *dSkip = (uint8_t *)(bk.b + o_skip);
     WVG_HIP(hipMemcpyAsync(dX, X, n * dim * 4, hipMemcpyHostToDevice, s));
+    // the training rows in the tiled layout K9 (the assignment) reads
+    WVG_HIP(hipMemsetAsync(dXt, 0, tiles_of(n) * 64 * (size_t)nch * 16, s));
+    WVG_HIP(launch_f32_store(dX, nullptr, n, dim, nch, 0, dXt, s));
+    const bool pairs = pq_has_pairs(ks, ds);
+    auto refresh_pairs = [&]() -> hipError_t {  // K9's ds = 4 pair copy of the current centers
+        return pairs ? launch_pq_pairs(dC, m, ks, dC + nc, s) : hipSuccess;
+    };
     // initCenters (kmeans.go:146-160): ks random rows (with replacement) per segment
     std::vector<float> C(nc);
     std::vector<uint64_t> ctr(m, 0);
@@ -2582,10 +2604,11 @@ int wvg_pq_fit(wvg_ctx *ctx, const float *X, uint64_t n, uint32_t dim, uint32_t 
             std::memcpy(&C[((size_t)sg * ks + c) * ds], X + r * dim + (size_t)sg * ds, ds * 4);
         }
     WVG_HIP(hipMemcpyAsync(dC, C.data(), nc * 4, hipMemcpyHostToDevice, s));
-    WVG_HIP(hipMemsetAsync(dP, 0, n * m, s));  // data.points = make([]uint64, n): all zero
+    WVG_HIP(refresh_pairs());
+    WVG_HIP(hipMemsetAsync(dP, 0, n * m, s));  // data.points = make([]uint64, n): all zero (kept [m][n])
     std::vector<uint8_t> active(m, 1), rec(m), skip((size_t)m * ks);
     std::vector<uint32_t> cnt((size_t)m * ks), chg(m), iters(m, 0);
-    std::vector<uint8_t> hp;  // host copy of points, only when a reseed needs it
+    std::vector<uint8_t> hp;  // host copy of points ([m][n]), only when a reseed needs it
     const int thresh = (int)((float)n * 0.01f);  // int(float32(dataSize) * DeltaThreshold), kmeans.go:217-219
     for (uint32_t it = 0;; it++) {
         bool any = false;
@@ -2594,7 +2617,10 @@ int wvg_pq_fit(wvg_ctx *ctx, const float *X, uint64_t n, uint32_t dim, uint32_t 
         WVG_HIP(hipMemcpyAsync(dAct, active.data(), m, hipMemcpyHostToDevice, s));
         WVG_HIP(hipMemsetAsync(dCnt, 0, (size_t)m * ks * 4, s));
         WVG_HIP(hipMemsetAsync(dChg, 0, (size_t)m * 4, s));
-        WVG_HIP(launch_kmeans_assign(dX, n, dim, dC, m, ks, ds, dAct, dP, dChg, dCnt, s));
+        // nNearest for every (row, segment): K9, the encoder (kmeans.go:103-135; ties to the
+        // highest index); then changes and cluster sizes of the active segments
+        WVG_HIP(launch_pq_encode(dXt, n, dim, dC, m, ks, dCode, s, false, false));
+        WVG_HIP(launch_kmeans_count(dCode, n, m, ks, dAct, dP, dChg, dCnt, s));
         WVG_HIP(hipMemcpyAsync(cnt.data(), dCnt, cnt.size() * 4, hipMemcpyDeviceToHost, s));
         WVG_HIP(hipMemcpyAsync(chg.data(), dChg, chg.size() * 4, hipMemcpyDeviceToHost, s));
         WVG_HIP(hipStreamSynchronize(s));
@@ -2618,10 +2644,10 @@ int wvg_pq_fit(wvg_ctx *ctx, const float *X, uint64_t n, uint32_t dim, uint32_t 
                 uint64_t ri;
                 for (;;) {
                     ri = kmeans_draw(seed, sg, ctr[sg], n);
-                    if (size[hp[ri * m + sg]] > 1) break;
+                    if (size[hp[(size_t)sg * n + ri]] > 1) break;
                 }
                 size[ci] = 1;
-                hp[ri * m + sg] = (uint8_t)ci;
+                hp[(size_t)sg * n + ri] = (uint8_t)ci;
                 skip[(size_t)sg * ks + ci] = 1;
                 moves.push_back({ri, {sg, ci}});
                 for (uint32_t j = 0; j < ds; j++)  // recalcCenters over cc[ci] = {ri}: (0 + x) / float32(1)
@@ -2634,15 +2660,16 @@ int wvg_pq_fit(wvg_ctx *ctx, const float *X, uint64_t n, uint32_t dim, uint32_t 
         WVG_HIP(hipMemcpyAsync(dSkip, skip.data(), skip.size(), hipMemcpyHostToDevice, s));
         // recalcCenters with the recluster assignment (the reseeded rows still
         // in their old clusters), then the reseeded clusters = their one row
-        WVG_HIP(launch_kmeans_recalc(dX, n, dim, dP, m, ks, ds, dRec, dCnt, dSkip, dC, s));
+        WVG_HIP(launch_kmeans_recalc2(dX, n, dim, dP, m, ks, ds, dRec, dCnt, dSkip, dMem, dOff, dC, s));
         for (auto &mv : moves) {
             const uint32_t sg = mv.second.first, ci = mv.second.second;
             const uint8_t code = (uint8_t)ci;
             WVG_HIP(hipMemcpyAsync(dC + ((size_t)sg * ks + ci) * ds, &C[((size_t)sg * ks + ci) * ds], ds * 4,
                                    hipMemcpyHostToDevice, s));
-            WVG_HIP(hipMemcpyAsync(dP + mv.first * m + sg, &code, 1, hipMemcpyHostToDevice, s));
+            WVG_HIP(hipMemcpyAsync(dP + (size_t)sg * n + mv.first, &code, 1, hipMemcpyHostToDevice, s));
             WVG_HIP(hipStreamSynchronize(s));  // `code` is a stack byte
         }
+        WVG_HIP(refresh_pairs());
         for (uint32_t sg = 0; sg < m; sg++) {
             if (!active[sg]) continue;
             iters[sg] = it + 1;

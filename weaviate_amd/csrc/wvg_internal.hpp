@@ -446,12 +446,15 @@ hipError_t sort_keys64(void *temp, size_t temp_bytes, const uint64_t *in, uint64
 hipError_t launch_emit_sorted(const uint64_t *sorted, uint64_t n, uint64_t id_base, uint64_t *ids,
                               float *dists, hipStream_t s);
 // k-means training (wvg_pq.hip K10) and the PQ symmetric-distance table.
-hipError_t launch_kmeans_assign(const float *X, uint64_t n, uint32_t dim, const float *centers, uint32_t m,
-                                uint32_t ks, uint32_t ds, const uint8_t *active, uint8_t *points,
-                                uint32_t *changes, uint32_t *counts, hipStream_t s);
-hipError_t launch_kmeans_recalc(const float *X, uint64_t n, uint32_t dim, const uint8_t *points, uint32_t m,
-                                uint32_t ks, uint32_t ds, const uint8_t *recalc, const uint32_t *counts,
-                                const uint8_t *skip, float *centers, hipStream_t s);
+// K10 (wvg_pq.hip): one Lloyd pass = K9 assignment, count, members, sums;
+// points segment-major [m][n]
+hipError_t launch_pq_pairs(const float *centers, uint32_t m, uint32_t ks, float *out, hipStream_t s);
+hipError_t launch_kmeans_count(const uint8_t *codes, uint64_t n, uint32_t m, uint32_t ks, const uint8_t *active,
+                               uint8_t *points, uint32_t *changes, uint32_t *counts, hipStream_t s);
+hipError_t launch_kmeans_recalc2(const float *X, uint64_t n, uint32_t dim, const uint8_t *points, uint32_t m,
+                                 uint32_t ks, uint32_t ds, const uint8_t *recalc, const uint32_t *counts,
+                                 const uint8_t *skip, uint32_t *members, uint32_t *offsets, float *centers,
+                                 hipStream_t s);
 hipError_t launch_pq_sdc_table(int metric, const float *centers, uint32_t m, uint32_t ks, uint32_t ds,
                                float *table, hipStream_t s);
 hipError_t launch_pq_sdc_rows(int metric, const float *table, uint32_t m, uint32_t ks, const uint8_t *x,

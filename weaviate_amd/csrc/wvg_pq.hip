@@ -1533,94 +1533,168 @@ hipError_t launch_pq_adc_rows(int metric, const float *lut, uint32_t m, uint32_t
 // ---------------------------------------------------------------------------
 namespace wvg {
 
-// recluster (kmeans.go:162-175): points[p][s] = nNearest(x_p, 1) for active
-// segments, counting changes against the previous assignment and cluster
-// sizes.  One thread per (row, segment); l2_256 order, ties -> highest index.
-__global__ void kmeans_assign_kernel(const float *X, uint64_t n, uint32_t dim, const float *centers, uint32_t m,
-                                     uint32_t ks, uint32_t ds, const uint8_t *active, uint8_t *points,
-                                     uint32_t *changes, uint32_t *counts)
+// One Lloyd pass:
+//   assignment = K9 (pq_encode_kernel: nNearest, kmeans.go:103-135, the same
+//                rule as the encoder, over a tiled copy of the training rows),
+//   kmeans_count_kernel   (changes per segment, cluster sizes, points updated),
+//   kmeans_members_kernel (per segment, a stable counting sort of the rows by
+//                          cluster: member lists in ascending row order),
+//   kmeans_sum_kernel     (one thread per (segment, cluster, dim): the
+//                          reference's sequential fp32 sum over the members).
+// Points are kept segment-major [m][n].  (Round 2's assign kernel -- one
+// thread per (row, segment), centroids from global memory, a global atomic per
+// row -- sat 96 % of its wave cycles parked: 8.45 ms per pass at 100k x 128;
+// its recalc scanned all n rows per output: 5.56 ms.)
+
+// The pair-interleaved copy of a [m][ks][4] codebook that K9's ds = 4 path
+// reads right after the table (pq_pair_layout on the device).
+__global__ __launch_bounds__(256) void pq_pairs_kernel(const float *centers, uint32_t m, uint32_t ks, float *out)
 {
-    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= n * m) return;
-    const uint64_t p = g / m;
-    const uint32_t s = (uint32_t)(g % m);
-    if (!active[s]) return;
-    const float *x = X + p * dim + (size_t)s * ds;
-    const float *cs = centers + (size_t)s * ks * ds;
-    uint32_t best = 0;
-    float minD = 3.40282346638528859812e+38f;  // math.MaxFloat32
-    auto xa = [&](int i) { return x[i]; };
-    for (uint32_t c = 0; c < ks; c++) {
-        const float *cv = cs + (size_t)c * ds;
-        auto ca = [&](int i) { return cv[i]; };
-        const float d = l2_256_acc(xa, ca, (int)ds);
-        if (!(minD < d)) {
-            minD = d;
-            best = c;
-        }
-    }
-    if (points[g] != best) {
-        points[g] = (uint8_t)best;
-        atomicAdd(&changes[s], 1u);
-    }
-    atomicAdd(&counts[(size_t)s * ks + best], 1u);
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;  // (s, p, k, h)
+    if (i >= (uint64_t)m * ks * 4) return;
+    const uint32_t h = (uint32_t)(i & 1), k = (uint32_t)((i >> 1) & 3);
+    const uint64_t sp = i >> 3;
+    const uint32_t sg = (uint32_t)(sp / (ks / 2)), pr = (uint32_t)(sp % (ks / 2));
+    out[i] = centers[((size_t)sg * ks + 2 * pr + h) * 4 + k];
 }
 
-hipError_t launch_kmeans_assign(const float *X, uint64_t n, uint32_t dim, const float *centers, uint32_t m,
-                                uint32_t ks, uint32_t ds, const uint8_t *active, uint8_t *points, uint32_t *changes,
-                                uint32_t *counts, hipStream_t s)
+hipError_t launch_pq_pairs(const float *centers, uint32_t m, uint32_t ks, float *out, hipStream_t s)
 {
-    const uint64_t total = n * m;
-    if (total == 0) return hipSuccess;
-    hipLaunchKernelGGL(kmeans_assign_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, X, n, dim,
-                       centers, m, ks, ds, active, points, changes, counts);
+    const uint64_t n = (uint64_t)m * ks * 4;
+    hipLaunchKernelGGL(pq_pairs_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, centers, m, ks, out);
     return hipGetLastError();
 }
 
-// recalcCenters (kmeans.go:200-218): centers[s][c][j] = (0 + sum over the
-// members p of cluster c, in ascending p) / float32(size).  A workgroup owns
-// 256 (cluster, dim) outputs of one segment and streams the rows through LDS
-// in chunks of 256, each thread keeping its own sequential fp32 sum.
-// Clusters flagged in `skip` (reseeded on the host) are left untouched.
-constexpr int KM_CHUNK = 256;
-
-__global__ __launch_bounds__(256) void kmeans_recalc_kernel(const float *X, uint64_t n, uint32_t dim,
-                                                             const uint8_t *points, uint32_t m, uint32_t ks,
-                                                             uint32_t ds, const uint8_t *recalc, const uint32_t *counts,
-                                                             const uint8_t *skip, float *centers, uint32_t groups_per_seg,
-                                                             uint32_t chunk)
+// Block (s, b): rows [b * rows_per, (b + 1) * rows_per) of an active segment s.
+__global__ __launch_bounds__(256) void kmeans_count_kernel(const uint8_t *codes, uint64_t n, uint32_t m, uint32_t ks,
+                                                           const uint8_t *active, uint8_t *points, uint32_t *changes,
+                                                           uint32_t *counts, uint64_t rows_per)
 {
-    extern __shared__ float xs[];  // [chunk][ds]
-    __shared__ uint8_t ps[KM_CHUNK];
-    const uint32_t s = blockIdx.x / groups_per_seg;
-    if (!recalc[s]) return;
-    const uint32_t o = (blockIdx.x % groups_per_seg) * 256 + threadIdx.x;  // output index within the segment
-    const bool live = o < ks * ds;
-    const uint32_t c = live ? o / ds : 0, j = live ? o % ds : 0;
-    float sum = 0.0f;
-    for (uint64_t p0 = 0; p0 < n; p0 += chunk) {
-        const uint32_t cnt = (uint32_t)min<uint64_t>(chunk, n - p0);
-        __syncthreads();
-        for (uint32_t i = threadIdx.x; i < cnt; i += 256) ps[i] = points[(p0 + i) * m + s];
-        for (uint32_t i = threadIdx.x; i < cnt * ds; i += 256)
-            xs[i] = X[(p0 + i / ds) * dim + (size_t)s * ds + i % ds];
-        __syncthreads();
-        if (live)
-            for (uint32_t i = 0; i < cnt; i++)
-                if (ps[i] == c) sum = sum + xs[i * ds + j];
+    __shared__ uint32_t hist[256];
+    __shared__ uint32_t chg;
+    const uint32_t sg = blockIdx.x;
+    if (!active[sg]) return;
+    hist[threadIdx.x] = 0;
+    if (threadIdx.x == 0) chg = 0;
+    __syncthreads();
+    const uint64_t p0 = (uint64_t)blockIdx.y * rows_per, p1 = min(n, p0 + rows_per);
+    uint32_t mine = 0;
+    for (uint64_t p = p0 + threadIdx.x; p < p1; p += 256) {
+        const uint8_t c = codes[p * m + sg];
+        uint8_t *pp = points + (size_t)sg * n + p;
+        if (*pp != c) {
+            *pp = c;
+            mine++;
+        }
+        atomicAdd(&hist[c], 1u);
     }
-    if (!live || skip[(size_t)s * ks + c]) return;
-    centers[((size_t)s * ks + c) * ds + j] = sum / (float)counts[(size_t)s * ks + c];
+    atomicAdd(&chg, mine);
+    __syncthreads();
+    for (uint32_t c = threadIdx.x; c < ks; c += 256)
+        if (hist[c]) atomicAdd(&counts[(size_t)sg * ks + c], hist[c]);
+    if (threadIdx.x == 0 && chg) atomicAdd(&changes[sg], chg);
 }
 
-hipError_t launch_kmeans_recalc(const float *X, uint64_t n, uint32_t dim, const uint8_t *points, uint32_t m,
-                                uint32_t ks, uint32_t ds, const uint8_t *recalc, const uint32_t *counts,
-                                const uint8_t *skip, float *centers, hipStream_t s)
+hipError_t launch_kmeans_count(const uint8_t *codes, uint64_t n, uint32_t m, uint32_t ks, const uint8_t *active,
+                               uint8_t *points, uint32_t *changes, uint32_t *counts, hipStream_t s)
 {
-    const uint32_t gps = (ks * ds + 255) / 256;
-    const uint32_t chunk = std::max<uint32_t>(1, std::min<uint32_t>(KM_CHUNK, 16384 / ds));  // <= 64 KiB of rows
-    hipLaunchKernelGGL(kmeans_recalc_kernel, dim3(m * gps), dim3(256), (size_t)chunk * ds * 4, s, X, n, dim,
-                       points, m, ks, ds, recalc, counts, skip, centers, gps, chunk);
+    const uint64_t rows_per = 4096;
+    hipLaunchKernelGGL(kmeans_count_kernel, dim3(m, (unsigned)((n + rows_per - 1) / rows_per)), dim3(256), 0, s, codes,
+                       n, m, ks, active, points, changes, counts, rows_per);
+    return hipGetLastError();
+}
+
+// One block per recalculated segment: offsets = exclusive prefix of the
+// cluster sizes, then the rows in 256-row chunks: a row's place = its
+// cluster's running base + the same-cluster rows of earlier waves of the
+// chunk + those of lower lanes of its own wave (an 8-ballot match), so every
+// member list is in ascending row order.
+__global__ __launch_bounds__(256) void kmeans_members_kernel(const uint8_t *points, uint64_t n, uint32_t ks,
+                                                             const uint32_t *counts, const uint8_t *recalc,
+                                                             uint32_t *members, uint32_t *offsets)
+{
+    __shared__ uint32_t base[256];
+    __shared__ uint32_t wcnt[4][256];
+    const uint32_t sg = blockIdx.x;
+    if (!recalc[sg]) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid == 0) {
+        uint32_t acc = 0;
+        for (uint32_t c = 0; c < ks; c++) {
+            base[c] = acc;
+            offsets[(size_t)sg * ks + c] = acc;
+            acc += counts[(size_t)sg * ks + c];
+        }
+    }
+    for (int i = tid; i < 4 * 256; i += 256) (&wcnt[0][0])[i] = 0;
+    __syncthreads();
+    const uint8_t *pts = points + (size_t)sg * n;
+    uint32_t *mem = members + (size_t)sg * n;
+    for (uint64_t p0 = 0; p0 < n; p0 += 256) {
+        const uint64_t p = p0 + (uint64_t)tid;
+        const bool live = p < n;
+        const uint32_t c = live ? pts[p] : 0u;
+        uint64_t same = __ballot(live);
+#pragma unroll
+        for (int b = 0; b < 8; b++) {
+            const uint64_t bb = __ballot(live && ((c >> b) & 1u));
+            same &= ((c >> b) & 1u) ? bb : ~bb;
+        }
+        const uint32_t below = (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
+        if (live && below == 0) wcnt[w][c] = (uint32_t)__popcll(same);  // the lowest lane of each value
+        __syncthreads();
+        if (live) {
+            uint32_t off = base[c] + below;
+            for (int v = 0; v < w; v++) off += wcnt[v][c];
+            mem[off] = (uint32_t)p;
+        }
+        __syncthreads();
+        for (uint32_t cc = (uint32_t)tid; cc < ks; cc += 256) {
+            base[cc] += wcnt[0][cc] + wcnt[1][cc] + wcnt[2][cc] + wcnt[3][cc];
+            wcnt[0][cc] = wcnt[1][cc] = wcnt[2][cc] = wcnt[3][cc] = 0;
+        }
+        __syncthreads();
+    }
+}
+
+// recalcCenters (kmeans.go:200-218) from the member lists: centers[s][c][j] =
+// (0 + x[m0][j] + x[m1][j] + ...) / float32(size), members ascending; the
+// loads of eight members are issued before their adds.  Clusters flagged in
+// `skip` (reseeded on the host) are left untouched.
+__global__ __launch_bounds__(256) void kmeans_sum_kernel(const float *X, uint64_t n, uint32_t dim, uint32_t m,
+                                                         uint32_t ks, uint32_t ds, const uint32_t *members,
+                                                         const uint32_t *offsets, const uint32_t *counts,
+                                                         const uint8_t *recalc, const uint8_t *skip, float *centers)
+{
+    const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;  // (s, c, j)
+    if (g >= (uint64_t)m * ks * ds) return;
+    const uint32_t j = (uint32_t)(g % ds), c = (uint32_t)((g / ds) % ks), sg = (uint32_t)(g / ((uint64_t)ds * ks));
+    if (!recalc[sg] || skip[(size_t)sg * ks + c]) return;
+    const uint32_t cnt = counts[(size_t)sg * ks + c];
+    const uint32_t *mem = members + (size_t)sg * n + offsets[(size_t)sg * ks + c];
+    const float *xs = X + (size_t)sg * ds + j;
+    float sum = 0.0f;
+    uint32_t i = 0;
+    for (; i + 8 <= cnt; i += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = xs[(size_t)mem[i + u] * dim];
+#pragma unroll
+        for (int u = 0; u < 8; u++) sum = sum + v[u];
+    }
+    for (; i < cnt; i++) sum = sum + xs[(size_t)mem[i] * dim];
+    centers[((size_t)sg * ks + c) * ds + j] = sum / (float)cnt;
+}
+
+hipError_t launch_kmeans_recalc2(const float *X, uint64_t n, uint32_t dim, const uint8_t *points, uint32_t m,
+                                 uint32_t ks, uint32_t ds, const uint8_t *recalc, const uint32_t *counts,
+                                 const uint8_t *skip, uint32_t *members, uint32_t *offsets, float *centers,
+                                 hipStream_t s)
+{
+    hipLaunchKernelGGL(kmeans_members_kernel, dim3(m), dim3(256), 0, s, points, n, ks, counts, recalc, members, offsets);
+    const uint64_t total = (uint64_t)m * ks * ds;
+    hipLaunchKernelGGL(kmeans_sum_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, X, n, dim, m, ks, ds,
+                       members, offsets, counts, recalc, skip, centers);
     return hipGetLastError();
 }
 

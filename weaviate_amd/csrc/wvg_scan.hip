@@ -151,8 +151,14 @@ __device__ __forceinline__ void scan_tiles(const ScanArgs &a, const float4 *q4, 
     }
 }
 
-// Variant 0 (and 2 = plain loads).
-template <int METRIC, int D, int E>
+// COS (a batch of 1 < nq < the MFMA threshold, ScanArgs::cosched): a 1D grid
+// of G row ranges x nq queries where workgroup id -> (range, query) puts the
+// nq queries of one range at consecutive ids on ONE XCD (equal id mod 8; K5 /
+// K8e use the same map).  They run side by side and each wave walks the same
+// rows as its partners, so all but the first read of a line hit that XCD's
+// L2 (the host sets default-policy loads for this).  Results are those of
+// single-query scans: the keys are lexicographic, the visiting order free.
+template <int METRIC, int D, int E, bool COS = false>
 __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_kernel(ScanArgs a, uint64_t *partials)
 {
     if (a.side.active && blockIdx.x == gridDim.x - 1) {  // the previous query's merge (uniform branch)
@@ -161,14 +167,25 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_kernel(ScanArgs a, u
                                             a.side.id_base, a.side.ids, a.side.dists, a.side.counts);
         return;
     }
-    const uint32_t qi = blockIdx.y;
-    const float4 *q4 = reinterpret_cast<const float4 *>(a.queries) + (size_t)qi * (a.qpitch / 4);
+    uint32_t qi = blockIdx.y, rng = blockIdx.x, G = gridDim.x;
     uint64_t t0, t1;
-    wave_range(a, SCAN_WAVES, t0, t1);
+    if constexpr (COS) {
+        G = gridDim.x / a.nq;
+        const uint32_t kk = blockIdx.x >> 3;
+        rng = (kk / a.nq) * 8u + (blockIdx.x & 7u);
+        qi = kk % a.nq;
+        const uint64_t ntiles = a.tile_end - a.tile_begin, total = (uint64_t)G * SCAN_WAVES;
+        const uint64_t gw = (uint64_t)rng * SCAN_WAVES + wave_id();
+        t0 = a.tile_begin + ntiles * gw / total;
+        t1 = a.tile_begin + ntiles * (gw + 1) / total;
+    } else {
+        wave_range(a, SCAN_WAVES, t0, t1);
+    }
+    const float4 *q4 = reinterpret_cast<const float4 *>(a.queries) + (size_t)qi * (a.qpitch / 4);
     WaveTopK<E> tk;
     tk.init((int)a.k);
     scan_tiles<METRIC, D, E>(a, q4, t0, t1, tk, a.reverse & 1u);
-    group_combine_store<E, SCAN_WAVES>(tk, partials + ((size_t)qi * gridDim.x + blockIdx.x) * a.k);
+    group_combine_store<E, SCAN_WAVES>(tk, partials + ((size_t)qi * G + rng) * a.k);
 }
 
 // The exact rescan of a query list (the K3c screen's flagged queries, whose
@@ -492,6 +509,16 @@ static void launch_fixed(const ScanArgs &a, uint64_t *partials, dim3 grid, dim3 
 template <int METRIC, int E>
 static hipError_t launch_f32_e(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
 {
+    if (a.cosched && a.nq > 1 && groups % 8 == 0 && !a.side.active) {
+        dim3 grid((unsigned)groups * a.nq), block(SCAN_WAVES * 64);
+        switch (a.dim) {
+        case 128: launch_timed((scan_f32_kernel<METRIC, 128, E, true>), grid, block, 0, s, a, partials); break;
+        case 768: launch_timed((scan_f32_kernel<METRIC, 768, E, true>), grid, block, 0, s, a, partials); break;
+        case 1536: launch_timed((scan_f32_kernel<METRIC, 1536, E, true>), grid, block, 0, s, a, partials); break;
+        default: launch_timed((scan_f32_kernel<METRIC, 0, E, true>), grid, block, 0, s, a, partials); break;
+        }
+        return hipGetLastError();
+    }
     dim3 grid(groups + (a.side.active ? 1 : 0), a.nq), block(SCAN_WAVES * 64);
     switch (a.dim) {
     case 128: launch_fixed<METRIC, 128, E>(a, partials, grid, block, s); break;

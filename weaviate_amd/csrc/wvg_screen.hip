@@ -21,10 +21,12 @@
 // per wave from its lists and across workgroups from finished row ranges.
 //
 // K3c.  A workgroup owns 128 queries x one range of 256-row blocks; per
-// 64-deep K stage it stages 16 KiB of query fragments and 32 KiB of row
-// fragments into LDS with global_load_lds (both pre-laid out in HBM in MFMA
-// operand order: 1 KiB = one 16 x 32 bf16 fragment, lane l = item l & 15,
-// k 8 (l >> 4) .. +7), double-buffered, one barrier per stage; 8 waves as
+// 32-deep K stage it stages 8 KiB of query fragments, 16 KiB of row
+// fragments and the block's row norms into LDS with global_load_lds (both
+// operands pre-laid out in HBM in MFMA operand order: 1 KiB = one 16 x 32
+// bf16 fragment, lane l = item l & 15, k 8 (l >> 4) .. +7), a ring of four
+// stage buffers with three stages in flight (counted vmcnt, raw s_barrier:
+// a __syncthreads would drain the DMA), one barrier per stage; 8 waves as
 // 4 (queries) x 2 (rows), each wave a 32 x 128 tile of 16x16x32 bf16 MFMAs.
 // After a row block: u per element, one compare with the query's threshold;
 // the rare survivors enter the wave's per-query list of the SC_M smallest
@@ -43,16 +45,22 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int SC_BQ = 128;                 // queries per workgroup
 constexpr int SC_WAVES = 8;                // 4 (query quarters) x 2 (row halves)
-constexpr int SC_AFR = 16;                 // query fragments per stage (8 groups of 16 x 2 K blocks)
-constexpr int SC_BFR = 32;                 // row fragments per stage (16 groups of 16 x 2 K blocks)
-constexpr int SC_STAGE = (SC_AFR + SC_BFR) * 1024;  // bytes per stage buffer
+constexpr int SC_AFR = 8;                  // query fragments per stage (8 groups of 16, one 32-deep K block)
+constexpr int SC_BFR = 16;                 // row fragments per stage (16 groups of 16)
+constexpr int SC_STAGE = (SC_AFR + SC_BFR + 1) * 1024;  // + the row block's 256 norms
+constexpr int SC_NBUF = 4;                 // stages in LDS: three in flight while one is computed
 constexpr int SC_LISTS = SC_WAVES * 32 * SCREEN_M * 8;
-constexpr int SC_LDS = 2 * SC_STAGE + SC_LISTS + SC_WAVES * 32 * 4 * 2 + SC_BQ * 4 * 3;
+constexpr int SC_LDS = SC_NBUF * SC_STAGE + SC_LISTS + SC_WAVES * 32 * 4 * 2 + SC_BQ * 4 * 3;
 
+// A wave-uniform 64-bit word through the scalar cache (the address is made
+// uniform explicitly: the compiler may hold a uniform index in VGPRs).
 __device__ __forceinline__ uint64_t sc_sload64(const uint64_t *p)
 {
+    const uint64_t a = (uint64_t)p;
+    const uint64_t u = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)) << 32) |
+                       (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
     uint64_t v;
-    asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+    asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(u) : "memory");
     return v;
 }
 
@@ -225,11 +233,43 @@ __device__ __forceinline__ float sc_tau_k(float lower_k, float emax, int cosine)
 
 __device__ __forceinline__ float key_lower(uint64_t key) { return wvg_unord_f32((uint32_t)(key >> 32)); }
 
+// Exact insertion of one survivor (wave-uniform arguments) into a wave's list
+// L of the SCREEN_M smallest (lower, slot) keys of one query, then the
+// query's thresholds: WT (distance space) = min(tau, k-th lower + 2 Emax,
+// M-th lower), WS its u-space form.  Out of line: it runs rarely and is
+// reached from 64 unrolled epilogue sites.
+__device__ __attribute__((noinline)) void sc_insert(uint64_t *L, float *WT, float *WS, float emax, int K, int cosine,
+                                                    float u, uint32_t slot)
+{
+    const int lane = threadIdx.x & 63, M = SCREEN_M;
+    const float lower = sc_lower(u, cosine);
+    if (!(lower <= *WT)) return;
+    const uint64_t key = ((uint64_t)wvg_ord_f32(lower) << 32) | slot;
+    const uint64_t v = lane < M ? L[lane] : WVG_KEY_NONE;
+    const uint64_t last = __shfl(v, M - 1);
+    if (!(key < last)) return;
+    const int pos = __popcll(__ballot(lane < M && v < key));
+    if (lane >= pos && lane < M - 1) L[lane + 1] = v;
+    if (lane == pos) L[pos] = key;
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const uint64_t nk = L[K - 1], nm = L[M - 1];
+    if (lane == 0) {
+        float t = *WT;
+        if (nk != WVG_KEY_NONE) t = fminf(t, sc_tau_k(key_lower(nk), emax, cosine));
+        if (nm != WVG_KEY_NONE) t = fminf(t, key_lower(nm));
+        *WT = t;
+        *WS = sc_sigma(t, cosine);
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
 __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint64_t *lists = reinterpret_cast<uint64_t *>(smem + 2 * SC_STAGE);  // [8][32][M]
-    float *tau = reinterpret_cast<float *>(smem + 2 * SC_STAGE + SC_LISTS);  // [8][32] distance-space threshold
+    uint64_t *lists = reinterpret_cast<uint64_t *>(smem + SC_NBUF * SC_STAGE);  // [8][32][M]
+    float *tau = reinterpret_cast<float *>(smem + SC_NBUF * SC_STAGE + SC_LISTS);  // [8][32] distance-space threshold
     float *sig = tau + SC_WAVES * 32;                                      // [8][32] u-space threshold
     float *ck1 = sig + SC_WAVES * 32;                                      // [128]
     float *ck2 = ck1 + SC_BQ;
@@ -255,7 +295,7 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
     const uint64_t nblk = (ntiles + 3) / 4;  // 256-row blocks
     const uint64_t blk0 = nblk * rr / a.nrr, blk1 = nblk * (rr + 1) / a.nrr;
     const uint32_t q0 = qb * SC_BQ;
-    const uint32_t NK = a.kbn / 2;  // 64-deep stages per row block
+    const uint32_t NK = a.kbn;  // 32-deep stages per row block
 
     // per-query constants and thresholds
     for (int i = tid; i < SC_BQ; i += SC_WAVES * 64) {
@@ -276,22 +316,44 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
     __syncthreads();
     if (blk0 >= blk1) goto publish;
     {
-        // stage loader: wave w moves fragments 6w .. 6w+5 of a stage (A 0..15, B 16..47)
+        // stage loader: wave w moves fragments 3w .. 3w+2 of a stage (A 0..7, B 8..23);
+        // waves 0-3 also one 256-byte quarter of the block's norms (so a wave's
+        // loads per stage: SC_LDW = 4 for waves 0-3, 3 for 4-7)
         auto load_stage = [&](unsigned char *dst, uint64_t blk, uint32_t ks) {
 #pragma unroll
-            for (int j = 0; j < 6; j++) {
-                const int f = 6 * w + j;
+            for (int j = 0; j < 3; j++) {
+                const int f = 3 * w + j;
                 const uint4 *src;
                 if (f < SC_AFR) {
-                    const int kb2 = f >> 3, g = f & 7;
-                    src = a.qfrag + ((size_t)(qb * 8 + g) * a.kbn + 2 * ks + kb2) * 64;
+                    src = a.qfrag + ((size_t)(qb * 8 + f) * a.kbn + ks) * 64;
                 } else {
-                    const int fb = f - SC_AFR, kb2 = fb >> 4, r16 = fb & 15, tt = r16 >> 2, rg = r16 & 3;
+                    const int r16 = f - SC_AFR, tt = r16 >> 2, rg = r16 & 3;
                     const uint64_t t = a.tile_begin + blk * 4 + tt;  // the shadow is padded by 4 tiles
-                    src = a.shadow + (((size_t)t * a.kbn + 2 * ks + kb2) * 4 + rg) * 64;
+                    src = a.shadow + (((size_t)t * a.kbn + ks) * 4 + rg) * 64;
                 }
                 __builtin_amdgcn_global_load_lds(src + lane, reinterpret_cast<uint4 *>(dst + f * 1024), 16, 0, 0);
             }
+            if (w < 4)
+                __builtin_amdgcn_global_load_lds(a.norms + (a.tile_begin + blk * 4 + w) * 64 + lane,
+                                                 reinterpret_cast<float *>(dst + (SC_AFR + SC_BFR) * 1024 + w * 256), 4,
+                                                 0, 0);
+        };
+        // wait until at most `younger` stages' loads of this wave are in flight
+        auto wait_stages = [&](int younger) {
+            if (w < 4) {
+                if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            } else {
+                if (younger >= 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                else if (younger == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        };
+        auto raw_barrier = [&]() {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
         };
         const int qlane = 4 * (lane >> 4);
         uint64_t qlive[2][4];
@@ -303,71 +365,37 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
         uint64_t *WL = lists + (size_t)w * 32 * M;
         float *WT = tau + w * 32, *WS = sig + w * 32;
 
-        // exact list insertion of one survivor (wave-uniform ql, u, slot)
-        auto insert = [&](int ql, float u, uint32_t slot) {
-            const float lower = sc_lower(u, cosine);
-            if (!(lower <= WT[ql])) return;
-            const uint64_t key = ((uint64_t)wvg_ord_f32(lower) << 32) | slot;
-            uint64_t *L = WL + ql * M;
-            const uint64_t v = lane < M ? L[lane] : WVG_KEY_NONE;
-            const uint64_t last = __shfl(v, M - 1);
-            if (!(key < last)) return;
-            const int pos = __popcll(__ballot(lane < M && v < key));
-            if (lane >= pos && lane < M - 1) L[lane + 1] = v;
-            if (lane == pos) L[pos] = key;
-            __builtin_amdgcn_wave_barrier();
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            const uint64_t nk = L[K - 1], nm = L[M - 1];
-            if (lane == 0) {
-                float t = WT[ql];
-                if (nk != WVG_KEY_NONE) t = fminf(t, sc_tau_k(key_lower(nk), cem[32 * wq + ql], cosine));
-                if (nm != WVG_KEY_NONE) t = fminf(t, key_lower(nm));
-                WT[ql] = t;
-                WS[ql] = sc_sigma(t, cosine);
-            }
-            __builtin_amdgcn_wave_barrier();
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        };
-
         floatx4 acc[2][8];
 #pragma unroll
         for (int mq = 0; mq < 2; mq++)
 #pragma unroll
             for (int nr = 0; nr < 8; nr++) acc[mq][nr] = (floatx4){0.f, 0.f, 0.f, 0.f};
-        float nrm[8];
-        uint64_t blk = blk0;
-        uint32_t ks = 0;
-        int cur = 0;
-        load_stage(smem, blk, 0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        for (;;) {
-            // next stage in flight while this one is computed
-            uint64_t nblk_ = blk;
-            uint32_t nks = ks + 1;
-            if (nks == NK) {
-                nks = 0;
-                nblk_ = blk + 1;
+        // the (row block, stage) units of the range form one stream: unit u in
+        // buffer u % 4, loaded three units ahead
+        const uint64_t U = (blk1 - blk0) * NK;
+        uint64_t lblk = blk0, blk = blk0;  // load cursor (three units ahead), compute cursor
+        uint32_t lks = 0, ks = 0;
+        auto unit_load = [&](uint64_t u) {
+            load_stage(smem + (u & (SC_NBUF - 1)) * SC_STAGE, lblk, lks);
+            if (++lks == NK) {
+                lks = 0;
+                ++lblk;
             }
-            const bool more = nblk_ < blk1;
-            if (more) load_stage(smem + (cur ^ 1) * SC_STAGE, nblk_, nks);
-            if (ks == 0) {
-#pragma unroll
-                for (int nr = 0; nr < 8; nr++) {
-                    const uint64_t slot = (a.tile_begin + blk * 4 + 2 * wr + (nr >> 2)) * 64 + 16 * (nr & 3) + (lane & 15);
-                    nrm[nr] = a.norms[slot];
-                }
-            }
-            const unsigned char *sb = smem + cur * SC_STAGE;
-#pragma unroll
-            for (int kb2 = 0; kb2 < 2; kb2++) {
+        };
+        for (uint64_t u = 0; u < 3 && u < U; u++) unit_load(u);
+        wait_stages(U >= 3 ? 2 : (int)U - 1);
+        raw_barrier();
+        for (uint64_t u = 0;; u++) {
+            if (u + 3 < U) unit_load(u + 3);  // buffer (u + 3) % 4 was last read in unit u - 1
+            const unsigned char *sb = smem + (u & (SC_NBUF - 1)) * SC_STAGE;
+            {
                 bf16x8 av[2], bv[8];
 #pragma unroll
                 for (int mq = 0; mq < 2; mq++)
-                    av[mq] = *reinterpret_cast<const bf16x8 *>(sb + (kb2 * 8 + 2 * wq + mq) * 1024 + lane * 16);
+                    av[mq] = *reinterpret_cast<const bf16x8 *>(sb + (2 * wq + mq) * 1024 + lane * 16);
 #pragma unroll
                 for (int nr = 0; nr < 8; nr++)
-                    bv[nr] = *reinterpret_cast<const bf16x8 *>(sb + (SC_AFR + kb2 * 16 + 8 * wr + nr) * 1024 + lane * 16);
+                    bv[nr] = *reinterpret_cast<const bf16x8 *>(sb + (SC_AFR + 8 * wr + nr) * 1024 + lane * 16);
 #pragma unroll
                 for (int mq = 0; mq < 2; mq++)
 #pragma unroll
@@ -376,6 +404,10 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
             }
             if (ks == NK - 1) {
                 // epilogue of row block blk: C layout row (query) qlane + r, column (row) lane & 15
+                float nrm[8];
+                const float *nrs = reinterpret_cast<const float *>(sb + (SC_AFR + SC_BFR) * 1024);
+#pragma unroll
+                for (int nr = 0; nr < 8; nr++) nrm[nr] = nrs[(2 * wr + (nr >> 2)) * 64 + 16 * (nr & 3) + (lane & 15)];
                 uint64_t vm[2];
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
@@ -410,7 +442,7 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
                                 const float us = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(u), src));
                                 const uint32_t slot = (uint32_t)((a.tile_begin + blk * 4) * 64 + 128 * wr + 16 * nr +
                                                                  (src & 15));
-                                insert(ql, us, slot);
+                                sc_insert(WL + ql * M, WT + ql, WS + ql, cem[32 * wq + ql], K, cosine, us, slot);
                             }
                         }
                     }
@@ -420,12 +452,14 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
 #pragma unroll
                     for (int nr = 0; nr < 8; nr++) acc[mq][nr] = (floatx4){0.f, 0.f, 0.f, 0.f};
             }
-            if (!more) break;
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            blk = nblk_;
-            ks = nks;
-            cur ^= 1;
+            if (u + 1 >= U) break;
+            if (++ks == NK) {
+                ks = 0;
+                ++blk;
+            }
+            // unit u + 1 landed (its loads are the oldest in flight), then everyone's
+            wait_stages(u + 3 < U ? 2 : (u + 2 < U ? 1 : 0));
+            raw_barrier();
         }
     }
 publish:
