@@ -347,7 +347,7 @@ def test_cosched_batches_equal_single_queries(ctx, orc, kind):
     if kind == KIND_PQ:
         centers = orc.synth_rows(601, 0, 32 * 256, d // 32, 0).reshape(32, 256, d // 32)
         c.set_codebook(centers)
-    else:
+    elif kind == KIND_BQ:
         f = Corpus(ctx, KIND_F32, METRIC_L2, d, n)
         f.upsert(np.arange(n, dtype=np.uint64), rows)
     c.upsert(np.arange(n, dtype=np.uint64), rows)
