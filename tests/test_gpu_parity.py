@@ -367,7 +367,8 @@ def _codebook(orc, m, ks, ds, seed):
     return orc.synth_rows(seed, 0, m * ks, ds, 0).reshape(m, ks, ds)
 
 
-@pytest.mark.parametrize("m,ks,d", [(32, 256, 128), (8, 16, 24), (16, 256, 256)])
+@pytest.mark.parametrize("m,ks,d", [(32, 256, 128), (8, 16, 24), (16, 256, 256), (32, 16, 128), (32, 24, 128),
+                                     (16, 6, 64)])
 def test_pq_encode_lut_adc_bitexact(ctx, orc, m, ks, d):
     from weaviate_amd.compressionhelpers import ProductQuantizer
 
@@ -425,9 +426,12 @@ def test_pq_encode_argmin_ties_and_nonfinite(ctx, orc):
     centers[:, 9] = centers[:, 8]      # a tie inside pair 4
     centers[:, 201] = centers[:, 8]    # ... and with a later pair
     centers[:, 130] = centers[:, 131]  # a tie inside pair 65 only
+    centers[:, 16] = centers[:, 15]    # ties across the first two 16-centroid argmin groups
+    centers[:, 30] = centers[:, 15]    # ... and inside the second group (30 wins)
     X = orc.synth_rows(911, 0, 700, d, 0)
     X[:4] = centers[np.arange(m)[None, :], np.array([[8] * m] * 4)].reshape(4, d)   # d = 0 at 8, 9, 201
     X[4:8] = centers[np.arange(m)[None, :], np.array([[131] * m] * 4)].reshape(4, d)  # d = 0 at 130, 131
+    X[11:14] = centers[np.arange(m)[None, :], np.array([[15] * m] * 3)].reshape(3, d)  # d = 0 at 15, 16, 30
     X[8, 5] = np.nan                   # segment 1 of row 8: NaN distances
     X[70, 127] = np.nan                # a NaN in the second wave of the batch
     X[9, 12:16] = np.float32(3e38)     # segment 3: every distance overflows to +inf

@@ -130,6 +130,8 @@ typedef float f32x2e __attribute__((ext_vector_type(2)));
 // centroid (centroid - row with finite centroids is never NaN: x = +-inf gives
 // +inf); `nan_free` says the codebook has none, and a wave whose segment has a
 // NaN takes the reference loop.
+constexpr int PQ_ENC_GROUP = 8;  // pairs per argmin group (16 centroids)
+
 template <int DS, bool TILED_OUT>
 __global__ void pq_encode_kernel(const float4 *__restrict__ tiled, uint64_t n, uint32_t dim, uint32_t nchunks,
                                  const float *__restrict__ centers, uint32_t m, uint32_t ks, uint32_t ds_rt,
@@ -167,22 +169,61 @@ __global__ void pq_encode_kernel(const float4 *__restrict__ tiled, uint64_t n, u
                         return sum;
                     };
                     float mn = minD;
-                    uint32_t bp = 0;
+                    if ((ks & (2 * PQ_ENC_GROUP - 1)) == 0) {
+                        // groups of PQ_ENC_GROUP pairs: the group's minimum by a
+                        // v_min3 chain, then ONE compare + select per group for
+                        // the last group holding the running minimum (group min
+                        // <= the minimum before it, ties included: later wins);
+                        // the winner inside it is found once at the end
+                        uint32_t bg = 0;
+                        for (uint32_t g = 0; g < ks / (2 * PQ_ENC_GROUP); g++) {
+                            float sx[2 * PQ_ENC_GROUP];
+#pragma unroll
+                            for (int j = 0; j < PQ_ENC_GROUP; j++) {
+                                const __attribute__((address_space(4))) float *pp =
+                                    cp + ((size_t)g * PQ_ENC_GROUP + j) * 8;
+                                const f32x2e d0 = f32x2e{pp[0], pp[1]} - xx, d1 = f32x2e{pp[2], pp[3]} - xy;
+                                const f32x2e d2 = f32x2e{pp[4], pp[5]} - xz, d3 = f32x2e{pp[6], pp[7]} - xw;
+                                f32x2e sum = d0 * d0;
+                                sum = sum + d1 * d1;
+                                sum = sum + d2 * d2;
+                                sum = sum + d3 * d3;
+                                sx[2 * j] = sum.x;
+                                sx[2 * j + 1] = sum.y;
+                            }
+                            float gm = __builtin_fminf(sx[0], sx[1]);
+#pragma unroll
+                            for (int j = 2; j < 2 * PQ_ENC_GROUP; j += 2)
+                                gm = __builtin_fminf(__builtin_fminf(gm, sx[j]), sx[j + 1]);
+                            if (gm <= mn) bg = g;
+                            mn = __builtin_fminf(mn, gm);
+                        }
+                        best = 0;  // when nothing reached math.MaxFloat32
+#pragma unroll
+                        for (int j = 0; j < PQ_ENC_GROUP; j++) {
+                            const uint32_t p = bg * PQ_ENC_GROUP + j;
+                            const f32x2e sb = pair_sum(pairs + ((size_t)s * ks + 2 * p) * 4);
+                            if (sb.x == mn) best = 2 * p;
+                            if (sb.y == mn) best = 2 * p + 1;
+                        }
+                    } else {
+                        uint32_t bp = 0;
 #pragma unroll 4
-                    for (uint32_t p = 0; p < ks / 2; p++) {
-                        const __attribute__((address_space(4))) float *pp = cp + (size_t)p * 8;
-                        const f32x2e d0 = f32x2e{pp[0], pp[1]} - xx, d1 = f32x2e{pp[2], pp[3]} - xy;
-                        const f32x2e d2 = f32x2e{pp[4], pp[5]} - xz, d3 = f32x2e{pp[6], pp[7]} - xw;
-                        f32x2e sum = d0 * d0;
-                        sum = sum + d1 * d1;
-                        sum = sum + d2 * d2;
-                        sum = sum + d3 * d3;
-                        const float m2 = __builtin_fminf(__builtin_fminf(mn, sum.x), sum.y);
-                        if ((sum.x == m2) | (sum.y == m2)) bp = p;
-                        mn = m2;
+                        for (uint32_t p = 0; p < ks / 2; p++) {
+                            const __attribute__((address_space(4))) float *pp = cp + (size_t)p * 8;
+                            const f32x2e d0 = f32x2e{pp[0], pp[1]} - xx, d1 = f32x2e{pp[2], pp[3]} - xy;
+                            const f32x2e d2 = f32x2e{pp[4], pp[5]} - xz, d3 = f32x2e{pp[6], pp[7]} - xw;
+                            f32x2e sum = d0 * d0;
+                            sum = sum + d1 * d1;
+                            sum = sum + d2 * d2;
+                            sum = sum + d3 * d3;
+                            const float m2 = __builtin_fminf(__builtin_fminf(mn, sum.x), sum.y);
+                            if ((sum.x == m2) | (sum.y == m2)) bp = p;
+                            mn = m2;
+                        }
+                        const f32x2e sb = pair_sum(pairs + ((size_t)s * ks + 2 * bp) * 4);
+                        best = sb.y == mn ? 2 * bp + 1 : 2 * bp;  // 0 when nothing beat math.MaxFloat32
                     }
-                    const f32x2e sb = pair_sum(pairs + ((size_t)s * ks + 2 * bp) * 4);
-                    best = sb.y == mn ? 2 * bp + 1 : 2 * bp;  // 0 when nothing beat math.MaxFloat32
                     minD = mn;
                 } else if (pairs) {
                     // two centroids per packed op: (c_k - x_k)^2 summed in k order,

@@ -319,24 +319,42 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
         // stage loader: wave w moves fragments 3w .. 3w+2 of a stage (A 0..7, B 8..23);
         // waves 0-3 also one 256-byte quarter of the block's norms (so a wave's
         // loads per stage: SC_LDW = 4 for waves 0-3, 3 for 4-7)
-        auto load_stage = [&](unsigned char *dst, uint64_t blk, uint32_t ks) {
+        // Per-lane source pointers of this wave's three fragments at stage 0 of
+        // the load cursor's row block: a stage adds one K block (A: 1 KiB,
+        // B: 4 KiB), a row block four tiles of B (the shadow is padded by 4
+        // tiles); the norms pointer moves by a row block.
+        const uint4 *lsrc[3];
+        uint32_t lstep[3];
+        uint64_t lblkstep[3];
 #pragma unroll
-            for (int j = 0; j < 3; j++) {
-                const int f = 3 * w + j;
-                const uint4 *src;
-                if (f < SC_AFR) {
-                    src = a.qfrag + ((size_t)(qb * 8 + f) * a.kbn + ks) * 64;
-                } else {
-                    const int r16 = f - SC_AFR, tt = r16 >> 2, rg = r16 & 3;
-                    const uint64_t t = a.tile_begin + blk * 4 + tt;  // the shadow is padded by 4 tiles
-                    src = a.shadow + (((size_t)t * a.kbn + ks) * 4 + rg) * 64;
-                }
-                __builtin_amdgcn_global_load_lds(src + lane, reinterpret_cast<uint4 *>(dst + f * 1024), 16, 0, 0);
+        for (int j = 0; j < 3; j++) {
+            const int f = 3 * w + j;
+            if (f < SC_AFR) {
+                lsrc[j] = a.qfrag + (size_t)(qb * 8 + f) * a.kbn * 64 + lane;
+                lstep[j] = 64;
+                lblkstep[j] = 0;
+            } else {
+                const int r16 = f - SC_AFR, tt = r16 >> 2, rg = r16 & 3;
+                const uint64_t t = a.tile_begin + blk0 * 4 + tt;
+                lsrc[j] = a.shadow + ((size_t)t * a.kbn * 4 + rg) * 64 + lane;
+                lstep[j] = 256;
+                lblkstep[j] = (uint64_t)4 * a.kbn * 256;
             }
+        }
+        const float *lnorm = a.norms + (a.tile_begin + blk0 * 4 + (w & 3)) * 64 + lane;
+        auto load_stage = [&](unsigned char *dst, uint32_t ks) {
+#pragma unroll
+            for (int j = 0; j < 3; j++)
+                __builtin_amdgcn_global_load_lds(lsrc[j] + (size_t)ks * lstep[j],
+                                                 reinterpret_cast<uint4 *>(dst + (3 * w + j) * 1024), 16, 0, 0);
             if (w < 4)
-                __builtin_amdgcn_global_load_lds(a.norms + (a.tile_begin + blk * 4 + w) * 64 + lane,
-                                                 reinterpret_cast<float *>(dst + (SC_AFR + SC_BFR) * 1024 + w * 256), 4,
-                                                 0, 0);
+                __builtin_amdgcn_global_load_lds(lnorm, reinterpret_cast<float *>(dst + (SC_AFR + SC_BFR) * 1024 + w * 256),
+                                                 4, 0, 0);
+        };
+        auto next_block = [&]() {  // the load cursor moves to the next row block
+#pragma unroll
+            for (int j = 0; j < 3; j++) lsrc[j] += lblkstep[j];
+            lnorm += 256;
         };
         // wait until at most `younger` stages' loads of this wave are in flight
         auto wait_stages = [&](int younger) {
@@ -376,10 +394,11 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
         uint64_t lblk = blk0, blk = blk0;  // load cursor (three units ahead), compute cursor
         uint32_t lks = 0, ks = 0;
         auto unit_load = [&](uint64_t u) {
-            load_stage(smem + (u & (SC_NBUF - 1)) * SC_STAGE, lblk, lks);
+            load_stage(smem + (u & (SC_NBUF - 1)) * SC_STAGE, lks);
             if (++lks == NK) {
                 lks = 0;
                 ++lblk;
+                next_block();
             }
         };
         for (uint64_t u = 0; u < 3 && u < U; u++) unit_load(u);
@@ -404,10 +423,27 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
             }
             if (ks == NK - 1) {
                 // epilogue of row block blk: C layout row (query) qlane + r, column (row) lane & 15
+                // The epilogue's LDS reads go through inline asm: the compiler's
+                // wait pass cannot tell them from reads of an in-flight LDS DMA
+                // buffer and would drain the whole prefetch (vmcnt(0)) first.
+                // None of them touches a buffer with a DMA in flight (the norms
+                // sit in this unit's buffer, which landed before the barrier).
                 float nrm[8];
-                const float *nrs = reinterpret_cast<const float *>(sb + (SC_AFR + SC_BFR) * 1024);
-#pragma unroll
-                for (int nr = 0; nr < 8; nr++) nrm[nr] = nrs[(2 * wr + (nr >> 2)) * 64 + 16 * (nr & 3) + (lane & 15)];
+                const uint32_t nrs = (uint32_t)(uintptr_t)(sb + (SC_AFR + SC_BFR) * 1024) +
+                                     4u * (uint32_t)((2 * wr) * 64 + (lane & 15));
+                asm volatile("ds_read_b32 %0, %8\n\t"
+                             "ds_read_b32 %1, %8 offset:64\n\t"
+                             "ds_read_b32 %2, %8 offset:128\n\t"
+                             "ds_read_b32 %3, %8 offset:192\n\t"
+                             "ds_read_b32 %4, %8 offset:256\n\t"
+                             "ds_read_b32 %5, %8 offset:320\n\t"
+                             "ds_read_b32 %6, %8 offset:384\n\t"
+                             "ds_read_b32 %7, %8 offset:448\n\t"
+                             "s_waitcnt lgkmcnt(0)"
+                             : "=v"(nrm[0]), "=v"(nrm[1]), "=v"(nrm[2]), "=v"(nrm[3]), "=v"(nrm[4]), "=v"(nrm[5]),
+                               "=v"(nrm[6]), "=v"(nrm[7])
+                             : "v"(nrs)
+                             : "memory");
                 uint64_t vm[2];
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
@@ -421,9 +457,16 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
                 }
 #pragma unroll
                 for (int mq = 0; mq < 2; mq++) {
-                    const float4 k1v = *reinterpret_cast<const float4 *>(ck1 + 32 * wq + 16 * mq + qlane);
-                    const float4 k2v = *reinterpret_cast<const float4 *>(ck2 + 32 * wq + 16 * mq + qlane);
-                    const float4 sv = *reinterpret_cast<const float4 *>(WS + 16 * mq + qlane);
+                    float4 k1v, k2v, sv;
+                    asm volatile("ds_read_b128 %0, %3\n\t"
+                                 "ds_read_b128 %1, %4\n\t"
+                                 "ds_read_b128 %2, %5\n\t"
+                                 "s_waitcnt lgkmcnt(0)"
+                                 : "=v"(k1v), "=v"(k2v), "=v"(sv)
+                                 : "v"((uint32_t)(uintptr_t)(ck1 + 32 * wq + 16 * mq + qlane)),
+                                   "v"((uint32_t)(uintptr_t)(ck2 + 32 * wq + 16 * mq + qlane)),
+                                   "v"((uint32_t)(uintptr_t)(WS + 16 * mq + qlane))
+                                 : "memory");
                     const float k1r[4] = {k1v.x, k1v.y, k1v.z, k1v.w};
                     const float k2r[4] = {k2v.x, k2v.y, k2v.z, k2v.w};
                     const float svr[4] = {sv.x, sv.y, sv.z, sv.w};
