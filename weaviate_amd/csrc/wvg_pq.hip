@@ -130,7 +130,7 @@ typedef float f32x2e __attribute__((ext_vector_type(2)));
 // centroid (centroid - row with finite centroids is never NaN: x = +-inf gives
 // +inf); `nan_free` says the codebook has none, and a wave whose segment has a
 // NaN takes the reference loop.
-constexpr int PQ_ENC_GROUP = 8;  // pairs per argmin group (16 centroids)
+constexpr int PQ_ENC_GROUP = 4;  // pairs per argmin group (8 centroids: 32 SGPRs of centroids)
 
 template <int DS, bool TILED_OUT>
 __global__ void pq_encode_kernel(const float4 *__restrict__ tiled, uint64_t n, uint32_t dim, uint32_t nchunks,
@@ -177,7 +177,7 @@ __global__ void pq_encode_kernel(const float4 *__restrict__ tiled, uint64_t n, u
                         // the winner inside it is found once at the end
                         uint32_t bg = 0;
                         for (uint32_t g = 0; g < ks / (2 * PQ_ENC_GROUP); g++) {
-                            float sx[2 * PQ_ENC_GROUP];
+                            float gm = 0.0f;
 #pragma unroll
                             for (int j = 0; j < PQ_ENC_GROUP; j++) {
                                 const __attribute__((address_space(4))) float *pp =
@@ -188,19 +188,16 @@ __global__ void pq_encode_kernel(const float4 *__restrict__ tiled, uint64_t n, u
                                 sum = sum + d1 * d1;
                                 sum = sum + d2 * d2;
                                 sum = sum + d3 * d3;
-                                sx[2 * j] = sum.x;
-                                sx[2 * j + 1] = sum.y;
+                                gm = j == 0 ? __builtin_fminf(sum.x, sum.y)
+                                            : __builtin_fminf(__builtin_fminf(gm, sum.x), sum.y);
                             }
-                            float gm = __builtin_fminf(sx[0], sx[1]);
-#pragma unroll
-                            for (int j = 2; j < 2 * PQ_ENC_GROUP; j += 2)
-                                gm = __builtin_fminf(__builtin_fminf(gm, sx[j]), sx[j + 1]);
-                            if (gm <= mn) bg = g;
-                            mn = __builtin_fminf(mn, gm);
+                            const bool miss = gm > mn;  // (NaN-free here; ties go to the later group)
+                            bg = miss ? bg : g;
+                            mn = miss ? mn : gm;
                         }
                         best = 0;  // when nothing reached math.MaxFloat32
-#pragma unroll
-                        for (int j = 0; j < PQ_ENC_GROUP; j++) {
+#pragma unroll 1
+                        for (int j = 0; j < PQ_ENC_GROUP; j++) {  // (per-lane group: vector loads, one pair at a time)
                             const uint32_t p = bg * PQ_ENC_GROUP + j;
                             const f32x2e sb = pair_sum(pairs + ((size_t)s * ks + 2 * p) * 4);
                             if (sb.x == mn) best = 2 * p;
