@@ -119,7 +119,7 @@ def _sized(run_fn, per_query_probe: int, target_s: float, threads: int, cap: int
     return int(max(threads, min(cap, target_s * threads / per_q)))
 
 
-def cpu_baseline(rows_n, d, k, gpu_ids, target_s):
+def cpu_baseline(rows_n, d, k, gpu_ids, target_s, pq_check=None):
     """Weaviate's CPU flat path (findTopVectors: l2_256 + bounded max-heap,
     V/flat/index.go:411-452) and BQ path (findTopVectorsCached Hamming top-200
     + exact rescore, :347-389, 456-495) over the same 1M x 128 rows, with the
@@ -159,6 +159,7 @@ def cpu_baseline(rows_n, d, k, gpu_ids, target_s):
     secs_b1 = bq(nb1, 1)
     kernel = "l2_256 compiled from the reference's C source (oracle/_ref)" if used_ref else \
         "oracle restatement of l2_256"
+    pq = cpu_pq_leg(target_s, threads, pq_check)
     return {
         "value": round(nq / secs, 3),
         "unit": "queries/s",
@@ -179,6 +180,57 @@ def cpu_baseline(rows_n, d, k, gpu_ids, target_s):
                        f"rescore of {R} rows, top-{k}; V/flat/index.go:347-389) over the same rows, "
                        f"{secs_b:.1f} s wall on {threads} threads"),
         },
+        "pq": pq,
+    }
+
+
+PQ_CPU_ROWS = 10_000_000  # codes in the CPU PQ leg (320 MB at m = 32)
+
+
+def pq_leg_data(n=PQ_CPU_ROWS, d=128, m=32, ks=256):
+    """Synthetic PQ corpus of the configs[3] code shape: uniform random codes
+    (seed 44), a synthetic codebook (counter RNG seed 45) and 64 queries."""
+    codes = np.random.default_rng(44).integers(0, ks, (n, m), dtype=np.uint8)
+    from oracle import wv_oracle as orc
+
+    centers = orc.synth_rows(45, 0, m * ks, d // m, 0).reshape(m, ks, d // m)
+    qs = np.random.default_rng(46).uniform(-1, 1, (64, d)).astype(np.float32)
+    return codes, centers, qs
+
+
+def cpu_pq_leg(target_s, threads, gpu_check):
+    """BASELINE configs[3]'s CPU reference point: PQ ADC top-10 (the
+    distancer's LUT, CH/product_quantization.go:85-104, sequential ADC sum +
+    Wrap :352-361, flat heap) over PQ_CPU_ROWS m = 32 codes, one query per
+    thread, restated in C (oracle/wv_oracle.c orc_bench_pq: the reference's
+    PQ path is pure Go, so there is no compiled reference kernel).  The rate
+    per 100M codes (configs[3]'s size) is the measured rate x rows / 1e8.
+    `gpu_check(codes, centers, qs, k)` returns the GPU's ids for the same
+    queries (K8e through the host API) for an ids cross-check."""
+    from oracle import wv_oracle as orc
+
+    codes, centers, qs = pq_leg_data()
+    n, k = len(codes), 10
+    nq = _sized(lambda q, th: orc.bench_pq(codes, centers, qs[:q], k, orc.L2, th)[0], 2, target_s, threads, 4096)
+    qq = np.resize(qs, (nq, qs.shape[1]))
+    secs, ids, _ = orc.bench_pq(codes, centers, qq, k, orc.L2, threads)
+    n1 = min(nq, max(2, int(nq / threads / 4)))
+    secs1 = orc.bench_pq(codes, centers, qq[:n1], k, orc.L2, 1)[0]
+    match = None
+    if gpu_check is not None:
+        gids = gpu_check(codes, centers, qs[:4], k)
+        match = bool(np.array_equal(ids[:4], gids))
+    return {
+        "value": round(nq / secs, 3),
+        "unit": "queries/s",
+        "cores": threads,
+        "kind": "port",
+        "single_core_qps": round(n1 / secs1, 3),
+        "qps_per_100M_codes": round(nq / secs * n / 1e8, 3),
+        "ids_match_gpu": match,
+        "sample": (f"{nq} PQ ADC top-{k} queries over {n:,} synthetic m=32 x ks=256 codes (configs[3] code shape; "
+                   f"LUT + sequential ADC + heap restated in C, oracle/wv_oracle.c orc_bench_pq), {secs:.1f} s wall "
+                   f"on {threads} threads"),
     }
 
 
@@ -393,7 +445,18 @@ def run_flat1m(args, world, rank, dev, torch, dist):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cq = np.random.default_rng(43).uniform(-1, 1, (16, d)).astype(np.float32)
         gids, _, _ = corpus.search(cq, k)  # GPU results of the baseline's first queries (full-size cross-check)
-        out["cpu_baseline"] = cpu_baseline(n, d, k, gids, args.cpu_seconds)
+
+        def pq_check(codes, centers, pqs, kk):  # the same PQ queries on the GPU (K8e via wvg_search)
+            from weaviate_amd._lib import KIND_PQ
+            pc = Corpus(ctx, KIND_PQ, METRIC_L2, d, len(codes))
+            try:
+                pc.set_codebook(centers)
+                pc.upsert_codes(np.arange(len(codes), dtype=np.uint64), codes)
+                return pc.search(pqs, kk)[0]
+            finally:
+                pc.destroy()
+
+        out["cpu_baseline"] = cpu_baseline(n, d, k, gids, args.cpu_seconds, pq_check)
     corpus.destroy()
     ctx.close()
     return out

@@ -278,9 +278,11 @@ int wvg_synthetic_rows(wvg_ctx *ctx, uint64_t seed, const uint64_t *ids, uint64_
 int wvg_profile_start(wvg_ctx *ctx);
 int wvg_profile_stop(wvg_ctx *ctx, double *scan_ms_total, uint64_t *scan_launches);
 /* Measurement helper: the HBM streaming-read rate of this GPU, in GB/s -- the
- * best of grid-stride 16-byte non-temporal reads of a `bytes` buffer (its
- * own allocation, freed again) over 1024..8192 workgroups, `reps` passes
- * each.  The ceiling the HBM-bound scans are compared with (roofline).    */
+ * best of 16-byte non-temporal reads of a `bytes` buffer (its own
+ * allocation, freed again) in two shapes -- grid-stride over 1024..8192
+ * workgroups, and the scans' contiguous chunk per workgroup (8 KiB per wave
+ * per step) over 256..2048 workgroups -- `reps` passes each.  The ceiling
+ * the HBM-bound scans are compared with (roofline).                       */
 int wvg_measure_hbm_read(wvg_ctx *ctx, uint64_t bytes, uint32_t reps, double *out_gbps);
 
 /* ---- bulk primitives (distancer.BatchProvider / compressionhelpers bulk) --- */

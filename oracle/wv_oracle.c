@@ -803,6 +803,65 @@ ORC_API double orc_bench_flat_bq(const float *rows, const uint64_t *codes, long 
     return run_jobs(p, nq, threads);
 }
 
+/* PQ ADC top-k over a code matrix [n][m] for one query: the distancer's
+ * LookUp table (CH/product_quantization.go:85-104, filled eagerly -- the
+ * same values as the lazy fill), one ADC sum per row + Wrap (:352-361) in
+ * ascending id order, insertToHeap(k), extractHeap (V/flat/index.go:441-452).
+ * `lut` is caller scratch of m*ks floats.  Returns count. */
+ORC_API long orc_pq_search(const uint8_t *codes, long n, long m, long ks, long ds, const float *centers,
+                           const float *q, long k, int metric, float *lut, uint64_t *out_ids, float *out_dists)
+{
+    if (k <= 0) return 0;
+    orc_pq_lut(metric, q, centers, m, ks, ds, lut);
+    orc_heap h = { (orc_item *)malloc(sizeof(orc_item) * (size_t)(k + 1)), 0 };
+    for (long i = 0; i < n; i++) insert_to_heap(&h, k, (uint64_t)i, orc_pq_adc(metric, lut, codes + i * m, m, ks));
+    long cnt = extract_heap(&h, out_ids, out_dists);
+    free(h.items);
+    return cnt;
+}
+
+typedef struct {
+    const uint8_t *codes; long n, m, ks, ds; const float *centers, *qs; long d, k; int metric;
+    long q0, q1; uint64_t *out_ids; float *out_dists;
+} orc_pq_job;
+
+static void *orc_pq_worker(void *arg)
+{
+    orc_pq_job *j = (orc_pq_job *)arg;
+    float *lut = (float *)malloc(sizeof(float) * (size_t)(j->m * j->ks));
+    for (long q = j->q0; q < j->q1; q++)
+        orc_pq_search(j->codes, j->n, j->m, j->ks, j->ds, j->centers, j->qs + q * j->d, j->k, j->metric, lut,
+                      j->out_ids + q * j->k, j->out_dists + q * j->k);
+    free(lut);
+    return NULL;
+}
+
+/* Runs nq PQ ADC searches (orc_pq_search) on `threads` threads, one query per
+ * thread at a time; returns wall seconds (the CPU leg of BASELINE configs[3]). */
+ORC_API double orc_bench_pq(const uint8_t *codes, long n, long m, long ks, long ds, const float *centers,
+                            const float *qs, long nq, long k, int metric, int threads, uint64_t *out_ids,
+                            float *out_dists)
+{
+    if (threads < 1) threads = 1;
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)threads);
+    orc_pq_job *jobs = (orc_pq_job *)malloc(sizeof(orc_pq_job) * (size_t)threads);
+    long split = (nq + threads - 1) / threads;
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int t = 0; t < threads; t++) {
+        long q0 = t * split, q1 = q0 + split;
+        if (q1 > nq) q1 = nq;
+        if (q0 > nq) q0 = nq;
+        orc_pq_job p = { codes, n, m, ks, ds, centers, qs, m * ds, k, metric, q0, q1, out_ids, out_dists };
+        jobs[t] = p;
+        pthread_create(&th[t], NULL, orc_pq_worker, &jobs[t]);
+    }
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    free(th); free(jobs);
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
 /* BinaryQuantizer.Encode of n rows into codes [n][ceil(d/64)] (test helper). */
 ORC_API void orc_bq_encode_rows(const float *rows, long n, long d, uint64_t *codes)
 {

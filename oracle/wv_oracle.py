@@ -83,6 +83,11 @@ def lib():
         l.orc_bench_flat_bq.argtypes = [_F, _U64, c_long, c_long, c_long, _F, c_long, c_long, c_long, c_int, c_void_p,
                                         c_int, _U64, _F]
         l.orc_bq_encode_rows.argtypes = [_F, c_long, c_long, _U64]
+        l.orc_pq_search.restype = c_long
+        l.orc_pq_search.argtypes = [_U8, c_long, c_long, c_long, c_long, _F, _F, c_long, c_int, _F, _U64, _F]
+        l.orc_bench_pq.restype = c_double
+        l.orc_bench_pq.argtypes = [_U8, c_long, c_long, c_long, c_long, _F, _F, c_long, c_long, c_int, c_int, _U64,
+                                   _F]
         _lib = l
     return _lib
 
@@ -336,6 +341,35 @@ def bench_flat_bq(rows, codes, qs, k, rescore_limit, metric, threads, use_ref_ke
     secs = lib().orc_bench_flat_bq(_f(rows), _u64(codes), n, d, d, _f(qs), nq, k, rescore_limit, metric, fn, threads,
                                    _u64(oid), _f(od))
     return secs, oid, od, fn is not None
+
+
+def pq_search(codes, centers, q, k, metric):
+    """PQ ADC top-k of one query over codes [n][m] (LUT + sequential ADC sums +
+    flat heap; CH/product_quantization.go:85-104,352-361)."""
+    codes = np.ascontiguousarray(codes, dtype=np.uint8)
+    centers, q = f32(centers), f32(q)
+    n, m = codes.shape
+    _, ks, ds = centers.shape
+    lut = np.empty(m * ks, dtype=np.float32)
+    oid = np.empty(max(k, 1), dtype=np.uint64)
+    od = np.empty(max(k, 1), dtype=np.float32)
+    cnt = lib().orc_pq_search(_u8(codes), n, m, ks, ds, _f(centers), _f(q), k, metric, _f(lut), _u64(oid), _f(od))
+    return oid[:cnt], od[:cnt]
+
+
+def bench_pq(codes, centers, qs, k, metric, threads):
+    """Times nq PQ ADC searches, one query per thread at a time; returns
+    (seconds, ids [nq][k], dists [nq][k])."""
+    codes = np.ascontiguousarray(codes, dtype=np.uint8)
+    centers, qs = f32(centers), f32(qs)
+    n, m = codes.shape
+    _, ks, ds = centers.shape
+    nq = qs.shape[0]
+    oid = np.empty((nq, k), dtype=np.uint64)
+    od = np.empty((nq, k), dtype=np.float32)
+    secs = lib().orc_bench_pq(_u8(codes), n, m, ks, ds, _f(centers), _f(qs), nq, k, metric, threads, _u64(oid),
+                              _f(od))
+    return secs, oid, od
 
 
 def ord_key(dists):

@@ -23,7 +23,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n, d, k, nq, dead, pipelined, side, out):
+def _worker(rank, world, port, n, d, k, nq, dead, pipelined, side, out, backend="gloo"):
     import sys
 
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -37,7 +37,10 @@ def _worker(rank, world, port, n, d, k, nq, dead, pipelined, side, out):
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":  # RCCL: the device all-gather of the product path (one rank per GPU)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         lo, cnt, per = shard_range(n, world, rank)
         ctx = Context(0)
@@ -77,12 +80,26 @@ def _worker(rank, world, port, n, d, k, nq, dead, pipelined, side, out):
                                              (50, True, False), (20_000 + 37, False, True), (20_000 + 37, True, True)])
 def test_two_ranks_packed_allgather_device_merge(orc, n, pipelined, side):
     """n = 50: rank 1's slab is empty (empty results from the device path)."""
-    world, d, k, nq = 2, 64, 10, 5
+    _run_sharded(orc, 2, n, pipelined, side, "gloo")
+
+
+@pytest.mark.parametrize("pipelined,side", [(False, False), (True, True)])
+def test_rccl_group_of_one_packed_allgather(orc, pipelined, side):
+    """The nccl (RCCL) backend on the box's one GPU: a process group of one
+    rank still takes the exchange path (ShardedFlatIndex exchanges whenever a
+    group is initialised), so the device all-gather of the packed block over
+    RCCL and wvg_topk_merge_packed run on hardware -- with torch's current
+    stream and with a caller side stream -- and equal the oracle."""
+    _run_sharded(orc, 1, 20_000 + 37, pipelined, side, "nccl")
+
+
+def _run_sharded(orc, world, n, pipelined, side, backend):
+    d, k, nq = 64, 10, 5
     dead = [0, 3, 777, 10_111, 20_036]
     ctxm = mp.get_context("spawn")
     q = ctxm.Queue()
     port = _free_port()
-    procs = [ctxm.Process(target=_worker, args=(r, world, port, n, d, k, nq, dead, pipelined, side, q))
+    procs = [ctxm.Process(target=_worker, args=(r, world, port, n, d, k, nq, dead, pipelined, side, q, backend))
              for r in range(world)]
     for p in procs:
         p.start()

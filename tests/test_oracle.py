@@ -155,6 +155,24 @@ def test_pq_lut_adc_and_encode_tie_rule(orc):
     assert orc.pq_adc(orc.L2, lut, code) == s
 
 
+def test_pq_search_is_lut_adc_plus_heap(orc):
+    """orc_pq_search / orc_bench_pq (the CPU PQ-ADC leg of bench.py) equal the
+    per-row LookUp sums fed through the flat heap."""
+    rng = np.random.default_rng(11)
+    n, m, ks, ds = 3000, 32, 256, 4
+    codes = rng.integers(0, ks, (n, m), dtype=np.uint8)
+    centers = orc.synth_rows(45, 0, m * ks, ds, 0).reshape(m, ks, ds)
+    qs = rng.uniform(-1, 1, (3, m * ds)).astype(np.float32)
+    _, bi, bd = orc.bench_pq(codes, centers, qs, 10, orc.L2, 2)
+    for j, q in enumerate(qs):
+        lut = orc.pq_lut(orc.L2, q, centers)
+        d = np.array([orc.pq_adc(orc.L2, lut, c) for c in codes], np.float32)
+        wi, wd = orc.heap_topk(d, np.arange(n, dtype=np.uint64), 10)
+        i, dd = orc.pq_search(codes, centers, q, 10, orc.L2)
+        assert np.array_equal(i, wi) and np.array_equal(dd.view(np.uint32), wd.view(np.uint32))
+        assert np.array_equal(bi[j], wi) and np.array_equal(bd[j].view(np.uint32), wd.view(np.uint32))
+
+
 def test_heap_topk_matches_lexicographic_modulo_ties(orc):
     rng = np.random.default_rng(7)
     d = rng.integers(0, 20, 2000).astype(np.float32)  # many ties

@@ -2317,7 +2317,8 @@ int wvg_measure_hbm_read(wvg_ctx *ctx, uint64_t bytes, uint32_t reps, double *ou
         hipEventCreate(&b) != hipSuccess)
         return done(fail(WVG_ERR_DEVICE, "probe setup"));
     double best = 0.0;
-    for (int blocks : {1024, 2048, 4096, 8192}) {
+    // grid-stride forms, then the scans' contiguous-chunk form (negative = chunk workgroups)
+    for (int blocks : {1024, 2048, 4096, 8192, -256, -512, -1024, -2048}) {
         for (int w = 0; w < 2; w++)
             if (launch_hbm_read(buf, bytes, blocks, sink, s) != hipSuccess) return done(fail(WVG_ERR_DEVICE, "probe"));
         (void)hipEventRecord(a, s);

@@ -1052,10 +1052,39 @@ __global__ __launch_bounds__(256) void hbm_read_kernel(const float4 *__restrict_
     if (acc == 12345.678f) out[0] = acc;  // keeps the loads live; never true for the zero-filled buffer
 }
 
+// The scans' own access shape: each workgroup streams one contiguous chunk,
+// each wave 8 consecutive KiB per step (8 non-temporal 16-byte loads per lane
+// in flight), so a DRAM page is read by one wave at a time.
+__global__ __launch_bounds__(256) void hbm_read_chunk_kernel(const float4 *__restrict__ p, uint64_t n4, float *out)
+{
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const uint64_t per = (n4 + gridDim.x - 1) / gridDim.x;
+    const uint64_t lo = (uint64_t)blockIdx.x * per;
+    const uint64_t hi = lo + per < n4 ? lo + per : n4;
+    const f4v *q = reinterpret_cast<const f4v *>(p);
+    const unsigned wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float acc = 0.f;
+    uint64_t i = lo + wave * 512 + lane;
+    for (; i + 7 * 64 < hi; i += 4 * 512) {
+        f4v v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = __builtin_nontemporal_load(q + i + u * 64);
+#pragma unroll
+        for (int u = 0; u < 8; u++) acc += v[u].x + v[u].y + v[u].z + v[u].w;
+    }
+    for (; i < hi; i += 64) acc += q[i].x;
+    if (acc == 12345.678f) out[0] = acc;
+}
+
 hipError_t launch_hbm_read(const void *p, uint64_t bytes, int blocks, float *out, hipStream_t s)
 {
-    hipLaunchKernelGGL(hbm_read_kernel, dim3(blocks), dim3(256), 0, s, reinterpret_cast<const float4 *>(p), bytes / 16,
-                       out);
+    // blocks < 0: the contiguous-chunk form with -blocks workgroups
+    if (blocks < 0)
+        hipLaunchKernelGGL(hbm_read_chunk_kernel, dim3(-blocks), dim3(256), 0, s, reinterpret_cast<const float4 *>(p),
+                           bytes / 16, out);
+    else
+        hipLaunchKernelGGL(hbm_read_kernel, dim3(blocks), dim3(256), 0, s, reinterpret_cast<const float4 *>(p),
+                           bytes / 16, out);
     return hipGetLastError();
 }
 

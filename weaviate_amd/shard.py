@@ -163,11 +163,12 @@ class ShardedFlatIndex:
         nq = q.shape[0]
         dev = q.device
         s_obj, s_raw = _stream_obj(stream, dev)
-        world = dist.get_world_size(self.group) if dist.is_initialized() else 1
+        grouped = dist.is_initialized()  # a group of any size (one included) exchanges through it
+        world = dist.get_world_size(self.group) if grouped else 1
         fn = self.lib.wvg_search_device_pipelined if pipelined else self.lib.wvg_search_device
         with torch.cuda.stream(s_obj):
             b = self._buffers(nq, k, dev, world)
-            if world == 1:
+            if not grouped:
                 ids = torch.empty((nq, k), dtype=torch.int64, device=dev)
                 dists = torch.empty((nq, k), dtype=torch.float32, device=dev)
                 counts = torch.empty(nq, dtype=torch.int32, device=dev)
