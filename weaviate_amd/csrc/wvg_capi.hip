@@ -1230,6 +1230,7 @@ static int run_screen(wvg_corpus *c, const ScanArgs &a, const SearchPlan &p, cha
     L.k = k;
     L.nrr = nrr;
     L.cosine = c->metric == WVG_METRIC_COSINE;
+    L.num_cus = c->ctx->num_cus;
     L.qfrag = ws + w.qf;
     L.k1 = (float *)(ws + w.k1);
     L.k2 = (float *)(ws + w.k2);
@@ -2227,10 +2228,19 @@ int wvg_synthetic_rows(wvg_ctx *ctx, uint64_t seed, const uint64_t *ids, uint64_
 }
 
 #ifdef WVG_TOOLS
+// tools build: K3c counters [row-block epilogues (per wave), slow-path entries, insert calls, 0]
+int wvgx_screen_counters(uint64_t *out4, int reset)
+{
+    if (!out4) return WVG_ERR_INVALID;
+    wvg::screen_counters(out4, reset != 0);
+    return WVG_OK;
+}
+
 // A/B knob of the tools build (not part of include/wvgpu.h): 0 = K1 scan variant,
 // 1 = K1 resident workgroups per CU, ... 7 = K8 ADC variant, 8 = query-stream merge wait (us),
 // 9 = serpentine scan order, 10 = K3b row-range length, 11 = K1 load policy, 12 = K3b SIMD pairing,
-// 13 = K3b partner priority, 14 = PQ encode min3 argmin, 15 = co-scheduled PQ / BQ batches, 16 = co-scheduled BQ workgroups per CU.  Returns the previous value.
+// 13 = K3b partner priority, 14 = PQ encode min3 argmin, 15 = co-scheduled PQ / BQ batches, 16 = co-scheduled BQ workgroups per CU, 17 = K3c row-range length,
+// 18 = K3c diagnostics (results not distances), 19 = K3c split launch.  Returns the previous value.
 int wvgx_set_tuning(int key, int value)
 {
     Tuning &t = tuning();
@@ -2286,6 +2296,15 @@ int wvgx_set_tuning(int key, int value)
     } else if (key == 16) {
         old = t.bq_cos_gpc;
         t.bq_cos_gpc = value;
+    } else if (key == 17) {
+        old = t.screen_range_blocks;
+        t.screen_range_blocks = value;
+    } else if (key == 18) {
+        old = t.screen_diag;
+        t.screen_diag = value;
+    } else if (key == 19) {
+        old = t.screen_split;
+        t.screen_split = value;
     }
     return old;
 }

@@ -270,6 +270,9 @@ constexpr int SCREEN_M = 16;  // lower bounds kept per (wave, query) and per (ro
 inline uint32_t screen_kblocks(uint32_t dim) { return (dim + 63) / 64 * 2; }
 bool screen_supported(uint32_t dim, int metric, uint32_t k);
 uint32_t screen_row_ranges(uint32_t nq, uint64_t ntiles, int num_cus);
+#ifdef WVG_TOOLS
+void screen_counters(uint64_t out[4], bool reset);
+#endif
 hipError_t launch_shadow_build(const float *tiled, uint32_t dim, uint64_t t0, uint64_t t1, void *shadow, float *norms,
                                uint32_t *nmax, hipStream_t s);
 struct ScreenLaunch {
@@ -284,6 +287,7 @@ struct ScreenLaunch {
     const float *queries;  // [nq][qpitch] (normalized for cosine)
     uint32_t qpitch, nq, k, nrr;
     int cosine;
+    int num_cus;           // sizes the split screen's first launch
     void *qfrag;           // [nq_pad / 16][kblocks][64] x 16 B
     float *k1, *k2, *emax; // [nq_pad]
     uint32_t *gbound;      // [nq]
@@ -335,6 +339,10 @@ struct Tuning {
                              // for the whole pass), 1..256 = forced (A/B; env WVG_K1_TAIL)
     int pq_encode_min3 = 1;  // PQ encode pair path: min3 argmin on NaN-free codebooks (1) or the
                              // reference's compare-and-select loop everywhere (0; A/B and parity)
+    int screen_split = 1;    // K3c: seed the later ranges' bound from the first wave of ranges (1) or not (0; A/B)
+    int screen_range_blocks = 0;  // K3c row-range length in 256-row blocks (0 = auto, ~128; A/B)
+    int screen_diag = 0;     // K3c diagnostics (tools build only; results are NOT distances): bit 0 = no
+                             // wait for the stage loads, bit 1 = no epilogue, bit 2 = no list insertions
 };
 #ifdef WVG_TOOLS
 Tuning &tuning();

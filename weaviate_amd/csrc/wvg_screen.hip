@@ -47,21 +47,16 @@ constexpr int SC_BQ = 128;                 // queries per workgroup
 constexpr int SC_WAVES = 8;                // 4 (query quarters) x 2 (row halves)
 constexpr int SC_AFR = 8;                  // query fragments per stage (8 groups of 16, one 32-deep K block)
 constexpr int SC_BFR = 16;                 // row fragments per stage (16 groups of 16)
-constexpr int SC_STAGE = (SC_AFR + SC_BFR + 1) * 1024;  // + the row block's 256 norms
+constexpr int SC_STAGE = (SC_AFR + SC_BFR + 1) * 1024 + 256;  // + the row block's 256 norms and tile words
 constexpr int SC_NBUF = 4;                 // stages in LDS: three in flight while one is computed
 constexpr int SC_LISTS = SC_WAVES * 32 * SCREEN_M * 8;
 constexpr int SC_LDS = SC_NBUF * SC_STAGE + SC_LISTS + SC_WAVES * 32 * 4 * 2 + SC_BQ * 4 * 3;
 
-// A wave-uniform 64-bit word through the scalar cache (the address is made
-// uniform explicitly: the compiler may hold a uniform index in VGPRs).
-__device__ __forceinline__ uint64_t sc_sload64(const uint64_t *p)
+// A wave-uniform 64-bit value from a VGPR.
+__device__ __forceinline__ uint64_t readfirstlane64(uint64_t v)
 {
-    const uint64_t a = (uint64_t)p;
-    const uint64_t u = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)) << 32) |
-                       (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
-    uint64_t v;
-    asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(u) : "memory");
-    return v;
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
 }
 
 // ---------------------------------------------------------------------------
@@ -202,7 +197,11 @@ struct ScreenArgs {
     const uint4 *qfrag;       // [nq16][kbn][64]
     const float *k1, *k2, *emax;  // [nq_pad]
     uint32_t nq, k, nqb, nrr;
+    uint32_t rr0, nrr_l;      // this launch's ranges: [rr0, rr0 + nrr_l) of nrr
     int cosine;
+#ifdef WVG_TOOLS
+    int diag;                 // Tuning::screen_diag
+#endif
     uint32_t *gbound;         // [nq] ordered tau; 0xFFFFFFFF = none yet
     uint64_t *partials;       // [nq][nrr][SCREEN_M]
 };
@@ -265,8 +264,15 @@ __device__ __attribute__((noinline)) void sc_insert(uint64_t *L, float *WT, floa
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
+#ifdef WVG_TOOLS
+__device__ unsigned long long g_screen_ctr[4];  // tools build: [0] row blocks, [1] slow-path entries, [2] insert calls
+#endif
+
 __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
 {
+#ifdef WVG_TOOLS
+    uint32_t n_blk = 0, n_slow = 0, n_call = 0;
+#endif
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint64_t *lists = reinterpret_cast<uint64_t *>(smem + SC_NBUF * SC_STAGE);  // [8][32][M]
     float *tau = reinterpret_cast<float *>(smem + SC_NBUF * SC_STAGE + SC_LISTS);  // [8][32] distance-space threshold
@@ -283,13 +289,13 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
     // the nqb query blocks of one row range share an XCD (blocks b, b+8, ...)
     const uint32_t b = blockIdx.x;
     uint32_t qb, rr;
-    if (a.nrr % 8 == 0) {
+    if (a.nrr_l % 8 == 0) {
         const uint32_t xcd = b % 8, wv = b / 8;
         qb = wv % a.nqb;
-        rr = (wv / a.nqb) * 8 + xcd;
+        rr = a.rr0 + (wv / a.nqb) * 8 + xcd;
     } else {
         qb = b % a.nqb;
-        rr = b / a.nqb;
+        rr = a.rr0 + b / a.nqb;
     }
     const uint64_t ntiles = a.tile_end - a.tile_begin;
     const uint64_t nblk = (ntiles + 3) / 4;  // 256-row blocks
@@ -307,7 +313,9 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
     for (int i = tid; i < SC_WAVES * 32; i += SC_WAVES * 64) {
         const int ww = i / 32, ql = i % 32;
         const uint32_t q = q0 + (uint32_t)((ww & 3) * 32 + ql);
-        const uint32_t g = q < a.nq ? a.gbound[q] : 0u;
+        // agent-scope load (L1 bypassed): the bounds are atomicMin'd by ranges that
+        // finished on any XCD; a plain load could return a stale line
+        const uint32_t g = q < a.nq ? __hip_atomic_load(a.gbound + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
         const float t = q >= a.nq ? -__builtin_inff() : (g == 0xFFFFFFFFu ? __builtin_inff() : wvg_unord_f32(g));
         tau[i] = t;
         sig[i] = q >= a.nq ? __builtin_inff() : sc_sigma(t, cosine);
@@ -317,8 +325,9 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
     if (blk0 >= blk1) goto publish;
     {
         // stage loader: wave w moves fragments 3w .. 3w+2 of a stage (A 0..7, B 8..23);
-        // waves 0-3 also one 256-byte quarter of the block's norms (so a wave's
-        // loads per stage: SC_LDW = 4 for waves 0-3, 3 for 4-7)
+        // waves 0-3 also one 256-byte quarter of the block's norms, wave 4 the
+        // block's validity and allow words (so a wave's loads per stage: 4 for
+        // waves 0-4, 3 for 5-7)
         // Per-lane source pointers of this wave's three fragments at stage 0 of
         // the load cursor's row block: a stage adds one K block (A: 1 KiB,
         // B: 4 KiB), a row block four tiles of B (the shadow is padded by 4
@@ -342,7 +351,7 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
             }
         }
         const float *lnorm = a.norms + (a.tile_begin + blk0 * 4 + (w & 3)) * 64 + lane;
-        auto load_stage = [&](unsigned char *dst, uint32_t ks) {
+        auto load_stage = [&](unsigned char *dst, uint32_t ks, uint64_t lb) {
 #pragma unroll
             for (int j = 0; j < 3; j++)
                 __builtin_amdgcn_global_load_lds(lsrc[j] + (size_t)ks * lstep[j],
@@ -350,6 +359,21 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
             if (w < 4)
                 __builtin_amdgcn_global_load_lds(lnorm, reinterpret_cast<float *>(dst + (SC_AFR + SC_BFR) * 1024 + w * 256),
                                                  4, 0, 0);
+            if (w == 4) {
+                // the block's tile words as dwords: lanes 0-7 validity (tile
+                // lane >> 1, half lane & 1), 8-15 allow; the epilogue reads them
+                // from LDS (a scalar load there waited the full memory latency:
+                // the words fall out of L2 behind the row stream)
+                const uint32_t wi = (uint32_t)(lane & 7) >> 1, half = lane & 1;
+                const uint64_t t = a.tile_begin + lb * 4 + wi;
+                const uint32_t *src = reinterpret_cast<const uint32_t *>(a.valid + (t < a.tile_end ? t : a.tile_end - 1)) + half;
+                if (lane >= 8 && lane < 16 && a.allow) {
+                    const uint64_t aw = t - a.allow_t0;
+                    src = reinterpret_cast<const uint32_t *>(a.allow + (aw < a.allow_words ? aw : 0)) + half;
+                }
+                __builtin_amdgcn_global_load_lds(src, reinterpret_cast<uint32_t *>(dst + (SC_AFR + SC_BFR + 1) * 1024),
+                                                 4, 0, 0);
+            }
         };
         auto next_block = [&]() {  // the load cursor moves to the next row block
 #pragma unroll
@@ -358,7 +382,10 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
         };
         // wait until at most `younger` stages' loads of this wave are in flight
         auto wait_stages = [&](int younger) {
-            if (w < 4) {
+#ifdef WVG_TOOLS
+            if (a.diag & 1) return;
+#endif
+            if (w < 5) {
                 if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
                 else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
                 else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -382,6 +409,14 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
                 qlive[mq][r] = __ballot(q0 + 32 * wq + 16 * mq + qlane + r < a.nq);
         uint64_t *WL = lists + (size_t)w * 32 * M;
         float *WT = tau + w * 32, *WS = sig + w * 32;
+        // +inf when one of this lane's queries is not fast-eligible (K1 > 2^50: a
+        // huge or non-finite query), so its elements always take the exact test
+        float lane_force = -__builtin_inff();
+#pragma unroll
+        for (int mq = 0; mq < 2; mq++)
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+                if (!(ck1[32 * wq + 16 * mq + qlane + r] <= 0x1p50f)) lane_force = __builtin_inff();
 
         floatx4 acc[2][8];
 #pragma unroll
@@ -394,7 +429,7 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
         uint64_t lblk = blk0, blk = blk0;  // load cursor (three units ahead), compute cursor
         uint32_t lks = 0, ks = 0;
         auto unit_load = [&](uint64_t u) {
-            load_stage(smem + (u & (SC_NBUF - 1)) * SC_STAGE, lks);
+            load_stage(smem + (u & (SC_NBUF - 1)) * SC_STAGE, lks, lblk);
             if (++lks == NK) {
                 lks = 0;
                 ++lblk;
@@ -421,7 +456,12 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
                     for (int nr = 0; nr < 8; nr++)
                         acc[mq][nr] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[mq], bv[nr], acc[mq][nr], 0, 0, 0);
             }
-            if (ks == NK - 1) {
+#ifdef WVG_TOOLS
+            const bool epi = ks == NK - 1 && !(a.diag & 2);
+#else
+            const bool epi = ks == NK - 1;
+#endif
+            if (epi) {
                 // epilogue of row block blk: C layout row (query) qlane + r, column (row) lane & 15
                 // The epilogue's LDS reads go through inline asm: the compiler's
                 // wait pass cannot tell them from reads of an in-flight LDS DMA
@@ -445,16 +485,29 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
                              : "v"(nrs)
                              : "memory");
                 uint64_t vm[2];
+                {
+                    uint4 vw, aw4;
+                    const uint32_t wa = (uint32_t)(uintptr_t)(sb + (SC_AFR + SC_BFR + 1) * 1024) + 16u * (uint32_t)wr;
+                    asm volatile("ds_read_b128 %0, %2\n\t"
+                                 "ds_read_b128 %1, %2 offset:32\n\t"
+                                 "s_waitcnt lgkmcnt(0)"
+                                 : "=v"(vw), "=v"(aw4)
+                                 : "v"(wa)
+                                 : "memory");
+                    const uint64_t words[2] = {((uint64_t)vw.y << 32) | vw.x, ((uint64_t)vw.w << 32) | vw.z};
+                    const uint64_t allows[2] = {((uint64_t)aw4.y << 32) | aw4.x, ((uint64_t)aw4.w << 32) | aw4.z};
 #pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    const uint64_t t = a.tile_begin + blk * 4 + 2 * wr + h;
-                    uint64_t m = t < a.tile_end ? sc_sload64(a.valid + t) : 0ull;
-                    if (a.allow && m) {
-                        const uint64_t aw = t - a.allow_t0;
-                        m &= aw < a.allow_words ? sc_sload64(a.allow + aw) : 0ull;
+                    for (int h = 0; h < 2; h++) {
+                        const uint64_t t = a.tile_begin + blk * 4 + 2 * wr + h;
+                        uint64_t m = t < a.tile_end ? readfirstlane64(words[h]) : 0ull;
+                        if (a.allow) {
+                            const uint64_t aw = t - a.allow_t0;
+                            m &= aw < a.allow_words ? readfirstlane64(allows[h]) : 0ull;
+                        }
+                        vm[h] = m;
                     }
-                    vm[h] = m;
                 }
+                float k1r[2][4], k2r[2][4], svr[2][4];
 #pragma unroll
                 for (int mq = 0; mq < 2; mq++) {
                     float4 k1v, k2v, sv;
@@ -467,17 +520,57 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
                                    "v"((uint32_t)(uintptr_t)(ck2 + 32 * wq + 16 * mq + qlane)),
                                    "v"((uint32_t)(uintptr_t)(WS + 16 * mq + qlane))
                                  : "memory");
-                    const float k1r[4] = {k1v.x, k1v.y, k1v.z, k1v.w};
-                    const float k2r[4] = {k2v.x, k2v.y, k2v.z, k2v.w};
-                    const float svr[4] = {sv.x, sv.y, sv.z, sv.w};
+                    k1r[mq][0] = k1v.x, k1r[mq][1] = k1v.y, k1r[mq][2] = k1v.z, k1r[mq][3] = k1v.w;
+                    k2r[mq][0] = k2v.x, k2r[mq][1] = k2v.y, k2r[mq][2] = k2v.z, k2r[mq][3] = k2v.w;
+                    svr[mq][0] = sv.x, svr[mq][1] = sv.y, svr[mq][2] = sv.z, svr[mq][3] = sv.w;
+                }
+                // Fast check, branch-free: the largest u - sigma over this
+                // lane's 64 elements.  On the fast-eligible inputs (query K1 <=
+                // 2^50, row norm bound <= 2^60) every u is finite and sigma is
+                // finite or +-inf, so u - sigma is never NaN and its sign is
+                // exactly that of u - sigma; a huge / non-finite query
+                // (lane_force = +inf) or row forces the exact path below, which
+                // is the per-element test (NaN-safe) with the list insertions.
+                const bool all_valid = (vm[0] & vm[1]) == ~0ull;
+                float mx = -__builtin_inff();
+#pragma unroll
+                for (int nr = 0; nr < 8; nr++) {
+                    float mnr = lane_force;
+#pragma unroll
+                    for (int mq = 0; mq < 2; mq++)
+#pragma unroll
+                        for (int r = 0; r < 4; r++) {
+                            const float u = acc[mq][nr][r] + __builtin_fmaf(nrm[nr], k1r[mq][r], k2r[mq][r]);
+                            mnr = __builtin_fmaxf(mnr, u - svr[mq][r]);
+                        }
+                    mnr = nrm[nr] <= 0x1p60f ? mnr : __builtin_inff();
+                    if (!all_valid) {
+                        const uint32_t m16 = (uint32_t)(vm[nr >> 2] >> (16 * (nr & 3)));
+                        mnr = (m16 >> (lane & 15)) & 1u ? mnr : -__builtin_inff();
+                    }
+                    mx = __builtin_fmaxf(mx, mnr);
+                }
+#ifdef WVG_TOOLS
+#ifdef WVG_TOOLS
+                n_blk++;
+#endif
+                if (__ballot(mx >= 0.f) && !(a.diag & 4)) {
+#ifdef WVG_TOOLS
+                n_slow++;
+#endif
+#else
+                if (__ballot(mx >= 0.f)) {
+#endif
+#pragma unroll
+                for (int mq = 0; mq < 2; mq++) {
 #pragma unroll
                     for (int nr = 0; nr < 8; nr++) {
                         const uint64_t m16 = (vm[nr >> 2] >> (16 * (nr & 3))) & 0xFFFFull;
                         const uint64_t m64 = m16 * 0x0001000100010001ull;
 #pragma unroll
                         for (int r = 0; r < 4; r++) {
-                            const float u = acc[mq][nr][r] + __builtin_fmaf(nrm[nr], k1r[r], k2r[r]);
-                            uint64_t pass = __ballot(!(u < svr[r])) & m64 & qlive[mq][r];
+                            const float u = acc[mq][nr][r] + __builtin_fmaf(nrm[nr], k1r[mq][r], k2r[mq][r]);
+                            uint64_t pass = __ballot(!(u < svr[mq][r])) & m64 & qlive[mq][r];
                             while (pass) {  // rare after the first row blocks of a range
                                 const int src = __builtin_ctzll(pass);
                                 pass &= pass - 1;
@@ -485,10 +578,14 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
                                 const float us = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(u), src));
                                 const uint32_t slot = (uint32_t)((a.tile_begin + blk * 4) * 64 + 128 * wr + 16 * nr +
                                                                  (src & 15));
+#ifdef WVG_TOOLS
+                                n_call++;
+#endif
                                 sc_insert(WL + ql * M, WT + ql, WS + ql, cem[32 * wq + ql], K, cosine, us, slot);
                             }
                         }
                     }
+                }
                 }
 #pragma unroll
                 for (int mq = 0; mq < 2; mq++)
@@ -506,6 +603,14 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
         }
     }
 publish:
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef WVG_TOOLS
+    if (lane == 0) {
+        atomicAdd(&g_screen_ctr[0], (unsigned long long)n_blk);
+        atomicAdd(&g_screen_ctr[1], (unsigned long long)n_slow);
+        atomicAdd(&g_screen_ctr[2], (unsigned long long)n_call);
+    }
+#endif
     __syncthreads();
     // merge the two row halves' lists per query (waves wq and wq + 4), by rank:
     // wave w takes queries w, w + 8, ... of the workgroup
@@ -541,16 +646,19 @@ publish:
 // digits) over the entries' ordered lower bounds in LDS.
 constexpr uint32_t SC_COLLECT_MAX = 8192;  // nrr * SCREEN_M (screen_row_ranges caps nrr at 512)
 
-__global__ __launch_bounds__(256) void screen_collect_kernel(const uint64_t *partials, uint32_t nrr, uint32_t k,
-                                                             const float *emax, int cosine, uint64_t *cand,
-                                                             uint32_t *flist, uint32_t *nflag)
+// seed (cand == nullptr): the same tau* over the lists of the first nrr_use
+// ranges only, folded into gbound (atomicMin) -- the bound the later ranges
+// of a split screen start from.
+__global__ __launch_bounds__(256) void screen_collect_kernel(const uint64_t *partials, uint32_t nrr, uint32_t nrr_use,
+                                                             uint32_t k, const float *emax, int cosine, uint64_t *cand,
+                                                             uint32_t *flist, uint32_t *nflag, uint32_t *gbound)
 {
     __shared__ uint32_t hv[SC_COLLECT_MAX];
     __shared__ uint32_t hist[256];
     __shared__ uint32_t sh_prefix, sh_need, sh_total;
     __shared__ int ovf;
-    const uint32_t q = blockIdx.x, n = nrr * SCREEN_M;
-    const uint64_t *src = partials + (size_t)q * n;
+    const uint32_t q = blockIdx.x, n = nrr_use * SCREEN_M;
+    const uint64_t *src = partials + (size_t)q * nrr * SCREEN_M;
     uint64_t *dst = cand + (size_t)q * n;
     if (threadIdx.x == 0) {
         ovf = 0;
@@ -595,6 +703,10 @@ __global__ __launch_bounds__(256) void screen_collect_kernel(const uint64_t *par
         }
         t = sc_tau_k(wvg_unord_f32(sh_prefix), emax[q], cosine);
     }
+    if (!cand) {
+        if (threadIdx.x == 0 && t < __builtin_inff()) atomicMin(gbound + q, wvg_ord_f32(t));
+        return;
+    }
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
         const uint64_t e = src[i];
         const bool keep = e != WVG_KEY_NONE && key_lower(e) <= t;
@@ -613,6 +725,21 @@ bool screen_supported(uint32_t dim, int metric, uint32_t k)
            (metric == WVG_M_DOT || metric == WVG_M_COSINE);
 }
 
+#ifdef WVG_TOOLS
+// tools build: the K3c counters summed over every launch since the last reset
+void screen_counters(uint64_t out[4], bool reset)
+{
+    unsigned long long v[4] = {0, 0, 0, 0};
+    (void)hipDeviceSynchronize();
+    (void)hipMemcpyFromSymbol(v, HIP_SYMBOL(g_screen_ctr), sizeof(v));
+    for (int i = 0; i < 4; i++) out[i] = v[i];
+    if (reset) {
+        const unsigned long long z[4] = {0, 0, 0, 0};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_screen_ctr), z, sizeof(z));
+    }
+}
+#endif
+
 uint32_t screen_row_ranges(uint32_t nq, uint64_t ntiles, int num_cus)
 {
     const uint32_t nqb = (nq + SC_BQ - 1) / SC_BQ;
@@ -621,6 +748,10 @@ uint32_t screen_row_ranges(uint32_t nq, uint64_t ntiles, int num_cus)
     // range start together on one XCD and share its L2 for the row fragments),
     // at least one workgroup per CU
     uint64_t want = std::max<uint64_t>(((uint64_t)num_cus + nqb - 1) / nqb, (nblk + 127) / 128);
+#ifdef WVG_TOOLS
+    if (tuning().screen_range_blocks > 0)
+        want = std::max<uint64_t>(want, (nblk + tuning().screen_range_blocks - 1) / tuning().screen_range_blocks);
+#endif
     want = std::min<uint64_t>((want + 7) / 8 * 8, SC_COLLECT_MAX / SCREEN_M);
     if (want > nblk) want = nblk;
     if (want < 1) want = 1;
@@ -660,6 +791,9 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
     a.nqb = nqb;
     a.nrr = L.nrr;
     a.cosine = L.cosine;
+#ifdef WVG_TOOLS
+    a.diag = tuning().screen_diag;
+#endif
     a.gbound = L.gbound;
     a.partials = L.partials;
     static bool attr = [] {
@@ -667,10 +801,50 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
                                    hipFuncAttributeMaxDynamicSharedMemorySize, SC_LDS) == hipSuccess;
     }();
     (void)attr;
-    launch_timed(screen_kernel, dim3(nqb * L.nrr), dim3(SC_WAVES * 64), (uint32_t)SC_LDS, s, a);
+    // Split screen: the first rA ranges (one workgroup per CU) run alone; their
+    // lists' joint tau* (k-th smallest lower bound over ~10 % of the rows,
+    // + 2 Emax) seeds every later range's threshold.  Without it a range
+    // starts from the k-th bound of single finished ranges (rows in the
+    // top-k of 1 % of the corpus), and most row blocks took the exact
+    // per-element path with list insertions.
+    uint32_t rA = 0;
+    if (L.nrr % 8 == 0) {
+        rA = std::max<uint32_t>(8, ((uint32_t)L.num_cus / nqb + 7) / 8 * 8);
+        if (rA > L.nrr / 4) rA = 0;
+    }
+#ifdef WVG_TOOLS
+    if (tuning().screen_split == 0) rA = 0;
+#endif
+    if (rA) {
+        // profiling: one event pair spans both launches and the seed between them
+        const LaunchEvents ev = armed_events();
+        armed_events() = LaunchEvents{};
+        a.rr0 = 0;
+        a.nrr_l = rA;
+        if (ev.start)
+            hipExtLaunchKernelGGL(screen_kernel, dim3(nqb * rA), dim3(SC_WAVES * 64), (uint32_t)SC_LDS, s, ev.start,
+                                  (hipEvent_t)nullptr, 0u, a);
+        else
+            hipLaunchKernelGGL(screen_kernel, dim3(nqb * rA), dim3(SC_WAVES * 64), (uint32_t)SC_LDS, s, a);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        hipLaunchKernelGGL(screen_collect_kernel, dim3(L.nq), dim3(256), 0, s, L.partials, L.nrr, rA, L.k, L.emax,
+                           L.cosine, (uint64_t *)nullptr, L.flist, L.nflag, L.gbound);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        a.rr0 = rA;
+        a.nrr_l = L.nrr - rA;
+        if (ev.stop)
+            hipExtLaunchKernelGGL(screen_kernel, dim3(nqb * a.nrr_l), dim3(SC_WAVES * 64), (uint32_t)SC_LDS, s,
+                                  (hipEvent_t)nullptr, ev.stop, 0u, a);
+        else
+            hipLaunchKernelGGL(screen_kernel, dim3(nqb * a.nrr_l), dim3(SC_WAVES * 64), (uint32_t)SC_LDS, s, a);
+    } else {
+        a.rr0 = 0;
+        a.nrr_l = L.nrr;
+        launch_timed(screen_kernel, dim3(nqb * a.nrr_l), dim3(SC_WAVES * 64), (uint32_t)SC_LDS, s, a);
+    }
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(screen_collect_kernel, dim3(L.nq), dim3(256), 0, s, L.partials, L.nrr, L.k, L.emax, L.cosine,
-                       L.cand, L.flist, L.nflag);
+    hipLaunchKernelGGL(screen_collect_kernel, dim3(L.nq), dim3(256), 0, s, L.partials, L.nrr, L.nrr, L.k, L.emax,
+                       L.cosine, L.cand, L.flist, L.nflag, L.gbound);
     return hipGetLastError();
 }
 
