@@ -113,6 +113,30 @@ def test_screen_nonfinite_and_zero(ctx, exact_ctx, orc):
             b.destroy()
 
 
+def test_screen_large_finite_magnitudes(ctx, exact_ctx, orc):
+    """Large finite rows and queries on both sides of the fast check's limits
+    (row norm bound 2^60, query K1 2^50: beyond them every element takes the
+    exact per-element test, inside them u - sigma must stay finite): dot
+    products up to ~1e38, products that overflow bf16 / fp32 accumulation."""
+    n, d = 6000, 128
+    rows = orc.synth_rows(1250, 0, n, d, 0)
+    rows[100:110] *= np.float32(1e10)     # norm ~1e11: fast-eligible
+    rows[200:210] *= np.float32(1e19)     # norm ~1e20 > 2^60: forced exact
+    rows[300] = np.float32(3e38)          # bf16 rounds it to inf
+    qs = orc.synth_rows(1251, 0, 40, d, 0)
+    qs[1] *= np.float32(1e10)             # K1 ~1e9: fast-eligible
+    qs[2] *= np.float32(1e17)             # K1 > 2^50: forced exact
+    qs[3] *= np.float32(1e25)
+    for metric in (METRIC_DOT, METRIC_COSINE):
+        a, b = _pair(ctx, exact_ctx, metric, d, rows)
+        try:
+            for k in (1, 10, 16):
+                _same(a.search(qs, k), b.search(qs, k))
+        finally:
+            a.destroy()
+            b.destroy()
+
+
 def test_screen_allow_sparse_small(ctx, exact_ctx, orc):
     """Allow lists, a corpus smaller than k, ragged tails, a sparse id space."""
     d = 128

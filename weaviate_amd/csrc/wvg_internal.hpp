@@ -342,7 +342,7 @@ struct Tuning {
     int screen_split = 1;    // K3c: seed the later ranges' bound from the first wave of ranges (1) or not (0; A/B)
     int screen_range_blocks = 0;  // K3c row-range length in 256-row blocks (0 = auto, ~128; A/B)
     int screen_diag = 0;     // K3c diagnostics (tools build only; results are NOT distances): bit 0 = no
-                             // wait for the stage loads, bit 1 = no epilogue, bit 2 = no list insertions
+                             // wait for the stage loads, bit 1 = no epilogue, bit 2 = no list insertions, bit 3 = no query-fragment loads
 };
 #ifdef WVG_TOOLS
 Tuning &tuning();

@@ -236,32 +236,35 @@ __device__ __forceinline__ float key_lower(uint64_t key) { return wvg_unord_f32(
 // L of the SCREEN_M smallest (lower, slot) keys of one query, then the
 // query's thresholds: WT (distance space) = min(tau, k-th lower + 2 Emax,
 // M-th lower), WS its u-space form.  Out of line: it runs rarely and is
-// reached from 64 unrolled epilogue sites.
-__device__ __attribute__((noinline)) void sc_insert(uint64_t *L, float *WT, float *WS, float emax, int K, int cosine,
-                                                    float u, uint32_t slot)
+// reached from 64 unrolled epilogue sites.  Returns the query's current WS, so
+// the caller drops the other candidates of that query it no longer admits.
+__device__ __attribute__((noinline)) float sc_insert(uint64_t *L, float *WT, float *WS, float emax, int K, int cosine,
+                                                     float u, uint32_t slot)
 {
     const int lane = threadIdx.x & 63, M = SCREEN_M;
     const float lower = sc_lower(u, cosine);
-    if (!(lower <= *WT)) return;
+    if (!(lower <= *WT)) return *WS;
     const uint64_t key = ((uint64_t)wvg_ord_f32(lower) << 32) | slot;
     const uint64_t v = lane < M ? L[lane] : WVG_KEY_NONE;
     const uint64_t last = __shfl(v, M - 1);
-    if (!(key < last)) return;
+    if (!(key < last)) return *WS;
     const int pos = __popcll(__ballot(lane < M && v < key));
     if (lane >= pos && lane < M - 1) L[lane + 1] = v;
     if (lane == pos) L[pos] = key;
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const uint64_t nk = L[K - 1], nm = L[M - 1];
+    float t = *WT;
+    if (nk != WVG_KEY_NONE) t = fminf(t, sc_tau_k(key_lower(nk), emax, cosine));
+    if (nm != WVG_KEY_NONE) t = fminf(t, key_lower(nm));
+    const float ws = sc_sigma(t, cosine);
     if (lane == 0) {
-        float t = *WT;
-        if (nk != WVG_KEY_NONE) t = fminf(t, sc_tau_k(key_lower(nk), emax, cosine));
-        if (nm != WVG_KEY_NONE) t = fminf(t, key_lower(nm));
         *WT = t;
-        *WS = sc_sigma(t, cosine);
+        *WS = ws;
     }
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    return ws;
 }
 
 #ifdef WVG_TOOLS
@@ -353,9 +356,13 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
         const float *lnorm = a.norms + (a.tile_begin + blk0 * 4 + (w & 3)) * 64 + lane;
         auto load_stage = [&](unsigned char *dst, uint32_t ks, uint64_t lb) {
 #pragma unroll
-            for (int j = 0; j < 3; j++)
+            for (int j = 0; j < 3; j++) {
+#ifdef WVG_TOOLS
+                if ((a.diag & 8) && 3 * w + j < SC_AFR) continue;  // diagnostic: no query-fragment loads
+#endif
                 __builtin_amdgcn_global_load_lds(lsrc[j] + (size_t)ks * lstep[j],
                                                  reinterpret_cast<uint4 *>(dst + (3 * w + j) * 1024), 16, 0, 0);
+            }
             if (w < 4)
                 __builtin_amdgcn_global_load_lds(lnorm, reinterpret_cast<float *>(dst + (SC_AFR + SC_BFR) * 1024 + w * 256),
                                                  4, 0, 0);
@@ -551,16 +558,13 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
                     mx = __builtin_fmaxf(mx, mnr);
                 }
 #ifdef WVG_TOOLS
-#ifdef WVG_TOOLS
                 n_blk++;
-#endif
-                if (__ballot(mx >= 0.f) && !(a.diag & 4)) {
-#ifdef WVG_TOOLS
-                n_slow++;
-#endif
+                const bool slow = __ballot(mx >= 0.f) && !(a.diag & 4);
+                n_slow += slow;
 #else
-                if (__ballot(mx >= 0.f)) {
+                const bool slow = __ballot(mx >= 0.f);
 #endif
+                if (slow) {
 #pragma unroll
                 for (int mq = 0; mq < 2; mq++) {
 #pragma unroll
@@ -581,7 +585,11 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
 #ifdef WVG_TOOLS
                                 n_call++;
 #endif
-                                sc_insert(WL + ql * M, WT + ql, WS + ql, cem[32 * wq + ql], K, cosine, us, slot);
+                                const float ws_now =
+                                    sc_insert(WL + ql * M, WT + ql, WS + ql, cem[32 * wq + ql], K, cosine, us, slot);
+                                // the other lanes of this 16-lane group hold the same query
+                                const uint64_t grp = 0xFFFFull << (16 * (src >> 4));
+                                pass &= ~grp | __ballot(!(u < ws_now));
                             }
                         }
                     }
