@@ -45,7 +45,7 @@ def _same(x, y):
 
 
 @pytest.mark.parametrize("metric,d", [(METRIC_COSINE, 768), (METRIC_DOT, 768), (METRIC_COSINE, 128), (METRIC_DOT, 256),
-                                      (METRIC_COSINE, 96), (METRIC_DOT, 1536)])
+                                      (METRIC_COSINE, 96), (METRIC_DOT, 1536), (METRIC_DOT, 512), (METRIC_COSINE, 512)])
 def test_screen_equals_exact(ctx, exact_ctx, orc, metric, d):
     n = 30_000 + 77
     rows = orc.synth_rows(1000 + d, 0, n, d, 0)
@@ -69,11 +69,12 @@ def test_screen_equals_exact(ctx, exact_ctx, orc, metric, d):
         b.destroy()
 
 
-def test_screen_ties_overflow_rescan(ctx, exact_ctx, orc):
+@pytest.mark.parametrize("d", [256, 768])  # K3c, K3d
+def test_screen_ties_overflow_rescan(ctx, exact_ctx, orc, d):
     """3000 copies of one row and a query equal to it: every copy ties at the
     k-th distance, the range lists fill below tau, the queries are flagged
     and rescanned exactly -- still the lexicographic (distance, docID) top-k."""
-    n, d = 20_000, 256
+    n = 20_000
     rows = orc.synth_rows(1100, 0, n, d, 0)
     dup = np.arange(1000, 4000)
     rows[dup] = rows[1000]
@@ -89,10 +90,11 @@ def test_screen_ties_overflow_rescan(ctx, exact_ctx, orc):
             b.destroy()
 
 
-def test_screen_nonfinite_and_zero(ctx, exact_ctx, orc):
+@pytest.mark.parametrize("d", [128, 768])  # K3c, K3d
+def test_screen_nonfinite_and_zero(ctx, exact_ctx, orc, d):
     """Rows and queries with inf / NaN / zero components: their bound is
     infinite (always rescored) or their distance exact; NaN sorts last."""
-    n, d = 8000, 128
+    n = 8000
     rows = np.floor(orc.synth_rows(1200, 0, n, d, 0) * 3).astype(np.float32)
     rows[10, 3] = np.nan
     rows[11, 4] = np.inf
@@ -118,7 +120,7 @@ def test_screen_large_finite_magnitudes(ctx, exact_ctx, orc):
     (row norm bound 2^60, query K1 2^50: beyond them every element takes the
     exact per-element test, inside them u - sigma must stay finite): dot
     products up to ~1e38, products that overflow bf16 / fp32 accumulation."""
-    n, d = 6000, 128
+    n, d = 6000, 768
     rows = orc.synth_rows(1250, 0, n, d, 0)
     rows[100:110] *= np.float32(1e10)     # norm ~1e11: fast-eligible
     rows[200:210] *= np.float32(1e19)     # norm ~1e20 > 2^60: forced exact
@@ -137,9 +139,9 @@ def test_screen_large_finite_magnitudes(ctx, exact_ctx, orc):
             b.destroy()
 
 
-def test_screen_allow_sparse_small(ctx, exact_ctx, orc):
+@pytest.mark.parametrize("d", [128, 768])  # K3c, K3d
+def test_screen_allow_sparse_small(ctx, exact_ctx, orc, d):
     """Allow lists, a corpus smaller than k, ragged tails, a sparse id space."""
-    d = 128
     qs = orc.synth_rows(1301, 0, 64, d, 0)
     for n in (5, 63, 300, 4097):
         rows = orc.synth_rows(1300 + n, 0, n, d, 0)

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--ranges", default="0")
     ap.add_argument("--diags", default="0")
     ap.add_argument("--splits", default="1", help="K3c split launch (tuning key 19)")
+    ap.add_argument("--variants", default="0", help="screen kernel (tuning key 20): 0 K3d where it applies, 1 K3c")
     a = ap.parse_args()
     import torch
 
@@ -51,9 +52,11 @@ def main():
     od = torch.empty((nq, k), dtype=torch.float32, device=dev)
     oc = torch.empty(nq, dtype=torch.int32, device=dev)
     ref = None
-    for sp, rb, dg in [(sp, rb, dg) for sp in [int(x) for x in a.splits.split(",")]
-                       for rb in [int(x) for x in a.ranges.split(",")] for dg in [int(x) for x in a.diags.split(",")]]:
+    for vr, sp, rb, dg in [(vr, sp, rb, dg) for vr in [int(x) for x in a.variants.split(",")]
+                           for sp in [int(x) for x in a.splits.split(",")]
+                           for rb in [int(x) for x in a.ranges.split(",")] for dg in [int(x) for x in a.diags.split(",")]]:
         if True:
+            lib.wvgx_set_tuning(20, vr)
             lib.wvgx_set_tuning(19, sp)
             lib.wvgx_set_tuning(17, rb)
             lib.wvgx_set_tuning(18, dg)
@@ -83,13 +86,14 @@ def main():
                 if ref is None:
                     ref = got
                 same = bool(np.array_equal(got, ref))
-            print(json.dumps({"split": sp, "range_blocks": rb, "diag": dg, "scoring_kernel_ms": round(kern, 3),
+            print(json.dumps({"variant": vr, "split": sp, "range_blocks": rb, "diag": dg, "scoring_kernel_ms": round(kern, 3),
                               "tflops": round(2.0 * nq * n * d / (kern / 1e3) / 1e12, 1),
                               "ids_equal_first": same, "wave_row_blocks": cnt[0], "slow_path_blocks": cnt[1],
                               "insert_calls": cnt[2]}), flush=True)
     lib.wvgx_set_tuning(17, 0)
     lib.wvgx_set_tuning(18, 0)
     lib.wvgx_set_tuning(19, 1)
+    lib.wvgx_set_tuning(20, 0)
     c.destroy()
     ctx.close()
 

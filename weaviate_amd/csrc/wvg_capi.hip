@@ -2240,7 +2240,8 @@ int wvgx_screen_counters(uint64_t *out4, int reset)
 // 1 = K1 resident workgroups per CU, ... 7 = K8 ADC variant, 8 = query-stream merge wait (us),
 // 9 = serpentine scan order, 10 = K3b row-range length, 11 = K1 load policy, 12 = K3b SIMD pairing,
 // 13 = K3b partner priority, 14 = PQ encode min3 argmin, 15 = co-scheduled PQ / BQ batches, 16 = co-scheduled BQ workgroups per CU, 17 = K3c row-range length,
-// 18 = K3c diagnostics (results not distances), 19 = K3c split launch.  Returns the previous value.
+// 18 = K3c diagnostics (results not distances), 19 = K3c split launch,
+// 20 = screen kernel (0 K3d where it applies, 1 K3c).  Returns the previous value.
 int wvgx_set_tuning(int key, int value)
 {
     Tuning &t = tuning();
@@ -2305,6 +2306,9 @@ int wvgx_set_tuning(int key, int value)
     } else if (key == 19) {
         old = t.screen_split;
         t.screen_split = value;
+    } else if (key == 20) {
+        old = t.screen_variant;
+        t.screen_variant = value;
     }
     return old;
 }

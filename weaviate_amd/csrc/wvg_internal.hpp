@@ -339,7 +339,8 @@ struct Tuning {
                              // for the whole pass), 1..256 = forced (A/B; env WVG_K1_TAIL)
     int pq_encode_min3 = 1;  // PQ encode pair path: min3 argmin on NaN-free codebooks (1) or the
                              // reference's compare-and-select loop everywhere (0; A/B and parity)
-    int screen_split = 1;    // K3c: seed the later ranges' bound from the first wave of ranges (1) or not (0; A/B)
+    int screen_variant = 0;  // batched screen kernel: 0 = K3d where it applies (d = 512, 768), 1 = K3c (A/B)
+    int screen_split = 1;    // K3c/K3d phases seeded from the earlier ones: 1 = up to three, 2 = two, 0 = one launch (A/B)
     int screen_range_blocks = 0;  // K3c row-range length in 256-row blocks (0 = auto, ~128; A/B)
     int screen_diag = 0;     // K3c diagnostics (tools build only; results are NOT distances): bit 0 = no
                              // wait for the stage loads, bit 1 = no epilogue, bit 2 = no list insertions, bit 3 = no query-fragment loads

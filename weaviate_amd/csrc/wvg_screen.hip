@@ -539,7 +539,7 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
                 // (lane_force = +inf) or row forces the exact path below, which
                 // is the per-element test (NaN-safe) with the list insertions.
                 const bool all_valid = (vm[0] & vm[1]) == ~0ull;
-                float mx = -__builtin_inff();
+                float mx = -__builtin_inff(), mnr_a[8];
 #pragma unroll
                 for (int nr = 0; nr < 8; nr++) {
                     float mnr = lane_force;
@@ -555,6 +555,7 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
                         const uint32_t m16 = (uint32_t)(vm[nr >> 2] >> (16 * (nr & 3)));
                         mnr = (m16 >> (lane & 15)) & 1u ? mnr : -__builtin_inff();
                     }
+                    mnr_a[nr] = mnr;
                     mx = __builtin_fmaxf(mx, mnr);
                 }
 #ifdef WVG_TOOLS
@@ -565,10 +566,13 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
                 const bool slow = __ballot(mx >= 0.f);
 #endif
                 if (slow) {
+                // only the row groups where some lane passed the fast check (their
+                // elements' exact tests are the only ones that can pass)
 #pragma unroll
-                for (int mq = 0; mq < 2; mq++) {
+                for (int nr = 0; nr < 8; nr++) {
+                    if (!__ballot(mnr_a[nr] >= 0.f)) continue;
 #pragma unroll
-                    for (int nr = 0; nr < 8; nr++) {
+                    for (int mq = 0; mq < 2; mq++) {
                         const uint64_t m16 = (vm[nr >> 2] >> (16 * (nr & 3))) & 0xFFFFull;
                         const uint64_t m64 = m16 * 0x0001000100010001ull;
 #pragma unroll
@@ -637,6 +641,356 @@ publish:
         if (lane < 2 * M && rank < M) out[rank] = x;
         if (lane < 2 * M && rank == K - 1 && x != WVG_KEY_NONE) {
             const float t = sc_tau_k(key_lower(x), cem[qw], cosine);
+            atomicMin(a.gbound + q, wvg_ord_f32(t));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K3d: K3c with the queries resident in registers (d = 32 KBN, KBN in {16, 24}).
+// A workgroup = 4 waves, one per SIMD, 128 queries (32 per wave) whose bf16
+// fragments for every K block are loaded once into VGPRs / AGPRs; only the row
+// fragments stream through LDS: per 32-deep stage 16 KiB (256 rows) by LDS DMA
+// into a ring of 8 stage buffers, six stages in flight (loads past the range
+// end re-read its last block, so every stage issues the same loads and the
+// vmcnt waits are constants).  Per stage and wave: the first half of the rows'
+// fragments (read one stage ahead) feeds 16 MFMAs while the second half is
+// read; the barrier for the next stage sits between the halves; the next
+// stage's first half is read during the second half's MFMAs.  Against K3c per
+// 128 x 256 x 32 tile: 16 KiB instead of 25 KiB from L2 (no query fragments,
+// one norm copy) and 64 KiB instead of 80 KiB of LDS reads.  The epilogue, the
+// bound, the lists and the partials are K3c's.
+constexpr int SD_WAVES = 4;
+constexpr int SD_BQ = 128;
+constexpr int SD_BFR = 16;
+constexpr int SD_STAGE = SD_BFR * 1024;
+constexpr int SD_NBUF = 8;
+constexpr int SD_NSLOT = 1280;
+constexpr int SD_RING = SD_NBUF * SD_STAGE + 2 * SD_NSLOT;
+constexpr int SD_LISTS = SD_WAVES * 32 * SCREEN_M * 8;
+constexpr int SD_LDS = SD_RING + SD_LISTS + SD_WAVES * 32 * 4 * 2 + SD_BQ * 4 * 3;
+
+template <int KBN>
+__global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs a)
+{
+    static_assert(KBN % SD_NBUF == 0, "the stage buffer of a K block must be a compile-time constant");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint64_t *lists = reinterpret_cast<uint64_t *>(smem + SD_RING);  // [4][32][M]
+    float *tau = reinterpret_cast<float *>(smem + SD_RING + SD_LISTS);
+    float *sig = tau + SD_WAVES * 32;
+    float *ck1 = sig + SD_WAVES * 32;
+    float *ck2 = ck1 + SD_BQ;
+    float *cem = ck2 + SD_BQ;
+#ifdef WVG_TOOLS
+    uint32_t n_blk = 0, n_slow = 0, n_call = 0;
+#endif
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int K = (int)a.k, M = SCREEN_M;
+    const int cosine = a.cosine;
+    const uint32_t b = blockIdx.x;
+    uint32_t qb, rr;
+    if (a.nrr_l % 8 == 0) {
+        const uint32_t xcd = b % 8, wv = b / 8;
+        qb = wv % a.nqb;
+        rr = a.rr0 + (wv / a.nqb) * 8 + xcd;
+    } else {
+        qb = b % a.nqb;
+        rr = a.rr0 + b / a.nqb;
+    }
+    const uint64_t ntiles = a.tile_end - a.tile_begin;
+    const uint64_t nblk = (ntiles + 3) / 4;
+    const uint64_t blk0 = nblk * rr / a.nrr, blk1 = nblk * (rr + 1) / a.nrr;
+    const uint32_t q0 = qb * SD_BQ;
+
+    for (int i = tid; i < SD_BQ; i += SD_WAVES * 64) {
+        const uint32_t q = q0 + (uint32_t)i;
+        ck1[i] = a.k1[q];
+        ck2[i] = a.k2[q];
+        cem[i] = a.emax[q];
+    }
+    for (int i = tid; i < SD_WAVES * 32; i += SD_WAVES * 64) {
+        const uint32_t q = q0 + (uint32_t)i;
+        const uint32_t g = q < a.nq ? __hip_atomic_load(a.gbound + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        const float t = q >= a.nq ? -__builtin_inff() : (g == 0xFFFFFFFFu ? __builtin_inff() : wvg_unord_f32(g));
+        tau[i] = t;
+        sig[i] = q >= a.nq ? __builtin_inff() : sc_sigma(t, cosine);
+    }
+    for (int i = tid; i < SD_WAVES * 32 * M; i += SD_WAVES * 64) lists[i] = WVG_KEY_NONE;
+    __syncthreads();
+    if (blk0 < blk1) {
+        // the wave's 32 queries, every K block, resident for the whole range
+        bf16x8 areg[KBN][2];
+#pragma unroll
+        for (int ks = 0; ks < KBN; ks++)
+#pragma unroll
+            for (int mq = 0; mq < 2; mq++)
+                areg[ks][mq] = *reinterpret_cast<const bf16x8 *>(
+                    a.qfrag + ((size_t)(qb * 8 + 2 * w + mq) * KBN + ks) * 64 + lane);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int ks = 0; ks < KBN; ks++)
+#pragma unroll
+            for (int mq = 0; mq < 2; mq++) asm volatile("" : "+v"(areg[ks][mq]));
+
+        // loads of one stage: wave w moves row fragments 4w .. 4w+3 (tile w,
+        // row groups 0..3), the norms of tile w, and wave 0 the block's tile
+        // words (so 6 loads per stage for wave 0, 5 for the others)
+        const uint4 *lsrc = a.shadow + ((size_t)(a.tile_begin + blk0 * 4 + w) * KBN * 4) * 64 + lane;
+        const float *lnorm = a.norms + (a.tile_begin + blk0 * 4 + w) * 64 + lane;
+        uint64_t lblk = blk0;
+        auto load_stage = [&](int ks) {
+            unsigned char *dst = smem + (ks % SD_NBUF) * SD_STAGE;
+#pragma unroll
+            for (int rg = 0; rg < 4; rg++)
+                __builtin_amdgcn_global_load_lds(lsrc + ((size_t)ks * 4 + rg) * 64,
+                                                 reinterpret_cast<uint4 *>(dst + (4 * w + rg) * 1024), 16, 0, 0);
+            unsigned char *nslot = smem + SD_NBUF * SD_STAGE + (lblk & 1) * SD_NSLOT;
+            __builtin_amdgcn_global_load_lds(lnorm, reinterpret_cast<float *>(nslot + w * 256), 4, 0, 0);
+            if (w == 0) {
+                const uint32_t wi = (uint32_t)(lane & 7) >> 1, half = lane & 1;
+                const uint64_t t = a.tile_begin + lblk * 4 + wi;
+                const uint32_t *src =
+                    reinterpret_cast<const uint32_t *>(a.valid + (t < a.tile_end ? t : a.tile_end - 1)) + half;
+                if (lane >= 8 && lane < 16 && a.allow) {
+                    const uint64_t aw = t - a.allow_t0;
+                    src = reinterpret_cast<const uint32_t *>(a.allow + (aw < a.allow_words ? aw : 0)) + half;
+                }
+                __builtin_amdgcn_global_load_lds(src, reinterpret_cast<uint32_t *>(nslot + 1024), 4, 0, 0);
+            }
+            if (ks == KBN - 1 && lblk + 1 < blk1) {  // the load cursor moves on; past the end it stays
+                ++lblk;
+                lsrc += (size_t)4 * KBN * 4 * 64;
+                lnorm += 256;
+            }
+        };
+        // six stages in flight at every wait: the unit being waited for + 5 younger
+        auto wait_next = [&]() {
+#ifdef WVG_TOOLS
+            if (a.diag & 1) return;
+#endif
+            if (w == 0) asm volatile("s_waitcnt vmcnt(30)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(25)" ::: "memory");
+        };
+        auto raw_barrier = [&]() {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+        };
+        auto read_half = [&](int ks, int h, bf16x8 (&br)[8]) {
+            const unsigned char *sb = smem + (ks % SD_NBUF) * SD_STAGE + h * 8 * 1024;
+#pragma unroll
+            for (int j = 0; j < 8; j++) br[j] = *reinterpret_cast<const bf16x8 *>(sb + j * 1024 + lane * 16);
+        };
+        const int qlane = 4 * (lane >> 4);
+        uint64_t qlive[2][4];
+#pragma unroll
+        for (int mq = 0; mq < 2; mq++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) qlive[mq][r] = __ballot(q0 + 32 * w + 16 * mq + qlane + r < a.nq);
+        uint64_t *WL = lists + (size_t)w * 32 * M;
+        float *WT = tau + w * 32, *WS = sig + w * 32;
+        float lane_force = -__builtin_inff();
+#pragma unroll
+        for (int mq = 0; mq < 2; mq++)
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+                if (!(ck1[32 * w + 16 * mq + qlane + r] <= 0x1p50f)) lane_force = __builtin_inff();
+
+        floatx4 acc[2][16];
+#pragma unroll
+        for (int mq = 0; mq < 2; mq++)
+#pragma unroll
+            for (int nr = 0; nr < 16; nr++) acc[mq][nr] = (floatx4){0.f, 0.f, 0.f, 0.f};
+        bf16x8 b0[8], b1[8];
+        // prologue: units 0 .. 6 of the range (a unit = one K block of one row
+        // block; the ring holds K block ks of any row block in buffer ks % 8)
+#pragma unroll
+        for (int ks = 0; ks < SD_NBUF - 1; ks++) load_stage(ks);
+        if (w == 0) asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(30)" ::: "memory");
+        raw_barrier();
+        read_half(0, 0, b0);
+        for (uint64_t blk = blk0; blk < blk1; blk++) {
+#pragma unroll
+            for (int ks = 0; ks < KBN; ks++) {
+                read_half(ks, 1, b1);
+#pragma unroll
+                for (int mq = 0; mq < 2; mq++)
+#pragma unroll
+                    for (int nr = 0; nr < 8; nr++)
+                        acc[mq][nr] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(areg[ks][mq], b0[nr], acc[mq][nr], 0, 0, 0);
+                wait_next();   // the next unit landed
+                raw_barrier(); // (lgkmcnt(0): this wave's second-half reads done)
+#pragma unroll
+                for (int j = 0; j < 8; j++) asm volatile("" : "+v"(b1[j]));
+                // unit + 7 into the buffer of unit - 1 (fully read before this barrier)
+                load_stage((ks + SD_NBUF - 1) % KBN);
+                read_half((ks + 1) % KBN, 0, b0);
+#pragma unroll
+                for (int mq = 0; mq < 2; mq++)
+#pragma unroll
+                    for (int nr = 0; nr < 8; nr++)
+                        acc[mq][8 + nr] =
+                            __builtin_amdgcn_mfma_f32_16x16x32_bf16(areg[ks][mq], b1[nr], acc[mq][8 + nr], 0, 0, 0);
+            }
+            // epilogue of row block blk (K3c's, over 16 row groups): C layout row
+            // (query) qlane + r, column (row) 16 nr + (lane & 15)
+#ifdef WVG_TOOLS
+            if (a.diag & 2) goto next_block;
+#endif
+            {
+                const unsigned char *nslot = smem + SD_NBUF * SD_STAGE + (blk & 1) * SD_NSLOT;
+                float nrm[16];
+                const uint32_t nrs = (uint32_t)(uintptr_t)nslot + 4u * (uint32_t)(lane & 15);
+#pragma unroll
+                for (int i = 0; i < 2; i++)
+                    asm volatile("ds_read_b32 %0, %8 offset:%9\n\t"
+                                 "ds_read_b32 %1, %8 offset:%10\n\t"
+                                 "ds_read_b32 %2, %8 offset:%11\n\t"
+                                 "ds_read_b32 %3, %8 offset:%12\n\t"
+                                 "ds_read_b32 %4, %8 offset:%13\n\t"
+                                 "ds_read_b32 %5, %8 offset:%14\n\t"
+                                 "ds_read_b32 %6, %8 offset:%15\n\t"
+                                 "ds_read_b32 %7, %8 offset:%16\n\t"
+                                 "s_waitcnt lgkmcnt(0)"
+                                 : "=v"(nrm[8 * i + 0]), "=v"(nrm[8 * i + 1]), "=v"(nrm[8 * i + 2]), "=v"(nrm[8 * i + 3]),
+                                   "=v"(nrm[8 * i + 4]), "=v"(nrm[8 * i + 5]), "=v"(nrm[8 * i + 6]), "=v"(nrm[8 * i + 7])
+                                 : "v"(nrs), "i"(512 * i + 0), "i"(512 * i + 64), "i"(512 * i + 128), "i"(512 * i + 192),
+                                   "i"(512 * i + 256), "i"(512 * i + 320), "i"(512 * i + 384), "i"(512 * i + 448)
+                                 : "memory");
+                uint64_t vm[4];
+                {
+                    uint4 vw0, vw1, aw0, aw1;
+                    const uint32_t wa = (uint32_t)(uintptr_t)(nslot + 1024);
+                    asm volatile("ds_read_b128 %0, %4\n\t"
+                                 "ds_read_b128 %1, %4 offset:16\n\t"
+                                 "ds_read_b128 %2, %4 offset:32\n\t"
+                                 "ds_read_b128 %3, %4 offset:48\n\t"
+                                 "s_waitcnt lgkmcnt(0)"
+                                 : "=v"(vw0), "=v"(vw1), "=v"(aw0), "=v"(aw1)
+                                 : "v"(wa)
+                                 : "memory");
+                    const uint64_t words[4] = {((uint64_t)vw0.y << 32) | vw0.x, ((uint64_t)vw0.w << 32) | vw0.z,
+                                               ((uint64_t)vw1.y << 32) | vw1.x, ((uint64_t)vw1.w << 32) | vw1.z};
+                    const uint64_t allows[4] = {((uint64_t)aw0.y << 32) | aw0.x, ((uint64_t)aw0.w << 32) | aw0.z,
+                                                ((uint64_t)aw1.y << 32) | aw1.x, ((uint64_t)aw1.w << 32) | aw1.z};
+#pragma unroll
+                    for (int h = 0; h < 4; h++) {
+                        const uint64_t t = a.tile_begin + blk * 4 + h;
+                        uint64_t m = t < a.tile_end ? readfirstlane64(words[h]) : 0ull;
+                        if (a.allow) {
+                            const uint64_t aw = t - a.allow_t0;
+                            m &= aw < a.allow_words ? readfirstlane64(allows[h]) : 0ull;
+                        }
+                        vm[h] = m;
+                    }
+                }
+                float k1r[2][4], k2r[2][4], svr[2][4];
+#pragma unroll
+                for (int mq = 0; mq < 2; mq++) {
+                    float4 k1v, k2v, sv;
+                    asm volatile("ds_read_b128 %0, %3\n\t"
+                                 "ds_read_b128 %1, %4\n\t"
+                                 "ds_read_b128 %2, %5\n\t"
+                                 "s_waitcnt lgkmcnt(0)"
+                                 : "=v"(k1v), "=v"(k2v), "=v"(sv)
+                                 : "v"((uint32_t)(uintptr_t)(ck1 + 32 * w + 16 * mq + qlane)),
+                                   "v"((uint32_t)(uintptr_t)(ck2 + 32 * w + 16 * mq + qlane)),
+                                   "v"((uint32_t)(uintptr_t)(WS + 16 * mq + qlane))
+                                 : "memory");
+                    k1r[mq][0] = k1v.x, k1r[mq][1] = k1v.y, k1r[mq][2] = k1v.z, k1r[mq][3] = k1v.w;
+                    k2r[mq][0] = k2v.x, k2r[mq][1] = k2v.y, k2r[mq][2] = k2v.z, k2r[mq][3] = k2v.w;
+                    svr[mq][0] = sv.x, svr[mq][1] = sv.y, svr[mq][2] = sv.z, svr[mq][3] = sv.w;
+                }
+                // fast check (K3c's): the largest u - sigma over the lane's 128 elements
+                const bool all_valid = (vm[0] & vm[1] & vm[2] & vm[3]) == ~0ull;
+                float mx = -__builtin_inff(), mnr_a[16];
+#pragma unroll
+                for (int nr = 0; nr < 16; nr++) {
+                    float mnr = lane_force;
+#pragma unroll
+                    for (int mq = 0; mq < 2; mq++)
+#pragma unroll
+                        for (int r = 0; r < 4; r++) {
+                            const float u = acc[mq][nr][r] + __builtin_fmaf(nrm[nr], k1r[mq][r], k2r[mq][r]);
+                            mnr = __builtin_fmaxf(mnr, u - svr[mq][r]);
+                        }
+                    mnr = nrm[nr] <= 0x1p60f ? mnr : __builtin_inff();
+                    if (!all_valid) {
+                        const uint32_t m16 = (uint32_t)(vm[nr >> 2] >> (16 * (nr & 3)));
+                        mnr = (m16 >> (lane & 15)) & 1u ? mnr : -__builtin_inff();
+                    }
+                    mnr_a[nr] = mnr;
+                    mx = __builtin_fmaxf(mx, mnr);
+                }
+#ifdef WVG_TOOLS
+                n_blk++;
+                const bool slow = __ballot(mx >= 0.f) && !(a.diag & 4);
+                n_slow += slow;
+#else
+                const bool slow = __ballot(mx >= 0.f);
+#endif
+                if (slow) {
+                    // only the row groups where some lane passed the fast check
+#pragma unroll
+                    for (int nr = 0; nr < 16; nr++) {
+                        if (!__ballot(mnr_a[nr] >= 0.f)) continue;
+#pragma unroll
+                        for (int mq = 0; mq < 2; mq++) {
+                            const uint64_t m16 = (vm[nr >> 2] >> (16 * (nr & 3))) & 0xFFFFull;
+                            const uint64_t m64 = m16 * 0x0001000100010001ull;
+#pragma unroll
+                            for (int r = 0; r < 4; r++) {
+                                const float u = acc[mq][nr][r] + __builtin_fmaf(nrm[nr], k1r[mq][r], k2r[mq][r]);
+                                uint64_t pass = __ballot(!(u < svr[mq][r])) & m64 & qlive[mq][r];
+                                while (pass) {
+                                    const int src = __builtin_ctzll(pass);
+                                    pass &= pass - 1;
+                                    const int ql = 16 * mq + 4 * (src >> 4) + r;
+                                    const float us = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(u), src));
+                                    const uint32_t slot =
+                                        (uint32_t)((a.tile_begin + blk * 4) * 64 + 16 * nr + (src & 15));
+#ifdef WVG_TOOLS
+                                    n_call++;
+#endif
+                                    const float ws_now =
+                                        sc_insert(WL + ql * M, WT + ql, WS + ql, cem[32 * w + ql], K, cosine, us, slot);
+                                    const uint64_t grp = 0xFFFFull << (16 * (src >> 4));
+                                    pass &= ~grp | __ballot(!(u < ws_now));
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+#ifdef WVG_TOOLS
+        next_block:
+#endif
+#pragma unroll
+            for (int mq = 0; mq < 2; mq++)
+#pragma unroll
+                for (int nr = 0; nr < 16; nr++) acc[mq][nr] = (floatx4){0.f, 0.f, 0.f, 0.f};
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef WVG_TOOLS
+    if (lane == 0) {
+        atomicAdd(&g_screen_ctr[0], (unsigned long long)n_blk);
+        atomicAdd(&g_screen_ctr[1], (unsigned long long)n_slow);
+        atomicAdd(&g_screen_ctr[2], (unsigned long long)n_call);
+    }
+#endif
+    __syncthreads();
+    // each wave owns whole lists: its 32 queries' range lists go straight to partials
+    for (int ql = 0; ql < 32; ql++) {
+        const uint32_t q = q0 + (uint32_t)(32 * w + ql);
+        if (q >= a.nq) break;
+        const uint64_t x = lane < M ? lists[((size_t)w * 32 + ql) * M + lane] : WVG_KEY_NONE;
+        uint64_t *out = a.partials + ((size_t)q * a.nrr + rr) * M;
+        if (lane < M) out[lane] = x;
+        if (lane == K - 1 && x != WVG_KEY_NONE) {
+            const float t = sc_tau_k(key_lower(x), cem[32 * w + ql], cosine);
             atomicMin(a.gbound + q, wvg_ord_f32(t));
         }
     }
@@ -806,49 +1160,58 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
     a.partials = L.partials;
     static bool attr = [] {
         return hipFuncSetAttribute(reinterpret_cast<const void *>(&screen_kernel),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, SC_LDS) == hipSuccess;
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, SC_LDS) == hipSuccess &&
+               hipFuncSetAttribute(reinterpret_cast<const void *>(&screen_ar_kernel<16>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, SD_LDS) == hipSuccess &&
+               hipFuncSetAttribute(reinterpret_cast<const void *>(&screen_ar_kernel<24>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, SD_LDS) == hipSuccess;
     }();
     (void)attr;
-    // Split screen: the first rA ranges (one workgroup per CU) run alone; their
+    // K3d (queries resident in registers) where its template applies, else K3c
+    void (*kern)(ScreenArgs) = kbn == 24 ? &screen_ar_kernel<24> : kbn == 16 ? &screen_ar_kernel<16> : nullptr;
+#ifdef WVG_TOOLS
+    if (tuning().screen_variant == 1) kern = nullptr;
+#endif
+    const uint32_t threads = kern ? SD_WAVES * 64 : SC_WAVES * 64, lds = kern ? SD_LDS : SC_LDS;
+    if (!kern) kern = &screen_kernel;
+    // Phased screen: the first r1 ranges (one workgroup per CU) run alone; their
     // lists' joint tau* (k-th smallest lower bound over ~10 % of the rows,
-    // + 2 Emax) seeds every later range's threshold.  Without it a range
-    // starts from the k-th bound of single finished ranges (rows in the
-    // top-k of 1 % of the corpus), and most row blocks took the exact
-    // per-element path with list insertions.
-    uint32_t rA = 0;
+    // + 2 Emax) seeds the next phase's thresholds, the next r2 - r1 ranges
+    // (~30 %) run, and the joint tau* over the first r2 seeds the rest.
+    // Without it a range starts from the k-th bound of single finished
+    // ranges (rows in the top-k of 1 % of the corpus), and most row blocks
+    // took the exact per-element path with list insertions.
+    uint32_t bounds[4] = {0, 0, 0, 0}, nph = 0;
+    bounds[nph++] = 0;
     if (L.nrr % 8 == 0) {
-        rA = std::max<uint32_t>(8, ((uint32_t)L.num_cus / nqb + 7) / 8 * 8);
-        if (rA > L.nrr / 4) rA = 0;
+        const uint32_t r1 = std::max<uint32_t>(8, ((uint32_t)L.num_cus / nqb + 7) / 8 * 8);
+        if (r1 <= L.nrr / 4) {
+            bounds[nph++] = r1;
+            if (4 * r1 <= L.nrr / 2) bounds[nph++] = 4 * r1;
+        }
     }
 #ifdef WVG_TOOLS
-    if (tuning().screen_split == 0) rA = 0;
+    if (tuning().screen_split == 0) nph = 1;
+    if (tuning().screen_split == 2 && nph > 2) nph = 2;
 #endif
-    if (rA) {
-        // profiling: one event pair spans both launches and the seed between them
-        const LaunchEvents ev = armed_events();
-        armed_events() = LaunchEvents{};
-        a.rr0 = 0;
-        a.nrr_l = rA;
-        if (ev.start)
-            hipExtLaunchKernelGGL(screen_kernel, dim3(nqb * rA), dim3(SC_WAVES * 64), (uint32_t)SC_LDS, s, ev.start,
-                                  (hipEvent_t)nullptr, 0u, a);
+    bounds[nph] = L.nrr;
+    // profiling: one event pair spans every phase and the seeds between them
+    const LaunchEvents ev = armed_events();
+    armed_events() = LaunchEvents{};
+    for (uint32_t ph = 0; ph < nph; ph++) {
+        a.rr0 = bounds[ph];
+        a.nrr_l = bounds[ph + 1] - bounds[ph];
+        const hipEvent_t e0 = ph == 0 ? ev.start : nullptr, e1 = ph + 1 == nph ? ev.stop : nullptr;
+        if (e0 || e1)
+            hipExtLaunchKernelGGL(kern, dim3(nqb * a.nrr_l), dim3(threads), lds, s, e0, e1, 0u, a);
         else
-            hipLaunchKernelGGL(screen_kernel, dim3(nqb * rA), dim3(SC_WAVES * 64), (uint32_t)SC_LDS, s, a);
+            hipLaunchKernelGGL(kern, dim3(nqb * a.nrr_l), dim3(threads), lds, s, a);
         if ((e = hipGetLastError()) != hipSuccess) return e;
-        hipLaunchKernelGGL(screen_collect_kernel, dim3(L.nq), dim3(256), 0, s, L.partials, L.nrr, rA, L.k, L.emax,
-                           L.cosine, (uint64_t *)nullptr, L.flist, L.nflag, L.gbound);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        a.rr0 = rA;
-        a.nrr_l = L.nrr - rA;
-        if (ev.stop)
-            hipExtLaunchKernelGGL(screen_kernel, dim3(nqb * a.nrr_l), dim3(SC_WAVES * 64), (uint32_t)SC_LDS, s,
-                                  (hipEvent_t)nullptr, ev.stop, 0u, a);
-        else
-            hipLaunchKernelGGL(screen_kernel, dim3(nqb * a.nrr_l), dim3(SC_WAVES * 64), (uint32_t)SC_LDS, s, a);
-    } else {
-        a.rr0 = 0;
-        a.nrr_l = L.nrr;
-        launch_timed(screen_kernel, dim3(nqb * a.nrr_l), dim3(SC_WAVES * 64), (uint32_t)SC_LDS, s, a);
+        if (ph + 1 < nph) {
+            hipLaunchKernelGGL(screen_collect_kernel, dim3(L.nq), dim3(256), 0, s, L.partials, L.nrr, bounds[ph + 1],
+                               L.k, L.emax, L.cosine, (uint64_t *)nullptr, L.flist, L.nflag, L.gbound);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(screen_collect_kernel, dim3(L.nq), dim3(256), 0, s, L.partials, L.nrr, L.nrr, L.k, L.emax,
