@@ -343,7 +343,7 @@ struct Tuning {
     int screen_split = 1;    // K3c/K3d phases seeded from the earlier ones: 1 = up to three, 2 = two, 0 = one launch (A/B)
     int screen_range_blocks = 0;  // K3c row-range length in 256-row blocks (0 = auto, ~128; A/B)
     int screen_diag = 0;     // K3c diagnostics (tools build only; results are NOT distances): bit 0 = no
-                             // wait for the stage loads, bit 1 = no epilogue, bit 2 = no list insertions, bit 3 = no query-fragment loads
+                             // wait for the stage loads, bit 1 = no epilogue, bit 2 = no list insertions, bit 3 = no query-fragment loads (K3c); K3d: 1, 2, 4 or 16 (= counters) select compiled variants
 };
 #ifdef WVG_TOOLS
 Tuning &tuning();

@@ -235,11 +235,17 @@ __device__ __forceinline__ float key_lower(uint64_t key) { return wvg_unord_f32(
 // Exact insertion of one survivor (wave-uniform arguments) into a wave's list
 // L of the SCREEN_M smallest (lower, slot) keys of one query, then the
 // query's thresholds: WT (distance space) = min(tau, k-th lower + 2 Emax,
-// M-th lower), WS its u-space form.  Out of line: it runs rarely and is
-// reached from 64 unrolled epilogue sites.  Returns the query's current WS, so
-// the caller drops the other candidates of that query it no longer admits.
-__device__ __attribute__((noinline)) float sc_insert(uint64_t *L, float *WT, float *WS, float emax, int K, int cosine,
-                                                     float u, uint32_t slot)
+// M-th lower), WS its u-space form.  Returns the query's current WS, so the
+// caller drops the other candidates of that query it no longer admits.
+// Out of line (it is reached from 64 / 128 unrolled epilogue sites; inlined,
+// the kernel spilled inside its main loop) with LDS-typed pointers: through
+// generic pointers every list access was a flat load / store, each followed by
+// a vmcnt(0) + lgkmcnt(0) wait.  (A call still begins with the ABI's full
+// wait, which drains the stage prefetch once per exact-path row block.)
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
+typedef __attribute__((address_space(3))) float lds_f32;
+__device__ __attribute__((noinline)) float sc_insert(lds_u64 *L, lds_f32 *WT, lds_f32 *WS, float emax, int K,
+                                                     int cosine, float u, uint32_t slot)
 {
     const int lane = threadIdx.x & 63, M = SCREEN_M;
     const float lower = sc_lower(u, cosine);
@@ -590,7 +596,7 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void screen_kernel(ScreenArgs a)
                                 n_call++;
 #endif
                                 const float ws_now =
-                                    sc_insert(WL + ql * M, WT + ql, WS + ql, cem[32 * wq + ql], K, cosine, us, slot);
+                                    sc_insert((lds_u64 *)(WL + ql * M), (lds_f32 *)(WT + ql), (lds_f32 *)(WS + ql), cem[32 * wq + ql], K, cosine, us, slot);
                                 // the other lanes of this 16-lane group hold the same query
                                 const uint64_t grp = 0xFFFFull << (16 * (src >> 4));
                                 pass &= ~grp | __ballot(!(u < ws_now));
@@ -670,7 +676,11 @@ constexpr int SD_RING = SD_NBUF * SD_STAGE + 2 * SD_NSLOT;
 constexpr int SD_LISTS = SD_WAVES * 32 * SCREEN_M * 8;
 constexpr int SD_LDS = SD_RING + SD_LISTS + SD_WAVES * 32 * 4 * 2 + SD_BQ * 4 * 3;
 
-template <int KBN>
+// DIAG (tools build only; 0 in the product): bit 0 = no wait for the stage
+// loads, bit 1 = no epilogue, bit 2 = no list insertions, bit 4 = count row
+// blocks / exact-path blocks / insertion calls.  Compile-time, so the tools
+// build's DIAG = 0 kernel is the product kernel, register allocation included.
+template <int KBN, int DIAG = 0>
 __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs a)
 {
     static_assert(KBN % SD_NBUF == 0, "the stage buffer of a K block must be a compile-time constant");
@@ -681,9 +691,7 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
     float *ck1 = sig + SD_WAVES * 32;
     float *ck2 = ck1 + SD_BQ;
     float *cem = ck2 + SD_BQ;
-#ifdef WVG_TOOLS
-    uint32_t n_blk = 0, n_slow = 0, n_call = 0;
-#endif
+    uint32_t n_blk = 0, n_slow = 0, n_call = 0;  // (DIAG & 16)
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int K = (int)a.k, M = SCREEN_M;
@@ -766,9 +774,7 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
         };
         // six stages in flight at every wait: the unit being waited for + 5 younger
         auto wait_next = [&]() {
-#ifdef WVG_TOOLS
-            if (a.diag & 1) return;
-#endif
+            if constexpr ((DIAG & 1) != 0) return;
             if (w == 0) asm volatile("s_waitcnt vmcnt(30)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(25)" ::: "memory");
         };
@@ -836,10 +842,7 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
             }
             // epilogue of row block blk (K3c's, over 16 row groups): C layout row
             // (query) qlane + r, column (row) 16 nr + (lane & 15)
-#ifdef WVG_TOOLS
-            if (a.diag & 2) goto next_block;
-#endif
-            {
+            if constexpr ((DIAG & 2) == 0) {
                 const unsigned char *nslot = smem + SD_NBUF * SD_STAGE + (blk & 1) * SD_NSLOT;
                 float nrm[16];
                 const uint32_t nrs = (uint32_t)(uintptr_t)nslot + 4u * (uint32_t)(lane & 15);
@@ -924,14 +927,13 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
                     mnr_a[nr] = mnr;
                     mx = __builtin_fmaxf(mx, mnr);
                 }
-#ifdef WVG_TOOLS
-                n_blk++;
-                const bool slow = __ballot(mx >= 0.f) && !(a.diag & 4);
-                n_slow += slow;
-#else
-                const bool slow = __ballot(mx >= 0.f);
-#endif
+                const bool slow = __ballot(mx >= 0.f) && (DIAG & 4) == 0;
+                if constexpr ((DIAG & 16) != 0) {
+                    n_blk++;
+                    n_slow += slow;
+                }
                 if (slow) {
+                    if constexpr ((DIAG & 64) != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // diagnostic
                     // only the row groups where some lane passed the fast check
 #pragma unroll
                     for (int nr = 0; nr < 16; nr++) {
@@ -951,11 +953,13 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
                                     const float us = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(u), src));
                                     const uint32_t slot =
                                         (uint32_t)((a.tile_begin + blk * 4) * 64 + 16 * nr + (src & 15));
-#ifdef WVG_TOOLS
-                                    n_call++;
-#endif
-                                    const float ws_now =
-                                        sc_insert(WL + ql * M, WT + ql, WS + ql, cem[32 * w + ql], K, cosine, us, slot);
+                                    if constexpr ((DIAG & 16) != 0) n_call++;
+                                    float ws_now;
+                                    if constexpr ((DIAG & 32) != 0)
+                                        ws_now = svr[mq][r];  // diagnostic: the scan of the exact path, no insertion
+                                    else
+                                        ws_now = sc_insert((lds_u64 *)(WL + ql * M), (lds_f32 *)(WT + ql),
+                                                           (lds_f32 *)(WS + ql), cem[32 * w + ql], K, cosine, us, slot);
                                     const uint64_t grp = 0xFFFFull << (16 * (src >> 4));
                                     pass &= ~grp | __ballot(!(u < ws_now));
                                 }
@@ -964,9 +968,6 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
                     }
                 }
             }
-#ifdef WVG_TOOLS
-        next_block:
-#endif
 #pragma unroll
             for (int mq = 0; mq < 2; mq++)
 #pragma unroll
@@ -975,10 +976,12 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #ifdef WVG_TOOLS
-    if (lane == 0) {
-        atomicAdd(&g_screen_ctr[0], (unsigned long long)n_blk);
-        atomicAdd(&g_screen_ctr[1], (unsigned long long)n_slow);
-        atomicAdd(&g_screen_ctr[2], (unsigned long long)n_call);
+    if constexpr ((DIAG & 16) != 0) {
+        if (lane == 0) {
+            atomicAdd(&g_screen_ctr[0], (unsigned long long)n_blk);
+            atomicAdd(&g_screen_ctr[1], (unsigned long long)n_slow);
+            atomicAdd(&g_screen_ctr[2], (unsigned long long)n_call);
+        }
     }
 #endif
     __syncthreads();
@@ -1170,6 +1173,20 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
     // K3d (queries resident in registers) where its template applies, else K3c
     void (*kern)(ScreenArgs) = kbn == 24 ? &screen_ar_kernel<24> : kbn == 16 ? &screen_ar_kernel<16> : nullptr;
 #ifdef WVG_TOOLS
+    if (kbn == 24) {  // K3d diagnostics: separately compiled instantiations
+        switch (tuning().screen_diag) {
+        case 1: kern = &screen_ar_kernel<24, 1>; break;
+        case 2: kern = &screen_ar_kernel<24, 2>; break;
+        case 4: kern = &screen_ar_kernel<24, 4>; break;
+        case 16: kern = &screen_ar_kernel<24, 16>; break;
+        case 32: kern = &screen_ar_kernel<24, 32>; break;
+        case 96: kern = &screen_ar_kernel<24, 96>; break;
+        default: break;
+        }
+        if (kern != &screen_ar_kernel<24>)
+            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      SD_LDS);
+    }
     if (tuning().screen_variant == 1) kern = nullptr;
 #endif
     const uint32_t threads = kern ? SD_WAVES * 64 : SC_WAVES * 64, lds = kern ? SD_LDS : SC_LDS;
