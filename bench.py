@@ -60,6 +60,9 @@ def parse(argv=None):
     ap.add_argument("--no-reuse-rows", type=int, default=4_000_000,
                     help="rows of the untimed no-reuse leg (frac_no_reuse); 8x the Infinity Cache at d = 128")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-run", action="store_true",
+                    help="only the timed headline launches (no no-reuse leg, read probe or CPU baseline), so a "
+                         "rocprofv3 --stats summary of the scan kernel covers exactly the launches `roofline` times")
     ap.add_argument("--dry-run", action="store_true", help="CPU-only rehearsal of the N-rank launch + exchange")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal: all ranks on cuda:0 with a gloo exchange (one-GPU boxes; not a measurement)")
@@ -387,8 +390,11 @@ def run_flat1m(args, world, rank, dev, torch, dist):
     traffic, traffic_src = stored_traffic(n, d, B)  # per launch, like `achieved`
     # untimed: the same kernel with no reuse between scans, and the HBM read ceiling
     nr_rows = max(n, args.no_reuse_rows)
-    nr_launch_s, ceiling = no_reuse_leg(args, dev, torch, nr_rows, d, k, B, tq, P, max(4, min(args.steps, 10)))
-    achieved_nr = nr_rows * d * 4 * B / nr_launch_s / 1e9
+    if args.profile_run:
+        nr_launch_s, ceiling, achieved_nr = float("nan"), float("nan"), float("nan")
+    else:
+        nr_launch_s, ceiling = no_reuse_leg(args, dev, torch, nr_rows, d, k, B, tq, P, max(4, min(args.steps, 10)))
+        achieved_nr = nr_rows * d * 4 * B / nr_launch_s / 1e9
     out = {
         "metric": METRIC,
         "value": round(total_queries / elapsed, 3),
@@ -424,12 +430,13 @@ def run_flat1m(args, world, rank, dev, torch, dist):
             "queries_per_launch": B,
             "algorithmic_bytes_per_launch": bytes_per_launch,
             "launches": int(launches.value),
-            "achieved_no_reuse": round(achieved_nr, 1),
-            "frac_no_reuse": round(achieved_nr / HBM_PEAK_GBS, 4),
-            "avg_launch_us_no_reuse": round(nr_launch_s * 1e6, 2),
+            "achieved_no_reuse": None if args.profile_run else round(achieved_nr, 1),
+            "frac_no_reuse": None if args.profile_run else round(achieved_nr / HBM_PEAK_GBS, 4),
+            "avg_launch_us_no_reuse": None if args.profile_run else round(nr_launch_s * 1e6, 2),
             "rows_no_reuse": nr_rows,
-            "ceiling_GBps": round(ceiling, 1),
-            "frac_of_ceiling_no_reuse": round(achieved_nr / ceiling, 4) if ceiling > 0 else None,
+            "ceiling_GBps": None if args.profile_run else round(ceiling, 1),
+            "frac_of_ceiling_no_reuse": (round(achieved_nr / ceiling, 4)
+                                         if not args.profile_run and ceiling > 0 else None),
             "note": ("`achieved` = ALGORITHMIC bytes (N*d*4 per query scan, every query a full scan) / the "
                      "kernel's average launch time, Infinity-Cache reuse included: consecutive scans alternate "
                      "direction and read the last ~320 MB of each pass with the default cache policy "
@@ -442,7 +449,7 @@ def run_flat1m(args, world, rank, dev, torch, dist):
         },
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_run:
         cq = np.random.default_rng(43).uniform(-1, 1, (16, d)).astype(np.float32)
         gids, _, _ = corpus.search(cq, k)  # GPU results of the baseline's first queries (full-size cross-check)
 

@@ -24,10 +24,10 @@ step() {  # step <limit> <name> <cmd...>
 }
 step 300 bench python3 bench.py
 grep '^{' $O/bench.log | tail -1 > $O/bench.json
-step 300 trace rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -- python3 bench.py --no-cpu-baseline
-step 200 pmc_fetch rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc_fetch -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline
+step 300 trace rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -- python3 bench.py --profile-run
+step 200 pmc_fetch rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc_fetch -- python3 bench.py --steps 10 --warmup 2 --profile-run
 step 240 screen rocprofv3 --kernel-trace --stats --output-format csv -d $O/screen_trace -- python3 tools/screen_bench.py
-step 400 configs rocprofv3 --kernel-trace --stats --output-format csv -d $O/configs_trace -- python3 tools/bench_configs.py --only bq,pq,slab,rescore
+WVG_LIB=$PWD/tools/libwvgpu_tools.so step 400 configs rocprofv3 --kernel-trace --stats --output-format csv -d $O/configs_trace -- python3 tools/bench_configs.py --only bq,pq,slab,rescore
 step 200 encode rocprofv3 --kernel-trace --stats --output-format csv -d $O/encode_trace -- python3 tools/encode_bench.py
 step 200 small rocprofv3 --kernel-trace --stats --output-format csv -d $O/small_trace -- python3 tools/small_batch_bench.py
 echo done
