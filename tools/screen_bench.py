@@ -2,7 +2,10 @@
 """BASELINE configs[1]: batched 10-NN over 10M x 768 fp32 cosine, 1024-query
 batches -- the K3c bf16 screen + exact rescore against the exact fp32 MFMA
 path (K3b), same corpus, same queries, results compared bit for bit.
-Device API (queries in HBM), HIP events bound to the scoring launch.
+Device API (queries in HBM), HIP events bound to the scoring launch(es);
+mfma_util against the dense peak of the kernel's MFMA type (bf16 2.5 PFLOP/s
+for the screen, fp32 157.3 TFLOP/s for K3b); rescored_rows = the candidates
+the exact fp32 rescore recomputed in the last batch.
 Tooling only (product library; no tuning knobs)."""
 import argparse
 import ctypes
@@ -15,6 +18,19 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+
+
+def screen_offsets(n, nq, k, d, num_cus=256):
+    """(candidate-array byte offset, candidates per query, flagged-count byte
+    offset) in a K3c / K3d workspace (screen_ws in wvg_capi.hip, after the
+    256-byte status block); mirrors screen_row_ranges."""
+    nqb = (nq + 127) // 128
+    nblk = ((n + 63) // 64 + 3) // 4
+    want = max((num_cus + nqb - 1) // nqb, (nblk + 127) // 128)
+    nrr = max(1, min(min((want + 7) // 8 * 8, 512), nblk))
+    ncand = nrr * 16
+    part = (nq * ncand * 8 + 255) // 256 * 256
+    return part, ncand, screen_nflag_offset(n, nq, k, d, num_cus)
 
 
 def screen_nflag_offset(n, nq, k, d, num_cus=256):
@@ -98,11 +114,17 @@ def main():
         res[mode] = (oi.cpu().numpy().copy(), od.cpu().numpy().copy(), oc.cpu().numpy().copy())
         if mode == "screen":  # flagged (rescanned) queries of the last batch: the screen workspace's nflag word
             out["flagged_queries"] = int(ws[256 + screen_nflag_offset(n, nq, k, d):][:4].cpu().numpy().view(np.uint32)[0])
+            # candidates the exact fp32 rescore recomputed (keys the collect kept, K6's input)
+            co, ncand, _ = screen_offsets(n, nq, k, d)
+            cand = ws[256 + co:256 + co + nq * ncand * 8].cpu().numpy().view(np.uint64)
+            out["rescored_rows"] = int((cand != np.iinfo(np.uint64).max).sum())
+            out["rescored_rows_per_query"] = round(out["rescored_rows"] / nq, 2)
         kern_ms = ms.value / max(1, nl.value)
         flop = 2.0 * nq * n * d
         out[mode] = {"batch_ms": round(wall * 1e3, 3), "qps": round(nq / wall, 1),
                      "scoring_kernel_ms": round(kern_ms, 3),
                      "tflops_kernel": round(flop / (kern_ms / 1e3) / 1e12, 1),
+                     "mfma_util": round(flop / (kern_ms / 1e3) / 1e12 / (2500.0 if mode == "screen" else 157.3), 3),
                      "first_call_s": round(first_s, 3), "fill_s": round(gen_s, 2)}
         print(json.dumps({mode: out[mode]}), flush=True)
         c.destroy()
