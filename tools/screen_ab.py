@@ -7,6 +7,7 @@ cosine, 1024 queries, k = 10 by default; HIP events bound to the scoring
 launch.  Usage: WVG_LIB=tools/libwvgpu_tools.so python tools/screen_ab.py
 [--ranges 0,16,32,64,256] [--diags 0,1,2,3]"""
 import argparse
+import time
 import ctypes
 import json
 import os
@@ -29,6 +30,7 @@ def main():
     ap.add_argument("--diags", default="0")
     ap.add_argument("--splits", default="1", help="K3c split launch (tuning key 19)")
     ap.add_argument("--variants", default="0", help="screen kernel (tuning key 20): 0 K3d where it applies, 1 K3c")
+    ap.add_argument("--pilots", default="16", help="tiles of the exact pilot scan that seeds the bound (tuning key 21; 0 = none)")
     a = ap.parse_args()
     import torch
 
@@ -52,10 +54,12 @@ def main():
     od = torch.empty((nq, k), dtype=torch.float32, device=dev)
     oc = torch.empty(nq, dtype=torch.int32, device=dev)
     ref = None
-    for vr, sp, rb, dg in [(vr, sp, rb, dg) for vr in [int(x) for x in a.variants.split(",")]
-                           for sp in [int(x) for x in a.splits.split(",")]
+    for pl, vr, sp, rb, dg in [(pl, vr, sp, rb, dg) for pl in [int(x) for x in a.pilots.split(",")]
+                               for vr in [int(x) for x in a.variants.split(",")]
+                               for sp in [int(x) for x in a.splits.split(",")]
                            for rb in [int(x) for x in a.ranges.split(",")] for dg in [int(x) for x in a.diags.split(",")]]:
         if True:
+            lib.wvgx_set_tuning(21, pl)
             lib.wvgx_set_tuning(20, vr)
             lib.wvgx_set_tuning(19, sp)
             lib.wvgx_set_tuning(17, rb)
@@ -72,9 +76,11 @@ def main():
             ctr = (ctypes.c_uint64 * 4)()
             lib.wvgx_screen_counters(ctr, 1)
             check(lib.wvg_profile_start(ctx.handle))
+            t0 = time.perf_counter()
             for _ in range(a.reps):
                 run()
             torch.cuda.synchronize()
+            wall = (time.perf_counter() - t0) * 1e3 / a.reps
             ms, nl = ctypes.c_double(), ctypes.c_uint64()
             check(lib.wvg_profile_stop(ctx.handle, ctypes.byref(ms), ctypes.byref(nl)))
             kern = ms.value / max(1, nl.value)
@@ -86,7 +92,7 @@ def main():
                 if ref is None:
                     ref = got
                 same = bool(np.array_equal(got, ref))
-            print(json.dumps({"variant": vr, "split": sp, "range_blocks": rb, "diag": dg, "scoring_kernel_ms": round(kern, 3),
+            print(json.dumps({"pilot": pl, "search_ms": round(wall, 3), "variant": vr, "split": sp, "range_blocks": rb, "diag": dg, "scoring_kernel_ms": round(kern, 3),
                               "tflops": round(2.0 * nq * n * d / (kern / 1e3) / 1e12, 1),
                               "ids_equal_first": same, "wave_row_blocks": cnt[0], "slow_path_blocks": cnt[1],
                               "insert_calls": cnt[2]}), flush=True)
@@ -94,6 +100,7 @@ def main():
     lib.wvgx_set_tuning(18, 0)
     lib.wvgx_set_tuning(19, 1)
     lib.wvgx_set_tuning(20, 0)
+    lib.wvgx_set_tuning(21, 16)
     c.destroy()
     ctx.close()
 

@@ -1240,6 +1240,12 @@ static int run_screen(wvg_corpus *c, const ScanArgs &a, const SearchPlan &p, cha
     L.cand = (uint64_t *)(ws + w.cand);
     L.flist = (uint32_t *)(ws + w.fl);
     L.nflag = (uint32_t *)(ws + w.nf);
+    L.pilot = &a;                             // exact K1 over the first tiles (the fallback's partials and
+    L.pilot_part = (uint64_t *)(ws + w.fbp);  // the result arrays are free until the rescan / final merge)
+    L.pilot_groups = std::max<uint32_t>(1, std::min<uint32_t>(p.fb_groups, 4));
+    L.pilot_ids = ids;
+    L.pilot_dists = dists;
+    L.pilot_counts = counts;
     WVG_HIP(launch_screen(L, s));
     uint64_t *keys = (uint64_t *)(ws + w.keys);
     WVG_HIP(launch_rescore_keys(c->metric, (const float *)a.queries, a.qpitch, (const float *)c->d_data, c->dim,
@@ -2241,7 +2247,7 @@ int wvgx_screen_counters(uint64_t *out4, int reset)
 // 9 = serpentine scan order, 10 = K3b row-range length, 11 = K1 load policy, 12 = K3b SIMD pairing,
 // 13 = K3b partner priority, 14 = PQ encode min3 argmin, 15 = co-scheduled PQ / BQ batches, 16 = co-scheduled BQ workgroups per CU, 17 = K3c row-range length,
 // 18 = K3c diagnostics (results not distances), 19 = K3c split launch,
-// 20 = screen kernel (0 K3d where it applies, 1 K3c).  Returns the previous value.
+// 20 = screen kernel (0 K3d where it applies, 1 K3c), 21 = screen pilot seed.  Returns the previous value.
 int wvgx_set_tuning(int key, int value)
 {
     Tuning &t = tuning();
@@ -2309,6 +2315,9 @@ int wvgx_set_tuning(int key, int value)
     } else if (key == 20) {
         old = t.screen_variant;
         t.screen_variant = value;
+    } else if (key == 21) {
+        old = t.screen_pilot;
+        t.screen_pilot = value;
     }
     return old;
 }

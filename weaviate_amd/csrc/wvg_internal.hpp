@@ -295,6 +295,14 @@ struct ScreenLaunch {
     uint64_t *cand;        // [nq][nrr * SCREEN_M]
     uint32_t *flist;       // [nq] flagged queries
     uint32_t *nflag;       // count
+    // pilot (optional): the exact K1 top-k of every query over the range's
+    // first tiles seeds the bound before the first phase
+    const ScanArgs *pilot = nullptr;
+    uint64_t *pilot_part = nullptr;  // [nq][pilot_groups][k] K1 partials
+    uint32_t pilot_groups = 1;
+    uint64_t *pilot_ids = nullptr;   // [nq][k] scratch (the caller's result arrays)
+    float *pilot_dists = nullptr;
+    uint32_t *pilot_counts = nullptr;
 };
 // screen + collect (the rescore, merge and rescan are launched by the host)
 hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s);
@@ -339,6 +347,7 @@ struct Tuning {
                              // for the whole pass), 1..256 = forced (A/B; env WVG_K1_TAIL)
     int pq_encode_min3 = 1;  // PQ encode pair path: min3 argmin on NaN-free codebooks (1) or the
                              // reference's compare-and-select loop everywhere (0; A/B and parity)
+    int screen_pilot = 16;   // K3c/K3d: tiles of the exact pilot scan that seeds the bound (0 = none; A/B)
     int screen_variant = 0;  // batched screen kernel: 0 = K3d where it applies (d = 512, 768), 1 = K3c (A/B)
     int screen_split = 1;    // K3c/K3d phases seeded from the earlier ones: 1 = up to three, 2 = two, 0 = one launch (A/B)
     int screen_range_blocks = 0;  // K3c row-range length in 256-row blocks (0 = auto, ~128; A/B)

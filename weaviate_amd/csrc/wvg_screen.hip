@@ -1082,6 +1082,23 @@ __global__ __launch_bounds__(256) void screen_collect_kernel(const uint64_t *par
     if (threadIdx.x == 0 && ovf) flist[atomicAdd(nflag, 1u)] = q;
 }
 
+__global__ __launch_bounds__(256) void screen_pilot_list_kernel(uint32_t *flist, uint32_t nq, uint32_t *nflag)
+{
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i < nq) flist[i] = i;
+    if (i == 0) *nflag = nq;
+}
+
+// gbound[q] = the ordered k-th exact distance of the pilot (when it found k rows)
+__global__ __launch_bounds__(256) void screen_pilot_seed_kernel(const float *dists, const uint32_t *counts, uint32_t nq,
+                                                               uint32_t k, uint32_t *gbound)
+{
+    const uint32_t q = blockIdx.x * 256 + threadIdx.x;
+    if (q >= nq || counts[q] < k) return;
+    const float t = dists[(size_t)q * k + k - 1];
+    if (t < __builtin_inff()) atomicMin(gbound + q, wvg_ord_f32(t));
+}
+
 // Whether K3c applies (the bound needs dim % 32 == 0 only for the fragment
 // layout; k <= SCREEN_M for the list to hold the k-th key).
 bool screen_supported(uint32_t dim, int metric, uint32_t k)
@@ -1136,6 +1153,33 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
     hipLaunchKernelGGL(screen_qconst_kernel, dim3(nq_pad / 4), dim3(256), 0, s, L.queries, L.nq, L.qpitch, L.dim,
                        nq_pad, L.cosine, L.nmax, L.k1, L.k2, L.emax);
     if ((e = hipMemsetAsync(L.gbound, 0xFF, (size_t)L.nq * 4, s)) != hipSuccess) return e;
+    uint64_t pilot_tiles = 16;
+#ifdef WVG_TOOLS
+    pilot_tiles = (uint64_t)std::max(tuning().screen_pilot, 0);
+#endif
+    if (L.pilot && pilot_tiles > 0) {
+        // Pilot: every query's exact top-k (K1, AVX2-order distances) over the
+        // range's first 16 tiles (1024 rows); its k-th distance bounds the final k-th
+        // (k real rows lie at or below it), so it seeds gbound before the
+        // first phase, whose lists otherwise start empty with no threshold
+        // and take an insertion for nearly every row of their first blocks.
+        ScanArgs f = *L.pilot;
+        f.nq = 1;
+        f.cosched = 0;
+        f.reverse = 0;
+        f.tile_end = std::min<uint64_t>(f.tile_end, f.tile_begin + pilot_tiles);
+        hipLaunchKernelGGL(screen_pilot_list_kernel, dim3((L.nq + 255) / 256), dim3(256), 0, s, L.flist, L.nq, L.nflag);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if ((e = launch_scan_f32_qlist(f, L.pilot_part, (int)L.pilot_groups, L.flist, L.nflag, L.nq, s)) !=
+            hipSuccess)
+            return e;
+        if ((e = launch_merge_lists_qlist(L.pilot_part, L.nq, L.pilot_groups, L.k, L.k, 0, L.pilot_ids, L.pilot_dists,
+                                          L.pilot_counts, L.flist, L.nflag, s)) != hipSuccess)
+            return e;
+        hipLaunchKernelGGL(screen_pilot_seed_kernel, dim3((L.nq + 255) / 256), dim3(256), 0, s, L.pilot_dists,
+                           L.pilot_counts, L.nq, L.k, L.gbound);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     if ((e = hipMemsetAsync(L.nflag, 0, 4, s)) != hipSuccess) return e;
     ScreenArgs a{};
     a.shadow = reinterpret_cast<const uint4 *>(L.shadow);
