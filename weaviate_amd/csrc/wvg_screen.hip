@@ -1072,13 +1072,26 @@ __global__ __launch_bounds__(256) void screen_collect_kernel(const uint64_t *par
         if (threadIdx.x == 0 && t < __builtin_inff()) atomicMin(gbound + q, wvg_ord_f32(t));
         return;
     }
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-        const uint64_t e = src[i];
+    __syncthreads();
+    if (threadIdx.x == 0) sh_total = 0;
+    __syncthreads();
+    // the kept keys are packed at the front of the query's row (the rescore's
+    // waves then run full; the merge reads an unordered key set), the rest is
+    // KEY_NONE
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t i0 = 0; i0 < n; i0 += blockDim.x) {
+        const uint32_t i = i0 + threadIdx.x;
+        const uint64_t e = i < n ? src[i] : WVG_KEY_NONE;
         const bool keep = e != WVG_KEY_NONE && key_lower(e) <= t;
-        dst[i] = keep ? e : WVG_KEY_NONE;
         if (keep && (i % SCREEN_M) == SCREEN_M - 1) ovf = 1;  // full list, last entry within tau*
+        const uint64_t bal = __ballot(keep);
+        uint32_t base = 0;
+        if (lane == 0 && bal) base = atomicAdd(&sh_total, (uint32_t)__popcll(bal));
+        base = __shfl(base, 0);
+        if (keep) dst[base + __popcll(bal & ((1ull << lane) - 1ull))] = e;
     }
     __syncthreads();
+    for (uint32_t i = sh_total + threadIdx.x; i < n; i += blockDim.x) dst[i] = WVG_KEY_NONE;
     if (threadIdx.x == 0 && ovf) flist[atomicAdd(nflag, 1u)] = q;
 }
 
