@@ -2610,7 +2610,8 @@ int wvg_pq_fit(wvg_ctx *ctx, const float *X, uint64_t n, uint32_t dim, uint32_t 
                  o_c = cv.take(pq_centers_alloc_bytes(m, ks, ds)), o_p = cv.take(n * m), o_code = cv.take(n * m),
                  o_mem = cv.take(n * m * 4), o_off = cv.take((size_t)m * ks * 4),
                  o_cnt = cv.take((size_t)m * ks * 4), o_chg = cv.take((size_t)m * 4), o_act = cv.take(m),
-                 o_rec = cv.take(m), o_skip = cv.take((size_t)m * ks);
+                 o_rec = cv.take(m), o_skip = cv.take((size_t)m * ks),
+                 o_bh = cv.take((size_t)m * kmeans_blocks(n) * ks * 4);
     Bulk bk(ctx);
     rc = bk.begin(cv.off);
     if (rc) return rc;
@@ -2620,6 +2621,7 @@ int wvg_pq_fit(wvg_ctx *ctx, const float *X, uint64_t n, uint32_t dim, uint32_t 
     uint32_t *dMem = (uint32_t *)(bk.b + o_mem), *dOff = (uint32_t *)(bk.b + o_off);
     uint32_t *dCnt = (uint32_t *)(bk.b + o_cnt), *dChg = (uint32_t *)(bk.b + o_chg);
     uint8_t *dAct = (uint8_t *)(bk.b + o_act), *dRec = (uint8_t *)(bk.b + o_rec), *dSkip = (uint8_t *)(bk.b + o_skip);
+    uint32_t *dBh = (uint32_t *)(bk.b + o_bh);
     WVG_HIP(hipMemcpyAsync(dX, X, n * dim * 4, hipMemcpyHostToDevice, s));
     // the training rows in the tiled layout K9 (the assignment) reads
     WVG_HIP(hipMemsetAsync(dXt, 0, tiles_of(n) * 64 * (size_t)nch * 16, s));
@@ -2653,7 +2655,7 @@ int wvg_pq_fit(wvg_ctx *ctx, const float *X, uint64_t n, uint32_t dim, uint32_t 
         // nNearest for every (row, segment): K9, the encoder (kmeans.go:103-135; ties to the
         // highest index); then changes and cluster sizes of the active segments
         WVG_HIP(launch_pq_encode(dXt, n, dim, dC, m, ks, dCode, s, false, false));
-        WVG_HIP(launch_kmeans_count(dCode, n, m, ks, dAct, dP, dChg, dCnt, s));
+        WVG_HIP(launch_kmeans_count(dCode, n, m, ks, dAct, dP, dChg, dCnt, dBh, s));
         WVG_HIP(hipMemcpyAsync(cnt.data(), dCnt, cnt.size() * 4, hipMemcpyDeviceToHost, s));
         WVG_HIP(hipMemcpyAsync(chg.data(), dChg, chg.size() * 4, hipMemcpyDeviceToHost, s));
         WVG_HIP(hipStreamSynchronize(s));
@@ -2693,7 +2695,7 @@ int wvg_pq_fit(wvg_ctx *ctx, const float *X, uint64_t n, uint32_t dim, uint32_t 
         WVG_HIP(hipMemcpyAsync(dSkip, skip.data(), skip.size(), hipMemcpyHostToDevice, s));
         // recalcCenters with the recluster assignment (the reseeded rows still
         // in their old clusters), then the reseeded clusters = their one row
-        WVG_HIP(launch_kmeans_recalc2(dX, n, dim, dP, m, ks, ds, dRec, dCnt, dSkip, dMem, dOff, dC, s));
+        WVG_HIP(launch_kmeans_recalc2(dX, n, dim, dP, m, ks, ds, dRec, dCnt, dBh, dSkip, dMem, dOff, dC, s));
         for (auto &mv : moves) {
             const uint32_t sg = mv.second.first, ci = mv.second.second;
             const uint8_t code = (uint8_t)ci;

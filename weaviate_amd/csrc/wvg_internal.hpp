@@ -467,12 +467,14 @@ hipError_t launch_emit_sorted(const uint64_t *sorted, uint64_t n, uint64_t id_ba
 // K10 (wvg_pq.hip): one Lloyd pass = K9 assignment, count, members, sums;
 // points segment-major [m][n]
 hipError_t launch_pq_pairs(const float *centers, uint32_t m, uint32_t ks, float *out, hipStream_t s);
+// row blocks per segment of the count / member kernels; bhist = [m][blocks][ks]
+uint32_t kmeans_blocks(uint64_t n);
 hipError_t launch_kmeans_count(const uint8_t *codes, uint64_t n, uint32_t m, uint32_t ks, const uint8_t *active,
-                               uint8_t *points, uint32_t *changes, uint32_t *counts, hipStream_t s);
+                               uint8_t *points, uint32_t *changes, uint32_t *counts, uint32_t *bhist, hipStream_t s);
 hipError_t launch_kmeans_recalc2(const float *X, uint64_t n, uint32_t dim, const uint8_t *points, uint32_t m,
                                  uint32_t ks, uint32_t ds, const uint8_t *recalc, const uint32_t *counts,
-                                 const uint8_t *skip, uint32_t *members, uint32_t *offsets, float *centers,
-                                 hipStream_t s);
+                                 const uint32_t *bhist, const uint8_t *skip, uint32_t *members, uint32_t *offsets,
+                                 float *centers, hipStream_t s);
 hipError_t launch_pq_sdc_table(int metric, const float *centers, uint32_t m, uint32_t ks, uint32_t ds,
                                float *table, hipStream_t s);
 hipError_t launch_pq_sdc_rows(int metric, const float *table, uint32_t m, uint32_t ks, const uint8_t *x,

@@ -1603,10 +1603,22 @@ hipError_t launch_pq_pairs(const float *centers, uint32_t m, uint32_t ks, float 
     return hipGetLastError();
 }
 
-// Block (s, b): rows [b * rows_per, (b + 1) * rows_per) of an active segment s.
+// Row blocks of the count / member kernels: at least 4096 rows, at most
+// KM_BLOCKS per segment (the member kernel sums the block histograms before
+// its own serially).
+constexpr uint32_t KM_BLOCKS = 64;
+uint64_t kmeans_rows_per(uint64_t n)
+{
+    const uint64_t r = (n + KM_BLOCKS - 1) / KM_BLOCKS;
+    return std::max<uint64_t>(4096, (r + 255) / 256 * 256);
+}
+uint32_t kmeans_blocks(uint64_t n) { return (uint32_t)((n + kmeans_rows_per(n) - 1) / kmeans_rows_per(n)); }
+
+// Block (s, b): rows [b * rows_per, (b + 1) * rows_per) of an active segment s;
+// its cluster histogram also goes to bhist[s][b] (the member kernel's bases).
 __global__ __launch_bounds__(256) void kmeans_count_kernel(const uint8_t *codes, uint64_t n, uint32_t m, uint32_t ks,
                                                            const uint8_t *active, uint8_t *points, uint32_t *changes,
-                                                           uint32_t *counts, uint64_t rows_per)
+                                                           uint32_t *counts, uint64_t rows_per, uint32_t *bhist)
 {
     __shared__ uint32_t hist[256];
     __shared__ uint32_t chg;
@@ -1628,63 +1640,80 @@ __global__ __launch_bounds__(256) void kmeans_count_kernel(const uint8_t *codes,
     }
     atomicAdd(&chg, mine);
     __syncthreads();
-    for (uint32_t c = threadIdx.x; c < ks; c += 256)
+    for (uint32_t c = threadIdx.x; c < ks; c += 256) {
         if (hist[c]) atomicAdd(&counts[(size_t)sg * ks + c], hist[c]);
+        bhist[((size_t)sg * gridDim.y + blockIdx.y) * ks + c] = hist[c];
+    }
     if (threadIdx.x == 0 && chg) atomicAdd(&changes[sg], chg);
 }
 
 hipError_t launch_kmeans_count(const uint8_t *codes, uint64_t n, uint32_t m, uint32_t ks, const uint8_t *active,
-                               uint8_t *points, uint32_t *changes, uint32_t *counts, hipStream_t s)
+                               uint8_t *points, uint32_t *changes, uint32_t *counts, uint32_t *bhist, hipStream_t s)
 {
-    const uint64_t rows_per = 4096;
-    hipLaunchKernelGGL(kmeans_count_kernel, dim3(m, (unsigned)((n + rows_per - 1) / rows_per)), dim3(256), 0, s, codes,
-                       n, m, ks, active, points, changes, counts, rows_per);
+    hipLaunchKernelGGL(kmeans_count_kernel, dim3(m, kmeans_blocks(n)), dim3(256), 0, s, codes, n, m, ks, active,
+                       points, changes, counts, kmeans_rows_per(n), bhist);
     return hipGetLastError();
 }
 
-// One block per recalculated segment: offsets = exclusive prefix of the
-// cluster sizes, then the rows in 256-row chunks: a row's place = its
-// cluster's running base + the same-cluster rows of earlier waves of the
-// chunk + those of lower lanes of its own wave (an 8-ballot match), so every
-// member list is in ascending row order.
+// Block (s, b) per recalculated segment s and row block b (the count
+// kernel's): a cluster's base = its offset (exclusive prefix of the cluster
+// sizes, an LDS scan) + its rows in the earlier blocks (bhist); then the
+// block's rows in 256-row chunks: a row's place = its cluster's running base +
+// the same-cluster rows of earlier waves of the chunk + those of lower lanes
+// of its own wave (an 8-ballot match), so every member list is in ascending
+// row order.  (Round 3 first had one block per segment walking all n rows
+// with a serial prefix: 324 us per pass at 100k rows.)
 __global__ __launch_bounds__(256) void kmeans_members_kernel(const uint8_t *points, uint64_t n, uint32_t ks,
-                                                             const uint32_t *counts, const uint8_t *recalc,
+                                                             const uint32_t *counts, const uint32_t *bhist,
+                                                             uint64_t rows_per, const uint8_t *recalc,
                                                              uint32_t *members, uint32_t *offsets)
 {
     __shared__ uint32_t base[256];
     __shared__ uint32_t wcnt[4][256];
-    const uint32_t sg = blockIdx.x;
+    const uint32_t sg = blockIdx.x, b = blockIdx.y;
     if (!recalc[sg]) return;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    if (tid == 0) {
-        uint32_t acc = 0;
-        for (uint32_t c = 0; c < ks; c++) {
-            base[c] = acc;
-            offsets[(size_t)sg * ks + c] = acc;
-            acc += counts[(size_t)sg * ks + c];
-        }
+    const uint32_t own = (uint32_t)tid < ks ? counts[(size_t)sg * ks + tid] : 0u;
+    uint32_t earlier = 0;
+    if ((uint32_t)tid < ks)
+        for (uint32_t bb = 0; bb < b; bb++) earlier += bhist[((size_t)sg * gridDim.y + bb) * ks + tid];
+    // inclusive scan of `own` over the 256 threads (Hillis-Steele in LDS)
+    base[tid] = own;
+    __syncthreads();
+    for (int d = 1; d < 256; d <<= 1) {
+        const uint32_t v = tid >= d ? base[tid - d] : 0u;
+        __syncthreads();
+        base[tid] += v;
+        __syncthreads();
+    }
+    const uint32_t off = base[tid] - own;
+    __syncthreads();
+    if ((uint32_t)tid < ks) {
+        if (b == 0) offsets[(size_t)sg * ks + tid] = off;
+        base[tid] = off + earlier;
     }
     for (int i = tid; i < 4 * 256; i += 256) (&wcnt[0][0])[i] = 0;
     __syncthreads();
     const uint8_t *pts = points + (size_t)sg * n;
     uint32_t *mem = members + (size_t)sg * n;
-    for (uint64_t p0 = 0; p0 < n; p0 += 256) {
+    const uint64_t r0 = (uint64_t)b * rows_per, r1 = min(n, r0 + rows_per);
+    for (uint64_t p0 = r0; p0 < r1; p0 += 256) {
         const uint64_t p = p0 + (uint64_t)tid;
-        const bool live = p < n;
+        const bool live = p < r1;
         const uint32_t c = live ? pts[p] : 0u;
         uint64_t same = __ballot(live);
 #pragma unroll
-        for (int b = 0; b < 8; b++) {
-            const uint64_t bb = __ballot(live && ((c >> b) & 1u));
-            same &= ((c >> b) & 1u) ? bb : ~bb;
+        for (int bit = 0; bit < 8; bit++) {
+            const uint64_t bb = __ballot(live && ((c >> bit) & 1u));
+            same &= ((c >> bit) & 1u) ? bb : ~bb;
         }
         const uint32_t below = (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
         if (live && below == 0) wcnt[w][c] = (uint32_t)__popcll(same);  // the lowest lane of each value
         __syncthreads();
         if (live) {
-            uint32_t off = base[c] + below;
-            for (int v = 0; v < w; v++) off += wcnt[v][c];
-            mem[off] = (uint32_t)p;
+            uint32_t o = base[c] + below;
+            for (int v = 0; v < w; v++) o += wcnt[v][c];
+            mem[o] = (uint32_t)p;
         }
         __syncthreads();
         for (uint32_t cc = (uint32_t)tid; cc < ks; cc += 256) {
@@ -1726,10 +1755,11 @@ __global__ __launch_bounds__(256) void kmeans_sum_kernel(const float *X, uint64_
 
 hipError_t launch_kmeans_recalc2(const float *X, uint64_t n, uint32_t dim, const uint8_t *points, uint32_t m,
                                  uint32_t ks, uint32_t ds, const uint8_t *recalc, const uint32_t *counts,
-                                 const uint8_t *skip, uint32_t *members, uint32_t *offsets, float *centers,
-                                 hipStream_t s)
+                                 const uint32_t *bhist, const uint8_t *skip, uint32_t *members, uint32_t *offsets,
+                                 float *centers, hipStream_t s)
 {
-    hipLaunchKernelGGL(kmeans_members_kernel, dim3(m), dim3(256), 0, s, points, n, ks, counts, recalc, members, offsets);
+    hipLaunchKernelGGL(kmeans_members_kernel, dim3(m, kmeans_blocks(n)), dim3(256), 0, s, points, n, ks, counts, bhist,
+                       kmeans_rows_per(n), recalc, members, offsets);
     const uint64_t total = (uint64_t)m * ks * ds;
     hipLaunchKernelGGL(kmeans_sum_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, X, n, dim, m, ks, ds,
                        members, offsets, counts, recalc, skip, centers);
