@@ -60,6 +60,8 @@ def parse(argv=None):
     ap.add_argument("--no-reuse-rows", type=int, default=4_000_000,
                     help="rows of the untimed no-reuse leg (frac_no_reuse); 8x the Infinity Cache at d = 128")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--configs", default="batched,bq,pq,slab",
+                    help="N = 1: BASELINE configs 2-5 measured after the headline (comma list; '' = none)")
     ap.add_argument("--profile-run", action="store_true",
                     help="only the timed headline launches (no no-reuse leg, read probe or CPU baseline), so a "
                          "rocprofv3 --stats summary of the scan kernel covers exactly the launches `roofline` times")
@@ -235,6 +237,353 @@ def cpu_pq_leg(target_s, threads, gpu_check):
                    f"LUT + sequential ADC + heap restated in C, oracle/wv_oracle.c orc_bench_pq), {secs:.1f} s wall "
                    f"on {threads} threads"),
     }
+
+
+# ---------------------------------------------------------------------------
+# BASELINE configs 2-5 on this GPU (rank 0, N = 1): the named shapes at full
+# per-GPU size through the host C ABI (what the Go binding calls), each timed
+# with HIP events bound to its dominant kernel and spot-checked afterwards.
+BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md; no 2:1 sparsity)
+# PQ encode: 5.5 VALU instructions per (row, segment, centroid) -- the reference's
+# unfused sub, mul, add per dimension, two centroids per packed op -- at one wave64
+# VALU instruction per SIMD per 4 cycles, 1024 SIMDs, 2.4 GHz
+PQ_ENCODE_PEAK_ROWS = 1024 * 2.4e9 / 4 * 64 / (32 * 256 * 5.5)
+
+
+def gpu_clock(dev, torch):
+    """Lease identity next to the roofline: the GPU's current shader / memory
+    clock levels from amdgpu's sysfs (read-only text), or None."""
+    try:
+        p = torch.cuda.get_device_properties(dev)
+        bdf = f"{getattr(p, 'pci_domain_id', 0):04x}:{p.pci_bus_id:02x}:{getattr(p, 'pci_device_id', 0):02x}.0"
+    except Exception:  # noqa: BLE001 -- no PCI location: no clock reading
+        return None
+    out = {"pci": bdf}
+    for name in ("pp_dpm_sclk", "pp_dpm_mclk", "pp_dpm_fclk"):
+        try:
+            lines = open(f"/sys/bus/pci/devices/{bdf}/{name}").read().splitlines()
+            cur = [ln.split(":", 1)[1].strip().rstrip("*").strip() for ln in lines if ln.rstrip().endswith("*")]
+            out[name[7:]] = cur[0] if cur else None
+        except (OSError, IndexError):
+            out[name[7:]] = None
+    return out
+
+
+def _prof(lib, ctx):
+    import ctypes
+
+    from weaviate_amd._lib import check
+
+    ms, nl = ctypes.c_double(), ctypes.c_uint64()
+    check(lib.wvg_profile_stop(ctx.handle, ctypes.byref(ms), ctypes.byref(nl)))
+    return ms.value / 1e3, int(nl.value)
+
+
+def _sorted_ok(orc, d):
+    return bool(np.all(np.diff(orc.ord_key(np.asarray(d, np.float32)).astype(np.int64)) >= 0))
+
+
+def _outside_ok(orc, sample_ids, sample_d, ids, dists):
+    """No sampled row outside the result is ahead of the k-th in (distance, id) order."""
+    outside = ~np.isin(sample_ids, np.asarray(ids).astype(np.int64))
+    kd, kid = int(orc.ord_key(np.asarray(dists[-1:], np.float32))[0]), int(ids[-1])
+    sk = orc.ord_key(np.asarray(sample_d, np.float32)[outside]).astype(np.int64)
+    return bool(np.all((sk > kd) | ((sk == kd) & (sample_ids[outside] > kid))))
+
+
+def _bits(x):
+    return np.asarray(x, np.float32).view(np.uint32)
+
+
+def config_batched(ctx, orc, metric_name, metric, reps=3):
+    """configs[1]: 10M x 768 fp32 dot / cosine, 1024-query batches (bf16 MFMA
+    screen + exact fp32 rescore); frac = 2 Q N d FLOP / the screen launches'
+    time vs the dense bf16 peak."""
+    from weaviate_amd._lib import KIND_F32
+    from weaviate_amd.device import Corpus
+
+    n, d, Q, k = 10_000_000, 768, 1024, 10
+    lib = ctx.lib
+    c = Corpus(ctx, KIND_F32, metric, d, n)
+    c.fill_synthetic(42, n, 0)
+    qs = orc.synth_rows(43, 0, Q, d, 0)
+    c.search(qs, k)  # untimed: builds the bf16 shadow
+    lib.wvg_profile_start(ctx.handle)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ids, dists, counts = c.search(qs, k)
+    wall = (time.perf_counter() - t0) / reps
+    ks, nl = _prof(lib, ctx)
+    screen_s = ks / reps  # the screen launches of one batch (one event pair spans its phases)
+    flop = 2.0 * Q * n * d
+    # spot check (checker only): rows sampled at the start, middle and end
+    starts = [0, n // 2 - 3, n - 10_000]
+    sample_ids = np.concatenate([np.arange(s, s + 10_000, dtype=np.int64) for s in starts])
+    srows = np.concatenate([orc.synth_rows(42, s, 10_000, d, 0) for s in starts])
+    om = 2 if metric_name == "cosine" else 1
+    if om == 2:
+        srows = orc.normalize_rows(srows)
+    ok = bool(np.all(counts == k))
+    for qi in (0, Q - 1):
+        q = orc.normalize(qs[qi]) if om == 2 else qs[qi]
+        got = np.stack([orc.synth_rows(42, int(i), 1, d, 0)[0] for i in ids[qi]])
+        if om == 2:
+            got = orc.normalize_rows(got)
+        ok &= _sorted_ok(orc, dists[qi])
+        ok &= bool(np.array_equal(_bits(orc.dist_all(om, q, got)), _bits(dists[qi])))
+        ok &= _outside_ok(orc, sample_ids, orc.dist_all(om, q, srows), ids[qi], dists[qi])
+    c.destroy()
+    tflops = flop / screen_s / 1e12
+    return {"workload": f"{n:,} x {d} fp32 {metric_name}, {Q}-query batches, exact {k}-NN (host API wvg_search)",
+            "qps": round(Q / wall, 1), "batch_ms": round(wall * 1e3, 3), "batches": reps,
+            "kernel": "bf16 MFMA screen (K3d screen_ar_kernel<24>) + exact fp32 AVX2-order rescore",
+            "roofline": {"bound": "mfma", "achieved": round(tflops, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(tflops / BF16_PEAK_TFLOPS, 4), "screen_ms_per_batch": round(screen_s * 1e3, 3),
+                         "frac_whole_batch": round(flop / wall / 1e12 / BF16_PEAK_TFLOPS, 4),
+                         "flop_per_batch": flop},
+            "check": {"ok": ok, "how": "queries 0 and 1023: results sorted, every distance a bit-exact oracle "
+                                       "recomputation of its row, no row of 30k sampled (start / middle / end) "
+                                       "ahead of the k-th; all counts = k"}}
+
+
+def config_bq(ctx, orc, nq=8):
+    """configs[2]: 100M x 1536 BQ (cosine) Hamming top-200 + exact fp32 rescore
+    to 10 (flat.searchByVectorBQ, V/flat/index.go:347-389).  The 614 GB of
+    float rows do not fit one GPU: the R rows are regenerated by id into the
+    caller's pinned gather buffer (stand-in for the LSM gets, timed apart) and
+    rescored through wvg_rescore.  frac: 19.2 GB of codes per scan."""
+    from weaviate_amd._lib import KIND_BQ, METRIC_COSINE, check, fptr, u32ptr, u64ptr
+    from weaviate_amd.device import Corpus
+
+    n, d, k, R = 100_000_000, 1536, 10, 200
+    w = (d + 63) // 64
+    lib = ctx.lib
+    c = Corpus(ctx, KIND_BQ, METRIC_COSINE, d, n)
+    c.fill_synthetic(42, n, 0)
+    qs = orc.synth_rows(43, 0, nq, d, 0)
+    c.search(qs[0], R)
+    rows = ctx.host_array((R, d), np.float32)
+    res, t_fetch = [], 0.0
+    lib.wvg_profile_start(ctx.handle)
+    t0 = time.perf_counter()
+    for i in range(nq):
+        ids, hd, cnt = c.search(qs[i], R)
+        t1 = time.perf_counter()
+        cand = np.ascontiguousarray(ids[0, :cnt[0]])
+        check(lib.wvg_synthetic_rows(ctx.handle, 42, u64ptr(cand), len(cand), d, 0, 1, fptr(rows)))
+        t_fetch += time.perf_counter() - t1
+        qn = np.empty(d, np.float32)
+        check(lib.wvg_normalize_batch(ctx.handle, fptr(qs[i]), 1, d, fptr(qn)))
+        oi, od, oc = np.empty(k, np.uint64), np.empty(k, np.float32), np.zeros(1, np.uint32)
+        check(lib.wvg_rescore(ctx.handle, METRIC_COSINE, fptr(qn), fptr(rows), u64ptr(cand), len(cand), d, k,
+                              u64ptr(oi), fptr(od), u32ptr(oc)))
+        res.append((ids[0], hd[0], cand, oi.copy(), od.copy()))
+    wall = (time.perf_counter() - t0) / nq
+    scan_s, nl = _prof(lib, ctx)
+    scan_s /= max(1, nl)
+    # batch mode: nq queries per call (co-scheduled K5), Hamming top-R only
+    c.search(qs, R)
+    t0 = time.perf_counter()
+    for _ in range(3):
+        c.search(qs, R)
+    wall_b = (time.perf_counter() - t0) / (3 * nq)
+    # spot check: sampled codes vs the oracle's encoder, Hamming results and the rescore
+    starts = [0, n // 2 - 13, n - 10_000]
+    sample_ids = np.concatenate([np.arange(s, s + 10_000, dtype=np.int64) for s in starts])
+    scodes = np.concatenate([orc.bq_encode_rows(orc.normalize_rows(orc.synth_rows(42, s, 10_000, d, 0)))
+                             for s in starts])
+    got, okb = c.get_batch(sample_ids[::499].astype(np.uint64))
+    ok = bool(okb.all() and np.array_equal(got, scodes[::499]))
+    for qi in (0, nq - 1):
+        hid, hdist, cand, oi, od = res[qi]
+        qc = orc.bq_encode(orc.normalize(qs[qi]))
+        codes, okc = c.get_batch(hid.astype(np.uint64))
+        ok &= bool(okc.all() and np.array_equal(_bits(orc.bq_dist_all(qc, codes.reshape(R, w))), _bits(hdist)))
+        ok &= bool(np.all(np.diff(hdist) >= 0)) and _outside_ok(orc, sample_ids, orc.bq_dist_all(qc, scodes), hid, hdist)
+        frows = orc.normalize_rows(np.stack([orc.synth_rows(42, int(i), 1, d, 0)[0] for i in cand]))
+        ed = orc.dist_all(2, orc.normalize(qs[qi]), frows)
+        wi, wd = orc.lex_topk(ed, cand.astype(np.uint64), k)
+        ok &= bool(np.array_equal(oi, wi) and np.array_equal(_bits(od), _bits(wd)))
+    ctx.free_host_array(rows)
+    c.destroy()
+    by = n * w * 8
+    gbps = by / scan_s / 1e9
+    return {"workload": f"{n:,} x {d} BQ (cosine, {w} words/row), Hamming top-{R} + exact fp32 rescore to {k}",
+            "qps": round(1 / wall, 2), "qps_without_row_fetch": round(1 / (wall - t_fetch / nq), 2),
+            "row_fetch_stand_in_ms": round(t_fetch / nq * 1e3, 3), "scan_ms": round(scan_s * 1e3, 3),
+            "batch_call_qps": round(1 / wall_b, 2), "batch_call_queries": nq,
+            "kernel": "K5 scan_bq_kernel (XOR + popcount, fused top-200)",
+            "roofline": {"bound": "hbm", "achieved": round(gbps, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(gbps / HBM_PEAK_GBS, 4), "bytes_per_scan": by},
+            "check": {"ok": ok, "how": "sampled codes = oracle BQ encode; queries 0 and last: Hamming distances "
+                                       "bit-exact on the returned codes, sorted, no sampled code (30k) ahead of the "
+                                       "R-th; rescore = oracle lexicographic top-10 of the 200 candidates, bit-exact"}}
+
+
+def config_pq(ctx, orc, nq=16):
+    """configs[3]: 100M x 128 PQ (m = 32, ks = 256): ProductQuantizer.Fit on
+    the first 100k rows, the bulk encode of all 100M rows (K9), then ADC
+    top-10 (K8e; LUT in LDS).  frac: 3.2 GB of codes per scan (HBM); the
+    encode against the packed-op peak of its instruction mix."""
+    from weaviate_amd._lib import KIND_F32, KIND_PQ, METRIC_L2, check, fptr, u32ptr, u64ptr
+    from weaviate_amd.device import Corpus
+
+    n, d, m, ks, k = 100_000_000, 128, 32, 256, 10
+    lib = ctx.lib
+    f = Corpus(ctx, KIND_F32, METRIC_L2, d, n)
+    f.fill_synthetic(42, n, 0)
+    nt = 100_000
+    trows = np.empty((nt, d), np.float32)
+    check(lib.wvg_synthetic_rows(ctx.handle, 42, u64ptr(np.arange(nt, dtype=np.uint64)), nt, d, 0, 0, fptr(trows)))
+    centers = np.empty((m, ks, d // m), np.float32)
+    passes = np.zeros(m, np.uint32)
+    t0 = time.perf_counter()
+    check(lib.wvg_pq_fit(ctx.handle, fptr(trows), nt, d, m, ks, 100_000, 7, fptr(centers), u32ptr(passes)))
+    fit_s = time.perf_counter() - t0
+    pq = Corpus(ctx, KIND_PQ, METRIC_L2, d, n)
+    pq.set_codebook(centers)
+    ctx.synchronize()
+    enc = []
+    for _ in range(2):
+        t0 = time.perf_counter()
+        check(lib.wvg_pq_encode_corpus(pq.handle, f.handle))
+        ctx.synchronize()
+        enc.append(time.perf_counter() - t0)
+    enc_s = min(enc)
+    f.destroy()
+    qs = orc.synth_rows(43, 0, nq, d, 0)
+    for i in range(32):  # untimed: clocks settle after the encode
+        pq.search(qs[i % nq], k)
+    lib.wvg_profile_start(ctx.handle)
+    res = []
+    t0 = time.perf_counter()
+    for i in range(nq):
+        res.append(pq.search(qs[i], k))
+    wall = (time.perf_counter() - t0) / nq
+    scan_s, nl = _prof(lib, ctx)
+    scan_s /= max(1, nl)
+    pq.search(qs, k)
+    t0 = time.perf_counter()
+    for _ in range(4):
+        pq.search(qs, k)
+    wall_b = (time.perf_counter() - t0) / (4 * nq)
+    # spot check: sampled codes vs the oracle encoder, ADC results on the returned codes
+    starts = [0, n // 2 - 7, n - 20_000]
+    sample_ids = np.concatenate([np.arange(s, s + 20_000, dtype=np.int64) for s in starts])
+    scodes = orc.pq_encode(np.concatenate([orc.synth_rows(42, s, 20_000, d, 0) for s in starts]), centers)
+    got, okb = pq.get_batch(sample_ids.astype(np.uint64), pq_m=m)
+    ok = bool(okb.all() and np.array_equal(got, scodes))
+    for qi in (0, nq - 1):
+        ids, dists, counts = res[qi]
+        lut = orc.pq_lut(0, qs[qi], centers)
+        codes, okc = pq.get_batch(ids[0].astype(np.uint64), pq_m=m)
+        ok &= bool(counts[0] == k and okc.all())
+        ok &= bool(np.array_equal(_bits([orc.pq_adc(0, lut, cc) for cc in codes]), _bits(dists[0])))
+        ok &= _sorted_ok(orc, dists[0])
+        ok &= _outside_ok(orc, sample_ids, [orc.pq_adc(0, lut, cc) for cc in scodes], ids[0], dists[0])
+    pq.destroy()
+    gbps = n * m / scan_s / 1e9
+    return {"workload": f"{n:,} x {d} fp32 -> PQ m={m} ks={ks}: fit (100k rows) + bulk encode + ADC top-{k}",
+            "qps": round(1 / wall, 2), "scan_ms": round(scan_s * 1e3, 4), "batch_call_qps": round(1 / wall_b, 2),
+            "batch_call_queries": nq, "fit_s": round(fit_s, 3), "lloyd_passes_mean": round(float(passes.mean()), 2),
+            "encode_s": round(enc_s, 4), "encode_rows_per_s": round(n / enc_s, 1),
+            "encode_frac_of_packed_op_peak": round(n / enc_s / PQ_ENCODE_PEAK_ROWS, 4),
+            "kernel": "K8e scan_pq32_wide_kernel (LUT image in LDS); encode K9 pq_encode_kernel",
+            "roofline": {"bound": "hbm", "achieved": round(gbps, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(gbps / HBM_PEAK_GBS, 4), "bytes_per_scan": n * m},
+            "check": {"ok": ok, "how": "60k sampled codes (start / middle / end) = oracle encode; queries 0 and "
+                                       "last: ADC distances bit-exact on the returned codes, sorted, no sampled "
+                                       "row ahead of the k-th"}}
+
+
+def config_slab(ctx, orc, dev, torch, nq=8):
+    """configs[4], one GPU's share: a 125M x 128 fp32 L2 slab holding global
+    docIDs [375M, 500M), exact 100-NN, nq single-query scans per
+    query-stream launch (device API).  frac: 64 GB per query scan."""
+    from weaviate_amd._lib import KIND_F32, METRIC_L2, check
+    from weaviate_amd.device import Corpus
+
+    n, d, k, base = 125_000_000, 128, 100, 375_000_000
+    lib = ctx.lib
+    c = Corpus(ctx, KIND_F32, METRIC_L2, d, n, id_base=base)
+    c.fill_synthetic(42, n, 0)
+    qs = orc.synth_rows(43, 0, nq, d, 0)
+    tq = torch.from_numpy(qs).to(dev)
+    ids = torch.empty((nq, k), dtype=torch.int64, device=dev)
+    dd = torch.empty((nq, k), dtype=torch.float32, device=dev)
+    cc = torch.empty(nq, dtype=torch.int32, device=dev)
+    wsb = lib.wvg_search_workspace_size(c.handle, nq, k)
+    ws = torch.zeros(wsb, dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+
+    def run():
+        check(lib.wvg_search_device_pipelined(c.handle, tq.data_ptr(), nq, k, ids.data_ptr(), dd.data_ptr(),
+                                              cc.data_ptr(), ws.data_ptr(), wsb, st))
+
+    run()
+    torch.cuda.synchronize(dev)
+    lib.wvg_profile_start(ctx.handle)
+    t0 = time.perf_counter()
+    reps = 2
+    for _ in range(reps):
+        run()
+    torch.cuda.synchronize(dev)
+    wall = (time.perf_counter() - t0) / (reps * nq)
+    ks_, nl = _prof(lib, ctx)
+    check(lib.wvg_search_device_check(ctx.handle, ws.data_ptr(), st))
+    scan_s = ks_ / max(1, nl) / nq
+    hi, hd, hc = ids.cpu().numpy().view(np.uint64), dd.cpu().numpy(), cc.cpu().numpy()
+    starts = [base, base + n // 2 - 5, base + n - 20_000]
+    sample_ids = np.concatenate([np.arange(s, s + 20_000, dtype=np.int64) for s in starts])
+    srows = np.concatenate([orc.synth_rows(42, s, 20_000, d, 0) for s in starts])
+    ok = bool(np.all(hc == k))
+    for qi in (0, nq - 1):
+        ok &= bool(np.all((hi[qi] >= base) & (hi[qi] < base + n))) and _sorted_ok(orc, hd[qi])
+        got = np.stack([orc.synth_rows(42, int(i), 1, d, 0)[0] for i in hi[qi]])
+        ok &= bool(np.array_equal(_bits(orc.dist_all(0, qs[qi], got)), _bits(hd[qi])))
+        ok &= _outside_ok(orc, sample_ids, orc.dist_all(0, qs[qi], srows), hi[qi], hd[qi])
+    c.destroy()
+    gbps = n * d * 4 / scan_s / 1e9
+    return {"workload": f"{n:,} x {d} fp32 L2 slab (global docIDs [{base:,}, {base + n:,}): slab 3 of the 1B corpus), "
+                        f"exact {k}-NN, {nq} single-query scans per query-stream launch",
+            "qps_per_slab": round(1 / wall, 2), "scan_ms_per_query": round(scan_s * 1e3, 3),
+            "qps_1b_one_gpu_8_slabs": round(1 / (8 * wall), 3),
+            "kernel": "K1 scan_f32_stream_kernel<L2,128,2>",
+            "roofline": {"bound": "hbm", "achieved": round(gbps, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(gbps / HBM_PEAK_GBS, 4), "bytes_per_scan": n * d * 4},
+            "check": {"ok": ok, "how": "queries 0 and last: ids inside the slab, sorted, distances bit-exact "
+                                       "recomputations, no row of 60k sampled ahead of the k-th; all counts = k"}}
+
+
+def run_configs(args, dev, torch):
+    """The configs object of the bench line (N = 1): BASELINE configs 2-5."""
+    from oracle import wv_oracle as orc  # the spot checks' checker only, never the measured path
+    from weaviate_amd.device import Context
+
+    want = [s for s in args.configs.split(",") if s]
+    ctx = Context(dev.index)
+    out = {}
+    t_all = time.perf_counter()
+    for name in want:
+        t0 = time.perf_counter()
+        try:
+            if name == "batched":
+                from weaviate_amd._lib import METRIC_COSINE, METRIC_DOT
+
+                out["config2_batched_10m_x_768"] = {"cosine": config_batched(ctx, orc, "cosine", METRIC_COSINE),
+                                                    "dot": config_batched(ctx, orc, "dot", METRIC_DOT)}
+            elif name == "bq":
+                out["config3_bq_100m_x_1536"] = config_bq(ctx, orc)
+            elif name == "pq":
+                out["config4_pq_100m_x_128"] = config_pq(ctx, orc)
+            elif name == "slab":
+                out["config5_slab_125m_x_128"] = config_slab(ctx, orc, dev, torch)
+        except Exception as e:  # noqa: BLE001 -- a failed leg is reported, the headline stands
+            out[f"{name}_error"] = f"{type(e).__name__}: {e}"
+        print(f"bench.py: config leg {name} {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
+    out["wall_s"] = round(time.perf_counter() - t_all, 1)
+    ctx.close()
+    return out
 
 
 # ---------------------------------------------------------------------------
@@ -437,6 +786,7 @@ def run_flat1m(args, world, rank, dev, torch, dist):
             "ceiling_GBps": None if args.profile_run else round(ceiling, 1),
             "frac_of_ceiling_no_reuse": (round(achieved_nr / ceiling, 4)
                                          if not args.profile_run and ceiling > 0 else None),
+            "gpu_clock": gpu_clock(dev, torch),
             "note": ("`achieved` = ALGORITHMIC bytes (N*d*4 per query scan, every query a full scan) / the "
                      "kernel's average launch time, Infinity-Cache reuse included: consecutive scans alternate "
                      "direction and read the last ~320 MB of each pass with the default cache policy "
@@ -448,7 +798,10 @@ def run_flat1m(args, world, rank, dev, torch, dist):
                      "streaming read) in this run.  `traffic`: see traffic_source"),
         },
         "cpu_baseline": None,
+        "configs": None,
     }
+    if rank == 0 and world == 1 and args.configs and not args.profile_run:
+        out["configs"] = run_configs(args, dev, torch)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_run:
         cq = np.random.default_rng(43).uniform(-1, 1, (16, d)).astype(np.float32)
         gids, _, _ = corpus.search(cq, k)  # GPU results of the baseline's first queries (full-size cross-check)

@@ -137,3 +137,44 @@ def test_search_device_bq_pq_equals_host_search(ctx, orc, kind, metric, d):
         wi, wd = orc.lex_topk(all_d[valid], np.arange(n, dtype=np.uint64)[valid], k)
         assert np.array_equal(hid[qi], wi) and np.array_equal(bits(hd[qi]), bits(wd))
     c.destroy()
+
+
+# The Go binding's empty-AllowList rule at the C ABI (V/flat/index.go:423-427):
+# a non-null bitmap with no bit set -- all-zero words, or zero words -- gives
+# counts of 0 on every search path; only a null bitmap means "no filter".
+@pytest.mark.parametrize("kind", [KIND_F32, KIND_BQ, KIND_PQ])
+def test_non_null_all_zero_allow_bitmap_returns_nothing(ctx, orc, kind):
+    import ctypes
+
+    from weaviate_amd._lib import fptr, u32ptr, u64ptr
+
+    n, d, k = 3000, 64, 10
+    rows = orc.synth_rows(611, 0, n, d, 0)
+    c = Corpus(ctx, kind, METRIC_L2, d, n)
+    if kind == KIND_PQ:
+        c.set_codebook(np.ascontiguousarray(rows[:256].reshape(256, 16, 4).transpose(1, 0, 2)))
+    c.upsert(np.arange(n, dtype=np.uint64), rows)
+    lib = _lib.load()
+    for nq in (1, 3, 40):
+        qs = np.ascontiguousarray(orc.synth_rows(612, 0, nq, d, 0))
+        for words in (np.zeros((n + 63) // 64, np.uint64), np.zeros(1, np.uint64)[:0]):
+            aw = np.zeros(max(1, len(words)), np.uint64)  # a real (non-null) buffer even for zero words
+            ids = np.full((nq, k), 7, np.uint64)
+            dists = np.zeros((nq, k), np.float32)
+            counts = np.full(nq, 99, np.uint32)
+            _lib.check(lib.wvg_search(c.handle, fptr(qs), nq, k, u64ptr(aw), len(words), u64ptr(ids), fptr(dists),
+                                      u32ptr(counts)))
+            assert np.all(counts == 0), (nq, len(words), counts)
+            assert np.all(ids == np.uint64(2**64 - 1)) and np.all(np.isinf(dists))
+        # the null bitmap is the unfiltered search
+        _, _, counts = c.search(qs, k)
+        assert np.all(counts == k)
+    cnt = ctypes.c_uint64(5)
+    out_i = np.zeros(16, np.uint64)
+    out_d = np.zeros(16, np.float32)
+    aw = np.zeros((n + 63) // 64, np.uint64)
+    if kind == KIND_F32:
+        _lib.check(lib.wvg_search_by_distance(c.handle, fptr(rows[0]), 1e30, -1, u64ptr(aw), len(aw), u64ptr(out_i),
+                                              fptr(out_d), 16, ctypes.byref(cnt)))
+        assert cnt.value == 0
+    c.destroy()

@@ -1,0 +1,378 @@
+// wvg_ctx.hip -- context, stream pool, errors, profiling and the tools-build
+// tuning knobs of the C ABI (include/wvgpu.h).  Errors are returned as
+// negative codes with a thread-local message; no HIP failure aborts the
+// process (no panics across cgo).
+
+#include "wvg_host.hpp"
+
+namespace wvg {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string &msg) { g_last_error = msg; }
+
+int fail(int code, const std::string &msg)
+{
+    g_last_error = msg;
+    return code;
+}
+
+int StreamSlot::device_scratch(size_t bytes, void **out)
+{
+    if (bytes > dscratch_bytes) {
+        if (dscratch) (void)hipFree(dscratch);
+        dscratch = nullptr;
+        dscratch_bytes = 0;
+        size_t want = std::max(bytes, (size_t)1 << 20);
+        hipError_t e = hipMalloc(&dscratch, want);
+        if (e != hipSuccess) return fail(WVG_ERR_NOMEM, std::string("scratch hipMalloc: ") + hipGetErrorString(e));
+        dscratch_bytes = want;
+    }
+    *out = dscratch;
+    return WVG_OK;
+}
+
+int StreamSlot::host_pinned(size_t bytes, void **out)
+{
+    if (bytes > hpinned_bytes) {
+        if (hpinned) (void)hipHostFree(hpinned);
+        hpinned = nullptr;
+        hpinned_bytes = 0;
+        size_t want = std::max(bytes, (size_t)1 << 16);
+        hipError_t e = hipHostMalloc(&hpinned, want, hipHostMallocDefault);
+        if (e != hipSuccess) return fail(WVG_ERR_NOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+        hpinned_bytes = want;
+    }
+    *out = hpinned;
+    return WVG_OK;
+}
+
+// Next free profiling event pair of the context (grown on demand).
+int prof_pair(wvg_ctx *ctx, std::pair<hipEvent_t, hipEvent_t> *out)
+{
+    std::lock_guard<std::mutex> g(ctx->prof_mu);
+    if (ctx->prof_used == ctx->prof_events.size()) {
+        hipEvent_t a, b;
+        WVG_HIP(hipEventCreate(&a));
+        WVG_HIP(hipEventCreate(&b));
+        ctx->prof_events.emplace_back(a, b);
+    }
+    *out = ctx->prof_events[ctx->prof_used++];
+    return WVG_OK;
+}
+
+}  // namespace wvg
+
+using namespace wvg;
+
+extern "C" {
+
+// ---------------------------------------------------------------------------
+int wvg_ctx::acquire(StreamSlot **out)
+{
+    {
+        std::lock_guard<std::mutex> g(pool_mu);
+        if (!free_slots.empty()) {
+            *out = free_slots.back();
+            free_slots.pop_back();
+            return WVG_OK;
+        }
+    }
+    StreamSlot *s = new StreamSlot();
+    hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete s;
+        return fail(WVG_ERR_DEVICE, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+    }
+    std::lock_guard<std::mutex> g(pool_mu);
+    all_slots.push_back(s);
+    *out = s;
+    return WVG_OK;
+}
+
+void wvg_ctx::release(StreamSlot *s)
+{
+    std::lock_guard<std::mutex> g(pool_mu);
+    free_slots.push_back(s);
+}
+
+int wvg_abi_version(void) { return WVG_ABI_VERSION; }
+
+const char *wvg_last_error(void) { return g_last_error.c_str(); }
+
+int wvg_device_count(int *out)
+{
+    if (!out) return fail(WVG_ERR_INVALID, "null out");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        *out = 0;
+        return fail(WVG_ERR_DEVICE, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+    }
+    *out = n;
+    return WVG_OK;
+}
+
+void wvg_options_default(wvg_options *o)
+{
+    if (!o) return;
+    *o = wvg_options{};
+    o->size = (uint32_t)sizeof(wvg_options);
+    o->mfma_min_queries = 32;
+    o->cache_reuse = 1;
+    o->merge_wait_us = 0;
+    o->batch_screen = 1;
+}
+
+int wvg_open(int device, wvg_ctx **out) { return wvg_open_ex(device, nullptr, out); }
+
+int wvg_open_ex(int device, const wvg_options *opts, wvg_ctx **out)
+{
+    if (!out) return fail(WVG_ERR_INVALID, "null out");
+    *out = nullptr;
+    wvg_options o;
+    wvg_options_default(&o);
+    if (opts) {
+        if (opts->size != sizeof(wvg_options)) return fail(WVG_ERR_INVALID, "wvg_options.size mismatch");
+        o = *opts;
+    }
+    int n = 0;
+    WVG_HIP(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) return fail(WVG_ERR_INVALID, "device index out of range");
+    WVG_HIP(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    WVG_HIP(hipGetDeviceProperties(&prop, device));
+    wvg_ctx *c = new wvg_ctx();
+    c->device = device;
+    c->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    c->opt = o;
+#ifdef WVG_TOOLS
+    if (const char *e = getenv("WVG_MFMA_MIN_QUERIES")) c->opt.mfma_min_queries = (uint32_t)strtoul(e, nullptr, 10);
+    if (const char *e = getenv("WVG_SERPENTINE")) tuning().serpentine = (int)strtol(e, nullptr, 10);  // A/B runs
+    if (const char *e = getenv("WVG_K1_TAIL")) tuning().k1_tail = (int)strtol(e, nullptr, 10);        // A/B runs
+    if (const char *e = getenv("WVG_K1_LOADS")) tuning().k1_loads = (int)strtol(e, nullptr, 10);        // A/B runs
+#endif
+    *out = c;
+    return WVG_OK;
+}
+
+int wvg_close(wvg_ctx *ctx)
+{
+    if (!ctx) return WVG_OK;
+    (void)hipSetDevice(ctx->device);
+    for (auto &e : ctx->prof_events) {
+        (void)hipEventDestroy(e.first);
+        (void)hipEventDestroy(e.second);
+    }
+    for (StreamSlot *s : ctx->all_slots) {
+        (void)hipStreamSynchronize(s->stream);
+        if (s->dscratch) (void)hipFree(s->dscratch);
+        if (s->hpinned) (void)hipHostFree(s->hpinned);
+        (void)hipStreamDestroy(s->stream);
+        delete s;
+    }
+    delete ctx;
+    return WVG_OK;
+}
+
+int wvg_set_distance_order(wvg_ctx *ctx, int order)
+{
+    if (!ctx) return fail(WVG_ERR_INVALID, "null ctx");
+    if (order != WVG_ORDER_AVX256 && order != WVG_ORDER_AVX512) return fail(WVG_ERR_INVALID, "unknown distance order");
+    ctx->order512 = order == WVG_ORDER_AVX512;
+    return WVG_OK;
+}
+
+int wvg_synchronize(wvg_ctx *ctx)
+{
+    if (!ctx) return fail(WVG_ERR_INVALID, "null ctx");
+    WVG_HIP(hipSetDevice(ctx->device));
+    WVG_HIP(hipDeviceSynchronize());
+    return WVG_OK;
+}
+
+int wvg_host_alloc(wvg_ctx *ctx, uint64_t bytes, void **out)
+{
+    if (!ctx || !out) return fail(WVG_ERR_INVALID, "null argument");
+    *out = nullptr;
+    if (bytes == 0) return WVG_OK;
+    WVG_HIP(hipSetDevice(ctx->device));
+    hipError_t e = hipHostMalloc(out, bytes, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        *out = nullptr;
+        return fail(WVG_ERR_NOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+    }
+    return WVG_OK;
+}
+
+int wvg_host_free(wvg_ctx *ctx, void *p)
+{
+    if (!ctx) return fail(WVG_ERR_INVALID, "null context");
+    if (!p) return WVG_OK;
+    WVG_HIP(hipSetDevice(ctx->device));
+    WVG_HIP(hipHostFree(p));
+    return WVG_OK;
+}
+
+#ifdef WVG_TOOLS
+// tools build: K3c counters [row-block epilogues (per wave), slow-path entries, insert calls, 0]
+int wvgx_screen_counters(uint64_t *out4, int reset)
+{
+    if (!out4) return WVG_ERR_INVALID;
+    wvg::screen_counters(out4, reset != 0);
+    return WVG_OK;
+}
+
+// A/B knob of the tools build (not part of include/wvgpu.h): 0 = K1 scan variant,
+// 1 = K1 resident workgroups per CU, ... 7 = K8 ADC variant, 8 = query-stream merge wait (us),
+// 9 = serpentine scan order, 10 = K3b row-range length, 11 = K1 load policy, 12 = K3b SIMD pairing,
+// 13 = K3b partner priority, 14 = PQ encode min3 argmin, 15 = co-scheduled PQ / BQ batches, 16 = co-scheduled BQ workgroups per CU, 17 = K3c row-range length,
+// 18 = K3c diagnostics (results not distances), 19 = K3c split launch,
+// 20 = screen kernel (0 K3d where it applies, 1 K3c), 21 = screen pilot seed.  Returns the previous value.
+int wvgx_set_tuning(int key, int value)
+{
+    Tuning &t = tuning();
+    int old = -1;
+    if (key == 0) {
+        old = t.scan_variant;
+        t.scan_variant = value;
+    } else if (key == 1) {
+        old = t.groups_per_cu;
+        t.groups_per_cu = value;
+    } else if (key == 2) {
+        old = t.pipeline_mode;
+        t.pipeline_mode = value;
+    } else if (key == 3) {
+        old = t.gemm_pf;
+        t.gemm_pf = value;
+    } else if (key == 4) {
+        old = t.gemm_kernel;
+        t.gemm_kernel = value;
+    } else if (key == 5) {
+        old = t.gemm_skew;
+        t.gemm_skew = value;
+    } else if (key == 6) {
+        old = t.gemm_lockstep;
+        t.gemm_lockstep = value;
+    } else if (key == 7) {
+        old = t.pq_variant;
+        t.pq_variant = value;
+    } else if (key == 8) {
+        old = t.merge_wait_us;
+        t.merge_wait_us = value;
+    } else if (key == 9) {
+        old = t.serpentine;
+        t.serpentine = value;
+    } else if (key == 10) {
+        old = t.gemm_range_tiles;
+        t.gemm_range_tiles = value;
+    } else if (key == 11) {
+        old = t.k1_loads;
+        t.k1_loads = value;
+    } else if (key == 12) {
+        old = t.gemm_pairing;
+        t.gemm_pairing = value;
+    } else if (key == 13) {
+        old = t.gemm_prio;
+        t.gemm_prio = value;
+    } else if (key == 14) {
+        old = t.pq_encode_min3;
+        t.pq_encode_min3 = value;
+    } else if (key == 15) {
+        old = t.pq_cosched;
+        t.pq_cosched = value;
+    } else if (key == 16) {
+        old = t.bq_cos_gpc;
+        t.bq_cos_gpc = value;
+    } else if (key == 17) {
+        old = t.screen_range_blocks;
+        t.screen_range_blocks = value;
+    } else if (key == 18) {
+        old = t.screen_diag;
+        t.screen_diag = value;
+    } else if (key == 19) {
+        old = t.screen_split;
+        t.screen_split = value;
+    } else if (key == 20) {
+        old = t.screen_variant;
+        t.screen_variant = value;
+    } else if (key == 21) {
+        old = t.screen_pilot;
+        t.screen_pilot = value;
+    }
+    return old;
+}
+#endif
+
+int wvg_measure_hbm_read(wvg_ctx *ctx, uint64_t bytes, uint32_t reps, double *out_gbps)
+{
+    if (!ctx || !out_gbps) return fail(WVG_ERR_INVALID, "null argument");
+    *out_gbps = 0.0;
+    bytes = bytes / 4096 * 4096;
+    if (bytes == 0 || reps == 0) return fail(WVG_ERR_INVALID, "bytes and reps must be > 0");
+    WVG_HIP(hipSetDevice(ctx->device));
+    void *buf = nullptr;
+    if (hipMalloc(&buf, bytes + 256) != hipSuccess) return fail(WVG_ERR_NOMEM, "probe buffer hipMalloc");
+    SlotGuard g(ctx);
+    hipEvent_t a = nullptr, b = nullptr;
+    auto done = [&](int rc) {
+        if (g.slot) (void)hipStreamSynchronize(g.slot->stream);
+        if (a) (void)hipEventDestroy(a);
+        if (b) (void)hipEventDestroy(b);
+        (void)hipFree(buf);
+        return rc;
+    };
+    int rc = ctx->acquire(&g.slot);
+    if (rc) return done(rc);
+    const hipStream_t s = g.slot->stream;
+    float *sink = (float *)((char *)buf + bytes);
+    if (hipMemsetAsync(buf, 0, bytes + 256, s) != hipSuccess || hipEventCreate(&a) != hipSuccess ||
+        hipEventCreate(&b) != hipSuccess)
+        return done(fail(WVG_ERR_DEVICE, "probe setup"));
+    double best = 0.0;
+    // grid-stride forms, then the scans' contiguous-chunk form (negative = chunk workgroups)
+    for (int blocks : {1024, 2048, 4096, 8192, -256, -512, -1024, -2048}) {
+        for (int w = 0; w < 2; w++)
+            if (launch_hbm_read(buf, bytes, blocks, sink, s) != hipSuccess) return done(fail(WVG_ERR_DEVICE, "probe"));
+        (void)hipEventRecord(a, s);
+        for (uint32_t r = 0; r < reps; r++)
+            if (launch_hbm_read(buf, bytes, blocks, sink, s) != hipSuccess) return done(fail(WVG_ERR_DEVICE, "probe"));
+        (void)hipEventRecord(b, s);
+        float ms = 0.f;
+        if (hipEventSynchronize(b) != hipSuccess || hipEventElapsedTime(&ms, a, b) != hipSuccess || ms <= 0.f)
+            return done(fail(WVG_ERR_DEVICE, "probe timing"));
+        best = std::max(best, (double)bytes * reps / (ms * 1e-3) / 1e9);
+    }
+    *out_gbps = best;
+    return done(WVG_OK);
+}
+
+int wvg_profile_start(wvg_ctx *ctx)
+{
+    if (!ctx) return fail(WVG_ERR_INVALID, "null ctx");
+    std::lock_guard<std::mutex> g(ctx->prof_mu);
+    ctx->prof_used = 0;
+    ctx->profiling.store(true);
+    return WVG_OK;
+}
+
+int wvg_profile_stop(wvg_ctx *ctx, double *scan_ms_total, uint64_t *scan_launches)
+{
+    if (!ctx) return fail(WVG_ERR_INVALID, "null ctx");
+    WVG_HIP(hipSetDevice(ctx->device));
+    ctx->profiling.store(false);
+    std::lock_guard<std::mutex> g(ctx->prof_mu);
+    double total = 0.0;
+    for (size_t i = 0; i < ctx->prof_used; i++) {
+        WVG_HIP(hipEventSynchronize(ctx->prof_events[i].second));
+        float ms = 0.0f;
+        WVG_HIP(hipEventElapsedTime(&ms, ctx->prof_events[i].first, ctx->prof_events[i].second));
+        total += ms;
+    }
+    if (scan_ms_total) *scan_ms_total = total;
+    if (scan_launches) *scan_launches = ctx->prof_used;
+    ctx->prof_used = 0;
+    return WVG_OK;
+}
+
+}  // extern "C"
