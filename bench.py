@@ -60,7 +60,7 @@ def parse(argv=None):
     ap.add_argument("--no-reuse-rows", type=int, default=4_000_000,
                     help="rows of the untimed no-reuse leg (frac_no_reuse); 8x the Infinity Cache at d = 128")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--configs", default="batched,bq,pq,slab",
+    ap.add_argument("--configs", default="host_api,batched,bq,pq,slab",
                     help="N = 1: BASELINE configs 2-5 measured after the headline (comma list; '' = none)")
     ap.add_argument("--profile-run", action="store_true",
                     help="only the timed headline launches (no no-reuse leg, read probe or CPU baseline), so a "
@@ -555,6 +555,86 @@ def config_slab(ctx, orc, dev, torch, nq=8):
                                        "recomputations, no row of 60k sampled ahead of the k-th; all counts = k"}}
 
 
+def config_host_api(ctx, orc, callers=(1, 16), seconds=1.0):
+    """The headline shape through the host API the Go binding calls: T caller
+    threads (goroutines) each issuing single-query wvg_search calls (1M x 128
+    L2, k = 10) for `seconds`; concurrent calls on one corpus are coalesced
+    into shared launches inside the library (wvg_options.coalesce).  frac (one
+    caller): N*d*4 bytes per call / the call's wall time vs 8 TB/s."""
+    import threading
+
+    from weaviate_amd._lib import KIND_F32, METRIC_L2, check, fptr, u32ptr, u64ptr
+    from weaviate_amd.device import Context, Corpus
+
+    n, d, k = 1_000_000, 128, 10
+    qs = np.ascontiguousarray(orc.synth_rows(43, 0, 256, d, 0))
+    out = {"workload": f"{n:,} x {d} fp32 L2 exact {k}-NN, one query per wvg_search call, T concurrent callers"}
+    for coalesce in (1, 0):
+        cx = ctx if coalesce else Context(ctx.device, coalesce=0)
+        lib = cx.lib
+        c = Corpus(cx, KIND_F32, METRIC_L2, d, n)
+        c.fill_synthetic(42, n, 0)
+        qp = [fptr(qs[i]) for i in range(len(qs))]
+
+        def call(i, bufs):
+            check(lib.wvg_search(c.handle, qp[i % len(qs)], 1, k, None, 0, *bufs[1]))
+
+        def bufs_new():
+            ids, ds, cnt = np.empty(k, np.uint64), np.empty(k, np.float32), np.empty(1, np.uint32)
+            return (ids, ds, cnt), (u64ptr(ids), fptr(ds), u32ptr(cnt))
+
+        # check: 16 concurrent calls return exactly what serial calls return
+        serial = []
+        for i in range(16):
+            b = bufs_new()
+            call(i, b)
+            serial.append((b[0][0].copy(), b[0][1].copy()))
+        got = [None] * 16
+
+        def one(i):
+            b = bufs_new()
+            call(i, b)
+            got[i] = (b[0][0].copy(), b[0][1].copy())
+
+        th = [threading.Thread(target=one, args=(i,)) for i in range(16)]
+        [t.start() for t in th]
+        [t.join() for t in th]
+        same = all(np.array_equal(g[0], s[0]) and np.array_equal(g[1].view(np.uint32), s[1].view(np.uint32))
+                   for g, s in zip(got, serial))
+        for T in callers:
+            done = [0] * T
+            start = threading.Barrier(T + 1)
+            stop_at = [0.0]
+
+            def worker(t):
+                b = bufs_new()
+                i = t
+                start.wait()
+                while time.perf_counter() < stop_at[0]:
+                    call(i, b)
+                    i += T
+                    done[t] += 1
+
+            th = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+            [t.start() for t in th]
+            stop_at[0] = time.perf_counter() + seconds + 0.2
+            start.wait()
+            t0 = time.perf_counter()
+            [t.join() for t in th]
+            el = time.perf_counter() - t0
+            qps = sum(done) / el
+            rec = {"qps": round(qps, 1), "calls": sum(done)}
+            if T == 1:
+                rec["us_per_call"] = round(1e6 / qps, 2)
+                rec["frac_of_8TBs"] = round(n * d * 4 * qps / 1e9 / HBM_PEAK_GBS, 4)
+            out[f"{'coalesced' if coalesce else 'uncoalesced'}_callers_{T}"] = rec
+        out[f"{'coalesced' if coalesce else 'uncoalesced'}_16_concurrent_equal_serial"] = bool(same)
+        c.destroy()
+        if not coalesce:
+            cx.close()
+    return out
+
+
 def run_configs(args, dev, torch):
     """The configs object of the bench line (N = 1): BASELINE configs 2-5."""
     from oracle import wv_oracle as orc  # the spot checks' checker only, never the measured path
@@ -578,6 +658,8 @@ def run_configs(args, dev, torch):
                 out["config4_pq_100m_x_128"] = config_pq(ctx, orc)
             elif name == "slab":
                 out["config5_slab_125m_x_128"] = config_slab(ctx, orc, dev, torch)
+            elif name == "host_api":
+                out["config1_host_api"] = config_host_api(ctx, orc)
         except Exception as e:  # noqa: BLE001 -- a failed leg is reported, the headline stands
             out[f"{name}_error"] = f"{type(e).__name__}: {e}"
         print(f"bench.py: config leg {name} {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
@@ -669,6 +751,36 @@ def no_reuse_leg(args, dev, torch, n, d, k, B, tq, P, launches):
     return ms.value / 1e3 / max(1, nl.value), gbps.value
 
 
+MERGE_CHECK_MAX_ROWS = 8_500_000  # the merged-result check's oracle regenerates every row on the host
+
+
+def merge_check(ranges, d, k, qs, got_ids, got_d):
+    """Rank 0's check of the multi-GPU merge (Index.objectVectorSearch,
+    adapters/repos/db/index.go:1567-1648) for the queries qs: the merged ids /
+    distances equal the oracle's lexicographic top-k over every rank's or
+    slab's rows, regenerated from the synthetic generator.  ranges: (first
+    docID, rows) of each shard.  Checker only: runs after the timed region."""
+    from oracle import wv_oracle as orc
+
+    total = sum(r[1] for r in ranges)
+    if total > MERGE_CHECK_MAX_ROWS:
+        return {"ok": None, "skipped": f"{total:,} rows above the host oracle's {MERGE_CHECK_MAX_ROWS:,}"}
+    ok = True
+    for qi in range(len(qs)):
+        bi, bd = np.empty(0, np.uint64), np.empty(0, np.float32)
+        for base, nrows in ranges:
+            for r0 in range(0, nrows, 1_000_000):
+                m = min(1_000_000, nrows - r0)
+                rows = orc.synth_rows(42, base + r0, m, d, 0)
+                ci, cd = orc.lex_topk(orc.dist_all(0, qs[qi], rows),
+                                      np.arange(base + r0, base + r0 + m, dtype=np.uint64), k)
+                bi, bd = orc.lex_topk(np.concatenate([bd, cd]), np.concatenate([bi, ci]), k)
+        ok &= bool(np.array_equal(np.asarray(got_ids[qi]).view(np.uint64), bi)
+                   and np.array_equal(np.asarray(got_d[qi], np.float32).view(np.uint32), bd.view(np.uint32)))
+    return {"ok": ok, "queries": len(qs), "rows": total,
+            "how": "merged ids and distance bits = the oracle's lexicographic top-k over every shard's rows"}
+
+
 def run_flat1m(args, world, rank, dev, torch, dist):
     from weaviate_amd._lib import KIND_F32, METRIC_L2, check
     from weaviate_amd.device import Context, Corpus
@@ -731,6 +843,15 @@ def run_flat1m(args, world, rank, dev, torch, dist):
     scan_ms, launches = ctypes.c_double(), ctypes.c_uint64()
     check(lib.wvg_profile_stop(ctx.handle, ctypes.byref(scan_ms), ctypes.byref(launches)))
     check(lib.wvg_search_device_check(ctx.handle, ws.data_ptr(), stream))  # no merge gave up in the timed run
+    mcheck = None
+    if world > 1:  # the last step's exchanged + merged lists against the oracle (untimed)
+        torch.cuda.synchronize(dev)
+        last = args.warmup + args.steps - 1
+        q0 = (last * B) % P
+        if rank == 0:
+            mcheck = merge_check([(r * cap, n) for r in range(world)], d, k, qs[q0:q0 + 2],
+                                 m_ids[last % 2][:2].cpu().numpy(), m_d[last % 2][:2].cpu().numpy())
+        dist.barrier()
 
     total_queries = world * B * args.steps  # 1M-row query scans over all GPUs
     avg_launch_s = scan_ms.value / 1e3 / max(1, launches.value)
@@ -799,6 +920,7 @@ def run_flat1m(args, world, rank, dev, torch, dist):
         },
         "cpu_baseline": None,
         "configs": None,
+        "merge_check": mcheck,
     }
     if rank == 0 and world == 1 and args.configs and not args.profile_run:
         out["configs"] = run_configs(args, dev, torch)
@@ -889,6 +1011,19 @@ def run_slab1b(args, world, rank, dev, torch, dist):
                                                 m_d[t].data_ptr(), m_c[t].data_ptr(), stream))
 
     elapsed += _timed(merge_all, dist, world, dev, torch)
+    # the last step's merged lists against the oracle (untimed; small corpora only)
+    mcheck = None
+    if rank == 0:
+        if world > 1:
+            gi, gd = m_ids[steps - 1][:2].cpu().numpy(), m_d[steps - 1][:2].cpu().numpy()
+        else:  # one GPU: the local merge wrote the packed block (ids [B][k], then dists)
+            blkh = send.cpu().numpy()
+            gi = blkh[:B * k * 8].view(np.uint64).reshape(B, k)[:2]
+            gd = blkh[B * k * 8:B * k * 12].view(np.float32).reshape(B, k)[:2]
+        mcheck = merge_check([(s * per, max(0, min(per, total - s * per))) for s in range(S)], d, k,
+                             qs[(steps - 1) * B:(steps - 1) * B + 2].cpu().numpy(), gi, gd)
+    if world > 1:
+        dist.barrier()
     avg_launch_s = scan_ms_tot / 1e3 / max(1, launches_tot)
     bytes_per_launch = per * d * 4 * B
     achieved = bytes_per_launch / avg_launch_s / 1e9
@@ -928,6 +1063,7 @@ def run_slab1b(args, world, rank, dev, torch, dist):
             "launches": launches_tot,
         },
         "cpu_baseline": None,
+        "merge_check": mcheck,
     }
 
 

@@ -134,12 +134,14 @@ type Options struct {
 	CacheReuse     int32  // 1: consecutive scans reuse the Infinity Cache (default); 0: streaming
 	MergeWaitUs    uint32 // query-stream merge wait bound (default 4 s)
 	BatchScreen    int32  // 1: bf16 screen + exact rescore for batches (default); 0: exact fp32 MFMA only
+	Coalesce       int32  // 1: concurrent single-query searches of a corpus share launches (default)
 }
 
 func DefaultOptions() Options {
 	var o C.wvg_options
 	C.wvg_options_default(&o)
-	return Options{uint32(o.mfma_min_queries), int32(o.cache_reuse), uint32(o.merge_wait_us), int32(o.batch_screen)}
+	return Options{uint32(o.mfma_min_queries), int32(o.cache_reuse), uint32(o.merge_wait_us), int32(o.batch_screen),
+		int32(o.coalesce)}
 }
 
 func OpenWith(device int, o Options) (*Ctx, error) {
@@ -153,6 +155,7 @@ func OpenWith(device int, o Options) (*Ctx, error) {
 	}
 	opt.cache_reuse = C.int32_t(o.CacheReuse)
 	opt.batch_screen = C.int32_t(o.BatchScreen)
+	opt.coalesce = C.int32_t(o.Coalesce)
 	var h *C.wvg_ctx
 	if e := err(C.wvg_open_ex(C.int(device), &opt, &h)); e != nil {
 		return nil, e

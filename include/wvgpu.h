@@ -79,7 +79,15 @@ typedef struct wvg_options {
                                   query gets empty results and wvg_search_device_check fails. */
     int32_t batch_screen;      /* 1 (default): batched dot / cosine searches screen every row with bf16
                                   MFMA and a per-row error bound, then rescore the candidates exactly in
-                                  fp32 (results identical to the exact path); 0: exact fp32 MFMA only. */
+                                  fp32 (results identical to the exact path); 0: exact fp32 MFMA only.
+                                  The first screened search of a corpus allocates its bf16 shadow:
+                                  2 * dim bytes per row of capacity + 4 bytes of row-norm bound per row
+                                  (15.4 GB at 10M x 768), kept until the corpus is destroyed or grows. */
+    int32_t coalesce;          /* 1 (default): concurrent single-query wvg_search calls on one corpus
+                                  (no allow list) join one batched launch -- while a batch runs, the calls
+                                  that arrive queue up and the next batch takes them all; each caller gets
+                                  exactly its own results (identical to a call of its own); a lone call
+                                  does not wait.  0: every call launches on its own. */
 } wvg_options;
 void wvg_options_default(wvg_options *opts);
 int wvg_open_ex(int device, const wvg_options *opts, wvg_ctx **out);

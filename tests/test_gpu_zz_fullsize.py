@@ -174,3 +174,84 @@ def test_full_size_slab_125m_global_ids_properties(ctx, orc):
         sk = orc.ord_key(sd[outside]).astype(np.int64)
         assert np.all((sk > kth[0]) | ((sk == kth[0]) & (sample_ids[outside] > kth[1])))
     c.destroy()
+
+
+def _exact_topk_chunked(orc, metric, q, seed, n, d, k, chunk=1_000_000, normalize=False):
+    """The oracle's lexicographic top-k of q over all n synthetic rows
+    (generated chunk by chunk, so the whole corpus never sits in host memory)."""
+    best_i = np.empty(0, np.uint64)
+    best_d = np.empty(0, np.float32)
+    for r0 in range(0, n, chunk):
+        rows = orc.synth_rows(seed, r0, min(chunk, n - r0), d, 0)
+        if normalize:
+            rows = orc.normalize_rows(rows)
+        dd = orc.dist_all(metric, q, rows)
+        ci, cd = orc.lex_topk(dd, np.arange(r0, r0 + len(rows), dtype=np.uint64), k)
+        best_i, best_d = orc.lex_topk(np.concatenate([best_d, cd]), np.concatenate([best_i, ci]), k)
+    return best_i, best_d
+
+
+# Full size (BASELINE config 2, dot): 10M x 768 fp32 dot, one 1024-query batch
+# through the bf16 screen + exact rescore -- properties on sampled rows for four
+# queries, and the whole 10M-row oracle top-k for two of them.
+def test_full_size_batched_10m_x_768_dot_exact(ctx, orc):
+    n, d, nq, k = 10_000_000, 768, 1024, 10
+    c = Corpus(ctx, KIND_F32, _lib.METRIC_DOT, d, n)
+    c.fill_synthetic(42, n, 0)
+    qs = orc.synth_rows(43, 0, nq, d, 0)
+    ids, dists, counts = c.search(qs, k)
+    assert np.all(counts == k)
+    starts = [0, n // 2 - 3, n - 10_000]
+    sample_ids = np.concatenate([np.arange(s, s + 10_000, dtype=np.int64) for s in starts])
+    srows = np.concatenate([orc.synth_rows(42, s, 10_000, d, 0) for s in starts])
+    for qi in (0, 1, 511, 1023):
+        assert np.all(np.diff(orc.ord_key(dists[qi]).astype(np.int64)) >= 0)
+        got = np.stack([orc.synth_rows(42, int(i), 1, d, 0)[0] for i in ids[qi]])
+        assert np.array_equal(bits(orc.dist_all(1, qs[qi], got)), bits(dists[qi]))
+        sd = orc.dist_all(1, qs[qi], srows)
+        outside = ~np.isin(sample_ids, ids[qi].astype(np.int64))
+        kth = (int(orc.ord_key(dists[qi][-1:])[0]), int(ids[qi][-1]))
+        sk = orc.ord_key(sd[outside]).astype(np.int64)
+        assert np.all((sk > kth[0]) | ((sk == kth[0]) & (sample_ids[outside] > kth[1])))
+    for qi in (0, 1023):  # the exact answer over all 10M rows
+        wi, wd = _exact_topk_chunked(orc, 1, qs[qi], 42, n, d, k)
+        assert np.array_equal(ids[qi], wi), qi
+        assert np.array_equal(bits(dists[qi]), bits(wd)), qi
+    c.destroy()
+
+
+# Config 3 at the largest size that fits with its float rows resident: 10M x
+# 1536 fp32 (61 GB) + its BQ codes, flat.searchByVectorBQ with the exact
+# rescore on the device (wvg_search_bq_rescore, R = 200, k = 10;
+# V/flat/index.go:347-389).  The result must be the oracle's top-10 of the
+# 200 Hamming candidates, and the candidates the Hamming top-200 (sampled
+# property, as the 100M test).
+def test_full_size_bq_rescore_10m_x_1536_resident(ctx, orc):
+    from weaviate_amd.device import search_bq_rescore
+
+    n, d, R, k = 10_000_000, 1536, 200, 10
+    f = Corpus(ctx, KIND_F32, METRIC_COSINE, d, n)
+    f.fill_synthetic(42, n, 0)
+    bq = Corpus(ctx, KIND_BQ, METRIC_COSINE, d, n)
+    bq.fill_synthetic(42, n, 0)
+    qs = orc.synth_rows(43, 0, 4, d, 0)
+    ids, dists, counts = search_bq_rescore(bq, f, qs, k, R)
+    cand, hd, hc = bq.search(qs, R)  # the Hamming top-R (the same kernel the flow runs)
+    starts = [0, n // 2 - 13, n - 10_000]
+    sample_ids = np.concatenate([np.arange(s, s + 10_000, dtype=np.int64) for s in starts])
+    scodes = orc.bq_encode_rows(orc.normalize_rows(np.concatenate([orc.synth_rows(42, s, 10_000, d, 0)
+                                                                     for s in starts])))
+    for qi in range(len(qs)):
+        assert counts[qi] == k and hc[qi] == R
+        qn = orc.normalize(qs[qi])
+        qc = orc.bq_encode(qn)
+        sd = orc.bq_dist_all(qc, scodes)
+        outside = ~np.isin(sample_ids, cand[qi].astype(np.int64))
+        kd, kid = float(hd[qi][-1]), int(cand[qi][-1])
+        assert np.all((sd[outside] > kd) | ((sd[outside] == kd) & (sample_ids[outside] > kid)))
+        rows = orc.normalize_rows(np.stack([orc.synth_rows(42, int(i), 1, d, 0)[0] for i in cand[qi]]))
+        wi, wd = orc.lex_topk(orc.dist_all(2, qn, rows), cand[qi].astype(np.uint64), k)
+        assert np.array_equal(ids[qi], wi), qi
+        assert np.array_equal(bits(dists[qi]), bits(wd)), qi
+    f.destroy()
+    bq.destroy()

@@ -34,7 +34,7 @@ METRIC_BY_NAME = {"l2-squared": METRIC_L2, "dot": METRIC_DOT, "cosine": METRIC_C
 class Options(ctypes.Structure):
     """struct wvg_options (include/wvgpu.h): context options fixed at wvg_open_ex."""
     _fields_ = [("size", c_uint32), ("mfma_min_queries", c_uint32), ("cache_reuse", ctypes.c_int32),
-                ("merge_wait_us", c_uint32), ("batch_screen", ctypes.c_int32)]
+                ("merge_wait_us", c_uint32), ("batch_screen", ctypes.c_int32), ("coalesce", ctypes.c_int32)]
 
 
 # name -> (restype, argtypes); every symbol declared in include/wvgpu.h.

@@ -32,6 +32,24 @@ int StreamSlot::device_scratch(size_t bytes, void **out)
     return WVG_OK;
 }
 
+int StreamSlot::control(uint32_t **out)
+{
+    if (!dctl) {
+        void *p = nullptr;
+        hipError_t e = hipMalloc(&p, 256);
+        if (e == hipSuccess) e = hipMemsetAsync(p, 0, 256, stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(stream);
+        if (e != hipSuccess) {
+            if (p) (void)hipFree(p);
+            return fail(WVG_ERR_NOMEM, std::string("slot control block: ") + hipGetErrorString(e));
+        }
+        dctl = (uint32_t *)p;
+        arrival_base = 0;
+    }
+    *out = dctl;
+    return WVG_OK;
+}
+
 int StreamSlot::host_pinned(size_t bytes, void **out)
 {
     if (bytes > hpinned_bytes) {
@@ -122,6 +140,7 @@ void wvg_options_default(wvg_options *o)
     o->cache_reuse = 1;
     o->merge_wait_us = 0;
     o->batch_screen = 1;
+    o->coalesce = 1;
 }
 
 int wvg_open(int device, wvg_ctx **out) { return wvg_open_ex(device, nullptr, out); }
@@ -168,6 +187,7 @@ int wvg_close(wvg_ctx *ctx)
         (void)hipStreamSynchronize(s->stream);
         if (s->dscratch) (void)hipFree(s->dscratch);
         if (s->hpinned) (void)hipHostFree(s->hpinned);
+        if (s->dctl) (void)hipFree(s->dctl);
         (void)hipStreamDestroy(s->stream);
         delete s;
     }

@@ -5,6 +5,8 @@
 #include <hip/hip_ext.h>
 
 #include <atomic>
+#include <condition_variable>
+#include <deque>
 #include <mutex>
 #include <shared_mutex>
 #include <string>
@@ -34,8 +36,14 @@ struct StreamSlot {
     size_t dscratch_bytes = 0;
     void *hpinned = nullptr;
     size_t hpinned_bytes = 0;
+    // a single-query host search's in-launch merge: a persistent arrival counter
+    // (and the merge's status word) on the device, and the count the next
+    // launch starts from -- no per-call memset
+    uint32_t *dctl = nullptr;
+    uint32_t arrival_base = 0;
     int device_scratch(size_t bytes, void **out);
     int host_pinned(size_t bytes, void **out);
+    int control(uint32_t **out);  // dctl, allocated and zeroed on first use
 };
 
 }  // namespace wvg
@@ -55,6 +63,17 @@ struct wvg_ctx {
     std::mutex prof_mu;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_events;
     size_t prof_used = 0;
+};
+
+// Concurrent single-query wvg_search calls on one corpus (one goroutine per
+// Weaviate query) join one batched launch: a request queue, and at most one
+// batch of it executing at a time (wvg_search.hip, search_coalesced).
+struct wvg_search_request;
+struct wvg_coalescer {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<wvg_search_request *> pending;
+    bool busy = false;  // a batch is executing
 };
 
 struct wvg_corpus {
@@ -85,6 +104,7 @@ struct wvg_corpus {
     hipEvent_t sh_ready = nullptr; // the last build, for searches on other streams
     std::shared_mutex rw;          // shared: search; exclusive: upsert/delete/grow
     std::atomic<uint64_t> scan_serial{0};  // query scans issued so far (parity = next scan direction)
+    wvg_coalescer co;                      // single-query searches batched across callers
 };
 
 namespace wvg {
@@ -245,7 +265,8 @@ hipError_t launch_scan_f32(const ScanArgs &a, uint64_t *partials, int groups, hi
 constexpr uint32_t WVG_STATUS_MERGE_TIMEOUT = 1u;
 struct StreamJob {
     uint64_t *partials;  // [nq][groups][k]
-    uint32_t *arrivals;  // [nq], zero at launch
+    uint32_t *arrivals;  // [nq], arrival_base at launch
+    uint32_t arrival_base;  // 0 for a zeroed workspace; a stream slot's running count otherwise
     uint32_t *status;    // WVG_STATUS_MERGE_TIMEOUT set if the merge workgroup gave up waiting
     uint64_t wait_limit; // merge workgroup's wait per query, s_memrealtime ticks (100 MHz)
     uint32_t groups;
@@ -431,10 +452,12 @@ hipError_t launch_pq_lut(int metric, const float *q, uint32_t nq, uint32_t qpitc
                          const float *centers, uint32_t m, uint32_t ks, uint32_t ds, float *lut,
                          hipStream_t s);
 // codes: row-major [n][m] bytes, or (tiled_out) the PQ corpus layout at slots 0..n-1.
-// nan_free: the codebook holds no NaN (enables the pair path's min3 argmin, pq_encode_kernel).
+// nan_free: the codebook holds no NaN (enables the pair path's min3 argmin, pq_encode_kernel);
+// seg_nan: per-segment NaN flags on the device (launch_pq_pairs), the same per segment.
+// Row-major codes of fewer rows than fill the chip split the segments over the grid.
 hipError_t launch_pq_encode(const float *tiled_rows, uint64_t n, uint32_t dim, const float *centers,
                             uint32_t m, uint32_t ks, uint8_t *codes, hipStream_t s, bool tiled_out = false,
-                            bool nan_free = false);
+                            bool nan_free = false, const uint32_t *seg_nan = nullptr);
 inline bool pq_nan_free(const float *centers, size_t count)
 {
     for (size_t i = 0; i < count; i++)
@@ -466,7 +489,9 @@ hipError_t launch_emit_sorted(const uint64_t *sorted, uint64_t n, uint64_t id_ba
 // k-means training (wvg_pq.hip K10) and the PQ symmetric-distance table.
 // K10 (wvg_pq.hip): one Lloyd pass = K9 assignment, count, members, sums;
 // points segment-major [m][n]
-hipError_t launch_pq_pairs(const float *centers, uint32_t m, uint32_t ks, float *out, hipStream_t s);
+// seg_nan (optional): m words, nonzero where a segment's centroids hold a NaN
+hipError_t launch_pq_pairs(const float *centers, uint32_t m, uint32_t ks, float *out, hipStream_t s,
+                           uint32_t *seg_nan = nullptr);
 // row blocks per segment of the count / member kernels; bhist = [m][blocks][ks]
 uint32_t kmeans_blocks(uint64_t n);
 hipError_t launch_kmeans_count(const uint8_t *codes, uint64_t n, uint32_t m, uint32_t ks, const uint8_t *active,

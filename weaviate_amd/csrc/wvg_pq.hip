@@ -132,22 +132,23 @@ typedef float f32x2e __attribute__((ext_vector_type(2)));
 // NaN takes the reference loop.
 constexpr int PQ_ENC_GROUP = 4;  // pairs per argmin group (8 centroids: 32 SGPRs of centroids)
 
+// seg_nan (k-means passes): per segment, nonzero when its centroids hold a NaN
+// (pq_pairs_kernel writes it with the pair copy); a segment without one takes
+// the min3 argmin like a nan_free codebook.  gridDim.y > 1 (row-major codes
+// only): workgroup row y encodes segments [y m / G, (y + 1) m / G) of its rows,
+// so a small row count (the 100k-row Lloyd assignment) still fills the chip.
 template <int DS, bool TILED_OUT>
 __global__ void pq_encode_kernel(const float4 *__restrict__ tiled, uint64_t n, uint32_t dim, uint32_t nchunks,
                                  const float *__restrict__ centers, uint32_t m, uint32_t ks, uint32_t ds_rt,
-                                 uint8_t *__restrict__ codes, const float *__restrict__ pairs, int nan_free)
+                                 uint8_t *__restrict__ codes, const float *__restrict__ pairs, int nan_free,
+                                 const uint32_t *__restrict__ seg_nan)
 {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
     const uint32_t ds = DS > 0 ? (uint32_t)DS : ds_rt;
     const float4 *rp = tiled + ((r >> 6) * nchunks) * 64 + (r & 63);
-    const uint32_t out_chunks = pq_chunks(m);
-    uint32_t w8[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};  // TILED_OUT, m = 32: all codes, rotated before the store
-    for (uint32_t oc = 0; oc < out_chunks; oc++) {
-        uint32_t w[4] = {0u, 0u, 0u, 0u};
-        for (uint32_t bsel = 0; bsel < 16; bsel++) {
-            const uint32_t s = oc * 16 + bsel;
-            if (s >= m) break;
+    // the nearest centroid of segment s (nNearest, CH/kmeans.go:103-135)
+    auto seg_best = [&](uint32_t s) -> uint32_t {
             const float *cs = centers + (size_t)s * ks * ds;
             uint32_t best = 0;
             float minD = 3.40282346638528859812e+38f;  // math.MaxFloat32
@@ -155,7 +156,7 @@ __global__ void pq_encode_kernel(const float4 *__restrict__ tiled, uint64_t n, u
                 // segment s is exactly chunk s (dim = 4m): one 16-byte load, scalar unfused path (n < 8)
                 const float4 x = rp[(size_t)s * 64];
                 const bool row_nan = !(x.x == x.x && x.y == x.y && x.z == x.z && x.w == x.w);
-                if (pairs && nan_free && __ballot(row_nan) == 0ull) {  // (see the argmin note above)
+                if (pairs && (nan_free || (seg_nan && seg_nan[s] == 0u)) && __ballot(row_nan) == 0ull) {  // (see the argmin note above)
                     const f32x2e xx = {x.x, x.x}, xy = {x.y, x.y}, xz = {x.z, x.z}, xw = {x.w, x.w};
                     const __attribute__((address_space(4))) float *cp =
                         (const __attribute__((address_space(4))) float *)(pairs + (size_t)s * ks * 4);
@@ -276,10 +277,22 @@ __global__ void pq_encode_kernel(const float4 *__restrict__ tiled, uint64_t n, u
                     }
                 }
             }
-            if constexpr (TILED_OUT)
-                w[bsel >> 2] |= best << (8 * (bsel & 3));
-            else
-                codes[r * m + s] = (uint8_t)best;
+            return best;
+    };
+    if constexpr (!TILED_OUT) {
+        const uint32_t s0 = (uint32_t)((uint64_t)m * blockIdx.y / gridDim.y);
+        const uint32_t s1 = (uint32_t)((uint64_t)m * (blockIdx.y + 1) / gridDim.y);
+        for (uint32_t s = s0; s < s1; s++) codes[r * m + s] = (uint8_t)seg_best(s);
+        return;
+    }
+    const uint32_t out_chunks = pq_chunks(m);
+    uint32_t w8[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};  // TILED_OUT, m = 32: all codes, rotated before the store
+    for (uint32_t oc = 0; oc < out_chunks; oc++) {
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        for (uint32_t bsel = 0; bsel < 16; bsel++) {
+            const uint32_t s = oc * 16 + bsel;
+            if (s >= m) break;
+            w[bsel >> 2] |= seg_best(s) << (8 * (bsel & 3));
         }
         if constexpr (TILED_OUT) {
             if (pq_rotated(m)) {
@@ -306,29 +319,34 @@ __global__ void pq_encode_kernel(const float4 *__restrict__ tiled, uint64_t n, u
 }
 
 hipError_t launch_pq_encode(const float *tiled, uint64_t n, uint32_t dim, const float *centers, uint32_t m,
-                            uint32_t ks, uint8_t *codes, hipStream_t s, bool tiled_out, bool nan_free)
+                            uint32_t ks, uint8_t *codes, hipStream_t s, bool tiled_out, bool nan_free,
+                            const uint32_t *seg_nan)
 {
     if (n == 0) return hipSuccess;
     const uint32_t ds = dim / m, nchunks = f32_chunks(dim);
-    dim3 grid((unsigned)((n + 255) / 256)), block(256);
+    const unsigned blocks = (unsigned)((n + 255) / 256);
+    // row-major output: segment groups until ~16k workgroups (64k waves) are in flight
+    const unsigned groups = tiled_out ? 1u : std::max(1u, std::min<unsigned>(m, 16384u / blocks));
+    dim3 grid(blocks, groups), block(256);
     const float4 *t4 = reinterpret_cast<const float4 *>(tiled);
     // codebook buffers (pq_centers_alloc_bytes) carry the pair layout after the table
     const float *pairs = pq_has_pairs(ks, ds) ? centers + (size_t)m * ks * ds : nullptr;
     nan_free = nan_free && tuning().pq_encode_min3 != 0;
+    if (tuning().pq_encode_min3 == 0) seg_nan = nullptr;
     if (ds == 4 && dim == 4 * m) {
         if (tiled_out)
             hipLaunchKernelGGL((pq_encode_kernel<4, true>), grid, block, 0, s, t4, n, dim, nchunks, centers, m, ks, ds,
-                               codes, pairs, (int)nan_free);
+                               codes, pairs, (int)nan_free, seg_nan);
         else
             hipLaunchKernelGGL((pq_encode_kernel<4, false>), grid, block, 0, s, t4, n, dim, nchunks, centers, m, ks, ds,
-                               codes, pairs, (int)nan_free);
+                               codes, pairs, (int)nan_free, seg_nan);
     } else {
         if (tiled_out)
             hipLaunchKernelGGL((pq_encode_kernel<0, true>), grid, block, 0, s, t4, n, dim, nchunks, centers, m, ks, ds,
-                               codes, nullptr, 0);
+                               codes, nullptr, 0, nullptr);
         else
             hipLaunchKernelGGL((pq_encode_kernel<0, false>), grid, block, 0, s, t4, n, dim, nchunks, centers, m, ks, ds,
-                               codes, nullptr, 0);
+                               codes, nullptr, 0, nullptr);
     }
     return hipGetLastError();
 }
@@ -370,6 +388,7 @@ __device__ __forceinline__ uint32_t code_at(const uint4 *cw, int i)
 }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ uint4 ld_codes(const uint4 *p)
 {
@@ -943,7 +962,12 @@ __global__ __launch_bounds__(PQ_SCAN_WAVES * 64) void scan_pq32_dense_kernel(Sca
 template <int E, int WV>
 constexpr uint32_t PQ32_WIDE_BASE = (uint32_t)WV * 64u * E * 8u;  // LDS address of the image (after sh[WV][64E])
 
-template <int E, int WV, int R, int NB, int TP, int METRIC, bool IL = false, bool COS = false>
+// MB (round 4): the 64-tile live masks come through buffer loads with no
+// branch (a lane past its stream reads 0 from the resource bound; no allow
+// list: an empty resource) and stay raw until their block starts.  Before,
+// the branchy global loads were waited on at once (s_waitcnt vmcnt(0) every
+// 64 tiles, draining the wave's code prefetch).
+template <int E, int WV, int R, int NB, int TP, int METRIC, bool IL = false, bool COS = false, bool MB = true>
 __global__ __launch_bounds__(WV * 64) void scan_pq32_wide_kernel(ScanArgs a, uint64_t *partials)
 {
     static_assert(64 % R == 0, "the ring length divides the 64-tile mask block");
@@ -1048,13 +1072,45 @@ __global__ __launch_bounds__(WV * 64) void scan_pq32_wide_kernel(ScanArgs a, uin
             }
             return m;
         };
-        uint64_t mcur[TP], mnxt[TP];
+        // MB: stream p's valid words from a.valid + s0[p], its allow words from a.allow (word t - allow_t0)
+        __amdgpu_buffer_rsrc_t vrs[TP], ars[TP];
+        const bool has_allow = a.allow != nullptr;
+#pragma unroll
+        for (int p = 0; p < TP; p++) {
+            vrs[p] = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t *>(a.valid + s0[p]), (short)0,
+                                                       (int)(span(p) / 256u), 0x00020000);  // span(p) / 2048 * 8
+            ars[p] = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t *>(a.allow), (short)0,
+                                                       has_allow ? (int)(a.allow_words * 8u) : 0, 0x00020000);
+        }
+        // raw words of stream p's (64 b + lane)-th tile: valid (.x) and allow (.y, 0 past the list)
+        auto load_raw = [&](int p, uint32_t b, uint64_t &v, uint64_t &al) {
+            const uint32_t ii = b * 64u + (uint32_t)lane;
+            const uint32_t tt = ii < n[p] ? tile_of(p, ii) * STRIDE : 0u;
+            const uint32_t vo = ii < n[p] ? tt * 8u : span(p) / 256u;  // past the bound: reads 0
+            const uint64_t wi = s0[p] + tt - a.allow_t0;
+            const uint32_t ao = (ii < n[p] && wi < a.allow_words) ? (uint32_t)wi * 8u : 0xFFFFFFF0u;
+            const u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(vrs[p], vo, 0, 0);
+            const u32x2 y = __builtin_amdgcn_raw_buffer_load_b64(ars[p], ao, 0, 0);
+            v = ((uint64_t)x.y << 32) | x.x;
+            al = ((uint64_t)y.y << 32) | y.x;
+        };
+        auto live_of = [&](uint64_t v, uint64_t al) -> uint64_t { return has_allow ? v & al : v; };
+        uint64_t mcur[TP], mnxt[TP], mnv[TP], mna[TP];
         uint32_t ring[TP][R][8];
         f32x2 acc[TP];
 #pragma unroll
         for (int p = 0; p < TP; p++) {
-            mcur[p] = load_masks(p, 0);
-            mnxt[p] = load_masks(p, 1);
+            if constexpr (MB) {
+                uint64_t v0, a0;
+                load_raw(p, 0, v0, a0);
+                mcur[p] = live_of(v0, a0);
+                load_raw(p, 1, mnv[p], mna[p]);
+                mnxt[p] = 0ull;
+            } else {
+                mcur[p] = load_masks(p, 0);
+                mnxt[p] = load_masks(p, 1);
+                mnv[p] = mna[p] = 0ull;
+            }
 #pragma unroll
             for (int s = 0; s < R - 1; s++) load(p, (uint32_t)s, ring[p][s]);
 #pragma unroll
@@ -1112,8 +1168,16 @@ __global__ __launch_bounds__(WV * 64) void scan_pq32_wide_kernel(ScanArgs a, uin
                     if (s == 1 && (tl & 63u) == 0u && tl != 0u) {  // (R | 64: block starts land on s == 1)
 #pragma unroll
                         for (int p = 0; p < TP; p++) {
-                            mcur[p] = mnxt[p];
-                            mnxt[p] = load_masks(p, (tl >> 6) + 1u);
+                            if constexpr (MB) {
+                                mcur[p] = live_of(mnv[p], mna[p]);
+                                // (the raw words die before the loads that replace them are issued, so
+                                // the loads land in the loop-carried registers: no copy, no wait here)
+                                asm volatile("" : "+v"(mcur[p]));
+                                load_raw(p, (tl >> 6) + 1u, mnv[p], mna[p]);
+                            } else {
+                                mcur[p] = mnxt[p];
+                                mnxt[p] = load_masks(p, (tl >> 6) + 1u);
+                            }
                         }
                     }
 #pragma unroll
@@ -1324,32 +1388,32 @@ static bool img7_ok()
 
 // K8e reads its image at the compile-time LDS address PQ32_WIDE_BASE: the
 // host launches an instantiation only where the static LDS really ends there
-template <int E, int WV, int R, int NB, int TP, bool IL = false, bool COS = false>
+template <int E, int WV, int R, int NB, int TP, bool IL = false, bool COS = false, bool MB = true>
 static bool wide_ok()
 {
     static const bool ok = [] {
         if (PQ32_WIDE_BASE<E, WV> + PQ32_IMG7_BYTES > 160u * 1024u) return false;
         hipFuncAttributes fa{};
         if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(
-                                          &scan_pq32_wide_kernel<E, WV, R, NB, TP, WVG_M_L2, IL, COS>)) != hipSuccess)
+                                          &scan_pq32_wide_kernel<E, WV, R, NB, TP, WVG_M_L2, IL, COS, MB>)) != hipSuccess)
             return false;
         return fa.sharedSizeBytes == PQ32_WIDE_BASE<E, WV>;
     }();
     return ok;
 }
 
-template <int E, int WV, int R, int NB, int TP, bool IL = false, bool COS = false>
+template <int E, int WV, int R, int NB, int TP, bool IL = false, bool COS = false, bool MB = true>
 static bool launch_pq_wide(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
 {
-    if (!wide_ok<E, WV, R, NB, TP, IL, COS>()) return false;
+    if (!wide_ok<E, WV, R, NB, TP, IL, COS, MB>()) return false;
     const dim3 grid = COS ? dim3((unsigned)groups * a.nq) : dim3(groups, a.nq), block(WV * 64);
     const uint32_t lds = PQ32_IMG7_BYTES;
     if (a.metric == WVG_M_L2 || a.metric == WVG_M_MANHATTAN || a.metric == WVG_M_HAMMING)  // Wrap = identity
-        launch_timed((scan_pq32_wide_kernel<E, WV, R, NB, TP, WVG_M_L2, IL, COS>), grid, block, lds, s, a, partials);
+        launch_timed((scan_pq32_wide_kernel<E, WV, R, NB, TP, WVG_M_L2, IL, COS, MB>), grid, block, lds, s, a, partials);
     else if (a.metric == WVG_M_DOT)
-        launch_timed((scan_pq32_wide_kernel<E, WV, R, NB, TP, WVG_M_DOT, IL, COS>), grid, block, lds, s, a, partials);
+        launch_timed((scan_pq32_wide_kernel<E, WV, R, NB, TP, WVG_M_DOT, IL, COS, MB>), grid, block, lds, s, a, partials);
     else
-        launch_timed((scan_pq32_wide_kernel<E, WV, R, NB, TP, WVG_M_COSINE, IL, COS>), grid, block, lds, s, a, partials);
+        launch_timed((scan_pq32_wide_kernel<E, WV, R, NB, TP, WVG_M_COSINE, IL, COS, MB>), grid, block, lds, s, a, partials);
     return true;
 }
 
@@ -1392,6 +1456,18 @@ static hipError_t launch_pq_e_variant(const ScanArgs &a, uint64_t *partials, int
         else if (v == 27) launch_pq_dense<E, 4, 16, 6>(a, partials, grid, block, 4 * lds, s);
         else launch_pq_dense<E, 2, 16, 6>(a, partials, grid, block, 4 * lds, s);
         return hipGetLastError();
+    }
+    if (m32 && v >= 50 && v <= 54) {
+        // K8e mask-load A/B (round 4): 50 = the round-3 product (8 waves, ring 4 / 16, branchy mask
+        // loads waited at once); MB (buffered raw masks): 51 = ring 4, 52 = ring 8, 53 = ring 16,
+        // 54 = 4 waves, ring 16
+        bool ok;
+        if (v == 50) ok = launch_pq_wide<E, 8, 4, 16, 1, false, false, false>(a, partials, groups, s);
+        else if (v == 51) ok = launch_pq_wide<E, 8, 4, 16, 1>(a, partials, groups, s);
+        else if (v == 52) ok = launch_pq_wide<E, 8, 8, 16, 1>(a, partials, groups, s);
+        else if (v == 53) ok = launch_pq_wide<E, 8, 16, 16, 1>(a, partials, groups, s);
+        else ok = launch_pq_wide<E, 4, 16, 16, 1>(a, partials, groups, s);
+        if (ok) return hipGetLastError();
     }
     if (m32 && (v == 46 || v == 47)) {  // K8e with interleaved waves (IL): 46 = 8 waves, ring 4 / 16; 47 = ring 8 / 16
         if (v == 46 ? launch_pq_wide<E, 8, 4, 16, 1, true>(a, partials, groups, s)
@@ -1586,20 +1662,25 @@ namespace wvg {
 
 // The pair-interleaved copy of a [m][ks][4] codebook that K9's ds = 4 path
 // reads right after the table (pq_pair_layout on the device).
-__global__ __launch_bounds__(256) void pq_pairs_kernel(const float *centers, uint32_t m, uint32_t ks, float *out)
+__global__ __launch_bounds__(256) void pq_pairs_kernel(const float *centers, uint32_t m, uint32_t ks, float *out,
+                                                       uint32_t *seg_nan)
 {
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;  // (s, p, k, h)
-    if (i >= (uint64_t)m * ks * 4) return;
-    const uint32_t h = (uint32_t)(i & 1), k = (uint32_t)((i >> 1) & 3);
-    const uint64_t sp = i >> 3;
-    const uint32_t sg = (uint32_t)(sp / (ks / 2)), pr = (uint32_t)(sp % (ks / 2));
-    out[i] = centers[((size_t)sg * ks + 2 * pr + h) * 4 + k];
+    // workgroup = segment blockIdx.x; element i = (p, k, h) of its ks * 4
+    const uint32_t sg = blockIdx.x;
+    bool nan = false;
+    for (uint32_t i = threadIdx.x; i < ks * 4u; i += 256u) {
+        const uint32_t h = i & 1u, k = (i >> 1) & 3u, pr = i >> 3;
+        const float v = centers[((size_t)sg * ks + 2 * pr + h) * 4 + k];
+        out[(size_t)sg * ks * 4 + i] = v;
+        nan |= v != v;
+    }
+    const int any = __syncthreads_or(nan);
+    if (seg_nan && threadIdx.x == 0) seg_nan[sg] = any ? 1u : 0u;
 }
 
-hipError_t launch_pq_pairs(const float *centers, uint32_t m, uint32_t ks, float *out, hipStream_t s)
+hipError_t launch_pq_pairs(const float *centers, uint32_t m, uint32_t ks, float *out, hipStream_t s, uint32_t *seg_nan)
 {
-    const uint64_t n = (uint64_t)m * ks * 4;
-    hipLaunchKernelGGL(pq_pairs_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, centers, m, ks, out);
+    hipLaunchKernelGGL(pq_pairs_kernel, dim3(m), dim3(256), 0, s, centers, m, ks, out, seg_nan);
     return hipGetLastError();
 }
 

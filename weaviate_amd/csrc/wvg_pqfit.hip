@@ -41,7 +41,7 @@ int wvg_pq_fit(wvg_ctx *ctx, const float *X, uint64_t n, uint32_t dim, uint32_t 
                  o_mem = cv.take(n * m * 4), o_off = cv.take((size_t)m * ks * 4),
                  o_cnt = cv.take((size_t)m * ks * 4), o_chg = cv.take((size_t)m * 4), o_act = cv.take(m),
                  o_rec = cv.take(m), o_skip = cv.take((size_t)m * ks),
-                 o_bh = cv.take((size_t)m * kmeans_blocks(n) * ks * 4);
+                 o_bh = cv.take((size_t)m * kmeans_blocks(n) * ks * 4), o_nan = cv.take((size_t)m * 4);
     Bulk bk(ctx);
     rc = bk.begin(cv.off);
     if (rc) return rc;
@@ -51,14 +51,17 @@ int wvg_pq_fit(wvg_ctx *ctx, const float *X, uint64_t n, uint32_t dim, uint32_t 
     uint32_t *dMem = (uint32_t *)(bk.b + o_mem), *dOff = (uint32_t *)(bk.b + o_off);
     uint32_t *dCnt = (uint32_t *)(bk.b + o_cnt), *dChg = (uint32_t *)(bk.b + o_chg);
     uint8_t *dAct = (uint8_t *)(bk.b + o_act), *dRec = (uint8_t *)(bk.b + o_rec), *dSkip = (uint8_t *)(bk.b + o_skip);
-    uint32_t *dBh = (uint32_t *)(bk.b + o_bh);
+    uint32_t *dBh = (uint32_t *)(bk.b + o_bh), *dNan = (uint32_t *)(bk.b + o_nan);
     WVG_HIP(hipMemcpyAsync(dX, X, n * dim * 4, hipMemcpyHostToDevice, s));
     // the training rows in the tiled layout K9 (the assignment) reads
     WVG_HIP(hipMemsetAsync(dXt, 0, tiles_of(n) * 64 * (size_t)nch * 16, s));
     WVG_HIP(launch_f32_store(dX, nullptr, n, dim, nch, 0, dXt, s));
     const bool pairs = pq_has_pairs(ks, ds);
-    auto refresh_pairs = [&]() -> hipError_t {  // K9's ds = 4 pair copy of the current centers
-        return pairs ? launch_pq_pairs(dC, m, ks, dC + nc, s) : hipSuccess;
+    // K9's ds = 4 pair copy of the current centers and their per-segment NaN flags (a segment
+    // without NaN centroids takes K9's min3 argmin; its rows' NaNs are checked per wave)
+    WVG_HIP(hipMemsetAsync(dNan, 0xFF, (size_t)m * 4, s));
+    auto refresh_pairs = [&]() -> hipError_t {
+        return pairs ? launch_pq_pairs(dC, m, ks, dC + nc, s, dNan) : hipSuccess;
     };
     // initCenters (kmeans.go:146-160): ks random rows (with replacement) per segment
     std::vector<float> C(nc);
@@ -84,7 +87,7 @@ int wvg_pq_fit(wvg_ctx *ctx, const float *X, uint64_t n, uint32_t dim, uint32_t 
         WVG_HIP(hipMemsetAsync(dChg, 0, (size_t)m * 4, s));
         // nNearest for every (row, segment): K9, the encoder (kmeans.go:103-135; ties to the
         // highest index); then changes and cluster sizes of the active segments
-        WVG_HIP(launch_pq_encode(dXt, n, dim, dC, m, ks, dCode, s, false, false));
+        WVG_HIP(launch_pq_encode(dXt, n, dim, dC, m, ks, dCode, s, false, false, pairs ? dNan : nullptr));
         WVG_HIP(launch_kmeans_count(dCode, n, m, ks, dAct, dP, dChg, dCnt, dBh, s));
         WVG_HIP(hipMemcpyAsync(cnt.data(), dCnt, cnt.size() * 4, hipMemcpyDeviceToHost, s));
         WVG_HIP(hipMemcpyAsync(chg.data(), dChg, chg.size() * 4, hipMemcpyDeviceToHost, s));

@@ -246,13 +246,16 @@ typedef __attribute__((address_space(1))) uint64_t gu64;
 
 // Thread 0 polls; false after `limit` ticks of s_memrealtime (100 MHz; 4 s
 // by default), so a waiting workgroup always exits.
-__device__ __forceinline__ bool wait_arrivals(uint32_t *ctr, uint32_t target, uint64_t limit)
+// The counter counts up from `base` (0 for a workspace zeroed per call; a
+// stream slot's persistent counter otherwise: the unsigned difference is
+// exact across the 2^32 wrap).
+__device__ __forceinline__ bool wait_arrivals(uint32_t *ctr, uint32_t base, uint32_t target, uint64_t limit)
 {
     __shared__ int ok;
     if (threadIdx.x == 0) {
         const uint64_t start = __builtin_amdgcn_s_memrealtime();
         int r = 1;
-        while (__hip_atomic_load((gu32 *)ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        while (__hip_atomic_load((gu32 *)ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - base < target) {
             if (__builtin_amdgcn_s_memrealtime() - start > limit) {
                 r = 0;
                 break;
@@ -318,7 +321,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_stream_kernel(ScanAr
     const uint32_t G = j.groups;
     if (blockIdx.x == G) {
         for (uint32_t q = 0; q < a.nq; q++) {
-            if (!wait_arrivals(j.arrivals + q, G, j.wait_limit)) {
+            if (!wait_arrivals(j.arrivals + q, j.arrival_base, G, j.wait_limit)) {
                 // gave up: queries q.. get empty results (never stale ones) and
                 // the sticky status word tells wvg_search_device_check
                 if (threadIdx.x == 0) atomicOr(j.status, WVG_STATUS_MERGE_TIMEOUT);

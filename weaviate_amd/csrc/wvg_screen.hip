@@ -664,8 +664,21 @@ publish:
 // read; the barrier for the next stage sits between the halves; the next
 // stage's first half is read during the second half's MFMAs.  Against K3c per
 // 128 x 256 x 32 tile: 16 KiB instead of 25 KiB from L2 (no query fragments,
-// one norm copy) and 64 KiB instead of 80 KiB of LDS reads.  The epilogue, the
-// bound, the lists and the partials are K3c's.
+// one norm copy) and 64 KiB instead of 80 KiB of LDS reads.  The bound and
+// the partials are K3c's.
+//
+// Survivors (round 4).  The epilogue of a row block only APPENDS its
+// survivors -- (u, query, row) -- to a per-wave LDS queue (one ballot, one
+// mbcnt and one ds_write per element group with a survivor); after the
+// epilogue ONE code site drains the queue into the wave's lists, which live
+// in registers (SurvivorLists), and refreshes the query thresholds the next
+// block's fast check reads.  The round-3 kernel called an out-of-line
+// insertion at each of the 128 unrolled epilogue sites: the call ABI spilled
+// registers around the main loop, and every spill reload is a scratch load
+// counted in vmcnt, so each epilogue ended in vmcnt(0) -- a drain of the six
+// stages in flight (profiles/r03/k3d_ab: the stage loop alone ran at 75% of
+// the bf16 peak, the product kernel at 32%).  Nothing in the loop now waits on
+// vmcnt except the ring's constant waits.
 constexpr int SD_WAVES = 4;
 constexpr int SD_BQ = 128;
 constexpr int SD_BFR = 16;
@@ -673,25 +686,124 @@ constexpr int SD_STAGE = SD_BFR * 1024;
 constexpr int SD_NBUF = 8;
 constexpr int SD_NSLOT = 1280;
 constexpr int SD_RING = SD_NBUF * SD_STAGE + 2 * SD_NSLOT;
+constexpr int SD_QCAP = 256;  // survivor queue entries per wave (8 B: u bits | query << 8 | row in block)
+constexpr int SD_QUEUE = SD_WAVES * SD_QCAP * 8;
 constexpr int SD_LISTS = SD_WAVES * 32 * SCREEN_M * 8;
-constexpr int SD_LDS = SD_RING + SD_LISTS + SD_WAVES * 32 * 4 * 2 + SD_BQ * 4 * 3;
+constexpr int SD_LDS = SD_RING + SD_QUEUE + SD_LISTS + SD_WAVES * 32 * 4 * 2 + SD_BQ * 4 * 3;
+static_assert(SD_LDS <= 160 * 1024, "K3d's LDS");
+
+// One accumulator element read where it is used.  Through C++ the compiler
+// copies the whole accumulator tile into VGPRs at the top of the epilogue (~100
+// live VGPRs next to the resident queries: spills); the asm names the element
+// in its AGPR, and asm statements keep their program order.
+__device__ __forceinline__ float agpr_read(float x)
+{
+    float r;
+    asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(r) : "a"(x));
+    return r;
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l)
+{
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+}
+
+// lane i of each 16-lane row takes lane i - 1's value (DPP row_shr:1; lane 0 keeps its own)
+__device__ __forceinline__ uint64_t row_shr1_64(uint64_t v)
+{
+    const int lo = __builtin_amdgcn_update_dpp((int)(uint32_t)v, (int)(uint32_t)v, 0x111, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(uint32_t)(v >> 32), (int)(uint32_t)(v >> 32), 0x111, 0xF, 0xF,
+                                               false);
+    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+// A wave's survivor state: the lists of the SCREEN_M smallest (lower, slot)
+// keys of its 32 queries stay in LDS (32 x 16 keys, ascending; only the
+// flush touches them), the per-query thresholds in registers: lane q < 32
+// holds query q's distance-space threshold WT = min(tau, k-th lower + 2 Emax,
+// M-th lower), its u-space form WS and Emax (sc_insert's state of round 3).
+struct SurvivorLists {
+    uint32_t laddr;  // LDS byte address of the wave's 32 lists
+    float wt, ws, em;
+};
+
+// One survivor (wave-uniform arguments) into query ql's list; K3c's insertion
+// rule: drop if lower > WT or the list is full of smaller keys, else insert in
+// order (ties by slot) and tighten WT / WS.  LDS through inline asm with its
+// own lgkmcnt wait (see sl_flush).
+__device__ __forceinline__ void sl_insert(SurvivorLists &S, int ql, float u, uint32_t slot, int K, int cosine)
+{
+    const int lane = threadIdx.x & 63;
+    const float lower = sc_lower(u, cosine);
+    float wt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(S.wt), ql));
+    if (!(lower <= wt)) return;
+    const uint64_t key = ((uint64_t)wvg_ord_f32(lower) << 32) | slot;
+    const uint32_t la = S.laddr + (uint32_t)ql * (SCREEN_M * 8) + 8u * (uint32_t)(lane & 15);
+    uint2 v2;
+    asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v2) : "v"(la) : "memory");
+    const uint64_t v = lane < SCREEN_M ? (((uint64_t)v2.y << 32) | v2.x) : WVG_KEY_NONE;
+    if (!(key < readlane64(v, SCREEN_M - 1))) return;
+    const int pos = __popcll(__ballot(lane < SCREEN_M && v < key));
+    const uint64_t sh = row_shr1_64(v);
+    const uint64_t nv = lane > pos ? sh : (lane == pos ? key : v);
+    if (lane >= pos && lane < SCREEN_M) {
+        const uint2 o = make_uint2((uint32_t)nv, (uint32_t)(nv >> 32));
+        asm volatile("ds_write_b64 %0, %1" ::"v"(la), "v"(o) : "memory");
+    }
+    const uint64_t nk = readlane64(nv, K - 1), nm = readlane64(nv, SCREEN_M - 1);
+    const float em = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(S.em), ql));
+    if (nk != WVG_KEY_NONE) wt = fminf(wt, sc_tau_k(key_lower(nk), em, cosine));
+    if (nm != WVG_KEY_NONE) wt = fminf(wt, key_lower(nm));
+    const float ws = sc_sigma(wt, cosine);
+    S.wt = lane == ql ? wt : S.wt;
+    S.ws = lane == ql ? ws : S.ws;
+}
+
+// Drains a wave's queue (n entries at LDS byte address qaddr) into its lists,
+// then stores the new WS of its 32 queries at LDS address wsaddr (read by the
+// next epilogue).  LDS only through inline asm, with its own lgkmcnt waits:
+// the compiler cannot tell these accesses from the in-flight LDS DMA of the
+// stage ring and would put a vmcnt(0) before each.
+__device__ __forceinline__ void sl_flush(SurvivorLists &S, uint32_t qaddr, uint32_t n, uint32_t wsaddr,
+                                         uint64_t slot0, int K, int cosine, uint32_t nlive)
+{
+    const int lane = threadIdx.x & 63;
+    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+        uint2 e;
+        asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(e) : "v"(qaddr + 8u * (i0 + lane)) : "memory");
+        const uint32_t cnt = n - i0 < 64 ? n - i0 : 64;
+        for (uint32_t j = 0; j < cnt; j++) {
+            const float u = __int_as_float(__builtin_amdgcn_readlane((int)e.x, (int)j));
+            const uint32_t tag = (uint32_t)__builtin_amdgcn_readlane((int)e.y, (int)j);
+            if ((tag >> 8) >= nlive) continue;  // a padded query of the last block (q >= nq)
+            sl_insert(S, (int)(tag >> 8), u, (uint32_t)(slot0 + (tag & 255u)), K, cosine);
+        }
+    }
+    if (lane < 32) asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" ::"v"(wsaddr + 4u * lane), "v"(S.ws) : "memory");
+}
 
 // DIAG (tools build only; 0 in the product): bit 0 = no wait for the stage
-// loads, bit 1 = no epilogue, bit 2 = no list insertions, bit 4 = count row
-// blocks / exact-path blocks / insertion calls.  Compile-time, so the tools
-// build's DIAG = 0 kernel is the product kernel, register allocation included.
+// loads, bit 1 = no epilogue (alone it lets the compiler delete the MFMAs, as
+// the round-3 "stage loop alone" diagnostics did: their 8.3 ms had no MFMA),
+// bit 1 + bit 3 (10) = the stage loop with its MFMAs and a one-sum consumer,
+// bit 2 = tests but no survivor queue, bit 4 = count row blocks / blocks with
+// survivors / queued survivors.  Compile-time, so the tools build's DIAG = 0
+// kernel is the product kernel, register allocation included.
 template <int KBN, int DIAG = 0>
 __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs a)
 {
     static_assert(KBN % SD_NBUF == 0, "the stage buffer of a K block must be a compile-time constant");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint64_t *lists = reinterpret_cast<uint64_t *>(smem + SD_RING);  // [4][32][M]
-    float *tau = reinterpret_cast<float *>(smem + SD_RING + SD_LISTS);
+    unsigned char *queue = smem + SD_RING;  // [4][SD_QCAP] x 8 B
+    uint64_t *lists = reinterpret_cast<uint64_t *>(smem + SD_RING + SD_QUEUE);  // [4][32][M]
+    float *tau = reinterpret_cast<float *>(smem + SD_RING + SD_QUEUE + SD_LISTS);
     float *sig = tau + SD_WAVES * 32;
     float *ck1 = sig + SD_WAVES * 32;
     float *ck2 = ck1 + SD_BQ;
     float *cem = ck2 + SD_BQ;
     uint32_t n_blk = 0, n_slow = 0, n_call = 0;  // (DIAG & 16)
+    (void)n_blk, (void)n_slow, (void)n_call;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int K = (int)a.k, M = SCREEN_M;
@@ -726,20 +838,41 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
     }
     for (int i = tid; i < SD_WAVES * 32 * M; i += SD_WAVES * 64) lists[i] = WVG_KEY_NONE;
     __syncthreads();
+    SurvivorLists S;
+    S.laddr = (uint32_t)(uintptr_t)(lists + (size_t)w * 32 * M);
+    S.wt = tau[w * 32 + (lane & 31)];
+    S.ws = sig[w * 32 + (lane & 31)];
+    S.em = cem[w * 32 + (lane & 31)];
     if (blk0 < blk1) {
         // the wave's 32 queries, every K block, resident for the whole range
         bf16x8 areg[KBN][2];
+        // The first SD_AKB K blocks' fragments live in AGPRs (an MFMA A operand may be
+        // an AGPR), the rest in VGPRs: 128 accumulator + 64 B-fragment + 48 such AGPRs,
+        // which leaves the epilogue ~100 VGPRs -- with all 192 in VGPRs the compiler
+        // spilled query fragments around the epilogue, and a scratch reload before the
+        // loop costs a vmcnt(0) (a drain of the stage ring) at every row block.
+        constexpr int SD_AKB = 6;
+        const uint4 *qsrc = a.qfrag + (size_t)(qb * 8 + 2 * w) * KBN * 64 + lane;
 #pragma unroll
         for (int ks = 0; ks < KBN; ks++)
 #pragma unroll
-            for (int mq = 0; mq < 2; mq++)
-                areg[ks][mq] = *reinterpret_cast<const bf16x8 *>(
-                    a.qfrag + ((size_t)(qb * 8 + 2 * w + mq) * KBN + ks) * 64 + lane);
+            for (int mq = 0; mq < 2; mq++) {
+                const uint4 *src = qsrc + ((size_t)mq * KBN + ks) * 64;
+                if (ks < SD_AKB)
+                    asm volatile("global_load_dwordx4 %0, %1, off" : "=a"(areg[ks][mq]) : "v"(src) : "memory");
+                else
+                    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(areg[ks][mq]) : "v"(src) : "memory");
+            }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
         for (int ks = 0; ks < KBN; ks++)
 #pragma unroll
-            for (int mq = 0; mq < 2; mq++) asm volatile("" : "+v"(areg[ks][mq]));
+            for (int mq = 0; mq < 2; mq++) {
+                if (ks < SD_AKB)
+                    asm volatile("" : "+a"(areg[ks][mq]));
+                else
+                    asm volatile("" : "+v"(areg[ks][mq]));
+            }
 
         // loads of one stage: wave w moves row fragments 4w .. 4w+3 (tile w,
         // row groups 0..3), the norms of tile w, and wave 0 the block's tile
@@ -748,14 +881,16 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
         const float *lnorm = a.norms + (a.tile_begin + blk0 * 4 + w) * 64 + lane;
         uint64_t lblk = blk0;
         auto load_stage = [&](int ks) {
+            if constexpr ((DIAG & 128) != 0) return;
             unsigned char *dst = smem + (ks % SD_NBUF) * SD_STAGE;
 #pragma unroll
             for (int rg = 0; rg < 4; rg++)
                 __builtin_amdgcn_global_load_lds(lsrc + ((size_t)ks * 4 + rg) * 64,
                                                  reinterpret_cast<uint4 *>(dst + (4 * w + rg) * 1024), 16, 0, 0);
             unsigned char *nslot = smem + SD_NBUF * SD_STAGE + (lblk & 1) * SD_NSLOT;
-            __builtin_amdgcn_global_load_lds(lnorm, reinterpret_cast<float *>(nslot + w * 256), 4, 0, 0);
-            if (w == 0) {
+            if constexpr ((DIAG & 32) == 0)
+                __builtin_amdgcn_global_load_lds(lnorm, reinterpret_cast<float *>(nslot + w * 256), 4, 0, 0);
+            if ((DIAG & 32) == 0 && w == 0) {
                 const uint32_t wi = (uint32_t)(lane & 7) >> 1, half = lane & 1;
                 const uint64_t t = a.tile_begin + lblk * 4 + wi;
                 const uint32_t *src =
@@ -774,34 +909,73 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
         };
         // six stages in flight at every wait: the unit being waited for + 5 younger
         auto wait_next = [&]() {
-            if constexpr ((DIAG & 1) != 0) return;
+            if constexpr ((DIAG & 129) != 0) return;
+            if constexpr ((DIAG & 32) != 0) {
+                asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+                return;
+            }
             if (w == 0) asm volatile("s_waitcnt vmcnt(30)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(25)" ::: "memory");
         };
         auto raw_barrier = [&]() {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
+            if constexpr ((DIAG & 64) == 0) __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
         };
+        // Half a stage's row fragments straight into AGPRs (the MFMA B operand may
+        // be an AGPR): the 512 registers hold the resident queries (192 VGPRs), the
+        // accumulators (128 AGPRs) and both halves (64 AGPRs), which leaves the
+        // VGPRs the epilogue needs.  The reads are asynchronous to the compiler:
+        // every consumer first passes a wait that names the registers (wait_b0,
+        // and the barrier's lgkmcnt(0) + the "+a" fence for the second half).
+        // One lane base address for every read: the stage / half offset is added
+        // inside the asm from an SGPR (16 precomputed addresses cost 16 VGPRs).
+        const uint32_t rbase = (uint32_t)(uintptr_t)smem + 16u * lane;
         auto read_half = [&](int ks, int h, bf16x8 (&br)[8]) {
-            const unsigned char *sb = smem + (ks % SD_NBUF) * SD_STAGE + h * 8 * 1024;
-#pragma unroll
-            for (int j = 0; j < 8; j++) br[j] = *reinterpret_cast<const bf16x8 *>(sb + j * 1024 + lane * 16);
+            const uint32_t soff = (uint32_t)((ks % SD_NBUF) * SD_STAGE + h * 8 * 1024);
+            uint32_t tmp;
+            asm volatile("v_add_u32 %8, %9, %10\n\t"
+                         "ds_read_b128 %0, %8\n\t"
+                         "ds_read_b128 %1, %8 offset:1024\n\t"
+                         "ds_read_b128 %2, %8 offset:2048\n\t"
+                         "ds_read_b128 %3, %8 offset:3072\n\t"
+                         "ds_read_b128 %4, %8 offset:4096\n\t"
+                         "ds_read_b128 %5, %8 offset:5120\n\t"
+                         "ds_read_b128 %6, %8 offset:6144\n\t"
+                         "ds_read_b128 %7, %8 offset:7168"
+                         : "=a"(br[0]), "=a"(br[1]), "=a"(br[2]), "=a"(br[3]), "=a"(br[4]), "=a"(br[5]), "=a"(br[6]),
+                           "=a"(br[7]), "=&v"(tmp)
+                         : "s"(soff), "v"(rbase)
+                         : "memory");
+        };
+        // the first half landed (the second half's eight reads may still be in flight)
+        auto wait_b0 = [&](bf16x8 (&br)[8]) {
+            asm volatile("s_waitcnt lgkmcnt(8)"
+                         : "+a"(br[0]), "+a"(br[1]), "+a"(br[2]), "+a"(br[3]), "+a"(br[4]), "+a"(br[5]), "+a"(br[6]),
+                           "+a"(br[7])
+                         :
+                         : "memory");
         };
         const int qlane = 4 * (lane >> 4);
-        uint64_t qlive[2][4];
-#pragma unroll
-        for (int mq = 0; mq < 2; mq++)
-#pragma unroll
-            for (int r = 0; r < 4; r++) qlive[mq][r] = __ballot(q0 + 32 * w + 16 * mq + qlane + r < a.nq);
-        uint64_t *WL = lists + (size_t)w * 32 * M;
-        float *WT = tau + w * 32, *WS = sig + w * 32;
-        float lane_force = -__builtin_inff();
+        // the wave's queries below nq (a batch's last workgroup is padded)
+        const uint32_t qw0 = q0 + 32 * (uint32_t)w;
+        const uint32_t nlive = a.nq > qw0 ? (a.nq - qw0 < 32 ? a.nq - qw0 : 32u) : 0u;
+        const uint32_t qaddr = (uint32_t)(uintptr_t)(queue + (size_t)w * SD_QCAP * 8);
+        const uint32_t wsaddr = (uint32_t)(uintptr_t)(sig + w * 32);
+        // epilogue lane bases: smem (+ the tile-word bytes, lane-independent), the
+        // row norm of this lane's column, this lane's first query in sig / ck1 / ck2
+        const uint32_t sbase = (uint32_t)(uintptr_t)smem;
+        const uint32_t nbase = sbase + 4u * (uint32_t)(lane & 15);
+        const uint32_t qbase = sbase + 4u * (uint32_t)qlane;
+        const uint32_t csoff = (uint32_t)((uintptr_t)sig - (uintptr_t)smem);
+        // +inf when one of this lane's queries is not fast-eligible (K1 > 2^50: a huge or
+        // non-finite query), so its elements always take the exact test
+        bool lane_force = false;
 #pragma unroll
         for (int mq = 0; mq < 2; mq++)
 #pragma unroll
             for (int r = 0; r < 4; r++)
-                if (!(ck1[32 * w + 16 * mq + qlane + r] <= 0x1p50f)) lane_force = __builtin_inff();
+                if (!(ck1[32 * w + 16 * mq + qlane + r] <= 0x1p50f)) lane_force = true;
 
         floatx4 acc[2][16];
 #pragma unroll
@@ -813,7 +987,8 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
         // block; the ring holds K block ks of any row block in buffer ks % 8)
 #pragma unroll
         for (int ks = 0; ks < SD_NBUF - 1; ks++) load_stage(ks);
-        if (w == 0) asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
+        if constexpr ((DIAG & 32) != 0) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+        else if (w == 0) asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(30)" ::: "memory");
         raw_barrier();
         read_half(0, 0, b0);
@@ -821,6 +996,7 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
 #pragma unroll
             for (int ks = 0; ks < KBN; ks++) {
                 read_half(ks, 1, b1);
+                wait_b0(b0);
 #pragma unroll
                 for (int mq = 0; mq < 2; mq++)
 #pragma unroll
@@ -829,10 +1005,10 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
                 wait_next();   // the next unit landed
                 raw_barrier(); // (lgkmcnt(0): this wave's second-half reads done)
 #pragma unroll
-                for (int j = 0; j < 8; j++) asm volatile("" : "+v"(b1[j]));
+                for (int j = 0; j < 8; j++) asm volatile("" : "+a"(b1[j]));
                 // unit + 7 into the buffer of unit - 1 (fully read before this barrier)
                 load_stage((ks + SD_NBUF - 1) % KBN);
-                read_half((ks + 1) % KBN, 0, b0);
+                if (ks + 1 < KBN) read_half(ks + 1, 0, b0);  // (the next block's first half: after the epilogue)
 #pragma unroll
                 for (int mq = 0; mq < 2; mq++)
 #pragma unroll
@@ -843,135 +1019,197 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
             // epilogue of row block blk (K3c's, over 16 row groups): C layout row
             // (query) qlane + r, column (row) 16 nr + (lane & 15)
             if constexpr ((DIAG & 2) == 0) {
-                const unsigned char *nslot = smem + SD_NBUF * SD_STAGE + (blk & 1) * SD_NSLOT;
-                float nrm[16];
-                const uint32_t nrs = (uint32_t)(uintptr_t)nslot + 4u * (uint32_t)(lane & 15);
-#pragma unroll
-                for (int i = 0; i < 2; i++)
-                    asm volatile("ds_read_b32 %0, %8 offset:%9\n\t"
-                                 "ds_read_b32 %1, %8 offset:%10\n\t"
-                                 "ds_read_b32 %2, %8 offset:%11\n\t"
-                                 "ds_read_b32 %3, %8 offset:%12\n\t"
-                                 "ds_read_b32 %4, %8 offset:%13\n\t"
-                                 "ds_read_b32 %5, %8 offset:%14\n\t"
-                                 "ds_read_b32 %6, %8 offset:%15\n\t"
-                                 "ds_read_b32 %7, %8 offset:%16\n\t"
+                // Fast check, then (rarely) the exact test per element.  The exact test
+                // !(u < WS) (NaN-safe: a non-finite row or query always passes) queues the
+                // survivors of an element group with one ballot, one mbcnt and one ds_write;
+                // after the pass they are inserted from one code site (sl_flush).  A pass
+                // that would overflow the queue stops at that element group, drains the
+                // queue and resumes there with the tightened thresholds.  Register budget:
+                // the resident queries hold most of the VGPRs, so the pass walks one query
+                // half (mq) and eight row groups at a time with only those constants and row
+                // norms in registers, and reads each accumulator element where it is used
+                // (agpr_read); every epilogue LDS address is a lane base + an SGPR offset.
+                const uint32_t nsoff = (uint32_t)(SD_NBUF * SD_STAGE + (blk & 1) * SD_NSLOT);  // the block's norms
+                auto read_norms8 = [&](int hh, float (&nrm)[8]) {  // row norms of row groups 8 hh .. 8 hh + 7
+                    uint32_t tmp;
+                    asm volatile("v_add_u32 %8, %9, %10\n\t"
+                                 "ds_read_b32 %0, %8\n\t"
+                                 "ds_read_b32 %1, %8 offset:64\n\t"
+                                 "ds_read_b32 %2, %8 offset:128\n\t"
+                                 "ds_read_b32 %3, %8 offset:192\n\t"
+                                 "ds_read_b32 %4, %8 offset:256\n\t"
+                                 "ds_read_b32 %5, %8 offset:320\n\t"
+                                 "ds_read_b32 %6, %8 offset:384\n\t"
+                                 "ds_read_b32 %7, %8 offset:448\n\t"
                                  "s_waitcnt lgkmcnt(0)"
-                                 : "=v"(nrm[8 * i + 0]), "=v"(nrm[8 * i + 1]), "=v"(nrm[8 * i + 2]), "=v"(nrm[8 * i + 3]),
-                                   "=v"(nrm[8 * i + 4]), "=v"(nrm[8 * i + 5]), "=v"(nrm[8 * i + 6]), "=v"(nrm[8 * i + 7])
-                                 : "v"(nrs), "i"(512 * i + 0), "i"(512 * i + 64), "i"(512 * i + 128), "i"(512 * i + 192),
-                                   "i"(512 * i + 256), "i"(512 * i + 320), "i"(512 * i + 384), "i"(512 * i + 448)
+                                 : "=v"(nrm[0]), "=v"(nrm[1]), "=v"(nrm[2]), "=v"(nrm[3]), "=v"(nrm[4]),
+                                   "=v"(nrm[5]), "=v"(nrm[6]), "=v"(nrm[7]), "=&v"(tmp)
+                                 : "s"(nsoff + 512u * hh), "v"(nbase)
                                  : "memory");
-                uint64_t vm[4];
+                };
+                auto read_consts = [&](int mq, float (&k1r)[4], float (&k2r)[4], float (&svr)[4]) {
+                    // sig, ck1, ck2 are consecutive 128-float arrays: one address, offsets 0 / 512 / 1024
+                    const uint32_t coff = (uint32_t)(csoff + 4 * (32 * w + 16 * mq));
+                    float4 k1v, k2v, sv;
+                    uint32_t tmp;
+                    asm volatile("v_add_u32 %3, %4, %5\n\t"
+                                 "ds_read_b128 %0, %3 offset:512\n\t"
+                                 "ds_read_b128 %1, %3 offset:1024\n\t"
+                                 "ds_read_b128 %2, %3\n\t"
+                                 "s_waitcnt lgkmcnt(0)"
+                                 : "=v"(k1v), "=v"(k2v), "=v"(sv), "=&v"(tmp)
+                                 : "s"(coff), "v"(qbase)
+                                 : "memory");
+                    k1r[0] = k1v.x, k1r[1] = k1v.y, k1r[2] = k1v.z, k1r[3] = k1v.w;
+                    k2r[0] = k2v.x, k2r[1] = k2v.y, k2r[2] = k2v.z, k2r[3] = k2v.w;
+                    svr[0] = sv.x, svr[1] = sv.y, svr[2] = sv.z, svr[3] = sv.w;
+                };
+                if constexpr ((DIAG & 16) != 0) n_blk++;
+                // fast check: the lane's 16 rows' largest norm bound bounds each of their E
+                // (E = fma(norm, K1q, K2q) is monotone in the norm), so per query the largest
+                // raw score of the lane's rows + that E against WS is a superset test of
+                // every element (monotone roundings); finite on the fast-eligible inputs
+                // (query K1 <= 2^50, row norms <= 2^60), else the exact test runs
+                float nmax;
                 {
-                    uint4 vw0, vw1, aw0, aw1;
-                    const uint32_t wa = (uint32_t)(uintptr_t)(nslot + 1024);
-                    asm volatile("ds_read_b128 %0, %4\n\t"
-                                 "ds_read_b128 %1, %4 offset:16\n\t"
-                                 "ds_read_b128 %2, %4 offset:32\n\t"
-                                 "ds_read_b128 %3, %4 offset:48\n\t"
-                                 "s_waitcnt lgkmcnt(0)"
-                                 : "=v"(vw0), "=v"(vw1), "=v"(aw0), "=v"(aw1)
-                                 : "v"(wa)
-                                 : "memory");
-                    const uint64_t words[4] = {((uint64_t)vw0.y << 32) | vw0.x, ((uint64_t)vw0.w << 32) | vw0.z,
-                                               ((uint64_t)vw1.y << 32) | vw1.x, ((uint64_t)vw1.w << 32) | vw1.z};
-                    const uint64_t allows[4] = {((uint64_t)aw0.y << 32) | aw0.x, ((uint64_t)aw0.w << 32) | aw0.z,
-                                                ((uint64_t)aw1.y << 32) | aw1.x, ((uint64_t)aw1.w << 32) | aw1.z};
+                    float n0[8], n1[8];
+                    read_norms8(0, n0);
+                    read_norms8(1, n1);
+                    nmax = n0[0];
 #pragma unroll
-                    for (int h = 0; h < 4; h++) {
-                        const uint64_t t = a.tile_begin + blk * 4 + h;
-                        uint64_t m = t < a.tile_end ? readfirstlane64(words[h]) : 0ull;
-                        if (a.allow) {
-                            const uint64_t aw = t - a.allow_t0;
-                            m &= aw < a.allow_words ? readfirstlane64(allows[h]) : 0ull;
-                        }
-                        vm[h] = m;
-                    }
+                    for (int j2 = 1; j2 < 8; j2++) nmax = __builtin_fmaxf(nmax, n0[j2]);
+#pragma unroll
+                    for (int j2 = 0; j2 < 8; j2++) nmax = __builtin_fmaxf(nmax, n1[j2]);
                 }
-                float k1r[2][4], k2r[2][4], svr[2][4];
+                float tmx = (lane_force || !(nmax <= 0x1p60f)) ? __builtin_inff() : -__builtin_inff();
 #pragma unroll
                 for (int mq = 0; mq < 2; mq++) {
-                    float4 k1v, k2v, sv;
-                    asm volatile("ds_read_b128 %0, %3\n\t"
-                                 "ds_read_b128 %1, %4\n\t"
-                                 "ds_read_b128 %2, %5\n\t"
-                                 "s_waitcnt lgkmcnt(0)"
-                                 : "=v"(k1v), "=v"(k2v), "=v"(sv)
-                                 : "v"((uint32_t)(uintptr_t)(ck1 + 32 * w + 16 * mq + qlane)),
-                                   "v"((uint32_t)(uintptr_t)(ck2 + 32 * w + 16 * mq + qlane)),
-                                   "v"((uint32_t)(uintptr_t)(WS + 16 * mq + qlane))
-                                 : "memory");
-                    k1r[mq][0] = k1v.x, k1r[mq][1] = k1v.y, k1r[mq][2] = k1v.z, k1r[mq][3] = k1v.w;
-                    k2r[mq][0] = k2v.x, k2r[mq][1] = k2v.y, k2r[mq][2] = k2v.z, k2r[mq][3] = k2v.w;
-                    svr[mq][0] = sv.x, svr[mq][1] = sv.y, svr[mq][2] = sv.z, svr[mq][3] = sv.w;
-                }
-                // fast check (K3c's): the largest u - sigma over the lane's 128 elements
-                const bool all_valid = (vm[0] & vm[1] & vm[2] & vm[3]) == ~0ull;
-                float mx = -__builtin_inff(), mnr_a[16];
+                    float k1r[4], k2r[4], svr[4];
+                    read_consts(mq, k1r, k2r, svr);
 #pragma unroll
-                for (int nr = 0; nr < 16; nr++) {
-                    float mnr = lane_force;
+                    for (int r = 0; r < 4; r++) {
+                        float m = agpr_read(acc[mq][0][r]);
 #pragma unroll
-                    for (int mq = 0; mq < 2; mq++)
-#pragma unroll
-                        for (int r = 0; r < 4; r++) {
-                            const float u = acc[mq][nr][r] + __builtin_fmaf(nrm[nr], k1r[mq][r], k2r[mq][r]);
-                            mnr = __builtin_fmaxf(mnr, u - svr[mq][r]);
-                        }
-                    mnr = nrm[nr] <= 0x1p60f ? mnr : __builtin_inff();
-                    if (!all_valid) {
-                        const uint32_t m16 = (uint32_t)(vm[nr >> 2] >> (16 * (nr & 3)));
-                        mnr = (m16 >> (lane & 15)) & 1u ? mnr : -__builtin_inff();
+                        for (int nr = 1; nr < 16; nr++) m = __builtin_fmaxf(m, agpr_read(acc[mq][nr][r]));
+                        tmx = __builtin_fmaxf(tmx, (m + __builtin_fmaf(nmax, k1r[r], k2r[r])) - svr[r]);
                     }
-                    mnr_a[nr] = mnr;
-                    mx = __builtin_fmaxf(mx, mnr);
                 }
-                const bool slow = __ballot(mx >= 0.f) && (DIAG & 4) == 0;
-                if constexpr ((DIAG & 16) != 0) {
-                    n_blk++;
-                    n_slow += slow;
-                }
+                const bool slow = __ballot(tmx >= 0.f) && (DIAG & 4) == 0;
                 if (slow) {
-                    if constexpr ((DIAG & 64) != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // diagnostic
-                    // only the row groups where some lane passed the fast check
+                    uint64_t vm[4];
+                    {
+                        uint4 vw0, vw1, aw0, aw1;
+                        uint32_t tmp;
+                        asm volatile("v_add_u32 %4, %5, %6\n\t"
+                                     "ds_read_b128 %0, %4 offset:1024\n\t"
+                                     "ds_read_b128 %1, %4 offset:1040\n\t"
+                                     "ds_read_b128 %2, %4 offset:1056\n\t"
+                                     "ds_read_b128 %3, %4 offset:1072\n\t"
+                                     "s_waitcnt lgkmcnt(0)"
+                                     : "=v"(vw0), "=v"(vw1), "=v"(aw0), "=v"(aw1), "=&v"(tmp)
+                                     : "s"(nsoff), "v"(sbase)
+                                     : "memory");
+                        const uint64_t words[4] = {((uint64_t)vw0.y << 32) | vw0.x, ((uint64_t)vw0.w << 32) | vw0.z,
+                                                   ((uint64_t)vw1.y << 32) | vw1.x, ((uint64_t)vw1.w << 32) | vw1.z};
+                        const uint64_t allows[4] = {((uint64_t)aw0.y << 32) | aw0.x, ((uint64_t)aw0.w << 32) | aw0.z,
+                                                    ((uint64_t)aw1.y << 32) | aw1.x, ((uint64_t)aw1.w << 32) | aw1.z};
 #pragma unroll
-                    for (int nr = 0; nr < 16; nr++) {
-                        if (!__ballot(mnr_a[nr] >= 0.f)) continue;
+                        for (int h = 0; h < 4; h++) {
+                            const uint64_t t = a.tile_begin + blk * 4 + h;
+                            uint64_t m = t < a.tile_end ? readfirstlane64(words[h]) : 0ull;
+                            if (a.allow) {
+                                const uint64_t aw = t - a.allow_t0;
+                                m &= aw < a.allow_words ? readfirstlane64(allows[h]) : 0ull;
+                            }
+                            vm[h] = m;
+                        }
+                    }
+                    const uint64_t slot0 = (a.tile_begin + blk * 4) * 64;
+                    // the lane's tag base (query qlane, row lane & 15)
+                    const uint32_t tagb = ((uint32_t)qlane << 8) | (uint32_t)(lane & 15);
+                    uint32_t resume = 0;
+                    for (;;) {
+                        uint32_t qn = 0, stop = 0xFFFFFFFFu;
+                        // re-defined every round: nothing derived from them is hoisted out of the
+                        // round loop (128 group masks and tags would not fit in registers)
+                        uint64_t vmr[4] = {vm[0], vm[1], vm[2], vm[3]};
+                        asm volatile("" : "+s"(vmr[0]), "+s"(vmr[1]), "+s"(vmr[2]), "+s"(vmr[3]));
+                        uint32_t tb = tagb;
+                        asm volatile("" : "+v"(tb));
 #pragma unroll
                         for (int mq = 0; mq < 2; mq++) {
-                            const uint64_t m16 = (vm[nr >> 2] >> (16 * (nr & 3))) & 0xFFFFull;
-                            const uint64_t m64 = m16 * 0x0001000100010001ull;
+                            float k1r[4], k2r[4], svr[4];
+                            read_consts(mq, k1r, k2r, svr);
 #pragma unroll
-                            for (int r = 0; r < 4; r++) {
-                                const float u = acc[mq][nr][r] + __builtin_fmaf(nrm[nr], k1r[mq][r], k2r[mq][r]);
-                                uint64_t pass = __ballot(!(u < svr[mq][r])) & m64 & qlive[mq][r];
-                                while (pass) {
-                                    const int src = __builtin_ctzll(pass);
-                                    pass &= pass - 1;
-                                    const int ql = 16 * mq + 4 * (src >> 4) + r;
-                                    const float us = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(u), src));
-                                    const uint32_t slot =
-                                        (uint32_t)((a.tile_begin + blk * 4) * 64 + 16 * nr + (src & 15));
-                                    if constexpr ((DIAG & 16) != 0) n_call++;
-                                    float ws_now;
-                                    if constexpr ((DIAG & 32) != 0)
-                                        ws_now = svr[mq][r];  // diagnostic: the scan of the exact path, no insertion
-                                    else
-                                        ws_now = sc_insert((lds_u64 *)(WL + ql * M), (lds_f32 *)(WT + ql),
-                                                           (lds_f32 *)(WS + ql), cem[32 * w + ql], K, cosine, us, slot);
-                                    const uint64_t grp = 0xFFFFull << (16 * (src >> 4));
-                                    pass &= ~grp | __ballot(!(u < ws_now));
+                            for (int hh = 0; hh < 2; hh++) {
+                                float nrm[8];
+                                read_norms8(hh, nrm);
+#pragma unroll
+                                for (int jn = 0; jn < 8; jn++) {
+                                    const int nr = 8 * hh + jn;
+                                    const uint64_t m64 =
+                                        ((vmr[nr >> 2] >> (16 * (nr & 3))) & 0xFFFFull) * 0x0001000100010001ull;
+#pragma unroll
+                                    for (int r = 0; r < 4; r++) {
+                                        const uint32_t gi = (uint32_t)((mq * 16 + nr) * 4 + r);
+                                        if (gi < resume || stop != 0xFFFFFFFFu) continue;
+                                        const float u =
+                                            agpr_read(acc[mq][nr][r]) + __builtin_fmaf(nrm[jn], k1r[r], k2r[r]);
+                                        // (padded queries are dropped by the flush: sl_flush's nlive)
+                                        const uint64_t pass = __ballot(!(u < svr[r])) & m64;
+                                        if (!pass) continue;
+                                        const uint32_t np = (uint32_t)__popcll(pass);
+                                        if (qn + np > (uint32_t)SD_QCAP) {
+                                            stop = gi;
+                                            continue;
+                                        }
+                                        if ((pass >> lane) & 1ull) {
+                                            const uint32_t pos =
+                                                qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(pass >> 32),
+                                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)pass, 0u));
+                                            // entry (u, tag = lane tag base + this group's query / row offset)
+                                            uint32_t tmp;
+                                            asm volatile("v_add_u32 %0, %2, %3\n\t"
+                                                         "ds_write2_b32 %1, %4, %0 offset1:1"
+                                                         : "=&v"(tmp)
+                                                         : "v"(qaddr + 8u * pos),
+                                                           "s"(((uint32_t)(16 * mq + r) << 8) + 16u * nr), "v"(tb), "v"(u)
+                                                         : "memory");
+                                        }
+                                        qn += np;
+                                    }
                                 }
                             }
                         }
+                        if constexpr ((DIAG & 16) != 0) {
+                            n_slow += resume == 0;
+                            n_call += qn;
+                        }
+                        if (qn) {
+                            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                            sl_flush(S, qaddr, qn, wsaddr, slot0, K, cosine, nlive);
+                        }
+                        if (stop == 0xFFFFFFFFu) break;
+                        resume = stop;
                     }
                 }
+            } else if constexpr ((DIAG & 8) != 0) {
+                // diagnostic (DIAG 10): the stage loop alone -- the accumulators are consumed by
+                // one sum, so the MFMAs stay (without any consumer the compiler removes them)
+                float x = 0.f;
+#pragma unroll
+                for (int mq = 0; mq < 2; mq++)
+#pragma unroll
+                    for (int nr = 0; nr < 16; nr++) x += agpr_read(acc[mq][nr][0]);
+                if (x == 0x1p-120f) a.partials[0] = 0;
             }
 #pragma unroll
             for (int mq = 0; mq < 2; mq++)
 #pragma unroll
                 for (int nr = 0; nr < 16; nr++) acc[mq][nr] = (floatx4){0.f, 0.f, 0.f, 0.f};
+            // the next block's first K block: its stage landed before the last barrier and is not
+            // overwritten before the next block's second barrier
+            read_half(0, 0, b0);
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1236,8 +1474,12 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
         case 2: kern = &screen_ar_kernel<24, 2>; break;
         case 4: kern = &screen_ar_kernel<24, 4>; break;
         case 16: kern = &screen_ar_kernel<24, 16>; break;
-        case 32: kern = &screen_ar_kernel<24, 32>; break;
-        case 96: kern = &screen_ar_kernel<24, 96>; break;
+        case 10: kern = &screen_ar_kernel<24, 10>; break;
+        case 42: kern = &screen_ar_kernel<24, 42>; break;    // 10 without the norm / tile-word loads
+        case 106: kern = &screen_ar_kernel<24, 106>; break;  // 42 without the per-unit s_barrier
+        case 138: kern = &screen_ar_kernel<24, 138>; break;  // 10 without any stage load
+        case 202: kern = &screen_ar_kernel<24, 202>; break;  // 138 without the s_barrier
+        case 32: kern = &screen_ar_kernel<24, 32>; break;    // the product without the norm / tile-word loads
         default: break;
         }
         if (kern != &screen_ar_kernel<24>)

@@ -280,7 +280,8 @@ static int run_screen(wvg_corpus *c, const ScanArgs &a, const SearchPlan &p, cha
 
 // Runs phase 1 + phase 2 for one corpus with device-resident prepared queries.
 int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t nq, uint32_t k, const uint64_t *d_allow,
-               const SearchPlan &p, uint64_t *partials, uint64_t *ids, float *dists, uint32_t *counts, hipStream_t s)
+               const SearchPlan &p, uint64_t *partials, uint64_t *ids, float *dists, uint32_t *counts, hipStream_t s,
+               StreamSlot *sl)
 {
     ScanArgs a{};
     a.data = c->d_data;
@@ -319,7 +320,32 @@ int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t nq, uin
         SearchPlan pe = p;  // no shadow: the exact MFMA path over the same workspace
         pe.screen = false;
         pe.groups = p.exact_groups;
-        return run_search(c, d_q, qpitch, nq, k, d_allow, pe, partials, ids, dists, counts, s);
+        return run_search(c, d_q, qpitch, nq, k, d_allow, pe, partials, ids, dists, counts, s, sl);
+    }
+    if (sl && nq == 1 && !p.gemm && !p.cosched && !d_allow && c->kind == WVG_KIND_F32 && tuning().pipeline_mode == 1) {
+        // One query of a host call: the query-stream kernel, whose extra workgroup merges
+        // the partial lists in the same launch (no second kernel, no gap between them);
+        // its arrival counter is the slot's persistent one, counted from the slot's base
+        // (no per-call memset).  A merge that gives up (4 s) leaves counts 0: the caller's
+        // check (search_batch) reports it.
+        uint32_t *ctl = nullptr;
+        int rc = sl->control(&ctl);
+        if (rc) return rc;
+        StreamJob j{};
+        j.partials = partials;
+        j.arrivals = ctl;
+        j.arrival_base = sl->arrival_base;
+        j.status = ctl + 1;
+        j.wait_limit = 400000000ull;
+        j.groups = (uint32_t)p.groups;
+        j.ids = ids;
+        j.dists = dists;
+        j.counts = counts;
+        ProfArm arm(c->ctx);
+        if (arm.rc) return arm.rc;
+        WVG_HIP(launch_scan_f32_stream(a, j, s));
+        sl->arrival_base += (uint32_t)p.groups;
+        return WVG_OK;
     }
     ProfArm arm(c->ctx);
     if (arm.rc) return arm.rc;
@@ -431,6 +457,106 @@ ScanArgs scan_args_for(const wvg_corpus *c, const void *d_q, uint32_t qpitch, ui
 
 using namespace wvg;
 
+// One caller's single-query search waiting in a corpus's coalescer.
+struct wvg_search_request {
+    const float *q;
+    uint32_t k;
+    uint64_t *ids;
+    float *dists;
+    uint32_t *counts;
+    int rc = WVG_OK;
+    std::string err;
+    bool done = false;
+};
+
+namespace wvg {
+
+// flat.SearchByVector for nq queries (the caller holds the corpus lock shared).
+static int search_batch(wvg_corpus *c, const float *queries, uint32_t nq, uint32_t k, const uint64_t *allow_bits,
+                        uint64_t allow_words, uint64_t *out_ids, float *out_dists, uint32_t *out_counts);
+
+// Queries a coalesced batch may take: K1 co-scheduled batches gain up to ~31
+// queries on one corpus (profiles/r03/measure_1/small.log.txt), dot / cosine
+// batches of >= mfma_min_queries go to the matrix cores.
+constexpr size_t COALESCE_MAX = 256;
+
+// Runs one coalesced batch (same k) and hands every request its own rows of
+// the result; a failure is every request's failure.
+static void run_coalesced(wvg_corpus *c, const std::vector<wvg_search_request *> &batch, uint32_t k)
+{
+    const size_t B = batch.size();
+    if (B == 1) {
+        wvg_search_request *r = batch[0];
+        r->rc = search_batch(c, r->q, 1, k, nullptr, 0, r->ids, r->dists, r->counts);
+        if (r->rc) r->err = wvg_last_error();
+        return;
+    }
+    const uint32_t d = c->dim;
+    std::vector<float> q(B * d), dists(B * k);
+    std::vector<uint64_t> ids(B * k);
+    std::vector<uint32_t> counts(B);
+    for (size_t i = 0; i < B; i++) std::memcpy(q.data() + i * d, batch[i]->q, (size_t)d * 4);
+    const int rc = search_batch(c, q.data(), (uint32_t)B, k, nullptr, 0, ids.data(), dists.data(), counts.data());
+    const std::string err = rc ? wvg_last_error() : std::string();
+    for (size_t i = 0; i < B; i++) {
+        wvg_search_request *r = batch[i];
+        r->rc = rc;
+        r->err = err;
+        if (rc) continue;
+        if (r->ids) std::memcpy(r->ids, ids.data() + i * k, (size_t)k * 8);
+        if (r->dists) std::memcpy(r->dists, dists.data() + i * k, (size_t)k * 4);
+        if (r->counts) *r->counts = counts[i];
+    }
+}
+
+// A single-query search through the corpus's coalescer: the request queues;
+// while no batch of this corpus executes, the first waiter takes every queued
+// request with the head's k (up to COALESCE_MAX) and runs them as one batch
+// (results identical to separate calls: tests/test_gpu_coalesce.py), then
+// wakes the others.  A lone call finds the coalescer idle and runs at once;
+// under load a batch forms from the calls that arrive while the previous one
+// runs, so the batch size follows the arrival rate.
+static int search_coalesced(wvg_corpus *c, const float *query, uint32_t k, uint64_t *out_ids, float *out_dists,
+                            uint32_t *out_counts)
+{
+    wvg_search_request r;
+    r.q = query;
+    r.k = k;
+    r.ids = out_ids;
+    r.dists = out_dists;
+    r.counts = out_counts;
+    wvg_coalescer &co = c->co;
+    std::unique_lock<std::mutex> g(co.mu);
+    co.pending.push_back(&r);
+    while (!r.done) {
+        if (co.busy) {
+            co.cv.wait(g);
+            continue;
+        }
+        co.busy = true;
+        std::vector<wvg_search_request *> batch;
+        const uint32_t kk = co.pending.front()->k;
+        for (auto it = co.pending.begin(); it != co.pending.end() && batch.size() < COALESCE_MAX;) {
+            if ((*it)->k == kk) {
+                batch.push_back(*it);
+                it = co.pending.erase(it);
+            } else {
+                ++it;
+            }
+        }
+        g.unlock();
+        run_coalesced(c, batch, kk);
+        g.lock();
+        for (wvg_search_request *b : batch) b->done = true;
+        co.busy = false;
+        co.cv.notify_all();
+    }
+    if (r.rc) set_error(r.err);
+    return r.rc;
+}
+
+}  // namespace wvg
+
 extern "C" {
 
 int wvg_search(wvg_corpus *c, const float *queries, uint32_t nq, uint32_t k, const uint64_t *allow_bits,
@@ -441,6 +567,17 @@ int wvg_search(wvg_corpus *c, const float *queries, uint32_t nq, uint32_t k, con
     if (nq > 0 && !queries) return fail(WVG_ERR_INVALID, "null queries");
     if (c->kind == WVG_KIND_PQ && !c->d_centers) return fail(WVG_ERR_INVALID, "PQ corpus has no codebook");
     std::shared_lock<std::shared_mutex> lk(c->rw);
+    if (nq == 1 && !allow_bits && k > 0 && k <= MAX_K && c->ctx->opt.coalesce)
+        return search_coalesced(c, queries, k, out_ids, out_dists, out_counts);
+    return search_batch(c, queries, nq, k, allow_bits, allow_words, out_ids, out_dists, out_counts);
+}
+
+}  // extern "C"
+
+static int wvg::search_batch(wvg_corpus *c, const float *queries, uint32_t nq, uint32_t k, const uint64_t *allow_bits,
+                             uint64_t allow_words, uint64_t *out_ids, float *out_dists, uint32_t *out_counts)
+{
+    int rc;
     SearchPlan p = plan_search(c, nq, std::min(k, MAX_K), allow_bits, allow_words);
     if (p.empty) {
         write_empty(nq, k, out_ids, out_dists, out_counts);
@@ -480,7 +617,7 @@ int wvg_search(wvg_corpus *c, const float *queries, uint32_t nq, uint32_t k, con
         d_allow = (const uint64_t *)(b + o_allow);
     }
     rc = run_search(c, b + o_q, qpitch, nq, k, d_allow, p, (uint64_t *)(b + o_part), (uint64_t *)(b + o_ids),
-                    (float *)(b + o_d), (uint32_t *)(b + o_cnt), s);
+                    (float *)(b + o_d), (uint32_t *)(b + o_cnt), s, g.slot);
     if (rc) return rc;
     const char *pin = out_b <= STAGE_MAX ? st.take(out_b) : nullptr;
     std::vector<char> big(pin ? 0 : out_b);
@@ -490,8 +627,15 @@ int wvg_search(wvg_corpus *c, const float *queries, uint32_t nq, uint32_t k, con
     if (out_ids) std::memcpy(out_ids, pin, (size_t)nq * k * 8);
     if (out_dists) std::memcpy(out_dists, pin + (o_d - o_ids), (size_t)nq * k * 4);
     if (out_counts) std::memcpy(out_counts, pin + (o_cnt - o_ids), (size_t)nq * 4);
+    if (nq == 1 && !d_allow && c->count > 0) {  // a live row exists: 0 results = the in-launch merge gave up
+        uint32_t c0 = 0;
+        std::memcpy(&c0, pin + (o_cnt - o_ids), 4);
+        if (c0 == 0) return fail(WVG_ERR_DEVICE, "single-query merge timed out waiting for the scan workgroups");
+    }
     return WVG_OK;
 }
+
+extern "C" {
 
 int wvg_search_bq_rescore(wvg_corpus *bq, wvg_corpus *f32, const float *queries, uint32_t nq, uint32_t k,
                           uint32_t rescore_limit, const uint64_t *allow_bits, uint64_t allow_words, uint64_t *out_ids,
