@@ -19,7 +19,8 @@ def main():
     ap.add_argument("--metric", default="cosine")
     ap.add_argument("--d", type=int, default=768)
     ap.add_argument("--n", type=int, default=30_077)
-    ap.add_argument("--nqs", default="32,64,96,128,129,160,256,300")
+    ap.add_argument("--cases", default="32:10,300:10,40:1,129:16,64:7,40:1,300:10")
+    ap.add_argument("--repeat", type=int, default=3)
     args = ap.parse_args()
     import torch
 
@@ -44,16 +45,17 @@ def main():
     a.delete(dead)
     b.delete(dead)
     srows = orc.normalize_rows(rows) if metric == METRIC_COSINE else rows
-    for nq in [int(x) for x in args.nqs.split(",")]:
-        for k in (10,):
+    for case in args.cases.split(","):
+        nq, k = (int(x) for x in case.split(":"))
+        bi, bd, bc = b.search(qs[:nq], k)
+        for rep in range(args.repeat):
             ai, ad, ac = a.search(qs[:nq], k)
-            bi, bd, bc = b.search(qs[:nq], k)
             bad = [q for q in range(nq) if not (np.array_equal(ai[q], bi[q]) and
                                                  np.array_equal(ad[q].view(np.uint32), bd[q].view(np.uint32)) and
                                                  ac[q] == bc[q])]
-            rec = {"nq": nq, "k": k, "mismatching_queries": len(bad), "first": bad[:12]}
+            rec = {"nq": nq, "k": k, "rep": rep, "mismatching_queries": len(bad), "first": bad[:12]}
             det = []
-            for q in bad[:4]:
+            for q in bad[:3]:
                 r = int(np.argmax((ai[q] != bi[q]) | (ad[q].view(np.uint32) != bd[q].view(np.uint32))))
                 qq = orc.normalize(qs[q]) if metric == METRIC_COSINE else qs[q]
                 od = orc.dist_all(2 if metric == METRIC_COSINE else 1, qq, srows)

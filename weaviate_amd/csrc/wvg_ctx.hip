@@ -65,6 +65,21 @@ int StreamSlot::host_pinned(size_t bytes, void **out)
     return WVG_OK;
 }
 
+int StreamSlot::host_coherent(size_t bytes, void **out)
+{
+    if (bytes > hcoh_bytes) {
+        if (hcoh) (void)hipHostFree(hcoh);
+        hcoh = nullptr;
+        hcoh_bytes = 0;
+        size_t want = std::max(bytes, (size_t)1 << 12);
+        hipError_t e = hipHostMalloc(&hcoh, want, hipHostMallocCoherent);
+        if (e != hipSuccess) return fail(WVG_ERR_NOMEM, std::string("hipHostMalloc (coherent): ") + hipGetErrorString(e));
+        hcoh_bytes = want;
+    }
+    *out = hcoh;
+    return WVG_OK;
+}
+
 // Next free profiling event pair of the context (grown on demand).
 int prof_pair(wvg_ctx *ctx, std::pair<hipEvent_t, hipEvent_t> *out)
 {
@@ -187,6 +202,7 @@ int wvg_close(wvg_ctx *ctx)
         (void)hipStreamSynchronize(s->stream);
         if (s->dscratch) (void)hipFree(s->dscratch);
         if (s->hpinned) (void)hipHostFree(s->hpinned);
+        if (s->hcoh) (void)hipHostFree(s->hcoh);
         if (s->dctl) (void)hipFree(s->dctl);
         (void)hipStreamDestroy(s->stream);
         delete s;

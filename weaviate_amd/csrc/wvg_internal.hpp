@@ -41,8 +41,13 @@ struct StreamSlot {
     // launch starts from -- no per-call memset
     uint32_t *dctl = nullptr;
     uint32_t arrival_base = 0;
+    // and its results: written by the merge workgroup straight into coherent
+    // (uncached, fine-grained) host memory -- no device-to-host copy per call
+    void *hcoh = nullptr;
+    size_t hcoh_bytes = 0;
     int device_scratch(size_t bytes, void **out);
     int host_pinned(size_t bytes, void **out);
+    int host_coherent(size_t bytes, void **out);
     int control(uint32_t **out);  // dctl, allocated and zeroed on first use
 };
 

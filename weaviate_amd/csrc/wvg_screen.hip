@@ -36,6 +36,8 @@
 // flags a query whose range list was full below tau (rows may have been
 // dropped): it is rescanned exactly (K1).
 // Roofline: bf16 MFMA, 2 Q N d FLOP per batch (2.5 PFLOP/s dense).
+#include <utility>
+
 #include "wvg_internal.hpp"
 
 namespace wvg {
@@ -783,6 +785,40 @@ __device__ __forceinline__ void sl_flush(SurvivorLists &S, uint32_t qaddr, uint3
     if (lane < 32) asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" ::"v"(wsaddr + 4u * lane), "v"(S.ws) : "memory");
 }
 
+// Compile-time loop (the K-block loop of K3d): the body sees its index as a
+// constant, so per-unit load counts and vmcnt waits are immediates.
+template <typename F, int... I>
+__device__ __forceinline__ void sd_static_for(F &f, std::integer_sequence<int, I...>)
+{
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void sd_static_for(F &&f)
+{
+    sd_static_for(f, std::make_integer_sequence<int, N>{});
+}
+
+// Vector-memory loads one K3d wave issues for unit u (K block u of a row
+// block): its 4 row-fragment pieces, and with unit 0 the block's row norms of
+// its tile (+ wave 0: the block's tile words).  DIAG 256 (tools): round 3's
+// norms / words with every unit.
+template <int DIAG>
+constexpr int sd_unit_loads(int u, bool w0)
+{
+    if ((DIAG & 128) != 0) return 0;
+    if ((DIAG & 32) != 0) return 4;
+    if ((DIAG & 256) != 0) return 5 + (w0 ? 1 : 0);
+    return 4 + (u == 0 ? 1 + (w0 ? 1 : 0) : 0);
+}
+// The loads issued after unit `first`'s, over units first + 1 .. first + n (mod KBN)
+template <int KBN, int DIAG>
+constexpr int sd_younger(int first, int n, bool w0)
+{
+    int c = 0;
+    for (int i = 1; i <= n; i++) c += sd_unit_loads<DIAG>((first + i) % KBN, w0);
+    return c;
+}
+
 // DIAG (tools build only; 0 in the product): bit 0 = no wait for the stage
 // loads, bit 1 = no epilogue (alone it lets the compiler delete the MFMAs, as
 // the round-3 "stage loop alone" diagnostics did: their 8.3 ms had no MFMA),
@@ -875,8 +911,9 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
             }
 
         // loads of one stage: wave w moves row fragments 4w .. 4w+3 (tile w,
-        // row groups 0..3), the norms of tile w, and wave 0 the block's tile
-        // words (so 6 loads per stage for wave 0, 5 for the others)
+        // row groups 0..3); with unit 0 also the norms of tile w, and wave 0
+        // the block's tile words (sd_unit_loads).  Round 3 reloaded the norms
+        // and words with every unit: 25 % more LDS-DMA issues per unit.
         const uint4 *lsrc = a.shadow + ((size_t)(a.tile_begin + blk0 * 4 + w) * KBN * 4) * 64 + lane;
         const float *lnorm = a.norms + (a.tile_begin + blk0 * 4 + w) * 64 + lane;
         uint64_t lblk = blk0;
@@ -888,9 +925,11 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
                 __builtin_amdgcn_global_load_lds(lsrc + ((size_t)ks * 4 + rg) * 64,
                                                  reinterpret_cast<uint4 *>(dst + (4 * w + rg) * 1024), 16, 0, 0);
             unsigned char *nslot = smem + SD_NBUF * SD_STAGE + (lblk & 1) * SD_NSLOT;
-            if constexpr ((DIAG & 32) == 0)
+            // the block's norms / tile words with its unit 0 (sd_unit_loads: the waits count them)
+            const bool with_norms = (DIAG & 32) == 0 && ((DIAG & 256) != 0 || ks == 0);
+            if (with_norms)
                 __builtin_amdgcn_global_load_lds(lnorm, reinterpret_cast<float *>(nslot + w * 256), 4, 0, 0);
-            if ((DIAG & 32) == 0 && w == 0) {
+            if (with_norms && w == 0) {
                 const uint32_t wi = (uint32_t)(lane & 7) >> 1, half = lane & 1;
                 const uint64_t t = a.tile_begin + lblk * 4 + wi;
                 const uint32_t *src =
@@ -907,15 +946,15 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
                 lnorm += 256;
             }
         };
-        // six stages in flight at every wait: the unit being waited for + 5 younger
-        auto wait_next = [&]() {
+        // six stages in flight at every wait: unit ks + 1 (waited for at K block ks) + the 5
+        // younger units ks + 2 .. ks + 6, whose loads the wait leaves outstanding
+        auto wait_next = [&](auto KS) {
             if constexpr ((DIAG & 129) != 0) return;
-            if constexpr ((DIAG & 32) != 0) {
-                asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
-                return;
-            }
-            if (w == 0) asm volatile("s_waitcnt vmcnt(30)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(25)" ::: "memory");
+            constexpr int ks = decltype(KS)::value;
+            constexpr int n0 = sd_younger<KBN, DIAG>(ks + 1, SD_NBUF - 3, true);
+            constexpr int n1 = sd_younger<KBN, DIAG>(ks + 1, SD_NBUF - 3, false);
+            if (w == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n0) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n1) : "memory");
         };
         auto raw_barrier = [&]() {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -987,14 +1026,14 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
         // block; the ring holds K block ks of any row block in buffer ks % 8)
 #pragma unroll
         for (int ks = 0; ks < SD_NBUF - 1; ks++) load_stage(ks);
-        if constexpr ((DIAG & 32) != 0) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-        else if (w == 0) asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(30)" ::: "memory");
+        // unit 0 landed: the 6 younger units 1 .. 6 outstanding
+        if (w == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(sd_younger<KBN, DIAG>(0, SD_NBUF - 2, true)) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(sd_younger<KBN, DIAG>(0, SD_NBUF - 2, false)) : "memory");
         raw_barrier();
         read_half(0, 0, b0);
         for (uint64_t blk = blk0; blk < blk1; blk++) {
-#pragma unroll
-            for (int ks = 0; ks < KBN; ks++) {
+            sd_static_for<KBN>([&](auto KS) {
+                constexpr int ks = decltype(KS)::value;
                 read_half(ks, 1, b1);
                 wait_b0(b0);
 #pragma unroll
@@ -1002,7 +1041,7 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
 #pragma unroll
                     for (int nr = 0; nr < 8; nr++)
                         acc[mq][nr] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(areg[ks][mq], b0[nr], acc[mq][nr], 0, 0, 0);
-                wait_next();   // the next unit landed
+                wait_next(KS);  // the next unit landed
                 raw_barrier(); // (lgkmcnt(0): this wave's second-half reads done)
 #pragma unroll
                 for (int j = 0; j < 8; j++) asm volatile("" : "+a"(b1[j]));
@@ -1015,7 +1054,15 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
                     for (int nr = 0; nr < 8; nr++)
                         acc[mq][8 + nr] =
                             __builtin_amdgcn_mfma_f32_16x16x32_bf16(areg[ks][mq], b1[nr], acc[mq][8 + nr], 0, 0, 0);
-            }
+            });
+            // The epilogue reads the accumulators through inline asm (agpr_read), which the
+            // compiler's hazard recognizer does not see: an MFMA's result may be read by a
+            // VALU op only after its passes + 2 wait states (XDL write -> VALU read; 11 for an
+            // 8-pass, 19 for a 16-pass op), so the block's last MFMAs get 24 here.  Without
+            // them a fast check could read a stale partial sum (seen as rare wrong top-k).
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
             // epilogue of row block blk (K3c's, over 16 row groups): C layout row
             // (query) qlane + r, column (row) 16 nr + (lane & 15)
             if constexpr ((DIAG & 2) == 0) {
@@ -1070,18 +1117,23 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
                 // raw score of the lane's rows + that E against WS is a superset test of
                 // every element (monotone roundings); finite on the fast-eligible inputs
                 // (query K1 <= 2^50, row norms <= 2^60), else the exact test runs
-                float nmax;
+                float nmax, nsum;  // (nsum: NaN when a norm is -- fmaxf would drop it)
                 {
                     float n0[8], n1[8];
                     read_norms8(0, n0);
                     read_norms8(1, n1);
                     nmax = n0[0];
+                    nsum = n0[0];
 #pragma unroll
-                    for (int j2 = 1; j2 < 8; j2++) nmax = __builtin_fmaxf(nmax, n0[j2]);
+                    for (int j2 = 1; j2 < 8; j2++) nmax = __builtin_fmaxf(nmax, n0[j2]), nsum += n0[j2];
 #pragma unroll
-                    for (int j2 = 0; j2 < 8; j2++) nmax = __builtin_fmaxf(nmax, n1[j2]);
+                    for (int j2 = 0; j2 < 8; j2++) nmax = __builtin_fmaxf(nmax, n1[j2]), nsum += n1[j2];
                 }
-                float tmx = (lane_force || !(nmax <= 0x1p60f)) ? __builtin_inff() : -__builtin_inff();
+                // per (query half mq, query r of the lane's four): whether some lane cannot rule
+                // out its 16 elements -- only those groups run the exact test (a wave-uniform
+                // bit each; typically one or two of the eight)
+                const bool force = lane_force || !(nmax <= 0x1p60f) || nsum != nsum;
+                uint32_t wact = 0;
 #pragma unroll
                 for (int mq = 0; mq < 2; mq++) {
                     float k1r[4], k2r[4], svr[4];
@@ -1091,10 +1143,11 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
                         float m = agpr_read(acc[mq][0][r]);
 #pragma unroll
                         for (int nr = 1; nr < 16; nr++) m = __builtin_fmaxf(m, agpr_read(acc[mq][nr][r]));
-                        tmx = __builtin_fmaxf(tmx, (m + __builtin_fmaf(nmax, k1r[r], k2r[r])) - svr[r]);
+                        const float t = (m + __builtin_fmaf(nmax, k1r[r], k2r[r])) - svr[r];
+                        if (__ballot(force || t >= 0.f)) wact |= 1u << (4 * mq + r);
                     }
                 }
-                const bool slow = __ballot(tmx >= 0.f) && (DIAG & 4) == 0;
+                const bool slow = wact != 0 && (DIAG & 4) == 0;
                 if (slow) {
                     uint64_t vm[4];
                     {
@@ -1138,21 +1191,23 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
                         asm volatile("" : "+v"(tb));
 #pragma unroll
                         for (int mq = 0; mq < 2; mq++) {
+                            if (((wact >> (4 * mq)) & 15u) == 0u) continue;
                             float k1r[4], k2r[4], svr[4];
                             read_consts(mq, k1r, k2r, svr);
 #pragma unroll
-                            for (int hh = 0; hh < 2; hh++) {
-                                float nrm[8];
-                                read_norms8(hh, nrm);
+                            for (int r = 0; r < 4; r++) {
+                                if (((wact >> (4 * mq + r)) & 1u) == 0u) continue;
 #pragma unroll
-                                for (int jn = 0; jn < 8; jn++) {
-                                    const int nr = 8 * hh + jn;
-                                    const uint64_t m64 =
-                                        ((vmr[nr >> 2] >> (16 * (nr & 3))) & 0xFFFFull) * 0x0001000100010001ull;
+                                for (int hh = 0; hh < 2; hh++) {
+                                    float nrm[8];
+                                    read_norms8(hh, nrm);
 #pragma unroll
-                                    for (int r = 0; r < 4; r++) {
-                                        const uint32_t gi = (uint32_t)((mq * 16 + nr) * 4 + r);
+                                    for (int jn = 0; jn < 8; jn++) {
+                                        const int nr = 8 * hh + jn;
+                                        const uint32_t gi = (uint32_t)((4 * mq + r) * 16 + nr);
                                         if (gi < resume || stop != 0xFFFFFFFFu) continue;
+                                        const uint64_t m64 =
+                                            ((vmr[nr >> 2] >> (16 * (nr & 3))) & 0xFFFFull) * 0x0001000100010001ull;
                                         const float u =
                                             agpr_read(acc[mq][nr][r]) + __builtin_fmaf(nrm[jn], k1r[r], k2r[r]);
                                         // (padded queries are dropped by the flush: sl_flush's nlive)
@@ -1480,6 +1535,8 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
         case 138: kern = &screen_ar_kernel<24, 138>; break;  // 10 without any stage load
         case 202: kern = &screen_ar_kernel<24, 202>; break;  // 138 without the s_barrier
         case 32: kern = &screen_ar_kernel<24, 32>; break;    // the product without the norm / tile-word loads
+        case 256: kern = &screen_ar_kernel<24, 256>; break;  // round 3's norms / words with every unit
+        case 266: kern = &screen_ar_kernel<24, 266>; break;  // 10 with round 3's per-unit norms / words
         default: break;
         }
         if (kern != &screen_ar_kernel<24>)

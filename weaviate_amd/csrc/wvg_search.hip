@@ -279,6 +279,13 @@ static int run_screen(wvg_corpus *c, const ScanArgs &a, const SearchPlan &p, cha
 }
 
 // Runs phase 1 + phase 2 for one corpus with device-resident prepared queries.
+// One query of a host call on the query-stream kernel with its in-launch merge
+// (run_search); its results can then go straight to host memory.
+static bool inlaunch_single(const wvg_corpus *c, uint32_t nq, const SearchPlan &p, bool has_allow)
+{
+    return nq == 1 && !p.gemm && !p.cosched && !has_allow && c->kind == WVG_KIND_F32 && tuning().pipeline_mode == 1;
+}
+
 int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t nq, uint32_t k, const uint64_t *d_allow,
                const SearchPlan &p, uint64_t *partials, uint64_t *ids, float *dists, uint32_t *counts, hipStream_t s,
                StreamSlot *sl)
@@ -322,7 +329,7 @@ int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t nq, uin
         pe.groups = p.exact_groups;
         return run_search(c, d_q, qpitch, nq, k, d_allow, pe, partials, ids, dists, counts, s, sl);
     }
-    if (sl && nq == 1 && !p.gemm && !p.cosched && !d_allow && c->kind == WVG_KIND_F32 && tuning().pipeline_mode == 1) {
+    if (sl && inlaunch_single(c, nq, p, d_allow != nullptr)) {
         // One query of a host call: the query-stream kernel, whose extra workgroup merges
         // the partial lists in the same launch (no second kernel, no gap between them);
         // its arrival counter is the slot's persistent one, counted from the slot's base
@@ -616,13 +623,24 @@ static int wvg::search_batch(wvg_corpus *c, const float *queries, uint32_t nq, u
         WVG_HIP(st.h2d(b + o_allow, p.allow_host, p.allow_bytes(), s));
         d_allow = (const uint64_t *)(b + o_allow);
     }
-    rc = run_search(c, b + o_q, qpitch, nq, k, d_allow, p, (uint64_t *)(b + o_part), (uint64_t *)(b + o_ids),
-                    (float *)(b + o_d), (uint32_t *)(b + o_cnt), s, g.slot);
+    // a single query merged in-launch writes its results straight into the slot's
+    // coherent host buffer: no device-to-host copy (and its ~10 us) per call
+    const bool zc = inlaunch_single(c, nq, p, d_allow != nullptr);
+    char *hc = nullptr;
+    if (zc) {
+        void *v = nullptr;
+        rc = g.slot->host_coherent(out_b, &v);
+        if (rc) return rc;
+        hc = (char *)v;
+    }
+    char *rspan = zc ? hc : b + o_ids;  // the result span [ids | dists | counts]
+    rc = run_search(c, b + o_q, qpitch, nq, k, d_allow, p, (uint64_t *)(b + o_part), (uint64_t *)rspan,
+                    (float *)(rspan + (o_d - o_ids)), (uint32_t *)(rspan + (o_cnt - o_ids)), s, g.slot);
     if (rc) return rc;
-    const char *pin = out_b <= STAGE_MAX ? st.take(out_b) : nullptr;
+    const char *pin = zc ? hc : out_b <= STAGE_MAX ? st.take(out_b) : nullptr;
     std::vector<char> big(pin ? 0 : out_b);
     if (!pin) pin = big.data();
-    WVG_HIP(hipMemcpyAsync((void *)pin, b + o_ids, out_b, hipMemcpyDeviceToHost, s));
+    if (!zc) WVG_HIP(hipMemcpyAsync((void *)pin, b + o_ids, out_b, hipMemcpyDeviceToHost, s));
     WVG_HIP(hipStreamSynchronize(s));
     if (out_ids) std::memcpy(out_ids, pin, (size_t)nq * k * 8);
     if (out_dists) std::memcpy(out_dists, pin + (o_d - o_ids), (size_t)nq * k * 4);
