@@ -218,7 +218,11 @@ int wvg_search_by_distance_window(wvg_corpus *c, const float *query, float targe
  * (a hipStream_t, NULL = default stream); no host synchronization, no
  * allocation (caller supplies a workspace of wvg_search_workspace_size bytes,
  * zero-filled once before its first use), so a call can be captured in a
- * hipGraph.  Queries must already be normalized for cosine.  One workspace
+ * hipGraph.  Exception: the first screened dot / cosine batch of a corpus
+ * (batch_screen) allocates and builds the corpus's bf16 shadow on `stream`;
+ * under capture that never happens -- a corpus without a current shadow takes
+ * the exact path, one with a shadow waits for it before the capture (run one
+ * uncaptured batch first to warm it).  d_counts may be NULL.  One workspace
  * serves any number of calls issued in order on one stream.  An empty corpus
  * (e.g. a rank whose slab holds no rows) yields empty results: ids
  * UINT64_MAX, dists +inf, counts 0 (as wvg_search).  wvg_search_device

@@ -224,6 +224,14 @@ def test_screen_device_path(ctx, exact_ctx, orc):
             torch.cuda.synchronize()
             _same((oi.cpu().numpy().view(np.uint64), od.cpu().numpy(), oc.cpu().numpy().astype(np.uint32)),
                   b.search(raw, k))
+        # d_counts = NULL (allowed by the header): the pilot and the merges keep their own counts
+        oi.fill_(0)
+        _lib.check(lib.wvg_search_device(a.handle, tq.data_ptr(), nq, k, oi.data_ptr(), od.data_ptr(), None,
+                                         ws.data_ptr(), ws.numel(), torch.cuda.current_stream().cuda_stream))
+        torch.cuda.synchronize()
+        ei, ed, _ = b.search(raw, k)
+        assert np.array_equal(oi.cpu().numpy().view(np.uint64), ei)
+        assert np.array_equal(od.cpu().numpy().view(np.uint32), ed.view(np.uint32))
     finally:
         a.destroy()
         b.destroy()

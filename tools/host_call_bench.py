@@ -22,6 +22,9 @@ def main():
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--dim", type=int, default=128)
     ap.add_argument("--calls", type=int, default=2000)
+    ap.add_argument("--gpcs", default="0", help="K1 workgroups per CU (tuning key 1; 0 = auto): comma list")
+    ap.add_argument("--modes", default="1,0", help="tuning key 2: 1 = in-launch merge, 0 = scan + merge kernel")
+    ap.add_argument("--coalesce", default="1,0")
     a = ap.parse_args()
     import torch
 
@@ -30,7 +33,7 @@ def main():
     from weaviate_amd.device import Context, Corpus
 
     out = {}
-    for coalesce in (1, 0):
+    for coalesce in (int(x) for x in a.coalesce.split(",")):
         ctx = Context(0, coalesce=coalesce)
         lib = ctx.lib
         lib.wvgx_set_tuning.restype = ctypes.c_int
@@ -40,8 +43,9 @@ def main():
         ids = np.empty(10, np.uint64)
         d = np.empty(10, np.float32)
         cnt = np.empty(1, np.uint32)
-        for mode in (1, 0):
+        for mode, gpc in ((int(m), int(g)) for m in a.modes.split(",") for g in a.gpcs.split(",")):
             prev = lib.wvgx_set_tuning(2, mode)
+            prevg = lib.wvgx_set_tuning(1, gpc)
             for i in range(50):
                 check(lib.wvg_search(c.handle, fptr(qs[i % 64]), 1, 10, None, 0, u64ptr(ids), fptr(d), u32ptr(cnt)))
             t0 = time.perf_counter()
@@ -55,13 +59,14 @@ def main():
             nl = ctypes.c_uint64()
             check(lib.wvg_profile_stop(ctx.handle, ctypes.byref(ms), ctypes.byref(nl)))
             kern_us = ms.value * 1e3 / max(1, nl.value)
-            out[f"coalesce{coalesce}_inlaunch{mode}"] = {
+            key = f"coalesce{coalesce}_inlaunch{mode}_gpc{gpc}"
+            out[key] = {
                 "us_per_call": round(wall * 1e6, 2), "scan_kernel_us": round(kern_us, 2),
                 "host_and_gap_us": round(wall * 1e6 - kern_us, 2), "profiled_launches": nl.value,
                 "frac_of_8TBs": round(a.rows * a.dim * 4 / wall / 8e12, 4)}
             lib.wvgx_set_tuning(2, prev)
-            print(json.dumps({f"coalesce{coalesce}_inlaunch{mode}": out[f"coalesce{coalesce}_inlaunch{mode}"]}),
-                  flush=True)
+            lib.wvgx_set_tuning(1, prevg)
+            print(json.dumps({key: out[key]}), flush=True)
         c.destroy()
         ctx.close()
 

@@ -197,9 +197,10 @@ int pq_dense(const wvg_corpus *c, const uint64_t *d_allow);
 void prepare_queries_host(const wvg_corpus *c, const float *queries, uint32_t nq, std::vector<float> &qf,
                           std::vector<uint64_t> &qb, uint32_t &qpitch);
 // sl: the calling host API's stream slot (a single query then merges in-launch), or null
+// qhost: the prepared host query of a single in-launch search (d_q null), passed in the kernel arguments
 int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t nq, uint32_t k, const uint64_t *d_allow,
                const SearchPlan &p, uint64_t *partials, uint64_t *ids, float *dists, uint32_t *counts, hipStream_t s,
-               StreamSlot *sl = nullptr);
+               StreamSlot *sl = nullptr, const float *qhost = nullptr);
 void write_empty(uint32_t nq, uint32_t k, uint64_t *ids, float *dists, uint32_t *counts);
 int stage_queries(wvg_corpus *c, StreamSlot *sl, const float *queries, uint32_t nq, char *dst, uint32_t &qpitch,
                   float *d_lut_or_null, char *d_qtmp, Staging *st = nullptr);

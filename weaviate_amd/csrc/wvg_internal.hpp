@@ -268,6 +268,7 @@ hipError_t launch_scan_f32(const ScanArgs &a, uint64_t *partials, int groups, hi
 // Sticky status word of a device-search workspace (its first bytes; read and
 // cleared by wvg_search_device_check).
 constexpr uint32_t WVG_STATUS_MERGE_TIMEOUT = 1u;
+constexpr uint32_t STREAM_QIN_FLOATS = 256;  // a query of up to 256 dims (f32 chunks) inline in StreamJob
 struct StreamJob {
     uint64_t *partials;  // [nq][groups][k]
     uint32_t *arrivals;  // [nq], arrival_base at launch
@@ -278,6 +279,9 @@ struct StreamJob {
     uint64_t *ids;
     float *dists;
     uint32_t *counts;
+    // a single host query rides in the kernel arguments (ScanArgs::queries null):
+    // no host-to-device copy (a blit dispatch + ~10 us of API time) per call
+    alignas(16) float qin[STREAM_QIN_FLOATS];
 };
 hipError_t launch_scan_f32_stream(const ScanArgs &a, const StreamJob &j, hipStream_t s);
 // ids KEY_NONE, dists +inf, counts 0 for nq queries (empty corpus / slab).

@@ -340,8 +340,10 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_stream_kernel(ScanAr
     const uint64_t gw = (uint64_t)blockIdx.x * SCAN_WAVES + wave_id();
     const uint64_t t0 = a.tile_begin + ntiles * gw / total;
     const uint64_t t1 = a.tile_begin + ntiles * (gw + 1) / total;
+    // (queries null: one query inline in the kernel arguments, StreamJob::qin)
+    const float4 *qsrc = a.queries ? reinterpret_cast<const float4 *>(a.queries) : reinterpret_cast<const float4 *>(j.qin);
     for (uint32_t q = 0; q < a.nq; q++) {
-        const float4 *q4 = reinterpret_cast<const float4 *>(a.queries) + (size_t)q * (a.qpitch / 4);
+        const float4 *q4 = qsrc + (size_t)q * (a.qpitch / 4);
         WaveTopK<E> tk;
         tk.init((int)a.k);
         scan_tiles<METRIC, D, E>(a, q4, t0, t1, tk, (a.reverse + q) & 1u);  // serpentine over the queries

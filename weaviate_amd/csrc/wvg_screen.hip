@@ -688,10 +688,8 @@ constexpr int SD_STAGE = SD_BFR * 1024;
 constexpr int SD_NBUF = 8;
 constexpr int SD_NSLOT = 1280;
 constexpr int SD_RING = SD_NBUF * SD_STAGE + 2 * SD_NSLOT;
-constexpr int SD_QCAP = 256;  // survivor queue entries per wave (8 B: u bits | query << 8 | row in block)
-constexpr int SD_QUEUE = SD_WAVES * SD_QCAP * 8;
 constexpr int SD_LISTS = SD_WAVES * 32 * SCREEN_M * 8;
-constexpr int SD_LDS = SD_RING + SD_QUEUE + SD_LISTS + SD_WAVES * 32 * 4 * 2 + SD_BQ * 4 * 3;
+constexpr int SD_LDS = SD_RING + SD_LISTS + SD_WAVES * 32 * 4 * 2 + SD_BQ * 4 * 3;
 static_assert(SD_LDS <= 160 * 1024, "K3d's LDS");
 
 // One accumulator element read where it is used.  Through C++ the compiler
@@ -720,70 +718,12 @@ __device__ __forceinline__ uint64_t row_shr1_64(uint64_t v)
     return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
 }
 
-// A wave's survivor state: the lists of the SCREEN_M smallest (lower, slot)
-// keys of its 32 queries stay in LDS (32 x 16 keys, ascending; only the
-// flush touches them), the per-query thresholds in registers: lane q < 32
-// holds query q's distance-space threshold WT = min(tau, k-th lower + 2 Emax,
-// M-th lower), its u-space form WS and Emax (sc_insert's state of round 3).
+// A wave's survivor lists: the SCREEN_M smallest (lower, slot) keys of each of
+// its 32 queries, ascending, in LDS (32 x 16 keys); a group of the epilogue
+// holds four of them in one register (see the slow path).
 struct SurvivorLists {
     uint32_t laddr;  // LDS byte address of the wave's 32 lists
-    float wt, ws, em;
 };
-
-// One survivor (wave-uniform arguments) into query ql's list; K3c's insertion
-// rule: drop if lower > WT or the list is full of smaller keys, else insert in
-// order (ties by slot) and tighten WT / WS.  LDS through inline asm with its
-// own lgkmcnt wait (see sl_flush).
-__device__ __forceinline__ void sl_insert(SurvivorLists &S, int ql, float u, uint32_t slot, int K, int cosine)
-{
-    const int lane = threadIdx.x & 63;
-    const float lower = sc_lower(u, cosine);
-    float wt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(S.wt), ql));
-    if (!(lower <= wt)) return;
-    const uint64_t key = ((uint64_t)wvg_ord_f32(lower) << 32) | slot;
-    const uint32_t la = S.laddr + (uint32_t)ql * (SCREEN_M * 8) + 8u * (uint32_t)(lane & 15);
-    uint2 v2;
-    asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v2) : "v"(la) : "memory");
-    const uint64_t v = lane < SCREEN_M ? (((uint64_t)v2.y << 32) | v2.x) : WVG_KEY_NONE;
-    if (!(key < readlane64(v, SCREEN_M - 1))) return;
-    const int pos = __popcll(__ballot(lane < SCREEN_M && v < key));
-    const uint64_t sh = row_shr1_64(v);
-    const uint64_t nv = lane > pos ? sh : (lane == pos ? key : v);
-    if (lane >= pos && lane < SCREEN_M) {
-        const uint2 o = make_uint2((uint32_t)nv, (uint32_t)(nv >> 32));
-        asm volatile("ds_write_b64 %0, %1" ::"v"(la), "v"(o) : "memory");
-    }
-    const uint64_t nk = readlane64(nv, K - 1), nm = readlane64(nv, SCREEN_M - 1);
-    const float em = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(S.em), ql));
-    if (nk != WVG_KEY_NONE) wt = fminf(wt, sc_tau_k(key_lower(nk), em, cosine));
-    if (nm != WVG_KEY_NONE) wt = fminf(wt, key_lower(nm));
-    const float ws = sc_sigma(wt, cosine);
-    S.wt = lane == ql ? wt : S.wt;
-    S.ws = lane == ql ? ws : S.ws;
-}
-
-// Drains a wave's queue (n entries at LDS byte address qaddr) into its lists,
-// then stores the new WS of its 32 queries at LDS address wsaddr (read by the
-// next epilogue).  LDS only through inline asm, with its own lgkmcnt waits:
-// the compiler cannot tell these accesses from the in-flight LDS DMA of the
-// stage ring and would put a vmcnt(0) before each.
-__device__ __forceinline__ void sl_flush(SurvivorLists &S, uint32_t qaddr, uint32_t n, uint32_t wsaddr,
-                                         uint64_t slot0, int K, int cosine, uint32_t nlive)
-{
-    const int lane = threadIdx.x & 63;
-    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
-        uint2 e;
-        asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(e) : "v"(qaddr + 8u * (i0 + lane)) : "memory");
-        const uint32_t cnt = n - i0 < 64 ? n - i0 : 64;
-        for (uint32_t j = 0; j < cnt; j++) {
-            const float u = __int_as_float(__builtin_amdgcn_readlane((int)e.x, (int)j));
-            const uint32_t tag = (uint32_t)__builtin_amdgcn_readlane((int)e.y, (int)j);
-            if ((tag >> 8) >= nlive) continue;  // a padded query of the last block (q >= nq)
-            sl_insert(S, (int)(tag >> 8), u, (uint32_t)(slot0 + (tag & 255u)), K, cosine);
-        }
-    }
-    if (lane < 32) asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" ::"v"(wsaddr + 4u * lane), "v"(S.ws) : "memory");
-}
 
 // Compile-time loop (the K-block loop of K3d): the body sees its index as a
 // constant, so per-unit load counts and vmcnt waits are immediates.
@@ -831,9 +771,8 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
 {
     static_assert(KBN % SD_NBUF == 0, "the stage buffer of a K block must be a compile-time constant");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    unsigned char *queue = smem + SD_RING;  // [4][SD_QCAP] x 8 B
-    uint64_t *lists = reinterpret_cast<uint64_t *>(smem + SD_RING + SD_QUEUE);  // [4][32][M]
-    float *tau = reinterpret_cast<float *>(smem + SD_RING + SD_QUEUE + SD_LISTS);
+    uint64_t *lists = reinterpret_cast<uint64_t *>(smem + SD_RING);  // [4][32][M]
+    float *tau = reinterpret_cast<float *>(smem + SD_RING + SD_LISTS);
     float *sig = tau + SD_WAVES * 32;
     float *ck1 = sig + SD_WAVES * 32;
     float *ck2 = ck1 + SD_BQ;
@@ -876,9 +815,9 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
     __syncthreads();
     SurvivorLists S;
     S.laddr = (uint32_t)(uintptr_t)(lists + (size_t)w * 32 * M);
-    S.wt = tau[w * 32 + (lane & 31)];
-    S.ws = sig[w * 32 + (lane & 31)];
-    S.em = cem[w * 32 + (lane & 31)];
+    // the wave's per-query thresholds WT (tau), their u-space form WS (sig) and Emax
+    // (cem): LDS byte address of tau[w][0]; sig, cem at + 512, + 2048
+    const uint32_t tbase = (uint32_t)(uintptr_t)(tau + w * 32);
     if (blk0 < blk1) {
         // the wave's 32 queries, every K block, resident for the whole range
         bf16x8 areg[KBN][2];
@@ -948,11 +887,17 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
         };
         // six stages in flight at every wait: unit ks + 1 (waited for at K block ks) + the 5
         // younger units ks + 2 .. ks + 6, whose loads the wait leaves outstanding
+        // PAIR (tools A/B, DIAG 1024): one wait + barrier per two K blocks -- at even ks for
+        // unit ks + 2 (units ks + 3 .. ks + 6 outstanding), which also covers the odd
+        // iteration's reads of unit ks + 1; the two units ks + 7, ks + 8 load after it
+        constexpr bool PAIR = (DIAG & 1024) != 0;
         auto wait_next = [&](auto KS) {
             if constexpr ((DIAG & 129) != 0) return;
             constexpr int ks = decltype(KS)::value;
-            constexpr int n0 = sd_younger<KBN, DIAG>(ks + 1, SD_NBUF - 3, true);
-            constexpr int n1 = sd_younger<KBN, DIAG>(ks + 1, SD_NBUF - 3, false);
+            if constexpr (PAIR && (ks & 1) != 0) return;
+            constexpr int first = PAIR ? ks + 2 : ks + 1, n = PAIR ? SD_NBUF - 4 : SD_NBUF - 3;
+            constexpr int n0 = sd_younger<KBN, DIAG>(first, n, true);
+            constexpr int n1 = sd_younger<KBN, DIAG>(first, n, false);
             if (w == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n0) : "memory");
             else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n1) : "memory");
         };
@@ -996,11 +941,6 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
                          : "memory");
         };
         const int qlane = 4 * (lane >> 4);
-        // the wave's queries below nq (a batch's last workgroup is padded)
-        const uint32_t qw0 = q0 + 32 * (uint32_t)w;
-        const uint32_t nlive = a.nq > qw0 ? (a.nq - qw0 < 32 ? a.nq - qw0 : 32u) : 0u;
-        const uint32_t qaddr = (uint32_t)(uintptr_t)(queue + (size_t)w * SD_QCAP * 8);
-        const uint32_t wsaddr = (uint32_t)(uintptr_t)(sig + w * 32);
         // epilogue lane bases: smem (+ the tile-word bytes, lane-independent), the
         // row norm of this lane's column, this lane's first query in sig / ck1 / ck2
         const uint32_t sbase = (uint32_t)(uintptr_t)smem;
@@ -1042,11 +982,20 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
                     for (int nr = 0; nr < 8; nr++)
                         acc[mq][nr] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(areg[ks][mq], b0[nr], acc[mq][nr], 0, 0, 0);
                 wait_next(KS);  // the next unit landed
-                raw_barrier(); // (lgkmcnt(0): this wave's second-half reads done)
+                if constexpr (!PAIR || (ks & 1) == 0)
+                    raw_barrier();  // (lgkmcnt(0): this wave's second-half reads done)
+                else
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
                 for (int j = 0; j < 8; j++) asm volatile("" : "+a"(b1[j]));
-                // unit + 7 into the buffer of unit - 1 (fully read before this barrier)
-                load_stage((ks + SD_NBUF - 1) % KBN);
+                // unit + 7 into the buffer of unit - 1 (fully read before this barrier); PAIR:
+                // also unit + 8 into the buffer of this unit (its reads done: the barrier's wait)
+                if constexpr (!PAIR) {
+                    load_stage((ks + SD_NBUF - 1) % KBN);
+                } else if constexpr ((ks & 1) == 0) {
+                    load_stage((ks + SD_NBUF - 1) % KBN);
+                    load_stage((ks + SD_NBUF) % KBN);
+                }
                 if (ks + 1 < KBN) read_half(ks + 1, 0, b0);  // (the next block's first half: after the epilogue)
 #pragma unroll
                 for (int mq = 0; mq < 2; mq++)
@@ -1058,24 +1007,21 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
             // The epilogue reads the accumulators through inline asm (agpr_read), which the
             // compiler's hazard recognizer does not see: an MFMA's result may be read by a
             // VALU op only after its passes + 2 wait states (XDL write -> VALU read; 11 for an
-            // 8-pass, 19 for a 16-pass op), so the block's last MFMAs get 24 here.  Without
-            // them a fast check could read a stale partial sum (seen as rare wrong top-k).
+            // 8-pass, 19 for a 16-pass op), so the block's last MFMAs get 24 here (the norm
+            // reads that come first usually cover them; this makes it unconditional).
             __builtin_amdgcn_sched_barrier(0);
             asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
             // epilogue of row block blk (K3c's, over 16 row groups): C layout row
             // (query) qlane + r, column (row) 16 nr + (lane & 15)
             if constexpr ((DIAG & 2) == 0) {
-                // Fast check, then (rarely) the exact test per element.  The exact test
-                // !(u < WS) (NaN-safe: a non-finite row or query always passes) queues the
-                // survivors of an element group with one ballot, one mbcnt and one ds_write;
-                // after the pass they are inserted from one code site (sl_flush).  A pass
-                // that would overflow the queue stops at that element group, drains the
-                // queue and resumes there with the tightened thresholds.  Register budget:
-                // the resident queries hold most of the VGPRs, so the pass walks one query
-                // half (mq) and eight row groups at a time with only those constants and row
-                // norms in registers, and reads each accumulator element where it is used
-                // (agpr_read); every epilogue LDS address is a lane base + an SGPR offset.
+                // Fast check per query group, then the exact test !(u < WS) (NaN-safe: a
+                // non-finite row or query always passes) on the groups the check could not
+                // rule out, survivors inserted into register-held lists (the slow path
+                // below).  Accumulators are read where they are used (agpr_read); every
+                // epilogue LDS access is inline asm with its own lgkmcnt wait (through C++
+                // the compiler cannot tell them from the stage ring's LDS DMA and waits
+                // vmcnt(0), draining the prefetch), at a lane base + an SGPR offset.
                 const uint32_t nsoff = (uint32_t)(SD_NBUF * SD_STAGE + (blk & 1) * SD_NSLOT);  // the block's norms
                 auto read_norms8 = [&](int hh, float (&nrm)[8]) {  // row norms of row groups 8 hh .. 8 hh + 7
                     uint32_t tmp;
@@ -1178,75 +1124,89 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
                         }
                     }
                     const uint64_t slot0 = (a.tile_begin + blk * 4) * 64;
-                    // the lane's tag base (query qlane, row lane & 15)
-                    const uint32_t tagb = ((uint32_t)qlane << 8) | (uint32_t)(lane & 15);
-                    uint32_t resume = 0;
-                    for (;;) {
-                        uint32_t qn = 0, stop = 0xFFFFFFFFu;
-                        // re-defined every round: nothing derived from them is hoisted out of the
-                        // round loop (128 group masks and tags would not fit in registers)
-                        uint64_t vmr[4] = {vm[0], vm[1], vm[2], vm[3]};
-                        asm volatile("" : "+s"(vmr[0]), "+s"(vmr[1]), "+s"(vmr[2]), "+s"(vmr[3]));
-                        uint32_t tb = tagb;
-                        asm volatile("" : "+v"(tb));
+                    if constexpr ((DIAG & 16) != 0) n_slow++;
+                    // Per active group gi = (mq, r): lane l tests its column's 16 rows against
+                    // query ql = 16 mq + r + qlane (C layout), and row l >> 4 of the register v
+                    // holds that same query's list (lane l: entry l & 15) -- the four queries of
+                    // the group, one per 16-lane row.  A survivor is inserted into its own row in
+                    // registers (DPP shift), the row's thresholds tighten at once, and the lists
+                    // and thresholds go back to LDS once per group.  The group loop is not
+                    // unrolled (the code would not fit the unroller's budget); its 16
+                    // accumulator elements come out of the AGPRs through one switch.
+                    float nrm16[16];
+                    read_norms8(0, *reinterpret_cast<float(*)[8]>(&nrm16[0]));
+                    read_norms8(1, *reinterpret_cast<float(*)[8]>(&nrm16[8]));
+                    for (uint32_t gw = wact; gw; gw &= gw - 1) {
+                        const int gi = __builtin_ctz(gw);
+                        float uv[16];
+                        switch (gi) {
+#define WVG_SD_GROUP(G)                                                                        \
+    case G:                                                                                    \
+        _Pragma("unroll") for (int nr = 0; nr < 16; nr++) uv[nr] = agpr_read(acc[(G) >> 2][nr][(G) & 3]); \
+        break;
+                        WVG_SD_GROUP(0) WVG_SD_GROUP(1) WVG_SD_GROUP(2) WVG_SD_GROUP(3)
+                        WVG_SD_GROUP(4) WVG_SD_GROUP(5) WVG_SD_GROUP(6) WVG_SD_GROUP(7)
+#undef WVG_SD_GROUP
+                        default: break;
+                        }
+                        const uint32_t ql = 16u * (uint32_t)(gi >> 2) + (uint32_t)(gi & 3) + (uint32_t)qlane;
+                        const uint32_t la = S.laddr + ql * (SCREEN_M * 8) + 8u * (uint32_t)(lane & 15);
+                        const uint32_t ta = tbase + 4u * ql;  // tau; sig + 512, ck1 + 1024, ck2 + 1536, cem + 2048
+                        uint2 v2;
+                        float wt, ws, em, k1, k2;
+                        asm volatile("ds_read_b64 %0, %6\n\t"
+                                     "ds_read_b32 %1, %7\n\t"
+                                     "ds_read_b32 %2, %7 offset:512\n\t"
+                                     "ds_read_b32 %3, %7 offset:2048\n\t"
+                                     "ds_read_b32 %4, %7 offset:1024\n\t"
+                                     "ds_read_b32 %5, %7 offset:1536\n\t"
+                                     "s_waitcnt lgkmcnt(0)"
+                                     : "=v"(v2), "=v"(wt), "=v"(ws), "=v"(em), "=v"(k1), "=v"(k2)
+                                     : "v"(la), "v"(ta)
+                                     : "memory");
+                        uint64_t v = ((uint64_t)v2.y << 32) | v2.x;
+                        const int li = lane & 15;
 #pragma unroll
-                        for (int mq = 0; mq < 2; mq++) {
-                            if (((wact >> (4 * mq)) & 15u) == 0u) continue;
-                            float k1r[4], k2r[4], svr[4];
-                            read_consts(mq, k1r, k2r, svr);
-#pragma unroll
-                            for (int r = 0; r < 4; r++) {
-                                if (((wact >> (4 * mq + r)) & 1u) == 0u) continue;
-#pragma unroll
-                                for (int hh = 0; hh < 2; hh++) {
-                                    float nrm[8];
-                                    read_norms8(hh, nrm);
-#pragma unroll
-                                    for (int jn = 0; jn < 8; jn++) {
-                                        const int nr = 8 * hh + jn;
-                                        const uint32_t gi = (uint32_t)((4 * mq + r) * 16 + nr);
-                                        if (gi < resume || stop != 0xFFFFFFFFu) continue;
-                                        const uint64_t m64 =
-                                            ((vmr[nr >> 2] >> (16 * (nr & 3))) & 0xFFFFull) * 0x0001000100010001ull;
-                                        const float u =
-                                            agpr_read(acc[mq][nr][r]) + __builtin_fmaf(nrm[jn], k1r[r], k2r[r]);
-                                        // (padded queries are dropped by the flush: sl_flush's nlive)
-                                        const uint64_t pass = __ballot(!(u < svr[r])) & m64;
-                                        if (!pass) continue;
-                                        const uint32_t np = (uint32_t)__popcll(pass);
-                                        if (qn + np > (uint32_t)SD_QCAP) {
-                                            stop = gi;
-                                            continue;
-                                        }
-                                        if ((pass >> lane) & 1ull) {
-                                            const uint32_t pos =
-                                                qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(pass >> 32),
-                                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)pass, 0u));
-                                            // entry (u, tag = lane tag base + this group's query / row offset)
-                                            uint32_t tmp;
-                                            asm volatile("v_add_u32 %0, %2, %3\n\t"
-                                                         "ds_write2_b32 %1, %4, %0 offset1:1"
-                                                         : "=&v"(tmp)
-                                                         : "v"(qaddr + 8u * pos),
-                                                           "s"(((uint32_t)(16 * mq + r) << 8) + 16u * nr), "v"(tb), "v"(u)
-                                                         : "memory");
-                                        }
-                                        qn += np;
-                                    }
-                                }
+                        for (int nr = 0; nr < 16; nr++) {
+                            const uint64_t m64 = ((vm[nr >> 2] >> (16 * (nr & 3))) & 0xFFFFull) * 0x0001000100010001ull;
+                            const float u = uv[nr] + __builtin_fmaf(nrm16[nr], k1, k2);
+                            uint64_t pass = __ballot(!(u < ws)) & m64;
+                            while (pass) {
+                                const int j = __builtin_ctzll(pass);
+                                pass &= pass - 1;
+                                const int g = j >> 4;
+                                const float lower =
+                                    sc_lower(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(u), j)), cosine);
+                                float wtg = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wt), j));
+                                if (!(lower <= wtg)) continue;
+                                if constexpr ((DIAG & 16) != 0) n_call++;
+                                const uint64_t key = ((uint64_t)wvg_ord_f32(lower) << 32) |
+                                                     (uint32_t)(slot0 + 16u * (uint32_t)nr + (uint32_t)(j & 15));
+                                if (!(key < readlane64(v, 16 * g + SCREEN_M - 1))) continue;
+                                const bool inrow = (lane >> 4) == g;
+                                const int pos = __popcll(__ballot(inrow && v < key));
+                                const uint64_t sh = row_shr1_64(v);
+                                v = inrow ? (li > pos ? sh : (li == pos ? key : v)) : v;
+                                const uint64_t nk = readlane64(v, 16 * g + K - 1);
+                                const uint64_t nm = readlane64(v, 16 * g + SCREEN_M - 1);
+                                const float emg = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(em), j));
+                                if (nk != WVG_KEY_NONE) wtg = fminf(wtg, sc_tau_k(key_lower(nk), emg, cosine));
+                                if (nm != WVG_KEY_NONE) wtg = fminf(wtg, key_lower(nm));
+                                const float wsg = sc_sigma(wtg, cosine);
+                                wt = inrow ? wtg : wt;
+                                ws = inrow ? wsg : ws;
+                                // the row's other survivors of this element group meet the new threshold
+                                pass &= ~(0xFFFFull << (16 * g)) | __ballot(!(u < ws));
                             }
                         }
-                        if constexpr ((DIAG & 16) != 0) {
-                            n_slow += resume == 0;
-                            n_call += qn;
-                        }
-                        if (qn) {
-                            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                            sl_flush(S, qaddr, qn, wsaddr, slot0, K, cosine, nlive);
-                        }
-                        if (stop == 0xFFFFFFFFu) break;
-                        resume = stop;
+                        const uint2 o2 = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+                        asm volatile("ds_write_b64 %0, %1" ::"v"(la), "v"(o2) : "memory");
+                        if (li == 0)
+                            asm volatile("ds_write_b32 %0, %1\n\t"
+                                         "ds_write_b32 %0, %2 offset:512" ::"v"(ta), "v"(wt), "v"(ws)
+                                         : "memory");
                     }
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 }
             } else if constexpr ((DIAG & 8) != 0) {
                 // diagnostic (DIAG 10): the stage loop alone -- the accumulators are consumed by
@@ -1537,6 +1497,8 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
         case 32: kern = &screen_ar_kernel<24, 32>; break;    // the product without the norm / tile-word loads
         case 256: kern = &screen_ar_kernel<24, 256>; break;  // round 3's norms / words with every unit
         case 266: kern = &screen_ar_kernel<24, 266>; break;  // 10 with round 3's per-unit norms / words
+        case 1024: kern = &screen_ar_kernel<24, 1024>; break;  // one barrier per two K blocks
+        case 1034: kern = &screen_ar_kernel<24, 1034>; break;  // 10 with one barrier per two K blocks
         default: break;
         }
         if (kern != &screen_ar_kernel<24>)

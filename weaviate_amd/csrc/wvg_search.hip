@@ -288,7 +288,7 @@ static bool inlaunch_single(const wvg_corpus *c, uint32_t nq, const SearchPlan &
 
 int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t nq, uint32_t k, const uint64_t *d_allow,
                const SearchPlan &p, uint64_t *partials, uint64_t *ids, float *dists, uint32_t *counts, hipStream_t s,
-               StreamSlot *sl)
+               StreamSlot *sl, const float *qhost)
 {
     ScanArgs a{};
     a.data = c->d_data;
@@ -348,6 +348,11 @@ int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t nq, uin
         j.ids = ids;
         j.dists = dists;
         j.counts = counts;
+        if (!d_q) {  // the query in the kernel arguments
+            if (!qhost || qpitch > STREAM_QIN_FLOATS) return fail(WVG_ERR_INVALID, "inline query missing or too long");
+            std::memcpy(j.qin, qhost, (size_t)qpitch * 4);
+            a.queries = nullptr;
+        }
         ProfArm arm(c->ctx);
         if (arm.rc) return arm.rc;
         WVG_HIP(launch_scan_f32_stream(a, j, s));
@@ -616,8 +621,17 @@ static int wvg::search_batch(wvg_corpus *c, const float *queries, uint32_t nq, u
                                 (p.allow_host ? stage_bytes(p.allow_bytes()) : 0) + stage_bytes(out_b));
     if (rc) return rc;
     uint32_t qpitch = 0;
-    rc = stage_queries(c, g.slot, queries, nq, b + o_q, qpitch, (float *)(b + o_q), b + o_qtmp, &st);
-    if (rc) return rc;
+    // a single in-launch F32 query of up to STREAM_QIN_FLOATS floats goes in the kernel arguments
+    std::vector<float> qinl;
+    const bool qin = inlaunch_single(c, nq, p, p.allow_host != nullptr) &&
+                     (size_t)f32_chunks(c->dim) * 4 <= STREAM_QIN_FLOATS;
+    if (qin) {
+        std::vector<uint64_t> qb;
+        prepare_queries_host(c, queries, nq, qinl, qb, qpitch);
+    } else {
+        rc = stage_queries(c, g.slot, queries, nq, b + o_q, qpitch, (float *)(b + o_q), b + o_qtmp, &st);
+        if (rc) return rc;
+    }
     const uint64_t *d_allow = nullptr;
     if (p.allow_host) {
         WVG_HIP(st.h2d(b + o_allow, p.allow_host, p.allow_bytes(), s));
@@ -634,8 +648,9 @@ static int wvg::search_batch(wvg_corpus *c, const float *queries, uint32_t nq, u
         hc = (char *)v;
     }
     char *rspan = zc ? hc : b + o_ids;  // the result span [ids | dists | counts]
-    rc = run_search(c, b + o_q, qpitch, nq, k, d_allow, p, (uint64_t *)(b + o_part), (uint64_t *)rspan,
-                    (float *)(rspan + (o_d - o_ids)), (uint32_t *)(rspan + (o_cnt - o_ids)), s, g.slot);
+    rc = run_search(c, qin ? nullptr : b + o_q, qpitch, nq, k, d_allow, p, (uint64_t *)(b + o_part), (uint64_t *)rspan,
+                    (float *)(rspan + (o_d - o_ids)), (uint32_t *)(rspan + (o_cnt - o_ids)), s, g.slot,
+                    qin ? qinl.data() : nullptr);
     if (rc) return rc;
     const char *pin = zc ? hc : out_b <= STAGE_MAX ? st.take(out_b) : nullptr;
     std::vector<char> big(pin ? 0 : out_b);
