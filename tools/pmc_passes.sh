@@ -23,5 +23,8 @@ if [ "${PMC_MFMA:-0}" = 1 ]; then  # matrix-core kernels: MFMA busy / co-issue a
   run p5 "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_MFMA SQ_VALU_MFMA_COEXEC_CYCLES SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE" "$@" || exit $?
   run p6 "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_DRAM_sum" "$@" || exit $?
 fi
+if [ "${PMC_ICACHE:-0}" = 1 ]; then  # instruction-cache misses (large unrolled kernels)
+  run p7 "SQC_ICACHE_MISSES SQC_ICACHE_HITS" "$@" || exit $?
+fi
 python3 tools/pmc_summary.py "$O" > "$O/summary.txt"
 cat "$O/summary.txt"

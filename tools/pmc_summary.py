@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-kernel averages of every PMC counter and the dispatch time in one or
-more rocprofv3 sqlite outputs (tooling).  Usage: pmc_summary.py <dir-or-db>... [--match SUBSTR]"""
+more rocprofv3 outputs, sqlite or csv (tooling).  Usage: pmc_summary.py <dir-or-db>... [--match SUBSTR]"""
 import argparse
 import collections
 import glob
@@ -21,16 +21,36 @@ def rows(db):
         yield name, dur, dict(vals.get(ev, {}))
 
 
+def csv_rows(path):
+    """rocprofv3 --output-format csv: one row per (dispatch, counter)."""
+    import csv
+    disp = {}
+    vals = collections.defaultdict(lambda: collections.defaultdict(float))
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            d = r.get("Dispatch_Id") or r.get("Correlation_Id")
+            try:
+                dur = int(r.get("End_Timestamp") or 0) - int(r.get("Start_Timestamp") or 0)
+            except ValueError:
+                dur = 0
+            disp[d] = (r.get("Kernel_Name", "?"), dur)
+            vals[d][r["Counter_Name"]] += float(r["Counter_Value"])
+    for d, (name, dur) in disp.items():
+        yield name, dur, dict(vals[d])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("paths", nargs="+")
     ap.add_argument("--match", default="")
     a = ap.parse_args()
     for p in a.paths:
-        dbs = [p] if p.endswith(".db") else glob.glob(os.path.join(p, "**", "*.db"), recursive=True)
+        dbs = [p] if p.endswith((".db", ".csv")) else (
+            glob.glob(os.path.join(p, "**", "*.db"), recursive=True) +
+            glob.glob(os.path.join(p, "**", "*counter_collection.csv"), recursive=True))
         for db in sorted(dbs):
             agg = collections.defaultdict(list)
-            for name, dur, cv in rows(db):
+            for name, dur, cv in (csv_rows(db) if db.endswith(".csv") else rows(db)):
                 if a.match in name:
                     agg[name].append((dur, cv))
             for name, lst in sorted(agg.items(), key=lambda x: -sum(d for d, _ in x[1])):

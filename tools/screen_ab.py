@@ -85,17 +85,17 @@ def main():
             check(lib.wvg_profile_stop(ctx.handle, ctypes.byref(ms), ctypes.byref(nl)))
             kern = ms.value / max(1, nl.value)
             lib.wvgx_screen_counters(ctr, 1)
-            cnt = [int(x) // a.reps for x in ctr[:3]]
+            cnt = [int(x) // a.reps for x in ctr[:4]]
             got = oi.cpu().numpy().copy()
             same = None
-            if dg == 0:
+            if (dg & (1 | 2 | 4 | 8 | 32 | 64 | 128)) == 0:  # variants whose results are search results
                 if ref is None:
                     ref = got
                 same = bool(np.array_equal(got, ref))
             print(json.dumps({"pilot": pl, "search_ms": round(wall, 3), "variant": vr, "split": sp, "range_blocks": rb, "diag": dg, "scoring_kernel_ms": round(kern, 3),
                               "tflops": round(2.0 * nq * n * d / (kern / 1e3) / 1e12, 1),
                               "ids_equal_first": same, "wave_row_blocks": cnt[0], "slow_path_blocks": cnt[1],
-                              "insert_calls": cnt[2]}), flush=True)
+                              "insert_calls": cnt[2], "exact_groups": cnt[3]}), flush=True)
     lib.wvgx_set_tuning(17, 0)
     lib.wvgx_set_tuning(18, 0)
     lib.wvgx_set_tuning(19, 1)

@@ -141,20 +141,27 @@ template <int DS, bool TILED_OUT>
 __global__ void pq_encode_kernel(const float4 *__restrict__ tiled, uint64_t n, uint32_t dim, uint32_t nchunks,
                                  const float *__restrict__ centers, uint32_t m, uint32_t ks, uint32_t ds_rt,
                                  uint8_t *__restrict__ codes, const float *__restrict__ pairs, int nan_free,
-                                 const uint32_t *__restrict__ seg_nan)
+                                 const uint32_t *__restrict__ seg_nan, uint64_t half)
 {
+    // two rows per thread, r and r + half (half: a multiple of 64 >= n / 2): the
+    // centroids a wave reads through its scalar loads serve both rows' packed ops
+    // (the scalar fetches, not the VALU, held round 3's kernel: SQ_INSTS_VALU at
+    // ~50% of the issue slots, 53% of wave cycles waiting; profiles/r04/pmc_enc/)
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
+    const uint64_t rb = r + half;
+    const bool hasb = rb < n;
     const uint32_t ds = DS > 0 ? (uint32_t)DS : ds_rt;
     const float4 *rp = tiled + ((r >> 6) * nchunks) * 64 + (r & 63);
-    // the nearest centroid of segment s (nNearest, CH/kmeans.go:103-135)
-    auto seg_best = [&](uint32_t s) -> uint32_t {
+    const float4 *rpb = hasb ? tiled + ((rb >> 6) * nchunks) * 64 + (rb & 63) : rp;
+    // the nearest centroid of segment s for the row at rpx (nNearest, CH/kmeans.go:103-135)
+    auto seg_best = [&](const float4 *rpx, uint32_t s) -> uint32_t {
             const float *cs = centers + (size_t)s * ks * ds;
             uint32_t best = 0;
             float minD = 3.40282346638528859812e+38f;  // math.MaxFloat32
             if constexpr (DS == 4) {
                 // segment s is exactly chunk s (dim = 4m): one 16-byte load, scalar unfused path (n < 8)
-                const float4 x = rp[(size_t)s * 64];
+                const float4 x = rpx[(size_t)s * 64];
                 const bool row_nan = !(x.x == x.x && x.y == x.y && x.z == x.z && x.w == x.w);
                 if (pairs && (nan_free || (seg_nan && seg_nan[s] == 0u)) && __ballot(row_nan) == 0ull) {  // (see the argmin note above)
                     const f32x2e xx = {x.x, x.x}, xy = {x.y, x.y}, xz = {x.z, x.z}, xw = {x.w, x.w};
@@ -265,7 +272,7 @@ __global__ void pq_encode_kernel(const float4 *__restrict__ tiled, uint64_t n, u
                 }
             } else {
                 const uint32_t base = s * ds;
-                auto xa = [&](int i) { return elem_at<64>(rp, (int)(base + i)); };
+                auto xa = [&](int i) { return elem_at<64>(rpx, (int)(base + i)); };
                 for (uint32_t c = 0; c < ks; c++) {
                     const __attribute__((address_space(4))) float *cv =
                         (const __attribute__((address_space(4))) float *)(cs + (size_t)c * ds);
@@ -279,31 +286,106 @@ __global__ void pq_encode_kernel(const float4 *__restrict__ tiled, uint64_t n, u
             }
             return best;
     };
+    // both rows' codes of segment s: the grouped min3 argmin of the two rows in one pass over the
+    // centroids where it applies (the same ops per row as seg_best), else seg_best per row
+    auto seg_best2 = [&](uint32_t s, uint32_t &ca, uint32_t &cb) {
+        if constexpr (DS == 4) {
+            if (pairs && (ks & (2 * PQ_ENC_GROUP - 1)) == 0 && (nan_free || (seg_nan && seg_nan[s] == 0u))) {
+                const float4 x = rp[(size_t)s * 64], y = rpb[(size_t)s * 64];
+                const bool nan2 = !(x.x == x.x && x.y == x.y && x.z == x.z && x.w == x.w) ||
+                                  !(y.x == y.x && y.y == y.y && y.z == y.z && y.w == y.w);
+                if (__ballot(nan2) == 0ull) {
+                    const f32x2e ax = {x.x, x.x}, ay = {x.y, x.y}, az = {x.z, x.z}, aw = {x.w, x.w};
+                    const f32x2e bx = {y.x, y.x}, by = {y.y, y.y}, bz = {y.z, y.z}, bw = {y.w, y.w};
+                    auto psum = [](const f32x2e c0, const f32x2e c1, const f32x2e c2, const f32x2e c3, f32x2e px,
+                                   f32x2e py, f32x2e pz, f32x2e pw) {
+                        const f32x2e d0 = c0 - px, d1 = c1 - py, d2 = c2 - pz, d3 = c3 - pw;
+                        f32x2e sum = d0 * d0;
+                        sum = sum + d1 * d1;
+                        sum = sum + d2 * d2;
+                        sum = sum + d3 * d3;
+                        return sum;
+                    };
+                    const __attribute__((address_space(4))) float *cp =
+                        (const __attribute__((address_space(4))) float *)(pairs + (size_t)s * ks * 4);
+                    float mna = 3.40282346638528859812e+38f, mnb = mna;
+                    uint32_t bga = 0, bgb = 0;
+                    for (uint32_t g = 0; g < ks / (2 * PQ_ENC_GROUP); g++) {
+                        float gma = 0.0f, gmb = 0.0f;
+#pragma unroll
+                        for (int j = 0; j < PQ_ENC_GROUP; j++) {
+                            const __attribute__((address_space(4))) float *pp = cp + ((size_t)g * PQ_ENC_GROUP + j) * 8;
+                            const f32x2e c0 = {pp[0], pp[1]}, c1 = {pp[2], pp[3]}, c2 = {pp[4], pp[5]}, c3 = {pp[6], pp[7]};
+                            const f32x2e sa = psum(c0, c1, c2, c3, ax, ay, az, aw);
+                            const f32x2e sb = psum(c0, c1, c2, c3, bx, by, bz, bw);
+                            gma = j == 0 ? __builtin_fminf(sa.x, sa.y) : __builtin_fminf(__builtin_fminf(gma, sa.x), sa.y);
+                            gmb = j == 0 ? __builtin_fminf(sb.x, sb.y) : __builtin_fminf(__builtin_fminf(gmb, sb.x), sb.y);
+                        }
+                        const bool missa = gma > mna, missb = gmb > mnb;  // (ties go to the later group)
+                        bga = missa ? bga : g;
+                        mna = missa ? mna : gma;
+                        bgb = missb ? bgb : g;
+                        mnb = missb ? mnb : gmb;
+                    }
+                    ca = 0;  // when nothing reached math.MaxFloat32
+                    cb = 0;
+#pragma unroll 1
+                    for (int j = 0; j < PQ_ENC_GROUP; j++) {  // the winners inside the last groups at the minimum
+                        const uint32_t pa = bga * PQ_ENC_GROUP + j, pb = bgb * PQ_ENC_GROUP + j;
+                        const float *qa = pairs + ((size_t)s * ks + 2 * pa) * 4, *qb = pairs + ((size_t)s * ks + 2 * pb) * 4;
+                        const f32x2e sa = psum(f32x2e{qa[0], qa[1]}, f32x2e{qa[2], qa[3]}, f32x2e{qa[4], qa[5]},
+                                               f32x2e{qa[6], qa[7]}, ax, ay, az, aw);
+                        const f32x2e sb = psum(f32x2e{qb[0], qb[1]}, f32x2e{qb[2], qb[3]}, f32x2e{qb[4], qb[5]},
+                                               f32x2e{qb[6], qb[7]}, bx, by, bz, bw);
+                        if (sa.x == mna) ca = 2 * pa;
+                        if (sa.y == mna) ca = 2 * pa + 1;
+                        if (sb.x == mnb) cb = 2 * pb;
+                        if (sb.y == mnb) cb = 2 * pb + 1;
+                    }
+                    return;
+                }
+            }
+        }
+        ca = seg_best(rp, s);
+        cb = hasb ? seg_best(rpb, s) : 0u;
+    };
     if constexpr (!TILED_OUT) {
         const uint32_t s0 = (uint32_t)((uint64_t)m * blockIdx.y / gridDim.y);
         const uint32_t s1 = (uint32_t)((uint64_t)m * (blockIdx.y + 1) / gridDim.y);
-        for (uint32_t s = s0; s < s1; s++) codes[r * m + s] = (uint8_t)seg_best(s);
+        for (uint32_t s = s0; s < s1; s++) {
+            uint32_t ca, cb;
+            seg_best2(s, ca, cb);
+            codes[r * m + s] = (uint8_t)ca;
+            if (hasb) codes[rb * m + s] = (uint8_t)cb;
+        }
         return;
     }
     const uint32_t out_chunks = pq_chunks(m);
     uint32_t w8[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};  // TILED_OUT, m = 32: all codes, rotated before the store
+    uint32_t w8b[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};  // (the second row's)
     for (uint32_t oc = 0; oc < out_chunks; oc++) {
-        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        uint32_t w[4] = {0u, 0u, 0u, 0u}, wb[4] = {0u, 0u, 0u, 0u};
         for (uint32_t bsel = 0; bsel < 16; bsel++) {
             const uint32_t s = oc * 16 + bsel;
             if (s >= m) break;
-            w[bsel >> 2] |= seg_best(s) << (8 * (bsel & 3));
+            uint32_t ca, cb;
+            seg_best2(s, ca, cb);
+            w[bsel >> 2] |= ca << (8 * (bsel & 3));
+            wb[bsel >> 2] |= cb << (8 * (bsel & 3));
         }
         if constexpr (TILED_OUT) {
             if (pq_rotated(m)) {
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
-                    if (oc == 0) w8[i] = w[i];
-                    else w8[4 + i] = w[i];
+                    if (oc == 0) w8[i] = w[i], w8b[i] = wb[i];
+                    else w8[4 + i] = w[i], w8b[4 + i] = wb[i];
                 }
             } else {
                 reinterpret_cast<uint4 *>(codes)[((r >> 6) * out_chunks + oc) * 64 + (r & 63)] =
                     make_uint4(w[0], w[1], w[2], w[3]);
+                if (hasb)
+                    reinterpret_cast<uint4 *>(codes)[((rb >> 6) * out_chunks + oc) * 64 + (rb & 63)] =
+                        make_uint4(wb[0], wb[1], wb[2], wb[3]);
             }
         }
     }
@@ -314,6 +396,12 @@ __global__ void pq_encode_kernel(const float4 *__restrict__ tiled, uint64_t n, u
             uint4 *o = reinterpret_cast<uint4 *>(codes) + ((r >> 6) * 2) * 64 + (r & 63);
             o[0] = make_uint4(st[0], st[1], st[2], st[3]);
             o[64] = make_uint4(st[4], st[5], st[6], st[7]);
+            if (hasb) {
+                pq32_window(w8b, (uint32_t)(rb & 31), st);
+                uint4 *ob = reinterpret_cast<uint4 *>(codes) + ((rb >> 6) * 2) * 64 + (rb & 63);
+                ob[0] = make_uint4(st[0], st[1], st[2], st[3]);
+                ob[64] = make_uint4(st[4], st[5], st[6], st[7]);
+            }
         }
     }
 }
@@ -324,7 +412,8 @@ hipError_t launch_pq_encode(const float *tiled, uint64_t n, uint32_t dim, const 
 {
     if (n == 0) return hipSuccess;
     const uint32_t ds = dim / m, nchunks = f32_chunks(dim);
-    const unsigned blocks = (unsigned)((n + 255) / 256);
+    const uint64_t half = (n + 127) / 128 * 64;  // two rows per thread: r and r + half
+    const unsigned blocks = (unsigned)((half + 255) / 256);
     // row-major output: segment groups until ~16k workgroups (64k waves) are in flight
     const unsigned groups = tiled_out ? 1u : std::max(1u, std::min<unsigned>(m, 16384u / blocks));
     dim3 grid(blocks, groups), block(256);
@@ -336,17 +425,17 @@ hipError_t launch_pq_encode(const float *tiled, uint64_t n, uint32_t dim, const 
     if (ds == 4 && dim == 4 * m) {
         if (tiled_out)
             hipLaunchKernelGGL((pq_encode_kernel<4, true>), grid, block, 0, s, t4, n, dim, nchunks, centers, m, ks, ds,
-                               codes, pairs, (int)nan_free, seg_nan);
+                               codes, pairs, (int)nan_free, seg_nan, half);
         else
             hipLaunchKernelGGL((pq_encode_kernel<4, false>), grid, block, 0, s, t4, n, dim, nchunks, centers, m, ks, ds,
-                               codes, pairs, (int)nan_free, seg_nan);
+                               codes, pairs, (int)nan_free, seg_nan, half);
     } else {
         if (tiled_out)
             hipLaunchKernelGGL((pq_encode_kernel<0, true>), grid, block, 0, s, t4, n, dim, nchunks, centers, m, ks, ds,
-                               codes, nullptr, 0, nullptr);
+                               codes, nullptr, 0, nullptr, half);
         else
             hipLaunchKernelGGL((pq_encode_kernel<0, false>), grid, block, 0, s, t4, n, dim, nchunks, centers, m, ks, ds,
-                               codes, nullptr, 0, nullptr);
+                               codes, nullptr, 0, nullptr, half);
     }
     return hipGetLastError();
 }

@@ -777,8 +777,8 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
     float *ck1 = sig + SD_WAVES * 32;
     float *ck2 = ck1 + SD_BQ;
     float *cem = ck2 + SD_BQ;
-    uint32_t n_blk = 0, n_slow = 0, n_call = 0;  // (DIAG & 16)
-    (void)n_blk, (void)n_slow, (void)n_call;
+    uint32_t n_blk = 0, n_slow = 0, n_call = 0, n_grp = 0;  // (DIAG & 16)
+    (void)n_blk, (void)n_slow, (void)n_call, (void)n_grp;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int K = (int)a.k, M = SCREEN_M;
@@ -1063,7 +1063,11 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
                 // raw score of the lane's rows + that E against WS is a superset test of
                 // every element (monotone roundings); finite on the fast-eligible inputs
                 // (query K1 <= 2^50, row norms <= 2^60), else the exact test runs
+                // TIGHT (tools A/B, DIAG 2048): the check on each element's own u (its row's E),
+                // i.e. exactly the exact test's verdict per group, at 32 more VALU per group
+                constexpr bool TIGHT = (DIAG & 2048) != 0;
                 float nmax, nsum;  // (nsum: NaN when a norm is -- fmaxf would drop it)
+                float nrmt[TIGHT ? 16 : 1];
                 {
                     float n0[8], n1[8];
                     read_norms8(0, n0);
@@ -1074,6 +1078,10 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
                     for (int j2 = 1; j2 < 8; j2++) nmax = __builtin_fmaxf(nmax, n0[j2]), nsum += n0[j2];
 #pragma unroll
                     for (int j2 = 0; j2 < 8; j2++) nmax = __builtin_fmaxf(nmax, n1[j2]), nsum += n1[j2];
+                    if constexpr (TIGHT) {
+#pragma unroll
+                        for (int j2 = 0; j2 < 8; j2++) nrmt[j2] = n0[j2], nrmt[8 + j2] = n1[j2];
+                    }
                 }
                 // per (query half mq, query r of the lane's four): whether some lane cannot rule
                 // out its 16 elements -- only those groups run the exact test (a wave-uniform
@@ -1086,10 +1094,19 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
                     read_consts(mq, k1r, k2r, svr);
 #pragma unroll
                     for (int r = 0; r < 4; r++) {
-                        float m = agpr_read(acc[mq][0][r]);
+                        float t;
+                        if constexpr (TIGHT) {
+                            float m = -__builtin_inff();
 #pragma unroll
-                        for (int nr = 1; nr < 16; nr++) m = __builtin_fmaxf(m, agpr_read(acc[mq][nr][r]));
-                        const float t = (m + __builtin_fmaf(nmax, k1r[r], k2r[r])) - svr[r];
+                            for (int nr = 0; nr < 16; nr++)
+                                m = __builtin_fmaxf(m, agpr_read(acc[mq][nr][r]) + __builtin_fmaf(nrmt[nr], k1r[r], k2r[r]));
+                            t = m - svr[r];
+                        } else {
+                            float m = agpr_read(acc[mq][0][r]);
+#pragma unroll
+                            for (int nr = 1; nr < 16; nr++) m = __builtin_fmaxf(m, agpr_read(acc[mq][nr][r]));
+                            t = (m + __builtin_fmaf(nmax, k1r[r], k2r[r])) - svr[r];
+                        }
                         if (__ballot(force || t >= 0.f)) wact |= 1u << (4 * mq + r);
                     }
                 }
@@ -1138,6 +1155,7 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
                     read_norms8(1, *reinterpret_cast<float(*)[8]>(&nrm16[8]));
                     for (uint32_t gw = wact; gw; gw &= gw - 1) {
                         const int gi = __builtin_ctz(gw);
+                        if constexpr ((DIAG & 16) != 0) n_grp++;
                         float uv[16];
                         switch (gi) {
 #define WVG_SD_GROUP(G)                                                                        \
@@ -1234,6 +1252,7 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
             atomicAdd(&g_screen_ctr[0], (unsigned long long)n_blk);
             atomicAdd(&g_screen_ctr[1], (unsigned long long)n_slow);
             atomicAdd(&g_screen_ctr[2], (unsigned long long)n_call);
+            atomicAdd(&g_screen_ctr[3], (unsigned long long)n_grp);
         }
     }
 #endif
@@ -1498,6 +1517,8 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
         case 256: kern = &screen_ar_kernel<24, 256>; break;  // round 3's norms / words with every unit
         case 266: kern = &screen_ar_kernel<24, 266>; break;  // 10 with round 3's per-unit norms / words
         case 1024: kern = &screen_ar_kernel<24, 1024>; break;  // one barrier per two K blocks
+        case 2048: kern = &screen_ar_kernel<24, 2048>; break;  // the per-element (tight) fast check
+        case 2064: kern = &screen_ar_kernel<24, 2064>; break;  // 2048 with the counters (16)
         case 1034: kern = &screen_ar_kernel<24, 1034>; break;  // 10 with one barrier per two K blocks
         default: break;
         }
