@@ -22,7 +22,7 @@ sys.path.insert(0, ROOT)
 
 def screen_offsets(n, nq, k, d, num_cus=256):
     """(candidate-array byte offset, candidates per query, flagged-count byte
-    offset) in a K3c / K3d workspace (screen_ws in wvg_capi.hip, after the
+    offset) in a K3c / K3d workspace (screen_ws in wvg_search.hip, after the
     256-byte status block); mirrors screen_row_ranges."""
     nqb = (nq + 127) // 128
     nblk = ((n + 63) // 64 + 3) // 4
@@ -35,7 +35,7 @@ def screen_offsets(n, nq, k, d, num_cus=256):
 
 def screen_nflag_offset(n, nq, k, d, num_cus=256):
     """Byte offset of the flagged-query count in a K3c workspace (screen_ws in
-    wvg_capi.hip, after the 256-byte status block); mirrors screen_row_ranges."""
+    wvg_search.hip, after the 256-byte status block); mirrors screen_row_ranges."""
     nqb = (nq + 127) // 128
     nblk = ((n + 63) // 64 + 3) // 4
     want = max((num_cus + nqb - 1) // nqb, (nblk + 127) // 128)
