@@ -119,3 +119,55 @@ def test_coalesced_results_match_oracle(ctx, orc):
         assert np.array_equal(got[qi][0], wi)
         assert np.array_equal(got[qi][1].view(np.uint32), wd.view(np.uint32))
     c.destroy()
+
+
+def test_coalesced_calls_with_concurrent_writes(ctx, orc):
+    """Single-query searches keep coalescing while another thread upserts and
+    deletes (writers take the corpus exclusively; queued searches wait, none
+    deadlocks); afterwards the corpus answers exactly as the oracle on its
+    final rows."""
+    n, d, k = 6000, 64, 10
+    rows = orc.synth_rows(706, 0, n, d, 0)
+    c = Corpus(ctx, KIND_F32, METRIC_L2, d, n)
+    c.upsert(np.arange(n, dtype=np.uint64), rows)
+    lib = _lib.load()
+    qs = np.ascontiguousarray(orc.synth_rows(707, 0, 48, d, 0))
+    stop = threading.Event()
+    errs = []
+
+    def writer():
+        try:
+            for i in range(20):
+                ids = np.arange(i * 50, i * 50 + 50, dtype=np.uint64)
+                c.upsert(ids, rows[ids.astype(np.int64)] * np.float32(1.0))
+                c.delete(ids[::7])
+            stop.set()
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+            stop.set()
+
+    def reader(t):
+        try:
+            while not stop.is_set():
+                ids, dd, cnt = one_search(lib, c, qs[t], k)
+                assert cnt == k
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = [threading.Thread(target=reader, args=(t,)) for t in range(12)] + [threading.Thread(target=writer)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in th), "a thread did not finish"
+    assert not errs, errs
+    valid = np.ones(n, bool)
+    for i in range(20):
+        valid[np.arange(i * 50, i * 50 + 50)[::7]] = False
+    live = np.flatnonzero(valid).astype(np.uint64)
+    for qi in (0, 47):
+        gi, gd, gc = one_search(lib, c, qs[qi], k)
+        wi, wd = orc.lex_topk(orc.dist_all(0, qs[qi], rows[live.astype(np.int64)]), live, k)
+        assert np.array_equal(gi, wi)
+        assert np.array_equal(gd.view(np.uint32), wd.view(np.uint32))
+    c.destroy()

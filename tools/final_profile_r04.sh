@@ -24,7 +24,8 @@ step 300 bench python3 bench.py
 grep '^{' $O/bench.log | tail -1 > $O/bench.json
 step 420 trace rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 bench.py
 grep '^{"metric"' $O/trace.log | tail -1 > $O/trace_bench.json
-python3 tools/trace_launch_avg.py "$(find $O/trace -name '*kernel_trace.csv' | head -1)" $O/trace_bench.json > $O/trace_vs_events.json
+python3 tools/trace_launch_avg.py "$(find $O/trace -name '*kernel_trace.csv' | head -1)" $O/trace_bench.json \
+  --keep $O/trace_headline_dispatches.csv > $O/trace_vs_events.json
 cat $O/trace_vs_events.json
 step 200 pmc_fetch rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc_fetch -o run -- python3 bench.py --steps 10 --warmup 2 --profile-run --configs "" --no-cpu-baseline
 python3 tools/pmc_summary.py $O/pmc_fetch --match scan_f32_stream > $O/pmc_fetch_summary.txt
