@@ -200,7 +200,7 @@ void prepare_queries_host(const wvg_corpus *c, const float *queries, uint32_t nq
 // qhost: the prepared host query of a single in-launch search (d_q null), passed in the kernel arguments
 int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t nq, uint32_t k, const uint64_t *d_allow,
                const SearchPlan &p, uint64_t *partials, uint64_t *ids, float *dists, uint32_t *counts, hipStream_t s,
-               StreamSlot *sl = nullptr, const float *qhost = nullptr);
+               StreamSlot *sl = nullptr, const float *qhost = nullptr, bool host_poll = false);
 void write_empty(uint32_t nq, uint32_t k, uint64_t *ids, float *dists, uint32_t *counts);
 int stage_queries(wvg_corpus *c, StreamSlot *sl, const float *queries, uint32_t nq, char *dst, uint32_t &qpitch,
                   float *d_lut_or_null, char *d_qtmp, Staging *st = nullptr);

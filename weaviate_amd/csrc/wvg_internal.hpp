@@ -279,6 +279,7 @@ struct StreamJob {
     uint64_t *ids;
     float *dists;
     uint32_t *counts;
+    uint32_t host_poll;  // counts live in host memory and the host polls them (see merge_lists_body)
     // a single host query rides in the kernel arguments (ScanArgs::queries null):
     // no host-to-device copy (a blit dispatch + ~10 us of API time) per call
     alignas(16) float qin[STREAM_QIN_FLOATS];

@@ -69,7 +69,8 @@ __device__ __forceinline__ void wave_range(const ScanArgs &a, int waves_per_grou
 // `nlists` ascending lists transposed, then tree-merge in LDS; wave 0 writes.
 template <int E, int WAVES>
 __device__ __forceinline__ void merge_lists_body(const uint64_t *src, uint32_t nlists, uint32_t list_len, uint32_t k,
-                                                 uint64_t id_base, uint64_t *ids, float *dists, uint32_t *count)
+                                                 uint64_t id_base, uint64_t *ids, float *dists, uint32_t *count,
+                                                 bool sys_release = false)
 {
     __shared__ uint64_t msh[WAVES][64 * E];
     const int lane = threadIdx.x & 63, wave = wave_id();
@@ -112,6 +113,9 @@ __device__ __forceinline__ void merge_lists_body(const uint64_t *src, uint32_t n
             dists[i] = live ? wvg_unord_f32((uint32_t)(key >> 32)) : __builtin_inff();
         }
     }
+    // sys_release: the host polls *count (in host memory) instead of synchronizing the
+    // stream, so the wave's ids / dists stores are ordered before it at system scope
+    if (sys_release) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     if (lane == 0 && count) *count = cnt;
 }
 
@@ -330,7 +334,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_stream_kernel(ScanAr
             }
             merge_lists_body<E, SCAN_WAVES>(j.partials + (size_t)q * G * a.k, G, a.k, a.k, a.id_base,
                                             j.ids + (size_t)q * a.k, j.dists + (size_t)q * a.k,
-                                            j.counts ? j.counts + q : nullptr);
+                                            j.counts ? j.counts + q : nullptr, j.host_poll != 0);
             __syncthreads();  // merge LDS reused by the next query
         }
         return;

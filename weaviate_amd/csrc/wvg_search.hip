@@ -4,6 +4,9 @@
 // (adapters/repos/db/index.go:1644-1648) and DistanceToNode by docID
 // (CH/compression.go:306-325).
 
+#include <atomic>
+#include <chrono>
+
 #include "wvg_host.hpp"
 
 namespace wvg {
@@ -288,7 +291,7 @@ static bool inlaunch_single(const wvg_corpus *c, uint32_t nq, const SearchPlan &
 
 int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t nq, uint32_t k, const uint64_t *d_allow,
                const SearchPlan &p, uint64_t *partials, uint64_t *ids, float *dists, uint32_t *counts, hipStream_t s,
-               StreamSlot *sl, const float *qhost)
+               StreamSlot *sl, const float *qhost, bool host_poll)
 {
     ScanArgs a{};
     a.data = c->d_data;
@@ -348,6 +351,7 @@ int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t nq, uin
         j.ids = ids;
         j.dists = dists;
         j.counts = counts;
+        j.host_poll = host_poll ? 1u : 0u;
         if (!d_q) {  // the query in the kernel arguments
             if (!qhost || qpitch > STREAM_QIN_FLOATS) return fail(WVG_ERR_INVALID, "inline query missing or too long");
             std::memcpy(j.qin, qhost, (size_t)qpitch * 4);
@@ -648,15 +652,33 @@ static int wvg::search_batch(wvg_corpus *c, const float *queries, uint32_t nq, u
         hc = (char *)v;
     }
     char *rspan = zc ? hc : b + o_ids;  // the result span [ids | dists | counts]
+    // zero-copy single query: the host polls the count word (preset to a sentinel) that
+    // the merge writes last, after a system-scope release -- no stream synchronization
+    // on the way back (nothing else of this call is in flight: no copies in this path)
+    volatile uint32_t *cflag = zc ? reinterpret_cast<volatile uint32_t *>(rspan + (o_cnt - o_ids)) : nullptr;
+    if (cflag) *cflag = 0xFFFFFFFFu;
     rc = run_search(c, qin ? nullptr : b + o_q, qpitch, nq, k, d_allow, p, (uint64_t *)(b + o_part), (uint64_t *)rspan,
                     (float *)(rspan + (o_d - o_ids)), (uint32_t *)(rspan + (o_cnt - o_ids)), s, g.slot,
-                    qin ? qinl.data() : nullptr);
+                    qin ? qinl.data() : nullptr, cflag != nullptr);
     if (rc) return rc;
     const char *pin = zc ? hc : out_b <= STAGE_MAX ? st.take(out_b) : nullptr;
     std::vector<char> big(pin ? 0 : out_b);
     if (!pin) pin = big.data();
     if (!zc) WVG_HIP(hipMemcpyAsync((void *)pin, b + o_ids, out_b, hipMemcpyDeviceToHost, s));
-    WVG_HIP(hipStreamSynchronize(s));
+    bool polled = false;
+    if (cflag) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t spin = 0;; spin++) {
+            if (*cflag != 0xFFFFFFFFu) {
+                polled = true;
+                break;
+            }
+            if ((spin & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50))
+                break;  // long scans (or a fault): the stream synchronization below decides
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+    }
+    if (!polled) WVG_HIP(hipStreamSynchronize(s));
     if (out_ids) std::memcpy(out_ids, pin, (size_t)nq * k * 8);
     if (out_dists) std::memcpy(out_dists, pin + (o_d - o_ids), (size_t)nq * k * 4);
     if (out_counts) std::memcpy(out_counts, pin + (o_cnt - o_ids), (size_t)nq * 4);
