@@ -79,12 +79,25 @@ __device__ __forceinline__ void merge_lists_body(const uint64_t *src, uint32_t n
     for (uint32_t g0 = (uint32_t)wave * 64; g0 < nlists; g0 += WAVES * 64) {
         const uint32_t list = g0 + lane;
         const uint64_t *lp = src + (size_t)list * list_len;
-        uint64_t cur = list < nlists ? lp[0] : WVG_KEY_NONE;
-        for (uint32_t r = 0; r < list_len; r++) {
-            const uint64_t nxt = (r + 1 < list_len && list < nlists) ? lp[r + 1] : WVG_KEY_NONE;  // prefetch
-            if (list_len > 1 && r > 0 && __ballot(cur < tk.tau) == 0ull) break;  // sorted lists: done
-            tk.offer(cur);
-            cur = nxt;
+        // four entries per lane in flight at a time (independent loads): a one-query
+        // merge sits on the launch's critical path, where one dependent load per entry
+        // (~1 us each from L2) was most of its time
+        bool done = false;
+        for (uint32_t r0 = 0; r0 < list_len && !done; r0 += 4) {
+            uint64_t c4[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                c4[i] = (r0 + i < list_len && list < nlists) ? lp[r0 + i] : WVG_KEY_NONE;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const uint32_t r = r0 + (uint32_t)i;
+                if (r >= list_len) break;
+                if (list_len > 1 && r > 0 && __ballot(c4[i] < tk.tau) == 0ull) {  // sorted lists: done
+                    done = true;
+                    break;
+                }
+                tk.offer(c4[i]);
+            }
         }
     }
 #pragma unroll
