@@ -326,11 +326,18 @@ struct ScreenLaunch {
     uint64_t *cand;        // [nq][nrr * SCREEN_M]
     uint32_t *flist;       // [nq] flagged queries
     uint32_t *nflag;       // count
+    // exact seeds between phases (optional): the rows and distance the final
+    // rescore uses, and [nq][nrr * SCREEN_M] keys of scratch
+    int metric = 0;
+    const float *data = nullptr;  // tiled fp32 rows
+    uint32_t nchunks = 0;
+    uint64_t *seed_keys = nullptr;
     // pilot (optional): the exact K1 top-k of every query over the range's
     // first tiles seeds the bound before the first phase
     const ScanArgs *pilot = nullptr;
-    uint64_t *pilot_part = nullptr;  // [nq][pilot_groups][k] K1 partials
+    uint64_t *pilot_part = nullptr;  // [nq][pilot_groups][k] K1 partials ([nq][rr][k] K3b partials)
     uint32_t pilot_groups = 1;
+    uint32_t pilot_part_lists = 0;   // pilot_part's capacity in k-lists per query
     uint64_t *pilot_ids = nullptr;   // [nq][k] scratch (the caller's result arrays)
     float *pilot_dists = nullptr;
     uint32_t *pilot_counts = nullptr;
@@ -379,8 +386,13 @@ struct Tuning {
     int pq_encode_min3 = 1;  // PQ encode pair path: min3 argmin on NaN-free codebooks (1) or the
                              // reference's compare-and-select loop everywhere (0; A/B and parity)
     int screen_pilot = 16;   // K3c/K3d: tiles of the exact pilot scan that seeds the bound (0 = none; A/B)
+    int screen_pilot_gemm = 256;  // K3c/K3d: tiles of the K3b (exact fp32 MFMA) pilot, which replaces the K1
+                                  // pilot (0 = the K1 pilot; A/B)
     int screen_variant = 0;  // batched screen kernel: 0 = K3d where it applies (d = 512, 768), 1 = K3c (A/B)
     int screen_split = 1;    // K3c/K3d phases seeded from the earlier ones: 1 = up to three, 2 = two, 0 = one launch (A/B)
+    int screen_seed = 3;     // K3c/K3d exact seeds (the exact k-th of the rescored k smallest lower bounds):
+                             // bit 0 between phases (else the lists' k-th lower bound + 2 Emax), bit 1 before
+                             // the final collect (A/B)
     int screen_range_blocks = 0;  // K3c row-range length in 256-row blocks (0 = auto, ~128; A/B)
     int screen_diag = 0;     // K3c diagnostics (tools build only; results are NOT distances): bit 0 = no
                              // wait for the stage loads, bit 1 = no epilogue, bit 2 = no list insertions, bit 3 = no query-fragment loads (K3c); K3d: 1, 2, 4 or 16 (= counters) select compiled variants

@@ -1282,10 +1282,52 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
 // the exact rescan.  The k-th smallest is a 4-pass radix select (8-bit
 // digits) over the entries' ordered lower bounds in LDS.
 constexpr uint32_t SC_COLLECT_MAX = 8192;  // nrr * SCREEN_M (screen_row_ranges caps nrr at 512)
+constexpr uint32_t SC_SEED_MAX = 64;       // exact-seed rescore entries per query (>= SCREEN_M >= k)
+
+// The k-th smallest (k >= 1) of the ordered values hv[0, n) in LDS, of which
+// at least k are not 0xFFFFFFFF: a 4-pass radix select over 8-bit digits.
+// Block-wide (every thread calls it); every thread gets the value.
+__device__ uint32_t block_kth_ordered(const uint32_t *hv, uint32_t n, uint32_t k, uint32_t *hist, uint32_t &sh_prefix,
+                                      uint32_t &sh_need)
+{
+    if (threadIdx.x == 0) {
+        sh_prefix = 0;
+        sh_need = k;
+    }
+    __syncthreads();
+    for (int shift = 24; shift >= 0; shift -= 8) {
+        for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) hist[i] = 0;
+        __syncthreads();
+        const uint32_t hi_mask = shift == 24 ? 0u : (0xFFFFFFFFu << (shift + 8));
+        const uint32_t pre = sh_prefix;
+        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+            const uint32_t v = hv[i];
+            if (v != 0xFFFFFFFFu && (v & hi_mask) == (pre & hi_mask)) atomicAdd(&hist[(v >> shift) & 255u], 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t need = sh_need, cum = 0, dg = 255;
+            for (uint32_t d = 0; d < 256; d++) {
+                if (cum + hist[d] >= need) {
+                    dg = d;
+                    break;
+                }
+                cum += hist[d];
+            }
+            sh_need = need - cum;
+            sh_prefix = pre | (dg << shift);
+        }
+        __syncthreads();
+    }
+    return sh_prefix;
+}
 
 // seed (cand == nullptr): the same tau* over the lists of the first nrr_use
 // ranges only, folded into gbound (atomicMin) -- the bound the later ranges
-// of a split screen start from.
+// of a split screen start from.  Exact seed (cand != nullptr, flist ==
+// nullptr): that tau* folded into gbound, and the entries with the k
+// smallest lower bounds packed into cand for an exact rescore whose k-th
+// distance is the tighter seed (screen_seed_kth_kernel).
 __global__ __launch_bounds__(256) void screen_collect_kernel(const uint64_t *partials, uint32_t nrr, uint32_t nrr_use,
                                                              uint32_t k, const float *emax, int cosine, uint64_t *cand,
                                                              uint32_t *flist, uint32_t *nflag, uint32_t *gbound)
@@ -1299,8 +1341,6 @@ __global__ __launch_bounds__(256) void screen_collect_kernel(const uint64_t *par
     uint64_t *dst = cand + (size_t)q * n;
     if (threadIdx.x == 0) {
         ovf = 0;
-        sh_prefix = 0;
-        sh_need = k;
         sh_total = 0;
     }
     __syncthreads();
@@ -1313,36 +1353,17 @@ __global__ __launch_bounds__(256) void screen_collect_kernel(const uint64_t *par
     atomicAdd(&sh_total, live);
     __syncthreads();
     float t = __builtin_inff();
+    uint32_t kth = 0xFFFFFFFFu;  // the k-th smallest ordered lower bound
     if (sh_total >= k) {
-        for (int shift = 24; shift >= 0; shift -= 8) {
-            for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) hist[i] = 0;
-            __syncthreads();
-            const uint32_t hi_mask = shift == 24 ? 0u : (0xFFFFFFFFu << (shift + 8));
-            const uint32_t pre = sh_prefix;
-            for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-                const uint32_t v = hv[i];
-                if (v != 0xFFFFFFFFu && (v & hi_mask) == (pre & hi_mask)) atomicAdd(&hist[(v >> shift) & 255u], 1u);
-            }
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                uint32_t need = sh_need, cum = 0, dg = 255;
-                for (uint32_t d = 0; d < 256; d++) {
-                    if (cum + hist[d] >= need) {
-                        dg = d;
-                        break;
-                    }
-                    cum += hist[d];
-                }
-                sh_need = need - cum;
-                sh_prefix = pre | (dg << shift);
-            }
-            __syncthreads();
-        }
-        t = sc_tau_k(wvg_unord_f32(sh_prefix), emax[q], cosine);
+        kth = block_kth_ordered(hv, n, k, hist, sh_prefix, sh_need);
+        t = sc_tau_k(wvg_unord_f32(kth), emax[q], cosine);
     }
-    if (!cand) {
+    // the candidates: gbound may hold a tighter valid bound than tau* (an exact seed)
+    const uint32_t gb = gbound[q];
+    if (cand && flist && gb != 0xFFFFFFFFu) t = fminf(t, wvg_unord_f32(gb));
+    if (!cand || !flist) {
         if (threadIdx.x == 0 && t < __builtin_inff()) atomicMin(gbound + q, wvg_ord_f32(t));
-        return;
+        if (!cand) return;
     }
     __syncthreads();
     if (threadIdx.x == 0) sh_total = 0;
@@ -1354,7 +1375,9 @@ __global__ __launch_bounds__(256) void screen_collect_kernel(const uint64_t *par
     for (uint32_t i0 = 0; i0 < n; i0 += blockDim.x) {
         const uint32_t i = i0 + threadIdx.x;
         const uint64_t e = i < n ? src[i] : WVG_KEY_NONE;
-        const bool keep = e != WVG_KEY_NONE && key_lower(e) <= t;
+        // exact seed: the k smallest lower bounds only (ties: all of them) -- any k
+        // rows bound the k-th, and these k are the likeliest to be the closest
+        const bool keep = e != WVG_KEY_NONE && (flist ? key_lower(e) <= t : (uint32_t)(e >> 32) <= kth);
         if (keep && (i % SCREEN_M) == SCREEN_M - 1) ovf = 1;  // full list, last entry within tau*
         const uint64_t bal = __ballot(keep);
         uint32_t base = 0;
@@ -1364,7 +1387,36 @@ __global__ __launch_bounds__(256) void screen_collect_kernel(const uint64_t *par
     }
     __syncthreads();
     for (uint32_t i = sh_total + threadIdx.x; i < n; i += blockDim.x) dst[i] = WVG_KEY_NONE;
-    if (threadIdx.x == 0 && ovf) flist[atomicAdd(nflag, 1u)] = q;
+    if (threadIdx.x == 0 && ovf && flist) flist[atomicAdd(nflag, 1u)] = q;
+}
+
+// Exact seed: the k-th smallest of a query's exactly rescored seed candidates
+// (keys: ordered distance << 32 | slot; n per query) -- k real rows at or
+// below it, so it bounds the final k-th like the pilot's -- into gbound.
+// Against the list seed (k-th lower bound + 2 Emax) it drops the bound's
+// error term, about one Emax: fewer rows of the later phases reach the
+// per-element test and the list insertions.
+__global__ __launch_bounds__(256) void screen_seed_kth_kernel(const uint64_t *keys, uint32_t n, uint32_t k,
+                                                              uint32_t *gbound)
+{
+    __shared__ uint32_t hv[SC_COLLECT_MAX];
+    __shared__ uint32_t hist[256];
+    __shared__ uint32_t sh_prefix, sh_need, sh_total;
+    const uint32_t q = blockIdx.x;
+    const uint64_t *src = keys + (size_t)q * n;
+    if (threadIdx.x == 0) sh_total = 0;
+    __syncthreads();
+    uint32_t live = 0;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint64_t e = src[i];
+        hv[i] = (uint32_t)(e >> 32);
+        live += e != WVG_KEY_NONE;
+    }
+    atomicAdd(&sh_total, live);
+    __syncthreads();
+    if (sh_total < k) return;
+    const uint32_t v = block_kth_ordered(hv, n, k, hist, sh_prefix, sh_need);
+    if (threadIdx.x == 0 && wvg_unord_f32(v) < __builtin_inff()) atomicMin(gbound + q, v);
 }
 
 __global__ __launch_bounds__(256) void screen_pilot_list_kernel(uint32_t *flist, uint32_t nq, uint32_t *nflag)
@@ -1438,11 +1490,38 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
     hipLaunchKernelGGL(screen_qconst_kernel, dim3(nq_pad / 4), dim3(256), 0, s, L.queries, L.nq, L.qpitch, L.dim,
                        nq_pad, L.cosine, L.nmax, L.k1, L.k2, L.emax);
     if ((e = hipMemsetAsync(L.gbound, 0xFF, (size_t)L.nq * 4, s)) != hipSuccess) return e;
-    uint64_t pilot_tiles = 16;
+    // profiling: one event pair spans every phase and the seeds between them (taken
+    // before the pilot, whose K3b launch would otherwise bind them)
+    const LaunchEvents ev = armed_events();
+    armed_events() = LaunchEvents{};
+    uint64_t pilot_tiles = 16, pilot_gemm_tiles = 0;
 #ifdef WVG_TOOLS
     pilot_tiles = (uint64_t)std::max(tuning().screen_pilot, 0);
+    pilot_gemm_tiles = (uint64_t)std::max(tuning().screen_pilot_gemm, 0);
 #endif
-    if (L.pilot && pilot_tiles > 0) {
+    uint32_t pilot_rr = 0;  // K3b pilot: its row ranges (0: the K1 pilot)
+    if (L.pilot && pilot_gemm_tiles > 0) {
+        const uint64_t nt = std::min<uint64_t>(L.pilot->tile_end - L.pilot->tile_begin, pilot_gemm_tiles);
+        pilot_rr = nt ? gemm_row_ranges(L.nq, nt, L.num_cus, L.dim, L.k) : 0;
+        if (pilot_rr > L.pilot_part_lists) pilot_rr = 0;
+    }
+    if (pilot_rr > 0) {
+        // Pilot (K3b): the exact top-k of every query over the first pilot_gemm_tiles
+        // tiles (16k rows), exact fp32 MFMA -- per row ~16x cheaper than K1's
+        // per-query scans, so 16x the rows of the K1 pilot at about its cost; its
+        // k-th distance bounds the final k-th and seeds gbound before the first phase
+        ScanArgs f = *L.pilot;
+        f.cosched = 0;
+        f.reverse = 0;
+        f.tile_end = std::min<uint64_t>(f.tile_end, f.tile_begin + pilot_gemm_tiles);
+        if ((e = launch_gemm_topk(f, pilot_rr, L.pilot_part, nullptr, nullptr, L.num_cus, s)) != hipSuccess) return e;
+        if ((e = launch_merge_lists(L.pilot_part, L.nq, pilot_rr, L.k, L.k, 0, L.pilot_ids, L.pilot_dists,
+                                    L.pilot_counts, s)) != hipSuccess)
+            return e;
+        hipLaunchKernelGGL(screen_pilot_seed_kernel, dim3((L.nq + 255) / 256), dim3(256), 0, s, L.pilot_dists,
+                           L.pilot_counts, L.nq, L.k, L.gbound);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    } else if (L.pilot && pilot_tiles > 0) {
         // Pilot: every query's exact top-k (K1, AVX2-order distances) over the
         // range's first 16 tiles (1024 rows); its k-th distance bounds the final k-th
         // (k real rows lie at or below it), so it seeds gbound before the
@@ -1551,9 +1630,26 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
     if (tuning().screen_split == 2 && nph > 2) nph = 2;
 #endif
     bounds[nph] = L.nrr;
-    // profiling: one event pair spans every phase and the seeds between them
-    const LaunchEvents ev = armed_events();
-    armed_events() = LaunchEvents{};
+    // seeds between phases: the exact k-th over the earlier ranges' candidates
+    // (rescored with the final rescore's distances) where the rows are at hand
+    bool seed_exact = L.data != nullptr && L.seed_keys != nullptr, seed_final = seed_exact;
+#ifdef WVG_TOOLS
+    seed_exact = seed_exact && (tuning().screen_seed & 1) != 0;
+    seed_final = seed_final && (tuning().screen_seed & 2) != 0;
+#endif
+    // an exact seed over the lists of ranges [0, nuse / SCREEN_M)
+    auto exact_seed = [&](uint32_t nr_use) -> hipError_t {
+        const uint32_t nuse = nr_use * SCREEN_M, nres = std::min<uint32_t>(nuse, SC_SEED_MAX);
+        hipLaunchKernelGGL(screen_collect_kernel, dim3(L.nq), dim3(256), 0, s, L.partials, L.nrr, nr_use, L.k, L.emax,
+                           L.cosine, L.cand, (uint32_t *)nullptr, (uint32_t *)nullptr, L.gbound);
+        hipError_t e2;
+        if ((e2 = hipGetLastError()) != hipSuccess) return e2;
+        if ((e2 = launch_rescore_keys(L.metric, L.queries, L.qpitch, L.data, L.dim, L.nchunks, L.cand, L.nq, nres,
+                                      nuse, L.seed_keys, s, 0)) != hipSuccess)
+            return e2;
+        hipLaunchKernelGGL(screen_seed_kth_kernel, dim3(L.nq), dim3(256), 0, s, L.seed_keys, nres, L.k, L.gbound);
+        return hipGetLastError();
+    };
     for (uint32_t ph = 0; ph < nph; ph++) {
         a.rr0 = bounds[ph];
         a.nrr_l = bounds[ph + 1] - bounds[ph];
@@ -1564,12 +1660,21 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
             hipLaunchKernelGGL(kern, dim3(nqb * a.nrr_l), dim3(threads), lds, s, a);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (ph + 1 < nph) {
-            hipLaunchKernelGGL(screen_collect_kernel, dim3(L.nq), dim3(256), 0, s, L.partials, L.nrr, bounds[ph + 1],
-                               L.k, L.emax, L.cosine, (uint64_t *)nullptr, L.flist, L.nflag, L.gbound);
+            if (seed_exact) {
+                if ((e = exact_seed(bounds[ph + 1])) != hipSuccess) return e;
+            } else {
+                hipLaunchKernelGGL(screen_collect_kernel, dim3(L.nq), dim3(256), 0, s, L.partials, L.nrr,
+                                   bounds[ph + 1], L.k, L.emax, L.cosine, (uint64_t *)nullptr, L.flist, L.nflag,
+                                   L.gbound);
+            }
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    // the final candidates: lower <= min(tau*, gbound); with the exact seed over every
+    // range, gbound ~ the k-th exact distance, about one Emax below tau* -- a third of
+    // the rows to rescore on 10M x 768 cosine
+    if (seed_final && (e = exact_seed(L.nrr)) != hipSuccess) return e;
     hipLaunchKernelGGL(screen_collect_kernel, dim3(L.nq), dim3(256), 0, s, L.partials, L.nrr, L.nrr, L.k, L.emax,
                        L.cosine, L.cand, L.flist, L.nflag, L.gbound);
     return hipGetLastError();

@@ -263,11 +263,16 @@ static int run_screen(wvg_corpus *c, const ScanArgs &a, const SearchPlan &p, cha
     L.pilot = &a;                             // exact K1 over the first tiles (the fallback's partials are
     L.pilot_part = (uint64_t *)(ws + w.fbp);  // free until the rescan)
     L.pilot_groups = std::max<uint32_t>(1, std::min<uint32_t>(p.fb_groups, 4));
+    L.pilot_part_lists = p.fb_groups;
     L.pilot_ids = (uint64_t *)(ws + w.pids);
     L.pilot_dists = (float *)(ws + w.pd);
     L.pilot_counts = (uint32_t *)(ws + w.pc);
-    WVG_HIP(launch_screen(L, s));
     uint64_t *keys = (uint64_t *)(ws + w.keys);
+    L.metric = c->metric;
+    L.data = (const float *)c->d_data;
+    L.nchunks = c->nchunks;
+    L.seed_keys = keys;  // free until the final rescore
+    WVG_HIP(launch_screen(L, s));
     WVG_HIP(launch_rescore_keys(c->metric, (const float *)a.queries, a.qpitch, (const float *)c->d_data, c->dim,
                                 c->nchunks, L.cand, nq, ncand, ncand, keys, s, 0));
     WVG_HIP(launch_merge_keys(keys, nq, ncand, k, c->id_base, ids, dists, counts, s));
