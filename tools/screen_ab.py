@@ -31,8 +31,8 @@ def main():
     ap.add_argument("--splits", default="1", help="K3c split launch (tuning key 19)")
     ap.add_argument("--variants", default="0", help="screen kernel (tuning key 20): 0 K3d where it applies, 1 K3c")
     ap.add_argument("--pilots", default="16", help="tiles of the exact pilot scan that seeds the bound (tuning key 21; 0 = none)")
-    ap.add_argument("--gpilots", default="256", help="tiles of the K3b pilot (tuning key 23; 0 = the K1 pilot)")
-    ap.add_argument("--seeds", default="1", help="exact seeds (tuning key 22): bit 0 between phases, bit 1 before the final collect")
+    ap.add_argument("--gpilots", default="512", help="tiles of the K3b pilot (tuning key 23; 0 = the K1 pilot)")
+    ap.add_argument("--seeds", default="3", help="exact seeds (tuning key 22): bit 0 between phases, bit 1 before the final collect")
     a = ap.parse_args()
     import torch
 
@@ -108,7 +108,7 @@ def main():
     lib.wvgx_set_tuning(20, 0)
     lib.wvgx_set_tuning(21, 16)
     lib.wvgx_set_tuning(22, 3)
-    lib.wvgx_set_tuning(23, 256)
+    lib.wvgx_set_tuning(23, 512)
     c.destroy()
     ctx.close()
 

@@ -265,7 +265,7 @@ int wvgx_screen_counters(uint64_t *out4, int reset)
 // 13 = K3b partner priority, 14 = PQ encode min3 argmin, 15 = co-scheduled PQ / BQ batches, 16 = co-scheduled BQ workgroups per CU, 17 = K3c row-range length,
 // 18 = K3c diagnostics (results not distances), 19 = K3c split launch,
 // 20 = screen kernel (0 K3d where it applies, 1 K3c), 21 = screen pilot seed, 22 = exact seeds between
-// screen phases, 23 = K3b pilot tiles.  Returns the previous value.
+// screen phases, 23 = K3b pilot tiles, 24 = single-query host path.  Returns the previous value.
 int wvgx_set_tuning(int key, int value)
 {
     Tuning &t = tuning();
@@ -342,6 +342,9 @@ int wvgx_set_tuning(int key, int value)
     } else if (key == 23) {
         old = t.screen_pilot_gemm;
         t.screen_pilot_gemm = value;
+    } else if (key == 24) {
+        old = t.single_path;
+        t.single_path = value;
     }
     return old;
 }

@@ -386,10 +386,15 @@ struct Tuning {
     int pq_encode_min3 = 1;  // PQ encode pair path: min3 argmin on NaN-free codebooks (1) or the
                              // reference's compare-and-select loop everywhere (0; A/B and parity)
     int screen_pilot = 16;   // K3c/K3d: tiles of the exact pilot scan that seeds the bound (0 = none; A/B)
-    int screen_pilot_gemm = 256;  // K3c/K3d: tiles of the K3b (exact fp32 MFMA) pilot, which replaces the K1
+    int screen_pilot_gemm = 512;  // K3c/K3d: tiles of the K3b (exact fp32 MFMA) pilot, which replaces the K1
                                   // pilot (0 = the K1 pilot; A/B)
     int screen_variant = 0;  // batched screen kernel: 0 = K3d where it applies (d = 512, 768), 1 = K3c (A/B)
-    int screen_split = 1;    // K3c/K3d phases seeded from the earlier ones: 1 = up to three, 2 = two, 0 = one launch (A/B)
+    int single_path = 2;     // single-query host calls: bit 0 = query staged by copy instead of in the kernel
+                             // arguments, bit 1 = stream synchronization instead of polling the count.  2: polling
+                             // the count in coherent host memory returned stale or mixed results in about 1 of 1000
+                             // concurrent calls (tools/single_query_stress.py, profiles/r04/single_query_stress/)
+    int screen_split = 1;    // K3c/K3d phases seeded from the earlier ones: 1 = up to three, 2 = two, 0 = one launch,
+                             // 3 = doubling (r1, 2 r1, 4 r1, ...; A/B)
     int screen_seed = 3;     // K3c/K3d exact seeds (the exact k-th of the rescored k smallest lower bounds):
                              // bit 0 between phases (else the lists' k-th lower bound + 2 Emax), bit 1 before
                              // the final collect (A/B)

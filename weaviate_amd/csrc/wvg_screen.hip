@@ -1494,11 +1494,8 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
     // before the pilot, whose K3b launch would otherwise bind them)
     const LaunchEvents ev = armed_events();
     armed_events() = LaunchEvents{};
-    uint64_t pilot_tiles = 16, pilot_gemm_tiles = 0;
-#ifdef WVG_TOOLS
-    pilot_tiles = (uint64_t)std::max(tuning().screen_pilot, 0);
-    pilot_gemm_tiles = (uint64_t)std::max(tuning().screen_pilot_gemm, 0);
-#endif
+    const uint64_t pilot_tiles = (uint64_t)std::max(tuning().screen_pilot, 0);
+    const uint64_t pilot_gemm_tiles = (uint64_t)std::max(tuning().screen_pilot_gemm, 0);
     uint32_t pilot_rr = 0;  // K3b pilot: its row ranges (0: the K1 pilot)
     if (L.pilot && pilot_gemm_tiles > 0) {
         const uint64_t nt = std::min<uint64_t>(L.pilot->tile_end - L.pilot->tile_begin, pilot_gemm_tiles);
@@ -1616,27 +1613,27 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
     // Without it a range starts from the k-th bound of single finished
     // ranges (rows in the top-k of 1 % of the corpus), and most row blocks
     // took the exact per-element path with list insertions.
-    uint32_t bounds[4] = {0, 0, 0, 0}, nph = 0;
+    uint32_t bounds[12] = {0}, nph = 0;
     bounds[nph++] = 0;
+    const int split = tuning().screen_split;
     if (L.nrr % 8 == 0) {
         const uint32_t r1 = std::max<uint32_t>(8, ((uint32_t)L.num_cus / nqb + 7) / 8 * 8);
         if (r1 <= L.nrr / 4) {
             bounds[nph++] = r1;
-            if (4 * r1 <= L.nrr / 2) bounds[nph++] = 4 * r1;
+            if (split == 3) {  // doubling phases (tools A/B)
+                for (uint32_t b = 2 * r1; b <= L.nrr / 2 && nph < 10; b *= 2) bounds[nph++] = b;
+            } else if (4 * r1 <= L.nrr / 2) {
+                bounds[nph++] = 4 * r1;
+            }
         }
     }
-#ifdef WVG_TOOLS
-    if (tuning().screen_split == 0) nph = 1;
-    if (tuning().screen_split == 2 && nph > 2) nph = 2;
-#endif
+    if (split == 0) nph = 1;
+    if (split == 2 && nph > 2) nph = 2;
     bounds[nph] = L.nrr;
     // seeds between phases: the exact k-th over the earlier ranges' candidates
     // (rescored with the final rescore's distances) where the rows are at hand
-    bool seed_exact = L.data != nullptr && L.seed_keys != nullptr, seed_final = seed_exact;
-#ifdef WVG_TOOLS
-    seed_exact = seed_exact && (tuning().screen_seed & 1) != 0;
-    seed_final = seed_final && (tuning().screen_seed & 2) != 0;
-#endif
+    const bool rows = L.data != nullptr && L.seed_keys != nullptr;
+    const bool seed_exact = rows && (tuning().screen_seed & 1) != 0, seed_final = rows && (tuning().screen_seed & 2) != 0;
     // an exact seed over the lists of ranges [0, nuse / SCREEN_M)
     auto exact_seed = [&](uint32_t nr_use) -> hipError_t {
         const uint32_t nuse = nr_use * SCREEN_M, nres = std::min<uint32_t>(nuse, SC_SEED_MAX);

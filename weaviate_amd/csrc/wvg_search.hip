@@ -633,7 +633,7 @@ static int wvg::search_batch(wvg_corpus *c, const float *queries, uint32_t nq, u
     // a single in-launch F32 query of up to STREAM_QIN_FLOATS floats goes in the kernel arguments
     std::vector<float> qinl;
     const bool qin = inlaunch_single(c, nq, p, p.allow_host != nullptr) &&
-                     (size_t)f32_chunks(c->dim) * 4 <= STREAM_QIN_FLOATS;
+                     (size_t)f32_chunks(c->dim) * 4 <= STREAM_QIN_FLOATS && (tuning().single_path & 1) == 0;
     if (qin) {
         std::vector<uint64_t> qb;
         prepare_queries_host(c, queries, nq, qinl, qb, qpitch);
@@ -657,10 +657,13 @@ static int wvg::search_batch(wvg_corpus *c, const float *queries, uint32_t nq, u
         hc = (char *)v;
     }
     char *rspan = zc ? hc : b + o_ids;  // the result span [ids | dists | counts]
-    // zero-copy single query: the host polls the count word (preset to a sentinel) that
-    // the merge writes last, after a system-scope release -- no stream synchronization
-    // on the way back (nothing else of this call is in flight: no copies in this path)
-    volatile uint32_t *cflag = zc ? reinterpret_cast<volatile uint32_t *>(rspan + (o_cnt - o_ids)) : nullptr;
+    // zero-copy single query, polled (tools A/B only, single_path bit 1 clear): the host polls
+    // the count word (preset to a sentinel) that the merge writes last, after a system-scope
+    // release.  Under concurrent calls about 1 in 1000 polled results was stale or mixed
+    // (tools/single_query_stress.py), so the product synchronizes the stream instead.
+    volatile uint32_t *cflag = zc && (tuning().single_path & 2) == 0
+                                   ? reinterpret_cast<volatile uint32_t *>(rspan + (o_cnt - o_ids))
+                                   : nullptr;
     if (cflag) *cflag = 0xFFFFFFFFu;
     rc = run_search(c, qin ? nullptr : b + o_q, qpitch, nq, k, d_allow, p, (uint64_t *)(b + o_part), (uint64_t *)rspan,
                     (float *)(rspan + (o_d - o_ids)), (uint32_t *)(rspan + (o_cnt - o_ids)), s, g.slot,
