@@ -28,6 +28,38 @@ static void normalize_host(const float *v, uint32_t n, float *out)
     for (uint32_t i = 0; i < n; i++) out[i] = v[i] / norm;
 }
 
+// normalize_host over nq rows (out pitch `pitch`), eight rows at a time: each
+// row's sum of squares is still its own sequential chain, but eight chains run
+// side by side (one chain of d dependent adds per query bounded a 1024 x 768
+// batch's host preparation at ~0.5 ms).
+static void normalize_host_rows(const float *v, uint32_t nq, uint32_t d, float *out, uint32_t pitch)
+{
+    constexpr uint32_t B = 8;
+    uint32_t i = 0;
+    for (; i + B <= nq; i += B) {
+        const float *r = v + (size_t)i * d;
+        float norm[B];
+        for (uint32_t j = 0; j < B; j++) norm[j] = 0.0f;
+        for (uint32_t e = 0; e < d; e++)
+            for (uint32_t j = 0; j < B; j++) {
+                const float x = r[(size_t)j * d + e];
+                const float p = x * x;
+                norm[j] = norm[j] + p;
+            }
+        for (uint32_t j = 0; j < B; j++) {
+            const float *src = r + (size_t)j * d;
+            float *dst = out + (size_t)(i + j) * pitch;
+            if (norm[j] == 0.0f) {
+                for (uint32_t e = 0; e < d; e++) dst[e] = 0.0f;
+                continue;
+            }
+            const float n = (float)std::sqrt((double)norm[j]);
+            for (uint32_t e = 0; e < d; e++) dst[e] = src[e] / n;
+        }
+    }
+    for (; i < nq; i++) normalize_host(v + (size_t)i * d, d, out + (size_t)i * pitch);
+}
+
 // BinaryQuantizer.Encode (CH/binary_quantization.go:32-45).
 static void bq_encode_host(const float *v, uint32_t d, uint64_t *code, uint32_t words)
 {
@@ -86,14 +118,11 @@ void prepare_queries_host(const wvg_corpus *c, const float *queries, uint32_t nq
     }
     qpitch = c->kind == WVG_KIND_F32 ? f32_chunks(d) * 4 : d;
     qf.assign((size_t)nq * qpitch, 0.0f);
-    for (uint32_t i = 0; i < nq; i++) {
-        const float *q = queries + (size_t)i * d;
-        float *dst = qf.data() + (size_t)i * qpitch;
-        if (c->metric == WVG_METRIC_COSINE)
-            normalize_host(q, d, dst);
-        else
-            std::memcpy(dst, q, sizeof(float) * d);
+    if (c->metric == WVG_METRIC_COSINE) {
+        normalize_host_rows(queries, nq, d, qf.data(), qpitch);
+        return;
     }
+    for (uint32_t i = 0; i < nq; i++) std::memcpy(qf.data() + (size_t)i * qpitch, queries + (size_t)i * d, sizeof(float) * d);
 }
 
 static hipError_t launch_scan(const ScanArgs &a, int kind, uint64_t *partials, int groups, hipStream_t s)
@@ -396,6 +425,14 @@ int stage_queries(wvg_corpus *c, StreamSlot *sl, const float *queries, uint32_t 
 {
     std::vector<float> qf;
     std::vector<uint64_t> qb;
+    if (c->kind == WVG_KIND_F32 && c->metric != WVG_METRIC_COSINE && f32_chunks(c->dim) * 4 == c->dim) {
+        // the prepared queries are the caller's rows as they are: one copy, no host pass
+        qpitch = c->dim;
+        hipStream_t s = sl->stream;
+        WVG_HIP(st ? st->h2d(dst, queries, (size_t)nq * c->dim * 4, s)
+                   : hipMemcpyAsync(dst, queries, (size_t)nq * c->dim * 4, hipMemcpyHostToDevice, s));
+        return WVG_OK;
+    }
     prepare_queries_host(c, queries, nq, qf, qb, qpitch);
     // A copy from pageable memory returns once the source has been staged, so
     // qf / qb may go out of scope without a stream sync (which would put a host
