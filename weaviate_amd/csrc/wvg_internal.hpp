@@ -326,12 +326,10 @@ struct ScreenLaunch {
     uint64_t *cand;        // [nq][nrr * SCREEN_M]
     uint32_t *flist;       // [nq] flagged queries
     uint32_t *nflag;       // count
-    // exact seeds between phases (optional): the rows and distance the final
-    // rescore uses, and [nq][nrr * SCREEN_M] keys of scratch
+    // exact seeds (optional): the rows and distance the final rescore uses
     int metric = 0;
     const float *data = nullptr;  // tiled fp32 rows
     uint32_t nchunks = 0;
-    uint64_t *seed_keys = nullptr;
     // pilot (optional): the exact K1 top-k of every query over the range's
     // first tiles seeds the bound before the first phase
     const ScanArgs *pilot = nullptr;
@@ -460,6 +458,11 @@ hipError_t launch_dist_keys(int metric, const float *q, const float *tiled, uint
                             uint64_t *keys, hipStream_t s, int o512 = 0);
 hipError_t launch_synth_rows(uint64_t seed, int dist, const uint64_t *ids, uint64_t n, uint32_t dim,
                              int normalize, float *out, hipStream_t s);
+// The screen's exact seed: the k-th exact distance of each query's <= 64 packed
+// candidate keys into gbound (atomicMin).
+hipError_t launch_seed_exact(int metric, const float *q, uint32_t qpitch, const float *tiled, uint32_t dim,
+                             uint32_t nchunks, const uint64_t *cand, uint32_t cand_stride, uint32_t n, uint32_t nq,
+                             uint32_t k, uint32_t *gbound, hipStream_t s);
 hipError_t launch_rescore_keys(int metric, const float *q, uint32_t qpitch, const float *tiled,
                                uint32_t dim, uint32_t nchunks, const uint64_t *cand_keys,
                                uint32_t nq, uint32_t ncand, uint32_t cand_stride,

@@ -1053,6 +1053,47 @@ hipError_t launch_rescore_keys(int metric, const float *q, uint32_t qpitch, cons
     return hipGetLastError();
 }
 
+// Screen seed (wvg_screen.hip exact_seed): per query, the exact distances of
+// its <= 64 packed seed candidates (the final rescore's distance) and their
+// k-th smallest, folded into gbound -- one wave per query, a rank by shuffles
+// instead of a second kernel's radix select.
+template <int METRIC>
+__global__ __launch_bounds__(64) void seed_exact_kernel(int metric, const float4 *q4, uint32_t qpitch,
+                                                        const float4 *tiled, uint32_t dim, uint32_t nchunks,
+                                                        const uint64_t *cand, uint32_t cand_stride, uint32_t n,
+                                                        uint32_t k, uint32_t *gbound)
+{
+    const uint32_t qi = blockIdx.x, lane = threadIdx.x;
+    const uint64_t key = lane < n ? cand[(size_t)qi * cand_stride + lane] : WVG_KEY_NONE;
+    uint32_t v = 0xFFFFFFFFu;
+    if (key != WVG_KEY_NONE) {
+        const uint32_t slot = (uint32_t)key;
+        const float4 *rp = tiled + ((size_t)(slot >> 6) * nchunks) * 64 + (slot & 63);
+        v = wvg_ord_f32(wrap_metric(metric, row_dist<METRIC, 64>(rp, q4 + (size_t)qi * (qpitch / 4), (int)dim, 0)));
+    }
+    const uint64_t live = __ballot(key != WVG_KEY_NONE);
+    if ((uint32_t)__popcll(live) < k) return;
+    uint32_t rank = 0;
+    for (int j = 0; j < 64; j++) {
+        const uint32_t o = (uint32_t)__shfl((int)v, j);
+        rank += (o < v) || (o == v && (uint32_t)j < lane);
+    }
+    if (key != WVG_KEY_NONE && rank == k - 1 && wvg_unord_f32(v) < __builtin_inff()) atomicMin(gbound + qi, v);
+}
+
+hipError_t launch_seed_exact(int metric, const float *q, uint32_t qpitch, const float *tiled, uint32_t dim,
+                             uint32_t nchunks, const uint64_t *cand, uint32_t cand_stride, uint32_t n, uint32_t nq,
+                             uint32_t k, uint32_t *gbound, hipStream_t s)
+{
+    if (nq == 0 || n == 0 || n > 64 || k == 0) return nq == 0 ? hipSuccess : hipErrorInvalidValue;
+    with_metric(metric, [&](auto M) {
+        hipLaunchKernelGGL((seed_exact_kernel<decltype(M)::value>), dim3(nq), dim3(64), 0, s, metric,
+                           reinterpret_cast<const float4 *>(q), qpitch, reinterpret_cast<const float4 *>(tiled), dim,
+                           nchunks, cand, cand_stride, n, k, gbound);
+    });
+    return hipGetLastError();
+}
+
 // Streaming-read probe behind wvg_measure_hbm_read: the HBM read ceiling the
 // scans are judged against, measured in-process (tools/hbm_read.hip's best
 // form: grid-stride 16-byte non-temporal loads, 8 in flight per lane).

@@ -1327,7 +1327,9 @@ __device__ uint32_t block_kth_ordered(const uint32_t *hv, uint32_t n, uint32_t k
 // of a split screen start from.  Exact seed (cand != nullptr, flist ==
 // nullptr): that tau* folded into gbound, and the entries with the k
 // smallest lower bounds packed into cand for an exact rescore whose k-th
-// distance is the tighter seed (screen_seed_kth_kernel).
+// distance is the tighter seed (launch_seed_exact).  Against the list seed
+// (k-th lower bound + 2 Emax) it drops the bound's error term, about one
+// Emax: fewer rows of the later phases reach the per-element test.
 __global__ __launch_bounds__(256) void screen_collect_kernel(const uint64_t *partials, uint32_t nrr, uint32_t nrr_use,
                                                              uint32_t k, const float *emax, int cosine, uint64_t *cand,
                                                              uint32_t *flist, uint32_t *nflag, uint32_t *gbound)
@@ -1390,34 +1392,6 @@ __global__ __launch_bounds__(256) void screen_collect_kernel(const uint64_t *par
     if (threadIdx.x == 0 && ovf && flist) flist[atomicAdd(nflag, 1u)] = q;
 }
 
-// Exact seed: the k-th smallest of a query's exactly rescored seed candidates
-// (keys: ordered distance << 32 | slot; n per query) -- k real rows at or
-// below it, so it bounds the final k-th like the pilot's -- into gbound.
-// Against the list seed (k-th lower bound + 2 Emax) it drops the bound's
-// error term, about one Emax: fewer rows of the later phases reach the
-// per-element test and the list insertions.
-__global__ __launch_bounds__(256) void screen_seed_kth_kernel(const uint64_t *keys, uint32_t n, uint32_t k,
-                                                              uint32_t *gbound)
-{
-    __shared__ uint32_t hv[SC_COLLECT_MAX];
-    __shared__ uint32_t hist[256];
-    __shared__ uint32_t sh_prefix, sh_need, sh_total;
-    const uint32_t q = blockIdx.x;
-    const uint64_t *src = keys + (size_t)q * n;
-    if (threadIdx.x == 0) sh_total = 0;
-    __syncthreads();
-    uint32_t live = 0;
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-        const uint64_t e = src[i];
-        hv[i] = (uint32_t)(e >> 32);
-        live += e != WVG_KEY_NONE;
-    }
-    atomicAdd(&sh_total, live);
-    __syncthreads();
-    if (sh_total < k) return;
-    const uint32_t v = block_kth_ordered(hv, n, k, hist, sh_prefix, sh_need);
-    if (threadIdx.x == 0 && wvg_unord_f32(v) < __builtin_inff()) atomicMin(gbound + q, v);
-}
 
 __global__ __launch_bounds__(256) void screen_pilot_list_kernel(uint32_t *flist, uint32_t nq, uint32_t *nflag)
 {
@@ -1632,7 +1606,7 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
     bounds[nph] = L.nrr;
     // seeds between phases: the exact k-th over the earlier ranges' candidates
     // (rescored with the final rescore's distances) where the rows are at hand
-    const bool rows = L.data != nullptr && L.seed_keys != nullptr;
+    const bool rows = L.data != nullptr;
     const bool seed_exact = rows && (tuning().screen_seed & 1) != 0, seed_final = rows && (tuning().screen_seed & 2) != 0;
     // an exact seed over the lists of ranges [0, nuse / SCREEN_M)
     auto exact_seed = [&](uint32_t nr_use) -> hipError_t {
@@ -1641,11 +1615,8 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
                            L.cosine, L.cand, (uint32_t *)nullptr, (uint32_t *)nullptr, L.gbound);
         hipError_t e2;
         if ((e2 = hipGetLastError()) != hipSuccess) return e2;
-        if ((e2 = launch_rescore_keys(L.metric, L.queries, L.qpitch, L.data, L.dim, L.nchunks, L.cand, L.nq, nres,
-                                      nuse, L.seed_keys, s, 0)) != hipSuccess)
-            return e2;
-        hipLaunchKernelGGL(screen_seed_kth_kernel, dim3(L.nq), dim3(256), 0, s, L.seed_keys, nres, L.k, L.gbound);
-        return hipGetLastError();
+        return launch_seed_exact(L.metric, L.queries, L.qpitch, L.data, L.dim, L.nchunks, L.cand, nuse, nres, L.nq,
+                                 L.k, L.gbound, s);
     };
     for (uint32_t ph = 0; ph < nph; ph++) {
         a.rr0 = bounds[ph];

@@ -300,7 +300,6 @@ static int run_screen(wvg_corpus *c, const ScanArgs &a, const SearchPlan &p, cha
     L.metric = c->metric;
     L.data = (const float *)c->d_data;
     L.nchunks = c->nchunks;
-    L.seed_keys = keys;  // free until the final rescore
     WVG_HIP(launch_screen(L, s));
     WVG_HIP(launch_rescore_keys(c->metric, (const float *)a.queries, a.qpitch, (const float *)c->d_data, c->dim,
                                 c->nchunks, L.cand, nq, ncand, ncand, keys, s, 0));
