@@ -458,11 +458,12 @@ hipError_t launch_dist_keys(int metric, const float *q, const float *tiled, uint
                             uint64_t *keys, hipStream_t s, int o512 = 0);
 hipError_t launch_synth_rows(uint64_t seed, int dist, const uint64_t *ids, uint64_t n, uint32_t dim,
                              int normalize, float *out, hipStream_t s);
-// The screen's exact seed: the k-th exact distance of each query's <= 64 packed
-// candidate keys into gbound (atomicMin).
+// The screen's exact seed: per query, the k smallest keys of its first `nlists`
+// ascending range lists (partials [nq][list_stride], lists of list_len keys)
+// rescored exactly; their k-th distance into gbound (atomicMin).
 hipError_t launch_seed_exact(int metric, const float *q, uint32_t qpitch, const float *tiled, uint32_t dim,
-                             uint32_t nchunks, const uint64_t *cand, uint32_t cand_stride, uint32_t n, uint32_t nq,
-                             uint32_t k, uint32_t *gbound, hipStream_t s);
+                             uint32_t nchunks, const uint64_t *partials, uint32_t list_stride, uint32_t list_len,
+                             uint32_t nlists, uint32_t nq, uint32_t k, uint32_t *gbound, hipStream_t s);
 hipError_t launch_rescore_keys(int metric, const float *q, uint32_t qpitch, const float *tiled,
                                uint32_t dim, uint32_t nchunks, const uint64_t *cand_keys,
                                uint32_t nq, uint32_t ncand, uint32_t cand_stride,

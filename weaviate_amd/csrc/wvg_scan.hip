@@ -1053,18 +1053,28 @@ hipError_t launch_rescore_keys(int metric, const float *q, uint32_t qpitch, cons
     return hipGetLastError();
 }
 
-// Screen seed (wvg_screen.hip exact_seed): per query, the exact distances of
-// its <= 64 packed seed candidates (the final rescore's distance) and their
-// k-th smallest, folded into gbound -- one wave per query, a rank by shuffles
-// instead of a second kernel's radix select.
+// Screen seed (wvg_screen.hip): per query, the k smallest lower-bound keys of
+// the first `nlists` range lists (ascending, so only their first k entries
+// can be among them; a wave top-k over those), rescored exactly with the
+// final rescore's distance, and their k-th distance -- k real rows at or
+// below it -- folded into gbound.  One wave per query, rank by shuffles.
 template <int METRIC>
 __global__ __launch_bounds__(64) void seed_exact_kernel(int metric, const float4 *q4, uint32_t qpitch,
                                                         const float4 *tiled, uint32_t dim, uint32_t nchunks,
-                                                        const uint64_t *cand, uint32_t cand_stride, uint32_t n,
-                                                        uint32_t k, uint32_t *gbound)
+                                                        const uint64_t *partials, uint32_t list_stride,
+                                                        uint32_t list_len, uint32_t nlists, uint32_t k,
+                                                        uint32_t *gbound)
 {
     const uint32_t qi = blockIdx.x, lane = threadIdx.x;
-    const uint64_t key = lane < n ? cand[(size_t)qi * cand_stride + lane] : WVG_KEY_NONE;
+    const uint64_t *src = partials + (size_t)qi * list_stride;
+    WaveTopK<1> tk;
+    tk.init((int)k);
+    const uint32_t n = nlists * k;
+    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        tk.offer(i < n ? src[(size_t)(i / k) * list_len + i % k] : WVG_KEY_NONE);
+    }
+    const uint64_t key = lane < k ? tk.l[0] : WVG_KEY_NONE;
     uint32_t v = 0xFFFFFFFFu;
     if (key != WVG_KEY_NONE) {
         const uint32_t slot = (uint32_t)key;
@@ -1082,14 +1092,15 @@ __global__ __launch_bounds__(64) void seed_exact_kernel(int metric, const float4
 }
 
 hipError_t launch_seed_exact(int metric, const float *q, uint32_t qpitch, const float *tiled, uint32_t dim,
-                             uint32_t nchunks, const uint64_t *cand, uint32_t cand_stride, uint32_t n, uint32_t nq,
-                             uint32_t k, uint32_t *gbound, hipStream_t s)
+                             uint32_t nchunks, const uint64_t *partials, uint32_t list_stride, uint32_t list_len,
+                             uint32_t nlists, uint32_t nq, uint32_t k, uint32_t *gbound, hipStream_t s)
 {
-    if (nq == 0 || n == 0 || n > 64 || k == 0) return nq == 0 ? hipSuccess : hipErrorInvalidValue;
+    if (nq == 0 || nlists == 0) return hipSuccess;
+    if (k == 0 || k > 64 || k > list_len) return hipErrorInvalidValue;
     with_metric(metric, [&](auto M) {
         hipLaunchKernelGGL((seed_exact_kernel<decltype(M)::value>), dim3(nq), dim3(64), 0, s, metric,
                            reinterpret_cast<const float4 *>(q), qpitch, reinterpret_cast<const float4 *>(tiled), dim,
-                           nchunks, cand, cand_stride, n, k, gbound);
+                           nchunks, partials, list_stride, list_len, nlists, k, gbound);
     });
     return hipGetLastError();
 }

@@ -1282,7 +1282,6 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
 // the exact rescan.  The k-th smallest is a 4-pass radix select (8-bit
 // digits) over the entries' ordered lower bounds in LDS.
 constexpr uint32_t SC_COLLECT_MAX = 8192;  // nrr * SCREEN_M (screen_row_ranges caps nrr at 512)
-constexpr uint32_t SC_SEED_MAX = 64;       // exact-seed rescore entries per query (>= SCREEN_M >= k)
 
 // The k-th smallest (k >= 1) of the ordered values hv[0, n) in LDS, of which
 // at least k are not 0xFFFFFFFF: a 4-pass radix select over 8-bit digits.
@@ -1324,12 +1323,9 @@ __device__ uint32_t block_kth_ordered(const uint32_t *hv, uint32_t n, uint32_t k
 
 // seed (cand == nullptr): the same tau* over the lists of the first nrr_use
 // ranges only, folded into gbound (atomicMin) -- the bound the later ranges
-// of a split screen start from.  Exact seed (cand != nullptr, flist ==
-// nullptr): that tau* folded into gbound, and the entries with the k
-// smallest lower bounds packed into cand for an exact rescore whose k-th
-// distance is the tighter seed (launch_seed_exact).  Against the list seed
-// (k-th lower bound + 2 Emax) it drops the bound's error term, about one
-// Emax: fewer rows of the later phases reach the per-element test.
+// of a split screen start from (without exact seeds; launch_seed_exact's
+// k-th exact distance drops that bound's error term, about one Emax).
+// Final (cand != nullptr): candidates within min(tau*, gbound).
 __global__ __launch_bounds__(256) void screen_collect_kernel(const uint64_t *partials, uint32_t nrr, uint32_t nrr_use,
                                                              uint32_t k, const float *emax, int cosine, uint64_t *cand,
                                                              uint32_t *flist, uint32_t *nflag, uint32_t *gbound)
@@ -1355,17 +1351,13 @@ __global__ __launch_bounds__(256) void screen_collect_kernel(const uint64_t *par
     atomicAdd(&sh_total, live);
     __syncthreads();
     float t = __builtin_inff();
-    uint32_t kth = 0xFFFFFFFFu;  // the k-th smallest ordered lower bound
-    if (sh_total >= k) {
-        kth = block_kth_ordered(hv, n, k, hist, sh_prefix, sh_need);
-        t = sc_tau_k(wvg_unord_f32(kth), emax[q], cosine);
-    }
+    if (sh_total >= k) t = sc_tau_k(wvg_unord_f32(block_kth_ordered(hv, n, k, hist, sh_prefix, sh_need)), emax[q], cosine);
     // the candidates: gbound may hold a tighter valid bound than tau* (an exact seed)
     const uint32_t gb = gbound[q];
-    if (cand && flist && gb != 0xFFFFFFFFu) t = fminf(t, wvg_unord_f32(gb));
-    if (!cand || !flist) {
+    if (cand && gb != 0xFFFFFFFFu) t = fminf(t, wvg_unord_f32(gb));
+    if (!cand) {
         if (threadIdx.x == 0 && t < __builtin_inff()) atomicMin(gbound + q, wvg_ord_f32(t));
-        if (!cand) return;
+        return;
     }
     __syncthreads();
     if (threadIdx.x == 0) sh_total = 0;
@@ -1377,9 +1369,7 @@ __global__ __launch_bounds__(256) void screen_collect_kernel(const uint64_t *par
     for (uint32_t i0 = 0; i0 < n; i0 += blockDim.x) {
         const uint32_t i = i0 + threadIdx.x;
         const uint64_t e = i < n ? src[i] : WVG_KEY_NONE;
-        // exact seed: the k smallest lower bounds only (ties: all of them) -- any k
-        // rows bound the k-th, and these k are the likeliest to be the closest
-        const bool keep = e != WVG_KEY_NONE && (flist ? key_lower(e) <= t : (uint32_t)(e >> 32) <= kth);
+        const bool keep = e != WVG_KEY_NONE && key_lower(e) <= t;
         if (keep && (i % SCREEN_M) == SCREEN_M - 1) ovf = 1;  // full list, last entry within tau*
         const uint64_t bal = __ballot(keep);
         uint32_t base = 0;
@@ -1389,7 +1379,7 @@ __global__ __launch_bounds__(256) void screen_collect_kernel(const uint64_t *par
     }
     __syncthreads();
     for (uint32_t i = sh_total + threadIdx.x; i < n; i += blockDim.x) dst[i] = WVG_KEY_NONE;
-    if (threadIdx.x == 0 && ovf && flist) flist[atomicAdd(nflag, 1u)] = q;
+    if (threadIdx.x == 0 && ovf) flist[atomicAdd(nflag, 1u)] = q;
 }
 
 
@@ -1608,15 +1598,10 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
     // (rescored with the final rescore's distances) where the rows are at hand
     const bool rows = L.data != nullptr;
     const bool seed_exact = rows && (tuning().screen_seed & 1) != 0, seed_final = rows && (tuning().screen_seed & 2) != 0;
-    // an exact seed over the lists of ranges [0, nuse / SCREEN_M)
+    // an exact seed over the lists of ranges [0, nr_use)
     auto exact_seed = [&](uint32_t nr_use) -> hipError_t {
-        const uint32_t nuse = nr_use * SCREEN_M, nres = std::min<uint32_t>(nuse, SC_SEED_MAX);
-        hipLaunchKernelGGL(screen_collect_kernel, dim3(L.nq), dim3(256), 0, s, L.partials, L.nrr, nr_use, L.k, L.emax,
-                           L.cosine, L.cand, (uint32_t *)nullptr, (uint32_t *)nullptr, L.gbound);
-        hipError_t e2;
-        if ((e2 = hipGetLastError()) != hipSuccess) return e2;
-        return launch_seed_exact(L.metric, L.queries, L.qpitch, L.data, L.dim, L.nchunks, L.cand, nuse, nres, L.nq,
-                                 L.k, L.gbound, s);
+        return launch_seed_exact(L.metric, L.queries, L.qpitch, L.data, L.dim, L.nchunks, L.partials,
+                                 L.nrr * SCREEN_M, SCREEN_M, nr_use, L.nq, L.k, L.gbound, s);
     };
     for (uint32_t ph = 0; ph < nph; ph++) {
         a.rr0 = bounds[ph];
