@@ -62,6 +62,9 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--configs", default="host_api,batched,bq,pq,slab",
                     help="N = 1: BASELINE configs 2-5 measured after the headline (comma list; '' = none)")
+    ap.add_argument("--scale-legs", default="slab1b,pq",
+                    help="strong-scaling legs at every N (comma list; '' = none): slab1b = configs[4] 1B x 128 as 8 "
+                         "slabs dealt to the N GPUs, pq = configs[3] 100M PQ sharded over the N GPUs")
     ap.add_argument("--profile-run", action="store_true",
                     help="only the timed headline launches (no no-reuse leg, read probe or CPU baseline), so a "
                          "rocprofv3 --stats summary of the scan kernel covers exactly the launches `roofline` times")
@@ -547,7 +550,8 @@ def config_slab(ctx, orc, dev, torch, nq=8):
     return {"workload": f"{n:,} x {d} fp32 L2 slab (global docIDs [{base:,}, {base + n:,}): slab 3 of the 1B corpus), "
                         f"exact {k}-NN, {nq} single-query scans per query-stream launch",
             "qps_per_slab": round(1 / wall, 2), "scan_ms_per_query": round(scan_s * 1e3, 3),
-            "qps_1b_one_gpu_8_slabs": round(1 / (8 * wall), 3),
+            "note": "one slab of the 1B corpus; the measured 8-slab pass (all slabs scanned and merged at this "
+                    "N) is configs.config5_1b_x_128",
             "kernel": "K1 scan_f32_stream_kernel<L2,128,2>",
             "roofline": {"bound": "hbm", "achieved": round(gbps, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbps / HBM_PEAK_GBS, 4), "bytes_per_scan": n * d * 4},
@@ -555,20 +559,71 @@ def config_slab(ctx, orc, dev, torch, nq=8):
                                        "recomputations, no row of 60k sampled ahead of the k-th; all counts = k"}}
 
 
+def _callers(call, T, seconds):
+    """T threads (goroutines) calling call(thread, i) back to back for about
+    `seconds`; returns (calls per second, per-call latencies in us)."""
+    import threading
+
+    done = [0] * T
+    lat = [[] for _ in range(T)]
+    start = threading.Barrier(T + 1)
+    stop_at = [0.0]
+
+    def worker(t):
+        i = t
+        start.wait()
+        pc = time.perf_counter
+        while True:
+            t0 = pc()
+            if t0 >= stop_at[0]:
+                break
+            call(t, i)
+            lat[t].append(pc() - t0)
+            i += T
+            done[t] += 1
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+    [t.start() for t in th]
+    stop_at[0] = time.perf_counter() + seconds + 0.2
+    start.wait()
+    t0 = time.perf_counter()
+    [t.join() for t in th]
+    el = time.perf_counter() - t0
+    return sum(done) / el, np.concatenate([np.asarray(x) for x in lat]) * 1e6
+
+
+def _lat_rec(qps, lat_us, n, d, T):
+    rec = {"qps": round(qps, 1), "calls": int(len(lat_us)),
+           "latency_us": {"p50": round(float(np.percentile(lat_us, 50)), 1),
+                          "p99": round(float(np.percentile(lat_us, 99)), 1),
+                          "max": round(float(lat_us.max()), 1)}}
+    if T == 1:
+        rec["us_per_call"] = round(1e6 / qps, 2)
+        rec["frac_of_8TBs"] = round(n * d * 4 * qps / 1e9 / HBM_PEAK_GBS, 4)
+    return rec
+
+
 def config_host_api(ctx, orc, callers=(1, 16), seconds=1.0):
     """The headline shape through the host API the Go binding calls: T caller
     threads (goroutines) each issuing single-query wvg_search calls (1M x 128
     L2, k = 10) for `seconds`; concurrent calls on one corpus are coalesced
     into shared launches inside the library (wvg_options.coalesce).  frac (one
-    caller): N*d*4 bytes per call / the call's wall time vs 8 TB/s."""
+    caller): N*d*4 bytes per call / the call's wall time vs 8 TB/s.  Per-call
+    latency percentiles (the queries_durations_ms histogram's view,
+    usecases/monitoring/prometheus.go:216) are taken around each call in the
+    calling thread (so they include ~2 us of Python / ctypes).  Filtered calls:
+    every call carries one of 8 allow lists (helpers.AllowList bitmaps,
+    V/flat/index.go:423-449) keeping 10 % or 1 % of the rows."""
     import threading
 
     from weaviate_amd._lib import KIND_F32, METRIC_L2, check, fptr, u32ptr, u64ptr
-    from weaviate_amd.device import Context, Corpus
+    from weaviate_amd.device import Context, Corpus, allow_bitmap
 
     n, d, k = 1_000_000, 128, 10
     qs = np.ascontiguousarray(orc.synth_rows(43, 0, 256, d, 0))
     out = {"workload": f"{n:,} x {d} fp32 L2 exact {k}-NN, one query per wvg_search call, T concurrent callers"}
+    rng = np.random.default_rng(47)
+    allows = {rate: [allow_bitmap(np.flatnonzero(rng.random(n) < rate), n) for _ in range(8)] for rate in (0.1, 0.01)}
     for coalesce in (1, 0):
         cx = ctx if coalesce else Context(ctx.device, coalesce=0)
         lib = cx.lib
@@ -576,24 +631,27 @@ def config_host_api(ctx, orc, callers=(1, 16), seconds=1.0):
         c.fill_synthetic(42, n, 0)
         qp = [fptr(qs[i]) for i in range(len(qs))]
 
-        def call(i, bufs):
-            check(lib.wvg_search(c.handle, qp[i % len(qs)], 1, k, None, 0, *bufs[1]))
-
         def bufs_new():
             ids, ds, cnt = np.empty(k, np.uint64), np.empty(k, np.float32), np.empty(1, np.uint32)
             return (ids, ds, cnt), (u64ptr(ids), fptr(ds), u32ptr(cnt))
 
+        bufs = [bufs_new() for _ in range(max(callers))]
+
+        def call(t, i, allow=None):
+            a = None if allow is None else allow[i % len(allow)]
+            check(lib.wvg_search(c.handle, qp[i % len(qs)], 1, k, u64ptr(a) if a is not None else None,
+                                 0 if a is None else len(a), *bufs[t][1]))
+
         # check: 16 concurrent calls return exactly what serial calls return
         serial = []
         for i in range(16):
-            b = bufs_new()
-            call(i, b)
-            serial.append((b[0][0].copy(), b[0][1].copy()))
+            call(0, i)
+            serial.append((bufs[0][0][0].copy(), bufs[0][0][1].copy()))
         got = [None] * 16
 
         def one(i):
             b = bufs_new()
-            call(i, b)
+            check(lib.wvg_search(c.handle, qp[i], 1, k, None, 0, *b[1]))
             got[i] = (b[0][0].copy(), b[0][1].copy())
 
         th = [threading.Thread(target=one, args=(i,)) for i in range(16)]
@@ -601,34 +659,35 @@ def config_host_api(ctx, orc, callers=(1, 16), seconds=1.0):
         [t.join() for t in th]
         same = all(np.array_equal(g[0], s[0]) and np.array_equal(g[1].view(np.uint32), s[1].view(np.uint32))
                    for g, s in zip(got, serial))
+        tag = "coalesced" if coalesce else "uncoalesced"
         for T in callers:
-            done = [0] * T
-            start = threading.Barrier(T + 1)
-            stop_at = [0.0]
+            qps, lat = _callers(call, T, seconds)
+            out[f"{tag}_callers_{T}"] = _lat_rec(qps, lat, n, d, T)
+        out[f"{tag}_16_concurrent_equal_serial"] = bool(same)
+        if coalesce:  # filtered single queries, 10 % and 1 % allow lists
+            for rate, al in allows.items():
+                for T in callers:
+                    qps, lat = _callers(lambda t, i: call(t, i, al), T, seconds / 2)
+                    rec = _lat_rec(qps, lat, n, d, T)
+                    rec.pop("frac_of_8TBs", None)  # a filtered scan skips tiles with no allowed row
+                    out[f"filtered_{int(rate * 100)}pct_callers_{T}"] = rec
+            # filtered concurrent calls = serial filtered calls
+            fs = []
+            for i in range(16):
+                call(0, i, allows[0.01])
+                fs.append(bufs[0][0][0].copy())
+            fg = [None] * 16
 
-            def worker(t):
+            def onef(i):
                 b = bufs_new()
-                i = t
-                start.wait()
-                while time.perf_counter() < stop_at[0]:
-                    call(i, b)
-                    i += T
-                    done[t] += 1
+                a = allows[0.01][i % 8]
+                check(lib.wvg_search(c.handle, qp[i], 1, k, u64ptr(a), len(a), *b[1]))
+                fg[i] = b[0][0].copy()
 
-            th = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+            th = [threading.Thread(target=onef, args=(i,)) for i in range(16)]
             [t.start() for t in th]
-            stop_at[0] = time.perf_counter() + seconds + 0.2
-            start.wait()
-            t0 = time.perf_counter()
             [t.join() for t in th]
-            el = time.perf_counter() - t0
-            qps = sum(done) / el
-            rec = {"qps": round(qps, 1), "calls": sum(done)}
-            if T == 1:
-                rec["us_per_call"] = round(1e6 / qps, 2)
-                rec["frac_of_8TBs"] = round(n * d * 4 * qps / 1e9 / HBM_PEAK_GBS, 4)
-            out[f"{'coalesced' if coalesce else 'uncoalesced'}_callers_{T}"] = rec
-        out[f"{'coalesced' if coalesce else 'uncoalesced'}_16_concurrent_equal_serial"] = bool(same)
+            out["filtered_16_concurrent_equal_serial"] = all(np.array_equal(x, y) for x, y in zip(fs, fg))
         c.destroy()
         if not coalesce:
             cx.close()
@@ -922,8 +981,24 @@ def run_flat1m(args, world, rank, dev, torch, dist):
         "configs": None,
         "merge_check": mcheck,
     }
+    legs = {}
+    if args.scale_legs and not args.profile_run:
+        # BASELINE configs[4] and configs[3] as strong scaling at this N (every rank takes part)
+        for name in args.scale_legs.split(","):
+            t0 = time.perf_counter()
+            try:
+                if name == "slab1b":
+                    legs["config5_1b_x_128"] = slab1b_leg(world, rank, dev, torch, dist)
+                elif name == "pq":
+                    legs["config4_pq_sharded"] = pq_sharded_leg(world, rank, dev, torch, dist)
+            except Exception as e:  # noqa: BLE001 -- a failed leg is reported, the headline stands
+                legs[f"{name}_error"] = f"{type(e).__name__}: {e}"
+            if rank == 0:
+                print(f"bench.py: scale leg {name} {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
     if rank == 0 and world == 1 and args.configs and not args.profile_run:
         out["configs"] = run_configs(args, dev, torch)
+    if legs:
+        out["configs"] = dict(out["configs"] or {}, **legs)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_run:
         cq = np.random.default_rng(43).uniform(-1, 1, (16, d)).astype(np.float32)
         gids, _, _ = corpus.search(cq, k)  # GPU results of the baseline's first queries (full-size cross-check)
@@ -944,14 +1019,57 @@ def run_flat1m(args, world, rank, dev, torch, dist):
     return out
 
 
-def run_slab1b(args, world, rank, dev, torch, dist):
+SLAB_SAMPLE = 10_000  # rows sampled at the start, middle and end of every slab by the 1B property check
+
+
+def sampled_check(total, per, S, d, k, qs, got_ids, got_d):
+    """Rank 0's check of a merged result over a corpus too large for the host
+    oracle (1B x 128): per query, the merged list is sorted in (distance,
+    docID) order, holds k distinct ids inside the corpus, every distance is a
+    bit-exact recomputation of its row (regenerated from the counter RNG), and
+    no row of 3 x SLAB_SAMPLE sampled from every slab (start, middle, end) lies
+    outside the result ahead of its k-th.  Checker only, after the timed region."""
+    from oracle import wv_oracle as orc
+
+    sample = []
+    for s in range(S):
+        n_s = max(0, min(per, total - s * per))
+        for off in (0, n_s // 2 - SLAB_SAMPLE // 2, n_s - SLAB_SAMPLE):
+            if n_s >= 3 * SLAB_SAMPLE:
+                sample.append((s * per + off, SLAB_SAMPLE))
+    sids = np.concatenate([np.arange(b, b + m, dtype=np.int64) for b, m in sample])
+    srows = np.concatenate([orc.synth_rows(42, b, m, d, 0) for b, m in sample])
+    ok = True
+    for qi in range(len(qs)):
+        gi = np.asarray(got_ids[qi]).view(np.uint64)
+        gd = np.asarray(got_d[qi], np.float32)
+        ok &= len(set(gi.tolist())) == k and bool(np.all(gi < total))
+        ok &= _sorted_ok(orc, gd)
+        rows = np.stack([orc.synth_rows(42, int(i), 1, d, 0)[0] for i in gi])
+        ok &= bool(np.array_equal(_bits(orc.dist_all(0, qs[qi], rows)), _bits(gd)))
+        ok &= _outside_ok(orc, sids, orc.dist_all(0, qs[qi], srows), gi.astype(np.int64), gd)
+    return {"ok": bool(ok), "queries": len(qs), "rows": total, "sampled_rows": int(len(sids)),
+            "how": "merged lists sorted, k distinct ids, every distance a bit-exact recomputation of its row, no "
+                   f"row of {len(sids):,} sampled (start / middle / end of each slab) ahead of the k-th"}
+
+
+def slab1b_leg(world, rank, dev, torch, dist, total=1_000_000_000, d=128, k=100, B=8, steps=2, W=1):
+    """BASELINE configs[4] at N GPUs (strong scaling): the 1B x 128 fp32 L2
+    corpus as 8 slabs of 125M rows dealt to the N ranks (8/N each).  A GPU
+    holds one slab in HBM at a time, regenerated in place between slabs
+    (generation untimed); every timed step scans B queries over it (one
+    query-stream launch, exact 100-NN), then -- timed -- the per-slab lists
+    are merged on device into this rank's packed block and exchanged with one
+    RCCL all-gather + device merge (Index.objectVectorSearch's shard merge,
+    adapters/repos/db/index.go:1567-1648).  At N = 1 all 8 slabs are scanned
+    and merged: QPS_1 is measured, not derived.  Returns the measurements; rank
+    0 checks the last step's merged lists on sampled rows."""
     import ctypes
 
     from weaviate_amd._lib import KIND_F32, METRIC_L2, check
     from weaviate_amd.device import Context, Corpus
     from weaviate_amd.shard import all_gather_packed
 
-    total, d, k, B = args.rows, args.dim, args.k, args.batch
     S = 8  # slabs of the corpus
     per = (total + S - 1) // S
     per = (per + 63) // 64 * 64
@@ -961,25 +1079,27 @@ def run_slab1b(args, world, rank, dev, torch, dist):
     L = len(mine)
     ctx = Context(dev.index)
     lib = ctx.lib
-    steps, W = args.steps, args.warmup
     qs = torch.from_numpy(np.random.default_rng(43).uniform(-1, 1, (steps * B, d)).astype(np.float32)).to(dev)
     # per (timed step, local slab) lists; warmup steps write into slot 0
     ids = torch.empty((steps, L, B, k), dtype=torch.int64, device=dev)
     dd = torch.empty((steps, L, B, k), dtype=torch.float32, device=dev)
     cc = torch.empty((steps, L, B), dtype=torch.int32, device=dev)
     blk = lib.wvg_topk_packed_bytes(B, k)
-    send = torch.empty(blk, dtype=torch.uint8, device=dev)
-    recv = torch.empty(world * blk, dtype=torch.uint8, device=dev)
+    send = torch.empty((steps, blk), dtype=torch.uint8, device=dev)
+    recv = torch.empty((steps, world * blk), dtype=torch.uint8, device=dev)
     m_ids = torch.empty((steps, B, k), dtype=torch.int64, device=dev)
     m_d = torch.empty((steps, B, k), dtype=torch.float32, device=dev)
     m_c = torch.empty((steps, B), dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
-    elapsed, scan_ms_tot, launches_tot = 0.0, 0.0, 0
+    scan_s, gen_s, scan_ms_tot, launches_tot = 0.0, 0.0, 0.0, 0
     for j, s in enumerate(mine):
         n_s = max(0, min(per, total - s * per))
+        t0 = time.perf_counter()
         c = Corpus(ctx, KIND_F32, METRIC_L2, d, per, id_base=s * per)
         if n_s:
             c.fill_synthetic(42, n_s, 0)  # untimed: the slab is (re)generated in place
+        torch.cuda.synchronize(dev)
+        gen_s += time.perf_counter() - t0
         wsb = lib.wvg_search_workspace_size(c.handle, B, k)
         ws = torch.zeros(wsb, dtype=torch.uint8, device=dev)
 
@@ -991,51 +1111,177 @@ def run_slab1b(args, world, rank, dev, torch, dist):
         for t in range(W):
             scan(t, 0)
         check(lib.wvg_profile_start(ctx.handle))
-        elapsed += _timed(lambda: [scan(t, t) for t in range(steps)], dist, world, dev, torch)
+        scan_s += _timed(lambda: [scan(t, t) for t in range(steps)], dist, world, dev, torch)
         ms, nl = ctypes.c_double(), ctypes.c_uint64()
         check(lib.wvg_profile_stop(ctx.handle, ctypes.byref(ms), ctypes.byref(nl)))
         check(lib.wvg_search_device_check(ctx.handle, ws.data_ptr(), stream))
         scan_ms_tot += ms.value
         launches_tot += nl.value
         c.destroy()
+        del ws
 
     def merge_all():
         for t in range(steps):
             # this GPU's slabs -> one list per query, straight into the packed block
             check(lib.wvg_topk_merge_device(ctx.handle, dd[t].data_ptr(), ids[t].data_ptr(), B, L, k, k,
-                                            send.data_ptr(), send.data_ptr() + B * k * 8, m_c[t].data_ptr(),
+                                            send[t].data_ptr(), send[t].data_ptr() + B * k * 8, m_c[t].data_ptr(),
                                             stream))
             if world > 1:
-                all_gather_packed(send, recv)
-                check(lib.wvg_topk_merge_packed(ctx.handle, recv.data_ptr(), B, world, k, k, m_ids[t].data_ptr(),
+                all_gather_packed(send[t], recv[t])
+                check(lib.wvg_topk_merge_packed(ctx.handle, recv[t].data_ptr(), B, world, k, k, m_ids[t].data_ptr(),
                                                 m_d[t].data_ptr(), m_c[t].data_ptr(), stream))
 
-    elapsed += _timed(merge_all, dist, world, dev, torch)
-    # the last step's merged lists against the oracle (untimed; small corpora only)
+    merge_s = _timed(merge_all, dist, world, dev, torch)
+    elapsed = scan_s + merge_s
     mcheck = None
-    if rank == 0:
+    if rank == 0:  # the last step's merged lists (untimed)
         if world > 1:
             gi, gd = m_ids[steps - 1][:2].cpu().numpy(), m_d[steps - 1][:2].cpu().numpy()
         else:  # one GPU: the local merge wrote the packed block (ids [B][k], then dists)
-            blkh = send.cpu().numpy()
+            blkh = send[steps - 1].cpu().numpy()
             gi = blkh[:B * k * 8].view(np.uint64).reshape(B, k)[:2]
             gd = blkh[B * k * 8:B * k * 12].view(np.float32).reshape(B, k)[:2]
-        mcheck = merge_check([(s * per, max(0, min(per, total - s * per))) for s in range(S)], d, k,
-                             qs[(steps - 1) * B:(steps - 1) * B + 2].cpu().numpy(), gi, gd)
+        q2 = qs[(steps - 1) * B:(steps - 1) * B + 2].cpu().numpy()
+        if total <= MERGE_CHECK_MAX_ROWS:
+            mcheck = merge_check([(s * per, max(0, min(per, total - s * per))) for s in range(S)], d, k, q2, gi, gd)
+        else:
+            mcheck = sampled_check(total, per, S, d, k, q2, gi, gd)
     if world > 1:
         dist.barrier()
     avg_launch_s = scan_ms_tot / 1e3 / max(1, launches_tot)
-    bytes_per_launch = per * d * 4 * B
-    achieved = bytes_per_launch / avg_launch_s / 1e9
+    achieved = per * d * 4 * B / avg_launch_s / 1e9
     ctx.close()
+    return {"qps": round(B * steps / elapsed, 3), "ms_per_step": round(elapsed / steps * 1e3, 3),
+            "scan_ms_per_step": round(scan_s / steps * 1e3, 3), "merge_ms_per_step": round(merge_s / steps * 1e3, 3),
+            "steps": steps, "warmup": W, "queries_per_step": B, "total_rows": total, "slabs": S,
+            "slabs_per_gpu": L, "rows_per_slab": per, "k": k, "untimed_generation_s": round(gen_s, 2),
+            "kernel": f"wvg::scan_f32_stream_kernel<L2,{d},2>",
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "avg_launch_us": round(avg_launch_s * 1e6, 2),
+                         "algorithmic_bytes_per_launch": per * d * 4 * B, "launches": int(launches_tot),
+                         "note": "per GPU (this rank's slab scans); the line's qps is over all GPUs"},
+            "merge_check": mcheck}
+
+
+def pq_sharded_leg(world, rank, dev, torch, dist, n=100_000_000, d=128, m=32, ks=256, k=10, B=16, steps=4, W=1):
+    """BASELINE configs[3] "1 vs 8 GPUs" at N GPUs (strong scaling over one
+    100M x 128 corpus): rank r holds docIDs shard_range(n, N, r) as fp32 rows;
+    rank 0 fits the codebook (ProductQuantizer.Fit on the first 100k rows,
+    CH/product_quantization.go:372-418) and broadcasts it once (RCCL), every
+    rank encodes its own slab (K9, no collective; V/hnsw/compress.go:98-104
+    per slab), then each step searches B queries: every rank's ADC scan of its
+    codes (K8e, LUT in LDS) into its packed block, one all-gather, the device
+    merge (ShardedFlatIndex.search_device).  Encode and search are timed with a
+    barrier on both sides, max over ranks.  Rank 0 checks the last merged lists
+    against the union of the gathered per-rank lists, and the ADC distances of
+    the entries it owns against the oracle."""
+    import ctypes
+
+    from weaviate_amd._lib import KIND_F32, KIND_PQ, METRIC_L2, check, fptr, u32ptr, u64ptr
+    from weaviate_amd.device import Context, Corpus
+    from weaviate_amd.shard import ShardedFlatIndex, compress_slab, shard_range, unpack_blocks
+
+    lo, cnt, per = shard_range(n, world, rank)
+    ctx = Context(dev.index)
+    lib = ctx.lib
+    f = Corpus(ctx, KIND_F32, METRIC_L2, d, per, id_base=lo)
+    if cnt:
+        f.fill_synthetic(42, cnt, 0)
+    centers = None
+    fit_s = 0.0
+    if rank == 0:
+        nt = 100_000
+        trows = np.empty((nt, d), np.float32)
+        check(lib.wvg_synthetic_rows(ctx.handle, 42, u64ptr(np.arange(nt, dtype=np.uint64)), nt, d, 0, 0,
+                                     fptr(trows)))
+        centers = np.empty((m, ks, d // m), np.float32)
+        passes = np.zeros(m, np.uint32)
+        t0 = time.perf_counter()
+        check(lib.wvg_pq_fit(ctx.handle, fptr(trows), nt, d, m, ks, nt, 7, fptr(centers), u32ptr(passes)))
+        fit_s = time.perf_counter() - t0
+    pq = Corpus(ctx, KIND_PQ, METRIC_L2, d, per, id_base=lo)
+    grouped = world > 1
+    cb = [None]
+
+    def encode():
+        if grouped:
+            bdev = dev if dist.get_backend() == "nccl" else None  # gloo (one-GPU rehearsal): host tensors
+            cb[0] = compress_slab(pq, f, centers, 0, None, bdev)
+        else:
+            pq.set_codebook(centers)
+            check(lib.wvg_pq_encode_corpus(pq.handle, f.handle))
+            cb[0] = centers
+
+    encode()  # untimed first pass (codebook upload, encoder warm-up); the timed pass re-encodes
+    enc_s = _timed(encode, dist, world, dev, torch)
+    f.destroy()
+    qs = torch.from_numpy(np.random.default_rng(46).uniform(-1, 1, (steps * B, d)).astype(np.float32)).to(dev)
+    idx = ShardedFlatIndex(ctx, pq)
+    res = [None]
+
+    def search(t):
+        res[0] = idx.search_device(qs[(t % steps) * B:(t % steps) * B + B], k)
+
+    for t in range(W):
+        search(t)
+    check(lib.wvg_profile_start(ctx.handle))
+    el = _timed(lambda: [search(t) for t in range(steps)], dist, world, dev, torch)
+    ms, nl = ctypes.c_double(), ctypes.c_uint64()
+    check(lib.wvg_profile_stop(ctx.handle, ctypes.byref(ms), ctypes.byref(nl)))
+    idx.check()
+    mcheck = None
+    if rank == 0:
+        from oracle import wv_oracle as orc
+
+        gi, gd, gc = (x.cpu().numpy() for x in res[0])
+        gi = gi.view(np.uint64)
+        ok = bool(np.all(gc == k))
+        if grouped:  # the merge: the lexicographic top-k of the union of every rank's gathered list
+            b = next(iter(idx._bufs.values()))
+            ui, ud = unpack_blocks(b.recv.cpu().numpy(), world, B, k)
+            for qi in range(B):
+                wi, wd = orc.lex_topk(ud[:, qi].reshape(-1), ui[:, qi].reshape(-1), k)
+                ok &= bool(np.array_equal(gi[qi], wi) and np.array_equal(_bits(gd[qi]), _bits(wd)))
+        q_last = qs[(steps - 1) * B:(steps - 1) * B + B].cpu().numpy()
+        owned = 0
+        for qi in (0, B - 1):  # the entries rank 0 owns: ADC distances bit-exact on their stored codes
+            mine_ = (gi[qi] >= lo) & (gi[qi] < lo + cnt)
+            ok &= _sorted_ok(orc, gd[qi])
+            if mine_.any():
+                codes, okc = pq.get_batch(gi[qi][mine_], pq_m=m)
+                lut = orc.pq_lut(0, q_last[qi], cb[0])
+                ok &= bool(okc.all() and np.array_equal(_bits([orc.pq_adc(0, lut, c) for c in codes]),
+                                                        _bits(gd[qi][mine_])))
+                owned += int(mine_.sum())
+        mcheck = {"ok": bool(ok), "owned_entries_checked": owned,
+                  "how": "merged lists = lexicographic top-k of the union of the gathered per-rank lists (N > 1); "
+                         "sorted; rank 0's own entries' ADC distances bit-exact vs the oracle on their codes"}
+    if world > 1:
+        dist.barrier()
+    pq.destroy()
+    ctx.close()
+    scan_s = ms.value / 1e3 / max(1, nl.value)  # one co-scheduled ADC launch of B queries on this rank
+    return {"qps": round(B * steps / el, 2), "ms_per_step": round(el / steps * 1e3, 3), "queries_per_step": B,
+            "steps": steps, "rows": n, "rows_per_gpu": per, "m": m, "ks": ks, "k": k,
+            "fit_s_rank0": round(fit_s, 3), "encode_s": round(enc_s, 4), "encode_rows_per_s": round(n / enc_s, 1),
+            "adc_launch_ms": round(scan_s * 1e3, 4),
+            "kernel": "K8e scan_pq32_wide_kernel co-scheduled (B queries per launch, LUT images in LDS)",
+            "note": "codebook fitted on rank 0 and broadcast; per-rank encode; per step one ADC launch per rank, "
+                    "one all-gather of packed top-k blocks, device merge",
+            "merge_check": mcheck}
+
+
+def run_slab1b(args, world, rank, dev, torch, dist):
+    r = slab1b_leg(world, rank, dev, torch, dist, args.rows, args.dim, args.k, args.batch, args.steps, args.warmup)
+    total, d, k = args.rows, args.dim, args.k
     return {
         "metric": METRIC,
-        "value": round(B * steps / elapsed, 3),
+        "value": r["qps"],
         "unit": "queries/s",
         "n_gpus": world,
-        "steps": steps,
-        "warmup": W,
-        "ms_per_step": round(elapsed / steps * 1e3, 4),
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": r["ms_per_step"],
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -1043,27 +1289,17 @@ def run_slab1b(args, world, rank, dev, torch, dist):
         "data": "synthetic: uniform[-1,1) rows from a counter RNG (seed 42) generated in HBM slab by slab "
                 "(generation untimed); uniform[-1,1) queries (seed 43)",
         "config": {
-            "workload": f"flat exact {k}-NN over {total:,} x {d} fp32 L2 as {S} slabs of {per:,} rows "
-                        f"(BASELINE configs[4]); {L} slab(s) per GPU scanned in sequence",
-            "total_rows": total, "dim": d, "k": k, "queries_per_step": B, "slabs": S, "slabs_per_gpu": L,
+            "workload": f"flat exact {k}-NN over {total:,} x {d} fp32 L2 as {r['slabs']} slabs of "
+                        f"{r['rows_per_slab']:,} rows (BASELINE configs[4]); {r['slabs_per_gpu']} slab(s) per GPU "
+                        f"scanned in sequence",
+            "total_rows": total, "dim": d, "k": k, "queries_per_step": args.batch, "slabs": r["slabs"],
+            "slabs_per_gpu": r["slabs_per_gpu"],
             "parallelism": f"slabs dealt to {world} GPU(s); per step a device merge of the local slabs, one RCCL "
                            f"all-gather of packed top-{k} blocks and a device merge",
         },
-        "roofline": {
-            "bound": "hbm",
-            "kernel": f"wvg::scan_f32_stream_kernel<L2,{d},2>",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None,
-            "avg_launch_us": round(avg_launch_s * 1e6, 2),
-            "queries_per_launch": B,
-            "algorithmic_bytes_per_launch": bytes_per_launch,
-            "launches": launches_tot,
-        },
+        "roofline": dict(r["roofline"], traffic=None),
         "cpu_baseline": None,
-        "merge_check": mcheck,
+        "merge_check": r["merge_check"],
     }
 
 

@@ -8,8 +8,12 @@
 // Every function maps one-to-one onto a wvg_* entry point (the Go symbol each
 // one replaces is cited in include/wvgpu.h).  Host slices are borrowed for the
 // duration of the call only -- the library never retains a Go pointer -- and
-// every status is a Go error carrying the library's thread-local message
-// (cgo runs the call and the wvg_last_error read on the same OS thread).
+// every status is a Go error carrying the library's thread-local message:
+// each method pins its goroutine to one OS thread across the call and the
+// wvg_last_error read (pin), and keeps its handles reachable until both are
+// done, so a finalizer can never free a corpus a running call still uses.
+// The binding is source only in this repository (no Go toolchain in the
+// build image): build it with `go build -tags rocm` (INTEGRATION.md).
 package gpu
 
 /*
@@ -24,6 +28,7 @@ import (
 	"fmt"
 	"math"
 	"runtime"
+	"sync/atomic"
 	"unsafe"
 
 	"github.com/pkg/errors"
@@ -75,6 +80,22 @@ func err(rc C.int) error {
 	return fmt.Errorf("wvgpu %d: %s", int(rc), msg)
 }
 
+// pin locks the calling goroutine to its OS thread until the returned
+// function runs (deferred by every method right at its start), so the C call
+// and err()'s read of the library's thread-local wvg_last_error happen on the
+// same thread -- the Go scheduler may otherwise move the goroutine between the
+// two cgo calls -- and keeps the given handles reachable until then
+// (runtime.KeepAlive), so no finalizer runs while a call uses them.
+func pin(handles ...interface{}) func() {
+	runtime.LockOSThread()
+	return func() {
+		runtime.UnlockOSThread()
+		for _, h := range handles {
+			runtime.KeepAlive(h)
+		}
+	}
+}
+
 func f32p(s []float32) *C.float {
 	if len(s) == 0 {
 		return nil
@@ -103,11 +124,20 @@ func u8p(s []byte) *C.uint8_t {
 	return (*C.uint8_t)(unsafe.Pointer(&s[0]))
 }
 
-// ABIVersion refuses a library built for another ABI (package init of the
-// caller) and DeviceCount sizes WEAVIATE_GPU_DEVICES.
+// ABIVersion is the loaded library's ABI; CheckABI refuses a library built
+// for another ABI than the header this package was compiled against (call it
+// from the caller's package init); DeviceCount sizes WEAVIATE_GPU_DEVICES.
 func ABIVersion() int { return int(C.wvg_abi_version()) }
 
+func CheckABI() error {
+	if got, want := ABIVersion(), int(C.WVG_ABI_VERSION); got != want {
+		return fmt.Errorf("wvgpu: library ABI %d, binding built for ABI %d", got, want)
+	}
+	return nil
+}
+
 func DeviceCount() (int, error) {
+	defer pin()()
 	var n C.int
 	if e := err(C.wvg_device_count(&n)); e != nil {
 		return 0, e
@@ -117,18 +147,26 @@ func DeviceCount() (int, error) {
 
 // ---- context -----------------------------------------------------------------
 
-type Ctx struct{ h *C.wvg_ctx }
+// Ctx is one GPU's context.  It counts its open corpora: Close refuses while
+// any is open, so no Corpus (nor its finalizer) ever uses a freed context.
+type Ctx struct {
+	h       *C.wvg_ctx
+	corpora int64
+}
 
 func Open(device int) (*Ctx, error) {
+	defer pin()()
 	var h *C.wvg_ctx
 	if e := err(C.wvg_open(C.int(device), &h)); e != nil {
 		return nil, e
 	}
-	return &Ctx{h}, nil
+	return &Ctx{h: h}, nil
 }
 
-// Options are fixed for the context's lifetime (wvg_options).  Zero fields
-// keep the library defaults except the two switches, which are explicit.
+// Options are fixed for the context's lifetime (wvg_options).  Start from
+// DefaultOptions() and change what differs: OpenWith copies every field,
+// including the three switches CacheReuse, BatchScreen and Coalesce, whose
+// zero value turns the feature off.  OpenWith(dev, nil) = the defaults.
 type Options struct {
 	MFMAMinQueries uint32 // dot / cosine batches of at least this many queries use MFMA (default 32)
 	CacheReuse     int32  // 1: consecutive scans reuse the Infinity Cache (default); 0: streaming
@@ -144,41 +182,48 @@ func DefaultOptions() Options {
 		int32(o.coalesce)}
 }
 
-func OpenWith(device int, o Options) (*Ctx, error) {
+func OpenWith(device int, o *Options) (*Ctx, error) {
+	defer pin()()
 	var opt C.wvg_options
 	C.wvg_options_default(&opt)
-	if o.MFMAMinQueries != 0 {
+	if o != nil {
 		opt.mfma_min_queries = C.uint32_t(o.MFMAMinQueries)
-	}
-	if o.MergeWaitUs != 0 {
 		opt.merge_wait_us = C.uint32_t(o.MergeWaitUs)
+		opt.cache_reuse = C.int32_t(o.CacheReuse)
+		opt.batch_screen = C.int32_t(o.BatchScreen)
+		opt.coalesce = C.int32_t(o.Coalesce)
 	}
-	opt.cache_reuse = C.int32_t(o.CacheReuse)
-	opt.batch_screen = C.int32_t(o.BatchScreen)
-	opt.coalesce = C.int32_t(o.Coalesce)
 	var h *C.wvg_ctx
 	if e := err(C.wvg_open_ex(C.int(device), &opt, &h)); e != nil {
 		return nil, e
 	}
-	return &Ctx{h}, nil
+	return &Ctx{h: h}, nil
 }
 
-// Close after every Corpus of the context is closed.
+// Close after every Corpus of the context is closed (an error otherwise).
 func (c *Ctx) Close() error {
+	defer pin(c)()
 	if c.h == nil {
 		return nil
+	}
+	if n := atomic.LoadInt64(&c.corpora); n != 0 {
+		return fmt.Errorf("wvgpu: context still has %d open corpora", n)
 	}
 	e := err(C.wvg_close(c.h))
 	c.h = nil
 	return e
 }
 
-func (c *Ctx) Synchronize() error { return err(C.wvg_synchronize(c.h)) }
+func (c *Ctx) Synchronize() error {
+	defer pin(c)()
+	return err(C.wvg_synchronize(c.h))
+}
 
 // MatchHostDistancer: on AMX + AVX-512 hosts Weaviate's init() picks l2_512 /
 // dot_512 (D/l2_amd64.go:19-25, D/dot_product_amd64.go:19-25); the GPU then
 // follows the same reduction order so distances stay bit-identical.
 func (c *Ctx) MatchHostDistancer() error {
+	defer pin(c)()
 	order := C.WVG_ORDER_AVX256
 	if cpu.X86.HasAVX512 && cpu.X86.HasAMXBF16 {
 		order = C.WVG_ORDER_AVX512
@@ -196,6 +241,7 @@ type HostBuffer struct {
 }
 
 func (c *Ctx) HostAlloc(bytes uint64) (*HostBuffer, error) {
+	defer pin(c)()
 	var p unsafe.Pointer
 	if e := err(C.wvg_host_alloc(c.h, C.uint64_t(bytes), &p)); e != nil {
 		return nil, e
@@ -206,6 +252,7 @@ func (c *Ctx) HostAlloc(bytes uint64) (*HostBuffer, error) {
 func (b *HostBuffer) Float32s() []float32 { return unsafe.Slice((*float32)(b.p), b.n/4) }
 
 func (b *HostBuffer) Free() error {
+	defer pin(b)()
 	if b.p == nil {
 		return nil
 	}
@@ -216,6 +263,7 @@ func (b *HostBuffer) Free() error {
 
 // MeasureHBMRead: the device's streaming-read rate in GB/s (roofline ceiling).
 func (c *Ctx) MeasureHBMRead(bytes uint64, reps uint32) (float64, error) {
+	defer pin(c)()
 	var gbps C.double
 	if e := err(C.wvg_measure_hbm_read(c.h, C.uint64_t(bytes), C.uint32_t(reps), &gbps)); e != nil {
 		return 0, e
@@ -225,13 +273,72 @@ func (c *Ctx) MeasureHBMRead(bytes uint64, reps uint32) (float64, error) {
 
 // ProfileStart / ProfileStop: per-dispatch scan-kernel time for the
 // vector_index_durations_ms metric (usecases/monitoring/prometheus.go:292).
-func (c *Ctx) ProfileStart() error { return err(C.wvg_profile_start(c.h)) }
+func (c *Ctx) ProfileStart() error {
+	defer pin(c)()
+	return err(C.wvg_profile_start(c.h))
+}
 
 func (c *Ctx) ProfileStop() (ms float64, launches uint64, e error) {
+	defer pin(c)()
 	var t C.double
 	var n C.uint64_t
 	e = err(C.wvg_profile_stop(c.h, &t, &n))
 	return float64(t), uint64(n), e
+}
+
+// ---- device memory and streams (for the device-resident serving loop) ----------
+
+// DeviceAlloc returns bytes of HBM on the context's GPU (zero-filled when zero:
+// a search workspace must be).  Free it with DeviceFree once the work using it
+// has finished (StreamSynchronize).
+func (c *Ctx) DeviceAlloc(bytes uint64, zero bool) (unsafe.Pointer, error) {
+	defer pin(c)()
+	var p unsafe.Pointer
+	z := C.int(0)
+	if zero {
+		z = 1
+	}
+	if e := err(C.wvg_device_alloc(c.h, C.uint64_t(bytes), z, &p)); e != nil {
+		return nil, e
+	}
+	return p, nil
+}
+
+func (c *Ctx) DeviceFree(p unsafe.Pointer) error {
+	defer pin(c)()
+	return err(C.wvg_device_free(c.h, p))
+}
+
+// NewStream creates a non-blocking HIP stream for DeviceBuffers.Stream.
+func (c *Ctx) NewStream() (unsafe.Pointer, error) {
+	defer pin(c)()
+	var s unsafe.Pointer
+	if e := err(C.wvg_stream_create(c.h, &s)); e != nil {
+		return nil, e
+	}
+	return s, nil
+}
+
+func (c *Ctx) StreamDestroy(s unsafe.Pointer) error {
+	defer pin(c)()
+	return err(C.wvg_stream_destroy(c.h, s))
+}
+
+func (c *Ctx) StreamSynchronize(s unsafe.Pointer) error {
+	defer pin(c)()
+	return err(C.wvg_stream_synchronize(c.h, s))
+}
+
+// CopyToDevice / CopyFromDevice copy between a Go slice and HBM on stream s;
+// they return when the copy is done (the slice is not retained).
+func (c *Ctx) CopyToDevice(dst unsafe.Pointer, src []float32, s unsafe.Pointer) error {
+	defer pin(c)()
+	return err(C.wvg_memcpy_h2d(c.h, dst, unsafe.Pointer(f32p(src)), C.uint64_t(4*len(src)), s))
+}
+
+func (c *Ctx) CopyFromDevice(dst []byte, src unsafe.Pointer, s unsafe.Pointer) error {
+	defer pin(c)()
+	return err(C.wvg_memcpy_d2h(c.h, unsafe.Pointer(u8p(dst)), src, C.uint64_t(len(dst)), s))
 }
 
 // ---- corpus --------------------------------------------------------------------
@@ -247,32 +354,42 @@ type Corpus struct {
 }
 
 func (c *Ctx) NewCorpus(kind, metric, dims int, idBase, capacity uint64) (*Corpus, error) {
+	defer pin(c)()
 	var h *C.wvg_corpus
 	if e := err(C.wvg_corpus_create(c.h, C.int(kind), C.int(metric), C.uint32_t(dims), C.uint64_t(idBase),
 		C.uint64_t(capacity), &h)); e != nil {
 		return nil, e
 	}
 	x := &Corpus{h: h, ctx: c, kind: kind, dims: dims}
-	runtime.SetFinalizer(x, func(x *Corpus) { _ = x.Close() }) // backstop; owners call Close
+	atomic.AddInt64(&c.corpora, 1)
+	// backstop for a leaked corpus (owners call Close): it runs only once x is
+	// unreachable, i.e. after every method's pin has released it, and the
+	// context cannot have been closed while x was open
+	runtime.SetFinalizer(x, func(x *Corpus) { _ = x.Close() })
 	return x, nil
 }
 
 // Close: flat.Drop / Shutdown.
 func (x *Corpus) Close() error {
+	defer pin(x)()
 	if x.h == nil {
 		return nil
 	}
 	e := err(C.wvg_corpus_destroy(x.h))
 	x.h = nil
+	atomic.AddInt64(&x.ctx.corpora, -1)
+	runtime.SetFinalizer(x, nil)
 	return e
 }
 
 // Reserve: cache.Grow (V/cache/sharded_lock_cache.go:251), contents kept.
 func (x *Corpus) Reserve(capacity uint64) error {
+	defer pin(x)()
 	return err(C.wvg_corpus_reserve(x.h, C.uint64_t(capacity)))
 }
 
 func (x *Corpus) Info() (count, highWater, capacity uint64, e error) {
+	defer pin(x)()
 	var a, b, c C.uint64_t
 	e = err(C.wvg_corpus_info(x.h, &a, &b, &c))
 	return uint64(a), uint64(b), uint64(c), e
@@ -281,6 +398,7 @@ func (x *Corpus) Info() (count, highWater, capacity uint64, e error) {
 // Add: flat.Add / AddBatch (V/flat/index.go:247-274); flat is len(ids)*dims
 // float32 (normalized inside for cosine, BQ / PQ encoded on the device).
 func (x *Corpus) Add(ids []uint64, flat []float32) error {
+	defer pin(x)()
 	if len(ids) == 0 {
 		return nil
 	}
@@ -293,6 +411,7 @@ func (x *Corpus) Add(ids []uint64, flat []float32) error {
 // AddCodes stores rows as the LSM holds them (F32 rows already normalized at
 // Add, BQ uint64 words, PQ m bytes): restores, and the BQ / PQ caches.
 func (x *Corpus) AddCodes(ids []uint64, codes unsafe.Pointer) error {
+	defer pin(x)()
 	if len(ids) == 0 {
 		return nil
 	}
@@ -302,6 +421,7 @@ func (x *Corpus) AddCodes(ids []uint64, codes unsafe.Pointer) error {
 // LoadKV: PostStartup bulk load straight from the LSM cursor's pairs
 // (V/flat/index.go:640-681): keys 8-byte big-endian docIDs, values the rows.
 func (x *Corpus) LoadKV(keys, values []byte, n int) error {
+	defer pin(x)()
 	if n == 0 {
 		return nil
 	}
@@ -310,6 +430,7 @@ func (x *Corpus) LoadKV(keys, values []byte, n int) error {
 
 // Delete: flat.Delete (V/flat/index.go:276-295).
 func (x *Corpus) Delete(ids ...uint64) error {
+	defer pin(x)()
 	if len(ids) == 0 {
 		return nil
 	}
@@ -318,6 +439,7 @@ func (x *Corpus) Delete(ids ...uint64) error {
 
 // Get: flat.vectorById (V/flat/index.go:401-407) of an F32 corpus.
 func (x *Corpus) Get(id uint64) ([]float32, error) {
+	defer pin(x)()
 	out := make([]float32, x.dims)
 	if e := err(C.wvg_corpus_get(x.h, C.uint64_t(id), unsafe.Pointer(&out[0]))); e != nil {
 		return nil, e
@@ -328,6 +450,7 @@ func (x *Corpus) Get(id uint64) ([]float32, error) {
 // GetBatch: vectorById for many ids of an F32 corpus; ok[i] == false where
 // ids[i] is not live.
 func (x *Corpus) GetBatch(ids []uint64) ([]float32, []bool, error) {
+	defer pin(x)()
 	out := make([]float32, len(ids)*x.dims)
 	ok := make([]uint8, len(ids))
 	if len(ids) == 0 {
@@ -342,6 +465,7 @@ func (x *Corpus) GetBatch(ids []uint64) ([]float32, []bool, error) {
 
 // SetCodebook: the PQ encoders' centers [m][ks][dims/m] (CH/kmeans.go:85-93).
 func (x *Corpus) SetCodebook(centers []float32, m, ks int) error {
+	defer pin(x)()
 	if e := err(C.wvg_pq_set_codebook(x.h, f32p(centers), C.uint32_t(m), C.uint32_t(ks))); e != nil {
 		return e
 	}
@@ -350,7 +474,10 @@ func (x *Corpus) SetCodebook(centers []float32, m, ks int) error {
 }
 
 // EncodeFrom: the PQ preload of a resident float corpus (V/hnsw/compress.go:98-104).
-func (x *Corpus) EncodeFrom(f32 *Corpus) error { return err(C.wvg_pq_encode_corpus(x.h, f32.h)) }
+func (x *Corpus) EncodeFrom(f32 *Corpus) error {
+	defer pin(x, f32)()
+	return err(C.wvg_pq_encode_corpus(x.h, f32.h))
+}
 
 func bools(b []uint8) []bool {
 	out := make([]bool, len(b))
@@ -421,6 +548,7 @@ func (x *Corpus) Search(q []float32, k int, allow helpers.AllowList) ([]uint64, 
 
 // SearchBatch: nq queries (qs is nq*dims floats) in one call.
 func (x *Corpus) SearchBatch(qs []float32, nq, k int, allow helpers.AllowList) (*Results, error) {
+	defer pin(x)()
 	r := emptyResults(nq, k)
 	if nq == 0 || k == 0 {
 		return r, nil
@@ -443,6 +571,7 @@ func (x *Corpus) SearchBatch(qs []float32, nq, k int, allow helpers.AllowList) (
 // float rows resident in f32 (same dims / idBase / metric as x).
 func (x *Corpus) SearchBQRescore(f32 *Corpus, qs []float32, nq, k, rescoreLimit int,
 	allow helpers.AllowList) (*Results, error) {
+	defer pin(x, f32)()
 	r := emptyResults(nq, k)
 	if nq == 0 || k == 0 {
 		return r, nil
@@ -463,6 +592,7 @@ func (x *Corpus) SearchBQRescore(f32 *Corpus, qs []float32, nq, k, rescoreLimit 
 // 85-151) in one device pass; the buffer grows if the count exceeds it.
 func (x *Corpus) SearchByDistance(q []float32, target float32, maxLimit int64,
 	allow helpers.AllowList) ([]uint64, []float32, error) {
+	defer pin(x)()
 	words, ok := allowBitmap(allow)
 	if !ok {
 		return nil, nil, nil
@@ -487,6 +617,7 @@ func (x *Corpus) SearchByDistance(q []float32, target float32, maxLimit int64,
 // (V/flat/index.go:531-591 as written: one window of `window` results).
 func (x *Corpus) SearchByDistanceWindow(q []float32, target float32, window int,
 	allow helpers.AllowList) ([]uint64, []float32, error) {
+	defer pin(x)()
 	if window == 0 {
 		return nil, nil, nil
 	}
@@ -507,6 +638,7 @@ func (x *Corpus) SearchByDistanceWindow(q []float32, target float32, window int,
 // DistanceByIDs: CompressorDistancer.DistanceToNode for a candidate batch
 // (CH/compression.go:306-325; the HNSW rescore, V/hnsw/search.go:564-581).
 func (x *Corpus) DistanceByIDs(q []float32, ids []uint64) ([]float32, []bool, error) {
+	defer pin(x)()
 	d := make([]float32, len(ids))
 	ok := make([]uint8, len(ids))
 	if len(ids) == 0 {
@@ -522,6 +654,7 @@ func (x *Corpus) DistanceByIDs(q []float32, ids []uint64) ([]float32, []bool, er
 // DistanceByIDsBatch: the rescore step of many concurrent searches in one
 // launch; qs is nq*dims floats, lists[q] query q's candidates.
 func (x *Corpus) DistanceByIDsBatch(qs []float32, lists [][]uint64) ([][]float32, [][]bool, error) {
+	defer pin(x)()
 	nq := len(lists)
 	if nq == 0 {
 		return nil, nil, nil
@@ -552,6 +685,7 @@ func (x *Corpus) DistanceByIDsBatch(qs []float32, lists [][]uint64) ([][]float32
 // over host rows fetched from the LSM (rows is len(ids)*dims floats; q
 // normalized by the caller for cosine, as index.go:352 does).
 func (c *Ctx) Rescore(metric int, q, rows []float32, ids []uint64, dims, k int) ([]uint64, []float32, error) {
+	defer pin(c)()
 	outIDs := make([]uint64, k)
 	outD := make([]float32, k)
 	if k == 0 || len(ids) == 0 {
@@ -568,7 +702,7 @@ func (c *Ctx) Rescore(metric int, q, rows []float32, ids []uint64, dims, k int) 
 // ---- device-resident serving loop (queries and results in HBM) ------------------
 
 // DeviceBuffers are HBM pointers owned by the caller (e.g. a serving loop's
-// pools); stream is a hipStream_t or nil.
+// pools, from Ctx.DeviceAlloc); Stream is a Ctx.NewStream stream or nil.
 type DeviceBuffers struct {
 	Queries   unsafe.Pointer // float [nq][dims], normalized for cosine
 	IDs       unsafe.Pointer // uint64 [nq][k]
@@ -580,17 +714,20 @@ type DeviceBuffers struct {
 }
 
 func (x *Corpus) WorkspaceSize(nq, k int) uint64 {
+	defer pin(x)()
 	return uint64(C.wvg_search_workspace_size(x.h, C.uint32_t(nq), C.uint32_t(k)))
 }
 
 // SearchDevice: nq searches on the device, asynchronous on b.Stream.
 func (x *Corpus) SearchDevice(b DeviceBuffers, nq, k int) error {
+	defer pin(x)()
 	return err(C.wvg_search_device(x.h, (*C.float)(b.Queries), C.uint32_t(nq), C.uint32_t(k), (*C.uint64_t)(b.IDs),
 		(*C.float)(b.Dists), (*C.uint32_t)(b.Counts), b.Workspace, C.size_t(b.WsBytes), b.Stream))
 }
 
 // SearchDevicePipelined: nq single-query scans in one query-stream launch.
 func (x *Corpus) SearchDevicePipelined(b DeviceBuffers, nq, k int) error {
+	defer pin(x)()
 	return err(C.wvg_search_device_pipelined(x.h, (*C.float)(b.Queries), C.uint32_t(nq), C.uint32_t(k),
 		(*C.uint64_t)(b.IDs), (*C.float)(b.Dists), (*C.uint32_t)(b.Counts), b.Workspace, C.size_t(b.WsBytes),
 		b.Stream))
@@ -598,6 +735,7 @@ func (x *Corpus) SearchDevicePipelined(b DeviceBuffers, nq, k int) error {
 
 // CheckDevice surfaces a device-side failure of earlier device searches.
 func (c *Ctx) CheckDevice(workspace, stream unsafe.Pointer) error {
+	defer pin(c)()
 	return err(C.wvg_search_device_check(c.h, workspace, stream))
 }
 
@@ -606,11 +744,13 @@ func (c *Ctx) CheckDevice(workspace, stream unsafe.Pointer) error {
 func PackedBytes(nq, k int) uint64 { return uint64(C.wvg_topk_packed_bytes(C.uint32_t(nq), C.uint32_t(k))) }
 
 func (c *Ctx) MergePacked(packed unsafe.Pointer, nq, nlists, kIn, k int, out DeviceBuffers) error {
+	defer pin(c)()
 	return err(C.wvg_topk_merge_packed(c.h, packed, C.uint32_t(nq), C.uint32_t(nlists), C.uint32_t(kIn),
 		C.uint32_t(k), (*C.uint64_t)(out.IDs), (*C.float)(out.Dists), (*C.uint32_t)(out.Counts), out.Stream))
 }
 
 func (c *Ctx) MergeLists(dists, ids unsafe.Pointer, nq, nlists, kIn, k int, out DeviceBuffers) error {
+	defer pin(c)()
 	return err(C.wvg_topk_merge_device(c.h, (*C.float)(dists), (*C.uint64_t)(ids), C.uint32_t(nq),
 		C.uint32_t(nlists), C.uint32_t(kIn), C.uint32_t(k), (*C.uint64_t)(out.IDs), (*C.float)(out.Dists),
 		(*C.uint32_t)(out.Counts), out.Stream))
@@ -620,6 +760,7 @@ func (c *Ctx) MergeLists(dists, ids unsafe.Pointer, nq, nlists, kIn, k int, out 
 
 // BatchDist: Provider.SingleDist of q against n rows (D/provider.go:14-20).
 func (c *Ctx) BatchDist(metric int, q, rows []float32, dims int) ([]float32, error) {
+	defer pin(c)()
 	n := len(rows) / dims
 	out := make([]float32, n)
 	if n == 0 {
@@ -634,6 +775,7 @@ func (c *Ctx) BatchDist(metric int, q, rows []float32, dims int) ([]float32, err
 
 // Normalize: distancer.Normalize of n rows (D/normalize.go:16-32).
 func (c *Ctx) Normalize(rows []float32, dims int) ([]float32, error) {
+	defer pin(c)()
 	out := make([]float32, len(rows))
 	n := len(rows) / dims
 	if n == 0 {
@@ -647,6 +789,7 @@ func (c *Ctx) Normalize(rows []float32, dims int) ([]float32, error) {
 
 // BQEncode: BinaryQuantizer.Encode (CH/binary_quantization.go:32-45).
 func (c *Ctx) BQEncode(rows []float32, dims int) ([]uint64, error) {
+	defer pin(c)()
 	n := len(rows) / dims
 	w := (dims + 63) / 64
 	out := make([]uint64, n*w)
@@ -661,6 +804,7 @@ func (c *Ctx) BQEncode(rows []float32, dims int) ([]uint64, error) {
 
 // BQDistance: DistanceBetweenCompressedVectors of q against n codes (:47-56).
 func (c *Ctx) BQDistance(q, codes []uint64) ([]float32, error) {
+	defer pin(c)()
 	w := len(q)
 	if w == 0 {
 		return nil, errors.New("empty code")
@@ -679,6 +823,7 @@ func (c *Ctx) BQDistance(q, codes []uint64) ([]float32, error) {
 
 // PQEncode: ProductQuantizer.Encode of host rows (CH/product_quantization.go:420-426).
 func (c *Ctx) PQEncode(centers []float32, m, ks int, rows []float32, dims int) ([]byte, error) {
+	defer pin(c)()
 	n := len(rows) / dims
 	out := make([]byte, n*m)
 	if n == 0 {
@@ -693,6 +838,7 @@ func (c *Ctx) PQEncode(centers []float32, m, ks int, rows []float32, dims int) (
 
 // PQLUT: DistanceLookUpTable of one query (CH/product_quantization.go:62-104).
 func (c *Ctx) PQLUT(metric int, centers []float32, m, ks, dims int, q []float32) ([]float32, error) {
+	defer pin(c)()
 	out := make([]float32, m*ks)
 	if e := err(C.wvg_pq_lut(c.h, C.int(metric), f32p(centers), C.uint32_t(m), C.uint32_t(ks), C.uint32_t(dims),
 		f32p(q), f32p(out))); e != nil {
@@ -703,6 +849,7 @@ func (c *Ctx) PQLUT(metric int, centers []float32, m, ks, dims int, q []float32)
 
 // PQADC: PQDistancer.Distance of n codes against a LUT (:352-361).
 func (c *Ctx) PQADC(metric int, lut []float32, m, ks int, codes []byte) ([]float32, error) {
+	defer pin(c)()
 	n := len(codes) / m
 	out := make([]float32, n)
 	if n == 0 {
@@ -718,6 +865,7 @@ func (c *Ctx) PQADC(metric int, lut []float32, m, ks int, codes []byte) ([]float
 // PQFit: ProductQuantizer.Fit (CH/product_quantization.go:372-418); centers
 // [m][ks][dims/m] for SetCodebook.
 func (c *Ctx) PQFit(data []float32, dims, m, ks int, trainingLimit, seed uint64) ([]float32, error) {
+	defer pin(c)()
 	n := len(data) / dims
 	if n == 0 {
 		return nil, errors.New("not enough data to fit kmeans")
@@ -732,6 +880,7 @@ func (c *Ctx) PQFit(data []float32, dims, m, ks int, trainingLimit, seed uint64)
 
 // PQGlobalDistances: buildGlobalDistances (CH/product_quantization.go:236-251).
 func (c *Ctx) PQGlobalDistances(metric int, centers []float32, m, ks, dims int) ([]float32, error) {
+	defer pin(c)()
 	out := make([]float32, m*ks*ks)
 	if e := err(C.wvg_pq_global_distances(c.h, C.int(metric), f32p(centers), C.uint32_t(m), C.uint32_t(ks),
 		C.uint32_t(dims), f32p(out))); e != nil {
@@ -742,6 +891,7 @@ func (c *Ctx) PQGlobalDistances(metric int, centers []float32, m, ks, dims int) 
 
 // PQSDC: DistanceBetweenCompressedVectors of code x against n codes (:297-311).
 func (c *Ctx) PQSDC(metric int, table []float32, m, ks int, x, codes []byte) ([]float32, error) {
+	defer pin(c)()
 	n := len(codes) / m
 	out := make([]float32, n)
 	if n == 0 {

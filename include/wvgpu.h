@@ -28,7 +28,9 @@
 extern "C" {
 #endif
 
-#define WVG_ABI_VERSION 1
+/* 2: wvg_options gained `coalesce` (round 4) and the device-memory / stream
+ * entry points were added (wvg_device_alloc ... wvg_memcpy_d2h). */
+#define WVG_ABI_VERSION 2
 
 #define WVG_OK 0
 #define WVG_ERR_INVALID -1       /* bad argument (null, k < 0 analogue, bad kind) */
@@ -100,6 +102,24 @@ int wvg_synchronize(wvg_ctx *ctx);
  * call's staging).  Free with wvg_host_free on the same context. */
 int wvg_host_alloc(wvg_ctx *ctx, uint64_t bytes, void **out);
 int wvg_host_free(wvg_ctx *ctx, void *p);
+/* Device memory and streams of the context's GPU for the device-pointer
+ * entry points below (wvg_search_device*, wvg_topk_merge_*), so a caller
+ * without a HIP binding of its own (the Go backend) can hold queries,
+ * results and workspaces in HBM: wvg_device_alloc returns `bytes` of HBM,
+ * zero-filled when `zero` != 0 (a search workspace must be); free it with
+ * wvg_device_free after the work using it has finished (wvg_stream_synchronize).
+ * wvg_stream_create makes a non-blocking stream (a hipStream_t) for `stream`
+ * arguments.  wvg_memcpy_h2d / _d2h copy on `stream` and return when the copy
+ * is complete (so `src` / `dst` host memory may be a Go slice); `stream` NULL
+ * = the default stream.  Replaces the cgo-side HIP plumbing a serving loop
+ * would need (adapters/repos/db/vector_index.go:24-45 callers hold no HIP). */
+int wvg_device_alloc(wvg_ctx *ctx, uint64_t bytes, int zero, void **out);
+int wvg_device_free(wvg_ctx *ctx, void *p);
+int wvg_stream_create(wvg_ctx *ctx, void **out);
+int wvg_stream_destroy(wvg_ctx *ctx, void *stream);
+int wvg_stream_synchronize(wvg_ctx *ctx, void *stream);
+int wvg_memcpy_h2d(wvg_ctx *ctx, void *d_dst, const void *src, uint64_t bytes, void *stream);
+int wvg_memcpy_d2h(wvg_ctx *ctx, void *dst, const void *d_src, uint64_t bytes, void *stream);
 /* The reduction order of the fp32 distances (l2 / dot / cosine), i.e. which
  * of the reference's SIMD kernels the results must match bit for bit: its
  * init() picks l2_512 / dot_512 on hosts with AMX-BF16 and AVX-512, else

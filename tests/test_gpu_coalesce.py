@@ -121,6 +121,35 @@ def test_coalesced_results_match_oracle(ctx, orc):
     c.destroy()
 
 
+def test_back_to_back_single_queries_on_one_slot(ctx, orc):
+    """The interleaving behind round 4's polled-path failure (What's
+    weak #1): one thread = one stream slot, so consecutive single-query calls
+    reuse the slot's host result buffer, its partial lists and its arrival
+    counter, and the previous call's complete result sits in that buffer when
+    the next call starts.  Each call's results arrive as tagged records
+    (StreamJob::records); a call may only return entries carrying its own tag.
+    Alternating queries with 8-query batches (other partial lists on the slot)
+    in between, every result must be its own query's oracle top-k -- never the
+    previous call's."""
+    n, d, k = 5000, 64, 10
+    rows = orc.synth_rows(708, 0, n, d, 0)
+    c = Corpus(ctx, KIND_F32, METRIC_L2, d, n)
+    c.upsert(np.arange(n, dtype=np.uint64), rows)
+    lib = _lib.load()
+    qs = np.ascontiguousarray(orc.synth_rows(709, 0, 7, d, 0))
+    want = [orc.lex_topk(orc.dist_all(0, q, rows), np.arange(n, dtype=np.uint64), k) for q in qs]
+    for r in range(700):
+        qi = (r * 3) % len(qs)
+        kk = k if r % 5 else 7  # a shorter result than the slot's previous one
+        gi, gd, gc = one_search(lib, c, qs[qi], kk)
+        assert gc == kk, r
+        assert np.array_equal(gi, want[qi][0][:kk]), (r, qi)
+        assert np.array_equal(gd.view(np.uint32), want[qi][1][:kk].view(np.uint32)), (r, qi)
+        if r % 4 == 3:
+            c.search(qs[:5], k)
+    c.destroy()
+
+
 def test_coalesced_calls_with_concurrent_writes(ctx, orc):
     """Single-query searches keep coalescing while another thread upserts and
     deletes (writers take the corpus exclusively; queued searches wait, none
@@ -170,4 +199,99 @@ def test_coalesced_calls_with_concurrent_writes(ctx, orc):
         wi, wd = orc.lex_topk(orc.dist_all(0, qs[qi], rows[live.astype(np.int64)]), live, k)
         assert np.array_equal(gi, wi)
         assert np.array_equal(gd.view(np.uint32), wd.view(np.uint32))
+    c.destroy()
+
+
+@pytest.mark.parametrize("metric,d", [(METRIC_L2, 128), (METRIC_COSINE, 96)])
+def test_filtered_calls_coalesce_equal_serial(ctx, orc, metric, d):
+    """Filtered single queries (every Weaviate query with a where-filter carries
+    its own allow list: adapters/repos/db/shard_read.go:341, the scan
+    restriction V/flat/index.go:423-449) join coalesced batches too: one
+    co-scheduled K1 launch over the union of their allow windows, each query
+    masked by its own (ScanArgs::allow_qstride).  16 threads with mixed lists
+    -- 10 %, 1 %, a narrow id range, a single id, an empty list, none -- and
+    mixed k must get exactly what serial calls return."""
+    from weaviate_amd.device import allow_bitmap
+
+    n = 30_000
+    c = make_corpus(ctx, orc, KIND_F32, metric, n, d)
+    lib = _lib.load()
+    rng = np.random.default_rng(710)
+    nq = 96
+    qs = np.ascontiguousarray(orc.synth_rows(711, 0, nq, d, 0))
+    allows = []
+    for i in range(nq):
+        kind = i % 6
+        if kind == 0:
+            allows.append(allow_bitmap(np.flatnonzero(rng.random(n) < 0.10), n))
+        elif kind == 1:
+            allows.append(allow_bitmap(np.flatnonzero(rng.random(n) < 0.01), n))
+        elif kind == 2:
+            lo = int(rng.integers(0, n - 3000))
+            allows.append(allow_bitmap(range(lo, lo + 2500), n))
+        elif kind == 3:
+            allows.append(allow_bitmap([int(rng.integers(0, n))], n))
+        elif kind == 4:
+            allows.append(np.zeros((n + 63) // 64, np.uint64))  # non-nil, empty: no results
+        else:
+            allows.append(None)
+    ks = [(10, 3, 10, 64, 10, 1)[(i // 6) % 6] for i in range(nq)]
+
+    def call(i):
+        ids = np.empty(ks[i], np.uint64)
+        dd = np.empty(ks[i], np.float32)
+        cnt = np.empty(1, np.uint32)
+        a = allows[i]
+        _lib.check(lib.wvg_search(c.handle, fptr(qs[i]), 1, ks[i], u64ptr(a) if a is not None else None,
+                                  0 if a is None else len(a), u64ptr(ids), fptr(dd), u32ptr(cnt)))
+        return ids, dd, int(cnt[0])
+
+    serial = [call(i) for i in range(nq)]
+    for rep in range(3):
+        out = [None] * nq
+        errs = []
+        start = threading.Barrier(16)
+
+        def worker(t):
+            try:
+                start.wait()
+                for i in range(t, nq, 16):
+                    out[i] = call(i)
+            except Exception as e:  # noqa: BLE001
+                errs.append(e)
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+        assert not errs, errs
+        for i in range(nq):
+            si, sd, sc = serial[i]
+            gi, gd, gc = out[i]
+            assert gc == sc, (rep, i)
+            assert np.array_equal(gi[:sc], si[:sc]), (rep, i)
+            assert np.array_equal(gd[:sc].view(np.uint32), sd[:sc].view(np.uint32)), (rep, i)
+    # and the serial results are the oracle's: the filtered lexicographic top-k
+    rows = orc.synth_rows(701, 0, n, d, 0)
+    live = np.ones(n, bool)
+    live[np.arange(5, n, 97)] = False
+    om = 2 if metric == METRIC_COSINE else 0
+    for i in range(0, nq, 7):
+        a = allows[i]
+        ok = live.copy()
+        if a is not None:
+            bitsv = np.unpackbits(a.view(np.uint8), bitorder="little")[:n].astype(bool)
+            ok &= bitsv
+        ids = np.flatnonzero(ok).astype(np.uint64)
+        want = min(ks[i], len(ids))
+        assert serial[i][2] == want
+        if want:
+            r = rows[ids.astype(np.int64)]
+            q = qs[i]
+            if om == 2:
+                r = orc.normalize_rows(r)
+                q = orc.normalize(q)
+            wi, wd = orc.lex_topk(orc.dist_all(om, q, r), ids, ks[i])
+            assert np.array_equal(serial[i][0][:want], wi[:want]), i
     c.destroy()

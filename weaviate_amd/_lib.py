@@ -26,6 +26,7 @@ WVG_ERR_CAPACITY = -7
 KIND_F32, KIND_BQ, KIND_PQ = 0, 1, 2
 METRIC_L2, METRIC_DOT, METRIC_COSINE, METRIC_MANHATTAN, METRIC_HAMMING = 0, 1, 2, 3, 4
 ORDER_AVX256, ORDER_AVX512 = 0, 1  # reference SIMD kernel whose reduction order distances follow
+ABI_VERSION = 2  # WVG_ABI_VERSION of include/wvgpu.h this binding follows
 METRIC_BY_NAME = {"l2-squared": METRIC_L2, "dot": METRIC_DOT, "cosine": METRIC_COSINE,
                   "cosine-dot": METRIC_COSINE, "manhattan": METRIC_MANHATTAN, "hamming": METRIC_HAMMING}
 
@@ -50,6 +51,13 @@ SIGNATURES = {
     "wvg_synchronize": (c_int, [c_void_p]),
     "wvg_host_alloc": (c_int, [c_void_p, c_uint64, POINTER(c_void_p)]),
     "wvg_host_free": (c_int, [c_void_p, c_void_p]),
+    "wvg_device_alloc": (c_int, [c_void_p, c_uint64, c_int, POINTER(c_void_p)]),
+    "wvg_device_free": (c_int, [c_void_p, c_void_p]),
+    "wvg_stream_create": (c_int, [c_void_p, POINTER(c_void_p)]),
+    "wvg_stream_destroy": (c_int, [c_void_p, c_void_p]),
+    "wvg_stream_synchronize": (c_int, [c_void_p, c_void_p]),
+    "wvg_memcpy_h2d": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p]),
+    "wvg_memcpy_d2h": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p]),
     "wvg_set_distance_order": (c_int, [c_void_p, c_int]),
     "wvg_corpus_create": (c_int, [c_void_p, c_int, c_int, c_uint32, c_uint64, c_uint64, _P(c_void_p)]),
     "wvg_corpus_destroy": (c_int, [c_void_p]),
@@ -133,6 +141,8 @@ def load() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.wvg_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"{LIB_PATH}: ABI {lib.wvg_abi_version()}, this binding needs {ABI_VERSION}")
     _lib = lib
     return lib
 

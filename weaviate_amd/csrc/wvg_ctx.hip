@@ -250,12 +250,97 @@ int wvg_host_free(wvg_ctx *ctx, void *p)
     return WVG_OK;
 }
 
+int wvg_device_alloc(wvg_ctx *ctx, uint64_t bytes, int zero, void **out)
+{
+    if (!ctx || !out) return fail(WVG_ERR_INVALID, "null argument");
+    *out = nullptr;
+    if (bytes == 0) return WVG_OK;
+    WVG_HIP(hipSetDevice(ctx->device));
+    void *p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) return fail(WVG_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    if (zero) {
+        e = hipMemset(p, 0, bytes);  // synchronous: the memory is ready for any stream on return
+        if (e != hipSuccess) {
+            (void)hipFree(p);
+            return fail(WVG_ERR_DEVICE, std::string("hipMemset: ") + hipGetErrorString(e));
+        }
+    }
+    *out = p;
+    return WVG_OK;
+}
+
+int wvg_device_free(wvg_ctx *ctx, void *p)
+{
+    if (!ctx) return fail(WVG_ERR_INVALID, "null context");
+    if (!p) return WVG_OK;
+    WVG_HIP(hipSetDevice(ctx->device));
+    WVG_HIP(hipFree(p));
+    return WVG_OK;
+}
+
+int wvg_stream_create(wvg_ctx *ctx, void **out)
+{
+    if (!ctx || !out) return fail(WVG_ERR_INVALID, "null argument");
+    *out = nullptr;
+    WVG_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = nullptr;
+    WVG_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *out = (void *)s;
+    return WVG_OK;
+}
+
+int wvg_stream_destroy(wvg_ctx *ctx, void *stream)
+{
+    if (!ctx) return fail(WVG_ERR_INVALID, "null context");
+    if (!stream) return WVG_OK;
+    WVG_HIP(hipSetDevice(ctx->device));
+    WVG_HIP(hipStreamDestroy((hipStream_t)stream));
+    return WVG_OK;
+}
+
+int wvg_stream_synchronize(wvg_ctx *ctx, void *stream)
+{
+    if (!ctx) return fail(WVG_ERR_INVALID, "null context");
+    WVG_HIP(hipSetDevice(ctx->device));
+    WVG_HIP(hipStreamSynchronize((hipStream_t)stream));
+    return WVG_OK;
+}
+
+int wvg_memcpy_h2d(wvg_ctx *ctx, void *d_dst, const void *src, uint64_t bytes, void *stream)
+{
+    if (!ctx || ((!d_dst || !src) && bytes)) return fail(WVG_ERR_INVALID, "null argument");
+    if (!bytes) return WVG_OK;
+    WVG_HIP(hipSetDevice(ctx->device));
+    WVG_HIP(hipMemcpyAsync(d_dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
+    WVG_HIP(hipStreamSynchronize((hipStream_t)stream));  // src may be Go memory: not retained past the call
+    return WVG_OK;
+}
+
+int wvg_memcpy_d2h(wvg_ctx *ctx, void *dst, const void *d_src, uint64_t bytes, void *stream)
+{
+    if (!ctx || ((!dst || !d_src) && bytes)) return fail(WVG_ERR_INVALID, "null argument");
+    if (!bytes) return WVG_OK;
+    WVG_HIP(hipSetDevice(ctx->device));
+    WVG_HIP(hipMemcpyAsync(dst, d_src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
+    WVG_HIP(hipStreamSynchronize((hipStream_t)stream));
+    return WVG_OK;
+}
+
 #ifdef WVG_TOOLS
 // tools build: K3c counters [row-block epilogues (per wave), slow-path entries, insert calls, 0]
 int wvgx_screen_counters(uint64_t *out4, int reset)
 {
     if (!out4) return WVG_ERR_INVALID;
     wvg::screen_counters(out4, reset != 0);
+    return WVG_OK;
+}
+
+// tools build: single-query host path counters (wvg_search.hip, single_counters)
+int wvgx_single_counters(uint64_t *out4, int reset)
+{
+    if (!out4) return WVG_ERR_INVALID;
+    wvg::single_counters(out4, reset != 0);
     return WVG_OK;
 }
 

@@ -175,6 +175,7 @@ struct SearchPlan {
     bool cosched = false; // PQ batch: co-scheduled K8e (ScanArgs::cosched)
     bool empty = false;
     const uint64_t *allow_host = nullptr;  // the caller's allow words of tiles [tb, te), or null
+    uint64_t allow_qstride = 0;            // per-query allow windows (ScanArgs::allow_qstride)
     size_t allow_bytes() const { return allow_host ? (size_t)(te - tb) * 8 : 0; }
     size_t partial_keys(uint32_t nq, uint32_t k) const { return (size_t)nq * groups * k; }
     // K3b's per-row-range progress counters, then its per-query distance
@@ -196,11 +197,17 @@ uint32_t next_direction(wvg_corpus *c, uint32_t nq);
 int pq_dense(const wvg_corpus *c, const uint64_t *d_allow);
 void prepare_queries_host(const wvg_corpus *c, const float *queries, uint32_t nq, std::vector<float> &qf,
                           std::vector<uint64_t> &qb, uint32_t &qpitch);
+// A single host query merged in-launch straight into host memory (StreamJob::records).
+struct SingleOut {
+    uint4 *records = nullptr;  // [k + 1] in the slot's coherent host buffer, or null (ids / dists / counts)
+    uint32_t tag = 0;
+    bool legacy_poll = false;  // tools A/B: round 4's untagged layout in host memory
+};
 // sl: the calling host API's stream slot (a single query then merges in-launch), or null
 // qhost: the prepared host query of a single in-launch search (d_q null), passed in the kernel arguments
 int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t nq, uint32_t k, const uint64_t *d_allow,
                const SearchPlan &p, uint64_t *partials, uint64_t *ids, float *dists, uint32_t *counts, hipStream_t s,
-               StreamSlot *sl = nullptr, const float *qhost = nullptr, bool host_poll = false);
+               StreamSlot *sl = nullptr, const float *qhost = nullptr, const SingleOut *so = nullptr);
 void write_empty(uint32_t nq, uint32_t k, uint64_t *ids, float *dists, uint32_t *counts);
 int stage_queries(wvg_corpus *c, StreamSlot *sl, const float *queries, uint32_t nq, char *dst, uint32_t &qpitch,
                   float *d_lut_or_null, char *d_qtmp, Staging *st = nullptr);

@@ -41,6 +41,7 @@ struct StreamSlot {
     // launch starts from -- no per-call memset
     uint32_t *dctl = nullptr;
     uint32_t arrival_base = 0;
+    uint32_t tag = 0;  // the slot's last single-query call tag (StreamJob::tag; never 0)
     // and its results: written by the merge workgroup straight into coherent
     // (uncached, fine-grained) host memory -- no device-to-host copy per call
     void *hcoh = nullptr;
@@ -227,6 +228,8 @@ struct ScanArgs {
     const uint64_t *allow;     // allow bitmap window, may be null: allow[i] masks tile allow_t0 + i
     uint64_t allow_words;      // tiles covered by the window (tiles outside it are not allowed)
     uint64_t allow_t0;
+    uint64_t allow_qstride;    // K1: words between consecutive queries' windows (coalesced filtered
+                               // single queries, each with its own allow list); 0 = one shared window
     uint64_t id_base;
     uint64_t tile_begin, tile_end;
     uint32_t dim, nchunks;
@@ -279,7 +282,14 @@ struct StreamJob {
     uint64_t *ids;
     float *dists;
     uint32_t *counts;
-    uint32_t host_poll;  // counts live in host memory and the host polls them (see merge_lists_body)
+    // Single host queries: the results go to host memory as tagged 16-byte records
+    // [nq][k + 1] (entries {id lo, id hi, dist, tag}, then the header {count, tag}),
+    // ids / dists / counts unused.  GPU writes to host memory can become visible
+    // out of order (a later header before earlier entries), so the host accepts a
+    // result only when the header AND every entry carry its call's tag.
+    uint4 *records;
+    uint32_t tag;
+    uint32_t legacy_poll;  // tools A/B: round 4's layout (ids / dists, a release, then the polled count)
     // a single host query rides in the kernel arguments (ScanArgs::queries null):
     // no host-to-device copy (a blit dispatch + ~10 us of API time) per call
     alignas(16) float qin[STREAM_QIN_FLOATS];
@@ -303,6 +313,7 @@ bool screen_supported(uint32_t dim, int metric, uint32_t k);
 uint32_t screen_row_ranges(uint32_t nq, uint64_t ntiles, int num_cus);
 #ifdef WVG_TOOLS
 void screen_counters(uint64_t out[4], bool reset);
+void single_counters(uint64_t out[4], bool reset);
 #endif
 hipError_t launch_shadow_build(const float *tiled, uint32_t dim, uint64_t t0, uint64_t t1, void *shadow, float *norms,
                                uint32_t *nmax, hipStream_t s);
@@ -387,10 +398,10 @@ struct Tuning {
     int screen_pilot_gemm = 512;  // K3c/K3d: tiles of the K3b (exact fp32 MFMA) pilot, which replaces the K1
                                   // pilot (0 = the K1 pilot; A/B)
     int screen_variant = 0;  // batched screen kernel: 0 = K3d where it applies (d = 512, 768), 1 = K3c (A/B)
-    int single_path = 2;     // single-query host calls: bit 0 = query staged by copy instead of in the kernel
-                             // arguments, bit 1 = stream synchronization instead of polling the count.  2: polling
-                             // the count in coherent host memory returned stale or mixed results in about 1 of 1000
-                             // concurrent calls (tools/single_query_stress.py, profiles/r04/single_query_stress/)
+    int single_path = 0;     // single-query host calls: bit 0 = query staged by copy instead of in the kernel
+                             // arguments, bit 1 = stream synchronization instead of polling, bit 2 = round 4's
+                             // untagged layout (ids / dists + a polled count: returned the slot's previous result
+                             // in ~1 of 1000 concurrent calls, profiles/r04/single_query_stress/; A/B only)
     int screen_split = 1;    // K3c/K3d phases seeded from the earlier ones: 1 = up to three, 2 = two, 0 = one launch,
                              // 3 = doubling (r1, 2 r1, 4 r1, ...; A/B)
     int screen_seed = 3;     // K3c/K3d exact seeds (the exact k-th of the rescored k smallest lower bounds):

@@ -43,13 +43,14 @@ LaunchEvents &armed_events()
 // loads and the skip branch are scalar.
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
-// Per-tile mask of live, allowed rows (one 64-bit word per tile = one bit per lane).
-__device__ __forceinline__ uint64_t tile_mask(const ScanArgs &a, uint64_t t)
+// Per-tile mask of live, allowed rows (one 64-bit word per tile = one bit per lane);
+// qi: the query whose allow window applies (ScanArgs::allow_qstride).
+__device__ __forceinline__ uint64_t tile_mask(const ScanArgs &a, uint64_t t, uint32_t qi = 0)
 {
     uint64_t m = a.valid[t];
     if (a.allow) {
         uint64_t w = t - a.allow_t0;  // allow[0] is tile allow_t0's word
-        m &= w < a.allow_words ? a.allow[w] : 0ull;
+        m &= w < a.allow_words ? a.allow[(uint64_t)qi * a.allow_qstride + w] : 0ull;
     }
     return m;
 }
@@ -67,10 +68,13 @@ __device__ __forceinline__ void wave_range(const ScanArgs &a, int waves_per_grou
 
 // Phase-2 merge body for one query (see merge_keys_kernel): WAVES waves read
 // `nlists` ascending lists transposed, then tree-merge in LDS; wave 0 writes.
+// rec (host-read results, see StreamJob::records): entry i goes to rec[i] as ONE
+// 16-byte store {id lo, id hi, dist bits, tag}, then the header {count, tag}
+// at rec[k] -- the host accepts only entries carrying its call's tag.
 template <int E, int WAVES>
 __device__ __forceinline__ void merge_lists_body(const uint64_t *src, uint32_t nlists, uint32_t list_len, uint32_t k,
                                                  uint64_t id_base, uint64_t *ids, float *dists, uint32_t *count,
-                                                 bool sys_release = false)
+                                                 uint4 *rec = nullptr, uint32_t tag = 0, bool sys_release = false)
 {
     __shared__ uint64_t msh[WAVES][64 * E];
     const int lane = threadIdx.x & 63, wave = wave_id();
@@ -122,12 +126,24 @@ __device__ __forceinline__ void merge_lists_body(const uint64_t *src, uint32_t n
         const bool live = i < k && key != WVG_KEY_NONE;
         cnt += (uint32_t)__popcll(__ballot(live));
         if (i < k) {
-            ids[i] = live ? id_base + (key & 0xFFFFFFFFull) : WVG_KEY_NONE;
-            dists[i] = live ? wvg_unord_f32((uint32_t)(key >> 32)) : __builtin_inff();
+            const uint64_t id = live ? id_base + (key & 0xFFFFFFFFull) : WVG_KEY_NONE;
+            const float dv = live ? wvg_unord_f32((uint32_t)(key >> 32)) : __builtin_inff();
+            if (rec)
+                rec[i] = make_uint4((uint32_t)id, (uint32_t)(id >> 32), __float_as_uint(dv), tag);
+            else {
+                ids[i] = id;
+                dists[i] = dv;
+            }
         }
     }
-    // sys_release: the host polls *count (in host memory) instead of synchronizing the
-    // stream, so the wave's ids / dists stores are ordered before it at system scope
+    if (rec) {
+        if (lane == 0)
+            __hip_atomic_store(reinterpret_cast<uint64_t *>(rec + k), ((uint64_t)tag << 32) | cnt, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
+    // sys_release (tools A/B of the round-4 polled layout): a system-scope release between
+    // the ids / dists stores and the count the host polls
     if (sys_release) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     if (lane == 0 && count) *count = cnt;
 }
@@ -143,18 +159,18 @@ __device__ __forceinline__ uint64_t lane_key(uint64_t m, float dist, uint64_t t,
 // the order (lexicographic keys), only the cache state the next scan finds.
 template <int METRIC, int D, int E>
 __device__ __forceinline__ void scan_tiles(const ScanArgs &a, const float4 *q4, uint64_t t0, uint64_t t1,
-                                           WaveTopK<E> &tk, bool rev = false)
+                                           WaveTopK<E> &tk, bool rev = false, uint32_t qi = 0)
 {
     const int lane = threadIdx.x & 63;
     const float4 *data = reinterpret_cast<const float4 *>(a.data);
     const uint64_t n = t1 - t0;
     // passes i >= split load with the default policy (cache_tail256: only the tail of the pass)
     const uint64_t split = a.cache_tail256 ? n - ((n * a.cache_tail256) >> 8) : (a.plain ? 0 : n);
-    uint64_t m_next = n ? tile_mask(a, rev ? t1 - 1 : t0) : 0ull;
+    uint64_t m_next = n ? tile_mask(a, rev ? t1 - 1 : t0, qi) : 0ull;
     for (uint64_t i = 0; i < n; ++i) {
         const uint64_t t = rev ? t1 - 1 - i : t0 + i;
         const uint64_t m = m_next;
-        if (i + 1 < n) m_next = tile_mask(a, rev ? t - 1 : t + 1);  // scalar prefetch of the next mask
+        if (i + 1 < n) m_next = tile_mask(a, rev ? t - 1 : t + 1, qi);  // scalar prefetch of the next mask
         if (m == 0ull) continue;  // wave-uniform: nothing live/allowed in this tile
         const float4 *rp = data + (size_t)t * a.nchunks * 64 + lane;
         float r;
@@ -201,7 +217,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_kernel(ScanArgs a, u
     const float4 *q4 = reinterpret_cast<const float4 *>(a.queries) + (size_t)qi * (a.qpitch / 4);
     WaveTopK<E> tk;
     tk.init((int)a.k);
-    scan_tiles<METRIC, D, E>(a, q4, t0, t1, tk, a.reverse & 1u);
+    scan_tiles<METRIC, D, E>(a, q4, t0, t1, tk, a.reverse & 1u, qi);
     group_combine_store<E, SCAN_WAVES>(tk, partials + ((size_t)qi * G + rng) * a.k);
 }
 
@@ -342,12 +358,27 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_stream_kernel(ScanAr
                 // gave up: queries q.. get empty results (never stale ones) and
                 // the sticky status word tells wvg_search_device_check
                 if (threadIdx.x == 0) atomicOr(j.status, WVG_STATUS_MERGE_TIMEOUT);
-                fill_empty_body(j.ids, j.dists, j.counts, q, a.nq, a.k);
+                if (j.records) {  // tagged empty entries and count 0: the host reports the timeout
+                    for (uint32_t qq = q; qq < a.nq; qq++) {
+                        uint4 *r = j.records + (size_t)qq * (a.k + 1);
+                        for (uint32_t i = threadIdx.x; i < a.k; i += blockDim.x)
+                            r[i] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0x7F800000u, j.tag);
+                        __syncthreads();
+                        if (threadIdx.x == 0)
+                            __hip_atomic_store(reinterpret_cast<uint64_t *>(r + a.k), (uint64_t)j.tag << 32,
+                                               __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
+                } else {
+                    fill_empty_body(j.ids, j.dists, j.counts, q, a.nq, a.k);
+                }
                 return;
             }
             merge_lists_body<E, SCAN_WAVES>(j.partials + (size_t)q * G * a.k, G, a.k, a.k, a.id_base,
-                                            j.ids + (size_t)q * a.k, j.dists + (size_t)q * a.k,
-                                            j.counts ? j.counts + q : nullptr, j.host_poll != 0);
+                                            j.ids ? j.ids + (size_t)q * a.k : nullptr,
+                                            j.dists ? j.dists + (size_t)q * a.k : nullptr,
+                                            j.counts ? j.counts + q : nullptr,
+                                            j.records ? j.records + (size_t)q * (a.k + 1) : nullptr, j.tag,
+                                            j.legacy_poll != 0);
             __syncthreads();  // merge LDS reused by the next query
         }
         return;

@@ -324,7 +324,7 @@ static bool inlaunch_single(const wvg_corpus *c, uint32_t nq, const SearchPlan &
 
 int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t nq, uint32_t k, const uint64_t *d_allow,
                const SearchPlan &p, uint64_t *partials, uint64_t *ids, float *dists, uint32_t *counts, hipStream_t s,
-               StreamSlot *sl, const float *qhost, bool host_poll)
+               StreamSlot *sl, const float *qhost, const SingleOut *so)
 {
     ScanArgs a{};
     a.data = c->d_data;
@@ -332,6 +332,7 @@ int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t nq, uin
     a.allow = d_allow;
     a.allow_words = d_allow ? p.te - p.tb : 0;
     a.allow_t0 = p.tb;
+    a.allow_qstride = d_allow ? p.allow_qstride : 0;
     a.id_base = c->id_base;
     a.tile_begin = p.tb;
     a.tile_end = p.te;
@@ -363,7 +364,7 @@ int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t nq, uin
         SearchPlan pe = p;  // no shadow: the exact MFMA path over the same workspace
         pe.screen = false;
         pe.groups = p.exact_groups;
-        return run_search(c, d_q, qpitch, nq, k, d_allow, pe, partials, ids, dists, counts, s, sl);
+        return run_search(c, d_q, qpitch, nq, k, d_allow, pe, partials, ids, dists, counts, s, sl, nullptr, so);
     }
     if (sl && inlaunch_single(c, nq, p, d_allow != nullptr)) {
         // One query of a host call: the query-stream kernel, whose extra workgroup merges
@@ -384,7 +385,11 @@ int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t nq, uin
         j.ids = ids;
         j.dists = dists;
         j.counts = counts;
-        j.host_poll = host_poll ? 1u : 0u;
+        if (so) {
+            j.records = so->records;
+            j.tag = so->tag;
+            j.legacy_poll = so->legacy_poll ? 1u : 0u;
+        }
         if (!d_q) {  // the query in the kernel arguments
             if (!qhost || qpitch > STREAM_QIN_FLOATS) return fail(WVG_ERR_INVALID, "inline query missing or too long");
             std::memcpy(j.qin, qhost, (size_t)qpitch * 4);
@@ -518,6 +523,8 @@ using namespace wvg;
 struct wvg_search_request {
     const float *q;
     uint32_t k;
+    const uint64_t *allow = nullptr;  // the caller's allow list (helpers.AllowList bitmap), or null
+    uint64_t allow_words = 0;
     uint64_t *ids;
     float *dists;
     uint32_t *counts;
@@ -528,6 +535,73 @@ struct wvg_search_request {
 
 namespace wvg {
 
+#ifdef WVG_TOOLS
+// tools-build counters of the single-query host path (wvgx_single_counters):
+// [0] tagged calls, [1] calls whose header carried the tag before every entry did
+// (out-of-order arrival observed), [2] calls that fell back to a stream sync,
+// [3] round-4 layout: ids that changed after the polled count was seen
+static std::atomic<uint64_t> g_single[4];
+void single_counter(int i, bool hit)
+{
+    if (hit) g_single[i].fetch_add(1, std::memory_order_relaxed);
+}
+void single_counters(uint64_t out[4], bool reset)
+{
+    for (int i = 0; i < 4; i++) out[i] = reset ? g_single[i].exchange(0) : g_single[i].load();
+}
+#else
+inline void single_counter(int, bool) {}
+#endif
+
+// Waits until a single query's tagged records (StreamJob::records) have all
+// landed in host memory: the header and every one of the k entries carry this
+// call's tag.  GPU stores to host memory may become visible out of order -- the
+// round-4 layout (ids / dists, a system-scope release, then a count the host
+// polled) returned the slot's PREVIOUS result in ~1 of 1000 concurrent calls
+// (profiles/r04/single_query_stress/, profiles/r05/single_query/): the count had
+// landed, the ids of this call not yet.  Checking a tag in every 16-byte entry
+// makes acceptance independent of the arrival order.  sync: synchronize the
+// stream first (tools A/B); a poll that has not seen the tags after 50 ms (long
+// scans, a fault) synchronizes too, and the tags must then arrive within 1 s.
+static int wait_records(const SingleOut &so, uint32_t k, hipStream_t s, bool sync)
+{
+    const volatile uint32_t *w = reinterpret_cast<const volatile uint32_t *>(so.records);
+    bool early = false;
+    auto landed = [&]() {
+        if (w[4 * k + 1] != so.tag) return false;
+        for (uint32_t i = 0; i < k; i++)
+            if (w[4 * i + 3] != so.tag) {
+                early = true;
+                return false;
+            }
+        return true;
+    };
+    single_counter(0, true);
+    bool ok = false;
+    if (!sync) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t spin = 0;; spin++) {
+            if (landed()) {
+                ok = true;
+                break;
+            }
+            if ((spin & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50))
+                break;
+        }
+    }
+    if (!ok) {
+        single_counter(2, !sync);
+        WVG_HIP(hipStreamSynchronize(s));
+        const auto t0 = std::chrono::steady_clock::now();
+        while (!landed())
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1))
+                return fail(WVG_ERR_DEVICE, "single-query results did not arrive in host memory (tag mismatch)");
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    single_counter(1, early);
+    return WVG_OK;
+}
+
 // flat.SearchByVector for nq queries (the caller holds the corpus lock shared).
 static int search_batch(wvg_corpus *c, const float *queries, uint32_t nq, uint32_t k, const uint64_t *allow_bits,
                         uint64_t allow_words, uint64_t *out_ids, float *out_dists, uint32_t *out_counts);
@@ -537,6 +611,12 @@ static int search_batch(wvg_corpus *c, const float *queries, uint32_t nq, uint32
 // batches of >= mfma_min_queries go to the matrix cores.
 constexpr size_t COALESCE_MAX = 256;
 
+// Filtered single queries of one coalesced batch (F32): one co-scheduled K1
+// launch over the union of their allow windows, every query masked by its
+// own window (ScanArgs::allow_qstride).
+static int search_batch_filtered(wvg_corpus *c, const std::vector<wvg_search_request *> &batch, uint32_t k,
+                                 uint64_t *out_ids, float *out_dists, uint32_t *out_counts);
+
 // Runs one coalesced batch (same k) and hands every request its own rows of
 // the result; a failure is every request's failure.
 static void run_coalesced(wvg_corpus *c, const std::vector<wvg_search_request *> &batch, uint32_t k)
@@ -544,7 +624,7 @@ static void run_coalesced(wvg_corpus *c, const std::vector<wvg_search_request *>
     const size_t B = batch.size();
     if (B == 1) {
         wvg_search_request *r = batch[0];
-        r->rc = search_batch(c, r->q, 1, k, nullptr, 0, r->ids, r->dists, r->counts);
+        r->rc = search_batch(c, r->q, 1, k, r->allow, r->allow_words, r->ids, r->dists, r->counts);
         if (r->rc) r->err = wvg_last_error();
         return;
     }
@@ -553,7 +633,9 @@ static void run_coalesced(wvg_corpus *c, const std::vector<wvg_search_request *>
     std::vector<uint64_t> ids(B * k);
     std::vector<uint32_t> counts(B);
     for (size_t i = 0; i < B; i++) std::memcpy(q.data() + i * d, batch[i]->q, (size_t)d * 4);
-    const int rc = search_batch(c, q.data(), (uint32_t)B, k, nullptr, 0, ids.data(), dists.data(), counts.data());
+    const int rc = batch[0]->allow
+                       ? search_batch_filtered(c, batch, k, ids.data(), dists.data(), counts.data())
+                       : search_batch(c, q.data(), (uint32_t)B, k, nullptr, 0, ids.data(), dists.data(), counts.data());
     const std::string err = rc ? wvg_last_error() : std::string();
     for (size_t i = 0; i < B; i++) {
         wvg_search_request *r = batch[i];
@@ -573,12 +655,14 @@ static void run_coalesced(wvg_corpus *c, const std::vector<wvg_search_request *>
 // wakes the others.  A lone call finds the coalescer idle and runs at once;
 // under load a batch forms from the calls that arrive while the previous one
 // runs, so the batch size follows the arrival rate.
-static int search_coalesced(wvg_corpus *c, const float *query, uint32_t k, uint64_t *out_ids, float *out_dists,
-                            uint32_t *out_counts)
+static int search_coalesced(wvg_corpus *c, const float *query, uint32_t k, const uint64_t *allow,
+                            uint64_t allow_words, uint64_t *out_ids, float *out_dists, uint32_t *out_counts)
 {
     wvg_search_request r;
     r.q = query;
     r.k = k;
+    r.allow = allow;
+    r.allow_words = allow_words;
     r.ids = out_ids;
     r.dists = out_dists;
     r.counts = out_counts;
@@ -593,8 +677,16 @@ static int search_coalesced(wvg_corpus *c, const float *query, uint32_t k, uint6
         co.busy = true;
         std::vector<wvg_search_request *> batch;
         const uint32_t kk = co.pending.front()->k;
-        for (auto it = co.pending.begin(); it != co.pending.end() && batch.size() < COALESCE_MAX;) {
-            if ((*it)->k == kk) {
+        // filtered and unfiltered requests form separate batches; filtered batches stay
+        // below the MFMA threshold (the co-scheduled K1 takes one allow window per query)
+        const bool filt = co.pending.front()->allow != nullptr;
+        const uint32_t mn = c->ctx->opt.mfma_min_queries;
+        const size_t cap = filt && mn > 1 && c->metric != WVG_METRIC_L2 && c->metric != WVG_METRIC_MANHATTAN &&
+                                   c->metric != WVG_METRIC_HAMMING
+                               ? std::min<size_t>(COALESCE_MAX, mn - 1)
+                               : COALESCE_MAX;
+        for (auto it = co.pending.begin(); it != co.pending.end() && batch.size() < cap;) {
+            if ((*it)->k == kk && ((*it)->allow != nullptr) == filt) {
                 batch.push_back(*it);
                 it = co.pending.erase(it);
             } else {
@@ -624,8 +716,14 @@ int wvg_search(wvg_corpus *c, const float *queries, uint32_t nq, uint32_t k, con
     if (nq > 0 && !queries) return fail(WVG_ERR_INVALID, "null queries");
     if (c->kind == WVG_KIND_PQ && !c->d_centers) return fail(WVG_ERR_INVALID, "PQ corpus has no codebook");
     std::shared_lock<std::shared_mutex> lk(c->rw);
-    if (nq == 1 && !allow_bits && k > 0 && k <= MAX_K && c->ctx->opt.coalesce)
-        return search_coalesced(c, queries, k, out_ids, out_dists, out_counts);
+    if (nq == 1 && k > 0 && k <= MAX_K && c->ctx->opt.coalesce && (!allow_bits || c->kind == WVG_KIND_F32)) {
+        uint64_t tb = 0, te = 0;
+        if (allow_bits && !allow_tile_range(c, allow_bits, allow_words, tb, te)) {  // nothing allowed here
+            write_empty(1, k, out_ids, out_dists, out_counts);
+            return WVG_OK;
+        }
+        return search_coalesced(c, queries, k, allow_bits, allow_words, out_ids, out_dists, out_counts);
+    }
     return search_batch(c, queries, nq, k, allow_bits, allow_words, out_ids, out_dists, out_counts);
 }
 
@@ -683,27 +781,51 @@ static int wvg::search_batch(wvg_corpus *c, const float *queries, uint32_t nq, u
         d_allow = (const uint64_t *)(b + o_allow);
     }
     // a single query merged in-launch writes its results straight into the slot's
-    // coherent host buffer: no device-to-host copy (and its ~10 us) per call
+    // coherent host buffer as tagged records: no device-to-host copy (and its ~10 us)
+    // and no stream synchronization per call (the host polls the tags)
     const bool zc = inlaunch_single(c, nq, p, d_allow != nullptr);
+    const int sp = tuning().single_path;
+    const bool legacy = zc && (sp & 4) != 0;  // tools A/B: round 4's untagged layout
+    SingleOut so;
     char *hc = nullptr;
     if (zc) {
         void *v = nullptr;
-        rc = g.slot->host_coherent(out_b, &v);
+        rc = g.slot->host_coherent(legacy ? out_b : (size_t)(k + 1) * 16, &v);
         if (rc) return rc;
         hc = (char *)v;
+        if (!legacy) {
+            so.records = reinterpret_cast<uint4 *>(hc);
+            so.tag = ++g.slot->tag ? g.slot->tag : ++g.slot->tag;  // never 0
+        }
+    }
+    if (zc && !legacy) {
+        rc = run_search(c, qin ? nullptr : b + o_q, qpitch, nq, k, d_allow, p, (uint64_t *)(b + o_part), nullptr,
+                        nullptr, nullptr, s, g.slot, qin ? qinl.data() : nullptr, &so);
+        if (rc) return rc;
+        rc = wait_records(so, k, s, (sp & 2) != 0);
+        if (rc) return rc;
+        const uint4 *r = so.records;
+        for (uint32_t i = 0; i < k; i++) {
+            if (out_ids) out_ids[i] = (uint64_t)r[i].x | (uint64_t)r[i].y << 32;
+            if (out_dists) std::memcpy(out_dists + i, &r[i].z, 4);
+        }
+        const uint32_t c0 = r[k].x;
+        if (out_counts) *out_counts = c0;
+        if (c->count > 0 && c0 == 0)  // a live row exists: 0 results = the in-launch merge gave up
+            return fail(WVG_ERR_DEVICE, "single-query merge timed out waiting for the scan workgroups");
+        return WVG_OK;
     }
     char *rspan = zc ? hc : b + o_ids;  // the result span [ids | dists | counts]
-    // zero-copy single query, polled (tools A/B only, single_path bit 1 clear): the host polls
-    // the count word (preset to a sentinel) that the merge writes last, after a system-scope
-    // release.  Under concurrent calls about 1 in 1000 polled results was stale or mixed
-    // (tools/single_query_stress.py), so the product synchronizes the stream instead.
-    volatile uint32_t *cflag = zc && (tuning().single_path & 2) == 0
+    // tools A/B (single_path bit 2): round 4's polled untagged layout -- the host polls the count
+    // word (preset to a sentinel) that the merge writes last, after a system-scope release
+    volatile uint32_t *cflag = legacy && (sp & 2) == 0
                                    ? reinterpret_cast<volatile uint32_t *>(rspan + (o_cnt - o_ids))
                                    : nullptr;
+    if (legacy) so.legacy_poll = cflag != nullptr;
     if (cflag) *cflag = 0xFFFFFFFFu;
     rc = run_search(c, qin ? nullptr : b + o_q, qpitch, nq, k, d_allow, p, (uint64_t *)(b + o_part), (uint64_t *)rspan,
                     (float *)(rspan + (o_d - o_ids)), (uint32_t *)(rspan + (o_cnt - o_ids)), s, g.slot,
-                    qin ? qinl.data() : nullptr, cflag != nullptr);
+                    qin ? qinl.data() : nullptr, &so);
     if (rc) return rc;
     const char *pin = zc ? hc : out_b <= STAGE_MAX ? st.take(out_b) : nullptr;
     std::vector<char> big(pin ? 0 : out_b);
@@ -726,11 +848,82 @@ static int wvg::search_batch(wvg_corpus *c, const float *queries, uint32_t nq, u
     if (out_ids) std::memcpy(out_ids, pin, (size_t)nq * k * 8);
     if (out_dists) std::memcpy(out_dists, pin + (o_d - o_ids), (size_t)nq * k * 4);
     if (out_counts) std::memcpy(out_counts, pin + (o_cnt - o_ids), (size_t)nq * 4);
+#ifdef WVG_TOOLS
+    if (polled && out_ids) {  // diagnostic: did ids land in host memory AFTER the polled count?
+        WVG_HIP(hipStreamSynchronize(s));
+        single_counter(3, std::memcmp(out_ids, hc, (size_t)k * 8) != 0);
+    }
+#endif
     if (nq == 1 && !d_allow && c->count > 0) {  // a live row exists: 0 results = the in-launch merge gave up
         uint32_t c0 = 0;
         std::memcpy(&c0, pin + (o_cnt - o_ids), 4);
         if (c0 == 0) return fail(WVG_ERR_DEVICE, "single-query merge timed out waiting for the scan workgroups");
     }
+    return WVG_OK;
+}
+
+static int wvg::search_batch_filtered(wvg_corpus *c, const std::vector<wvg_search_request *> &batch, uint32_t k,
+                                      uint64_t *out_ids, float *out_dists, uint32_t *out_counts)
+{
+    const uint32_t B = (uint32_t)batch.size(), d = c->dim;
+    // every query's window [tb_i, te_i) and their union [TB, TE)
+    std::vector<uint64_t> tb(B), te(B);
+    std::vector<char> live(B);
+    uint64_t TB = UINT64_MAX, TE = 0;
+    for (uint32_t i = 0; i < B; i++) {
+        live[i] = allow_tile_range(c, batch[i]->allow, batch[i]->allow_words, tb[i], te[i]);
+        if (!live[i]) continue;
+        TB = std::min(TB, tb[i]);
+        TE = std::max(TE, te[i]);
+    }
+    write_empty(B, k, out_ids, out_dists, out_counts);
+    if (TE <= TB) return WVG_OK;
+    const uint64_t W = TE - TB, wb = c->id_base / 64;
+    std::vector<uint64_t> win((size_t)B * W, 0ull);  // query i's allow words of tiles [TB, TE) (0 outside its own)
+    for (uint32_t i = 0; i < B; i++)
+        if (live[i]) std::memcpy(win.data() + (size_t)i * W + (tb[i] - TB), batch[i]->allow + wb + tb[i], (te[i] - tb[i]) * 8);
+    SearchPlan p = plan_search(c, B, k, nullptr, 0);
+    if (p.empty) return WVG_OK;
+    if (p.gemm || !p.cosched) return fail(WVG_ERR_INVALID, "filtered coalesced batch needs the co-scheduled K1");
+    p.tb = TB;
+    p.te = TE;
+    p.allow_qstride = W;
+    std::vector<float> q((size_t)B * d);
+    for (uint32_t i = 0; i < B; i++) std::memcpy(q.data() + (size_t)i * d, batch[i]->q, (size_t)d * 4);
+    SlotGuard g(c->ctx);
+    int rc = c->ctx->acquire(&g.slot);
+    if (rc) return rc;
+    Carver cv;
+    const size_t o_q = cv.take(query_bytes(c, B));
+    const size_t o_allow = cv.take((size_t)B * W * 8);
+    const size_t o_part = cv.take(p.workspace_bytes(B, k));
+    const size_t o_ids = cv.take((size_t)B * k * 8);
+    const size_t o_d = cv.take((size_t)B * k * 4);
+    const size_t o_cnt = cv.take((size_t)B * 4);
+    void *base = nullptr;
+    rc = g.slot->device_scratch(cv.off, &base);
+    if (rc) return rc;
+    char *b = (char *)base;
+    hipStream_t s = g.slot->stream;
+    const size_t out_b = o_cnt + (size_t)B * 4 - o_ids;
+    Staging st;
+    rc = st.reserve(g.slot, stage_bytes(staged_query_bytes(c, B)) + stage_bytes((size_t)B * W * 8) + stage_bytes(out_b));
+    if (rc) return rc;
+    uint32_t qpitch = 0;
+    rc = stage_queries(c, g.slot, q.data(), B, b + o_q, qpitch, nullptr, nullptr, &st);
+    if (rc) return rc;
+    WVG_HIP(st.h2d(b + o_allow, win.data(), (size_t)B * W * 8, s));
+    rc = run_search(c, b + o_q, qpitch, B, k, (const uint64_t *)(b + o_allow), p, (uint64_t *)(b + o_part),
+                    (uint64_t *)(b + o_ids), (float *)(b + o_d), (uint32_t *)(b + o_cnt), s);
+    if (rc) return rc;
+    const char *pin = out_b <= STAGE_MAX ? st.take(out_b) : nullptr;
+    std::vector<char> big(pin ? 0 : out_b);
+    if (!pin) pin = big.data();
+    WVG_HIP(hipMemcpyAsync((void *)pin, b + o_ids, out_b, hipMemcpyDeviceToHost, s));
+    WVG_HIP(hipStreamSynchronize(s));  // also keeps q / win alive until their copies are done
+    std::memcpy(out_ids, pin, (size_t)B * k * 8);
+    std::memcpy(out_dists, pin + (o_d - o_ids), (size_t)B * k * 4);
+    std::memcpy(out_counts, pin + (o_cnt - o_ids), (size_t)B * 4);
     return WVG_OK;
 }
 
