@@ -251,6 +251,10 @@ BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md; no 2:1 sparsi
 # unfused sub, mul, add per dimension, two centroids per packed op -- at one wave64
 # VALU instruction per SIMD per 4 cycles, 1024 SIMDs, 2.4 GHz
 PQ_ENCODE_PEAK_ROWS = 1024 * 2.4e9 / 4 * 64 / (32 * 256 * 5.5)
+# SURVEY.md 8(d)'s count for the same encode: N*m*ks*ds*3 fp32 ops (unfused sub, mul, add per
+# dimension), against the packed non-FMA fp32 rate (2 ops per lane per v_pk_* instruction:
+# 1024 SIMDs x 64 lanes x 2 / 4 cycles x 2.4 GHz = 78.6 Tops/s)
+PQ_ENCODE_PEAK_OPS = 1024 * 64 * 2 / 4 * 2.4e9
 
 
 def gpu_clock(dev, torch):
@@ -491,6 +495,11 @@ def config_pq(ctx, orc, nq=16):
             "batch_call_queries": nq, "fit_s": round(fit_s, 3), "lloyd_passes_mean": round(float(passes.mean()), 2),
             "encode_s": round(enc_s, 4), "encode_rows_per_s": round(n / enc_s, 1),
             "encode_frac_of_packed_op_peak": round(n / enc_s / PQ_ENCODE_PEAK_ROWS, 4),
+            "encode_ops_8d": n * m * ks * (d // m) * 3,
+            "encode_frac_8d_ops": round(n * m * ks * (d // m) * 3 / enc_s / PQ_ENCODE_PEAK_OPS, 4),
+            "encode_frac_note": ("encode_frac_of_packed_op_peak prices the kernel's 5.5 VALU instructions per (row, "
+                                 "segment, centroid) at full issue; encode_frac_8d_ops divides SURVEY.md 8(d)'s "
+                                 "N*m*ks*ds*3 fp32 ops by the packed non-FMA rate (78.6 Tops/s)"),
             "kernel": "K8e scan_pq32_wide_kernel (LUT image in LDS); encode K9 pq_encode_kernel",
             "roofline": {"bound": "hbm", "achieved": round(gbps, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbps / HBM_PEAK_GBS, 4), "bytes_per_scan": n * m},

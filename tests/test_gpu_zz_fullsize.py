@@ -118,7 +118,9 @@ def test_full_size_bq_100m_x_1536_properties(ctx, orc):
 
 
 # Full size (BASELINE config 2): 10M x 768 fp32 cosine, one 1024-query batch
-# through the batched MFMA path (K3b) -- properties on sampled rows and queries.
+# through the default batched path -- the K3d bf16 MFMA screen (a K3b exact
+# fp32 MFMA pilot, exact seeds, the exact AVX2-order rescore of the kept
+# candidates) -- properties on sampled rows and queries.
 def test_full_size_batched_10m_x_768_cosine_properties(ctx, orc):
     n, d, nq, k = 10_000_000, 768, 1024, 10
     c = Corpus(ctx, KIND_F32, METRIC_COSINE, d, n)

@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--gpcs", default="0", help="K1 workgroups per CU (tuning key 1; 0 = auto): comma list")
     ap.add_argument("--modes", default="1,0", help="tuning key 2: 1 = in-launch merge, 0 = scan + merge kernel")
     ap.add_argument("--coalesce", default="1,0")
+    ap.add_argument("--variants", default="0", help="tuning key 25 (query-stream K1): bit 0 = tile-granular ranges, "
+                                                   "bit 1 = arrival-counter merge (round 4); comma list")
     a = ap.parse_args()
     import torch
 
@@ -43,7 +45,9 @@ def main():
         ids = np.empty(10, np.uint64)
         d = np.empty(10, np.float32)
         cnt = np.empty(1, np.uint32)
-        for mode, gpc in ((int(m), int(g)) for m in a.modes.split(",") for g in a.gpcs.split(",")):
+        for mode, gpc, var in ((int(m), int(g), int(v)) for m in a.modes.split(",") for g in a.gpcs.split(",")
+                               for v in a.variants.split(",")):
+            prevv = lib.wvgx_set_tuning(25, var)
             prev = lib.wvgx_set_tuning(2, mode)
             prevg = lib.wvgx_set_tuning(1, gpc)
             for i in range(50):
@@ -59,12 +63,13 @@ def main():
             nl = ctypes.c_uint64()
             check(lib.wvg_profile_stop(ctx.handle, ctypes.byref(ms), ctypes.byref(nl)))
             kern_us = ms.value * 1e3 / max(1, nl.value)
-            key = f"coalesce{coalesce}_inlaunch{mode}_gpc{gpc}"
+            key = f"coalesce{coalesce}_inlaunch{mode}_gpc{gpc}_streamvar{var}"
             out[key] = {
                 "us_per_call": round(wall * 1e6, 2), "scan_kernel_us": round(kern_us, 2),
                 "host_and_gap_us": round(wall * 1e6 - kern_us, 2), "profiled_launches": nl.value,
                 "frac_of_8TBs": round(a.rows * a.dim * 4 / wall / 8e12, 4)}
             lib.wvgx_set_tuning(2, prev)
+            lib.wvgx_set_tuning(25, prevv)
             lib.wvgx_set_tuning(1, prevg)
             print(json.dumps({key: out[key]}), flush=True)
         c.destroy()

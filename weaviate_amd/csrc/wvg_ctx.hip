@@ -36,8 +36,9 @@ int StreamSlot::control(uint32_t **out)
 {
     if (!dctl) {
         void *p = nullptr;
-        hipError_t e = hipMalloc(&p, 256);
-        if (e == hipSuccess) e = hipMemsetAsync(p, 0, 256, stream);
+        const size_t bytes = 4 * (SLOT_READY_OFF + SLOT_READY_MAX);
+        hipError_t e = hipMalloc(&p, bytes);
+        if (e == hipSuccess) e = hipMemsetAsync(p, 0, bytes, stream);
         if (e == hipSuccess) e = hipStreamSynchronize(stream);
         if (e != hipSuccess) {
             if (p) (void)hipFree(p);
@@ -185,6 +186,8 @@ int wvg_open_ex(int device, const wvg_options *opts, wvg_ctx **out)
     if (const char *e = getenv("WVG_SERPENTINE")) tuning().serpentine = (int)strtol(e, nullptr, 10);  // A/B runs
     if (const char *e = getenv("WVG_K1_TAIL")) tuning().k1_tail = (int)strtol(e, nullptr, 10);        // A/B runs
     if (const char *e = getenv("WVG_K1_LOADS")) tuning().k1_loads = (int)strtol(e, nullptr, 10);        // A/B runs
+    if (const char *e = getenv("WVG_SCREEN_VARIANT")) tuning().screen_variant = (int)strtol(e, nullptr, 10);  // A/B
+    if (const char *e = getenv("WVG_STREAM_VARIANT")) tuning().stream_variant = (int)strtol(e, nullptr, 10);  // A/B
 #endif
     *out = c;
     return WVG_OK;
@@ -430,6 +433,9 @@ int wvgx_set_tuning(int key, int value)
     } else if (key == 24) {
         old = t.single_path;
         t.single_path = value;
+    } else if (key == 25) {
+        old = t.stream_variant;
+        t.stream_variant = value;
     }
     return old;
 }

@@ -28,6 +28,8 @@ int fail(int code, const std::string &msg);
             return ::wvg::fail(WVG_ERR_DEVICE, std::string(#expr ": ") + hipGetErrorString(_e)); \
     } while (0)
 
+constexpr uint32_t SLOT_READY_OFF = 64;     // words
+constexpr uint32_t SLOT_READY_MAX = 4032;   // lists (scan workgroups) of a single query with per-list hand-offs
 // A pooled HIP stream with its own grow-only device scratch and pinned host
 // staging, borrowed by one C-ABI call at a time (callers are many goroutines).
 struct StreamSlot {
@@ -49,7 +51,8 @@ struct StreamSlot {
     int device_scratch(size_t bytes, void **out);
     int host_pinned(size_t bytes, void **out);
     int host_coherent(size_t bytes, void **out);
-    int control(uint32_t **out);  // dctl, allocated and zeroed on first use
+    int control(uint32_t **out);  // dctl, allocated and zeroed on first use: [0] arrivals, [1] status,
+                                  // [SLOT_READY_OFF ..) the single query's per-list ready words
 };
 
 }  // namespace wvg
@@ -271,6 +274,7 @@ hipError_t launch_scan_f32(const ScanArgs &a, uint64_t *partials, int groups, hi
 // Sticky status word of a device-search workspace (its first bytes; read and
 // cleared by wvg_search_device_check).
 constexpr uint32_t WVG_STATUS_MERGE_TIMEOUT = 1u;
+constexpr uint32_t WVG_RECORDS_TIMEOUT = 0xFFFFFFFFu;  // header count of a merge that gave up (StreamJob::records)
 constexpr uint32_t STREAM_QIN_FLOATS = 256;  // a query of up to 256 dims (f32 chunks) inline in StreamJob
 struct StreamJob {
     uint64_t *partials;  // [nq][groups][k]
@@ -290,6 +294,12 @@ struct StreamJob {
     uint4 *records;
     uint32_t tag;
     uint32_t legacy_poll;  // tools A/B: round 4's layout (ids / dists, a release, then the polled count)
+    // per-list hand-off (instead of the arrival counter): scan workgroup g of query q
+    // sc1-stores ready_tag + q into ready[q * groups + g] after its list; the merge
+    // workgroup merges each list as soon as its word matches (merge_lists_ready)
+    uint32_t *ready;
+    uint32_t ready_tag;
+    uint32_t row_split;    // row-granular wave ranges (scan_f32_stream_kernel)
     // a single host query rides in the kernel arguments (ScanArgs::queries null):
     // no host-to-device copy (a blit dispatch + ~10 us of API time) per call
     alignas(16) float qin[STREAM_QIN_FLOATS];
@@ -397,7 +407,10 @@ struct Tuning {
     int screen_pilot = 16;   // K3c/K3d: tiles of the exact pilot scan that seeds the bound (0 = none; A/B)
     int screen_pilot_gemm = 512;  // K3c/K3d: tiles of the K3b (exact fp32 MFMA) pilot, which replaces the K1
                                   // pilot (0 = the K1 pilot; A/B)
-    int screen_variant = 0;  // batched screen kernel: 0 = K3d where it applies (d = 512, 768), 1 = K3c (A/B)
+    int screen_variant = 0;  // batched screen kernel: 0 = K3d where it applies (d = 512, 768), 1 = K3c,
+                             // 2 = K3e (K3d with 32x32x16 MFMAs)
+    int stream_variant = 0;  // query-stream K1 (tuning key 25): bit 0 = tile-granular wave ranges, bit 1 = the
+                             // arrival-counter merge after all lists (round 4) instead of per-list hand-offs (A/B)
     int single_path = 0;     // single-query host calls: bit 0 = query staged by copy instead of in the kernel
                              // arguments, bit 1 = stream synchronization instead of polling, bit 2 = round 4's
                              // untagged layout (ids / dists + a polled count: returned the slot's previous result

@@ -72,11 +72,14 @@ __device__ __forceinline__ void wave_range(const ScanArgs &a, int waves_per_grou
 // 16-byte store {id lo, id hi, dist bits, tag}, then the header {count, tag}
 // at rec[k] -- the host accepts only entries carrying its call's tag.
 template <int E, int WAVES>
+__device__ __forceinline__ void merge_finish(WaveTopK<E> &tk, uint32_t k, uint64_t id_base, uint64_t *ids,
+                                             float *dists, uint32_t *count, uint4 *rec, uint32_t tag, bool sys_release);
+
+template <int E, int WAVES>
 __device__ __forceinline__ void merge_lists_body(const uint64_t *src, uint32_t nlists, uint32_t list_len, uint32_t k,
                                                  uint64_t id_base, uint64_t *ids, float *dists, uint32_t *count,
                                                  uint4 *rec = nullptr, uint32_t tag = 0, bool sys_release = false)
 {
-    __shared__ uint64_t msh[WAVES][64 * E];
     const int lane = threadIdx.x & 63, wave = wave_id();
     WaveTopK<E> tk;
     tk.init((int)k);
@@ -104,6 +107,17 @@ __device__ __forceinline__ void merge_lists_body(const uint64_t *src, uint32_t n
             }
         }
     }
+    merge_finish<E, WAVES>(tk, k, id_base, ids, dists, count, rec, tag, sys_release);
+}
+
+// The merge's end: the WAVES waves' lists tree-merged in LDS, wave 0 writes
+// ids / dists / count, or the tagged records (rec) for a host-read result.
+template <int E, int WAVES>
+__device__ __forceinline__ void merge_finish(WaveTopK<E> &tk, uint32_t k, uint64_t id_base, uint64_t *ids,
+                                             float *dists, uint32_t *count, uint4 *rec, uint32_t tag, bool sys_release)
+{
+    __shared__ uint64_t msh[WAVES][64 * E];
+    const int lane = threadIdx.x & 63, wave = wave_id();
 #pragma unroll
     for (int e = 0; e < E; e++) msh[wave][e * 64 + lane] = tk.l[e];
     for (int step = 1; step < WAVES; step <<= 1) {
@@ -153,13 +167,88 @@ __device__ __forceinline__ uint64_t lane_key(uint64_t m, float dist, uint64_t t,
     return ((m >> lane) & 1ull) ? wvg_make_key(dist, (uint32_t)(t * 64 + lane)) : WVG_KEY_NONE;
 }
 
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(1))) uint64_t gu64;
+
+// The query-stream merge of one query as its lists ARRIVE (StreamJob::ready):
+// scan workgroup g stores its list sc1, drains it, then sc1-stores `tag` into
+// ready[g]; lane l of merge wave w owns list g = 64 w + l (+ 64 WAVES ...),
+// polls its ready word (sc1 load) and, once it matches, reads the list with sc1
+// loads (MI355X_MICROARCH.md correctness boundaries: the valid hand-off form
+// without an acquire) and offers it to the wave's top-k -- lists that arrive
+// early are merged while the scan's stragglers still run, so after the last
+// arrival only its own list is left to read.  False after `limit` ticks of
+// s_memrealtime without every list.
+template <int E, int WAVES>
+__device__ __forceinline__ bool merge_lists_ready(const uint64_t *src, const uint32_t *ready, uint32_t tag,
+                                                  uint32_t nlists, uint32_t k, uint64_t limit, uint64_t id_base,
+                                                  uint64_t *ids, float *dists, uint32_t *count, uint4 *rec,
+                                                  uint32_t rtag)
+{
+    __shared__ int ok_sh;
+    const int lane = threadIdx.x & 63, wave = wave_id();
+    WaveTopK<E> tk;
+    tk.init((int)k);
+    const uint64_t start = __builtin_amdgcn_s_memrealtime();
+    bool ok = true;
+    for (uint32_t g0 = (uint32_t)wave * 64; g0 < nlists && ok; g0 += WAVES * 64) {
+        const uint32_t list = g0 + lane;
+        bool done = list >= nlists;
+        const gu64 *lp = (const gu64 *)(src + (size_t)list * k);
+        while (true) {
+            const bool rdy = !done && __hip_atomic_load((const gu32 *)(ready + list), __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT) == tag;
+            if (__ballot(rdy)) {
+                for (uint32_t r0 = 0; r0 < k; r0 += 4) {
+                    uint64_t c4[4];
+#pragma unroll
+                    for (int i = 0; i < 4; i++)
+                        c4[i] = rdy && r0 + i < k ? __hip_atomic_load(lp + r0 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                                  : WVG_KEY_NONE;
+                    bool stop = false;
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const uint32_t r = r0 + (uint32_t)i;
+                        if (r >= k) break;
+                        if (r > 0 && __ballot(c4[i] < tk.tau) == 0ull) {  // sorted lists: the rest cannot enter
+                            stop = true;
+                            break;
+                        }
+                        tk.offer(c4[i]);
+                    }
+                    if (stop) break;
+                }
+                done = done || rdy;
+            }
+            if (__ballot(!done) == 0ull) break;
+            if (__builtin_amdgcn_s_memrealtime() - start > limit) {
+                ok = false;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    if (threadIdx.x == 0) ok_sh = 1;
+    __syncthreads();
+    if (!ok && lane == 0) ok_sh = 0;
+    __syncthreads();
+    if (!ok_sh) return false;
+    merge_finish<E, WAVES>(tk, k, id_base, ids, dists, count, rec, rtag, false);
+    return true;
+}
+
 // One wave's tiles [t0, t1) for one query: one tile's loads in flight per
 // wave; tiles with no live/allowed row are skipped without touching their rows.
 // rev: walk the range downwards (t1-1 .. t0); the result does not depend on
 // the order (lexicographic keys), only the cache state the next scan finds.
+// first_mask / last_mask: lanes of tiles t0 / t1 - 1 this wave owns (a
+// row-granular split of the range, see scan_f32_stream_kernel); on such a
+// partial tile only the owned lanes load, so two waves sharing a tile fetch it
+// once between them.
 template <int METRIC, int D, int E>
 __device__ __forceinline__ void scan_tiles(const ScanArgs &a, const float4 *q4, uint64_t t0, uint64_t t1,
-                                           WaveTopK<E> &tk, bool rev = false, uint32_t qi = 0)
+                                           WaveTopK<E> &tk, bool rev = false, uint32_t qi = 0,
+                                           uint64_t first_mask = ~0ull, uint64_t last_mask = ~0ull)
 {
     const int lane = threadIdx.x & 63;
     const float4 *data = reinterpret_cast<const float4 *>(a.data);
@@ -169,17 +258,27 @@ __device__ __forceinline__ void scan_tiles(const ScanArgs &a, const float4 *q4, 
     uint64_t m_next = n ? tile_mask(a, rev ? t1 - 1 : t0, qi) : 0ull;
     for (uint64_t i = 0; i < n; ++i) {
         const uint64_t t = rev ? t1 - 1 - i : t0 + i;
-        const uint64_t m = m_next;
+        uint64_t m = m_next;
         if (i + 1 < n) m_next = tile_mask(a, rev ? t - 1 : t + 1, qi);  // scalar prefetch of the next mask
+        const uint64_t own = (t == t0 ? first_mask : ~0ull) & (t == t1 - 1 ? last_mask : ~0ull);
+        m &= own;
         if (m == 0ull) continue;  // wave-uniform: nothing live/allowed in this tile
         const float4 *rp = data + (size_t)t * a.nchunks * 64 + lane;
-        float r;
-        if (a.order512)  // wave-uniform: the AVX-512 kernels' order (generic length)
-            r = row_dist_512<METRIC, 64>(rp, q4, (int)a.dim);
-        else if constexpr (D > 0)
-            r = i >= split ? row_dot_or_l2_fixed<METRIC, D, 64, false>(rp, q4) : row_dot_or_l2_fixed<METRIC, D, 64>(rp, q4);
-        else
-            r = row_dot_or_l2_generic<METRIC, 64>(rp, q4, (int)a.dim);
+        auto dist = [&]() -> float {
+            if (a.order512)  // wave-uniform: the AVX-512 kernels' order (generic length)
+                return row_dist_512<METRIC, 64>(rp, q4, (int)a.dim);
+            else if constexpr (D > 0)
+                return i >= split ? row_dot_or_l2_fixed<METRIC, D, 64, false>(rp, q4)
+                                  : row_dot_or_l2_fixed<METRIC, D, 64>(rp, q4);
+            else
+                return row_dot_or_l2_generic<METRIC, 64>(rp, q4, (int)a.dim);
+        };
+        float r = 0.0f;
+        if (own != ~0ull) {  // a shared edge tile (wave-uniform): only this wave's lanes load
+            if ((own >> lane) & 1ull) r = dist();
+        } else {
+            r = dist();
+        }
         tk.offer(lane_key(m, wrap_metric(a.metric, r), t, lane));
     }
 }
@@ -274,9 +373,6 @@ hipError_t launch_fill_empty(uint64_t *ids, float *dists, uint32_t *counts, uint
 // sc1), drains them (s_waitcnt vmcnt(0)) and adds to an arrival counter; no
 // release fence, so no per-query L2 writeback.  The consumer polls the counter
 // relaxed with s_sleep, then ONE agent-scope acquire drops its stale L1 lines.
-typedef __attribute__((address_space(1))) uint32_t gu32;
-typedef __attribute__((address_space(1))) uint64_t gu64;
-
 // Thread 0 polls; false after `limit` ticks of s_memrealtime (100 MHz; 4 s
 // by default), so a waiting workgroup always exits.
 // The counter counts up from `base` (0 for a workspace zeroed per call; a
@@ -306,7 +402,8 @@ __device__ __forceinline__ bool wait_arrivals(uint32_t *ctr, uint32_t base, uint
 // group_combine_store with write-through stores, then the storing wave drains
 // and publishes one arrival.
 template <int E, int WAVES>
-__device__ __forceinline__ void group_combine_publish(WaveTopK<E> &tk, uint64_t *out, uint32_t *arrivals)
+__device__ __forceinline__ void group_combine_publish(WaveTopK<E> &tk, uint64_t *out, uint32_t *arrivals,
+                                                      uint32_t *ready = nullptr, uint32_t tag = 0)
 {
     __shared__ uint64_t sh[WAVES][64 * E];
     const int lane = threadIdx.x & 63;
@@ -340,7 +437,12 @@ __device__ __forceinline__ void group_combine_publish(WaveTopK<E> &tk, uint64_t 
             if (i < tk.k) __hip_atomic_store((gu64 *)(out + i), tk.l[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_fetch_add((gu32 *)arrivals, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) {
+            if (ready)  // StreamJob::ready: this list's own flag
+                __hip_atomic_store((gu32 *)ready, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+                __hip_atomic_fetch_add((gu32 *)arrivals, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
     __syncthreads();  // sh is reused by the next query
 }
@@ -354,7 +456,14 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_stream_kernel(ScanAr
     const uint32_t G = j.groups;
     if (blockIdx.x == G) {
         for (uint32_t q = 0; q < a.nq; q++) {
-            if (!wait_arrivals(j.arrivals + q, j.arrival_base, G, j.wait_limit)) {
+            const bool got = j.ready
+                                 ? merge_lists_ready<E, SCAN_WAVES>(
+                                       j.partials + (size_t)q * G * a.k, j.ready + (size_t)q * G, j.ready_tag + q, G,
+                                       a.k, j.wait_limit, a.id_base, j.ids ? j.ids + (size_t)q * a.k : nullptr,
+                                       j.dists ? j.dists + (size_t)q * a.k : nullptr, j.counts ? j.counts + q : nullptr,
+                                       j.records ? j.records + (size_t)q * (a.k + 1) : nullptr, j.tag)
+                                 : wait_arrivals(j.arrivals + q, j.arrival_base, G, j.wait_limit);
+            if (!got) {
                 // gave up: queries q.. get empty results (never stale ones) and
                 // the sticky status word tells wvg_search_device_check
                 if (threadIdx.x == 0) atomicOr(j.status, WVG_STATUS_MERGE_TIMEOUT);
@@ -365,20 +474,22 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_stream_kernel(ScanAr
                             r[i] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0x7F800000u, j.tag);
                         __syncthreads();
                         if (threadIdx.x == 0)
-                            __hip_atomic_store(reinterpret_cast<uint64_t *>(r + a.k), (uint64_t)j.tag << 32,
-                                               __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                            __hip_atomic_store(reinterpret_cast<uint64_t *>(r + a.k),
+                                               (uint64_t)j.tag << 32 | WVG_RECORDS_TIMEOUT, __ATOMIC_RELEASE,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
                     }
                 } else {
                     fill_empty_body(j.ids, j.dists, j.counts, q, a.nq, a.k);
                 }
                 return;
             }
-            merge_lists_body<E, SCAN_WAVES>(j.partials + (size_t)q * G * a.k, G, a.k, a.k, a.id_base,
-                                            j.ids ? j.ids + (size_t)q * a.k : nullptr,
-                                            j.dists ? j.dists + (size_t)q * a.k : nullptr,
-                                            j.counts ? j.counts + q : nullptr,
-                                            j.records ? j.records + (size_t)q * (a.k + 1) : nullptr, j.tag,
-                                            j.legacy_poll != 0);
+            if (!j.ready)
+                merge_lists_body<E, SCAN_WAVES>(j.partials + (size_t)q * G * a.k, G, a.k, a.k, a.id_base,
+                                                j.ids ? j.ids + (size_t)q * a.k : nullptr,
+                                                j.dists ? j.dists + (size_t)q * a.k : nullptr,
+                                                j.counts ? j.counts + q : nullptr,
+                                                j.records ? j.records + (size_t)q * (a.k + 1) : nullptr, j.tag,
+                                                j.legacy_poll != 0);
             __syncthreads();  // merge LDS reused by the next query
         }
         return;
@@ -386,16 +497,31 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_stream_kernel(ScanAr
     const uint64_t ntiles = a.tile_end - a.tile_begin;
     const uint64_t total = (uint64_t)G * SCAN_WAVES;
     const uint64_t gw = (uint64_t)blockIdx.x * SCAN_WAVES + wave_id();
-    const uint64_t t0 = a.tile_begin + ntiles * gw / total;
-    const uint64_t t1 = a.tile_begin + ntiles * (gw + 1) / total;
+    uint64_t t0, t1, fmask = ~0ull, lmask = ~0ull;
+    if (j.row_split) {
+        // row-granular: every wave gets the same number of rows (+-1), so none ends a
+        // whole tile after the others (tile-granular: 15 or 16 tiles per wave at 1M rows)
+        const uint64_t nrows = ntiles * 64, r0 = nrows * gw / total, r1 = nrows * (gw + 1) / total;
+        t0 = a.tile_begin + r0 / 64;
+        t1 = a.tile_begin + (r1 + 63) / 64;
+        fmask = ~0ull << (r0 % 64);
+        const uint32_t hi = (uint32_t)(r1 - (t1 - 1 - a.tile_begin) * 64);  // 1..64 lanes of the last tile
+        lmask = hi >= 64 ? ~0ull : (1ull << hi) - 1ull;
+        if (r0 == r1) t1 = t0;
+    } else {
+        t0 = a.tile_begin + ntiles * gw / total;
+        t1 = a.tile_begin + ntiles * (gw + 1) / total;
+    }
     // (queries null: one query inline in the kernel arguments, StreamJob::qin)
     const float4 *qsrc = a.queries ? reinterpret_cast<const float4 *>(a.queries) : reinterpret_cast<const float4 *>(j.qin);
     for (uint32_t q = 0; q < a.nq; q++) {
         const float4 *q4 = qsrc + (size_t)q * (a.qpitch / 4);
         WaveTopK<E> tk;
         tk.init((int)a.k);
-        scan_tiles<METRIC, D, E>(a, q4, t0, t1, tk, (a.reverse + q) & 1u);  // serpentine over the queries
-        group_combine_publish<E, SCAN_WAVES>(tk, j.partials + ((size_t)q * G + blockIdx.x) * a.k, j.arrivals + q);
+        scan_tiles<METRIC, D, E>(a, q4, t0, t1, tk, (a.reverse + q) & 1u, 0, fmask, lmask);  // serpentine
+        group_combine_publish<E, SCAN_WAVES>(tk, j.partials + ((size_t)q * G + blockIdx.x) * a.k, j.arrivals + q,
+                                             j.ready ? j.ready + (size_t)q * G + blockIdx.x : nullptr,
+                                             j.ready_tag + q);
     }
 }
 

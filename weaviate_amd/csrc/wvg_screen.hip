@@ -1272,6 +1272,413 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
 }
 
 // ---------------------------------------------------------------------------
+// K3e (round 5): K3d with 32x32x16 bf16 MFMAs.  K3d's 16x16x32 MFMA takes 16
+// cycles of the matrix pipe and holds the wave's issue for 8 of them, so per
+// 32-deep unit (32 MFMAs, 512 pipe cycles) only ~256 issue cycles are left for
+// the unit's 16 ds_read_b128, 4 LDS-DMA pieces (~60 cycles each among MFMAs,
+// MI355X_MICROARCH.md) and the barrier: one wave per SIMD cannot keep the pipe
+// busy (K3d counters: MFMA busy 40 %).  v_mfma_f32_32x32x16_bf16 does the same
+// work in half the instructions -- 16 per unit, 32 pipe cycles each, 8 of them
+// issue -- which leaves ~384 issue cycles per unit for the same reads, DMA and
+// barrier.  Registers, LDS ring, loads, waits and barriers are K3d's.
+//   A operand = the wave's 32 queries (resident; lane l: query l % 32, k 8 (l / 32) + 0..7
+//   of each 16-deep step -- gathered once from qfrag's 16 x 32 fragments);
+//   B operand = 32 rows of the row block (lane l: row l % 32 of the group, same k),
+//   read straight from the ring's 16 x 32 fragments with a per-lane address
+//   (conflict-free: the 16 lanes of each ds_read_b128 group hit 16 distinct
+//   16-byte bank groups);
+//   C: lane l holds row n = 32 g + (l & 31) of row group g and queries
+//   m = 8 (r >> 2) + 4 (l >> 5) + (r & 3), r = 0..15.
+// Epilogue: per lane and query slot r the largest raw score of its 8 rows +
+// E(its rows' largest norm) against WS (a superset test of every element);
+// one ballot per slot gives 16 wave-uniform bits, each covering two queries
+// (lanes 0-31 and 32-63) x 256 rows; an active slot's two lists sit in lanes
+// 0-15 and 32-47 of one register and survivors are inserted as in K3d.
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+template <int KBN, int DIAG = 0>
+__global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar32_kernel(ScreenArgs a)
+{
+    static_assert(KBN % SD_NBUF == 0, "the stage buffer of a K block must be a compile-time constant");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint64_t *lists = reinterpret_cast<uint64_t *>(smem + SD_RING);  // [4][32][M]
+    float *tau = reinterpret_cast<float *>(smem + SD_RING + SD_LISTS);
+    float *sig = tau + SD_WAVES * 32;
+    float *ck1 = sig + SD_WAVES * 32;
+    float *ck2 = ck1 + SD_BQ;
+    float *cem = ck2 + SD_BQ;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int K = (int)a.k, M = SCREEN_M;
+    const int cosine = a.cosine;
+    const uint32_t b = blockIdx.x;
+    uint32_t qb, rr;
+    if (a.nrr_l % 8 == 0) {
+        const uint32_t xcd = b % 8, wv = b / 8;
+        qb = wv % a.nqb;
+        rr = a.rr0 + (wv / a.nqb) * 8 + xcd;
+    } else {
+        qb = b % a.nqb;
+        rr = a.rr0 + b / a.nqb;
+    }
+    const uint64_t ntiles = a.tile_end - a.tile_begin;
+    const uint64_t nblk = (ntiles + 3) / 4;
+    const uint64_t blk0 = nblk * rr / a.nrr, blk1 = nblk * (rr + 1) / a.nrr;
+    const uint32_t q0 = qb * SD_BQ;
+
+    for (int i = tid; i < SD_BQ; i += SD_WAVES * 64) {
+        const uint32_t q = q0 + (uint32_t)i;
+        ck1[i] = a.k1[q];
+        ck2[i] = a.k2[q];
+        cem[i] = a.emax[q];
+    }
+    for (int i = tid; i < SD_WAVES * 32; i += SD_WAVES * 64) {
+        const uint32_t q = q0 + (uint32_t)i;
+        const uint32_t g = q < a.nq ? __hip_atomic_load(a.gbound + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        const float t = q >= a.nq ? -__builtin_inff() : (g == 0xFFFFFFFFu ? __builtin_inff() : wvg_unord_f32(g));
+        tau[i] = t;
+        sig[i] = q >= a.nq ? __builtin_inff() : sc_sigma(t, cosine);
+    }
+    for (int i = tid; i < SD_WAVES * 32 * M; i += SD_WAVES * 64) lists[i] = WVG_KEY_NONE;
+    __syncthreads();
+    const uint32_t laddr = (uint32_t)(uintptr_t)(lists + (size_t)w * 32 * M);
+    const uint32_t tbase = (uint32_t)(uintptr_t)(tau + w * 32);
+    if (blk0 < blk1) {
+        // the wave's 32 queries, every K block and step, resident for the whole range
+        bf16x8 areg[KBN][2];
+        constexpr int SD_AKB = 6;  // K blocks whose fragments live in AGPRs (as K3d)
+        {
+            const uint32_t ql = (uint32_t)lane & 31u;
+            const uint4 *qsrc = a.qfrag + (size_t)(qb * 8 + 2 * w + (ql >> 4)) * KBN * 64 + (ql & 15u);
+#pragma unroll
+            for (int ks = 0; ks < KBN; ks++)
+#pragma unroll
+                for (int st = 0; st < 2; st++) {
+                    const uint4 *src = qsrc + (size_t)ks * 64 + (2 * st + (lane >> 5)) * 16;
+                    if (ks < SD_AKB)
+                        asm volatile("global_load_dwordx4 %0, %1, off" : "=a"(areg[ks][st]) : "v"(src) : "memory");
+                    else
+                        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(areg[ks][st]) : "v"(src) : "memory");
+                }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int ks = 0; ks < KBN; ks++)
+#pragma unroll
+            for (int st = 0; st < 2; st++) {
+                if (ks < SD_AKB)
+                    asm volatile("" : "+a"(areg[ks][st]));
+                else
+                    asm volatile("" : "+v"(areg[ks][st]));
+            }
+
+        // the stage loads: K3d's (wave w moves tile w's four 16-row fragments; unit 0 also
+        // its norms, wave 0 the block's tile words)
+        const uint4 *lsrc = a.shadow + ((size_t)(a.tile_begin + blk0 * 4 + w) * KBN * 4) * 64 + lane;
+        const float *lnorm = a.norms + (a.tile_begin + blk0 * 4 + w) * 64 + lane;
+        uint64_t lblk = blk0;
+        auto load_stage = [&](int ks) {
+            unsigned char *dst = smem + (ks % SD_NBUF) * SD_STAGE;
+#pragma unroll
+            for (int rg = 0; rg < 4; rg++)
+                __builtin_amdgcn_global_load_lds(lsrc + ((size_t)ks * 4 + rg) * 64,
+                                                 reinterpret_cast<uint4 *>(dst + (4 * w + rg) * 1024), 16, 0, 0);
+            unsigned char *nslot = smem + SD_NBUF * SD_STAGE + (lblk & 1) * SD_NSLOT;
+            if (ks == 0)
+                __builtin_amdgcn_global_load_lds(lnorm, reinterpret_cast<float *>(nslot + w * 256), 4, 0, 0);
+            if (ks == 0 && w == 0) {
+                const uint32_t wi = (uint32_t)(lane & 7) >> 1, half = lane & 1;
+                const uint64_t t = a.tile_begin + lblk * 4 + wi;
+                const uint32_t *src =
+                    reinterpret_cast<const uint32_t *>(a.valid + (t < a.tile_end ? t : a.tile_end - 1)) + half;
+                if (lane >= 8 && lane < 16 && a.allow) {
+                    const uint64_t aw = t - a.allow_t0;
+                    src = reinterpret_cast<const uint32_t *>(a.allow + (aw < a.allow_words ? aw : 0)) + half;
+                }
+                __builtin_amdgcn_global_load_lds(src, reinterpret_cast<uint32_t *>(nslot + 1024), 4, 0, 0);
+            }
+            if (ks == KBN - 1 && lblk + 1 < blk1) {
+                ++lblk;
+                lsrc += (size_t)4 * KBN * 4 * 64;
+                lnorm += 256;
+            }
+        };
+        auto wait_next = [&](auto KS) {
+            constexpr int ks = decltype(KS)::value;
+            constexpr int n0 = sd_younger<KBN, 0>(ks + 1, SD_NBUF - 3, true);
+            constexpr int n1 = sd_younger<KBN, 0>(ks + 1, SD_NBUF - 3, false);
+            if (w == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n0) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n1) : "memory");
+        };
+        auto raw_barrier = [&]() {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+        };
+        // B fragments of step st (8 row groups of 32) straight into AGPRs: lane l reads row
+        // l % 32 of group g, k 8 (2 st + l / 32) .. + 7 of the unit, i.e. 16-row fragment
+        // 2 g + ((l & 31) >> 4), lane (2 st + l / 32) * 16 + (l & 15) of it
+        const uint32_t rbase = (uint32_t)(uintptr_t)smem + (uint32_t)(lane >> 5) * 256u +
+                               (uint32_t)((lane & 31) >> 4) * 1024u + (uint32_t)(lane & 15) * 16u;
+        auto read_half = [&](int ks, int st, bf16x8 (&br)[8]) {
+            const uint32_t soff = (uint32_t)((ks % SD_NBUF) * SD_STAGE + st * 512);
+            uint32_t tmp;
+            asm volatile("v_add_u32 %8, %9, %10\n\t"
+                         "ds_read_b128 %0, %8\n\t"
+                         "ds_read_b128 %1, %8 offset:2048\n\t"
+                         "ds_read_b128 %2, %8 offset:4096\n\t"
+                         "ds_read_b128 %3, %8 offset:6144\n\t"
+                         "ds_read_b128 %4, %8 offset:8192\n\t"
+                         "ds_read_b128 %5, %8 offset:10240\n\t"
+                         "ds_read_b128 %6, %8 offset:12288\n\t"
+                         "ds_read_b128 %7, %8 offset:14336"
+                         : "=a"(br[0]), "=a"(br[1]), "=a"(br[2]), "=a"(br[3]), "=a"(br[4]), "=a"(br[5]), "=a"(br[6]),
+                           "=a"(br[7]), "=&v"(tmp)
+                         : "s"(soff), "v"(rbase)
+                         : "memory");
+        };
+        auto wait_b0 = [&](bf16x8 (&br)[8]) {
+            asm volatile("s_waitcnt lgkmcnt(8)"
+                         : "+a"(br[0]), "+a"(br[1]), "+a"(br[2]), "+a"(br[3]), "+a"(br[4]), "+a"(br[5]), "+a"(br[6]),
+                           "+a"(br[7])
+                         :
+                         : "memory");
+        };
+        // this lane's queries: m(r) = 8 (r >> 2) + qh + (r & 3), qh = 4 (l >> 5)
+        const int qh = 4 * (lane >> 5);
+        const uint32_t sbase = (uint32_t)(uintptr_t)smem;
+        const uint32_t nbase = sbase + 4u * (uint32_t)(lane & 31);  // norm of row 32 g + (l & 31): + 128 g
+        const uint32_t csoff = (uint32_t)((uintptr_t)sig - (uintptr_t)smem);
+        bool lane_force = false;
+#pragma unroll
+        for (int r = 0; r < 16; r++)
+            if (!(ck1[32 * w + 8 * (r >> 2) + qh + (r & 3)] <= 0x1p50f)) lane_force = true;
+
+        floatx16 acc[8];
+#pragma unroll
+        for (int g = 0; g < 8; g++)
+#pragma unroll
+            for (int e = 0; e < 16; e++) acc[g][e] = 0.f;
+        bf16x8 b0[8], b1[8];
+#pragma unroll
+        for (int ks = 0; ks < SD_NBUF - 1; ks++) load_stage(ks);
+        if (w == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(sd_younger<KBN, 0>(0, SD_NBUF - 2, true)) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(sd_younger<KBN, 0>(0, SD_NBUF - 2, false)) : "memory");
+        raw_barrier();
+        read_half(0, 0, b0);
+        for (uint64_t blk = blk0; blk < blk1; blk++) {
+            sd_static_for<KBN>([&](auto KS) {
+                constexpr int ks = decltype(KS)::value;
+                read_half(ks, 1, b1);
+                wait_b0(b0);
+#pragma unroll
+                for (int g = 0; g < 8; g++)
+                    acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(areg[ks][0], b0[g], acc[g], 0, 0, 0);
+                wait_next(KS);
+                raw_barrier();  // (lgkmcnt(0): this wave's second-step reads done)
+#pragma unroll
+                for (int j = 0; j < 8; j++) asm volatile("" : "+a"(b1[j]));
+                load_stage((ks + SD_NBUF - 1) % KBN);  // unit + 7 into the buffer of unit - 1
+                if (ks + 1 < KBN) read_half(ks + 1, 0, b0);
+#pragma unroll
+                for (int g = 0; g < 8; g++)
+                    acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(areg[ks][1], b1[g], acc[g], 0, 0, 0);
+            });
+            // 32x32x16: 16 passes, 18 wait states before a VALU reads its result (agpr_read
+            // is inline asm the hazard recognizer does not see)
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr ((DIAG & 2) == 0) {
+                const uint32_t nsoff = (uint32_t)(SD_NBUF * SD_STAGE + (blk & 1) * SD_NSLOT);
+                float nrm[8];
+                {
+                    uint32_t tmp;
+                    asm volatile("v_add_u32 %8, %9, %10\n\t"
+                                 "ds_read_b32 %0, %8\n\t"
+                                 "ds_read_b32 %1, %8 offset:128\n\t"
+                                 "ds_read_b32 %2, %8 offset:256\n\t"
+                                 "ds_read_b32 %3, %8 offset:384\n\t"
+                                 "ds_read_b32 %4, %8 offset:512\n\t"
+                                 "ds_read_b32 %5, %8 offset:640\n\t"
+                                 "ds_read_b32 %6, %8 offset:768\n\t"
+                                 "ds_read_b32 %7, %8 offset:896\n\t"
+                                 "s_waitcnt lgkmcnt(0)"
+                                 : "=v"(nrm[0]), "=v"(nrm[1]), "=v"(nrm[2]), "=v"(nrm[3]), "=v"(nrm[4]),
+                                   "=v"(nrm[5]), "=v"(nrm[6]), "=v"(nrm[7]), "=&v"(tmp)
+                                 : "s"(nsoff), "v"(nbase)
+                                 : "memory");
+                }
+                float nmax = nrm[0], nsum = nrm[0];
+#pragma unroll
+                for (int g = 1; g < 8; g++) nmax = __builtin_fmaxf(nmax, nrm[g]), nsum += nrm[g];
+                const bool force = lane_force || !(nmax <= 0x1p60f) || nsum != nsum;
+                uint32_t wact = 0;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    // queries 32 w + 8 i + qh + 0..3: sig, ck1, ck2 (128-float arrays, +512 / +1024 B)
+                    const uint32_t coff = (uint32_t)(csoff + 4 * (32 * w + 8 * i));
+                    const uint32_t qbase = sbase + 4u * (uint32_t)qh;
+                    float4 k1v, k2v, sv;
+                    uint32_t tmp;
+                    asm volatile("v_add_u32 %3, %4, %5\n\t"
+                                 "ds_read_b128 %0, %3 offset:512\n\t"
+                                 "ds_read_b128 %1, %3 offset:1024\n\t"
+                                 "ds_read_b128 %2, %3\n\t"
+                                 "s_waitcnt lgkmcnt(0)"
+                                 : "=v"(k1v), "=v"(k2v), "=v"(sv), "=&v"(tmp)
+                                 : "s"(coff), "v"(qbase)
+                                 : "memory");
+                    const float k1r[4] = {k1v.x, k1v.y, k1v.z, k1v.w}, k2r[4] = {k2v.x, k2v.y, k2v.z, k2v.w};
+                    const float svr[4] = {sv.x, sv.y, sv.z, sv.w};
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const int r = 4 * i + j;
+                        float m = agpr_read(acc[0][r]);
+#pragma unroll
+                        for (int g = 1; g < 8; g++) m = __builtin_fmaxf(m, agpr_read(acc[g][r]));
+                        const float t = (m + __builtin_fmaf(nmax, k1r[j], k2r[j])) - svr[j];
+                        if (__ballot(force || t >= 0.f)) wact |= 1u << r;
+                    }
+                }
+                if (wact != 0 && (DIAG & 4) == 0) {
+                    uint64_t vm[4];
+                    {
+                        uint4 vw0, vw1, aw0, aw1;
+                        uint32_t tmp;
+                        asm volatile("v_add_u32 %4, %5, %6\n\t"
+                                     "ds_read_b128 %0, %4 offset:1024\n\t"
+                                     "ds_read_b128 %1, %4 offset:1040\n\t"
+                                     "ds_read_b128 %2, %4 offset:1056\n\t"
+                                     "ds_read_b128 %3, %4 offset:1072\n\t"
+                                     "s_waitcnt lgkmcnt(0)"
+                                     : "=v"(vw0), "=v"(vw1), "=v"(aw0), "=v"(aw1), "=&v"(tmp)
+                                     : "s"(nsoff), "v"(sbase)
+                                     : "memory");
+                        const uint64_t words[4] = {((uint64_t)vw0.y << 32) | vw0.x, ((uint64_t)vw0.w << 32) | vw0.z,
+                                                   ((uint64_t)vw1.y << 32) | vw1.x, ((uint64_t)vw1.w << 32) | vw1.z};
+                        const uint64_t allows[4] = {((uint64_t)aw0.y << 32) | aw0.x, ((uint64_t)aw0.w << 32) | aw0.z,
+                                                    ((uint64_t)aw1.y << 32) | aw1.x, ((uint64_t)aw1.w << 32) | aw1.z};
+#pragma unroll
+                        for (int h = 0; h < 4; h++) {
+                            const uint64_t t = a.tile_begin + blk * 4 + h;
+                            uint64_t m = t < a.tile_end ? readfirstlane64(words[h]) : 0ull;
+                            if (a.allow) {
+                                const uint64_t aw = t - a.allow_t0;
+                                m &= aw < a.allow_words ? readfirstlane64(allows[h]) : 0ull;
+                            }
+                            vm[h] = m;
+                        }
+                    }
+                    const uint64_t slot0 = (a.tile_begin + blk * 4) * 64;
+                    // live rows of each row group g (lane l: row 32 g + (l & 31))
+                    uint64_t live[8];
+#pragma unroll
+                    for (int g = 0; g < 8; g++)
+                        live[g] = __ballot((vm[g >> 1] >> (32 * (g & 1) + (lane & 31))) & 1ull);
+                    const int hrow = 2 * (lane >> 5);  // the list row (16 lanes) of this lane's query
+                    const int li = lane & 15;
+                    for (uint32_t gw = wact; gw; gw &= gw - 1) {
+                        const int r = __builtin_ctz(gw);
+                        float uv[8];
+                        switch (r) {
+#define WVG_SE_SLOT(R)                                                                          \
+    case R:                                                                                     \
+        _Pragma("unroll") for (int g = 0; g < 8; g++) uv[g] = agpr_read(acc[g][R]);           \
+        break;
+                        WVG_SE_SLOT(0) WVG_SE_SLOT(1) WVG_SE_SLOT(2) WVG_SE_SLOT(3)
+                        WVG_SE_SLOT(4) WVG_SE_SLOT(5) WVG_SE_SLOT(6) WVG_SE_SLOT(7)
+                        WVG_SE_SLOT(8) WVG_SE_SLOT(9) WVG_SE_SLOT(10) WVG_SE_SLOT(11)
+                        WVG_SE_SLOT(12) WVG_SE_SLOT(13) WVG_SE_SLOT(14) WVG_SE_SLOT(15)
+#undef WVG_SE_SLOT
+                        default: break;
+                        }
+                        const uint32_t ql = 8u * (uint32_t)(r >> 2) + (uint32_t)qh + (uint32_t)(r & 3);
+                        const uint32_t la = laddr + ql * (SCREEN_M * 8) + 8u * (uint32_t)li;
+                        const uint32_t ta = tbase + 4u * ql;  // tau; sig + 512, ck1 + 1024, ck2 + 1536, cem + 2048
+                        uint2 v2;
+                        float wt, ws, em, k1, k2;
+                        asm volatile("ds_read_b64 %0, %6\n\t"
+                                     "ds_read_b32 %1, %7\n\t"
+                                     "ds_read_b32 %2, %7 offset:512\n\t"
+                                     "ds_read_b32 %3, %7 offset:2048\n\t"
+                                     "ds_read_b32 %4, %7 offset:1024\n\t"
+                                     "ds_read_b32 %5, %7 offset:1536\n\t"
+                                     "s_waitcnt lgkmcnt(0)"
+                                     : "=v"(v2), "=v"(wt), "=v"(ws), "=v"(em), "=v"(k1), "=v"(k2)
+                                     : "v"(la), "v"(ta)
+                                     : "memory");
+                        uint64_t v = ((uint64_t)v2.y << 32) | v2.x;
+#pragma unroll
+                        for (int g = 0; g < 8; g++) {
+                            const float u = uv[g] + __builtin_fmaf(nrm[g], k1, k2);
+                            uint64_t pass = __ballot(!(u < ws)) & live[g];
+                            while (pass) {
+                                const int j = __builtin_ctzll(pass);
+                                pass &= pass - 1;
+                                const int gr = 2 * (j >> 5);  // the survivor's query's list row
+                                const float lower =
+                                    sc_lower(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(u), j)), cosine);
+                                float wtg = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wt), j));
+                                if (!(lower <= wtg)) continue;
+                                const uint64_t key = ((uint64_t)wvg_ord_f32(lower) << 32) |
+                                                     (uint32_t)(slot0 + 32u * (uint32_t)g + (uint32_t)(j & 31));
+                                if (!(key < readlane64(v, 16 * gr + SCREEN_M - 1))) continue;
+                                const bool inrow = (lane >> 4) == gr;
+                                const int pos = __popcll(__ballot(inrow && v < key));
+                                const uint64_t sh = row_shr1_64(v);
+                                v = inrow ? (li > pos ? sh : (li == pos ? key : v)) : v;
+                                const uint64_t nk = readlane64(v, 16 * gr + K - 1);
+                                const uint64_t nm = readlane64(v, 16 * gr + SCREEN_M - 1);
+                                const float emg = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(em), j));
+                                if (nk != WVG_KEY_NONE) wtg = fminf(wtg, sc_tau_k(key_lower(nk), emg, cosine));
+                                if (nm != WVG_KEY_NONE) wtg = fminf(wtg, key_lower(nm));
+                                const float wsg = sc_sigma(wtg, cosine);
+                                const bool mine = (lane >> 5) == (j >> 5);  // lanes of the survivor's query
+                                wt = mine ? wtg : wt;
+                                ws = mine ? wsg : ws;
+                                // that query's other survivors of this row group meet the new threshold
+                                pass &= ~(0xFFFFFFFFull << (32 * (j >> 5))) | __ballot(!(u < ws));
+                            }
+                        }
+                        const uint2 o2 = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+                        if (((lane >> 4) & 1) == 0) asm volatile("ds_write_b64 %0, %1" ::"v"(la), "v"(o2) : "memory");
+                        if ((lane & 31) == 0)
+                            asm volatile("ds_write_b32 %0, %1\n\t"
+                                         "ds_write_b32 %0, %2 offset:512" ::"v"(ta), "v"(wt), "v"(ws)
+                                         : "memory");
+                    }
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                }
+            } else if constexpr ((DIAG & 8) != 0) {
+                float x = 0.f;
+#pragma unroll
+                for (int g = 0; g < 8; g++) x += agpr_read(acc[g][0]);
+                if (x == 0x1p-120f) a.partials[0] = 0;
+            }
+#pragma unroll
+            for (int g = 0; g < 8; g++)
+#pragma unroll
+                for (int e = 0; e < 16; e++) acc[g][e] = 0.f;
+            read_half(0, 0, b0);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int ql = 0; ql < 32; ql++) {
+        const uint32_t q = q0 + (uint32_t)(32 * w + ql);
+        if (q >= a.nq) break;
+        const uint64_t x = lane < M ? lists[((size_t)w * 32 + ql) * M + lane] : WVG_KEY_NONE;
+        uint64_t *out = a.partials + ((size_t)q * a.nrr + rr) * M;
+        if (lane < M) out[lane] = x;
+        if (lane == K - 1 && x != WVG_KEY_NONE) {
+            const float t = sc_tau_k(key_lower(x), cem[32 * w + ql], cosine);
+            atomicMin(a.gbound + q, wvg_ord_f32(t));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Collect, per query.  Every range list holds its range's SCREEN_M smallest
 // lower bounds, so their union holds the global k smallest: tau* = the k-th
 // smallest lower of the union + 2 Emax is a valid bound (k rows at or below
@@ -1536,11 +1943,17 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
                hipFuncSetAttribute(reinterpret_cast<const void *>(&screen_ar_kernel<16>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, SD_LDS) == hipSuccess &&
                hipFuncSetAttribute(reinterpret_cast<const void *>(&screen_ar_kernel<24>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, SD_LDS) == hipSuccess &&
+               hipFuncSetAttribute(reinterpret_cast<const void *>(&screen_ar32_kernel<16>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, SD_LDS) == hipSuccess &&
+               hipFuncSetAttribute(reinterpret_cast<const void *>(&screen_ar32_kernel<24>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, SD_LDS) == hipSuccess;
     }();
     (void)attr;
     // K3d (queries resident in registers) where its template applies, else K3c
     void (*kern)(ScreenArgs) = kbn == 24 ? &screen_ar_kernel<24> : kbn == 16 ? &screen_ar_kernel<16> : nullptr;
+    if (tuning().screen_variant == 2 && kern)  // K3e (32x32x16 MFMAs)
+        kern = kbn == 24 ? &screen_ar32_kernel<24> : &screen_ar32_kernel<16>;
 #ifdef WVG_TOOLS
     if (kbn == 24) {  // K3d diagnostics: separately compiled instantiations
         switch (tuning().screen_diag) {
@@ -1562,7 +1975,8 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
         case 1034: kern = &screen_ar_kernel<24, 1034>; break;  // 10 with one barrier per two K blocks
         default: break;
         }
-        if (kern != &screen_ar_kernel<24>)
+        if (tuning().screen_variant == 2 && tuning().screen_diag == 10) kern = &screen_ar32_kernel<24, 10>;
+        if (kern != &screen_ar_kernel<24> && kern != &screen_ar32_kernel<24>)
             (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                       SD_LDS);
     }

@@ -317,9 +317,11 @@ static int run_screen(wvg_corpus *c, const ScanArgs &a, const SearchPlan &p, cha
 // Runs phase 1 + phase 2 for one corpus with device-resident prepared queries.
 // One query of a host call on the query-stream kernel with its in-launch merge
 // (run_search); its results can then go straight to host memory.
+// (a filtered query too: its allow window is copied with the call, the scan masks tiles with it)
 static bool inlaunch_single(const wvg_corpus *c, uint32_t nq, const SearchPlan &p, bool has_allow)
 {
-    return nq == 1 && !p.gemm && !p.cosched && !has_allow && c->kind == WVG_KIND_F32 && tuning().pipeline_mode == 1;
+    (void)has_allow;
+    return nq == 1 && !p.gemm && !p.cosched && c->kind == WVG_KIND_F32 && tuning().pipeline_mode == 1;
 }
 
 int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t nq, uint32_t k, const uint64_t *d_allow,
@@ -390,6 +392,13 @@ int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t nq, uin
             j.tag = so->tag;
             j.legacy_poll = so->legacy_poll ? 1u : 0u;
         }
+        j.row_split = (tuning().stream_variant & 1) == 0;
+        // per-list hand-offs: the slot's ready words (zeroed once), tagged with the call's tag
+        const bool ready = (tuning().stream_variant & 2) == 0 && so && so->tag && (uint32_t)p.groups <= SLOT_READY_MAX;
+        if (ready) {
+            j.ready = ctl + SLOT_READY_OFF;
+            j.ready_tag = so->tag;
+        }
         if (!d_q) {  // the query in the kernel arguments
             if (!qhost || qpitch > STREAM_QIN_FLOATS) return fail(WVG_ERR_INVALID, "inline query missing or too long");
             std::memcpy(j.qin, qhost, (size_t)qpitch * 4);
@@ -398,7 +407,7 @@ int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t nq, uin
         ProfArm arm(c->ctx);
         if (arm.rc) return arm.rc;
         WVG_HIP(launch_scan_f32_stream(a, j, s));
-        sl->arrival_base += (uint32_t)p.groups;
+        if (!ready) sl->arrival_base += (uint32_t)p.groups;
         return WVG_OK;
     }
     ProfArm arm(c->ctx);
@@ -810,9 +819,11 @@ static int wvg::search_batch(wvg_corpus *c, const float *queries, uint32_t nq, u
             if (out_dists) std::memcpy(out_dists + i, &r[i].z, 4);
         }
         const uint32_t c0 = r[k].x;
-        if (out_counts) *out_counts = c0;
-        if (c->count > 0 && c0 == 0)  // a live row exists: 0 results = the in-launch merge gave up
+        if (c0 == WVG_RECORDS_TIMEOUT) {  // the in-launch merge gave up (empty entries were written)
+            if (out_counts) *out_counts = 0;
             return fail(WVG_ERR_DEVICE, "single-query merge timed out waiting for the scan workgroups");
+        }
+        if (out_counts) *out_counts = c0;
         return WVG_OK;
     }
     char *rspan = zc ? hc : b + o_ids;  // the result span [ids | dists | counts]
@@ -1022,16 +1033,18 @@ int wvg_search_bq_rescore(wvg_corpus *bq, wvg_corpus *f32, const float *queries,
 static const size_t WS_STATUS_BYTES = 256;
 
 // Workspace of the query-stream scan (after the status block): partial lists
-// [nq][groups][k], then the per-query arrival counters.
+// [nq][groups][k], then the per-query arrival counters and the per-list ready
+// words [nq][groups] (both zeroed per call by one memset).
 struct StreamLayout {
-    size_t partials = 0, arrivals = 0, total = 0;
+    size_t partials = 0, arrivals = 0, ready = 0, total = 0;
 };
 static StreamLayout stream_layout(const SearchPlan &p1, uint32_t nq, uint32_t k)
 {
     StreamLayout l;
     l.partials = WS_STATUS_BYTES;
     l.arrivals = l.partials + align_up((size_t)nq * p1.groups * k * 8, 256);
-    l.total = l.arrivals + align_up((size_t)nq * 4, 256);  // memset block: 16-B multiple
+    l.ready = l.arrivals + align_up((size_t)nq * 4, 256);
+    l.total = l.ready + align_up((size_t)nq * p1.groups * 4, 256);  // memset block: 16-B multiple
     return l;
 }
 
@@ -1111,8 +1124,13 @@ int wvg_search_device_pipelined(wvg_corpus *c, const float *d_queries, uint32_t 
         a.reverse = next_direction(c, nq);
         a.order512 = c->ctx->order512;
         a.plain = plain_loads(c, p.tb, p.te);
-    a.cache_tail256 = k1_cache_tail(c, p.tb, p.te);
-        WVG_HIP(hipMemsetAsync(j.arrivals, 0, align_up((size_t)nq * 4, 16), s));
+        a.cache_tail256 = k1_cache_tail(c, p.tb, p.te);
+        j.row_split = (tuning().stream_variant & 1) == 0;
+        if ((tuning().stream_variant & 2) == 0) {  // per-list hand-offs; the words are zeroed with the counters
+            j.ready = (uint32_t *)(w + l.ready);
+            j.ready_tag = 1;
+        }
+        WVG_HIP(hipMemsetAsync(j.arrivals, 0, l.total - l.arrivals, s));
         ProfArm arm(c->ctx);
         if (arm.rc) return arm.rc;
         WVG_HIP(launch_scan_f32_stream(a, j, s));
