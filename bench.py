@@ -65,6 +65,8 @@ def parse(argv=None):
     ap.add_argument("--scale-legs", default="slab1b,pq",
                     help="strong-scaling legs at every N (comma list; '' = none): slab1b = configs[4] 1B x 128 as 8 "
                          "slabs dealt to the N GPUs, pq = configs[3] 100M PQ sharded over the N GPUs")
+    ap.add_argument("--s1b-rows", type=int, default=1_000_000_000, help="rows of the slab1b scale leg (tests: less)")
+    ap.add_argument("--pq-rows", type=int, default=100_000_000, help="rows of the sharded PQ scale leg (tests: less)")
     ap.add_argument("--profile-run", action="store_true",
                     help="only the timed headline launches (no no-reuse leg, read probe or CPU baseline), so a "
                          "rocprofv3 --stats summary of the scan kernel covers exactly the launches `roofline` times")
@@ -997,9 +999,12 @@ def run_flat1m(args, world, rank, dev, torch, dist):
             t0 = time.perf_counter()
             try:
                 if name == "slab1b":
-                    legs["config5_1b_x_128"] = slab1b_leg(world, rank, dev, torch, dist)
+                    if 8 % world:  # the 8 slabs are dealt evenly (the driver's N = 1, 2, 4, 8)
+                        legs["config5_1b_x_128"] = {"skipped": f"8 slabs do not deal evenly to {world} GPUs"}
+                    else:
+                        legs["config5_1b_x_128"] = slab1b_leg(world, rank, dev, torch, dist, total=args.s1b_rows)
                 elif name == "pq":
-                    legs["config4_pq_sharded"] = pq_sharded_leg(world, rank, dev, torch, dist)
+                    legs["config4_pq_sharded"] = pq_sharded_leg(world, rank, dev, torch, dist, n=args.pq_rows)
             except Exception as e:  # noqa: BLE001 -- a failed leg is reported, the headline stands
                 legs[f"{name}_error"] = f"{type(e).__name__}: {e}"
             if rank == 0:
@@ -1083,7 +1088,7 @@ def slab1b_leg(world, rank, dev, torch, dist, total=1_000_000_000, d=128, k=100,
     per = (total + S - 1) // S
     per = (per + 63) // 64 * 64
     if S % world:
-        raise SystemExit(f"bench.py: slab1b deals {S} slabs evenly, --gpus must divide {S}")
+        raise ValueError(f"slab1b deals {S} slabs evenly, --gpus must divide {S}")
     mine = [s for s in range(S) if s % world == rank]
     L = len(mine)
     ctx = Context(dev.index)
@@ -1281,6 +1286,8 @@ def pq_sharded_leg(world, rank, dev, torch, dist, n=100_000_000, d=128, m=32, ks
 
 
 def run_slab1b(args, world, rank, dev, torch, dist):
+    if 8 % world:
+        raise SystemExit(f"bench.py: slab1b deals 8 slabs evenly, --gpus must divide 8")
     r = slab1b_leg(world, rank, dev, torch, dist, args.rows, args.dim, args.k, args.batch, args.steps, args.warmup)
     total, d, k = args.rows, args.dim, args.k
     return {

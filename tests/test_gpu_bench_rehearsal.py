@@ -27,9 +27,19 @@ def run_bench(*args, timeout=240):
 
 @pytest.mark.parametrize("gpus", [2, 3])
 def test_flat_share_gpu_exchange_and_merge(gpus):
-    out = run_bench("--gpus", str(gpus), "--share-gpu", "--rows", "300000", "--steps", "3", "--warmup", "1")
+    out = run_bench("--gpus", str(gpus), "--share-gpu", "--rows", "300000", "--steps", "3", "--warmup", "1",
+                    "--s1b-rows", "4000000", "--pq-rows", "400000")
     assert out["n_gpus"] == gpus and out["value"] > 0
     assert out["merge_check"]["ok"] is True, out["merge_check"]
+    # the strong-scaling legs the driver's SCALE line carries (configs[4] and configs[3]), at test sizes
+    legs = out["configs"]
+    if gpus == 3:
+        assert "skipped" in legs["config5_1b_x_128"]
+    else:
+        assert legs["config5_1b_x_128"]["slabs_per_gpu"] == 8 // gpus
+        assert legs["config5_1b_x_128"]["merge_check"]["ok"] is True, legs["config5_1b_x_128"]
+    assert legs["config4_pq_sharded"]["merge_check"]["ok"] is True, legs["config4_pq_sharded"]
+    assert legs["config4_pq_sharded"]["rows_per_gpu"] >= 400000 // gpus
 
 
 @pytest.mark.parametrize("gpus", [1, 2])

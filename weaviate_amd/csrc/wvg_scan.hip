@@ -264,20 +264,18 @@ __device__ __forceinline__ void scan_tiles(const ScanArgs &a, const float4 *q4, 
         m &= own;
         if (m == 0ull) continue;  // wave-uniform: nothing live/allowed in this tile
         const float4 *rp = data + (size_t)t * a.nchunks * 64 + lane;
-        auto dist = [&]() -> float {
-            if (a.order512)  // wave-uniform: the AVX-512 kernels' order (generic length)
-                return row_dist_512<METRIC, 64>(rp, q4, (int)a.dim);
-            else if constexpr (D > 0)
-                return i >= split ? row_dot_or_l2_fixed<METRIC, D, 64, false>(rp, q4)
-                                  : row_dot_or_l2_fixed<METRIC, D, 64>(rp, q4);
-            else
-                return row_dot_or_l2_generic<METRIC, 64>(rp, q4, (int)a.dim);
-        };
+        // ONE call site of the distance (a lambda called from two branches was not
+        // inlined: its captures then forced the kernel arguments into scratch); on a
+        // shared edge tile only this wave's lanes are active, so only they load
         float r = 0.0f;
-        if (own != ~0ull) {  // a shared edge tile (wave-uniform): only this wave's lanes load
-            if ((own >> lane) & 1ull) r = dist();
-        } else {
-            r = dist();
+        if ((own >> lane) & 1ull) {
+            if (a.order512)  // wave-uniform: the AVX-512 kernels' order (generic length)
+                r = row_dist_512<METRIC, 64>(rp, q4, (int)a.dim);
+            else if constexpr (D > 0)
+                r = i >= split ? row_dot_or_l2_fixed<METRIC, D, 64, false>(rp, q4)
+                               : row_dot_or_l2_fixed<METRIC, D, 64>(rp, q4);
+            else
+                r = row_dot_or_l2_generic<METRIC, 64>(rp, q4, (int)a.dim);
         }
         tk.offer(lane_key(m, wrap_metric(a.metric, r), t, lane));
     }

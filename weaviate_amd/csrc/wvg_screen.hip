@@ -1576,7 +1576,6 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar32_kernel(ScreenArg
 #pragma unroll
                     for (int g = 0; g < 8; g++)
                         live[g] = __ballot((vm[g >> 1] >> (32 * (g & 1) + (lane & 31))) & 1ull);
-                    const int hrow = 2 * (lane >> 5);  // the list row (16 lanes) of this lane's query
                     const int li = lane & 15;
                     for (uint32_t gw = wact; gw; gw &= gw - 1) {
                         const int r = __builtin_ctz(gw);

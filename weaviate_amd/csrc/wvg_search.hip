@@ -774,12 +774,16 @@ static int wvg::search_batch(wvg_corpus *c, const float *queries, uint32_t nq, u
     if (rc) return rc;
     uint32_t qpitch = 0;
     // a single in-launch F32 query of up to STREAM_QIN_FLOATS floats goes in the kernel arguments
-    std::vector<float> qinl;
+    alignas(16) float qinl[STREAM_QIN_FLOATS];  // (no heap allocation on the single-query path)
     const bool qin = inlaunch_single(c, nq, p, p.allow_host != nullptr) &&
                      (size_t)f32_chunks(c->dim) * 4 <= STREAM_QIN_FLOATS && (tuning().single_path & 1) == 0;
-    if (qin) {
-        std::vector<uint64_t> qb;
-        prepare_queries_host(c, queries, nq, qinl, qb, qpitch);
+    if (qin) {  // prepare_queries_host for one F32 query, into the kernel-argument buffer
+        qpitch = f32_chunks(c->dim) * 4;
+        for (uint32_t i = c->dim; i < qpitch; i++) qinl[i] = 0.0f;
+        if (c->metric == WVG_METRIC_COSINE)
+            normalize_host(queries, c->dim, qinl);
+        else
+            std::memcpy(qinl, queries, (size_t)c->dim * 4);
     } else {
         rc = stage_queries(c, g.slot, queries, nq, b + o_q, qpitch, (float *)(b + o_q), b + o_qtmp, &st);
         if (rc) return rc;
@@ -809,7 +813,7 @@ static int wvg::search_batch(wvg_corpus *c, const float *queries, uint32_t nq, u
     }
     if (zc && !legacy) {
         rc = run_search(c, qin ? nullptr : b + o_q, qpitch, nq, k, d_allow, p, (uint64_t *)(b + o_part), nullptr,
-                        nullptr, nullptr, s, g.slot, qin ? qinl.data() : nullptr, &so);
+                        nullptr, nullptr, s, g.slot, qin ? qinl : nullptr, &so);
         if (rc) return rc;
         rc = wait_records(so, k, s, (sp & 2) != 0);
         if (rc) return rc;
@@ -836,7 +840,7 @@ static int wvg::search_batch(wvg_corpus *c, const float *queries, uint32_t nq, u
     if (cflag) *cflag = 0xFFFFFFFFu;
     rc = run_search(c, qin ? nullptr : b + o_q, qpitch, nq, k, d_allow, p, (uint64_t *)(b + o_part), (uint64_t *)rspan,
                     (float *)(rspan + (o_d - o_ids)), (uint32_t *)(rspan + (o_cnt - o_ids)), s, g.slot,
-                    qin ? qinl.data() : nullptr, &so);
+                    qin ? qinl : nullptr, &so);
     if (rc) return rc;
     const char *pin = zc ? hc : out_b <= STAGE_MAX ? st.take(out_b) : nullptr;
     std::vector<char> big(pin ? 0 : out_b);
