@@ -409,8 +409,11 @@ struct Tuning {
                                   // pilot (0 = the K1 pilot; A/B)
     int screen_variant = 0;  // batched screen kernel: 0 = K3d where it applies (d = 512, 768), 1 = K3c,
                              // 2 = K3e (K3d with 32x32x16 MFMAs)
-    int stream_variant = 0;  // query-stream K1 (tuning key 25): bit 0 = tile-granular wave ranges, bit 1 = the
-                             // arrival-counter merge after all lists (round 4) instead of per-list hand-offs (A/B)
+    int stream_variant = 1;  // query-stream K1 (tuning key 25): bit 0 = tile-granular wave ranges (the default:
+                             // row-granular ranges let every wave touch one more, shared tile, and a wave's time
+                             // follows its tile count -- 85.1 vs 82.5 us per 1M-row query, profiles/r05/stream_ab/),
+                             // bit 1 = the arrival-counter merge after all lists (round 4) instead of the per-list
+                             // hand-offs (83.7 vs 82.5 us)
     int single_path = 0;     // single-query host calls: bit 0 = query staged by copy instead of in the kernel
                              // arguments, bit 1 = stream synchronization instead of polling, bit 2 = round 4's
                              // untagged layout (ids / dists + a polled count: returned the slot's previous result

@@ -789,7 +789,14 @@ static int wvg::search_batch(wvg_corpus *c, const float *queries, uint32_t nq, u
         if (rc) return rc;
     }
     const uint64_t *d_allow = nullptr;
-    if (p.allow_host) {
+    if (p.allow_host && inlaunch_single(c, nq, p, true) && p.allow_bytes() <= STAGE_MAX) {
+        // a single in-launch query reads its allow window straight from the slot's pinned
+        // staging over the bus (each wave's next tile word is prefetched a tile ahead): no
+        // host-to-device copy (~10 us of a 125 KB window's copy and its API time)
+        char *h = st.take(p.allow_bytes());
+        std::memcpy(h, p.allow_host, p.allow_bytes());
+        d_allow = reinterpret_cast<const uint64_t *>(h);
+    } else if (p.allow_host) {
         WVG_HIP(st.h2d(b + o_allow, p.allow_host, p.allow_bytes(), s));
         d_allow = (const uint64_t *)(b + o_allow);
     }
