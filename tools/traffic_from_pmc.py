@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                   "profiles", "traffic.json"))
     ap.add_argument("--note", default="")
+    ap.add_argument("--source", default="", help="where the counter file is committed (cited by bench.py)")
     a = ap.parse_args()
     vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(a.csv))
             if a.kernel in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE"]
@@ -47,6 +48,8 @@ def main():
         "method": "rocprofv3 --pmc FETCH_SIZE --kernel-trace, separate pass; FETCH_SIZE KiB x 1024 x 2 "
                   "(gfx950 half-count of 16 B/lane streaming reads); mean over launches",
     }
+    if a.source:
+        rec["source"] = a.source
     if a.note:
         rec["note"] = a.note
     db = json.load(open(a.out)) if os.path.exists(a.out) else {}
