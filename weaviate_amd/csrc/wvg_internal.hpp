@@ -408,7 +408,8 @@ struct Tuning {
     int screen_pilot_gemm = 512;  // K3c/K3d: tiles of the K3b (exact fp32 MFMA) pilot, which replaces the K1
                                   // pilot (0 = the K1 pilot; A/B)
     int screen_variant = 0;  // batched screen kernel: 0 = K3d where it applies (d = 512, 768), 1 = K3c,
-                             // 2 = K3e (K3d with 32x32x16 MFMAs)
+                             // 2 = K3e (K3d with 32x32x16 MFMAs), 3 = K3f (two waves per SIMD); 2 and 3
+                             // exist in the tools build only (profiles/r05/k3e, k3f)
     int stream_variant = 1;  // query-stream K1 (tuning key 25): bit 0 = tile-granular wave ranges (the default:
                              // row-granular ranges let every wave touch one more, shared tile, and a wave's time
                              // follows its tile count -- 85.1 vs 82.5 us per 1M-row query, profiles/r05/stream_ab/),

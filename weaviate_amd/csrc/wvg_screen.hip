@@ -1271,6 +1271,9 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
     }
 }
 
+constexpr int SF_WAVES = 8;  // K3f's waves per workgroup
+
+#ifdef WVG_TOOLS  // K3e and K3f: round-5 A/B variants (tools build only; the product runs K3d)
 // ---------------------------------------------------------------------------
 // K3e (round 5): K3d with 32x32x16 bf16 MFMAs.  K3d's 16x16x32 MFMA takes 16
 // cycles of the matrix pipe and holds the wave's issue for 8 of them, so per
@@ -1692,7 +1695,6 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar32_kernel(ScreenArg
 // issue stream, bounds the loop.  Ring, loads (2 pieces per wave), waits,
 // epilogue tests and lists are K3d's; lists and thresholds keep K3d's LDS
 // layout (wave w owns queries 16 w .. 16 w + 15 of the workgroup's 128).
-constexpr int SF_WAVES = 8;
 static_assert(SF_WAVES * 16 == SD_BQ && SD_WAVES * 32 == SD_BQ, "K3f keeps K3d's 128-query LDS layout");
 
 // Vector-memory loads one K3f wave issues for unit u: its 2 row-fragment
@@ -1835,7 +1837,7 @@ __global__ __launch_bounds__(SF_WAVES * 64) void screen_ar16_kernel(ScreenArgs a
         // The stage / quarter offset is an instruction literal (as SGPR operands the
         // 32 distinct offsets were hoisted into SGPRs and spilled).
         const uint32_t rbase = (uint32_t)(uintptr_t)smem + 16u * lane;
-        auto read_q = [rbase](auto KS, auto QQ, bf16x8 (&br)[4]) {
+        auto read_q = [](auto KS, auto QQ, bf16x8 (&br)[4], uint32_t rb) {
             constexpr uint32_t soff =
                 (uint32_t)((decltype(KS)::value % SD_NBUF) * SD_STAGE + decltype(QQ)::value * 4 * 1024);
             uint32_t tmp;
@@ -1845,7 +1847,7 @@ __global__ __launch_bounds__(SF_WAVES * 64) void screen_ar16_kernel(ScreenArgs a
                          "ds_read_b128 %2, %4 offset:2048\n\t"
                          "ds_read_b128 %3, %4 offset:3072"
                          : "=a"(br[0]), "=a"(br[1]), "=a"(br[2]), "=a"(br[3]), "=&v"(tmp)
-                         : "n"(soff), "v"(rbase)
+                         : "n"(soff), "v"(rb)
                          : "memory");
         };
         using I0 = std::integral_constant<int, 0>;
@@ -1879,17 +1881,17 @@ __global__ __launch_bounds__(SF_WAVES * 64) void screen_ar16_kernel(ScreenArgs a
         if (ex) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(sf_younger<KBN>(0, SD_NBUF - 2, true)) : "memory");
         else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(sf_younger<KBN>(0, SD_NBUF - 2, false)) : "memory");
         raw_barrier();
-        read_q(I0{}, I0{}, bq0);
+        read_q(I0{}, I0{}, bq0, rbase);
         for (uint64_t blk = blk0; blk < blk1; blk++) {
             sd_static_for<KBN>([&](auto KS) {
                 constexpr int ks = decltype(KS)::value;
-                read_q(KS, I1{}, bq1);
+                read_q(KS, I1{}, bq1, rbase);
                 wait_q(bq0);
                 mfma4(ks, 0, bq0);
-                read_q(KS, I2{}, bq0);
+                read_q(KS, I2{}, bq0, rbase);
                 wait_q(bq1);
                 mfma4(ks, 1, bq1);
-                read_q(KS, I3{}, bq1);
+                read_q(KS, I3{}, bq1, rbase);
                 wait_q(bq0);
                 mfma4(ks, 2, bq0);
                 wait_next(KS);  // the next unit landed
@@ -1897,7 +1899,7 @@ __global__ __launch_bounds__(SF_WAVES * 64) void screen_ar16_kernel(ScreenArgs a
 #pragma unroll
                 for (int j = 0; j < 4; j++) asm volatile("" : "+a"(bq1[j]));
                 load_stage((ks + SD_NBUF - 1) % KBN);  // into the buffer of unit - 1, read before the barrier
-                if constexpr (ks + 1 < KBN) read_q(std::integral_constant<int, ks + 1>{}, I0{}, bq0);
+                if constexpr (ks + 1 < KBN) read_q(std::integral_constant<int, ks + 1>{}, I0{}, bq0, rbase);
                 mfma4(ks, 3, bq1);
             });
             // XDL write -> VALU read of the accumulators through agpr_read: see K3d
@@ -2072,7 +2074,7 @@ __global__ __launch_bounds__(SF_WAVES * 64) void screen_ar16_kernel(ScreenArgs a
             }
 #pragma unroll
             for (int nr = 0; nr < 16; nr++) acc[nr] = (floatx4){0.f, 0.f, 0.f, 0.f};
-            read_q(I0{}, I0{}, bq0);
+            read_q(I0{}, I0{}, bq0, rbase);
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2089,6 +2091,8 @@ __global__ __launch_bounds__(SF_WAVES * 64) void screen_ar16_kernel(ScreenArgs a
         }
     }
 }
+
+#endif  // WVG_TOOLS
 
 // ---------------------------------------------------------------------------
 // Collect, per query.  Every range list holds its range's SCREEN_M smallest
@@ -2355,24 +2359,20 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
                hipFuncSetAttribute(reinterpret_cast<const void *>(&screen_ar_kernel<16>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, SD_LDS) == hipSuccess &&
                hipFuncSetAttribute(reinterpret_cast<const void *>(&screen_ar_kernel<24>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, SD_LDS) == hipSuccess &&
-               hipFuncSetAttribute(reinterpret_cast<const void *>(&screen_ar32_kernel<16>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, SD_LDS) == hipSuccess &&
-               hipFuncSetAttribute(reinterpret_cast<const void *>(&screen_ar32_kernel<24>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, SD_LDS) == hipSuccess &&
-               hipFuncSetAttribute(reinterpret_cast<const void *>(&screen_ar16_kernel<16>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, SD_LDS) == hipSuccess &&
-               hipFuncSetAttribute(reinterpret_cast<const void *>(&screen_ar16_kernel<24>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, SD_LDS) == hipSuccess;
     }();
     (void)attr;
     // K3d (queries resident in registers) where its template applies, else K3c
     void (*kern)(ScreenArgs) = kbn == 24 ? &screen_ar_kernel<24> : kbn == 16 ? &screen_ar_kernel<16> : nullptr;
+    bool k3f = false;
+#ifdef WVG_TOOLS
     if (tuning().screen_variant == 2 && kern)  // K3e (32x32x16 MFMAs)
         kern = kbn == 24 ? &screen_ar32_kernel<24> : &screen_ar32_kernel<16>;
     if (tuning().screen_variant == 3 && kern)  // K3f (two waves per SIMD)
         kern = kbn == 24 ? &screen_ar16_kernel<24> : &screen_ar16_kernel<16>;
-#ifdef WVG_TOOLS
+    if (tuning().screen_variant >= 2 && kern)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  SD_LDS);
     if (kbn == 24) {  // K3d diagnostics: separately compiled instantiations
         switch (tuning().screen_diag) {
         case 1: kern = &screen_ar_kernel<24, 1>; break;
@@ -2400,12 +2400,8 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
                                       SD_LDS);
     }
     if (tuning().screen_variant == 1) kern = nullptr;
+    k3f = kern == &screen_ar16_kernel<24> || kern == &screen_ar16_kernel<16> || kern == &screen_ar16_kernel<24, 10>;
 #endif
-    const bool k3f = kern == &screen_ar16_kernel<24> || kern == &screen_ar16_kernel<16>
-#ifdef WVG_TOOLS
-                     || kern == &screen_ar16_kernel<24, 10>
-#endif
-        ;
     const uint32_t threads = k3f ? SF_WAVES * 64 : kern ? SD_WAVES * 64 : SC_WAVES * 64, lds = kern ? SD_LDS : SC_LDS;
     if (!kern) kern = &screen_kernel;
     // Phased screen: the first r1 ranges (one workgroup per CU) run alone; their
