@@ -603,6 +603,53 @@ def _callers(call, T, seconds):
     return sum(done) / el, np.concatenate([np.asarray(x) for x in lat]) * 1e6
 
 
+_HOSTCALLS = []
+
+
+def _host_calls_lib():
+    """tools/libhostcalls.so (tools/host_calls.c, built by __graft_entry__.build()):
+    native caller threads, or None when it was not built."""
+    if not _HOSTCALLS:
+        import ctypes
+
+        path = os.path.join(ROOT, "tools", "libhostcalls.so")
+        lib = None
+        if os.path.exists(path):
+            lib = ctypes.CDLL(path)
+            lib.wvgb_call_loop.restype = ctypes.c_int
+            lib.wvgb_call_loop.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint32] * 3 + [
+                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_double,
+                ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
+        _HOSTCALLS.append(lib)
+    return _HOSTCALLS[0]
+
+
+def _native_callers(hc, lib, corpus, qs, k, T, seconds, allows=None):
+    """T native threads (tools/host_calls.c) calling wvg_search back to back for
+    about `seconds` -- the goroutine shape without the interpreter: returns
+    (calls per second, per-call latencies in us)."""
+    import ctypes
+
+    cap = 400_000
+    lat = np.zeros(T * cap, np.float64)
+    cnt = np.zeros(T, np.uint64)
+    el = ctypes.c_double()
+    qs = np.ascontiguousarray(qs, dtype=np.float32)
+    if allows:
+        arr = (ctypes.c_void_p * len(allows))(*[x.ctypes.data for x in allows])
+        words = np.array([len(x) for x in allows], np.uint64)
+        ap, wp, na = ctypes.cast(arr, ctypes.c_void_p), words.ctypes.data, len(allows)
+    else:
+        arr, words, ap, wp, na = None, None, None, None, 0
+    fn = ctypes.cast(lib.wvg_search, ctypes.c_void_p).value
+    rc = hc.wvgb_call_loop(fn, corpus, qs.ctypes.data, qs.shape[0], qs.shape[1], k, ap, wp, na, T, seconds,
+                           lat.ctypes.data, cap, cnt.ctypes.data, ctypes.byref(el))
+    if rc != 0:
+        raise RuntimeError(f"native caller loop failed: {rc}")
+    got = np.concatenate([lat[t * cap:t * cap + int(cnt[t])] for t in range(T)])
+    return float(cnt.sum()) / el.value, got
+
+
 def _lat_rec(qps, lat_us, n, d, T):
     rec = {"qps": round(qps, 1), "calls": int(len(lat_us)),
            "latency_us": {"p50": round(float(np.percentile(lat_us, 50)), 1),
@@ -622,7 +669,10 @@ def config_host_api(ctx, orc, callers=(1, 16), seconds=1.0):
     caller): N*d*4 bytes per call / the call's wall time vs 8 TB/s.  Per-call
     latency percentiles (the queries_durations_ms histogram's view,
     usecases/monitoring/prometheus.go:216) are taken around each call in the
-    calling thread (so they include ~2 us of Python / ctypes).  Filtered calls:
+    calling thread.  The callers are native threads (tools/host_calls.c: a
+    goroutine's shape, whose cgo call adds ~0.1 us) when tools/libhostcalls.so
+    was built; `python_caller_1` is the same single caller from a Python thread
+    (~2-4 us more per call: interpreter + ctypes).  Filtered calls:
     every call carries one of 8 allow lists (helpers.AllowList bitmaps,
     V/flat/index.go:423-449) keeping 10 % or 1 % of the rows."""
     import threading
@@ -671,14 +721,24 @@ def config_host_api(ctx, orc, callers=(1, 16), seconds=1.0):
         same = all(np.array_equal(g[0], s[0]) and np.array_equal(g[1].view(np.uint32), s[1].view(np.uint32))
                    for g, s in zip(got, serial))
         tag = "coalesced" if coalesce else "uncoalesced"
+        hc = _host_calls_lib()
+
+        def drive(T, secs, allow=None):
+            if hc is not None:
+                return _native_callers(hc, lib, c.handle, qs, k, T, secs, allow)
+            return _callers(call if allow is None else (lambda t, i: call(t, i, allow)), T, secs)
+
         for T in callers:
-            qps, lat = _callers(call, T, seconds)
+            qps, lat = drive(T, seconds)
             out[f"{tag}_callers_{T}"] = _lat_rec(qps, lat, n, d, T)
+        if coalesce and hc is not None:  # the same single caller from a Python thread (ctypes + interpreter)
+            qps, lat = _callers(call, 1, seconds / 2)
+            out["python_caller_1"] = _lat_rec(qps, lat, n, d, 1)
         out[f"{tag}_16_concurrent_equal_serial"] = bool(same)
         if coalesce:  # filtered single queries, 10 % and 1 % allow lists
             for rate, al in allows.items():
                 for T in callers:
-                    qps, lat = _callers(lambda t, i: call(t, i, al), T, seconds / 2)
+                    qps, lat = drive(T, seconds / 2, al)
                     rec = _lat_rec(qps, lat, n, d, T)
                     rec.pop("frac_of_8TBs", None)  # a filtered scan skips tiles with no allowed row
                     out[f"filtered_{int(rate * 100)}pct_callers_{T}"] = rec
