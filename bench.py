@@ -618,16 +618,17 @@ def _host_calls_lib():
             lib = ctypes.CDLL(path)
             lib.wvgb_call_loop.restype = ctypes.c_int
             lib.wvgb_call_loop.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint32] * 3 + [
-                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_double,
-                ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
+                ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                ctypes.c_double, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
         _HOSTCALLS.append(lib)
     return _HOSTCALLS[0]
 
 
-def _native_callers(hc, lib, corpus, qs, k, T, seconds, allows=None):
+def _native_callers(hc, lib, corpus, qs, k, T, seconds, allows=None, ks=None):
     """T native threads (tools/host_calls.c) calling wvg_search back to back for
-    about `seconds` -- the goroutine shape without the interpreter: returns
-    (calls per second, per-call latencies in us)."""
+    about `seconds` -- the goroutine shape without the interpreter; call i uses
+    ks[i % len(ks)] when ks is given, else k: returns (calls per second,
+    per-call latencies in us)."""
     import ctypes
 
     cap = 400_000
@@ -642,7 +643,9 @@ def _native_callers(hc, lib, corpus, qs, k, T, seconds, allows=None):
     else:
         arr, words, ap, wp, na = None, None, None, None, 0
     fn = ctypes.cast(lib.wvg_search, ctypes.c_void_p).value
-    rc = hc.wvgb_call_loop(fn, corpus, qs.ctypes.data, qs.shape[0], qs.shape[1], k, ap, wp, na, T, seconds,
+    kv = np.asarray(ks if ks else [], np.uint32)
+    rc = hc.wvgb_call_loop(fn, corpus, qs.ctypes.data, qs.shape[0], qs.shape[1], k,
+                           kv.ctypes.data if len(kv) else None, len(kv), ap, wp, na, T, seconds,
                            lat.ctypes.data, cap, cnt.ctypes.data, ctypes.byref(el))
     if rc != 0:
         raise RuntimeError(f"native caller loop failed: {rc}")
@@ -734,6 +737,9 @@ def config_host_api(ctx, orc, callers=(1, 16), seconds=1.0):
         if coalesce and hc is not None:  # the same single caller from a Python thread (ctypes + interpreter)
             qps, lat = _callers(call, 1, seconds / 2)
             out["python_caller_1"] = _lat_rec(qps, lat, n, d, 1)
+        if hc is not None:  # 16 callers with k = 1 / 10 / 100 mixed (one coalesced batch runs at the largest k)
+            qps, lat = _native_callers(hc, lib, c.handle, qs, k, 16, seconds / 2, ks=[10, 1, 100, 10])
+            out[f"{tag}_mixed_k_callers_16"] = _lat_rec(qps, lat, n, d, 16)
         out[f"{tag}_16_concurrent_equal_serial"] = bool(same)
         if coalesce:  # filtered single queries, 10 % and 1 % allow lists
             for rate, al in allows.items():

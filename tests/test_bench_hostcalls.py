@@ -53,6 +53,20 @@ def test_native_caller_loop_passes_queries_and_allow_lists(bench_mod):
         assert words == first == (3, 5, 7)[i % 3]
 
 
+def test_native_caller_loop_mixed_k(bench_mod):
+    seen = []
+
+    def fake(corpus, q, nq, k, allow, words, ids, dists, cnt):
+        seen.append(int(k))
+        return 0
+
+    lib = _Lib()
+    lib.wvg_search = SEARCH(fake)
+    bench_mod._native_callers(bench_mod._host_calls_lib(), lib, None, np.zeros((2, 4), np.float32), 5, 1, 0.02,
+                              ks=[10, 1, 100])
+    assert len(seen) > 6 and seen == [(10, 1, 100)[i % 3] for i in range(len(seen))]
+
+
 def test_native_caller_loop_reports_errors(bench_mod):
     lib = _Lib()
     lib.wvg_search = SEARCH(lambda *a: -3)

@@ -626,14 +626,16 @@ constexpr size_t COALESCE_MAX = 256;
 static int search_batch_filtered(wvg_corpus *c, const std::vector<wvg_search_request *> &batch, uint32_t k,
                                  uint64_t *out_ids, float *out_dists, uint32_t *out_counts);
 
-// Runs one coalesced batch (same k) and hands every request its own rows of
-// the result; a failure is every request's failure.
+// Runs one coalesced batch at k = the largest k of its requests and hands every
+// request the first r->k rows of its result: the top-k order is a strict total
+// order on (distance, docID) keys, so a smaller k's result is exactly a prefix of
+// a larger k's (counts: min(count, r->k)); a failure is every request's failure.
 static void run_coalesced(wvg_corpus *c, const std::vector<wvg_search_request *> &batch, uint32_t k)
 {
     const size_t B = batch.size();
     if (B == 1) {
         wvg_search_request *r = batch[0];
-        r->rc = search_batch(c, r->q, 1, k, r->allow, r->allow_words, r->ids, r->dists, r->counts);
+        r->rc = search_batch(c, r->q, 1, r->k, r->allow, r->allow_words, r->ids, r->dists, r->counts);
         if (r->rc) r->err = wvg_last_error();
         return;
     }
@@ -651,17 +653,17 @@ static void run_coalesced(wvg_corpus *c, const std::vector<wvg_search_request *>
         r->rc = rc;
         r->err = err;
         if (rc) continue;
-        if (r->ids) std::memcpy(r->ids, ids.data() + i * k, (size_t)k * 8);
-        if (r->dists) std::memcpy(r->dists, dists.data() + i * k, (size_t)k * 4);
-        if (r->counts) *r->counts = counts[i];
+        if (r->ids) std::memcpy(r->ids, ids.data() + i * k, (size_t)r->k * 8);
+        if (r->dists) std::memcpy(r->dists, dists.data() + i * k, (size_t)r->k * 4);
+        if (r->counts) *r->counts = std::min(counts[i], r->k);
     }
 }
 
 // A single-query search through the corpus's coalescer: the request queues;
 // while no batch of this corpus executes, the first waiter takes every queued
-// request with the head's k (up to COALESCE_MAX) and runs them as one batch
-// (results identical to separate calls: tests/test_gpu_coalesce.py), then
-// wakes the others.  A lone call finds the coalescer idle and runs at once;
+// request of the head's class (filtered or not; any k, the batch runs at the
+// largest; up to COALESCE_MAX) and runs them as one batch (results identical to
+// separate calls: tests/test_gpu_coalesce.py), then wakes the others.  A lone call finds the coalescer idle and runs at once;
 // under load a batch forms from the calls that arrive while the previous one
 // runs, so the batch size follows the arrival rate.
 static int search_coalesced(wvg_corpus *c, const float *query, uint32_t k, const uint64_t *allow,
@@ -685,7 +687,7 @@ static int search_coalesced(wvg_corpus *c, const float *query, uint32_t k, const
         }
         co.busy = true;
         std::vector<wvg_search_request *> batch;
-        const uint32_t kk = co.pending.front()->k;
+        uint32_t kk = 0;  // the batch's k: the largest of its requests' (round 4: the head's k only)
         // filtered and unfiltered requests form separate batches; filtered batches stay
         // below the MFMA threshold (the co-scheduled K1 takes one allow window per query)
         const bool filt = co.pending.front()->allow != nullptr;
@@ -695,7 +697,8 @@ static int search_coalesced(wvg_corpus *c, const float *query, uint32_t k, const
                                ? std::min<size_t>(COALESCE_MAX, mn - 1)
                                : COALESCE_MAX;
         for (auto it = co.pending.begin(); it != co.pending.end() && batch.size() < cap;) {
-            if ((*it)->k == kk && ((*it)->allow != nullptr) == filt) {
+            if (((*it)->allow != nullptr) == filt) {
+                kk = std::max(kk, (*it)->k);
                 batch.push_back(*it);
                 it = co.pending.erase(it);
             } else {
