@@ -737,6 +737,9 @@ def config_host_api(ctx, orc, callers=(1, 16), seconds=1.0):
         if coalesce and hc is not None:  # the same single caller from a Python thread (ctypes + interpreter)
             qps, lat = _callers(call, 1, seconds / 2)
             out["python_caller_1"] = _lat_rec(qps, lat, n, d, 1)
+        if coalesce and hc is not None:  # 64 callers: batches of up to 64 (the latency a caller pays under load)
+            qps, lat = _native_callers(hc, lib, c.handle, qs, k, 64, seconds / 2)
+            out["coalesced_callers_64"] = _lat_rec(qps, lat, n, d, 64)
         if hc is not None:  # 16 callers with k = 1 / 10 / 100 mixed (one coalesced batch runs at the largest k)
             qps, lat = _native_callers(hc, lib, c.handle, qs, k, 16, seconds / 2, ks=[10, 1, 100, 10])
             out[f"{tag}_mixed_k_callers_16"] = _lat_rec(qps, lat, n, d, 16)
