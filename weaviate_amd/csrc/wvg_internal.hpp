@@ -276,6 +276,7 @@ hipError_t launch_scan_f32(const ScanArgs &a, uint64_t *partials, int groups, hi
 constexpr uint32_t WVG_STATUS_MERGE_TIMEOUT = 1u;
 constexpr uint32_t WVG_RECORDS_TIMEOUT = 0xFFFFFFFFu;  // header count of a merge that gave up (StreamJob::records)
 constexpr uint32_t STREAM_QIN_FLOATS = 256;  // a query of up to 256 dims (f32 chunks) inline in StreamJob
+constexpr int SCAN_WAVES = 4;  // waves per K1 / query-stream scan workgroup
 struct StreamJob {
     uint64_t *partials;  // [nq][groups][k]
     uint32_t *arrivals;  // [nq], arrival_base at launch

@@ -17,8 +17,6 @@
 
 namespace wvg {
 
-constexpr int SCAN_WAVES = 4;
-
 #ifdef WVG_TOOLS
 Tuning &tuning()
 {

@@ -663,9 +663,10 @@ static void run_coalesced(wvg_corpus *c, const std::vector<wvg_search_request *>
 // while no batch of this corpus executes, the first waiter takes every queued
 // request of the head's class (filtered or not; any k, the batch runs at the
 // largest; up to COALESCE_MAX) and runs them as one batch (results identical to
-// separate calls: tests/test_gpu_coalesce.py), then wakes the others.  A lone call finds the coalescer idle and runs at once;
-// under load a batch forms from the calls that arrive while the previous one
-// runs, so the batch size follows the arrival rate.
+// separate calls: tests/test_gpu_coalesce.py), then wakes the others.  A lone
+// call finds the coalescer idle and runs at once; under load a batch forms from
+// the calls that arrive while the previous one runs, so the batch size follows
+// the arrival rate.
 static int search_coalesced(wvg_corpus *c, const float *query, uint32_t k, const uint64_t *allow,
                             uint64_t allow_words, uint64_t *out_ids, float *out_dists, uint32_t *out_counts)
 {
@@ -752,6 +753,16 @@ static int wvg::search_batch(wvg_corpus *c, const float *queries, uint32_t nq, u
     }
     if (k > MAX_K)  // beyond the fused register top-k: select + sort in HBM
         return search_large_k(c, queries, nq, k, allow_bits, allow_words, p, out_ids, out_dists, out_counts);
+    // A lone query's launch pays its ramp and its wave tail (+-1 tile per wave)
+    // once, not amortized as in the 16-query stream launch: where the auto rule
+    // gives one K1 workgroup per CU (L2, d <= 128), two halve every wave's range
+    // -- 82.5 -> 80.8 us per 1M x 128 query (three leave the merge workgroup no
+    // slot until a scan workgroup ends: 93.6; profiles/r05/single_query_gpc/).
+    if (inlaunch_single(c, nq, p, allow_bits != nullptr) && tuning().groups_per_cu == 0 &&
+        p.groups == (int)c->ctx->num_cus) {
+        const uint64_t cap = (p.te - p.tb + 2 * SCAN_WAVES - 1) / (2 * SCAN_WAVES);  // >= 2 tiles a wave
+        p.groups = (int)std::min<uint64_t>(2ull * c->ctx->num_cus, std::max<uint64_t>(cap, 1));
+    }
     SlotGuard g(c->ctx);
     rc = c->ctx->acquire(&g.slot);
     if (rc) return rc;
