@@ -188,6 +188,7 @@ int wvg_open_ex(int device, const wvg_options *opts, wvg_ctx **out)
     if (const char *e = getenv("WVG_K1_LOADS")) tuning().k1_loads = (int)strtol(e, nullptr, 10);        // A/B runs
     if (const char *e = getenv("WVG_SCREEN_VARIANT")) tuning().screen_variant = (int)strtol(e, nullptr, 10);  // A/B
     if (const char *e = getenv("WVG_STREAM_VARIANT")) tuning().stream_variant = (int)strtol(e, nullptr, 10);  // A/B
+    if (const char *e = getenv("WVG_SCREEN_SP")) tuning().screen_pilot_screen = (int)strtol(e, nullptr, 10);  // A/B
 #endif
     *out = c;
     return WVG_OK;
@@ -436,6 +437,9 @@ int wvgx_set_tuning(int key, int value)
     } else if (key == 25) {
         old = t.stream_variant;
         t.stream_variant = value;
+    } else if (key == 26) {
+        old = t.screen_pilot_screen;
+        t.screen_pilot_screen = value;
     }
     return old;
 }

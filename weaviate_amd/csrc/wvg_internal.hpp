@@ -426,6 +426,9 @@ struct Tuning {
                              // bit 0 between phases (else the lists' k-th lower bound + 2 Emax), bit 1 before
                              // the final collect (A/B)
     int screen_range_blocks = 0;  // K3c row-range length in 256-row blocks (0 = auto, ~128; A/B)
+    int screen_pilot_screen = 0;  // K3c/K3d (tuning key 26): tiles of the SCREEN pilot -- the bf16 screen itself over
+                                  // the first tiles in short ranges + one exact seed from their lists -- which
+                                  // replaces the K3b pilot (0 = the K3b pilot; A/B)
     int screen_diag = 0;     // K3c diagnostics (tools build only; results are NOT distances): bit 0 = no
                              // wait for the stage loads, bit 1 = no epilogue, bit 2 = no list insertions, bit 3 = no query-fragment loads (K3c); K3d: 1, 2, 4 or 16 (= counters) select compiled variants
 };

@@ -2283,8 +2283,22 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
     armed_events() = LaunchEvents{};
     const uint64_t pilot_tiles = (uint64_t)std::max(tuning().screen_pilot, 0);
     const uint64_t pilot_gemm_tiles = (uint64_t)std::max(tuning().screen_pilot_gemm, 0);
+    // Screen pilot: short ranges of the screen itself over the first sp_tiles tiles
+    // (one workgroup per CU), lists into the pilot scratch ([nq][sp_rr][SCREEN_M]),
+    // then one exact seed from them (below, once the kernel is chosen)
+    const uint64_t sp_tiles = std::min<uint64_t>((uint64_t)std::max(tuning().screen_pilot_screen, 0),
+                                                 L.tile_end - L.tile_begin);
+    uint32_t sp_rr = 0;
+    if (sp_tiles > 0 && L.pilot_part && L.data && L.pilot_part_lists > 0) {
+        const uint64_t nb = (sp_tiles + 3) / 4;
+        uint64_t want = std::min<uint64_t>(((uint64_t)L.num_cus / nqb + 7) / 8 * 8, nb);
+        want = std::min<uint64_t>(want, (uint64_t)L.pilot_part_lists * L.k / SCREEN_M);  // the scratch's capacity
+        sp_rr = want >= 8 ? (uint32_t)(want / 8 * 8) : 0;
+    }
     uint32_t pilot_rr = 0;  // K3b pilot: its row ranges (0: the K1 pilot)
-    if (L.pilot && pilot_gemm_tiles > 0) {
+    if (sp_rr > 0) {
+        // (the screen pilot replaces the K3b / K1 pilots)
+    } else if (L.pilot && pilot_gemm_tiles > 0) {
         const uint64_t nt = std::min<uint64_t>(L.pilot->tile_end - L.pilot->tile_begin, pilot_gemm_tiles);
         pilot_rr = nt ? gemm_row_ranges(L.nq, nt, L.num_cus, L.dim, L.k) : 0;
         if (pilot_rr > L.pilot_part_lists) pilot_rr = 0;
@@ -2305,7 +2319,7 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
         hipLaunchKernelGGL(screen_pilot_seed_kernel, dim3((L.nq + 255) / 256), dim3(256), 0, s, L.pilot_dists,
                            L.pilot_counts, L.nq, L.k, L.gbound);
         if ((e = hipGetLastError()) != hipSuccess) return e;
-    } else if (L.pilot && pilot_tiles > 0) {
+    } else if (sp_rr == 0 && L.pilot && pilot_tiles > 0) {
         // Pilot: every query's exact top-k (K1, AVX2-order distances) over the
         // range's first 16 tiles (1024 rows); its k-th distance bounds the final k-th
         // (k real rows lie at or below it), so it seeds gbound before the
@@ -2411,6 +2425,25 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
     // Without it a range starts from the k-th bound of single finished
     // ranges (rows in the top-k of 1 % of the corpus), and most row blocks
     // took the exact per-element path with list insertions.
+    if (sp_rr > 0) {
+        // Screen pilot (round 5): the bf16 screen over the first sp_tiles tiles in sp_rr
+        // short ranges (a few row blocks each, every CU busy), its lists into the pilot
+        // scratch, then the exact seed over them: the k smallest lower bounds rescored
+        // exactly, their k-th distance into gbound -- k real rows at or below it, so a
+        // valid bound, as the K3b pilot's exact k-th over its rows (which cost ~0.76 ms
+        // per 1024-query batch: K3b's start-up on a short range)
+        ScreenArgs f = a;
+        f.tile_end = L.tile_begin + sp_tiles;
+        f.nrr = sp_rr;
+        f.rr0 = 0;
+        f.nrr_l = sp_rr;
+        f.partials = L.pilot_part;
+        hipLaunchKernelGGL(kern, dim3(nqb * sp_rr), dim3(threads), lds, s, f);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if ((e = launch_seed_exact(L.metric, L.queries, L.qpitch, L.data, L.dim, L.nchunks, L.pilot_part,
+                                   sp_rr * SCREEN_M, SCREEN_M, sp_rr, L.nq, L.k, L.gbound, s)) != hipSuccess)
+            return e;
+    }
     uint32_t bounds[12] = {0}, nph = 0;
     bounds[nph++] = 0;
     const int split = tuning().screen_split;
