@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Coalescer under load (tools build): 1M x 128 L2, k = 10, T native caller
+threads (bench.py's tools/host_calls.c loop) calling wvg_search with one query
+each for `--seconds`; per T the QPS, latency percentiles and the coalescer's
+batch counters (wvgx_coalesce_counters: batches, requests, time running
+batches, largest batch), plus a direct nq-query call's time for reference.
+Usage: WVG_LIB=tools/libwvgpu_tools.so python tools/coalesce_probe.py [--callers 1,16,32,64]"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("WVG_LIB", os.path.join(ROOT, "tools", "libwvgpu_tools.so"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--callers", default="1,16,32,64")
+    ap.add_argument("--seconds", type=float, default=1.0)
+    a = ap.parse_args()
+    import bench
+    from oracle import wv_oracle as orc
+    from weaviate_amd._lib import KIND_F32, METRIC_L2
+    from weaviate_amd.device import Context, Corpus
+
+    ctx = Context(0)
+    lib = ctx.lib
+    n, d, k = 1_000_000, 128, 10
+    c = Corpus(ctx, KIND_F32, METRIC_L2, d, n)
+    c.fill_synthetic(42, n, 0)
+    qs = np.ascontiguousarray(orc.synth_rows(43, 0, 256, d, 0))
+    hc = bench._host_calls_lib()
+    cnt = (ctypes.c_uint64 * 4)()
+    for nq in (16, 32, 64):
+        c.search(qs[:nq], k)
+        t0 = time.perf_counter()
+        for _ in range(5):
+            c.search(qs[:nq], k)
+        print(json.dumps({"direct_call_nq": nq, "ms_per_call": round((time.perf_counter() - t0) / 5 * 1e3, 3)}),
+              flush=True)
+    for T in (int(x) for x in a.callers.split(",")):
+        lib.wvgx_coalesce_counters(cnt, 1)
+        qps, lat = bench._native_callers(hc, lib, c.handle, qs, k, T, a.seconds)
+        lib.wvgx_coalesce_counters(cnt, 1)
+        b, r, ns, mx = (int(x) for x in cnt)
+        print(json.dumps({"callers": T, "qps": round(qps, 1), "p50_us": round(float(np.percentile(lat, 50)), 1),
+                          "p99_us": round(float(np.percentile(lat, 99)), 1), "batches": b,
+                          "mean_batch": round(r / max(1, b), 2), "max_batch": mx,
+                          "mean_batch_run_us": round(ns / max(1, b) / 1e3, 1),
+                          "busy_frac": round(ns / 1e9 / a.seconds, 3)}), flush=True)
+    c.destroy()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -5,6 +5,7 @@
 #include <hip/hip_ext.h>
 
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <mutex>
@@ -81,8 +82,14 @@ struct wvg_search_request;
 struct wvg_coalescer {
     std::mutex mu;
     std::condition_variable cv;
+    std::condition_variable gather_cv;  // arrivals wake a runner that is gathering its batch
     std::deque<wvg_search_request *> pending;
-    bool busy = false;  // a batch is executing
+    bool busy = false;       // a batch is executing (or its runner is gathering)
+    bool gathering = false;
+    size_t last_n = 0;       // requests of the last batch
+    size_t carry = 0;        // requests that were waiting when it ended (not its own callers)
+    std::chrono::steady_clock::time_point last_done{};
+    std::chrono::nanoseconds last_run{0};
 };
 
 struct wvg_corpus {
@@ -325,6 +332,7 @@ uint32_t screen_row_ranges(uint32_t nq, uint64_t ntiles, int num_cus);
 #ifdef WVG_TOOLS
 void screen_counters(uint64_t out[4], bool reset);
 void single_counters(uint64_t out[4], bool reset);
+void coalesce_counters(uint64_t out[4], bool reset);
 #endif
 hipError_t launch_shadow_build(const float *tiled, uint32_t dim, uint64_t t0, uint64_t t1, void *shadow, float *norms,
                                uint32_t *nmax, hipStream_t s);

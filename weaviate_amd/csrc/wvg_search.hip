@@ -558,8 +558,25 @@ void single_counters(uint64_t out[4], bool reset)
 {
     for (int i = 0; i < 4; i++) out[i] = reset ? g_single[i].exchange(0) : g_single[i].load();
 }
+// the coalescer's batches (wvgx_coalesce_counters): [0] batches, [1] requests,
+// [2] ns spent running batches, [3] the largest batch
+static std::atomic<uint64_t> g_coal[4];
+static void coalesce_counter(size_t reqs, uint64_t ns)
+{
+    g_coal[0].fetch_add(1, std::memory_order_relaxed);
+    g_coal[1].fetch_add(reqs, std::memory_order_relaxed);
+    g_coal[2].fetch_add(ns, std::memory_order_relaxed);
+    uint64_t m = g_coal[3].load();
+    while (reqs > m && !g_coal[3].compare_exchange_weak(m, reqs)) {
+    }
+}
+void coalesce_counters(uint64_t out[4], bool reset)
+{
+    for (int i = 0; i < 4; i++) out[i] = reset ? g_coal[i].exchange(0) : g_coal[i].load();
+}
 #else
 inline void single_counter(int, bool) {}
+inline void coalesce_counter(size_t, uint64_t) {}
 #endif
 
 // Waits until a single query's tagged records (StreamJob::records) have all
@@ -681,12 +698,36 @@ static int search_coalesced(wvg_corpus *c, const float *query, uint32_t k, const
     wvg_coalescer &co = c->co;
     std::unique_lock<std::mutex> g(co.mu);
     co.pending.push_back(&r);
+    if (co.gathering) co.gather_cv.notify_one();
     while (!r.done) {
         if (co.busy) {
             co.cv.wait(g);
             continue;
         }
         co.busy = true;
+        // Gathering: callers come back right after their batch returns, so the batch
+        // that starts next would otherwise hold only those that queued meanwhile --
+        // with T closed-loop callers the batches settled at T / 2, alternating halves
+        // (profiles/r05/coalesce/).  When the last batch (of more than one request)
+        // ended moments ago, the runner waits a short window until its callers are back
+        // too: the requests that were waiting when it ended + as many as it held.  The
+        // window is at most an eighth of that batch's run time and 50 us + 3 us per
+        // caller to wake (64 callers on 16 cores take ~200 us to return), at least 10
+        // us.  A lone caller's batches hold one request, so it never waits.
+        const size_t want = std::min(co.carry + co.last_n, COALESCE_MAX);
+        if (co.last_n > 1 && co.pending.size() < want) {
+            const auto window = std::max<std::chrono::nanoseconds>(
+                std::chrono::microseconds(10),
+                std::min<std::chrono::nanoseconds>(std::chrono::microseconds(50 + 3 * (int64_t)co.last_n),
+                                                   co.last_run / 8));
+            const auto until = co.last_done + window;
+            if (std::chrono::steady_clock::now() < until) {
+                co.gathering = true;
+                while (co.pending.size() < want && co.gather_cv.wait_until(g, until) != std::cv_status::timeout) {
+                }
+                co.gathering = false;
+            }
+        }
         std::vector<wvg_search_request *> batch;
         uint32_t kk = 0;  // the batch's k: the largest of its requests' (round 4: the head's k only)
         // filtered and unfiltered requests form separate batches; filtered batches stay
@@ -707,8 +748,15 @@ static int search_coalesced(wvg_corpus *c, const float *query, uint32_t k, const
             }
         }
         g.unlock();
+        const auto tb0 = std::chrono::steady_clock::now();
         run_coalesced(c, batch, kk);
+        const auto tb1 = std::chrono::steady_clock::now();
+        coalesce_counter(batch.size(), (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(tb1 - tb0).count());
         g.lock();
+        co.last_n = batch.size();
+        co.carry = co.pending.size();
+        co.last_done = tb1;
+        co.last_run = std::chrono::duration_cast<std::chrono::nanoseconds>(tb1 - tb0);
         for (wvg_search_request *b : batch) b->done = true;
         co.busy = false;
         co.cv.notify_all();
