@@ -189,6 +189,7 @@ int wvg_open_ex(int device, const wvg_options *opts, wvg_ctx **out)
     if (const char *e = getenv("WVG_SCREEN_VARIANT")) tuning().screen_variant = (int)strtol(e, nullptr, 10);  // A/B
     if (const char *e = getenv("WVG_STREAM_VARIANT")) tuning().stream_variant = (int)strtol(e, nullptr, 10);  // A/B
     if (const char *e = getenv("WVG_SCREEN_SP")) tuning().screen_pilot_screen = (int)strtol(e, nullptr, 10);  // A/B
+    if (const char *e = getenv("WVG_GROUPS_PER_CU")) tuning().groups_per_cu = (int)strtol(e, nullptr, 10);  // A/B
 #endif
     *out = c;
     return WVG_OK;
