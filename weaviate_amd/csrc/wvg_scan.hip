@@ -647,17 +647,18 @@ int scan_groups_for(const ScanArgs &a, int num_cus)
 {
     const uint64_t ntiles = a.tile_end > a.tile_begin ? a.tile_end - a.tile_begin : 0;
     uint64_t g = (ntiles + SCAN_WAVES * 2 - 1) / (SCAN_WAVES * 2);
-    // groups_per_cu 0 = auto (tools/k1_dim_ab.py, profiles/r01/k1_grid/):
-    // - d <= 128, L2: one per CU (32 KiB of row loads in flight per wave
-    //   already saturate HBM: 7.15 TB/s at 20M x 128; the 1M-row headline
-    //   is 3-6 % slower with two);
-    // - d <= 128, dot / cosine: two (one ran 20M x 128 cosine at 4.2 TB/s,
-    //   two at 6.7);
+    // groups_per_cu 0 = auto (tools/k1_dim_ab.py, profiles/r01/k1_grid/,
+    // profiles/r05/headline_gpc/):
+    // - d <= 128: two per CU (round 1 measured L2 3-6 % slower with two on
+    //   its kernel; with round 5's query-stream kernel -- tile ranges, per-list
+    //   hand-offs -- the 16-query headline launch is 8 % faster with two:
+    //   1126 -> 1041 us, and a lone query 82.6 -> 80.4 us; dot / cosine: one
+    //   ran 20M x 128 cosine at 4.2 TB/s, two at 6.7);
     // - d > 128 (F32 only; a.dim is 0 for BQ / PQ): three (a d = 768 row is
     //   loaded 16 KiB at a time per wave: 4.2 -> 7.15 TB/s at 10M x 768,
     //   4.2 -> 7.0 at 3M x 1536).
     int gpc = tuning().groups_per_cu;
-    if (gpc <= 0) gpc = a.dim > 128 ? 3 : (a.dim > 0 && a.metric != WVG_M_L2 ? 2 : 1);
+    if (gpc <= 0) gpc = a.dim > 128 ? 3 : (a.dim > 0 ? 2 : 1);
     uint64_t cap = (uint64_t)num_cus * (uint64_t)gpc;
     if (a.nq > 1) cap = std::max<uint64_t>((uint64_t)num_cus / 4, cap / a.nq);
     if (g > cap) g = cap;

@@ -801,16 +801,6 @@ static int wvg::search_batch(wvg_corpus *c, const float *queries, uint32_t nq, u
     }
     if (k > MAX_K)  // beyond the fused register top-k: select + sort in HBM
         return search_large_k(c, queries, nq, k, allow_bits, allow_words, p, out_ids, out_dists, out_counts);
-    // A lone query's launch pays its ramp and its wave tail (+-1 tile per wave)
-    // once, not amortized as in the 16-query stream launch: where the auto rule
-    // gives one K1 workgroup per CU (L2, d <= 128), two halve every wave's range
-    // -- 82.5 -> 80.8 us per 1M x 128 query (three leave the merge workgroup no
-    // slot until a scan workgroup ends: 93.6; profiles/r05/single_query_gpc/).
-    if (inlaunch_single(c, nq, p, allow_bits != nullptr) && tuning().groups_per_cu == 0 &&
-        p.groups == (int)c->ctx->num_cus) {
-        const uint64_t cap = (p.te - p.tb + 2 * SCAN_WAVES - 1) / (2 * SCAN_WAVES);  // >= 2 tiles a wave
-        p.groups = (int)std::min<uint64_t>(2ull * c->ctx->num_cus, std::max<uint64_t>(cap, 1));
-    }
     SlotGuard g(c->ctx);
     rc = c->ctx->acquire(&g.slot);
     if (rc) return rc;
