@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-5 GPU call Q: full GPU suite, smoke, and the driver's default bench line on
+# Round-5 GPU call W (and Q before it): full GPU suite, smoke, and the driver's default bench line on
 # the current build (lone queries at two workgroups per CU, mixed-k coalescing,
 # native host-API callers).
 set -o pipefail
-O=gpurun_out/r05q
+O=gpurun_out/r05w
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || exit 1
