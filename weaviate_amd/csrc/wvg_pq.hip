@@ -1546,15 +1546,17 @@ static hipError_t launch_pq_e_variant(const ScanArgs &a, uint64_t *partials, int
         else launch_pq_dense<E, 2, 16, 6>(a, partials, grid, block, 4 * lds, s);
         return hipGetLastError();
     }
-    if (m32 && v >= 50 && v <= 54) {
+    if (m32 && v >= 50 && v <= 56) {
         // K8e mask-load A/B (round 4): 50 = the round-3 product (8 waves, ring 4 / 16, branchy mask
         // loads waited at once); MB (buffered raw masks): 51 = ring 4, 52 = ring 8, 53 = ring 16,
-        // 54 = 4 waves, ring 16
+        // 54 = 4 waves, ring 16; round 5: 55 = 16 waves, ring 4; 56 = 16 waves, ring 2
         bool ok;
         if (v == 50) ok = launch_pq_wide<E, 8, 4, 16, 1, false, false, false>(a, partials, groups, s);
         else if (v == 51) ok = launch_pq_wide<E, 8, 4, 16, 1>(a, partials, groups, s);
         else if (v == 52) ok = launch_pq_wide<E, 8, 8, 16, 1>(a, partials, groups, s);
         else if (v == 53) ok = launch_pq_wide<E, 8, 16, 16, 1>(a, partials, groups, s);
+        else if (v == 55) ok = launch_pq_wide<E, 16, 4, 16, 1>(a, partials, groups, s);
+        else if (v == 56) ok = launch_pq_wide<E, 16, 2, 16, 1>(a, partials, groups, s);
         else ok = launch_pq_wide<E, 4, 16, 16, 1>(a, partials, groups, s);
         if (ok) return hipGetLastError();
     }
