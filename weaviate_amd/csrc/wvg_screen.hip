@@ -2092,6 +2092,399 @@ __global__ __launch_bounds__(SF_WAVES * 64) void screen_ar16_kernel(ScreenArgs a
     }
 }
 
+// ---------------------------------------------------------------------------
+// K3g (round 5, tools variant 4): K3f's 16-query waves in 4-wave workgroups of
+// 64 queries, TWO workgroups per CU, each with its own 4-stage ring and its
+// own barrier.  K3f's 8 waves shared one barrier per unit, so the two waves of
+// a SIMD issued MFMAs, DMA and reads in the same phase; two independent
+// workgroups drift apart, so one wave's DMA issue and barrier wait can fall in
+// the other's MFMA stream.  Costs: every CU streams each row block twice (once
+// per 64-query workgroup; L2 hits) and the ring holds 2 stages in flight
+// instead of 6.
+constexpr int SG_WAVES = 4;
+constexpr int SG_BQ = 64;
+constexpr int SG_NBUF = 4;
+constexpr int SG_RING = SG_NBUF * SD_STAGE + 2 * SD_NSLOT;
+constexpr int SG_LISTS = SG_BQ * SCREEN_M * 8;
+constexpr int SG_LDS = SG_RING + SG_LISTS + SG_BQ * 4 * 5;
+static_assert(2 * SG_LDS <= 160 * 1024, "K3g: two workgroups per CU");
+static_assert(SG_WAVES * 16 == SG_BQ, "K3g: 16 queries per wave");
+
+template <int KBN, int DIAG = 0>
+__global__ __launch_bounds__(SG_WAVES * 64, 2) void screen_ar16x2_kernel(ScreenArgs a)
+{
+    static_assert(KBN % SG_NBUF == 0, "the stage buffer of a K block must be a compile-time constant");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint64_t *lists = reinterpret_cast<uint64_t *>(smem + SG_RING);  // [4][16][M]
+    float *tau = reinterpret_cast<float *>(smem + SG_RING + SG_LISTS);
+    float *sig = tau + SG_BQ;
+    float *ck1 = sig + SG_BQ;
+    float *ck2 = ck1 + SG_BQ;
+    float *cem = ck2 + SG_BQ;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int K = (int)a.k, M = SCREEN_M;
+    const int cosine = a.cosine;
+    const uint32_t b = blockIdx.x;
+    uint32_t qb, rr;
+    if (a.nrr_l % 8 == 0) {
+        const uint32_t xcd = b % 8, wv = b / 8;
+        qb = wv % a.nqb;
+        rr = a.rr0 + (wv / a.nqb) * 8 + xcd;
+    } else {
+        qb = b % a.nqb;
+        rr = a.rr0 + b / a.nqb;
+    }
+    const uint64_t ntiles = a.tile_end - a.tile_begin;
+    const uint64_t nblk = (ntiles + 3) / 4;
+    const uint64_t blk0 = nblk * rr / a.nrr, blk1 = nblk * (rr + 1) / a.nrr;
+    const uint32_t q0 = qb * SG_BQ;
+
+    for (int i = tid; i < SG_BQ; i += SG_WAVES * 64) {
+        const uint32_t q = q0 + (uint32_t)i;
+        ck1[i] = a.k1[q];
+        ck2[i] = a.k2[q];
+        cem[i] = a.emax[q];
+        const uint32_t g = q < a.nq ? __hip_atomic_load(a.gbound + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        const float t = q >= a.nq ? -__builtin_inff() : (g == 0xFFFFFFFFu ? __builtin_inff() : wvg_unord_f32(g));
+        tau[i] = t;
+        sig[i] = q >= a.nq ? __builtin_inff() : sc_sigma(t, cosine);
+    }
+    for (int i = tid; i < SG_BQ * M; i += SG_WAVES * 64) lists[i] = WVG_KEY_NONE;
+    __syncthreads();
+    const uint32_t laddr = (uint32_t)(uintptr_t)(lists + (size_t)w * 16 * M);
+    const uint32_t tbase = (uint32_t)(uintptr_t)(tau + w * 16);  // sig + 256, ck1 + 512, ck2 + 768, cem + 1024
+    if (blk0 < blk1) {
+        // the wave's 16 queries, every K block, resident for the whole range: the
+        // compiler splits a 256-register wave's file 128 / 128 between VGPRs and
+        // AGPRs, so the first SF_AKB K blocks sit next to the accumulators (64) and
+        // the quarter buffers (32) in AGPRs, the rest in VGPRs
+        constexpr int SF_AKB = 8;
+        bf16x8 areg[KBN];
+        {
+            const uint4 *qsrc = a.qfrag + (size_t)(qb * 4 + w) * KBN * 64 + lane;
+#pragma unroll
+            for (int ks = 0; ks < KBN; ks++) {
+                if (ks < SF_AKB)
+                    asm volatile("global_load_dwordx4 %0, %1, off" : "=a"(areg[ks]) : "v"(qsrc + (size_t)ks * 64) : "memory");
+                else
+                    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(areg[ks]) : "v"(qsrc + (size_t)ks * 64) : "memory");
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int ks = 0; ks < KBN; ks++) {
+                if (ks < SF_AKB)
+                    asm volatile("" : "+a"(areg[ks]));
+                else
+                    asm volatile("" : "+v"(areg[ks]));
+            }
+        }
+        // loads of one stage (K3d's): wave w moves row fragments 4 w .. 4 w + 3 (tile w),
+        // with unit 0 also the norms of tile w, and wave 0 the block's tile words
+        const uint4 *lsrc = a.shadow + ((size_t)(a.tile_begin + blk0 * 4 + w) * KBN * 4) * 64;
+        const float *lnorm = a.norms + (a.tile_begin + blk0 * 4 + w) * 64;
+        uint64_t lblk = blk0;
+        auto load_stage = [&](int ks) {
+            unsigned char *dst = smem + (ks % SG_NBUF) * SD_STAGE;
+#pragma unroll
+            for (int rg = 0; rg < 4; rg++)
+                __builtin_amdgcn_global_load_lds(lsrc + ((size_t)ks * 4 + rg) * 64 + lane,
+                                                 reinterpret_cast<uint4 *>(dst + (4 * w + rg) * 1024), 16, 0, 0);
+            unsigned char *nslot = smem + SG_NBUF * SD_STAGE + (lblk & 1) * SD_NSLOT;
+            if (ks == 0)
+                __builtin_amdgcn_global_load_lds(lnorm + lane, reinterpret_cast<float *>(nslot + w * 256), 4, 0, 0);
+            if (ks == 0 && w == 0) {
+                const uint32_t wi = (uint32_t)(lane & 7) >> 1, half = lane & 1;
+                const uint64_t t = a.tile_begin + lblk * 4 + wi;
+                const uint32_t *src =
+                    reinterpret_cast<const uint32_t *>(a.valid + (t < a.tile_end ? t : a.tile_end - 1)) + half;
+                if (lane >= 8 && lane < 16 && a.allow) {
+                    const uint64_t aw = t - a.allow_t0;
+                    src = reinterpret_cast<const uint32_t *>(a.allow + (aw < a.allow_words ? aw : 0)) + half;
+                }
+                __builtin_amdgcn_global_load_lds(src, reinterpret_cast<uint32_t *>(nslot + 1024), 4, 0, 0);
+            }
+            if (ks == KBN - 1 && lblk + 1 < blk1) {  // the load cursor moves on; past the end it stays
+                ++lblk;
+                lsrc += (size_t)4 * KBN * 4 * 64;
+                lnorm += 256;
+            }
+        };
+        // SG_NBUF - 2 stages in flight at every wait: unit ks + 1 landed, the loads of
+        // units ks + 2 .. ks + SG_NBUF - 2 left outstanding (K3d's per-unit load counts)
+        auto wait_next = [&](auto KS) {
+            constexpr int ks = decltype(KS)::value;
+            constexpr int n0 = sd_younger<KBN, 0>(ks + 1, SG_NBUF - 3, true);
+            constexpr int n1 = sd_younger<KBN, 0>(ks + 1, SG_NBUF - 3, false);
+            if (w == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n0) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n1) : "memory");
+        };
+        auto raw_barrier = [&]() {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+        };
+        // A quarter stage (row fragments 4 qq .. 4 qq + 3) straight into AGPRs, in
+        // flight while the previous quarter's MFMAs issue; consumers pass wait_q
+        // (lgkmcnt(4): every read but the 4 younger ones landed) or the barrier.
+        // The stage / quarter offset is an instruction literal (as SGPR operands the
+        // 32 distinct offsets were hoisted into SGPRs and spilled).
+        const uint32_t rbase = (uint32_t)(uintptr_t)smem + 16u * lane;
+        auto read_q = [](auto KS, auto QQ, bf16x8 (&br)[4], uint32_t rb) {
+            constexpr uint32_t soff =
+                (uint32_t)((decltype(KS)::value % SG_NBUF) * SD_STAGE + decltype(QQ)::value * 4 * 1024);
+            uint32_t tmp;
+            asm volatile("v_add_u32 %4, %5, %6\n\t"
+                         "ds_read_b128 %0, %4\n\t"
+                         "ds_read_b128 %1, %4 offset:1024\n\t"
+                         "ds_read_b128 %2, %4 offset:2048\n\t"
+                         "ds_read_b128 %3, %4 offset:3072"
+                         : "=a"(br[0]), "=a"(br[1]), "=a"(br[2]), "=a"(br[3]), "=&v"(tmp)
+                         : "n"(soff), "v"(rb)
+                         : "memory");
+        };
+        using I0 = std::integral_constant<int, 0>;
+        using I1 = std::integral_constant<int, 1>;
+        using I2 = std::integral_constant<int, 2>;
+        using I3 = std::integral_constant<int, 3>;
+        auto wait_q = [&](bf16x8 (&br)[4]) {
+            asm volatile("s_waitcnt lgkmcnt(4)" : "+a"(br[0]), "+a"(br[1]), "+a"(br[2]), "+a"(br[3]) : : "memory");
+        };
+        const int qlane = 4 * (lane >> 4);
+        const uint32_t sbase = (uint32_t)(uintptr_t)smem;
+        const uint32_t nbase = sbase + 4u * (uint32_t)(lane & 15);
+        const uint32_t qbase = sbase + 4u * (uint32_t)qlane;
+        const uint32_t csoff = (uint32_t)((uintptr_t)sig - (uintptr_t)smem);
+        bool lane_force = false;
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+            if (!(ck1[16 * w + qlane + r] <= 0x1p50f)) lane_force = true;
+
+        floatx4 acc[16];
+#pragma unroll
+        for (int nr = 0; nr < 16; nr++) acc[nr] = (floatx4){0.f, 0.f, 0.f, 0.f};
+        bf16x8 bq0[4], bq1[4];
+        auto mfma4 = [&](int ks, int qq, bf16x8 (&br)[4]) {
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                acc[4 * qq + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(areg[ks], br[j], acc[4 * qq + j], 0, 0, 0);
+        };
+#pragma unroll
+        for (int ks = 0; ks < SG_NBUF - 1; ks++) load_stage(ks);
+        if (w == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(sd_younger<KBN, 0>(0, SG_NBUF - 2, true)) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(sd_younger<KBN, 0>(0, SG_NBUF - 2, false)) : "memory");
+        raw_barrier();
+        read_q(I0{}, I0{}, bq0, rbase);
+        for (uint64_t blk = blk0; blk < blk1; blk++) {
+            sd_static_for<KBN>([&](auto KS) {
+                constexpr int ks = decltype(KS)::value;
+                read_q(KS, I1{}, bq1, rbase);
+                wait_q(bq0);
+                mfma4(ks, 0, bq0);
+                read_q(KS, I2{}, bq0, rbase);
+                wait_q(bq1);
+                mfma4(ks, 1, bq1);
+                read_q(KS, I3{}, bq1, rbase);
+                wait_q(bq0);
+                mfma4(ks, 2, bq0);
+                wait_next(KS);  // the next unit landed
+                raw_barrier();  // (lgkmcnt(0): quarter 3 landed)
+#pragma unroll
+                for (int j = 0; j < 4; j++) asm volatile("" : "+a"(bq1[j]));
+                load_stage((ks + SG_NBUF - 1) % KBN);  // into the buffer of unit - 1, read before the barrier
+                if constexpr (ks + 1 < KBN) read_q(std::integral_constant<int, ks + 1>{}, I0{}, bq0, rbase);
+                mfma4(ks, 3, bq1);
+            });
+            // XDL write -> VALU read of the accumulators through agpr_read: see K3d
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr ((DIAG & 2) == 0) {
+                // K3d's epilogue over the wave's 16 queries: C layout row (query) qlane + r,
+                // column (row) 16 nr + (lane & 15); fast check per query r, exact test on
+                // the groups it could not rule out
+                const uint32_t nsoff = (uint32_t)(SG_NBUF * SD_STAGE + (blk & 1) * SD_NSLOT);
+                auto read_norms8 = [&](int hh, float (&nrm)[8]) {
+                    uint32_t tmp;
+                    asm volatile("v_add_u32 %8, %9, %10\n\t"
+                                 "ds_read_b32 %0, %8\n\t"
+                                 "ds_read_b32 %1, %8 offset:64\n\t"
+                                 "ds_read_b32 %2, %8 offset:128\n\t"
+                                 "ds_read_b32 %3, %8 offset:192\n\t"
+                                 "ds_read_b32 %4, %8 offset:256\n\t"
+                                 "ds_read_b32 %5, %8 offset:320\n\t"
+                                 "ds_read_b32 %6, %8 offset:384\n\t"
+                                 "ds_read_b32 %7, %8 offset:448\n\t"
+                                 "s_waitcnt lgkmcnt(0)"
+                                 : "=v"(nrm[0]), "=v"(nrm[1]), "=v"(nrm[2]), "=v"(nrm[3]), "=v"(nrm[4]),
+                                   "=v"(nrm[5]), "=v"(nrm[6]), "=v"(nrm[7]), "=&v"(tmp)
+                                 : "s"(nsoff + 512u * hh), "v"(nbase)
+                                 : "memory");
+                };
+                float nmax, nsum;
+                {
+                    float n0[8], n1[8];
+                    read_norms8(0, n0);
+                    read_norms8(1, n1);
+                    nmax = n0[0];
+                    nsum = n0[0];
+#pragma unroll
+                    for (int j2 = 1; j2 < 8; j2++) nmax = __builtin_fmaxf(nmax, n0[j2]), nsum += n0[j2];
+#pragma unroll
+                    for (int j2 = 0; j2 < 8; j2++) nmax = __builtin_fmaxf(nmax, n1[j2]), nsum += n1[j2];
+                }
+                const bool force = lane_force || !(nmax <= 0x1p60f) || nsum != nsum;
+                uint32_t wact = 0;
+                {
+                    const uint32_t coff = (uint32_t)(csoff + 4 * (16 * w));
+                    float4 k1v, k2v, sv;
+                    uint32_t tmp;
+                    asm volatile("v_add_u32 %3, %4, %5\n\t"
+                                 "ds_read_b128 %0, %3 offset:256\n\t"
+                                 "ds_read_b128 %1, %3 offset:512\n\t"
+                                 "ds_read_b128 %2, %3\n\t"
+                                 "s_waitcnt lgkmcnt(0)"
+                                 : "=v"(k1v), "=v"(k2v), "=v"(sv), "=&v"(tmp)
+                                 : "s"(coff), "v"(qbase)
+                                 : "memory");
+                    const float k1r[4] = {k1v.x, k1v.y, k1v.z, k1v.w};
+                    const float k2r[4] = {k2v.x, k2v.y, k2v.z, k2v.w};
+                    const float svr[4] = {sv.x, sv.y, sv.z, sv.w};
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        float m = agpr_read(acc[0][r]);
+#pragma unroll
+                        for (int nr = 1; nr < 16; nr++) m = __builtin_fmaxf(m, agpr_read(acc[nr][r]));
+                        const float t = (m + __builtin_fmaf(nmax, k1r[r], k2r[r])) - svr[r];
+                        if (__ballot(force || t >= 0.f)) wact |= 1u << r;
+                    }
+                }
+                if (wact != 0) {
+                    uint64_t vm[4];
+                    {
+                        uint4 vw0, vw1, aw0, aw1;
+                        uint32_t tmp;
+                        asm volatile("v_add_u32 %4, %5, %6\n\t"
+                                     "ds_read_b128 %0, %4 offset:1024\n\t"
+                                     "ds_read_b128 %1, %4 offset:1040\n\t"
+                                     "ds_read_b128 %2, %4 offset:1056\n\t"
+                                     "ds_read_b128 %3, %4 offset:1072\n\t"
+                                     "s_waitcnt lgkmcnt(0)"
+                                     : "=v"(vw0), "=v"(vw1), "=v"(aw0), "=v"(aw1), "=&v"(tmp)
+                                     : "s"(nsoff), "v"(sbase)
+                                     : "memory");
+                        const uint64_t words[4] = {((uint64_t)vw0.y << 32) | vw0.x, ((uint64_t)vw0.w << 32) | vw0.z,
+                                                   ((uint64_t)vw1.y << 32) | vw1.x, ((uint64_t)vw1.w << 32) | vw1.z};
+                        const uint64_t allows[4] = {((uint64_t)aw0.y << 32) | aw0.x, ((uint64_t)aw0.w << 32) | aw0.z,
+                                                    ((uint64_t)aw1.y << 32) | aw1.x, ((uint64_t)aw1.w << 32) | aw1.z};
+#pragma unroll
+                        for (int h = 0; h < 4; h++) {
+                            const uint64_t t = a.tile_begin + blk * 4 + h;
+                            uint64_t m = t < a.tile_end ? readfirstlane64(words[h]) : 0ull;
+                            if (a.allow) {
+                                const uint64_t aw = t - a.allow_t0;
+                                m &= aw < a.allow_words ? readfirstlane64(allows[h]) : 0ull;
+                            }
+                            vm[h] = m;
+                        }
+                    }
+                    const uint64_t slot0 = (a.tile_begin + blk * 4) * 64;
+                    // per active query slot gi: lane l tests its column's 16 rows against query
+                    // qlane + gi, and row l >> 4 of v holds that query's list (K3d's slow path;
+                    // four groups, each its own unrolled copy reading its accumulators in place)
+                    sd_static_for<4>([&](auto G) {
+                        constexpr int gi = decltype(G)::value;
+                        if (((wact >> gi) & 1u) == 0) return;
+                        const uint32_t ql = (uint32_t)gi + (uint32_t)qlane;
+                        const uint32_t la = laddr + ql * (SCREEN_M * 8) + 8u * (uint32_t)(lane & 15);
+                        const uint32_t ta = tbase + 4u * ql;
+                        uint2 v2;
+                        float wt, ws, em, k1, k2;
+                        asm volatile("ds_read_b64 %0, %6\n\t"
+                                     "ds_read_b32 %1, %7\n\t"
+                                     "ds_read_b32 %2, %7 offset:256\n\t"
+                                     "ds_read_b32 %3, %7 offset:1024\n\t"
+                                     "ds_read_b32 %4, %7 offset:512\n\t"
+                                     "ds_read_b32 %5, %7 offset:768\n\t"
+                                     "s_waitcnt lgkmcnt(0)"
+                                     : "=v"(v2), "=v"(wt), "=v"(ws), "=v"(em), "=v"(k1), "=v"(k2)
+                                     : "v"(la), "v"(ta)
+                                     : "memory");
+                        uint64_t v = ((uint64_t)v2.y << 32) | v2.x;
+                        const int li = lane & 15;
+#pragma unroll
+                        for (int nr = 0; nr < 16; nr++) {
+                            const uint64_t m64 = ((vm[nr >> 2] >> (16 * (nr & 3))) & 0xFFFFull) * 0x0001000100010001ull;
+                            float nrm;  // the row norm of this lane's column (read here: 16 fewer live VGPRs)
+                            asm volatile("ds_read_b32 %0, %1 offset:%2\n\t"
+                                         "s_waitcnt lgkmcnt(0)"
+                                         : "=v"(nrm)
+                                         : "v"(nbase + nsoff), "n"(64 * nr)
+                                         : "memory");
+                            const float u = agpr_read(acc[nr][gi]) + __builtin_fmaf(nrm, k1, k2);
+                            uint64_t pass = __ballot(!(u < ws)) & m64;
+                            while (pass) {
+                                const int j = __builtin_ctzll(pass);
+                                pass &= pass - 1;
+                                const int g = j >> 4;
+                                const float lower =
+                                    sc_lower(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(u), j)), cosine);
+                                float wtg = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wt), j));
+                                if (!(lower <= wtg)) continue;
+                                const uint64_t key = ((uint64_t)wvg_ord_f32(lower) << 32) |
+                                                     (uint32_t)(slot0 + 16u * (uint32_t)nr + (uint32_t)(j & 15));
+                                if (!(key < readlane64(v, 16 * g + SCREEN_M - 1))) continue;
+                                const bool inrow = (lane >> 4) == g;
+                                const int pos = __popcll(__ballot(inrow && v < key));
+                                const uint64_t sh = row_shr1_64(v);
+                                v = inrow ? (li > pos ? sh : (li == pos ? key : v)) : v;
+                                const uint64_t nk = readlane64(v, 16 * g + K - 1);
+                                const uint64_t nm = readlane64(v, 16 * g + SCREEN_M - 1);
+                                const float emg = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(em), j));
+                                if (nk != WVG_KEY_NONE) wtg = fminf(wtg, sc_tau_k(key_lower(nk), emg, cosine));
+                                if (nm != WVG_KEY_NONE) wtg = fminf(wtg, key_lower(nm));
+                                const float wsg = sc_sigma(wtg, cosine);
+                                wt = inrow ? wtg : wt;
+                                ws = inrow ? wsg : ws;
+                                pass &= ~(0xFFFFull << (16 * g)) | __ballot(!(u < ws));
+                            }
+                        }
+                        const uint2 o2 = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+                        asm volatile("ds_write_b64 %0, %1" ::"v"(la), "v"(o2) : "memory");
+                        if (li == 0)
+                            asm volatile("ds_write_b32 %0, %1\n\t"
+                                         "ds_write_b32 %0, %2 offset:256" ::"v"(ta), "v"(wt), "v"(ws)
+                                         : "memory");
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    });
+                }
+            } else if constexpr ((DIAG & 8) != 0) {
+                // diagnostic (DIAG 10): the stage loop alone, the accumulators consumed by one sum
+                float x = 0.f;
+#pragma unroll
+                for (int nr = 0; nr < 16; nr++) x += agpr_read(acc[nr][0]);
+                if (x == 0x1p-120f) a.partials[0] = 0;
+            }
+#pragma unroll
+            for (int nr = 0; nr < 16; nr++) acc[nr] = (floatx4){0.f, 0.f, 0.f, 0.f};
+            read_q(I0{}, I0{}, bq0, rbase);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int ql = 0; ql < 16; ql++) {
+        const uint32_t q = q0 + (uint32_t)(16 * w + ql);
+        if (q >= a.nq) break;
+        const uint64_t x = lane < M ? lists[((size_t)w * 16 + ql) * M + lane] : WVG_KEY_NONE;
+        uint64_t *out = a.partials + ((size_t)q * a.nrr + rr) * M;
+        if (lane < M) out[lane] = x;
+        if (lane == K - 1 && x != WVG_KEY_NONE) {
+            const float t = sc_tau_k(key_lower(x), cem[16 * w + ql], cosine);
+            atomicMin(a.gbound + q, wvg_ord_f32(t));
+        }
+    }
+}
+
 #endif  // WVG_TOOLS
 
 // ---------------------------------------------------------------------------
@@ -2268,7 +2661,7 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
 {
     const uint32_t kbn = screen_kblocks(L.dim);
     const uint32_t nq16 = (L.nq + 15) / 16, nq_pad = (L.nq + SC_BQ - 1) / SC_BQ * SC_BQ;
-    const uint32_t nqb = nq_pad / SC_BQ;
+    uint32_t nqb = nq_pad / SC_BQ;  // (K3g, tools: 64-query blocks)
     hipError_t e;
     // query fragments for every 16-query group of the padded batch
     hipLaunchKernelGGL(screen_qfrag_kernel, dim3((unsigned)(((uint64_t)nq_pad / 16 * kbn * 64 + 255) / 256)), dim3(256),
@@ -2384,9 +2777,11 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
         kern = kbn == 24 ? &screen_ar32_kernel<24> : &screen_ar32_kernel<16>;
     if (tuning().screen_variant == 3 && kern)  // K3f (two waves per SIMD)
         kern = kbn == 24 ? &screen_ar16_kernel<24> : &screen_ar16_kernel<16>;
+    const bool k3g = tuning().screen_variant == 4 && kern;  // K3g (two 4-wave workgroups per CU)
+    if (k3g) kern = kbn == 24 ? &screen_ar16x2_kernel<24> : &screen_ar16x2_kernel<16>;
     if (tuning().screen_variant >= 2 && kern)
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  SD_LDS);
+                                  k3g ? SG_LDS : SD_LDS);
     if (kbn == 24) {  // K3d diagnostics: separately compiled instantiations
         switch (tuning().screen_diag) {
         case 1: kern = &screen_ar_kernel<24, 1>; break;
@@ -2416,7 +2811,16 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
     if (tuning().screen_variant == 1) kern = nullptr;
     k3f = kern == &screen_ar16_kernel<24> || kern == &screen_ar16_kernel<16> || kern == &screen_ar16_kernel<24, 10>;
 #endif
-    const uint32_t threads = k3f ? SF_WAVES * 64 : kern ? SD_WAVES * 64 : SC_WAVES * 64, lds = kern ? SD_LDS : SC_LDS;
+#ifdef WVG_TOOLS
+    if (k3g) {  // 64-query workgroups: twice the query blocks
+        nqb = nq_pad / SG_BQ;
+        a.nqb = nqb;
+    }
+    const uint32_t lds = k3g ? SG_LDS : kern ? SD_LDS : SC_LDS;
+#else
+    const uint32_t lds = kern ? SD_LDS : SC_LDS;
+#endif
+    const uint32_t threads = k3f ? SF_WAVES * 64 : kern ? SD_WAVES * 64 : SC_WAVES * 64;
     if (!kern) kern = &screen_kernel;
     // Phased screen: the first r1 ranges (one workgroup per CU) run alone; their
     // lists' joint tau* (k-th smallest lower bound over ~10 % of the rows,
