@@ -86,10 +86,13 @@ typedef struct wvg_options {
                                   2 * dim bytes per row of capacity + 4 bytes of row-norm bound per row
                                   (15.4 GB at 10M x 768), kept until the corpus is destroyed or grows. */
     int32_t coalesce;          /* 1 (default): concurrent single-query wvg_search calls on one corpus
-                                  (no allow list) join one batched launch -- while a batch runs, the calls
-                                  that arrive queue up and the next batch takes them all; each caller gets
-                                  exactly its own results (identical to a call of its own); a lone call
-                                  does not wait.  0: every call launches on its own. */
+                                  join one batched launch -- while a batch runs, the calls that arrive
+                                  queue up and the next batch takes them all (filtered calls, each with its
+                                  own allow list, in batches of their own; any mix of k, run at the
+                                  largest); right after a batch the next one waits a short window (at most
+                                  an eighth of that batch's run time) for the callers just answered; each
+                                  caller gets exactly its own results (identical to a call of its own); a
+                                  lone call does not wait.  0: every call launches on its own. */
 } wvg_options;
 void wvg_options_default(wvg_options *opts);
 int wvg_open_ex(int device, const wvg_options *opts, wvg_ctx **out);
