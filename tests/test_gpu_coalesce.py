@@ -89,6 +89,35 @@ def test_concurrent_calls_equal_serial_calls(ctx, orc, kind, metric, d, threads)
     c.destroy()
 
 
+@pytest.mark.parametrize("kind,metric,n", [
+    (KIND_F32, METRIC_L2, 20_000),
+    (KIND_F32, METRIC_L2, 150),    # fewer live rows than the batch's k: counts = min(live, k)
+    (KIND_BQ, METRIC_COSINE, 20_000),
+])
+def test_mixed_k_batches_give_each_caller_its_prefix(ctx, orc, kind, metric, n):
+    """Round 5: a coalesced batch runs at the largest k of its requests (up to
+    256) and hands each caller the first k of its rows -- exactly what a call
+    of its own returns, counts and the entries past the count included."""
+    d = 128
+    c = make_corpus(ctx, orc, kind, metric, n, d)
+    lib = _lib.load()
+    threads = 16
+    nq = 4 * threads
+    qs = np.ascontiguousarray(orc.synth_rows(711, 0, nq, d, 0))
+    ks = [(1, 256, 10, 100)[i % 4] for i in range(nq)]
+    live = n - len(range(5, n, 97))  # make_corpus deletes every 97th row from 5
+    serial = [one_search(lib, c, qs[i], ks[i]) for i in range(nq)]
+    for rep in range(3):
+        got = concurrent(lib, c, qs, ks, threads)
+        for i in range(nq):
+            si, sd, sc = serial[i]
+            gi, gd, gc = got[i]
+            assert gc == sc == min(ks[i], live), (rep, i)
+            assert np.array_equal(gi, si), (rep, i)
+            assert np.array_equal(gd.view(np.uint32), sd.view(np.uint32)), (rep, i)
+    c.destroy()
+
+
 def test_coalescing_can_be_switched_off(ctx, orc):
     """wvg_options.coalesce = 0: every call launches alone -- same results."""
     n, d = 5000, 64
