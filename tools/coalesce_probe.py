@@ -3,7 +3,9 @@
 threads (bench.py's tools/host_calls.c loop) calling wvg_search with one query
 each for `--seconds`; per T the QPS, latency percentiles and the coalescer's
 batch counters (wvgx_coalesce_counters: batches, requests, time running
-batches, largest batch), plus a direct nq-query call's time for reference.
+batches, largest batch), plus a direct nq-query call's time for reference;
+at T = 1 also the host time inside the in-launch single-query path
+(wvgx_single_timing).
 Usage: WVG_LIB=tools/libwvgpu_tools.so python tools/coalesce_probe.py [--callers 1,16,32,64]"""
 import argparse
 import ctypes
@@ -44,10 +46,20 @@ def main():
             c.search(qs[:nq], k)
         print(json.dumps({"direct_call_nq": nq, "ms_per_call": round((time.perf_counter() - t0) / 5 * 1e3, 3)}),
               flush=True)
+    st = (ctypes.c_uint64 * 5)()
     for T in (int(x) for x in a.callers.split(",")):
         lib.wvgx_coalesce_counters(cnt, 1)
+        lib.wvgx_single_timing(st, 1)
         qps, lat = bench._native_callers(hc, lib, c.handle, qs, k, T, a.seconds)
         lib.wvgx_coalesce_counters(cnt, 1)
+        lib.wvgx_single_timing(st, 1)
+        if T == 1 and st[4]:  # host time inside search_batch of the in-launch single-query path
+            n1 = int(st[4])
+            print(json.dumps({"single_host_us": {"entry_to_launch": round(st[0] / n1 / 1e3, 2),
+                                                 "launch_call": round(st[1] / n1 / 1e3, 2),
+                                                 "poll_records": round(st[2] / n1 / 1e3, 2),
+                                                 "copy_out": round(st[3] / n1 / 1e3, 2), "calls": n1}}),
+                  flush=True)
         b, r, ns, mx = (int(x) for x in cnt)
         print(json.dumps({"callers": T, "qps": round(qps, 1), "p50_us": round(float(np.percentile(lat, 50)), 1),
                           "p99_us": round(float(np.percentile(lat, 99)), 1), "batches": b,

@@ -356,6 +356,13 @@ int wvgx_coalesce_counters(uint64_t *out4, int reset)
     return WVG_OK;
 }
 
+int wvgx_single_timing(uint64_t *out5, int reset)
+{
+    if (!out5) return WVG_ERR_INVALID;
+    wvg::single_timing_read(out5, reset != 0);
+    return WVG_OK;
+}
+
 // A/B knob of the tools build (not part of include/wvgpu.h): 0 = K1 scan variant,
 // 1 = K1 resident workgroups per CU, ... 7 = K8 ADC variant, 8 = query-stream merge wait (us),
 // 9 = serpentine scan order, 10 = K3b row-range length, 11 = K1 load policy, 12 = K3b SIMD pairing,

@@ -333,6 +333,7 @@ uint32_t screen_row_ranges(uint32_t nq, uint64_t ntiles, int num_cus);
 void screen_counters(uint64_t out[4], bool reset);
 void single_counters(uint64_t out[4], bool reset);
 void coalesce_counters(uint64_t out[4], bool reset);
+void single_timing_read(uint64_t out[5], bool reset);
 #endif
 hipError_t launch_shadow_build(const float *tiled, uint32_t dim, uint64_t t0, uint64_t t1, void *shadow, float *norms,
                                uint32_t *nmax, hipStream_t s);

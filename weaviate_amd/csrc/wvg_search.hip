@@ -574,9 +574,26 @@ void coalesce_counters(uint64_t out[4], bool reset)
 {
     for (int i = 0; i < 4; i++) out[i] = reset ? g_coal[i].exchange(0) : g_coal[i].load();
 }
+// host time of the in-launch single-query path (wvgx_single_timing): ns summed over
+// calls -- [0] search_batch entry -> launch call, [1] the launch call (run_search),
+// [2] polling for the tagged records, [3] copying them out; [4] calls
+static std::atomic<uint64_t> g_stime[5];
+static void single_timing(const std::chrono::steady_clock::time_point (&t)[5])
+{
+    for (int i = 0; i < 4; i++)
+        g_stime[i].fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t[i + 1] - t[i]).count(),
+                             std::memory_order_relaxed);
+    g_stime[4].fetch_add(1, std::memory_order_relaxed);
+}
+void single_timing_read(uint64_t out[5], bool reset)
+{
+    for (int i = 0; i < 5; i++) out[i] = reset ? g_stime[i].exchange(0) : g_stime[i].load();
+}
+#define WVG_STAMP(i) tstamp[i] = std::chrono::steady_clock::now()
 #else
 inline void single_counter(int, bool) {}
 inline void coalesce_counter(size_t, uint64_t) {}
+#define WVG_STAMP(i) ((void)0)
 #endif
 
 // Waits until a single query's tagged records (StreamJob::records) have all
@@ -793,6 +810,10 @@ int wvg_search(wvg_corpus *c, const float *queries, uint32_t nq, uint32_t k, con
 static int wvg::search_batch(wvg_corpus *c, const float *queries, uint32_t nq, uint32_t k, const uint64_t *allow_bits,
                              uint64_t allow_words, uint64_t *out_ids, float *out_dists, uint32_t *out_counts)
 {
+#ifdef WVG_TOOLS
+    std::chrono::steady_clock::time_point tstamp[5];
+#endif
+    WVG_STAMP(0);
     int rc;
     SearchPlan p = plan_search(c, nq, std::min(k, MAX_K), allow_bits, allow_words);
     if (p.empty) {
@@ -871,16 +892,23 @@ static int wvg::search_batch(wvg_corpus *c, const float *queries, uint32_t nq, u
         }
     }
     if (zc && !legacy) {
+        WVG_STAMP(1);
         rc = run_search(c, qin ? nullptr : b + o_q, qpitch, nq, k, d_allow, p, (uint64_t *)(b + o_part), nullptr,
                         nullptr, nullptr, s, g.slot, qin ? qinl : nullptr, &so);
         if (rc) return rc;
+        WVG_STAMP(2);
         rc = wait_records(so, k, s, (sp & 2) != 0);
         if (rc) return rc;
+        WVG_STAMP(3);
         const uint4 *r = so.records;
         for (uint32_t i = 0; i < k; i++) {
             if (out_ids) out_ids[i] = (uint64_t)r[i].x | (uint64_t)r[i].y << 32;
             if (out_dists) std::memcpy(out_dists + i, &r[i].z, 4);
         }
+#ifdef WVG_TOOLS
+        WVG_STAMP(4);
+        single_timing(tstamp);
+#endif
         const uint32_t c0 = r[k].x;
         if (c0 == WVG_RECORDS_TIMEOUT) {  // the in-launch merge gave up (empty entries were written)
             if (out_counts) *out_counts = 0;
