@@ -161,6 +161,9 @@ void wvg_options_default(wvg_options *o)
 
 int wvg_open(int device, wvg_ctx **out) { return wvg_open_ex(device, nullptr, out); }
 
+#ifdef WVG_TOOLS
+int wvgx_set_tuning(int key, int value);  // (tools A/B knobs, below)
+#endif
 int wvg_open_ex(int device, const wvg_options *opts, wvg_ctx **out)
 {
     if (!out) return fail(WVG_ERR_INVALID, "null out");
@@ -190,6 +193,18 @@ int wvg_open_ex(int device, const wvg_options *opts, wvg_ctx **out)
     if (const char *e = getenv("WVG_STREAM_VARIANT")) tuning().stream_variant = (int)strtol(e, nullptr, 10);  // A/B
     if (const char *e = getenv("WVG_SCREEN_SP")) tuning().screen_pilot_screen = (int)strtol(e, nullptr, 10);  // A/B
     if (const char *e = getenv("WVG_GROUPS_PER_CU")) tuning().groups_per_cu = (int)strtol(e, nullptr, 10);  // A/B
+    if (const char *e = getenv("WVG_TUNING")) {  // A/B: "key:value,key:value" -- any wvgx_set_tuning key
+        for (const char *p = e; *p;) {
+            char *end = nullptr;
+            const long key = strtol(p, &end, 10);
+            if (end == p || *end != ':') break;
+            p = end + 1;
+            const long val = strtol(p, &end, 10);
+            if (end == p) break;
+            (void)wvgx_set_tuning((int)key, (int)val);
+            p = *end == ',' ? end + 1 : end;
+        }
+    }
 #endif
     *out = c;
     return WVG_OK;
