@@ -470,6 +470,9 @@ int wvgx_set_tuning(int key, int value)
     } else if (key == 26) {
         old = t.screen_pilot_screen;
         t.screen_pilot_screen = value;
+    } else if (key == 27) {
+        old = t.k1_mq;
+        t.k1_mq = value;
     }
     return old;
 }

@@ -173,6 +173,7 @@ struct SearchPlan {
     uint32_t fb_groups = 0; // screen: K1 workgroups per flagged query's rescan
     uint32_t kbn = 0;       // screen: 32-element K blocks
     bool cosched = false; // PQ batch: co-scheduled K8e (ScanArgs::cosched)
+    int mq = 0;           // F32 co-scheduled batch: queries per K1Q workgroup (0 = one, the COS K1)
     bool empty = false;
     const uint64_t *allow_host = nullptr;  // the caller's allow words of tiles [tb, te), or null
     uint64_t allow_qstride = 0;            // per-query allow windows (ScanArgs::allow_qstride)
@@ -192,7 +193,8 @@ struct SearchPlan {
 };
 
 bool allow_tile_range(const wvg_corpus *c, const uint64_t *allow, uint64_t allow_words, uint64_t &tb, uint64_t &te);
-SearchPlan plan_search(wvg_corpus *c, uint32_t nq, uint32_t k, const uint64_t *allow, uint64_t allow_words);
+SearchPlan plan_search(wvg_corpus *c, uint32_t nq, uint32_t k, const uint64_t *allow, uint64_t allow_words,
+                       bool mq_ok = true);
 uint32_t next_direction(wvg_corpus *c, uint32_t nq);
 int pq_dense(const wvg_corpus *c, const uint64_t *d_allow);
 void prepare_queries_host(const wvg_corpus *c, const float *queries, uint32_t nq, std::vector<float> &qf,

@@ -316,6 +316,76 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_kernel(ScanArgs a, u
     group_combine_store<E, SCAN_WAVES>(tk, partials + ((size_t)qi * G + rng) * a.k);
 }
 
+// K1Q (round 5): co-scheduled small batches with Q queries per workgroup.  The
+// COS grid gives each (row range, query) its own workgroup; the nq workgroups of a
+// range read the same rows side by side, so every row crosses from L2 to the CUs
+// nq times and the batch is L2-bound (64 queries over 1M x 128: 32 GB of L2 reads,
+// ~2 ms).  Here a wave loads each 32-float block of its row once and folds it into
+// the Q queries' AVX2-order chains (acc[Q][4][8]: every query's distance is the
+// same chain as a scan of its own, so results are bit-identical), then offers each
+// query its key: a quarter of the L2 traffic at Q = 4.  Unfiltered batches only
+// (every query's tile mask is the validity word), L2 / dot / cosine, fixed D.
+template <int METRIC, int D, int E, int Q>
+__global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_mq_kernel(ScanArgs a, uint64_t *partials)
+{
+    static_assert(D % 32 == 0 && D > 0 && !is_abs_or_neq<METRIC>, "K1Q: fixed D, the AVX2 chains");
+    const uint32_t nqg = (a.nq + Q - 1) / Q;
+    const uint32_t G = gridDim.x / nqg;
+    const uint32_t kk = blockIdx.x >> 3;
+    const uint32_t rng = (kk / nqg) * 8u + (blockIdx.x & 7u), qg = kk % nqg;
+    const uint64_t ntiles = a.tile_end - a.tile_begin, total = (uint64_t)G * SCAN_WAVES;
+    const uint64_t gw = (uint64_t)rng * SCAN_WAVES + wave_id();
+    const uint64_t t0 = a.tile_begin + ntiles * gw / total, t1 = a.tile_begin + ntiles * (gw + 1) / total;
+    const int lane = threadIdx.x & 63;
+    const float4 *q4[Q];
+#pragma unroll
+    for (int j = 0; j < Q; j++) {  // (a short last group repeats its last query and stores nothing for it)
+        const uint32_t qi = qg * Q + j < a.nq ? qg * Q + j : a.nq - 1;
+        q4[j] = reinterpret_cast<const float4 *>(a.queries) + (size_t)qi * (a.qpitch / 4);
+    }
+    WaveTopK<E> tk[Q];
+#pragma unroll
+    for (int j = 0; j < Q; j++) tk[j].init((int)a.k);
+    const float4 *data = reinterpret_cast<const float4 *>(a.data);
+    const bool rev = (a.reverse & 1u) != 0;
+    const uint64_t n = t1 - t0;
+    uint64_t m_next = n ? a.valid[rev ? t1 - 1 : t0] : 0ull;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t t = rev ? t1 - 1 - i : t0 + i;
+        const uint64_t m = m_next;
+        if (i + 1 < n) m_next = a.valid[rev ? t - 1 : t + 1];  // scalar prefetch of the next mask
+        if (m == 0ull) continue;
+        const float4 *rp = data + (size_t)t * a.nchunks * 64 + lane;
+        float acc[Q][4][8];
+#pragma unroll
+        for (int j = 0; j < Q; j++)
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+#pragma unroll
+                for (int l = 0; l < 8; l++) acc[j][r][l] = 0.0f;
+        constexpr int NB = D / 32;
+#pragma unroll 2
+        for (int b = 0; b < NB; b++) {
+            float4 xs[8];
+#pragma unroll
+            for (int cc = 0; cc < 8; cc++) xs[cc] = rp[(size_t)(b * 8 + cc) * 64];
+#pragma unroll
+            for (int j = 0; j < Q; j++)
+#pragma unroll
+                for (int cc = 0; cc < 8; cc++) chunk_update<METRIC>(acc[j], cc, q4[j][b * 8 + cc], xs[cc]);
+        }
+#pragma unroll
+        for (int j = 0; j < Q; j++)
+            tk[j].offer(lane_key(m, wrap_metric(a.metric, avx256_reduce(acc[j], 0.0f)), t, lane));
+    }
+#pragma unroll
+    for (int j = 0; j < Q; j++) {
+        const uint32_t qi = qg * Q + j;
+        if (qi < a.nq) group_combine_store<E, SCAN_WAVES>(tk[j], partials + ((size_t)qi * G + rng) * a.k);
+        __syncthreads();  // the combine's LDS is reused by the next query
+    }
+}
+
 // The exact rescan of a query list (the K3c screen's flagged queries, whose
 // candidate lists overflowed): block (g, f) scans slice g for the listed
 // queries f, f + gridDim.y, ... < *nlist; partials [f][groups][k].
@@ -685,6 +755,23 @@ static void launch_fixed(const ScanArgs &a, uint64_t *partials, dim3 grid, dim3 
 template <int METRIC, int E>
 static hipError_t launch_f32_e(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
 {
+    if constexpr (!is_abs_or_neq<METRIC>) {
+        // K1Q: ScanArgs::cosched = Q >= 2 queries per workgroup (plan_search sets it for unfiltered
+        // L2 / dot / cosine batches at d = 128 / 768; groups = its row ranges)
+        if ((a.cosched == 2 || a.cosched == 4) && a.nq > 1 && groups % 8 == 0 && !a.side.active && !a.allow &&
+            !a.order512 && (a.dim == 128 || a.dim == 768)) {
+            const uint32_t nqg = (a.nq + (uint32_t)a.cosched - 1) / (uint32_t)a.cosched;
+            dim3 grid((unsigned)groups * nqg), block(SCAN_WAVES * 64);
+            if (a.cosched == 4) {
+                if (a.dim == 128) launch_timed((scan_f32_mq_kernel<METRIC, 128, E, 4>), grid, block, 0, s, a, partials);
+                else launch_timed((scan_f32_mq_kernel<METRIC, 768, E, 4>), grid, block, 0, s, a, partials);
+            } else {
+                if (a.dim == 128) launch_timed((scan_f32_mq_kernel<METRIC, 128, E, 2>), grid, block, 0, s, a, partials);
+                else launch_timed((scan_f32_mq_kernel<METRIC, 768, E, 2>), grid, block, 0, s, a, partials);
+            }
+            return hipGetLastError();
+        }
+    }
     if (a.cosched && a.nq > 1 && groups % 8 == 0 && !a.side.active) {
         dim3 grid((unsigned)groups * a.nq), block(SCAN_WAVES * 64);
         switch (a.dim) {

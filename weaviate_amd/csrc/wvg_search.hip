@@ -208,7 +208,8 @@ ScreenWs screen_ws(uint32_t nq, uint32_t k, uint32_t nrr, uint32_t kbn, uint32_t
     return w;
 }
 
-SearchPlan plan_search(wvg_corpus *c, uint32_t nq, uint32_t k, const uint64_t *allow, uint64_t allow_words)
+SearchPlan plan_search(wvg_corpus *c, uint32_t nq, uint32_t k, const uint64_t *allow, uint64_t allow_words,
+                       bool mq_ok)
 {
     SearchPlan p;
     p.empty = !allow_tile_range(c, allow, allow_words, p.tb, p.te) || k == 0 || nq == 0;
@@ -250,7 +251,15 @@ SearchPlan plan_search(wvg_corpus *c, uint32_t nq, uint32_t k, const uint64_t *a
         ScanArgs a1 = a;
         a1.nq = 1;
         p.cosched = true;
-        p.groups = pq_cosched_groups(nq, std::max(scan_groups_for(a1, c->ctx->num_cus), 8));
+        // K1Q (unfiltered L2 / dot / cosine at d = 128 / 768): Q queries per workgroup, so the
+        // grid is sized for the nq / Q query groups (profiles/r05/k1q/)
+        const int q = tuning().k1_mq;
+        p.mq = mq_ok && !allow && (q == 2 || q == 4) && !c->ctx->order512 && (c->dim == 128 || c->dim == 768) &&
+                       (c->metric == WVG_METRIC_L2 || c->metric == WVG_METRIC_DOT || c->metric == WVG_METRIC_COSINE)
+                   ? q
+                   : 0;
+        p.groups = pq_cosched_groups(p.mq ? (nq + p.mq - 1) / p.mq : nq,
+                                     std::max(scan_groups_for(a1, c->ctx->num_cus), 8));
     }
     return p;
 }
@@ -348,7 +357,7 @@ int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t nq, uin
     a.pq_m = c->pq_m;
     a.pq_ks = c->pq_ks;
     a.dense = pq_dense(c, d_allow);
-    a.cosched = p.cosched;
+    a.cosched = p.cosched ? (p.mq >= 2 ? p.mq : 1) : 0;  // (K1Q: queries per workgroup)
     a.order512 = c->ctx->order512;
     a.plain = plain_loads(c, p.tb, p.te);
     a.cache_tail256 = k1_cache_tail(c, p.tb, p.te);
@@ -986,7 +995,7 @@ static int wvg::search_batch_filtered(wvg_corpus *c, const std::vector<wvg_searc
     std::vector<uint64_t> win((size_t)B * W, 0ull);  // query i's allow words of tiles [TB, TE) (0 outside its own)
     for (uint32_t i = 0; i < B; i++)
         if (live[i]) std::memcpy(win.data() + (size_t)i * W + (tb[i] - TB), batch[i]->allow + wb + tb[i], (te[i] - tb[i]) * 8);
-    SearchPlan p = plan_search(c, B, k, nullptr, 0);
+    SearchPlan p = plan_search(c, B, k, nullptr, 0, false);  // (per-query allow windows: the COS K1)
     if (p.empty) return WVG_OK;
     if (p.gemm || !p.cosched) return fail(WVG_ERR_INVALID, "filtered coalesced batch needs the co-scheduled K1");
     p.tb = TB;
