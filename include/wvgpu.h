@@ -90,7 +90,7 @@ typedef struct wvg_options {
                                   queue up and the next batch takes them all (filtered calls, each with its
                                   own allow list, in batches of their own; any mix of k, run at the
                                   largest); right after a batch of 4 or more the next one waits a short window
-                                  (at most an eighth of that batch's run time) for the callers just answered; each
+                                  (at most a quarter of that batch's run time) for the callers just answered; each
                                   caller gets exactly its own results (identical to a call of its own); a
                                   lone call does not wait.  0: every call launches on its own. */
 } wvg_options;

@@ -473,6 +473,9 @@ int wvgx_set_tuning(int key, int value)
     } else if (key == 27) {
         old = t.k1_mq;
         t.k1_mq = value;
+    } else if (key == 28 && value > 0) {
+        old = t.gather_div;
+        t.gather_div = value;
     }
     return old;
 }

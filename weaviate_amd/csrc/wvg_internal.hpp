@@ -435,6 +435,9 @@ struct Tuning {
                              // bit 0 between phases (else the lists' k-th lower bound + 2 Emax), bit 1 before
                              // the final collect (A/B)
     int screen_range_blocks = 0;  // K3c row-range length in 256-row blocks (0 = auto, ~128; A/B)
+    int gather_div = 4;      // coalescer gathering window: at most the last batch's run time / this (key 28;
+                             // with K1Q batches 4 beat 8: 16 callers 47.6-54.7k -> 64.7k QPS,
+                             // profiles/r05/coalesce/gather_window_k1q.txt)
     int k1_mq = 4;           // F32 co-scheduled batches (tuning key 27): queries per K1Q workgroup, 2 or 4
                              // (0 = the COS K1, one query per workgroup)
     int screen_pilot_screen = 0;  // K3c/K3d (tuning key 26): tiles of the SCREEN pilot -- the bf16 screen itself over

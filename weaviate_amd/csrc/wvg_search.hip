@@ -737,8 +737,8 @@ static int search_coalesced(wvg_corpus *c, const float *query, uint32_t k, const
         // (profiles/r05/coalesce/).  When the last batch (of more than one request)
         // ended moments ago, the runner waits a short window until its callers are back
         // too: the requests that were waiting when it ended + as many as it held.  The
-        // window is at most an eighth of that batch's run time and 50 us + 3 us per
-        // caller to wake (64 callers on 16 cores take ~200 us to return), at least 10
+        // window is at most a quarter of that batch's run time (tuning gather_div) and
+        // 50 us + 3 us per caller to wake (64 callers on 16 cores take ~200 us), at least 10
         // us.  Only after batches of 4 or more: a lone caller never waits, and two or
         // three callers gain little from merged batches (2 queries: 0.10 ms vs 0.08 ms
         // for one) but would pay the window whenever one of them does not come back.
@@ -747,7 +747,7 @@ static int search_coalesced(wvg_corpus *c, const float *query, uint32_t k, const
             const auto window = std::max<std::chrono::nanoseconds>(
                 std::chrono::microseconds(10),
                 std::min<std::chrono::nanoseconds>(std::chrono::microseconds(50 + 3 * (int64_t)co.last_n),
-                                                   co.last_run / 8));
+                                                   co.last_run / tuning().gather_div));
             const auto until = co.last_done + window;
             if (std::chrono::steady_clock::now() < until) {
                 co.gathering = true;
