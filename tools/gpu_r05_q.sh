@@ -3,7 +3,7 @@
 # the current build (lone queries at two workgroups per CU, mixed-k coalescing,
 # native host-API callers).
 set -o pipefail
-O=gpurun_out/r05final3
+O=gpurun_out/r05final4
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || exit 1
