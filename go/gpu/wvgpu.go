@@ -173,13 +173,14 @@ type Options struct {
 	MergeWaitUs    uint32 // query-stream merge wait bound (default 4 s)
 	BatchScreen    int32  // 1: bf16 screen + exact rescore for batches (default); 0: exact fp32 MFMA only
 	Coalesce       int32  // 1: concurrent single-query searches of a corpus share launches (default)
+	HeapReplay     int32  // 1: BQ candidates / rescore exactly as Weaviate's heaps pick them (default)
 }
 
 func DefaultOptions() Options {
 	var o C.wvg_options
 	C.wvg_options_default(&o)
 	return Options{uint32(o.mfma_min_queries), int32(o.cache_reuse), uint32(o.merge_wait_us), int32(o.batch_screen),
-		int32(o.coalesce)}
+		int32(o.coalesce), int32(o.heap_replay)}
 }
 
 func OpenWith(device int, o *Options) (*Ctx, error) {
@@ -192,6 +193,7 @@ func OpenWith(device int, o *Options) (*Ctx, error) {
 		opt.cache_reuse = C.int32_t(o.CacheReuse)
 		opt.batch_screen = C.int32_t(o.BatchScreen)
 		opt.coalesce = C.int32_t(o.Coalesce)
+		opt.heap_replay = C.int32_t(o.HeapReplay)
 	}
 	var h *C.wvg_ctx
 	if e := err(C.wvg_open_ex(C.int(device), &opt, &h)); e != nil {
@@ -583,6 +585,28 @@ func (x *Corpus) SearchBQRescore(f32 *Corpus, qs []float32, nq, k, rescoreLimit 
 	if e := err(C.wvg_search_bq_rescore(x.h, f32.h, f32p(qs), C.uint32_t(nq), C.uint32_t(k),
 		C.uint32_t(rescoreLimit), u64p(words), C.uint64_t(len(words)), u64p(r.IDs), f32p(r.Dists),
 		u32p(r.Counts))); e != nil {
+		return nil, e
+	}
+	return r, nil
+}
+
+// SearchBQCandidates: the first half of flat.searchByVectorBQ when the float
+// rows stay in the LSM store (V/flat/index.go:355-374): the ids and Hamming
+// distances findTopVectorsCached leaves in its heap of rescoreLimit, in the
+// order heap.Pop() returns them.  Fetch those rows with vectorById and pass
+// them, in this order, to Ctx.Rescore.
+func (x *Corpus) SearchBQCandidates(qs []float32, nq, rescoreLimit int, allow helpers.AllowList) (*Results, error) {
+	defer pin(x)()
+	r := emptyResults(nq, rescoreLimit)
+	if nq == 0 || rescoreLimit == 0 {
+		return r, nil
+	}
+	words, ok := allowBitmap(allow)
+	if !ok {
+		return r, nil
+	}
+	if e := err(C.wvg_search_bq_candidates(x.h, f32p(qs), C.uint32_t(nq), C.uint32_t(rescoreLimit), u64p(words),
+		C.uint64_t(len(words)), u64p(r.IDs), f32p(r.Dists), u32p(r.Counts))); e != nil {
 		return nil, e
 	}
 	return r, nil

@@ -29,8 +29,10 @@ extern "C" {
 #endif
 
 /* 2: wvg_options gained `coalesce` (round 4) and the device-memory / stream
- * entry points were added (wvg_device_alloc ... wvg_memcpy_d2h). */
-#define WVG_ABI_VERSION 2
+ * entry points were added (wvg_device_alloc ... wvg_memcpy_d2h).
+ * 3: wvg_options gained `heap_replay`; wvg_search_bq_candidates; the
+ * multi-GPU handle (wvg_multi_*). */
+#define WVG_ABI_VERSION 3
 
 #define WVG_OK 0
 #define WVG_ERR_INVALID -1       /* bad argument (null, k < 0 analogue, bad kind) */
@@ -93,6 +95,14 @@ typedef struct wvg_options {
                                   (at most a quarter of that batch's run time) for the callers just answered; each
                                   caller gets exactly its own results (identical to a call of its own); a
                                   lone call does not wait.  0: every call launches on its own. */
+    int32_t heap_replay;       /* 1 (default): wvg_search_bq_rescore / wvg_search_bq_candidates return
+                                  exactly what Weaviate's heaps return (V/flat/index.go:347-389,
+                                  497-520): which rows of a tie at the R-th Hamming distance become
+                                  candidates, their pop order, and the k-heap's choice and order among
+                                  equal exact distances.  The scan also records the rows the heap could
+                                  insert and the host replays the heap over them (~R ln(rows) per query).
+                                  0: candidates = the (distance, docID)-lexicographic top-R, results
+                                  ascending by (distance, docID) -- identical except at such ties. */
 } wvg_options;
 void wvg_options_default(wvg_options *opts);
 int wvg_open_ex(int device, const wvg_options *opts, wvg_ctx **out);
@@ -213,6 +223,17 @@ int wvg_search_bq_rescore(wvg_corpus *bq, wvg_corpus *f32, const float *queries,
                           uint32_t k, uint32_t rescore_limit, const uint64_t *allow_bits,
                           uint64_t allow_words, uint64_t *out_ids, float *out_dists,
                           uint32_t *out_counts);
+/* The first half of searchByVectorBQ for callers whose float rows are not on
+ * the GPU (the LSM "vectors" bucket, V/flat/index.go:375-380): the candidates
+ * findTopVectorsCached leaves in its heap of R = rescore_limit (index.go:
+ * 355-357, 456-495) in the order heap.Pop() returns them (:369-374), i.e.
+ * descending Hamming distance with the heap's own order among ties.  Outputs
+ * [nq][R] ids / Hamming distances, counts[nq]; feed them in this order to
+ * wvg_rescore (which inserts in input order, as :375-385 does).  With
+ * heap_replay = 0: the lexicographic top-R, descending.  R <= 256.         */
+int wvg_search_bq_candidates(wvg_corpus *bq, const float *queries, uint32_t nq, uint32_t rescore_limit,
+                             const uint64_t *allow_bits, uint64_t allow_words, uint64_t *out_ids,
+                             float *out_dists, uint32_t *out_counts);
 
 /* flat.SearchByVectorDistance (V/flat/index.go:531-591): every row with
  * dist <= target_distance or |dist - target| <= 1e-6 (floatcomp.InDelta,
@@ -292,7 +313,10 @@ int wvg_topk_merge_packed(wvg_ctx *ctx, const void *d_packed, uint32_t nq, uint3
 /* The rescore loop of flat.searchByVectorBQ (V/flat/index.go:375-385) when
  * the candidate rows come from the host (LSM point gets): exact SingleDist of
  * q against rows [n][dim] (q used as given: normalize it first for cosine,
- * as index.go:352 does) and the top-k of (dist, id).  out_count = min(k, n). */
+ * as index.go:352 does), each inserted into a heap of k in input order
+ * (insertToHeap, :384) and extracted (extractHeap, :508-520), so ties among
+ * equal distances resolve exactly as the reference's heap resolves them
+ * (heap_replay = 0: ascending by (dist, input position)).  out_count = min(k, n). */
 int wvg_rescore(wvg_ctx *ctx, int metric, const float *q, const float *rows, const uint64_t *ids,
                 uint64_t n, uint32_t dim, uint32_t k, uint64_t *out_ids, float *out_dists,
                 uint32_t *out_count);

@@ -670,6 +670,30 @@ ORC_API long orc_flat_search_bq(const float *rows, const uint64_t *codes, long n
                              out_dists, cand_ids);
 }
 
+/* The candidate half of searchByVectorBQ alone, over precomputed Hamming
+ * distances of ids 0..n-1 (so a caller can stream a corpus too large for
+ * one buffer of codes through orc_bq_dist_all): findTopVectorsCached's heap
+ * of `rescore` over ascending ids (V/flat/index.go:456-495) and the pop loop
+ * (:369-374).  Writes the ids / distances in pop order; returns the count. */
+ORC_API long orc_heap_pops(const float *dists, long n, const uint8_t *valid, long rescore, uint64_t *out_ids,
+                           float *out_dists)
+{
+    if (rescore <= 0) return 0;
+    orc_heap h = { (orc_item *)malloc(sizeof(orc_item) * (size_t)(rescore + 1)), 0 };
+    for (long i = 0; i < n; i++) {
+        if (valid && !valid[i]) continue;
+        insert_to_heap(&h, rescore, (uint64_t)i, dists[i]);
+    }
+    long nc = h.len;
+    for (long i = 0; i < nc; i++) {
+        orc_item it = heap_pop(&h);
+        out_ids[i] = it.id;
+        out_dists[i] = it.dist;
+    }
+    free(h.items);
+    return nc;
+}
+
 /* The same with the rescore distance from `fn` (the reference's own l2_256 /
  * dot_256 from oracle/_ref in the CPU baseline), else the restatement. */
 static long flat_search_bq_fn(const float *rows, const uint64_t *codes, long n, long d, long pitch,

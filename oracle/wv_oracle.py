@@ -71,6 +71,8 @@ def lib():
         l.orc_flat_search_bq.restype = c_long
         l.orc_flat_search_bq.argtypes = [_F, _U64, c_long, c_long, c_long, _U8, _F, c_long, c_long, c_int, _U64, _F,
                                          _U64]
+        l.orc_heap_pops.restype = c_long
+        l.orc_heap_pops.argtypes = [_F, c_long, _U8, c_long, _U64, _F]
         l.orc_synth_value.restype = c_float
         l.orc_synth_value.argtypes = [c_uint64, c_uint64, c_uint64, c_int]
         l.orc_synth_rows.argtypes = [c_uint64, c_uint64, c_long, c_long, c_long, c_int, _F]
@@ -295,6 +297,23 @@ def flat_search_bq(rows, q, k, rescore_limit, metric, valid=None):
     cnt = lib().orc_flat_search_bq(_f(rows), _u64(codes), n, d, d, _u8(v) if v is not None else None, _f(q), k,
                                    rescore_limit, metric, _u64(oid), _f(od), _u64(cand))
     return oid[:cnt], od[:cnt]
+
+
+def heap_pops(dists, rescore, valid=None):
+    """findTopVectorsCached's heap of `rescore` over ids 0..n-1 with these
+    distances, and the pop loop of searchByVectorBQ (V/flat/index.go:369-374):
+    (ids, dists) in pop order."""
+    dists = f32(dists)
+    oid = np.empty(max(rescore, 1), dtype=np.uint64)
+    od = np.empty(max(rescore, 1), dtype=np.float32)
+    v = None if valid is None else np.ascontiguousarray(valid, dtype=np.uint8)
+    cnt = lib().orc_heap_pops(_f(dists), len(dists), _u8(v) if v is not None else None, rescore, _u64(oid), _f(od))
+    return oid[:cnt], od[:cnt]
+
+
+def bq_heap_pops(codes, qcode, rescore, valid=None):
+    """heap_pops over the Hamming distances of codes [n][w] to qcode."""
+    return heap_pops(bq_dist_all(qcode, codes), rescore, valid)
 
 
 def synth_rows(seed, row0, n, d, dist=0):

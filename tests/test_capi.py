@@ -37,7 +37,7 @@ def test_abi_version_and_error_path():
     from weaviate_amd import _lib
 
     lib = _lib.load()
-    assert lib.wvg_abi_version() == _lib.ABI_VERSION == 2
+    assert lib.wvg_abi_version() == _lib.ABI_VERSION == 3
     # a null-argument call returns a negative status and sets the message
     rc = lib.wvg_device_count(None)
     assert rc == _lib.WVG_ERR_INVALID

@@ -236,10 +236,10 @@ def test_bq_rescore_and_distance_to_node(ctx, orc, metric):
     b.upsert(np.arange(n, dtype=np.uint64), rows)
     ids, dists, counts = search_bq_rescore(b, f, q, k, rescore)
     codes = np.stack([orc.bq_encode(r) for r in rows])
-    ham = orc.bq_dist_all(orc.bq_encode(q), codes)
-    cand, _ = orc.lex_topk(ham, np.arange(n, dtype=np.uint64), rescore)
+    # the reference flow: Hamming heap, pop order, exact distances into a k-heap in that order
+    cand, _ = orc.bq_heap_pops(codes, orc.bq_encode(q), rescore)
     exact = orc.dist_all(ORC[metric], q, rows[cand.astype(np.int64)])
-    li, ld = orc.lex_topk(exact, cand, k)
+    li, ld = orc.heap_topk(exact, cand, k)
     assert counts[0] == k
     assert np.array_equal(ids[0], li) and np.array_equal(bits(dists[0]), bits(ld))
     probe = np.array([0, 5, 63, 64, 3999, 4000], np.uint64)

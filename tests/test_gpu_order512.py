@@ -91,9 +91,9 @@ def test_bq_rescore_and_host_rescore_512_order(ctx512, orc):
     b.upsert(np.arange(n, dtype=np.uint64), rows)
     ids, dists, counts = search_bq_rescore(b, f, q, k, R)
     codes = np.stack([orc.bq_encode(r) for r in rows])
-    cand, _ = orc.lex_topk(orc.bq_dist_all(orc.bq_encode(q), codes), np.arange(n, dtype=np.uint64), R)
+    cand, _ = orc.bq_heap_pops(codes, orc.bq_encode(q), R)  # the reference heap's pop order
     exact = orc.dist_all_512(1, q, rows[cand.astype(np.int64)])
-    li, ld = orc.lex_topk(exact, cand, k)
+    li, ld = orc.heap_topk(exact, cand, k)
     assert counts[0] == k and np.array_equal(ids[0], li) and np.array_equal(bits(dists[0]), bits(ld))
     # wvg_rescore (candidate rows from the host)
     lib = _lib.load()
@@ -104,7 +104,7 @@ def test_bq_rescore_and_host_rescore_512_order(ctx512, orc):
     _lib.check(lib.wvg_rescore(ctx512.handle, METRIC_DOT, _lib.fptr(q), _lib.fptr(sub),
                                _lib.u64ptr(np.arange(300, dtype=np.uint64)), 300, d, k, _lib.u64ptr(oi),
                                _lib.fptr(od), ctypes.byref(cnt)))
-    wi, wd = orc.lex_topk(orc.dist_all_512(1, q, sub), np.arange(300, dtype=np.uint64), k)
+    wi, wd = orc.heap_topk(orc.dist_all_512(1, q, sub), np.arange(300, dtype=np.uint64), k)
     assert np.array_equal(oi, wi) and np.array_equal(bits(od), bits(wd))
     f.destroy()
     b.destroy()

@@ -133,10 +133,10 @@ def test_rescore_host_rows_large_k(ctx, orc):
         _lib.check(lib.wvg_rescore(ctx.handle, METRIC_L2, _lib.fptr(q), _lib.fptr(rows), _lib.u64ptr(ids), n, d, k,
                                    _lib.u64ptr(oi), _lib.fptr(od), ctypes.byref(cnt)))
         all_d = orc.dist_all(0, q, rows)
-        li, ld = orc.lex_topk(all_d, np.arange(n, dtype=np.uint64), k)
+        hi, hd = orc.heap_topk(all_d, ids, k)  # the rescore loop's heap of k, input order
         assert cnt.value == min(k, n)
-        assert np.array_equal(oi[:cnt.value], ids[li.astype(np.int64)])
-        assert np.array_equal(bits(od[:cnt.value]), bits(ld))
+        assert np.array_equal(oi[:cnt.value], hi)
+        assert np.array_equal(bits(od[:cnt.value]), bits(hd))
         assert np.all(oi[cnt.value:] == np.uint64(2**64 - 1)) and np.all(np.isinf(od[cnt.value:]))
 
 

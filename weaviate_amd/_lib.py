@@ -26,7 +26,7 @@ WVG_ERR_CAPACITY = -7
 KIND_F32, KIND_BQ, KIND_PQ = 0, 1, 2
 METRIC_L2, METRIC_DOT, METRIC_COSINE, METRIC_MANHATTAN, METRIC_HAMMING = 0, 1, 2, 3, 4
 ORDER_AVX256, ORDER_AVX512 = 0, 1  # reference SIMD kernel whose reduction order distances follow
-ABI_VERSION = 2  # WVG_ABI_VERSION of include/wvgpu.h this binding follows
+ABI_VERSION = 3  # WVG_ABI_VERSION of include/wvgpu.h this binding follows
 METRIC_BY_NAME = {"l2-squared": METRIC_L2, "dot": METRIC_DOT, "cosine": METRIC_COSINE,
                   "cosine-dot": METRIC_COSINE, "manhattan": METRIC_MANHATTAN, "hamming": METRIC_HAMMING}
 
@@ -35,7 +35,8 @@ METRIC_BY_NAME = {"l2-squared": METRIC_L2, "dot": METRIC_DOT, "cosine": METRIC_C
 class Options(ctypes.Structure):
     """struct wvg_options (include/wvgpu.h): context options fixed at wvg_open_ex."""
     _fields_ = [("size", c_uint32), ("mfma_min_queries", c_uint32), ("cache_reuse", ctypes.c_int32),
-                ("merge_wait_us", c_uint32), ("batch_screen", ctypes.c_int32), ("coalesce", ctypes.c_int32)]
+                ("merge_wait_us", c_uint32), ("batch_screen", ctypes.c_int32), ("coalesce", ctypes.c_int32),
+                ("heap_replay", ctypes.c_int32)]
 
 
 # name -> (restype, argtypes); every symbol declared in include/wvgpu.h.
@@ -78,6 +79,8 @@ SIGNATURES = {
                            _P(c_uint64), _P(c_float), _P(c_uint32)]),
     "wvg_search_bq_rescore": (c_int, [c_void_p, c_void_p, _P(c_float), c_uint32, c_uint32, c_uint32,
                                       _P(c_uint64), c_uint64, _P(c_uint64), _P(c_float), _P(c_uint32)]),
+    "wvg_search_bq_candidates": (c_int, [c_void_p, _P(c_float), c_uint32, c_uint32, _P(c_uint64), c_uint64,
+                                         _P(c_uint64), _P(c_float), _P(c_uint32)]),
     "wvg_search_by_distance": (c_int, [c_void_p, _P(c_float), c_float, ctypes.c_int64, _P(c_uint64), c_uint64,
                                        _P(c_uint64), _P(c_float), c_uint64, _P(c_uint64)]),
     "wvg_search_by_distance_window": (c_int, [c_void_p, _P(c_float), c_float, c_uint32, _P(c_uint64), c_uint64,

@@ -14,7 +14,7 @@
 
 namespace wvg {
 
-constexpr int BQ_WAVES = 4;
+constexpr int BQ_WAVES = BQ_SCAN_WAVES;
 
 __device__ __forceinline__ uint64_t bq_tile_mask(const ScanArgs &a, uint64_t t)
 {
@@ -37,7 +37,9 @@ __device__ __forceinline__ u64x2 ld_codes(const u64x2 *p) { return __builtin_non
 // COS (a batch, ScanArgs::cosched): the 1D grid's consecutive ids on one XCD
 // are the nq queries of one row range, which read the same codes side by side
 // from that XCD's L2 (default-policy loads; K8e COS in wvg_pq.hip).
-template <int E, int NCH, bool COS = false>
+// EMIT (the heap replay, wvg_replay.hip): each wave also writes the keys of the
+// rows the reference's heap could insert (WaveTopK::offer_dist_emit).
+template <int E, int NCH, bool COS = false, bool EMIT = false>
 __global__ __launch_bounds__(BQ_WAVES * 64) void scan_bq_kernel(ScanArgs a, uint64_t *partials)
 {
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -64,6 +66,13 @@ __global__ __launch_bounds__(BQ_WAVES * 64) void scan_bq_kernel(ScanArgs a, uint
     WaveTopK<E> tk;
     tk.init((int)a.k);
     tk.init_fast();
+    uint64_t *ebuf = nullptr;
+    uint32_t ecnt = 0;
+    float eseed = __builtin_inff();
+    if constexpr (EMIT) {
+        ebuf = a.emit + ((size_t)qi * total + gw) * a.emit_cap;
+        if (a.emit_seed) eseed = a.emit_seed[(size_t)qi * G + rng];
+    }
     if constexpr (NCH > 0) {
         // next live tile at or after t (wave-uniform), its mask in m
         auto next_live = [&](uint64_t t, uint64_t &m) {
@@ -94,7 +103,10 @@ __global__ __launch_bounds__(BQ_WAVES * 64) void scan_bq_kernel(ScanArgs a, uint
                 tot += (uint32_t)__popcll(cur[c].x ^ q[2 * c]) + (uint32_t)__popcll(cur[c].y ^ q[2 * c + 1]);
             const float dist = (float)tot;  // exact: sum of float32(popcount) is an integer < 2^24
             // rejection on the float distance first: the key is built only when some lane passes
-            tk.offer_dist_fast(dist, (uint32_t)(t * 64 + lane), m_cur);
+            if constexpr (EMIT)
+                tk.offer_dist_emit(dist, (uint32_t)(t * 64 + lane), m_cur, eseed, ebuf, ecnt, a.emit_cap);
+            else
+                tk.offer_dist_fast(dist, (uint32_t)(t * 64 + lane), m_cur);
 #pragma unroll
             for (int c = 0; c < NCH; c++) cur[c] = nxt[c];
             t = tn;
@@ -111,37 +123,55 @@ __global__ __launch_bounds__(BQ_WAVES * 64) void scan_bq_kernel(ScanArgs a, uint
                 tot += (uint32_t)__popcll(x.x ^ q[2 * c]) + (uint32_t)__popcll(x.y ^ q[2 * c + 1]);
             }
             const float dist = (float)tot;
-            tk.offer_dist_fast(dist, (uint32_t)(t * 64 + lane), m);
+            if constexpr (EMIT)
+                tk.offer_dist_emit(dist, (uint32_t)(t * 64 + lane), m, eseed, ebuf, ecnt, a.emit_cap);
+            else
+                tk.offer_dist_fast(dist, (uint32_t)(t * 64 + lane), m);
         }
+    }
+    if constexpr (EMIT) {
+        if (lane == 0) a.emit_cnt[(size_t)qi * total + gw] = ecnt;
     }
     group_combine_store<E, BQ_WAVES>(tk, partials + ((size_t)qi * G + rng) * a.k);
 }
 
-template <int E, bool COS>
+template <int E, bool COS, bool EMIT>
 static hipError_t launch_bq_ec(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
 {
     const dim3 grid = COS ? dim3((unsigned)groups * a.nq) : dim3(groups, a.nq), block(BQ_WAVES * 64);
     switch (a.nchunks) {
-    case 1: launch_timed((scan_bq_kernel<E, 1, COS>), grid, block, 0, s, a, partials); break;   // d <= 128
-    case 6: launch_timed((scan_bq_kernel<E, 6, COS>), grid, block, 0, s, a, partials); break;   // d = 768
-    case 12: launch_timed((scan_bq_kernel<E, 12, COS>), grid, block, 0, s, a, partials); break; // d = 1536
-    default: launch_timed((scan_bq_kernel<E, 0, COS>), grid, block, 0, s, a, partials); break;
+    case 1: launch_timed((scan_bq_kernel<E, 1, COS, EMIT>), grid, block, 0, s, a, partials); break;   // d <= 128
+    case 6: launch_timed((scan_bq_kernel<E, 6, COS, EMIT>), grid, block, 0, s, a, partials); break;   // d = 768
+    case 12: launch_timed((scan_bq_kernel<E, 12, COS, EMIT>), grid, block, 0, s, a, partials); break; // d = 1536
+    default: launch_timed((scan_bq_kernel<E, 0, COS, EMIT>), grid, block, 0, s, a, partials); break;
     }
     return hipGetLastError();
 }
 
-template <int E>
+template <int E, bool EMIT>
 static hipError_t launch_bq_e(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
 {
-    if (a.cosched && a.nq > 1 && groups % 8 == 0) return launch_bq_ec<E, true>(a, partials, groups, s);
-    return launch_bq_ec<E, false>(a, partials, groups, s);
+    if (a.cosched && a.nq > 1 && groups % 8 == 0) return launch_bq_ec<E, true, EMIT>(a, partials, groups, s);
+    return launch_bq_ec<E, false, EMIT>(a, partials, groups, s);
+}
+
+template <bool EMIT>
+static hipError_t launch_bq_k(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
+{
+    if (a.k <= 64) return launch_bq_e<1, EMIT>(a, partials, groups, s);
+    if (a.k <= 128) return launch_bq_e<2, EMIT>(a, partials, groups, s);
+    return launch_bq_e<4, EMIT>(a, partials, groups, s);
 }
 
 hipError_t launch_scan_bq(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
 {
-    if (a.k <= 64) return launch_bq_e<1>(a, partials, groups, s);
-    if (a.k <= 128) return launch_bq_e<2>(a, partials, groups, s);
-    return launch_bq_e<4>(a, partials, groups, s);
+    return launch_bq_k<false>(a, partials, groups, s);
+}
+
+hipError_t launch_scan_bq_emit(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
+{
+    if (!a.emit || !a.emit_cnt || a.k == 0 || a.k > 256) return hipErrorInvalidValue;
+    return launch_bq_k<true>(a, partials, groups, s);
 }
 
 // Encode row-major float rows; `normalize` is applied per row first (cosine).

@@ -38,7 +38,7 @@ int wvg_rescore(wvg_ctx *ctx, int metric, const float *q, const float *rows, con
     const size_t o_x = cv.take(n * dim * 4), o_t = cv.take(tiles_of(n) * 64 * (size_t)nch * 16),
                  o_q = cv.take((size_t)nch * 16), o_k = cv.take(n * 8), o_i = cv.take((size_t)k * 8),
                  o_d = cv.take((size_t)k * 4), o_c = cv.take(4);
-    const bool large = k > MAX_K;  // beyond the fused top-k: sort the n keys
+    const bool large = !ctx->opt.heap_replay && k > MAX_K;  // beyond the fused top-k: sort the n keys
     const size_t temp_bytes = large ? sort_temp_bytes(n) : 0;
     const size_t o_s = cv.take(large ? n * 8 : 0), o_tmp = cv.take(temp_bytes);
     Bulk bk(ctx);
@@ -59,6 +59,24 @@ int wvg_rescore(wvg_ctx *ctx, int metric, const float *q, const float *rows, con
     WVG_HIP(launch_f32_store((const float *)(bk.b + o_x), nullptr, n, dim, nch, 0, (float *)(bk.b + o_t), bk.s()));
     WVG_HIP(launch_dist_keys(metric, (const float *)(bk.b + o_q), (const float *)(bk.b + o_t), n, dim,
                              (uint64_t *)(bk.b + o_k), bk.s(), ctx->order512));
+    if (ctx->opt.heap_replay) {
+        // the rescore loop's own heap (V/flat/index.go:375-387): every distance back,
+        // inserted in input order into a heap of k on the host, then extracted
+        std::vector<uint64_t> keys(n);
+        WVG_HIP(hipMemcpyAsync(keys.data(), bk.b + o_k, n * 8, hipMemcpyDeviceToHost, bk.s()));
+        WVG_HIP(hipStreamSynchronize(bk.s()));
+        GoMaxHeap h(std::min<uint64_t>(k, n));
+        for (uint64_t i = 0; i < n; i++) insert_to_heap(h, k, ids[i], wvg_unord_f32((uint32_t)(keys[i] >> 32)));
+        std::vector<uint64_t> oi(h.len());
+        std::vector<float> od(h.len());
+        const size_t cnt = extract_heap(h, oi.data(), od.data());
+        for (uint32_t i = 0; i < k; i++) {
+            if (out_ids) out_ids[i] = i < cnt ? oi[i] : WVG_KEY_NONE;
+            if (out_dists) out_dists[i] = i < cnt ? od[i] : INFINITY;
+        }
+        if (out_count) *out_count = (uint32_t)cnt;
+        return WVG_OK;
+    }
     if (large) {
         const uint32_t kk = (uint32_t)std::min<uint64_t>(k, n);
         WVG_HIP(sort_keys64(bk.b + o_tmp, temp_bytes, (const uint64_t *)(bk.b + o_k), (uint64_t *)(bk.b + o_s), n,

@@ -157,6 +157,7 @@ void wvg_options_default(wvg_options *o)
     o->merge_wait_us = 0;
     o->batch_screen = 1;
     o->coalesce = 1;
+    o->heap_replay = 1;
 }
 
 int wvg_open(int device, wvg_ctx **out) { return wvg_open_ex(device, nullptr, out); }

@@ -12,6 +12,7 @@
 #include <string>
 #include <vector>
 
+#include "wvg_heap.hpp"
 #include "wvg_internal.hpp"
 
 namespace wvg {
@@ -218,6 +219,19 @@ size_t query_bytes(const wvg_corpus *c, uint32_t nq);
 size_t staged_query_bytes(const wvg_corpus *c, uint32_t nq);
 ScanArgs scan_args_for(const wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t nq, uint32_t k,
                        const uint64_t *d_allow, uint64_t tb, uint64_t te);
+
+// ---- the reference heap's exact result (wvg_replay.hip) -------------------------
+// Device workspace of bq_heap_candidates (per-wave emission buffers, the kept rows).
+size_t replay_workspace_bytes(uint32_t nq, uint32_t R, const SearchPlan &p);
+// findTopVectorsCached into a heap of R + the pop loop (V/flat/index.go:355-374)
+// for nq prepared BQ queries: pops[q] = (slot, Hamming distance) in pop order.
+int bq_heap_candidates(wvg_corpus *bq, StreamSlot *sl, const void *d_qb, uint32_t qpb, uint32_t nq, uint32_t R,
+                       const uint64_t *d_allow, const SearchPlan &p, char *ws, std::vector<std::vector<GoItem>> &pops);
+// searchByVectorBQ exactly (R <= MAX_K): the candidates above, their exact
+// distances on the device, the k-heap in pop order on the host.  f32 null:
+// outputs are the candidates themselves ([nq][R], pop order).
+int bq_rescore_replay(wvg_corpus *bq, wvg_corpus *f32, const float *queries, uint32_t nq, uint32_t k, uint32_t R,
+                      const SearchPlan &p, uint64_t *out_ids, float *out_dists, uint32_t *out_counts);
 
 // ---- unbounded selections (wvg_range.hip) ---------------------------------------
 int search_large_k(wvg_corpus *c, const float *queries, uint32_t nq, uint32_t k, const uint64_t *allow_bits,

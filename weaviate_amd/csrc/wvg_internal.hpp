@@ -262,6 +262,15 @@ struct ScanArgs {
     uint32_t cache_tail256;    // K1 (A/B): if > 0, each wave reads the last cache_tail256/256 of its pass
                                // with the default policy and the rest non-temporal -- the serpentine's
                                // next pass starts on exactly those rows
+    // Reference-heap replay (K5 EMIT, wvg_replay.hip): every wave also writes the
+    // keys of the rows the reference's sequential heap could insert -- those
+    // strictly below min(the wave's own running k-th distance, its range's
+    // prefix seed) -- in docID order, [nq][groups * 4][emit_cap]; emit_cnt
+    // [nq][groups * 4] holds each wave's full count (> emit_cap: overflowed).
+    uint64_t *emit;
+    uint32_t *emit_cnt;
+    uint32_t emit_cap;
+    const float *emit_seed;    // [nq][groups] thresholds (a rerun seeded from the first pass), or null
 };
 // Phase 1 writes dense partials [nq][groups][K] (keys, KEY_NONE = empty).
 int scan_groups_for(const ScanArgs &a, int num_cus);
@@ -316,6 +325,22 @@ hipError_t launch_scan_f32_stream(const ScanArgs &a, const StreamJob &j, hipStre
 // ids KEY_NONE, dists +inf, counts 0 for nq queries (empty corpus / slab).
 hipError_t launch_fill_empty(uint64_t *ids, float *dists, uint32_t *counts, uint32_t nq, uint32_t k, hipStream_t s);
 hipError_t launch_scan_bq(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s);
+// K5 with the heap-replay emission (a.emit set; groups * BQ_SCAN_WAVES waves per query).
+constexpr int BQ_SCAN_WAVES = 4;
+hipError_t launch_scan_bq_emit(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s);
+// Heap replay (wvg_replay.hip).  prefix: per query, thr[q][g] = the k-th smallest
+// distance of ranges 0..g-1's lists (partials [nq][groups][k], ascending; +inf
+// while fewer than k rows precede range g).  filter: each wave's emitted keys
+// with distance < its range's thr, compacted in place (fcnt [nq][waves]; a wave
+// whose count exceeded emit_cap sets oflow[q]).  gather: per query the kept keys
+// of all waves in wave (= docID) order into out [nq][out_cap], totals [nq].
+hipError_t launch_emit_prefix(const uint64_t *partials, uint32_t nq, uint32_t groups, uint32_t k, float *thr,
+                              hipStream_t s);
+hipError_t launch_emit_filter(uint64_t *emit, const uint32_t *emit_cnt, uint32_t emit_cap, const float *thr,
+                              uint32_t nq, uint32_t groups, uint32_t waves_per_group, uint32_t *fcnt, uint32_t *oflow,
+                              hipStream_t s);
+hipError_t launch_emit_gather(const uint64_t *emit, const uint32_t *fcnt, uint32_t emit_cap, uint32_t nq,
+                              uint32_t waves, uint64_t *out, uint32_t out_cap, uint32_t *totals, hipStream_t s);
 hipError_t launch_scan_pq(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s);
 // The exact K1 rescan of a device-resident query list (qlist[0 .. *nlist)),
 // `slots` queries in flight: partials [f][groups][k]; and its merge.

@@ -1064,6 +1064,8 @@ int wvg_search_bq_rescore(wvg_corpus *bq, wvg_corpus *f32, const float *queries,
     if (R > MAX_K)
         return bq_rescore_large(bq, f32, queries, nq, k, R, allow_bits, allow_words, p, out_ids, out_dists,
                                 out_counts);
+    if (bq->ctx->opt.heap_replay)  // the reference heaps' exact result (wvg_replay.hip)
+        return bq_rescore_replay(bq, f32, queries, nq, k, R, p, out_ids, out_dists, out_counts);
     SlotGuard g(bq->ctx);
     rc = bq->ctx->acquire(&g.slot);
     if (rc) return rc;
@@ -1128,6 +1130,35 @@ int wvg_search_bq_rescore(wvg_corpus *bq, wvg_corpus *f32, const float *queries,
     if (out_counts) WVG_HIP(hipMemcpyAsync(out_counts, b + o_cnt, (size_t)nq * 4, hipMemcpyDeviceToHost, s));
     WVG_HIP(hipStreamSynchronize(s));
     return WVG_OK;
+}
+
+int wvg_search_bq_candidates(wvg_corpus *bq, const float *queries, uint32_t nq, uint32_t rescore_limit,
+                             const uint64_t *allow_bits, uint64_t allow_words, uint64_t *out_ids, float *out_dists,
+                             uint32_t *out_counts)
+{
+    int rc = check_corpus(bq);
+    if (rc) return rc;
+    if (bq->kind != WVG_KIND_BQ) return fail(WVG_ERR_INVALID, "need a BQ corpus");
+    if (nq > 0 && !queries) return fail(WVG_ERR_INVALID, "null queries");
+    const uint32_t R = rescore_limit;
+    if (R > MAX_K) return fail(WVG_ERR_UNSUPPORTED, "rescore_limit above 256");
+    if (!bq->ctx->opt.heap_replay) {  // the lexicographic top-R, in pop (descending) order
+        rc = wvg_search(bq, queries, nq, R, allow_bits, allow_words, out_ids, out_dists, out_counts);
+        if (rc) return rc;
+        for (uint32_t q = 0; q < nq; q++) {
+            const uint32_t c = out_counts ? out_counts[q] : R;
+            if (out_ids) std::reverse(out_ids + (size_t)q * R, out_ids + (size_t)q * R + c);
+            if (out_dists) std::reverse(out_dists + (size_t)q * R, out_dists + (size_t)q * R + c);
+        }
+        return WVG_OK;
+    }
+    std::shared_lock<std::shared_mutex> lk(bq->rw);
+    SearchPlan p = plan_search(bq, nq, R, allow_bits, allow_words);
+    if (p.empty) {
+        write_empty(nq, R, out_ids, out_dists, out_counts);
+        return WVG_OK;
+    }
+    return bq_rescore_replay(bq, nullptr, queries, nq, R, R, p, out_ids, out_dists, out_counts);
 }
 
 // Device-search workspaces start with a 256-byte status block (the sticky

@@ -237,6 +237,37 @@ struct WaveTopK {
         tau_open = tau == WVG_KEY_NONE || tau_f != tau_f;
     }
 
+    // offer_dist_fast that also records the rows the reference's sequential
+    // heap could insert (the heap replay, wvg_replay.hip).  The reference
+    // (V/flat/index.go:497-506) inserts row i iff fewer than k rows precede it
+    // or d_i < Top().Dist, the k-th smallest distance of ALL rows before i;
+    // this wave's k-th smallest over its own rows before this batch of 64 is
+    // never below that, nor is `seed` (the k-th smallest before the wave's
+    // range), so d_i < min(both) keeps a superset of the inserted rows: the
+    // rows it drops are no-ops of insertToHeap.  Distances must not be NaN
+    // (Hamming).  Kept keys go to buf[cnt ...] in lane (= docID) order; cnt
+    // counts past cap so the host can tell an overflow.
+    __device__ __forceinline__ void offer_dist_emit(float dist, uint32_t slot, uint64_t live, float seed, uint64_t *buf,
+                                                    uint32_t &cnt, uint32_t cap)
+    {
+        const uint64_t cand = tau_open ? live : (__ballot(dist <= tau_f) & live);
+        if (cand == 0ull) return;
+        const int lane = threadIdx.x & 63;
+        const float et = fminf(tau_open ? __builtin_inff() : tau_f, seed);
+        const uint64_t em = __ballot(dist < et) & live;
+        const uint64_t key = ((live >> lane) & 1ull) ? wvg_make_key(dist, slot) : WVG_KEY_NONE;
+        if (em) {
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0u));
+            const uint32_t pos = cnt + below;
+            if (((em >> lane) & 1ull) && pos < cap) buf[pos] = key;
+            cnt += (uint32_t)__popcll(em);
+        }
+        offer(key);
+        tau_f = wvg_unord_f32((uint32_t)(tau >> 32));
+        tau_open = tau == WVG_KEY_NONE || tau_f != tau_f;
+    }
+
     // Offer one key per lane (KEY_NONE for an empty lane).
     __device__ __forceinline__ void offer(uint64_t key)
     {

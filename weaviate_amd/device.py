@@ -252,6 +252,22 @@ class Corpus:
         return ids[:cnt.value], dists[:cnt.value]
 
 
+def search_bq_candidates(bq: Corpus, queries, rescore_limit: int, allow=None):
+    """wvg_search_bq_candidates: findTopVectorsCached's heap of rescore_limit and
+    its pop order (V/flat/index.go:355-374): (ids [nq][R], dists [nq][R], counts)."""
+    q = np.ascontiguousarray(queries, dtype=np.float32)
+    if q.ndim == 1:
+        q = q[None, :]
+    nq, R = q.shape[0], rescore_limit
+    ids = np.empty((nq, R), dtype=np.uint64)
+    dists = np.empty((nq, R), dtype=np.float32)
+    counts = np.empty(nq, dtype=np.uint32)
+    aw, an = (None, 0) if allow is None else (np.ascontiguousarray(allow, dtype=np.uint64), len(allow))
+    check(bq.lib.wvg_search_bq_candidates(bq.handle, fptr(q), nq, R, u64ptr(aw) if aw is not None else None, an,
+                                          u64ptr(ids), fptr(dists), u32ptr(counts)))
+    return ids, dists, counts
+
+
 def search_bq_rescore(bq: Corpus, f32: Corpus, queries, k: int, rescore_limit: int, allow=None):
     q = np.ascontiguousarray(queries, dtype=np.float32)
     if q.ndim == 1:
