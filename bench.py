@@ -357,12 +357,15 @@ def config_batched(ctx, orc, metric_name, metric, reps=3):
 
 def config_bq(ctx, orc, nq=8):
     """configs[2]: 100M x 1536 BQ (cosine) Hamming top-200 + exact fp32 rescore
-    to 10 (flat.searchByVectorBQ, V/flat/index.go:347-389).  The 614 GB of
-    float rows do not fit one GPU: the R rows are regenerated by id into the
+    to 10 (flat.searchByVectorBQ, V/flat/index.go:347-389), exactly as
+    Weaviate's heaps pick and order the candidates (wvg_search_bq_candidates:
+    the K5 scan records the rows the heap could insert, the host replays the
+    heap; wvg_rescore replays the k-heap in pop order).  The 614 GB of float
+    rows do not fit one GPU: the R rows are regenerated by id into the
     caller's pinned gather buffer (stand-in for the LSM gets, timed apart) and
     rescored through wvg_rescore.  frac: 19.2 GB of codes per scan."""
     from weaviate_amd._lib import KIND_BQ, METRIC_COSINE, check, fptr, u32ptr, u64ptr
-    from weaviate_amd.device import Corpus
+    from weaviate_amd.device import Corpus, search_bq_candidates
 
     n, d, k, R = 100_000_000, 1536, 10, 200
     w = (d + 63) // 64
@@ -370,13 +373,13 @@ def config_bq(ctx, orc, nq=8):
     c = Corpus(ctx, KIND_BQ, METRIC_COSINE, d, n)
     c.fill_synthetic(42, n, 0)
     qs = orc.synth_rows(43, 0, nq, d, 0)
-    c.search(qs[0], R)
+    search_bq_candidates(c, qs[0], R)
     rows = ctx.host_array((R, d), np.float32)
     res, t_fetch = [], 0.0
     lib.wvg_profile_start(ctx.handle)
     t0 = time.perf_counter()
     for i in range(nq):
-        ids, hd, cnt = c.search(qs[i], R)
+        ids, hd, cnt = search_bq_candidates(c, qs[i], R)  # pop order (descending Hamming, heap ties)
         t1 = time.perf_counter()
         cand = np.ascontiguousarray(ids[0, :cnt[0]])
         check(lib.wvg_synthetic_rows(ctx.handle, 42, u64ptr(cand), len(cand), d, 0, 1, fptr(rows)))
@@ -390,43 +393,88 @@ def config_bq(ctx, orc, nq=8):
     wall = (time.perf_counter() - t0) / nq
     scan_s, nl = _prof(lib, ctx)
     scan_s /= max(1, nl)
+    # the cost of the exact heap: candidates call vs the plain lexicographic Hamming top-R
+    # (the same K5 scan without the recording, one device merge)
+    reps = 4
+    t0 = time.perf_counter()
+    for i in range(reps):
+        search_bq_candidates(c, qs[i % nq], R)
+    t_exact = (time.perf_counter() - t0) / reps
+    c.search(qs[0], R)
+    lib.wvg_profile_start(ctx.handle)
+    t0 = time.perf_counter()
+    for i in range(reps):
+        c.search(qs[i % nq], R)
+    t_lex = (time.perf_counter() - t0) / reps
+    scan_lex_s, nl2 = _prof(lib, ctx)
+    scan_lex_s /= max(1, nl2)
     # batch mode: nq queries per call (co-scheduled K5), Hamming top-R only
     c.search(qs, R)
     t0 = time.perf_counter()
     for _ in range(3):
         c.search(qs, R)
     wall_b = (time.perf_counter() - t0) / (3 * nq)
-    # spot check: sampled codes vs the oracle's encoder, Hamming results and the rescore
+    search_bq_candidates(c, qs, R)
+    t0 = time.perf_counter()
+    for _ in range(2):
+        search_bq_candidates(c, qs, R)
+    wall_bx = (time.perf_counter() - t0) / (2 * nq)
+    # check: sampled codes vs the oracle's encoder; query 0 EXACTLY against the
+    # reference flow restated -- its Hamming heap over all 100M stored codes
+    # (read back from the device), the pop order, the k-heap of the exact
+    # distances; the last query: distances bit-exact, rescore = the k-heap
     starts = [0, n // 2 - 13, n - 10_000]
     sample_ids = np.concatenate([np.arange(s, s + 10_000, dtype=np.int64) for s in starts])
     scodes = np.concatenate([orc.bq_encode_rows(orc.normalize_rows(orc.synth_rows(42, s, 10_000, d, 0)))
                              for s in starts])
     got, okb = c.get_batch(sample_ids[::499].astype(np.uint64))
     ok = bool(okb.all() and np.array_equal(got, scodes[::499]))
+    t_chk = time.perf_counter()
     for qi in (0, nq - 1):
         hid, hdist, cand, oi, od = res[qi]
         qc = orc.bq_encode(orc.normalize(qs[qi]))
         codes, okc = c.get_batch(hid.astype(np.uint64))
         ok &= bool(okc.all() and np.array_equal(_bits(orc.bq_dist_all(qc, codes.reshape(R, w))), _bits(hdist)))
-        ok &= bool(np.all(np.diff(hdist) >= 0)) and _outside_ok(orc, sample_ids, orc.bq_dist_all(qc, scodes), hid, hdist)
+        if qi == 0:
+            alld = np.empty(n, np.float32)
+            for r0 in range(0, n, 4_000_000):
+                cc, okr = c.get_batch(np.arange(r0, min(n, r0 + 4_000_000), dtype=np.uint64))
+                ok &= bool(okr.all())
+                alld[r0:r0 + len(cc)] = orc.bq_dist_all(qc, cc)
+                del cc
+            pi, pd = orc.heap_pops(alld, R)
+            del alld
+            ok &= bool(np.array_equal(hid, pi) and np.array_equal(_bits(hdist), _bits(pd)))
         frows = orc.normalize_rows(np.stack([orc.synth_rows(42, int(i), 1, d, 0)[0] for i in cand]))
         ed = orc.dist_all(2, orc.normalize(qs[qi]), frows)
-        wi, wd = orc.lex_topk(ed, cand.astype(np.uint64), k)
+        wi, wd = orc.heap_topk(ed, cand.astype(np.uint64), k)
         ok &= bool(np.array_equal(oi, wi) and np.array_equal(_bits(od), _bits(wd)))
+    t_chk = time.perf_counter() - t_chk
     ctx.free_host_array(rows)
     c.destroy()
     by = n * w * 8
     gbps = by / scan_s / 1e9
-    return {"workload": f"{n:,} x {d} BQ (cosine, {w} words/row), Hamming top-{R} + exact fp32 rescore to {k}",
+    gbps_lex = by / scan_lex_s / 1e9
+    return {"workload": f"{n:,} x {d} BQ (cosine, {w} words/row), Hamming top-{R} + exact fp32 rescore to {k}, "
+                        f"Weaviate's heap order (heap_replay)",
             "qps": round(1 / wall, 2), "qps_without_row_fetch": round(1 / (wall - t_fetch / nq), 2),
             "row_fetch_stand_in_ms": round(t_fetch / nq * 1e3, 3), "scan_ms": round(scan_s * 1e3, 3),
+            "heap_replay": {"candidates_call_ms": round(t_exact * 1e3, 3),
+                            "lexicographic_top_r_call_ms": round(t_lex * 1e3, 3),
+                            "cost_ms": round((t_exact - t_lex) * 1e3, 3),
+                            "scan_ms_recording": round(scan_s * 1e3, 3),
+                            "scan_ms_plain": round(scan_lex_s * 1e3, 3),
+                            "batch_candidates_qps": round(1 / wall_bx, 2)},
             "batch_call_qps": round(1 / wall_b, 2), "batch_call_queries": nq,
-            "kernel": "K5 scan_bq_kernel (XOR + popcount, fused top-200)",
+            "kernel": "K5 scan_bq_kernel<..., EMIT> (XOR + popcount, fused top-200, heap-candidate recording)",
             "roofline": {"bound": "hbm", "achieved": round(gbps, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(gbps / HBM_PEAK_GBS, 4), "bytes_per_scan": by},
-            "check": {"ok": ok, "how": "sampled codes = oracle BQ encode; queries 0 and last: Hamming distances "
-                                       "bit-exact on the returned codes, sorted, no sampled code (30k) ahead of the "
-                                       "R-th; rescore = oracle lexicographic top-10 of the 200 candidates, bit-exact"}}
+                         "frac": round(gbps / HBM_PEAK_GBS, 4), "bytes_per_scan": by,
+                         "frac_plain_scan": round(gbps_lex / HBM_PEAK_GBS, 4)},
+            "check": {"ok": ok, "seconds": round(t_chk, 1),
+                      "how": "sampled codes = oracle BQ encode; query 0: candidates (ids in pop order, Hamming "
+                             "bits) = the oracle heap over all 100M stored codes; queries 0 and last: Hamming "
+                             "distances bit-exact on the returned codes, rescore = the oracle k-heap of the exact "
+                             "distances in pop order, ids and bits"}}
 
 
 def config_pq(ctx, orc, nq=16):
@@ -894,30 +942,35 @@ MERGE_CHECK_MAX_ROWS = 8_500_000  # the merged-result check's oracle regenerates
 
 
 def merge_check(ranges, d, k, qs, got_ids, got_d):
-    """Rank 0's check of the multi-GPU merge (Index.objectVectorSearch,
-    adapters/repos/db/index.go:1567-1648) for the queries qs: the merged ids /
+    """Rank 0's check of the (merged) top-k for the queries qs: the ids /
     distances equal the oracle's lexicographic top-k over every rank's or
-    slab's rows, regenerated from the synthetic generator.  ranges: (first
-    docID, rows) of each shard.  Checker only: runs after the timed region."""
+    slab's rows, regenerated from the synthetic generator (at N = 1 the
+    scan's own result; at N > 1 after the all-gather and the device merge,
+    Index.objectVectorSearch, adapters/repos/db/index.go:1567-1648).  ranges:
+    (first docID, rows) of each shard.  Checker only: runs after the timed
+    region."""
     from oracle import wv_oracle as orc
 
     total = sum(r[1] for r in ranges)
     if total > MERGE_CHECK_MAX_ROWS:
         return {"ok": None, "skipped": f"{total:,} rows above the host oracle's {MERGE_CHECK_MAX_ROWS:,}"}
+    best = [(np.empty(0, np.uint64), np.empty(0, np.float32)) for _ in qs]
+    for base, nrows in ranges:
+        for r0 in range(0, nrows, 1_000_000):
+            m = min(1_000_000, nrows - r0)
+            rows = orc.synth_rows(42, base + r0, m, d, 0)  # once per chunk, for every query
+            ids = np.arange(base + r0, base + r0 + m, dtype=np.uint64)
+            for qi in range(len(qs)):
+                ci, cd = orc.lex_topk(orc.dist_all(0, qs[qi], rows), ids, k)
+                bi, bd = best[qi]
+                best[qi] = orc.lex_topk(np.concatenate([bd, cd]), np.concatenate([bi, ci]), k)
     ok = True
     for qi in range(len(qs)):
-        bi, bd = np.empty(0, np.uint64), np.empty(0, np.float32)
-        for base, nrows in ranges:
-            for r0 in range(0, nrows, 1_000_000):
-                m = min(1_000_000, nrows - r0)
-                rows = orc.synth_rows(42, base + r0, m, d, 0)
-                ci, cd = orc.lex_topk(orc.dist_all(0, qs[qi], rows),
-                                      np.arange(base + r0, base + r0 + m, dtype=np.uint64), k)
-                bi, bd = orc.lex_topk(np.concatenate([bd, cd]), np.concatenate([bi, ci]), k)
+        bi, bd = best[qi]
         ok &= bool(np.array_equal(np.asarray(got_ids[qi]).view(np.uint64), bi)
                    and np.array_equal(np.asarray(got_d[qi], np.float32).view(np.uint32), bd.view(np.uint32)))
     return {"ok": ok, "queries": len(qs), "rows": total,
-            "how": "merged ids and distance bits = the oracle's lexicographic top-k over every shard's rows"}
+            "how": "ids and distance bits = the oracle's lexicographic top-k over every shard's rows"}
 
 
 def run_flat1m(args, world, rank, dev, torch, dist):
@@ -982,15 +1035,24 @@ def run_flat1m(args, world, rank, dev, torch, dist):
     scan_ms, launches = ctypes.c_double(), ctypes.c_uint64()
     check(lib.wvg_profile_stop(ctx.handle, ctypes.byref(scan_ms), ctypes.byref(launches)))
     check(lib.wvg_search_device_check(ctx.handle, ws.data_ptr(), stream))  # no merge gave up in the timed run
+    # the last timed step's result against the oracle (untimed): at N = 1 the
+    # query-stream launch's own packed block (every query of the step), at
+    # N > 1 the exchanged + merged lists
+    torch.cuda.synchronize(dev)
+    last = args.warmup + args.steps - 1
+    q0 = (last * B) % P
     mcheck = None
-    if world > 1:  # the last step's exchanged + merged lists against the oracle (untimed)
-        torch.cuda.synchronize(dev)
-        last = args.warmup + args.steps - 1
-        q0 = (last * B) % P
+    if world > 1:
         if rank == 0:
             mcheck = merge_check([(r * cap, n) for r in range(world)], d, k, qs[q0:q0 + 2],
                                  m_ids[last % 2][:2].cpu().numpy(), m_d[last % 2][:2].cpu().numpy())
         dist.barrier()
+    else:
+        blk_h = send[last % 2].cpu().numpy()
+        got_i = blk_h[:B * k * 8].view(np.uint64).reshape(B, k)
+        got_d = blk_h[B * k * 8:B * k * 12].view(np.float32).reshape(B, k)
+        mcheck = merge_check([(0, n)], d, k, qs[q0:q0 + B], got_i, got_d)
+        mcheck["what"] = f"the last timed launch's {B} queries (scan_f32_stream_kernel's packed block)"
 
     total_queries = world * B * args.steps  # 1M-row query scans over all GPUs
     avg_launch_s = scan_ms.value / 1e3 / max(1, launches.value)
@@ -1022,9 +1084,10 @@ def run_flat1m(args, world, rank, dev, torch, dist):
             "workload": "flat exact k-NN, 1M x 128 fp32 L2 per GPU, single-query scans "
                         "(BASELINE configs[0] shape on MI355X)",
             "rows_per_gpu": n, "dim": d, "k": k, "queries_per_step": B,
-            "parallelism": f"shard rows by docID range over {world} GPU(s); one RCCL all-gather of packed "
-                           f"per-GPU top-k blocks per step + device merge, on a second stream overlapping "
-                           f"the next step's scan",
+            "parallelism": (f"shard rows by docID range over {world} GPUs; one RCCL all-gather of packed "
+                            f"per-GPU top-k blocks per step + device merge, on a second stream overlapping "
+                            f"the next step's scan" if world > 1 else
+                            "one GPU: no exchange (the scan's own top-k is the result)"),
         },
         "roofline": {
             "bound": "hbm",

@@ -126,7 +126,8 @@ def test_hot_kernels_use_no_scratch(tmp_path):
     if not os.path.exists(readelf):
         pytest.skip("llvm-readelf not available")
     hot = ("scan_f32_stream_kernel", "scan_f32_kernel", "screen_ar_kernel", "screen_kernel", "scan_pq32_wide_kernel",
-           "scan_pq32_rot_kernel", "scan_bq_kernel", "gemm_rs_kernel", "pq_encode_kernel", "merge_keys_kernel")
+           "scan_pq32_rot_kernel", "scan_bq_kernel", "gemm_rs_kernel", "pq_encode_kernel", "merge_keys_kernel",
+           "scan_f32_mq_kernel", "emit_prefix_kernel", "emit_filter_kernel", "emit_gather_kernel")
     bad, seen = [], 0
     for j, co in enumerate(_gfx950_code_objects(_lib.LIB_PATH)):
         f = tmp_path / f"co{j}.o"

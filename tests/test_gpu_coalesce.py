@@ -93,6 +93,7 @@ def test_concurrent_calls_equal_serial_calls(ctx, orc, kind, metric, d, threads)
     (KIND_F32, METRIC_L2, 20_000),
     (KIND_F32, METRIC_L2, 150),    # fewer live rows than the batch's k: counts = min(live, k)
     (KIND_BQ, METRIC_COSINE, 20_000),
+    (KIND_PQ, METRIC_L2, 20_000),
 ])
 def test_mixed_k_batches_give_each_caller_its_prefix(ctx, orc, kind, metric, n):
     """Round 5: a coalesced batch runs at the largest k of its requests (up to
@@ -240,18 +241,38 @@ def test_filtered_calls_coalesce_equal_serial(ctx, orc, metric, d):
     masked by its own (ScanArgs::allow_qstride).  16 threads with mixed lists
     -- 10 %, 1 %, a narrow id range, a single id, an empty list, none -- and
     mixed k must get exactly what serial calls return."""
+    _filtered_vs_serial(ctx, orc, metric, d)
+
+
+def test_filtered_calls_coalesce_with_mfma_min_queries_1(orc):
+    """with mfma_min_queries = 1 a filtered cosine batch used to be
+    planned onto the MFMA path, which takes no per-query allow windows, and
+    every caller of the batch failed.  Filtered batches never go to MFMA."""
+    with Context(0, mfma_min_queries=1) as c1:
+        _filtered_vs_serial(c1, orc, METRIC_COSINE, 96)
+
+
+def test_filtered_batches_stay_within_the_byte_budget(ctx, orc):
+    """80 concurrent callers with wide allow lists over 1.2M rows: one batch of
+    all of them would hold 80 x 150 KB of allow words, above the 8 MB budget
+    (ADVICE r5), so the coalescer splits them -- every caller still gets its
+    own call's result."""
+    _filtered_vs_serial(ctx, orc, METRIC_L2, 32, n=1_200_000, nq=160, threads=80, wide=True)
+
+
+def _filtered_vs_serial(ctx, orc, metric, d, n=30_000, nq=96, threads=16, wide=False):
     from weaviate_amd.device import allow_bitmap
 
-    n = 30_000
     c = make_corpus(ctx, orc, KIND_F32, metric, n, d)
     lib = _lib.load()
     rng = np.random.default_rng(710)
-    nq = 96
     qs = np.ascontiguousarray(orc.synth_rows(711, 0, nq, d, 0))
     allows = []
     for i in range(nq):
-        kind = i % 6
-        if kind == 0:
+        kind = 0 if wide else i % 6
+        if wide:
+            allows.append(allow_bitmap(np.flatnonzero(rng.random(n) < 0.5), n))
+        elif kind == 0:
             allows.append(allow_bitmap(np.flatnonzero(rng.random(n) < 0.10), n))
         elif kind == 1:
             allows.append(allow_bitmap(np.flatnonzero(rng.random(n) < 0.01), n))
@@ -279,17 +300,17 @@ def test_filtered_calls_coalesce_equal_serial(ctx, orc, metric, d):
     for rep in range(3):
         out = [None] * nq
         errs = []
-        start = threading.Barrier(16)
+        start = threading.Barrier(threads)
 
         def worker(t):
             try:
                 start.wait()
-                for i in range(t, nq, 16):
+                for i in range(t, nq, threads):
                     out[i] = call(i)
             except Exception as e:  # noqa: BLE001
                 errs.append(e)
 
-        th = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(threads)]
         for t in th:
             t.start()
         for t in th:

@@ -51,6 +51,62 @@ def test_full_size_1m_x_128_exact(ctx, orc):
     c.destroy()
 
 
+# The headline's own kernel on the headline's own shape:
+# the query-stream launch (wvg_search_device_pipelined, 16 single-query scans
+# per launch, as bench.py times it) three times in a row over 1M x 128 -- so
+# the scans alternate direction and each starts on the default-policy tail
+# the previous one left in the Infinity Cache -- and lone wvg_search calls
+# (the in-launch merge into host memory), every result the oracle's exact
+# top-10 over all 1M rows.
+def test_full_size_headline_stream_and_lone_queries_exact(ctx, orc):
+    import ctypes
+
+    lib = _lib.load()
+    n, d, k, nq, launches = 1_000_000, 128, 10, 16, 3
+    c = Corpus(ctx, KIND_F32, METRIC_L2, d, n)
+    c.fill_synthetic(42, n, 0)
+    rows = orc.synth_rows(42, 0, n, d, 0)
+    all_ids = np.arange(n, dtype=np.uint64)
+    h = ctx.handle
+
+    def alloc(nbytes, zero=0):
+        p = ctypes.c_void_p()
+        _lib.check(lib.wvg_device_alloc(h, nbytes, zero, ctypes.byref(p)))
+        return p
+
+    s = ctypes.c_void_p()
+    _lib.check(lib.wvg_stream_create(h, ctypes.byref(s)))
+    wsb = lib.wvg_search_workspace_size(c.handle, nq, k)
+    dq, di, dd, dc, ws = alloc(nq * d * 4), alloc(nq * k * 8), alloc(nq * k * 4), alloc(nq * 4), alloc(wsb, 1)
+    try:
+        results = []
+        for L in range(launches):  # back to back on one stream, no host sync between launches
+            qs = np.ascontiguousarray(orc.synth_rows(4300 + L, 0, nq, d, 0))
+            _lib.check(lib.wvg_memcpy_h2d(h, dq, qs.ctypes.data_as(ctypes.c_void_p), qs.nbytes, s))
+            _lib.check(lib.wvg_search_device_pipelined(c.handle, dq, nq, k, di, dd, dc, ws, wsb, s))
+            gi, gd, gc = np.empty((nq, k), np.uint64), np.empty((nq, k), np.float32), np.empty(nq, np.uint32)
+            for host, dev in ((gi, di), (gd, dd), (gc, dc)):
+                _lib.check(lib.wvg_memcpy_d2h(h, host.ctypes.data_as(ctypes.c_void_p), dev, host.nbytes, s))
+            results.append((qs, gi, gd, gc))
+        _lib.check(lib.wvg_search_device_check(h, ws, s))
+        for qs, gi, gd, gc in results:
+            assert np.all(gc == k)
+            for qi in range(nq):
+                wi, wd = orc.lex_topk(orc.dist_all(0, qs[qi], rows), all_ids, k)
+                assert np.array_equal(gi[qi], wi), qi
+                assert np.array_equal(bits(gd[qi]), bits(wd)), qi
+    finally:
+        for p in (dq, di, dd, dc, ws):
+            _lib.check(lib.wvg_device_free(h, p))
+        _lib.check(lib.wvg_stream_destroy(h, s))
+    lone = orc.synth_rows(4400, 0, 4, d, 0)
+    for qi in range(len(lone)):  # one query per call: alternating directions between calls
+        gi, gd, gc = c.search(lone[qi], k)
+        wi, wd = orc.lex_topk(orc.dist_all(0, lone[qi], rows), all_ids, k)
+        assert gc[0] == k and np.array_equal(gi[0], wi) and np.array_equal(bits(gd[0]), bits(wd)), qi
+    c.destroy()
+
+
 # Full size (BASELINE config 4): 100M x 128 L2, PQ m=32 ks=256 -- bulk encode on
 # the device, then ADC top-10 over all 100M codes; checked by properties on
 # sampled rows (the oracle cannot encode and scan 100M rows in seconds).
@@ -114,7 +170,29 @@ def test_full_size_bq_100m_x_1536_properties(ctx, orc):
         outside = ~np.isin(sample_ids, ids[qi].astype(np.int64))
         kd, kid = float(dists[qi][-1]), int(ids[qi][-1])
         assert np.all((sd[outside] > kd) | ((sd[outside] == kd) & (sample_ids[outside] > kid)))
+    # the reference heap's candidates exactly: findTopVectorsCached over all 100M
+    # stored codes (streamed back from the device), its pop order, vs the library's
+    from weaviate_amd.device import search_bq_candidates
+
+    ci, cd, cc = search_bq_candidates(c, qs, R)
+    for qi in range(len(qs)):
+        qc = orc.bq_encode(orc.normalize(qs[qi]))
+        pi, pd = orc.heap_pops(_bq_dists_chunked(orc, c, qc, n), R)
+        assert cc[qi] == R
+        assert np.array_equal(ci[qi], pi), qi
+        assert np.array_equal(bits(cd[qi]), bits(pd)), qi
     c.destroy()
+
+
+def _bq_dists_chunked(orc, c, qc, n, chunk=4_000_000):
+    """Hamming distances of qc to every stored code of BQ corpus c (ids 0..n-1),
+    read back chunk by chunk (wvg_corpus_get_batch)."""
+    out = np.empty(n, np.float32)
+    for r0 in range(0, n, chunk):
+        codes, ok = c.get_batch(np.arange(r0, min(n, r0 + chunk), dtype=np.uint64))
+        assert ok.all()
+        out[r0:r0 + len(codes)] = orc.bq_dist_all(qc, codes)
+    return out
 
 
 # Full size (BASELINE config 2): 10M x 768 fp32 cosine, one 1024-query batch
@@ -225,11 +303,12 @@ def test_full_size_batched_10m_x_768_dot_exact(ctx, orc):
 # Config 3 at the largest size that fits with its float rows resident: 10M x
 # 1536 fp32 (61 GB) + its BQ codes, flat.searchByVectorBQ with the exact
 # rescore on the device (wvg_search_bq_rescore, R = 200, k = 10;
-# V/flat/index.go:347-389).  The result must be the oracle's top-10 of the
-# 200 Hamming candidates, and the candidates the Hamming top-200 (sampled
-# property, as the 100M test).
+# V/flat/index.go:347-389), checked EXACTLY against the reference flow
+# restated: the Hamming heap over all 10M stored codes (streamed back), its
+# pop order, the exact cosine distances of those rows inserted into a heap of
+# k in that order, extracted -- ids in order and distance bits equal.
 def test_full_size_bq_rescore_10m_x_1536_resident(ctx, orc):
-    from weaviate_amd.device import search_bq_rescore
+    from weaviate_amd.device import search_bq_candidates, search_bq_rescore
 
     n, d, R, k = 10_000_000, 1536, 200, 10
     f = Corpus(ctx, KIND_F32, METRIC_COSINE, d, n)
@@ -238,21 +317,14 @@ def test_full_size_bq_rescore_10m_x_1536_resident(ctx, orc):
     bq.fill_synthetic(42, n, 0)
     qs = orc.synth_rows(43, 0, 4, d, 0)
     ids, dists, counts = search_bq_rescore(bq, f, qs, k, R)
-    cand, hd, hc = bq.search(qs, R)  # the Hamming top-R (the same kernel the flow runs)
-    starts = [0, n // 2 - 13, n - 10_000]
-    sample_ids = np.concatenate([np.arange(s, s + 10_000, dtype=np.int64) for s in starts])
-    scodes = orc.bq_encode_rows(orc.normalize_rows(np.concatenate([orc.synth_rows(42, s, 10_000, d, 0)
-                                                                     for s in starts])))
+    ci, cd, cc = search_bq_candidates(bq, qs, R)
     for qi in range(len(qs)):
-        assert counts[qi] == k and hc[qi] == R
         qn = orc.normalize(qs[qi])
-        qc = orc.bq_encode(qn)
-        sd = orc.bq_dist_all(qc, scodes)
-        outside = ~np.isin(sample_ids, cand[qi].astype(np.int64))
-        kd, kid = float(hd[qi][-1]), int(cand[qi][-1])
-        assert np.all((sd[outside] > kd) | ((sd[outside] == kd) & (sample_ids[outside] > kid)))
-        rows = orc.normalize_rows(np.stack([orc.synth_rows(42, int(i), 1, d, 0)[0] for i in cand[qi]]))
-        wi, wd = orc.lex_topk(orc.dist_all(2, qn, rows), cand[qi].astype(np.uint64), k)
+        pi, pd = orc.heap_pops(_bq_dists_chunked(orc, bq, orc.bq_encode(qn), n), R)
+        assert cc[qi] == R and np.array_equal(ci[qi], pi) and np.array_equal(bits(cd[qi]), bits(pd)), qi
+        rows = orc.normalize_rows(np.stack([orc.synth_rows(42, int(i), 1, d, 0)[0] for i in pi]))
+        wi, wd = orc.heap_topk(orc.dist_all(2, qn, rows), pi, k)
+        assert counts[qi] == k
         assert np.array_equal(ids[qi], wi), qi
         assert np.array_equal(bits(dists[qi]), bits(wd)), qi
     f.destroy()

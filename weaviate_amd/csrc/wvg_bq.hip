@@ -37,11 +37,15 @@ __device__ __forceinline__ u64x2 ld_codes(const u64x2 *p) { return __builtin_non
 // COS (a batch, ScanArgs::cosched): the 1D grid's consecutive ids on one XCD
 // are the nq queries of one row range, which read the same codes side by side
 // from that XCD's L2 (default-policy loads; K8e COS in wvg_pq.hip).
-// EMIT (the heap replay, wvg_replay.hip): each wave also writes the keys of the
-// rows the reference's heap could insert (WaveTopK::offer_dist_emit).
-template <int E, int NCH, bool COS = false, bool EMIT = false>
+// EMIT (the heap replay, wvg_replay.hip): each wave also records the keys of
+// the rows the reference's heap could insert (WaveTopK::offer_dist_emit):
+// 1 = into an LDS buffer of emit_cap keys per wave (dynamic shared memory),
+// copied to a.emit after the scan loop; 2 = straight into a.emit (the rerun
+// with buffers as large as the wave's rows).
+template <int E, int NCH, bool COS = false, int EMIT = 0>
 __global__ __launch_bounds__(BQ_WAVES * 64) void scan_bq_kernel(ScanArgs a, uint64_t *partials)
 {
+    extern __shared__ uint64_t emit_lds[];
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint32_t qi = blockIdx.y, rng = blockIdx.x, G = gridDim.x;
     if constexpr (COS) {
@@ -69,8 +73,8 @@ __global__ __launch_bounds__(BQ_WAVES * 64) void scan_bq_kernel(ScanArgs a, uint
     uint64_t *ebuf = nullptr;
     uint32_t ecnt = 0;
     float eseed = __builtin_inff();
-    if constexpr (EMIT) {
-        ebuf = a.emit + ((size_t)qi * total + gw) * a.emit_cap;
+    if constexpr (EMIT != 0) {
+        ebuf = EMIT == 1 ? emit_lds + (size_t)wave * a.emit_cap : a.emit + ((size_t)qi * total + gw) * a.emit_cap;
         if (a.emit_seed) eseed = a.emit_seed[(size_t)qi * G + rng];
     }
     if constexpr (NCH > 0) {
@@ -103,7 +107,7 @@ __global__ __launch_bounds__(BQ_WAVES * 64) void scan_bq_kernel(ScanArgs a, uint
                 tot += (uint32_t)__popcll(cur[c].x ^ q[2 * c]) + (uint32_t)__popcll(cur[c].y ^ q[2 * c + 1]);
             const float dist = (float)tot;  // exact: sum of float32(popcount) is an integer < 2^24
             // rejection on the float distance first: the key is built only when some lane passes
-            if constexpr (EMIT)
+            if constexpr (EMIT != 0)
                 tk.offer_dist_emit(dist, (uint32_t)(t * 64 + lane), m_cur, eseed, ebuf, ecnt, a.emit_cap);
             else
                 tk.offer_dist_fast(dist, (uint32_t)(t * 64 + lane), m_cur);
@@ -123,39 +127,45 @@ __global__ __launch_bounds__(BQ_WAVES * 64) void scan_bq_kernel(ScanArgs a, uint
                 tot += (uint32_t)__popcll(x.x ^ q[2 * c]) + (uint32_t)__popcll(x.y ^ q[2 * c + 1]);
             }
             const float dist = (float)tot;
-            if constexpr (EMIT)
+            if constexpr (EMIT != 0)
                 tk.offer_dist_emit(dist, (uint32_t)(t * 64 + lane), m, eseed, ebuf, ecnt, a.emit_cap);
             else
                 tk.offer_dist_fast(dist, (uint32_t)(t * 64 + lane), m);
         }
     }
-    if constexpr (EMIT) {
+    if constexpr (EMIT != 0) {
+        if constexpr (EMIT == 1) {  // the wave's LDS record to its global buffer (after every load)
+            uint64_t *g = a.emit + ((size_t)qi * total + gw) * a.emit_cap;
+            const uint32_t n = min(ecnt, a.emit_cap);
+            for (uint32_t i = (uint32_t)lane; i < n; i += 64) g[i] = ebuf[i];
+        }
         if (lane == 0) a.emit_cnt[(size_t)qi * total + gw] = ecnt;
     }
     group_combine_store<E, BQ_WAVES>(tk, partials + ((size_t)qi * G + rng) * a.k);
 }
 
-template <int E, bool COS, bool EMIT>
+template <int E, bool COS, int EMIT>
 static hipError_t launch_bq_ec(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
 {
     const dim3 grid = COS ? dim3((unsigned)groups * a.nq) : dim3(groups, a.nq), block(BQ_WAVES * 64);
+    const uint32_t lds = EMIT == 1 ? (uint32_t)(BQ_WAVES * a.emit_cap * 8) : 0u;
     switch (a.nchunks) {
-    case 1: launch_timed((scan_bq_kernel<E, 1, COS, EMIT>), grid, block, 0, s, a, partials); break;   // d <= 128
-    case 6: launch_timed((scan_bq_kernel<E, 6, COS, EMIT>), grid, block, 0, s, a, partials); break;   // d = 768
-    case 12: launch_timed((scan_bq_kernel<E, 12, COS, EMIT>), grid, block, 0, s, a, partials); break; // d = 1536
-    default: launch_timed((scan_bq_kernel<E, 0, COS, EMIT>), grid, block, 0, s, a, partials); break;
+    case 1: launch_timed((scan_bq_kernel<E, 1, COS, EMIT>), grid, block, lds, s, a, partials); break;   // d <= 128
+    case 6: launch_timed((scan_bq_kernel<E, 6, COS, EMIT>), grid, block, lds, s, a, partials); break;   // d = 768
+    case 12: launch_timed((scan_bq_kernel<E, 12, COS, EMIT>), grid, block, lds, s, a, partials); break; // d = 1536
+    default: launch_timed((scan_bq_kernel<E, 0, COS, EMIT>), grid, block, lds, s, a, partials); break;
     }
     return hipGetLastError();
 }
 
-template <int E, bool EMIT>
+template <int E, int EMIT>
 static hipError_t launch_bq_e(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
 {
     if (a.cosched && a.nq > 1 && groups % 8 == 0) return launch_bq_ec<E, true, EMIT>(a, partials, groups, s);
     return launch_bq_ec<E, false, EMIT>(a, partials, groups, s);
 }
 
-template <bool EMIT>
+template <int EMIT>
 static hipError_t launch_bq_k(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
 {
     if (a.k <= 64) return launch_bq_e<1, EMIT>(a, partials, groups, s);
@@ -165,13 +175,14 @@ static hipError_t launch_bq_k(const ScanArgs &a, uint64_t *partials, int groups,
 
 hipError_t launch_scan_bq(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
 {
-    return launch_bq_k<false>(a, partials, groups, s);
+    return launch_bq_k<0>(a, partials, groups, s);
 }
 
-hipError_t launch_scan_bq_emit(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
+hipError_t launch_scan_bq_emit(const ScanArgs &a, uint64_t *partials, int groups, bool lds, hipStream_t s)
 {
     if (!a.emit || !a.emit_cnt || a.k == 0 || a.k > 256) return hipErrorInvalidValue;
-    return launch_bq_k<true>(a, partials, groups, s);
+    if (lds && (size_t)BQ_WAVES * a.emit_cap * 8 > BQ_EMIT_LDS_MAX) return hipErrorInvalidValue;
+    return lds ? launch_bq_k<1>(a, partials, groups, s) : launch_bq_k<2>(a, partials, groups, s);
 }
 
 // Encode row-major float rows; `normalize` is applied per row first (cosine).

@@ -194,8 +194,10 @@ struct SearchPlan {
 };
 
 bool allow_tile_range(const wvg_corpus *c, const uint64_t *allow, uint64_t allow_words, uint64_t &tb, uint64_t &te);
+// mq_ok: K1Q may take the batch; gemm_ok: the MFMA kernels may (neither takes
+// per-query allow windows, ScanArgs::allow_qstride)
 SearchPlan plan_search(wvg_corpus *c, uint32_t nq, uint32_t k, const uint64_t *allow, uint64_t allow_words,
-                       bool mq_ok = true);
+                       bool mq_ok = true, bool gemm_ok = true);
 uint32_t next_direction(wvg_corpus *c, uint32_t nq);
 int pq_dense(const wvg_corpus *c, const uint64_t *d_allow);
 void prepare_queries_host(const wvg_corpus *c, const float *queries, uint32_t nq, std::vector<float> &qf,
@@ -222,7 +224,7 @@ ScanArgs scan_args_for(const wvg_corpus *c, const void *d_q, uint32_t qpitch, ui
 
 // ---- the reference heap's exact result (wvg_replay.hip) -------------------------
 // Device workspace of bq_heap_candidates (per-wave emission buffers, the kept rows).
-size_t replay_workspace_bytes(uint32_t nq, uint32_t R, const SearchPlan &p);
+size_t replay_workspace_bytes(const wvg_corpus *bq, uint32_t nq, uint32_t R, const SearchPlan &p);
 // findTopVectorsCached into a heap of R + the pop loop (V/flat/index.go:355-374)
 // for nq prepared BQ queries: pops[q] = (slot, Hamming distance) in pop order.
 int bq_heap_candidates(wvg_corpus *bq, StreamSlot *sl, const void *d_qb, uint32_t qpb, uint32_t nq, uint32_t R,

@@ -325,9 +325,11 @@ hipError_t launch_scan_f32_stream(const ScanArgs &a, const StreamJob &j, hipStre
 // ids KEY_NONE, dists +inf, counts 0 for nq queries (empty corpus / slab).
 hipError_t launch_fill_empty(uint64_t *ids, float *dists, uint32_t *counts, uint32_t nq, uint32_t k, hipStream_t s);
 hipError_t launch_scan_bq(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s);
-// K5 with the heap-replay emission (a.emit set; groups * BQ_SCAN_WAVES waves per query).
+// K5 with the heap-replay emission (a.emit set; groups * BQ_SCAN_WAVES waves per query):
+// lds = record into LDS (4 * emit_cap * 8 <= BQ_EMIT_LDS_MAX bytes), else straight to HBM.
 constexpr int BQ_SCAN_WAVES = 4;
-hipError_t launch_scan_bq_emit(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s);
+constexpr size_t BQ_EMIT_LDS_MAX = 128u << 10;
+hipError_t launch_scan_bq_emit(const ScanArgs &a, uint64_t *partials, int groups, bool lds, hipStream_t s);
 // Heap replay (wvg_replay.hip).  prefix: per query, thr[q][g] = the k-th smallest
 // distance of ranges 0..g-1's lists (partials [nq][groups][k], ascending; +inf
 // while fewer than k rows precede range g).  filter: each wave's emitted keys

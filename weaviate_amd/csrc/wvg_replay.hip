@@ -229,15 +229,35 @@ namespace {
 constexpr uint32_t REPLAY_OUT_CAP = 65536;  // kept rows per query held on the device (more: the rerun)
 constexpr uint32_t REPLAY_HEAD = 4096;      // kept rows per query copied back with the totals
 
-// Per-wave buffer: the wave-local filter keeps about R (1 + ln(n / R)) of a
-// wave's n rows on a random order; twice that plus a margin, never more than
-// the wave's rows.
-uint32_t emit_cap_for(uint64_t ntiles, uint32_t waves, uint32_t R)
+// Per-wave record buffer.  On a random docID order the wave-local filter
+// keeps about R (1 + ln(n / R)) of a wave's n rows (~1.4k of 98k at 100M x
+// 1536, R = 200; a sum of independent Bernoulli(R / i), so its variance is
+// at most its mean).  Fast mode records into LDS (no global store in the scan
+// loop): as many keys as the LDS left by the workgroups sharing a CU holds,
+// used when that is the wave's whole range or 6 standard deviations above the
+// estimate; otherwise the keys go straight to HBM with twice the estimate.
+// Either way a wave that overflows reruns its query (rerun_full).
+struct EmitPlan {
+    uint32_t cap = 0;
+    bool lds = false;
+};
+EmitPlan emit_plan_for(uint64_t ntiles, int groups, uint32_t nq, uint32_t R, int num_cus)
 {
-    const uint64_t rows = (ntiles / std::max<uint32_t>(waves, 1) + 2) * 64;
+    const uint32_t waves = (uint32_t)groups * BQ_SCAN_WAVES;
+    const uint64_t rows = align_up((ntiles / std::max<uint32_t>(waves, 1) + 2) * 64, 64);
     const double est = (double)R * (1.0 + std::log(std::max(1.0, (double)rows / std::max<uint32_t>(R, 1))));
-    const uint64_t cap = (uint64_t)(2.0 * est) + 256;
-    return (uint32_t)std::min<uint64_t>(align_up(std::min(cap, rows), 64), 0xFFFFFFC0ull);
+    const uint64_t wg_per_cu = std::max<uint64_t>(1, ((uint64_t)groups * nq + num_cus - 1) / num_cus);
+    const size_t lds_wg = std::min<size_t>(BQ_EMIT_LDS_MAX, std::max<size_t>(16u << 10, (160u << 10) / wg_per_cu -
+                                                                                            (16u << 10)));
+    const uint64_t lcap = std::min<uint64_t>(rows, lds_wg / (BQ_SCAN_WAVES * 8) / 64 * 64);
+    EmitPlan e;
+    if (lcap >= rows || (double)lcap >= est + 6.0 * std::sqrt(est) + 64) {  // the count's variance <= its mean
+        e.cap = (uint32_t)lcap;
+        e.lds = true;
+        return e;
+    }
+    e.cap = (uint32_t)std::min<uint64_t>(rows, align_up((uint64_t)(2.0 * est) + 256, 64));
+    return e;
 }
 
 struct ReplayWs {
@@ -262,8 +282,8 @@ ReplayWs replay_ws(uint32_t nq, uint32_t groups, uint32_t R, uint32_t cap, uint3
 
 // The four device steps over ScanArgs `a` (queries, allow window, k = R set),
 // into `ws` laid out by `w`; no host synchronization.
-int run_emit(const ScanArgs &a0, int groups, uint32_t cap, uint32_t out_cap, char *ws, const ReplayWs &w,
-             const float *seed, hipStream_t s)
+int run_emit(wvg_ctx *ctx, const ScanArgs &a0, int groups, uint32_t cap, bool lds, uint32_t out_cap, char *ws,
+             const ReplayWs &w, const float *seed, hipStream_t s)
 {
     ScanArgs a = a0;
     a.emit = (uint64_t *)(ws + w.emit);
@@ -274,7 +294,11 @@ int run_emit(const ScanArgs &a0, int groups, uint32_t cap, uint32_t out_cap, cha
     uint32_t *tot = (uint32_t *)(ws + w.tot);
     WVG_HIP(hipMemsetAsync(tot, 0, (size_t)nq * 8, s));
     uint64_t *part = (uint64_t *)(ws + w.part);
-    WVG_HIP(launch_scan_bq_emit(a, part, groups, s));
+    {
+        ProfArm arm(ctx);  // wvg_profile_*: the scan dispatch's own events
+        if (arm.rc) return arm.rc;
+        WVG_HIP(launch_scan_bq_emit(a, part, groups, lds, s));
+    }
     WVG_HIP(launch_emit_prefix(part, nq, (uint32_t)groups, R, (float *)(ws + w.thr), s));
     WVG_HIP(launch_emit_filter(a.emit, a.emit_cnt, cap, (const float *)(ws + w.thr), nq, (uint32_t)groups,
                                BQ_SCAN_WAVES, (uint32_t *)(ws + w.fcnt), tot + nq, s));
@@ -300,7 +324,8 @@ void replay_pops(const uint64_t *keys, size_t n, uint32_t R, std::vector<GoItem>
 // One query again with buffers that cannot overflow (every row of a wave),
 // seeded with the first pass's thresholds: its own device allocation (this
 // path is for adversarial docID orders only).
-int rerun_full(const ScanArgs &a0, int groups, const float *d_thr_q, hipStream_t s, std::vector<uint64_t> &keys)
+int rerun_full(wvg_ctx *ctx, const ScanArgs &a0, int groups, const float *d_thr_q, hipStream_t s,
+               std::vector<uint64_t> &keys)
 {
     const uint64_t ntiles = a0.tile_end - a0.tile_begin;
     const uint32_t waves = (uint32_t)groups * BQ_SCAN_WAVES;
@@ -325,7 +350,7 @@ int rerun_full(const ScanArgs &a0, int groups, const float *d_thr_q, hipStream_t
         ScanArgs a = a0;
         a.nq = 1;
         a.cosched = 0;  // same groups, so the same ranges as the first pass
-        rc = run_emit(a, groups, cap, out_cap, ws, w, (const float *)(ws + seed_off), s);
+        rc = run_emit(ctx, a, groups, cap, false, out_cap, ws, w, (const float *)(ws + seed_off), s);
         if (rc) break;
         uint32_t tot[2] = {0, 0};
         if (hipMemcpyAsync(tot, ws + w.tot, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -352,10 +377,10 @@ int rerun_full(const ScanArgs &a0, int groups, const float *d_thr_q, hipStream_t
 
 }  // namespace
 
-size_t replay_workspace_bytes(uint32_t nq, uint32_t R, const SearchPlan &p)
+size_t replay_workspace_bytes(const wvg_corpus *bq, uint32_t nq, uint32_t R, const SearchPlan &p)
 {
-    const uint32_t waves = (uint32_t)p.groups * BQ_SCAN_WAVES;
-    return replay_ws(nq, (uint32_t)p.groups, R, emit_cap_for(p.te - p.tb, waves, R), REPLAY_OUT_CAP).total;
+    const EmitPlan e = emit_plan_for(p.te - p.tb, p.groups, nq, R, bq->ctx->num_cus);
+    return replay_ws(nq, (uint32_t)p.groups, R, e.cap, REPLAY_OUT_CAP).total;
 }
 
 int bq_heap_candidates(wvg_corpus *bq, StreamSlot *sl, const void *d_qb, uint32_t qpb, uint32_t nq, uint32_t R,
@@ -363,9 +388,8 @@ int bq_heap_candidates(wvg_corpus *bq, StreamSlot *sl, const void *d_qb, uint32_
 {
     hipStream_t s = sl->stream;
     const int groups = p.groups;
-    const uint32_t waves = (uint32_t)groups * BQ_SCAN_WAVES;
-    const uint32_t cap = emit_cap_for(p.te - p.tb, waves, R);
-    const ReplayWs w = replay_ws(nq, (uint32_t)groups, R, cap, REPLAY_OUT_CAP);
+    const EmitPlan e = emit_plan_for(p.te - p.tb, groups, nq, R, bq->ctx->num_cus);
+    const ReplayWs w = replay_ws(nq, (uint32_t)groups, R, e.cap, REPLAY_OUT_CAP);
     ScanArgs a{};
     a.data = bq->d_data;
     a.valid = bq->d_valid;
@@ -383,7 +407,7 @@ int bq_heap_candidates(wvg_corpus *bq, StreamSlot *sl, const void *d_qb, uint32_
     a.nq = nq;
     a.k = R;
     a.cosched = p.cosched;
-    int rc = run_emit(a, groups, cap, REPLAY_OUT_CAP, ws, w, nullptr, s);
+    int rc = run_emit(bq->ctx, a, groups, e.cap, e.lds, REPLAY_OUT_CAP, ws, w, nullptr, s);
     if (rc) return rc;
     // totals, overflow flags and the first REPLAY_HEAD kept rows of every query in one round trip
     const uint32_t head = REPLAY_HEAD;
@@ -408,7 +432,7 @@ int bq_heap_candidates(wvg_corpus *bq, StreamSlot *sl, const void *d_qb, uint32_
             ScanArgs aq = a;
             aq.queries = (const uint64_t *)d_qb + (size_t)q * qpb;
             aq.allow = d_allow;  // filtered batches use one shared window (no per-query stride here)
-            rc = rerun_full(aq, groups, (const float *)(ws + w.thr) + (size_t)q * groups, s, keys);
+            rc = rerun_full(bq->ctx, aq, groups, (const float *)(ws + w.thr) + (size_t)q * groups, s, keys);
             if (rc) return rc;
             qk = keys.data();
             n = keys.size();
@@ -436,7 +460,7 @@ int bq_rescore_replay(wvg_corpus *bq, wvg_corpus *f32, const float *queries, uin
     const size_t o_qb = cv.take(query_bytes(bq, nq));
     const size_t o_qf = cv.take(f32 ? (size_t)nq * fpitch * 4 : 0);
     const size_t o_allow = cv.take(p.allow_bytes());
-    const size_t o_rep = cv.take(replay_workspace_bytes(nq, R, p));
+    const size_t o_rep = cv.take(replay_workspace_bytes(bq, nq, R, p));
     const size_t o_cand = cv.take(f32 ? (size_t)nq * R * 8 : 0);
     const size_t o_resc = cv.take(f32 ? (size_t)nq * R * 8 : 0);
     void *base = nullptr;

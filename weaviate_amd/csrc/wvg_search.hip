@@ -209,7 +209,7 @@ ScreenWs screen_ws(uint32_t nq, uint32_t k, uint32_t nrr, uint32_t kbn, uint32_t
 }
 
 SearchPlan plan_search(wvg_corpus *c, uint32_t nq, uint32_t k, const uint64_t *allow, uint64_t allow_words,
-                       bool mq_ok)
+                       bool mq_ok, bool gemm_ok)
 {
     SearchPlan p;
     p.empty = !allow_tile_range(c, allow, allow_words, p.tb, p.te) || k == 0 || nq == 0;
@@ -221,7 +221,7 @@ SearchPlan plan_search(wvg_corpus *c, uint32_t nq, uint32_t k, const uint64_t *a
     a.dim = c->kind == WVG_KIND_F32 ? c->dim : 0;  // K1 grid depends on the row size and metric
     a.metric = c->metric;
     const uint32_t mn = c->ctx->opt.mfma_min_queries;
-    p.gemm = c->kind == WVG_KIND_F32 && mn > 0 && nq >= mn && gemm_supported(c->dim, c->metric) &&
+    p.gemm = gemm_ok && c->kind == WVG_KIND_F32 && mn > 0 && nq >= mn && gemm_supported(c->dim, c->metric) &&
              !c->ctx->order512;  // K3's 32 MFMA slices are the AVX2 order's chains
     if (p.gemm)
         p.groups = (int)gemm_row_ranges(nq, std::max<uint64_t>(1, p.te - p.tb), c->ctx->num_cus, c->dim, k);
@@ -327,9 +327,8 @@ static int run_screen(wvg_corpus *c, const ScanArgs &a, const SearchPlan &p, cha
 // One query of a host call on the query-stream kernel with its in-launch merge
 // (run_search); its results can then go straight to host memory.
 // (a filtered query too: its allow window is copied with the call, the scan masks tiles with it)
-static bool inlaunch_single(const wvg_corpus *c, uint32_t nq, const SearchPlan &p, bool has_allow)
+static bool inlaunch_single(const wvg_corpus *c, uint32_t nq, const SearchPlan &p)
 {
-    (void)has_allow;
     return nq == 1 && !p.gemm && !p.cosched && c->kind == WVG_KIND_F32 && tuning().pipeline_mode == 1;
 }
 
@@ -377,12 +376,12 @@ int run_search(wvg_corpus *c, const void *d_q, uint32_t qpitch, uint32_t nq, uin
         pe.groups = p.exact_groups;
         return run_search(c, d_q, qpitch, nq, k, d_allow, pe, partials, ids, dists, counts, s, sl, nullptr, so);
     }
-    if (sl && inlaunch_single(c, nq, p, d_allow != nullptr)) {
+    if (sl && inlaunch_single(c, nq, p)) {
         // One query of a host call: the query-stream kernel, whose extra workgroup merges
         // the partial lists in the same launch (no second kernel, no gap between them);
         // its arrival counter is the slot's persistent one, counted from the slot's base
-        // (no per-call memset).  A merge that gives up (4 s) leaves counts 0: the caller's
-        // check (search_batch) reports it.
+        // (no per-call memset).  A merge that gives up (4 s) writes empty entries and the
+        // header count WVG_RECORDS_TIMEOUT: search_batch reports it as WVG_ERR_DEVICE.
         uint32_t *ctl = nullptr;
         int rc = sl->control(&ctl);
         if (rc) return rc;
@@ -543,6 +542,7 @@ struct wvg_search_request {
     uint32_t k;
     const uint64_t *allow = nullptr;  // the caller's allow list (helpers.AllowList bitmap), or null
     uint64_t allow_words = 0;
+    uint64_t tb = 0, te = 0;          // its tile window (allow_tile_range), for filtered requests
     uint64_t *ids;
     float *dists;
     uint32_t *counts;
@@ -662,6 +662,13 @@ static int search_batch(wvg_corpus *c, const float *queries, uint32_t nq, uint32
 // queries on one corpus (profiles/r03/measure_1/small.log.txt), dot / cosine
 // batches of >= mfma_min_queries go to the matrix cores.
 constexpr size_t COALESCE_MAX = 256;
+// A filtered batch's per-query allow windows (B x union width x 8 bytes) stay
+// within this (256 callers over a 125M-row slab would need 4 GB).
+constexpr size_t FILTER_BATCH_BYTES = (size_t)8 << 20;
+// k classes of coalesced batches: the bf16 screen takes k <= 16, the register
+// top-k holds 64 / 128 / 256 keys per wave (a k = 256 caller put
+// every k = 10 caller of its batch on the E = 4 top-k and off the screen).
+static int coalesce_kclass(uint32_t k) { return k <= 16 ? 0 : k <= 64 ? 1 : k <= 128 ? 2 : 3; }
 
 // Filtered single queries of one coalesced batch (F32): one co-scheduled K1
 // launch over the union of their allow windows, every query masked by its
@@ -711,13 +718,16 @@ static void run_coalesced(wvg_corpus *c, const std::vector<wvg_search_request *>
 // the calls that arrive while the previous one runs, so the batch size follows
 // the arrival rate.
 static int search_coalesced(wvg_corpus *c, const float *query, uint32_t k, const uint64_t *allow,
-                            uint64_t allow_words, uint64_t *out_ids, float *out_dists, uint32_t *out_counts)
+                            uint64_t allow_words, uint64_t tb, uint64_t te, uint64_t *out_ids, float *out_dists,
+                            uint32_t *out_counts)
 {
     wvg_search_request r;
     r.q = query;
     r.k = k;
     r.allow = allow;
     r.allow_words = allow_words;
+    r.tb = tb;
+    r.te = te;
     r.ids = out_ids;
     r.dists = out_dists;
     r.counts = out_counts;
@@ -758,22 +768,29 @@ static int search_coalesced(wvg_corpus *c, const float *query, uint32_t k, const
         }
         std::vector<wvg_search_request *> batch;
         uint32_t kk = 0;  // the batch's k: the largest of its requests' (round 4: the head's k only)
-        // filtered and unfiltered requests form separate batches; filtered batches stay
-        // below the MFMA threshold (the co-scheduled K1 takes one allow window per query)
+        // filtered and unfiltered requests form separate batches.  A filtered batch
+        // holds every query's allow words over the union of their windows (B x W
+        // words on the host, in scratch and over the bus), so it stops growing at
+        // FILTER_BATCH_BYTES; the requests left over run in the next batch.
+        // Requests of one batch also share a k class (coalesce_kclass), so a large-k
+        // caller never moves small-k callers to a larger register top-k or off the screen.
         const bool filt = co.pending.front()->allow != nullptr;
-        const uint32_t mn = c->ctx->opt.mfma_min_queries;
-        const size_t cap = filt && mn > 1 && c->metric != WVG_METRIC_L2 && c->metric != WVG_METRIC_MANHATTAN &&
-                                   c->metric != WVG_METRIC_HAMMING
-                               ? std::min<size_t>(COALESCE_MAX, mn - 1)
-                               : COALESCE_MAX;
-        for (auto it = co.pending.begin(); it != co.pending.end() && batch.size() < cap;) {
-            if (((*it)->allow != nullptr) == filt) {
-                kk = std::max(kk, (*it)->k);
-                batch.push_back(*it);
-                it = co.pending.erase(it);
-            } else {
+        const int kcl = coalesce_kclass(co.pending.front()->k);
+        uint64_t TB = UINT64_MAX, TE = 0;
+        for (auto it = co.pending.begin(); it != co.pending.end() && batch.size() < COALESCE_MAX;) {
+            if (((*it)->allow != nullptr) != filt || coalesce_kclass((*it)->k) != kcl) {
                 ++it;
+                continue;
             }
+            if (filt) {
+                const uint64_t nb = std::min(TB, (*it)->tb), ne = std::max(TE, (*it)->te);
+                if (!batch.empty() && (batch.size() + 1) * (ne - nb) * 8 > FILTER_BATCH_BYTES) break;
+                TB = nb;
+                TE = ne;
+            }
+            kk = std::max(kk, (*it)->k);
+            batch.push_back(*it);
+            it = co.pending.erase(it);
         }
         g.unlock();
         const auto tb0 = std::chrono::steady_clock::now();
@@ -811,7 +828,7 @@ int wvg_search(wvg_corpus *c, const float *queries, uint32_t nq, uint32_t k, con
             write_empty(1, k, out_ids, out_dists, out_counts);
             return WVG_OK;
         }
-        return search_coalesced(c, queries, k, allow_bits, allow_words, out_ids, out_dists, out_counts);
+        return search_coalesced(c, queries, k, allow_bits, allow_words, tb, te, out_ids, out_dists, out_counts);
     }
     return search_batch(c, queries, nq, k, allow_bits, allow_words, out_ids, out_dists, out_counts);
 }
@@ -859,7 +876,7 @@ static int wvg::search_batch(wvg_corpus *c, const float *queries, uint32_t nq, u
     uint32_t qpitch = 0;
     // a single in-launch F32 query of up to STREAM_QIN_FLOATS floats goes in the kernel arguments
     alignas(16) float qinl[STREAM_QIN_FLOATS];  // (no heap allocation on the single-query path)
-    const bool qin = inlaunch_single(c, nq, p, p.allow_host != nullptr) &&
+    const bool qin = inlaunch_single(c, nq, p) &&
                      (size_t)f32_chunks(c->dim) * 4 <= STREAM_QIN_FLOATS && (tuning().single_path & 1) == 0;
     if (qin) {  // prepare_queries_host for one F32 query, into the kernel-argument buffer
         qpitch = f32_chunks(c->dim) * 4;
@@ -873,7 +890,7 @@ static int wvg::search_batch(wvg_corpus *c, const float *queries, uint32_t nq, u
         if (rc) return rc;
     }
     const uint64_t *d_allow = nullptr;
-    if (p.allow_host && inlaunch_single(c, nq, p, true) && p.allow_bytes() <= STAGE_MAX) {
+    if (p.allow_host && inlaunch_single(c, nq, p) && p.allow_bytes() <= STAGE_MAX) {
         // a single in-launch query reads its allow window straight from the slot's pinned
         // staging over the bus (each wave's next tile word is prefetched a tile ahead): no
         // host-to-device copy (~10 us of a 125 KB window's copy and its API time)
@@ -887,7 +904,7 @@ static int wvg::search_batch(wvg_corpus *c, const float *queries, uint32_t nq, u
     // a single query merged in-launch writes its results straight into the slot's
     // coherent host buffer as tagged records: no device-to-host copy (and its ~10 us)
     // and no stream synchronization per call (the host polls the tags)
-    const bool zc = inlaunch_single(c, nq, p, d_allow != nullptr);
+    const bool zc = inlaunch_single(c, nq, p);
     const int sp = tuning().single_path;
     const bool legacy = zc && (sp & 4) != 0;  // tools A/B: round 4's untagged layout
     SingleOut so;
@@ -983,8 +1000,10 @@ static int wvg::search_batch_filtered(wvg_corpus *c, const std::vector<wvg_searc
     std::vector<uint64_t> tb(B), te(B);
     std::vector<char> live(B);
     uint64_t TB = UINT64_MAX, TE = 0;
-    for (uint32_t i = 0; i < B; i++) {
-        live[i] = allow_tile_range(c, batch[i]->allow, batch[i]->allow_words, tb[i], te[i]);
+    for (uint32_t i = 0; i < B; i++) {  // (windows found by wvg_search: a request with none never queues)
+        tb[i] = batch[i]->tb;
+        te[i] = batch[i]->te;
+        live[i] = te[i] > tb[i];
         if (!live[i]) continue;
         TB = std::min(TB, tb[i]);
         TE = std::max(TE, te[i]);
@@ -995,7 +1014,7 @@ static int wvg::search_batch_filtered(wvg_corpus *c, const std::vector<wvg_searc
     std::vector<uint64_t> win((size_t)B * W, 0ull);  // query i's allow words of tiles [TB, TE) (0 outside its own)
     for (uint32_t i = 0; i < B; i++)
         if (live[i]) std::memcpy(win.data() + (size_t)i * W + (tb[i] - TB), batch[i]->allow + wb + tb[i], (te[i] - tb[i]) * 8);
-    SearchPlan p = plan_search(c, B, k, nullptr, 0, false);  // (per-query allow windows: the COS K1)
+    SearchPlan p = plan_search(c, B, k, nullptr, 0, false, false);  // per-query allow windows: the COS K1
     if (p.empty) return WVG_OK;
     if (p.gemm || !p.cosched) return fail(WVG_ERR_INVALID, "filtered coalesced batch needs the co-scheduled K1");
     p.tb = TB;

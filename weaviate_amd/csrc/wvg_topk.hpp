@@ -246,7 +246,11 @@ struct WaveTopK {
     // range), so d_i < min(both) keeps a superset of the inserted rows: the
     // rows it drops are no-ops of insertToHeap.  Distances must not be NaN
     // (Hamming).  Kept keys go to buf[cnt ...] in lane (= docID) order; cnt
-    // counts past cap so the host can tell an overflow.
+    // counts past cap so the host can tell an overflow.  buf is LDS in the
+    // scan's fast mode: a global store inside the scan loop would make every
+    // load of the loop "maybe clobbered" for the compiler, turning the
+    // wave-uniform query words and tile masks into vector loads whose vmcnt(0)
+    // waits drain the prefetched tile (K5 3.43 vs 2.81 ms per 100M x 1536).
     __device__ __forceinline__ void offer_dist_emit(float dist, uint32_t slot, uint64_t live, float seed, uint64_t *buf,
                                                     uint32_t &cnt, uint32_t cap)
     {
