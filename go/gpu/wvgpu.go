@@ -150,8 +150,9 @@ func DeviceCount() (int, error) {
 // Ctx is one GPU's context.  It counts its open corpora: Close refuses while
 // any is open, so no Corpus (nor its finalizer) ever uses a freed context.
 type Ctx struct {
-	h       *C.wvg_ctx
-	corpora int64
+	h        *C.wvg_ctx
+	corpora  int64
+	borrowed bool // a device context of a Multi: closed by Multi.Close
 }
 
 func Open(device int) (*Ctx, error) {
@@ -206,6 +207,9 @@ func OpenWith(device int, o *Options) (*Ctx, error) {
 func (c *Ctx) Close() error {
 	defer pin(c)()
 	if c.h == nil {
+		return nil
+	}
+	if c.borrowed {
 		return nil
 	}
 	if n := atomic.LoadInt64(&c.corpora); n != 0 {
@@ -926,4 +930,169 @@ func (c *Ctx) PQSDC(metric int, table []float32, m, ks int, x, codes []byte) ([]
 		return nil, e
 	}
 	return out, nil
+}
+
+// ---- several GPUs in one process ---------------------------------------------
+
+// Multi serves one index from several GPUs of this process, as Weaviate's
+// Index fans a search out over its shards (adapters/repos/db/index.go:
+// 1567-1648): one context per device and, for distinct devices, one RCCL
+// communicator per device inside the library.  Close refuses while a
+// MultiCorpus of it is open.
+type Multi struct {
+	h       *C.wvg_multi
+	corpora int64
+}
+
+// OpenMulti opens devices (e.g. every index of WEAVIATE_GPU_DEVICES) with
+// options o (nil = defaults).
+func OpenMulti(devices []int, o *Options) (*Multi, error) {
+	defer pin()()
+	if len(devices) == 0 {
+		return nil, errors.New("wvgpu: OpenMulti needs at least one device")
+	}
+	devs := make([]C.int, len(devices))
+	for i, d := range devices {
+		devs[i] = C.int(d)
+	}
+	var opt C.wvg_options
+	C.wvg_options_default(&opt)
+	if o != nil {
+		opt.mfma_min_queries = C.uint32_t(o.MFMAMinQueries)
+		opt.merge_wait_us = C.uint32_t(o.MergeWaitUs)
+		opt.cache_reuse = C.int32_t(o.CacheReuse)
+		opt.batch_screen = C.int32_t(o.BatchScreen)
+		opt.coalesce = C.int32_t(o.Coalesce)
+		opt.heap_replay = C.int32_t(o.HeapReplay)
+	}
+	var h *C.wvg_multi
+	if e := err(C.wvg_multi_open(&devs[0], C.int(len(devices)), &opt, &h)); e != nil {
+		return nil, e
+	}
+	return &Multi{h: h}, nil
+}
+
+func (m *Multi) Close() error {
+	defer pin(m)()
+	if m.h == nil {
+		return nil
+	}
+	if n := atomic.LoadInt64(&m.corpora); n != 0 {
+		return fmt.Errorf("wvgpu: %d multi corpora still open", n)
+	}
+	e := err(C.wvg_multi_close(m.h))
+	m.h = nil
+	return e
+}
+
+// Info: the device count and whether the exchange runs over RCCL (false: peer
+// copies, e.g. a one-GPU rehearsal with a repeated device).
+func (m *Multi) Info() (ndev int, rccl bool, e error) {
+	defer pin(m)()
+	var n, r C.int
+	e = err(C.wvg_multi_info(m.h, &n, &r))
+	return int(n), r != 0, e
+}
+
+// MultiCorpus deals docIDs to the devices in contiguous slabs of rows/ndev
+// (rounded up to 64): shard i holds [i*slab, (i+1)*slab).
+type MultiCorpus struct {
+	h     *C.wvg_multi_corpus
+	m     *Multi
+	dims  int
+	shard int
+}
+
+func (m *Multi) NewCorpus(kind, metric, dims int, rows uint64) (*MultiCorpus, error) {
+	defer pin(m)()
+	var h *C.wvg_multi_corpus
+	if e := err(C.wvg_multi_corpus_create(m.h, C.int(kind), C.int(metric), C.uint32_t(dims), C.uint64_t(rows),
+		&h)); e != nil {
+		return nil, e
+	}
+	atomic.AddInt64(&m.corpora, 1)
+	x := &MultiCorpus{h: h, m: m, dims: dims}
+	runtime.SetFinalizer(x, func(x *MultiCorpus) { _ = x.Close() })
+	return x, nil
+}
+
+func (x *MultiCorpus) Close() error {
+	defer pin(x)()
+	if x.h == nil {
+		return nil
+	}
+	e := err(C.wvg_multi_corpus_destroy(x.h))
+	x.h = nil
+	atomic.AddInt64(&x.m.corpora, -1)
+	runtime.SetFinalizer(x, nil)
+	return e
+}
+
+// Shard i's slab: its docID base and rows (its own corpus handle stays
+// inside the library; per-shard work goes through the Multi methods).
+func (x *MultiCorpus) Shard(i int) (idBase, slabRows uint64, e error) {
+	defer pin(x)()
+	var b, s C.uint64_t
+	e = err(C.wvg_multi_corpus_shard(x.h, C.int(i), nil, &b, &s))
+	return uint64(b), uint64(s), e
+}
+
+// Add / AddBatch / Delete routed to the shard owning each docID.
+func (x *MultiCorpus) AddBatch(ids []uint64, vectors [][]float32) error {
+	defer pin(x)()
+	if len(ids) != len(vectors) {
+		return errors.Errorf("ids and vectors have different lengths")
+	}
+	if len(ids) == 0 {
+		return nil
+	}
+	flat := make([]float32, 0, len(ids)*x.dims)
+	for _, v := range vectors {
+		if len(v) != x.dims {
+			return errors.Errorf("insert called with a vector of the wrong size")
+		}
+		flat = append(flat, v...)
+	}
+	return err(C.wvg_multi_corpus_upsert(x.h, u64p(ids), f32p(flat), C.uint64_t(len(ids)), C.uint32_t(x.dims)))
+}
+
+func (x *MultiCorpus) Delete(ids ...uint64) error {
+	defer pin(x)()
+	return err(C.wvg_multi_corpus_delete(x.h, u64p(ids), C.uint64_t(len(ids))))
+}
+
+// SetCodebook: the PQ codebook (centers [m][ks][dims/m]) of every shard.
+func (x *MultiCorpus) SetCodebook(centers []float32, m, ks int) error {
+	defer pin(x)()
+	return err(C.wvg_multi_corpus_set_codebook(x.h, f32p(centers), C.uint32_t(m), C.uint32_t(ks)))
+}
+
+// SearchBatch: nq queries over every shard -- the per-device scans, one RCCL
+// all-gather of their top-k blocks, the merge (index.go:1644-1648).
+func (x *MultiCorpus) SearchBatch(qs []float32, nq, k int, allow helpers.AllowList) (*Results, error) {
+	defer pin(x)()
+	r := emptyResults(nq, k)
+	if nq == 0 || k == 0 {
+		return r, nil
+	}
+	words, ok := allowBitmap(allow)
+	if !ok {
+		return r, nil
+	}
+	if e := err(C.wvg_multi_search(x.h, f32p(qs), C.uint32_t(nq), C.uint32_t(k), u64p(words),
+		C.uint64_t(len(words)), u64p(r.IDs), f32p(r.Dists), u32p(r.Counts))); e != nil {
+		return nil, e
+	}
+	return r, nil
+}
+
+// Ctx: device i's context (for that device's own corpora and bulk calls);
+// owned by the Multi, so its Close does nothing.
+func (m *Multi) Ctx(i int) (*Ctx, error) {
+	defer pin(m)()
+	var h *C.wvg_ctx
+	if e := err(C.wvg_multi_ctx(m.h, C.int(i), &h)); e != nil {
+		return nil, e
+	}
+	return &Ctx{h: h, borrowed: true}, nil
 }

@@ -310,6 +310,43 @@ int wvg_topk_merge_packed(wvg_ctx *ctx, const void *d_packed, uint32_t nq, uint3
                           uint32_t k, uint64_t *d_out_ids, float *d_out_dists, uint32_t *d_out_counts,
                           void *stream);
 
+/* ---- several GPUs in one process ------------------------------------------
+ * Index.objectVectorSearch (adapters/repos/db/index.go:1567-1648) fans a
+ * search out over the shards of one process and merges their results by
+ * distance.  A multi handle holds one context per device (opts as
+ * wvg_open_ex) and, when the devices are distinct and RCCL loads, one
+ * communicator per device (ncclCommInitAll).  A multi corpus deals docIDs to
+ * the devices in contiguous slabs: shard i holds [i * slab, (i + 1) * slab),
+ * slab = rows / ndev rounded up to 64.  wvg_multi_search runs every shard's
+ * scan on its own device stream into a packed block, ONE grouped RCCL
+ * all-gather of the blocks over xGMI (peer copies to device 0 when devices
+ * repeat, e.g. a one-GPU rehearsal {0, 0}), the merge on device 0, and returns
+ * [nq][k] ascending by (distance, docID) -- identical to one corpus holding
+ * every row.  Per-shard operations (PQ codebooks, other search kinds) take
+ * the shard's own handle from wvg_multi_corpus_shard.                      */
+typedef struct wvg_multi wvg_multi;
+typedef struct wvg_multi_corpus wvg_multi_corpus;
+int wvg_multi_open(const int *devices, int ndev, const wvg_options *opts, wvg_multi **out);
+int wvg_multi_close(wvg_multi *m);  /* after every multi corpus is destroyed */
+int wvg_multi_info(wvg_multi *m, int *ndev, int *uses_rccl);
+int wvg_multi_ctx(wvg_multi *m, int i, wvg_ctx **out);
+int wvg_multi_corpus_create(wvg_multi *m, int kind, int metric, uint32_t dim, uint64_t rows,
+                            wvg_multi_corpus **out);
+int wvg_multi_corpus_destroy(wvg_multi_corpus *mc);
+int wvg_multi_corpus_shard(wvg_multi_corpus *mc, int i, wvg_corpus **out, uint64_t *id_base, uint64_t *slab_rows);
+/* flat.Add / Delete routed to the shard owning each docID (WVG_ERR_CAPACITY
+ * for an id beyond the last slab). */
+int wvg_multi_corpus_upsert(wvg_multi_corpus *mc, const uint64_t *ids, const float *vectors, uint64_t n,
+                            uint32_t dim);
+int wvg_multi_corpus_delete(wvg_multi_corpus *mc, const uint64_t *ids, uint64_t n);
+/* As wvg_corpus_fill_synthetic over docIDs [0, n) of the whole corpus. */
+int wvg_multi_corpus_fill_synthetic(wvg_multi_corpus *mc, uint64_t seed, uint64_t n, int distribution);
+int wvg_multi_corpus_set_codebook(wvg_multi_corpus *mc, const float *centers, uint32_t m, uint32_t ks);
+/* wvg_search over all shards (any kind; k <= 256; allow_bits over global docIDs). */
+int wvg_multi_search(wvg_multi_corpus *mc, const float *queries, uint32_t nq, uint32_t k,
+                     const uint64_t *allow_bits, uint64_t allow_words, uint64_t *out_ids, float *out_dists,
+                     uint32_t *out_counts);
+
 /* The rescore loop of flat.searchByVectorBQ (V/flat/index.go:375-385) when
  * the candidate rows come from the host (LSM point gets): exact SingleDist of
  * q against rows [n][dim] (q used as given: normalize it first for cosine,

@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "wvgpu.h")
 GO_DIR = os.path.join(ROOT, "go", "gpu")
 # bench / test helpers with no Go caller
-NOT_BOUND = {"wvg_corpus_fill_synthetic", "wvg_synthetic_rows"}
+NOT_BOUND = {"wvg_corpus_fill_synthetic", "wvg_synthetic_rows", "wvg_multi_corpus_fill_synthetic"}  # test helpers
 
 
 def header_prototypes():

@@ -99,6 +99,19 @@ SIGNATURES = {
     "wvg_rescore": (c_int, [c_void_p, c_int, _P(c_float), _P(c_float), _P(c_uint64), c_uint64, c_uint32, c_uint32,
                             _P(c_uint64), _P(c_float), _P(c_uint32)]),
     "wvg_pq_encode_corpus": (c_int, [c_void_p, c_void_p]),
+    "wvg_multi_open": (c_int, [_P(c_int), c_int, _P(Options), _P(c_void_p)]),
+    "wvg_multi_close": (c_int, [c_void_p]),
+    "wvg_multi_info": (c_int, [c_void_p, _P(c_int), _P(c_int)]),
+    "wvg_multi_ctx": (c_int, [c_void_p, c_int, _P(c_void_p)]),
+    "wvg_multi_corpus_create": (c_int, [c_void_p, c_int, c_int, c_uint32, c_uint64, _P(c_void_p)]),
+    "wvg_multi_corpus_destroy": (c_int, [c_void_p]),
+    "wvg_multi_corpus_shard": (c_int, [c_void_p, c_int, _P(c_void_p), _P(c_uint64), _P(c_uint64)]),
+    "wvg_multi_corpus_upsert": (c_int, [c_void_p, _P(c_uint64), _P(c_float), c_uint64, c_uint32]),
+    "wvg_multi_corpus_delete": (c_int, [c_void_p, _P(c_uint64), c_uint64]),
+    "wvg_multi_corpus_fill_synthetic": (c_int, [c_void_p, c_uint64, c_uint64, c_int]),
+    "wvg_multi_corpus_set_codebook": (c_int, [c_void_p, _P(c_float), c_uint32, c_uint32]),
+    "wvg_multi_search": (c_int, [c_void_p, _P(c_float), c_uint32, c_uint32, _P(c_uint64), c_uint64,
+                                 _P(c_uint64), _P(c_float), _P(c_uint32)]),
     "wvg_synthetic_rows": (c_int, [c_void_p, c_uint64, _P(c_uint64), c_uint64, c_uint32, c_int, c_int, _P(c_float)]),
     "wvg_profile_start": (c_int, [c_void_p]),
     "wvg_profile_stop": (c_int, [c_void_p, _P(ctypes.c_double), _P(c_uint64)]),

@@ -1,7 +1,9 @@
 """Device context and device-resident corpora (handles of the C ABI).
 
-One :class:`Context` per GPU; the multi-GPU deployment runs one process per
-GPU (see weaviate_amd/shard.py).
+One :class:`Context` per GPU.  Several GPUs serve one index either from one
+process (:class:`Multi` / :class:`MultiCorpus`: wvg_multi_*, RCCL inside the
+library) or with one process per GPU (weaviate_amd/shard.py, RCCL through
+torch.distributed).
 """
 from __future__ import annotations
 
@@ -281,3 +283,89 @@ def search_bq_rescore(bq: Corpus, f32: Corpus, queries, k: int, rescore_limit: i
                                        u64ptr(aw) if aw is not None else None, an,
                                        u64ptr(ids), fptr(dists), u32ptr(counts)))
     return ids, dists, counts
+
+
+class Multi:
+    """wvg_multi_open / wvg_multi_close: one context per device in this process
+    and, for distinct devices, an RCCL communicator per device."""
+
+    def __init__(self, devices, **options):
+        self.lib = _lib.load()
+        opts = _lib.Options()
+        self.lib.wvg_options_default(byref(opts))
+        for name, value in options.items():
+            if name == "size" or name not in dict(_lib.Options._fields_):
+                raise TypeError(f"unknown context option {name!r}")
+            setattr(opts, name, int(value))
+        devs = (c_int * len(devices))(*devices)
+        h = c_void_p()
+        check(self.lib.wvg_multi_open(devs, len(devices), byref(opts), byref(h)))
+        self.handle = h
+        nd, rc = c_int(), c_int()
+        check(self.lib.wvg_multi_info(h, byref(nd), byref(rc)))
+        self.ndev, self.uses_rccl = nd.value, bool(rc.value)
+
+    def close(self) -> None:
+        if self.handle:
+            check(self.lib.wvg_multi_close(self.handle))
+            self.handle = c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+class MultiCorpus:
+    """wvg_multi_corpus_*: docIDs dealt to the devices in contiguous slabs;
+    search = every slab's scan on its device, one RCCL all-gather, the merge."""
+
+    def __init__(self, multi: Multi, kind: int, metric: int, dim: int, rows: int):
+        self.multi, self.lib = multi, multi.lib
+        self.kind, self.metric, self.dim = kind, metric, dim
+        h = c_void_p()
+        check(self.lib.wvg_multi_corpus_create(multi.handle, kind, metric, dim, rows, byref(h)))
+        self.handle = h
+
+    def destroy(self) -> None:
+        if self.handle:
+            check(self.lib.wvg_multi_corpus_destroy(self.handle))
+            self.handle = c_void_p()
+
+    def shard(self, i: int):
+        """(wvg_corpus handle, id_base, slab rows) of shard i."""
+        h, base, slab = c_void_p(), c_uint64(), c_uint64()
+        check(self.lib.wvg_multi_corpus_shard(self.handle, i, byref(h), byref(base), byref(slab)))
+        return h, base.value, slab.value
+
+    def upsert(self, ids, vectors) -> None:
+        ids = np.ascontiguousarray(ids, dtype=np.uint64)
+        vectors = np.ascontiguousarray(vectors, dtype=np.float32).reshape(len(ids), -1)
+        check(self.lib.wvg_multi_corpus_upsert(self.handle, u64ptr(ids), fptr(vectors), len(ids),
+                                               vectors.shape[1] if vectors.size else self.dim))
+
+    def delete(self, ids) -> None:
+        ids = np.ascontiguousarray(ids, dtype=np.uint64)
+        check(self.lib.wvg_multi_corpus_delete(self.handle, u64ptr(ids), len(ids)))
+
+    def fill_synthetic(self, seed: int, n: int, distribution: int = 0) -> None:
+        check(self.lib.wvg_multi_corpus_fill_synthetic(self.handle, seed, n, distribution))
+
+    def set_codebook(self, centers) -> None:
+        centers = np.ascontiguousarray(centers, dtype=np.float32)
+        m, ks, _ = centers.shape
+        check(self.lib.wvg_multi_corpus_set_codebook(self.handle, fptr(centers), m, ks))
+
+    def search(self, queries, k: int, allow=None):
+        q = np.ascontiguousarray(queries, dtype=np.float32)
+        if q.ndim == 1:
+            q = q[None, :]
+        nq = q.shape[0]
+        ids = np.empty((nq, k), dtype=np.uint64)
+        dists = np.empty((nq, k), dtype=np.float32)
+        counts = np.empty(nq, dtype=np.uint32)
+        aw, an = (None, 0) if allow is None else (np.ascontiguousarray(allow, dtype=np.uint64), len(allow))
+        check(self.lib.wvg_multi_search(self.handle, fptr(q), nq, k, u64ptr(aw) if aw is not None else None, an,
+                                        u64ptr(ids), fptr(dists), u32ptr(counts)))
+        return ids, dists, counts
