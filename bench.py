@@ -62,7 +62,7 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--configs", default="host_api,batched,bq,pq,slab",
                     help="N = 1: BASELINE configs 2-5 measured after the headline (comma list; '' = none)")
-    ap.add_argument("--scale-legs", default="slab1b,pq",
+    ap.add_argument("--scale-legs", default="slab1b,pq,multi",
                     help="strong-scaling legs at every N (comma list; '' = none): slab1b = configs[4] 1B x 128 as 8 "
                          "slabs dealt to the N GPUs, pq = configs[3] 100M PQ sharded over the N GPUs")
     ap.add_argument("--s1b-rows", type=int, default=1_000_000_000, help="rows of the slab1b scale leg (tests: less)")
@@ -1137,6 +1137,10 @@ def run_flat1m(args, world, rank, dev, torch, dist):
                         legs["config5_1b_x_128"] = slab1b_leg(world, rank, dev, torch, dist, total=args.s1b_rows)
                 elif name == "pq":
                     legs["config4_pq_sharded"] = pq_sharded_leg(world, rank, dev, torch, dist, n=args.pq_rows)
+                elif name == "multi":
+                    r = multi_handle_leg(world, rank, dist)
+                    if rank == 0:
+                        legs["multi_gpu_one_process"] = r
             except Exception as e:  # noqa: BLE001 -- a failed leg is reported, the headline stands
                 legs[f"{name}_error"] = f"{type(e).__name__}: {e}"
             if rank == 0:
@@ -1197,6 +1201,51 @@ def sampled_check(total, per, S, d, k, qs, got_ids, got_d):
     return {"ok": bool(ok), "queries": len(qs), "rows": total, "sampled_rows": int(len(sids)),
             "how": "merged lists sorted, k distinct ids, every distance a bit-exact recomputation of its row, no "
                    f"row of {len(sids):,} sampled (start / middle / end of each slab) ahead of the k-th"}
+
+
+def multi_handle_leg(world, rank, dist, rows_per_gpu=1_000_000, d=128, k=10, B=16, calls=30):
+    """The single-process multi-GPU design at this N (wvg_multi_*): rank 0
+    opens all N GPUs of the job in ONE process -- one context and one RCCL
+    communicator per device (ncclCommInitAll) -- deals N x 1M x 128 rows to
+    them in docID slabs, and times host-API calls of B queries: per call every
+    device scans its slab, one grouped RCCL all-gather moves the packed top-k
+    blocks, device 0 merges (adapters/repos/db/index.go:1567-1648).  The other
+    ranks wait at a barrier.  Rank 0's merged results are checked against the
+    oracle over all N x 1M rows."""
+    from weaviate_amd._lib import KIND_F32, METRIC_L2
+    from weaviate_amd.device import Multi, MultiCorpus, device_count
+
+    out = None
+    if rank == 0:
+        if device_count() < world:
+            out = {"skipped": f"this process sees {device_count()} devices, fewer than {world}"}
+        else:
+            n = rows_per_gpu * world
+            qs = np.random.default_rng(47).uniform(-1, 1, (64, d)).astype(np.float32)
+            with Multi(list(range(world))) as m:
+                mc = MultiCorpus(m, KIND_F32, METRIC_L2, d, n)
+                try:
+                    mc.fill_synthetic(42, n, 0)
+                    for i in range(3):
+                        mc.search(qs[(i * B) % 64:(i * B) % 64 + B], k)
+                    t0 = time.perf_counter()
+                    for i in range(calls):
+                        q0 = (i * B) % 64
+                        gi, gd, gc = mc.search(qs[q0:q0 + B], k)
+                    wall = (time.perf_counter() - t0) / calls
+                    slab = mc.shard(0)[2]
+                    chk = merge_check([(s * slab, max(0, min(slab, n - s * slab))) for s in range(world)], d, k,
+                                      qs[q0:q0 + 2], gi[:2], gd[:2])
+                    out = {"workload": f"{world} x 1M x {d} fp32 L2 (docID slabs, one process), exact {k}-NN, "
+                                       f"{B} queries per wvg_multi_search call",
+                           "qps": round(B / wall, 1), "ms_per_call": round(wall * 1e3, 3), "ndev": m.ndev,
+                           "exchange": "RCCL all-gather (ncclCommInitAll)" if m.uses_rccl else "peer copies",
+                           "merge_check": chk}
+                finally:
+                    mc.destroy()
+    if world > 1:
+        dist.barrier()
+    return out
 
 
 def slab1b_leg(world, rank, dev, torch, dist, total=1_000_000_000, d=128, k=100, B=8, steps=2, W=1):

@@ -40,6 +40,8 @@ def test_flat_share_gpu_exchange_and_merge(gpus):
         assert legs["config5_1b_x_128"]["merge_check"]["ok"] is True, legs["config5_1b_x_128"]
     assert legs["config4_pq_sharded"]["merge_check"]["ok"] is True, legs["config4_pq_sharded"]
     assert legs["config4_pq_sharded"]["rows_per_gpu"] >= 400000 // gpus
+    # the one-process multi-GPU leg needs N devices in one process: skipped on a shared GPU
+    assert "skipped" in legs["multi_gpu_one_process"]
 
 
 @pytest.mark.parametrize("gpus", [1, 2])
