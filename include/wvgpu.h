@@ -230,7 +230,7 @@ int wvg_search_bq_rescore(wvg_corpus *bq, wvg_corpus *f32, const float *queries,
  * descending Hamming distance with the heap's own order among ties.  Outputs
  * [nq][R] ids / Hamming distances, counts[nq]; feed them in this order to
  * wvg_rescore (which inserts in input order, as :375-385 does).  With
- * heap_replay = 0: the lexicographic top-R, descending.  R <= 256.         */
+ * heap_replay = 0: the lexicographic top-R, descending.  Any R.           */
 int wvg_search_bq_candidates(wvg_corpus *bq, const float *queries, uint32_t nq, uint32_t rescore_limit,
                              const uint64_t *allow_bits, uint64_t allow_words, uint64_t *out_ids,
                              float *out_dists, uint32_t *out_counts);

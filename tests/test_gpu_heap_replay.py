@@ -90,7 +90,7 @@ def test_bq_candidates_heavy_ties_batches_allow_deletes(ctx, orc):
         b.upsert(np.arange(n, dtype=np.uint64), rows)
         codes = orc.bq_encode_rows(rows)
         qcodes = [orc.bq_encode(q) for q in qs]
-        for R in (1, 7, 64, 200, 256):
+        for R in (1, 7, 64, 200, 256, 257, 700, 3000):  # above 256: the select-based superset
             assert_pops(orc, b, qs, codes, qcodes, R)
             assert_pops(orc, b, qs[:1], codes, qcodes[:1], R)
         rng = np.random.default_rng(7)
@@ -99,6 +99,7 @@ def test_bq_candidates_heavy_ties_batches_allow_deletes(ctx, orc):
         valid = np.ones(n, np.uint8)
         valid[gone.astype(np.int64)] = 0
         assert_pops(orc, b, qs, codes, qcodes, 200, valid)
+        assert_pops(orc, b, qs[:2], codes, qcodes[:2], 500, valid)
         allowed = np.sort(rng.choice(n, int(n * 0.3), replace=False)).astype(np.uint64)
         bm = allow_bitmap(allowed, n)
         av = np.zeros(n, np.uint8)
@@ -127,6 +128,13 @@ def test_bq_rescore_integer_rows_ties_in_both_heaps(ctx, orc, metric):
     try:
         f.upsert(np.arange(n, dtype=np.uint64), rows)
         b.upsert(np.arange(n, dtype=np.uint64), rows)
+        for RR in (R, 600):  # 600: the select-based superset above 256
+            gi, gd, gc = search_bq_rescore(b, f, qs, k, RR)
+            for qi in range(len(qs)):
+                ri, rd = orc.flat_search_bq(rows, qs[qi], k, RR, ORC_METRIC[metric])
+                assert gc[qi] == len(ri)
+                assert np.array_equal(gi[qi], ri), (RR, qi, gi[qi], ri)
+                assert np.array_equal(bits(gd[qi]), bits(rd)), (RR, qi)
         gi, gd, gc = search_bq_rescore(b, f, qs, k, R)
         for qi in range(len(qs)):
             ri, rd = orc.flat_search_bq(rows, qs[qi], k, R, ORC_METRIC[metric])
@@ -161,7 +169,7 @@ def test_bq_candidates_overflow_rerun(ctx, orc):
         b.upsert_codes(np.arange(n, dtype=np.uint64), codes)
         q = np.ones((2, d), np.float32)  # code 0: distance = set bits
         qc = [np.zeros(w, np.uint64)] * 2
-        for R in (1, 4, 200):
+        for R in (1, 4, 200, 600):
             assert_pops(orc, b, q, codes, qc, R)
             assert_pops(orc, b, q[:1], codes, qc[:1], R)
     finally:

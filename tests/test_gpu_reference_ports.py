@@ -215,7 +215,7 @@ def test_flat_from_user_config_and_rescore_update(ctx, orc):
             idx.UpdateUserConfig(upd)
         assert idx.searchTimeRescore(k) == R
         ids, dists = idx.SearchByVector(q, k)
-        cand, _ = orc.lex_topk(ham, np.arange(n, dtype=np.uint64), R)
-        li, ld = orc.lex_topk(exact[cand.astype(np.int64)], cand, k)
+        cand, _ = orc.heap_pops(ham, R)  # the reference's Hamming heap, in pop order
+        li, ld = orc.heap_topk(exact[cand.astype(np.int64)], cand, k)
         assert np.array_equal(ids, li)
         assert np.array_equal(dists.view(np.uint32), ld.view(np.uint32))

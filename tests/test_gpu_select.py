@@ -111,11 +111,11 @@ def test_bq_rescore_window_above_256(ctx, orc, metric):
     srows, qn = _prep(orc, metric, rows, q)
     codes = np.stack([orc.bq_encode(r) for r in srows])
     ham = orc.bq_dist_all(orc.bq_encode(qn), codes)
-    cand, _ = orc.lex_topk(ham, np.arange(n, dtype=np.uint64), rescore)
+    cand, _ = orc.heap_pops(ham, rescore)  # the reference's Hamming heap of 700, in pop order
     exact = orc.dist_all(ORC_METRIC[metric], qn, srows[cand.astype(np.int64)])
     for kk in [k, 300]:
         ids, dists, counts = search_bq_rescore(b, f, q, kk, rescore)
-        li, ld = orc.lex_topk(exact, cand, kk)
+        li, ld = orc.heap_topk(exact, cand, kk)
         assert counts[0] == kk
         assert np.array_equal(ids[0], li) and np.array_equal(bits(dists[0]), bits(ld))
 

@@ -229,7 +229,13 @@ size_t replay_workspace_bytes(const wvg_corpus *bq, uint32_t nq, uint32_t R, con
 // for nq prepared BQ queries: pops[q] = (slot, Hamming distance) in pop order.
 int bq_heap_candidates(wvg_corpus *bq, StreamSlot *sl, const void *d_qb, uint32_t qpb, uint32_t nq, uint32_t R,
                        const uint64_t *d_allow, const SearchPlan &p, char *ws, std::vector<std::vector<GoItem>> &pops);
-// searchByVectorBQ exactly (R <= MAX_K): the candidates above, their exact
+// The same for windows above MAX_K (wvg_range.hip): S1 keys, doubling chunks
+// with prefix-select thresholds, compaction, sort, the host heap.
+size_t select_replay_bytes(const SearchPlan &p);
+int bq_heap_candidates_select(wvg_corpus *bq, StreamSlot *sl, const void *d_qb, uint32_t qpb, uint32_t nq,
+                              uint32_t R, const uint64_t *d_allow, const SearchPlan &p, char *ws,
+                              std::vector<std::vector<GoItem>> &pops);
+// searchByVectorBQ exactly (any R): the candidates above, their exact
 // distances on the device, the k-heap in pop order on the host.  f32 null:
 // outputs are the candidates themselves ([nq][R], pop order).
 int bq_rescore_replay(wvg_corpus *bq, wvg_corpus *f32, const float *queries, uint32_t nq, uint32_t k, uint32_t R,

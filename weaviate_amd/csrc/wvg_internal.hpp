@@ -304,7 +304,7 @@ struct StreamJob {
     float *dists;
     uint32_t *counts;
     // Single host queries: the results go to host memory as tagged 16-byte records
-    // [nq][k + 1] (entries {id lo, id hi, dist, tag}, then the header {count, tag}),
+    // [nq][k + 1] (entries {slot, tag, dist, tag} -- the host adds id_base -- then the header {count, tag}),
     // ids / dists / counts unused.  GPU writes to host memory can become visible
     // out of order (a later header before earlier entries), so the host accepts a
     // result only when the header AND every entry carry its call's tag.
@@ -585,6 +585,11 @@ hipError_t launch_key_count(const uint32_t *keys, uint64_t n, uint32_t t_le, uin
 hipError_t launch_key_compact(const uint32_t *keys, uint64_t n, const void *st_dev, uint32_t thr,
                               uint32_t slot0, int num_cus, uint64_t *out, unsigned long long *count,
                               hipStream_t s);
+hipError_t read_select_kth(const void *st_dev, uint32_t *kth, hipStream_t s);  // synchronizes s
+// The heap replay's superset above 256 (key_compact_chunks_kernel): slot i of
+// chunk j kept iff keys[i] < thr[j]; out (slot << 32 | key), unordered.
+hipError_t launch_key_compact_chunks(const uint32_t *keys, uint64_t n, const uint32_t *thr, uint64_t R, uint32_t slot0,
+                                     int num_cus, uint64_t *out, unsigned long long *count, hipStream_t s);
 size_t sort_temp_bytes(uint64_t n);
 hipError_t sort_keys64(void *temp, size_t temp_bytes, const uint64_t *in, uint64_t *out, uint64_t n,
                        hipStream_t s);

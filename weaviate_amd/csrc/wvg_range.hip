@@ -212,6 +212,82 @@ int bq_rescore_large(wvg_corpus *bq, wvg_corpus *f32, const float *queries, uint
     return WVG_OK;
 }
 
+// findTopVectorsCached's heap of R > 256 and its pop order (V/flat/index.go:
+// 355-374), exactly (the heap replay of wvg_replay.hip for windows the scan's
+// register top-k cannot hold): S1 keys of every slot; chunks of the slot
+// window doubling from R (chunk 0 = [0, R), chunk j = [R 2^(j-1), R 2^j)), each
+// with thr[j] = the R-th smallest key before it (a radix select over the
+// prefix; no threshold while fewer than R live rows precede); the slots of
+// chunk j below thr[j] are a superset of the rows the heap inserts there
+// (about R per chunk, R (1 + log2(rows / R)) in all), compacted, sorted into
+// docID order, copied back and replayed through the heap on the host.
+size_t select_replay_bytes(const SearchPlan &p)
+{
+    const uint64_t nslots = (p.te - p.tb) * 64;
+    Carver cv;
+    size_t o[6], temp_bytes = 0;
+    SelectBufs::layout(cv, nslots, o, temp_bytes);
+    cv.take(temp_bytes);
+    cv.take(65 * 4);
+    return cv.off;
+}
+
+int bq_heap_candidates_select(wvg_corpus *bq, StreamSlot *sl, const void *d_qb, uint32_t qpb, uint32_t nq,
+                              uint32_t R, const uint64_t *d_allow, const SearchPlan &p, char *ws,
+                              std::vector<std::vector<GoItem>> &pops)
+{
+    hipStream_t s = sl->stream;
+    const int cus = bq->ctx->num_cus;
+    const uint64_t nslots = (p.te - p.tb) * 64;
+    Carver cv;
+    size_t o_sel[6], temp_bytes = 0;
+    SelectBufs::layout(cv, nslots, o_sel, temp_bytes);
+    const size_t o_temp = cv.take(temp_bytes), o_thr = cv.take(65 * 4);
+    SelectBufs sb;
+    sb.bind(ws, o_sel, o_temp, temp_bytes);
+    uint32_t *d_thr = (uint32_t *)(ws + o_thr);
+    pops.assign(nq, {});
+    std::vector<uint64_t> keys;
+    for (uint32_t qi = 0; qi < nq; qi++) {
+        ScanArgs a1 = scan_args_for(bq, (const uint64_t *)d_qb + (size_t)qi * qpb, qpb, 1, R, d_allow, p.tb, p.te);
+        WVG_HIP(launch_ordkeys(a1, bq->kind, cus, sb.keys, s));
+        uint32_t thr[65];
+        thr[0] = 0xFFFFFFFFu;  // chunk 0: no row precedes -- keep every live one
+        bool enough = false;   // R live rows precede the chunk (then for every later chunk too)
+        int J = 1;
+        for (; J < 64 && ((uint64_t)R << (J - 1)) < nslots; J++) {
+            const uint64_t b = (uint64_t)R << (J - 1);
+            if (!enough) {
+                WVG_HIP(launch_key_count(sb.keys, b, 0u, 0u, cus, sb.cnt, s));
+                unsigned long long cnt[3] = {0, 0, 0};
+                WVG_HIP(hipMemcpyAsync(cnt, sb.cnt, sizeof(cnt), hipMemcpyDeviceToHost, s));
+                WVG_HIP(hipStreamSynchronize(s));
+                enough = cnt[2] >= R;
+            }
+            thr[J] = 0xFFFFFFFFu;
+            if (enough) {
+                WVG_HIP(launch_select_kth(sb.keys, b, R, cus, sb.st, sb.hist, s));
+                WVG_HIP(read_select_kth(sb.st, &thr[J], s));
+            }
+        }
+        WVG_HIP(hipMemcpyAsync(d_thr, thr, (size_t)J * 4, hipMemcpyHostToDevice, s));
+        WVG_HIP(launch_key_compact_chunks(sb.keys, nslots, d_thr, R, (uint32_t)(p.tb * 64), cus, sb.cmp, sb.cnt, s));
+        unsigned long long n = 0;
+        WVG_HIP(hipMemcpyAsync(&n, sb.cnt, 8, hipMemcpyDeviceToHost, s));
+        WVG_HIP(hipStreamSynchronize(s));  // (also keeps `thr` alive until its copy is done)
+        WVG_HIP(sort_keys64(sb.temp, sb.temp_bytes, sb.cmp, sb.sorted, n, s));
+        keys.resize(n);
+        if (n) WVG_HIP(hipMemcpyAsync(keys.data(), sb.sorted, n * 8, hipMemcpyDeviceToHost, s));
+        WVG_HIP(hipStreamSynchronize(s));
+        GoMaxHeap h(R);
+        for (uint64_t i = 0; i < n; i++)
+            insert_to_heap(h, R, (uint32_t)(keys[i] >> 32), wvg_unord_f32((uint32_t)keys[i]));
+        pops[qi].reserve(h.len());
+        while (h.len()) pops[qi].push_back(h.pop());
+    }
+    return WVG_OK;
+}
+
 // How many of the ascending results SearchByVectorDistance returns, given
 // p_le = #rows with dist <= target, p_q = #rows kept by the threshold test
 // (dist <= target || InDelta 1e-6), live = #rows.  Restates the growing-limit

@@ -460,7 +460,8 @@ int bq_rescore_replay(wvg_corpus *bq, wvg_corpus *f32, const float *queries, uin
     const size_t o_qb = cv.take(query_bytes(bq, nq));
     const size_t o_qf = cv.take(f32 ? (size_t)nq * fpitch * 4 : 0);
     const size_t o_allow = cv.take(p.allow_bytes());
-    const size_t o_rep = cv.take(replay_workspace_bytes(bq, nq, R, p));
+    const bool large = R > MAX_K;  // beyond the scan's register top-k: the select-based superset
+    const size_t o_rep = cv.take(large ? select_replay_bytes(p) : replay_workspace_bytes(bq, nq, R, p));
     const size_t o_cand = cv.take(f32 ? (size_t)nq * R * 8 : 0);
     const size_t o_resc = cv.take(f32 ? (size_t)nq * R * 8 : 0);
     void *base = nullptr;
@@ -481,7 +482,8 @@ int bq_rescore_replay(wvg_corpus *bq, wvg_corpus *f32, const float *queries, uin
         d_allow = (const uint64_t *)(b + o_allow);
     }
     std::vector<std::vector<GoItem>> pops;
-    rc = bq_heap_candidates(bq, g.slot, b + o_qb, qpb, nq, R, d_allow, p, b + o_rep, pops);
+    rc = large ? bq_heap_candidates_select(bq, g.slot, b + o_qb, qpb, nq, R, d_allow, p, b + o_rep, pops)
+               : bq_heap_candidates(bq, g.slot, b + o_qb, qpb, nq, R, d_allow, p, b + o_rep, pops);
     if (rc) return rc;
     if (!f32) {  // the candidates themselves, in pop order
         for (uint32_t q = 0; q < nq; q++) {

@@ -11,6 +11,8 @@
 // wave's register top-k.  The workgroup merges its waves' lists in LDS and
 // writes K keys per (query, workgroup).  Phase 2 merges those lists.
 // Roofline: HBM, N*d*4 bytes per query.
+#include <type_traits>
+
 #include "wvg_internal.hpp"
 #include "wvg_rowdist.hpp"
 #include "wvg_topk.hpp"
@@ -140,8 +142,8 @@ __device__ __forceinline__ void merge_finish(WaveTopK<E> &tk, uint32_t k, uint64
         if (i < k) {
             const uint64_t id = live ? id_base + (key & 0xFFFFFFFFull) : WVG_KEY_NONE;
             const float dv = live ? wvg_unord_f32((uint32_t)(key >> 32)) : __builtin_inff();
-            if (rec)
-                rec[i] = make_uint4((uint32_t)id, (uint32_t)(id >> 32), __float_as_uint(dv), tag);
+            if (rec)  // {slot, tag, dist, tag}: each 8-byte half carries the tag (the host adds id_base)
+                rec[i] = make_uint4(live ? (uint32_t)key : 0xFFFFFFFFu, tag, __float_as_uint(dv), tag);
             else {
                 ids[i] = id;
                 dists[i] = dv;
@@ -316,6 +318,18 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_kernel(ScanArgs a, u
     group_combine_store<E, SCAN_WAVES>(tk, partials + ((size_t)qi * G + rng) * a.k);
 }
 
+// K1Q's per-query tile masks: the validity word, and with FILT each query's own
+// allow word (a function, not a lambda: an out-of-line lambda once moved a
+// kernel's arguments to scratch).
+template <int Q, bool FILT>
+__device__ __forceinline__ void mq_tile_masks(const ScanArgs &a, uint64_t t, const uint32_t (&qix)[Q],
+                                              uint64_t (&mq)[Q])
+{
+    const uint64_t v = a.valid[t];
+#pragma unroll
+    for (int j = 0; j < Q; j++) mq[j] = FILT ? tile_mask(a, t, qix[j]) : v;
+}
+
 // K1Q (round 5): co-scheduled small batches with Q queries per workgroup.  The
 // COS grid gives each (row range, query) its own workgroup; the nq workgroups of a
 // range read the same rows side by side, so every row crosses from L2 to the CUs
@@ -323,9 +337,11 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_kernel(ScanArgs a, u
 // ~2 ms).  Here a wave loads each 32-float block of its row once and folds it into
 // the Q queries' AVX2-order chains (acc[Q][4][8]: every query's distance is the
 // same chain as a scan of its own, so results are bit-identical), then offers each
-// query its key: a quarter of the L2 traffic at Q = 4.  Unfiltered batches only
-// (every query's tile mask is the validity word), L2 / dot / cosine, fixed D.
-template <int METRIC, int D, int E, int Q>
+// query its key: a quarter of the L2 traffic at Q = 4.  L2 / dot / cosine, fixed D.
+// FILT (round 6): coalesced filtered single queries, each with its own allow
+// window (ScanArgs::allow_qstride): a tile is loaded if any of the Q queries
+// may see a row of it, every query offers only its own rows.
+template <int METRIC, int D, int E, int Q, bool FILT = false>
 __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_mq_kernel(ScanArgs a, uint64_t *partials)
 {
     static_assert(D % 32 == 0 && D > 0 && !is_abs_or_neq<METRIC>, "K1Q: fixed D, the AVX2 chains");
@@ -338,10 +354,11 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_mq_kernel(ScanArgs a
     const uint64_t t0 = a.tile_begin + ntiles * gw / total, t1 = a.tile_begin + ntiles * (gw + 1) / total;
     const int lane = threadIdx.x & 63;
     const float4 *q4[Q];
+    uint32_t qix[Q];
 #pragma unroll
     for (int j = 0; j < Q; j++) {  // (a short last group repeats its last query and stores nothing for it)
-        const uint32_t qi = qg * Q + j < a.nq ? qg * Q + j : a.nq - 1;
-        q4[j] = reinterpret_cast<const float4 *>(a.queries) + (size_t)qi * (a.qpitch / 4);
+        qix[j] = qg * Q + j < a.nq ? qg * Q + j : a.nq - 1;
+        q4[j] = reinterpret_cast<const float4 *>(a.queries) + (size_t)qix[j] * (a.qpitch / 4);
     }
     WaveTopK<E> tk[Q];
 #pragma unroll
@@ -349,11 +366,19 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_mq_kernel(ScanArgs a
     const float4 *data = reinterpret_cast<const float4 *>(a.data);
     const bool rev = (a.reverse & 1u) != 0;
     const uint64_t n = t1 - t0;
-    uint64_t m_next = n ? a.valid[rev ? t1 - 1 : t0] : 0ull;
+    // per-query tile masks (scalar; the next tile's prefetched): the validity word, and with
+    // FILT each query's own allow word
+    uint64_t mq_next[Q];
+    if (n) mq_tile_masks<Q, FILT>(a, rev ? t1 - 1 : t0, qix, mq_next);
     for (uint64_t i = 0; i < n; ++i) {
         const uint64_t t = rev ? t1 - 1 - i : t0 + i;
-        const uint64_t m = m_next;
-        if (i + 1 < n) m_next = a.valid[rev ? t - 1 : t + 1];  // scalar prefetch of the next mask
+        uint64_t mq[Q];
+#pragma unroll
+        for (int j = 0; j < Q; j++) mq[j] = mq_next[j];
+        if (i + 1 < n) mq_tile_masks<Q, FILT>(a, rev ? t - 1 : t + 1, qix, mq_next);
+        uint64_t m = 0ull;
+#pragma unroll
+        for (int j = 0; j < Q; j++) m |= mq[j];
         if (m == 0ull) continue;
         const float4 *rp = data + (size_t)t * a.nchunks * 64 + lane;
         float acc[Q][4][8];
@@ -376,7 +401,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_mq_kernel(ScanArgs a
         }
 #pragma unroll
         for (int j = 0; j < Q; j++)
-            tk[j].offer(lane_key(m, wrap_metric(a.metric, avx256_reduce(acc[j], 0.0f)), t, lane));
+            tk[j].offer(lane_key(mq[j], wrap_metric(a.metric, avx256_reduce(acc[j], 0.0f)), t, lane));
     }
 #pragma unroll
     for (int j = 0; j < Q; j++) {
@@ -537,7 +562,7 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_stream_kernel(ScanAr
                     for (uint32_t qq = q; qq < a.nq; qq++) {
                         uint4 *r = j.records + (size_t)qq * (a.k + 1);
                         for (uint32_t i = threadIdx.x; i < a.k; i += blockDim.x)
-                            r[i] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0x7F800000u, j.tag);
+                            r[i] = make_uint4(0xFFFFFFFFu, j.tag, 0x7F800000u, j.tag);
                         __syncthreads();
                         if (threadIdx.x == 0)
                             __hip_atomic_store(reinterpret_cast<uint64_t *>(r + a.k),
@@ -756,19 +781,26 @@ template <int METRIC, int E>
 static hipError_t launch_f32_e(const ScanArgs &a, uint64_t *partials, int groups, hipStream_t s)
 {
     if constexpr (!is_abs_or_neq<METRIC>) {
-        // K1Q: ScanArgs::cosched = Q >= 2 queries per workgroup (plan_search sets it for unfiltered
-        // L2 / dot / cosine batches at d = 128 / 768; groups = its row ranges)
-        if ((a.cosched == 2 || a.cosched == 4) && a.nq > 1 && groups % 8 == 0 && !a.side.active && !a.allow &&
-            !a.order512 && (a.dim == 128 || a.dim == 768)) {
+        // K1Q: ScanArgs::cosched = Q >= 2 queries per workgroup (plan_search sets it for L2 / dot /
+        // cosine batches at d = 128 / 768 without a shared allow window; groups = its row ranges);
+        // coalesced filtered queries (per-query windows, allow_qstride) take the FILT variant
+        const bool filt = a.allow && a.allow_qstride;
+        if ((a.cosched == 2 || a.cosched == 4) && a.nq > 1 && groups % 8 == 0 && !a.side.active &&
+            (!a.allow || filt) && !a.order512 && (a.dim == 128 || a.dim == 768)) {
             const uint32_t nqg = (a.nq + (uint32_t)a.cosched - 1) / (uint32_t)a.cosched;
             dim3 grid((unsigned)groups * nqg), block(SCAN_WAVES * 64);
-            if (a.cosched == 4) {
-                if (a.dim == 128) launch_timed((scan_f32_mq_kernel<METRIC, 128, E, 4>), grid, block, 0, s, a, partials);
-                else launch_timed((scan_f32_mq_kernel<METRIC, 768, E, 4>), grid, block, 0, s, a, partials);
-            } else {
-                if (a.dim == 128) launch_timed((scan_f32_mq_kernel<METRIC, 128, E, 2>), grid, block, 0, s, a, partials);
-                else launch_timed((scan_f32_mq_kernel<METRIC, 768, E, 2>), grid, block, 0, s, a, partials);
-            }
+            auto go = [&](auto fq) {
+                constexpr bool F = decltype(fq)::value;
+                if (a.cosched == 4) {
+                    if (a.dim == 128) launch_timed((scan_f32_mq_kernel<METRIC, 128, E, 4, F>), grid, block, 0, s, a, partials);
+                    else launch_timed((scan_f32_mq_kernel<METRIC, 768, E, 4, F>), grid, block, 0, s, a, partials);
+                } else {
+                    if (a.dim == 128) launch_timed((scan_f32_mq_kernel<METRIC, 128, E, 2, F>), grid, block, 0, s, a, partials);
+                    else launch_timed((scan_f32_mq_kernel<METRIC, 768, E, 2, F>), grid, block, 0, s, a, partials);
+                }
+            };
+            if (filt) go(std::true_type{});
+            else go(std::false_type{});
             return hipGetLastError();
         }
     }

@@ -611,8 +611,12 @@ inline void coalesce_counter(size_t, uint64_t) {}
 // round-4 layout (ids / dists, a system-scope release, then a count the host
 // polled) returned the slot's PREVIOUS result in ~1 of 1000 concurrent calls
 // (profiles/r04/single_query_stress/, profiles/r05/single_query/): the count had
-// landed, the ids of this call not yet.  Checking a tag in every 16-byte entry
-// makes acceptance independent of the arrival order.  sync: synchronize the
+// landed, the ids of this call not yet.  Checking the tag in every entry makes
+// acceptance independent of the arrival order.  An entry is {slot, tag, dist,
+// tag} (the slot, not the 64-bit docID: id_base is the host's), so BOTH 8-byte
+// halves carry the tag and acceptance does not assume that a 16-byte store
+// reaches host memory as one unit -- only that an aligned 8-byte one does (a
+// single PCIe / xGMI write of it is never split).  sync: synchronize the
 // stream first (tools A/B); a poll that has not seen the tags after 50 ms (long
 // scans, a fault) synchronizes too, and the tags must then arrive within 1 s.
 static int wait_records(const SingleOut &so, uint32_t k, hipStream_t s, bool sync)
@@ -622,7 +626,7 @@ static int wait_records(const SingleOut &so, uint32_t k, hipStream_t s, bool syn
     auto landed = [&]() {
         if (w[4 * k + 1] != so.tag) return false;
         for (uint32_t i = 0; i < k; i++)
-            if (w[4 * i + 3] != so.tag) {
+            if (w[4 * i + 1] != so.tag || w[4 * i + 3] != so.tag) {
                 early = true;
                 return false;
             }
@@ -930,7 +934,7 @@ static int wvg::search_batch(wvg_corpus *c, const float *queries, uint32_t nq, u
         WVG_STAMP(3);
         const uint4 *r = so.records;
         for (uint32_t i = 0; i < k; i++) {
-            if (out_ids) out_ids[i] = (uint64_t)r[i].x | (uint64_t)r[i].y << 32;
+            if (out_ids) out_ids[i] = r[i].x == 0xFFFFFFFFu ? WVG_KEY_NONE : c->id_base + r[i].x;
             if (out_dists) std::memcpy(out_dists + i, &r[i].z, 4);
         }
 #ifdef WVG_TOOLS
@@ -1014,7 +1018,8 @@ static int wvg::search_batch_filtered(wvg_corpus *c, const std::vector<wvg_searc
     std::vector<uint64_t> win((size_t)B * W, 0ull);  // query i's allow words of tiles [TB, TE) (0 outside its own)
     for (uint32_t i = 0; i < B; i++)
         if (live[i]) std::memcpy(win.data() + (size_t)i * W + (tb[i] - TB), batch[i]->allow + wb + tb[i], (te[i] - tb[i]) * 8);
-    SearchPlan p = plan_search(c, B, k, nullptr, 0, false, false);  // per-query allow windows: the COS K1
+    // per-query allow windows: K1Q's filtered variant (d = 128 / 768, L2 / dot / cosine) or the COS K1
+    SearchPlan p = plan_search(c, B, k, nullptr, 0, true, false);
     if (p.empty) return WVG_OK;
     if (p.gemm || !p.cosched) return fail(WVG_ERR_INVALID, "filtered coalesced batch needs the co-scheduled K1");
     p.tb = TB;
@@ -1080,11 +1085,11 @@ int wvg_search_bq_rescore(wvg_corpus *bq, wvg_corpus *f32, const float *queries,
         write_empty(nq, k, out_ids, out_dists, out_counts);
         return WVG_OK;
     }
+    if (bq->ctx->opt.heap_replay)  // the reference heaps' exact result (wvg_replay.hip), any R
+        return bq_rescore_replay(bq, f32, queries, nq, k, R, p, out_ids, out_dists, out_counts);
     if (R > MAX_K)
         return bq_rescore_large(bq, f32, queries, nq, k, R, allow_bits, allow_words, p, out_ids, out_dists,
                                 out_counts);
-    if (bq->ctx->opt.heap_replay)  // the reference heaps' exact result (wvg_replay.hip)
-        return bq_rescore_replay(bq, f32, queries, nq, k, R, p, out_ids, out_dists, out_counts);
     SlotGuard g(bq->ctx);
     rc = bq->ctx->acquire(&g.slot);
     if (rc) return rc;
@@ -1160,7 +1165,6 @@ int wvg_search_bq_candidates(wvg_corpus *bq, const float *queries, uint32_t nq, 
     if (bq->kind != WVG_KIND_BQ) return fail(WVG_ERR_INVALID, "need a BQ corpus");
     if (nq > 0 && !queries) return fail(WVG_ERR_INVALID, "null queries");
     const uint32_t R = rescore_limit;
-    if (R > MAX_K) return fail(WVG_ERR_UNSUPPORTED, "rescore_limit above 256");
     if (!bq->ctx->opt.heap_replay) {  // the lexicographic top-R, in pop (descending) order
         rc = wvg_search(bq, queries, nq, R, allow_bits, allow_words, out_ids, out_dists, out_counts);
         if (rc) return rc;
@@ -1172,8 +1176,8 @@ int wvg_search_bq_candidates(wvg_corpus *bq, const float *queries, uint32_t nq, 
         return WVG_OK;
     }
     std::shared_lock<std::shared_mutex> lk(bq->rw);
-    SearchPlan p = plan_search(bq, nq, R, allow_bits, allow_words);
-    if (p.empty) {
+    SearchPlan p = plan_search(bq, nq, std::min(R, MAX_K), allow_bits, allow_words);
+    if (p.empty || R == 0) {
         write_empty(nq, R, out_ids, out_dists, out_counts);
         return WVG_OK;
     }

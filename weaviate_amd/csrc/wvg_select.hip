@@ -300,6 +300,44 @@ hipError_t launch_key_compact(const uint32_t *keys, uint64_t n, const void *st_d
     return hipGetLastError();
 }
 
+// The heap replay's superset for windows above 256 (wvg_range.hip,
+// bq_heap_candidates_select): slot i of chunk j (chunk 0 = [0, R), chunk j >= 1
+// = [R 2^(j-1), R 2^j)) is kept iff its key is below thr[j], the R-th smallest
+// key of every slot before the chunk (ORD_NONE: fewer than R rows precede, keep
+// all) -- a row the reference heap inserts is below the R-th of ITS prefix,
+// which is at most thr[j].  Output (slot << 32 | key): sorted, docID order.
+__global__ __launch_bounds__(256) void key_compact_chunks_kernel(const uint32_t *keys, uint64_t n, const uint32_t *thr,
+                                                                 uint64_t R, uint32_t slot0, uint64_t *out,
+                                                                 unsigned long long *count)
+{
+    const int lane = threadIdx.x & 63;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t base0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u);
+    for (uint64_t base = base0; base < n; base += stride) {
+        const uint64_t i = base + lane;
+        const uint32_t k = i < n ? keys[i] : ORD_NONE;
+        const uint32_t j = i < R ? 0u : 64u - (uint32_t)__clzll((unsigned long long)(i / R));
+        const bool take = k != ORD_NONE && k < thr[j];
+        const uint64_t m = __ballot(take);
+        if (m == 0ull) continue;
+        unsigned long long pos = 0;
+        if (lane == 0) pos = atomicAdd(count, (unsigned long long)__popcll(m));
+        pos = __shfl(pos, 0, 64);
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (take) out[pos + below] = ((uint64_t)(slot0 + (uint32_t)i) << 32) | k;
+    }
+}
+
+hipError_t launch_key_compact_chunks(const uint32_t *keys, uint64_t n, const uint32_t *thr, uint64_t R, uint32_t slot0,
+                                     int num_cus, uint64_t *out, unsigned long long *count, hipStream_t s)
+{
+    hipError_t e = hipMemsetAsync(count, 0, 8, s);
+    if (e != hipSuccess || n == 0) return e;
+    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, (uint64_t)num_cus * 8));
+    hipLaunchKernelGGL(key_compact_chunks_kernel, dim3(grid), dim3(256), 0, s, keys, n, thr, R, slot0, out, count);
+    return hipGetLastError();
+}
+
 // ---- S4: sort + emit ----------------------------------------------------------
 size_t sort_temp_bytes(uint64_t n)
 {
