@@ -172,7 +172,7 @@ type Options struct {
 	MFMAMinQueries uint32 // dot / cosine batches of at least this many queries use MFMA (default 32)
 	CacheReuse     int32  // 1: consecutive scans reuse the Infinity Cache (default); 0: streaming
 	MergeWaitUs    uint32 // query-stream merge wait bound (default 4 s)
-	BatchScreen    int32  // 1: bf16 screen + exact rescore for batches (default); 0: exact fp32 MFMA only
+	BatchScreen    int32  // 2: int8 screen (d 512/768/1024, else bf16) + exact rescore (default); 1: bf16; 0: exact only
 	Coalesce       int32  // 1: concurrent single-query searches of a corpus share launches (default)
 	HeapReplay     int32  // 1: BQ candidates / rescore exactly as Weaviate's heaps pick them (default)
 }

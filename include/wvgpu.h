@@ -81,12 +81,15 @@ typedef struct wvg_options {
     uint32_t merge_wait_us;    /* bound on the in-launch merge's wait for one query's scan workgroups
                                   (wvg_search_device_pipelined); 0 = the default, 4 s.  On expiry the
                                   query gets empty results and wvg_search_device_check fails. */
-    int32_t batch_screen;      /* 1 (default): batched dot / cosine searches screen every row with bf16
-                                  MFMA and a per-row error bound, then rescore the candidates exactly in
-                                  fp32 (results identical to the exact path); 0: exact fp32 MFMA only.
-                                  The first screened search of a corpus allocates its bf16 shadow:
-                                  2 * dim bytes per row of capacity + 4 bytes of row-norm bound per row
-                                  (15.4 GB at 10M x 768), kept until the corpus is destroyed or grows. */
+    int32_t batch_screen;      /* 2 (default): batched dot / cosine searches screen every row with int8
+                                  MFMA (d = 512 / 768 / 1024; other d: bf16) and a per-row error bound,
+                                  then rescore the candidates exactly in fp32 (results identical to the
+                                  exact path); 1: the bf16 screen for every d; 0: exact fp32 MFMA only.
+                                  The first screened search of a corpus allocates its shadow: int8 = dim
+                                  + 8 bytes per row of capacity (7.7 GB at 10M x 768; its first build
+                                  also takes one pass over the rows for the corpus scale and one host
+                                  wait), bf16 = 2 * dim + 4 bytes per row (15.4 GB), kept until the
+                                  corpus is destroyed or grows. */
     int32_t coalesce;          /* 1 (default): concurrent single-query wvg_search calls on one corpus
                                   join one batched launch -- while a batch runs, the calls that arrive
                                   queue up and the next batch takes them all (filtered calls, each with its
@@ -263,7 +266,7 @@ int wvg_search_by_distance_window(wvg_corpus *c, const float *query, float targe
  * allocation (caller supplies a workspace of wvg_search_workspace_size bytes,
  * zero-filled once before its first use), so a call can be captured in a
  * hipGraph.  Exception: the first screened dot / cosine batch of a corpus
- * (batch_screen) allocates and builds the corpus's bf16 shadow on `stream`;
+ * (batch_screen) allocates and builds the corpus's shadow on `stream`;
  * under capture that never happens -- a corpus without a current shadow takes
  * the exact path, one with a shadow waits for it before the capture (run one
  * uncaptured batch first to warm it).  d_counts may be NULL.  One workspace

@@ -84,7 +84,7 @@ def test_options_struct_matches_library():
     o = _lib.Options()
     lib.wvg_options_default(ct.byref(o))
     assert o.size == ct.sizeof(_lib.Options)
-    assert (o.mfma_min_queries, o.cache_reuse, o.merge_wait_us, o.batch_screen, o.coalesce) == (32, 1, 0, 1, 1)
+    assert (o.mfma_min_queries, o.cache_reuse, o.merge_wait_us, o.batch_screen, o.coalesce) == (32, 1, 0, 2, 1)
     bad = _lib.Options()
     lib.wvg_options_default(ct.byref(bad))
     bad.size = 3

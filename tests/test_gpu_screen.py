@@ -1,6 +1,7 @@
-"""K3c -- the bf16 MFMA screen with a per-row error bound + the exact fp32
-rescore of every row the bound cannot rule out (weaviate_amd/csrc/wvg_screen.hip)
--- returns exactly what the exact path returns: the same ids, the same
+"""K3c / K3d -- the bf16 MFMA screen -- and K3i -- the int8 MFMA screen (the
+default for d = 512 / 768 / 1024, wvg_options.batch_screen = 2) -- each with a
+per-row error bound + the exact fp32 rescore of every row the bound cannot rule
+out (weaviate_amd/csrc/wvg_screen.hip) -- return exactly what the exact path returns: the same ids, the same
 distance bits, the same counts, for batched dot and cosine searches
 (Q flat.searchByVector calls, V/flat/index.go:319; SingleDist = dot_256,
 D/dot_product.go:68-98, D/cosine_dist.go:38-68).  The exact path here is a
@@ -21,6 +22,13 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(scope="module")
 def exact_ctx(ctx):
     c = Context(0, batch_screen=0)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def bf16_ctx(ctx):
+    c = Context(0, batch_screen=1)  # the bf16 screen (K3c / K3d) for every d
     yield c
     c.close()
 
@@ -232,6 +240,88 @@ def test_screen_device_path(ctx, exact_ctx, orc):
         ei, ed, _ = b.search(raw, k)
         assert np.array_equal(oi.cpu().numpy().view(np.uint64), ei)
         assert np.array_equal(od.cpu().numpy().view(np.uint32), ed.view(np.uint32))
+    finally:
+        a.destroy()
+        b.destroy()
+
+
+@pytest.mark.parametrize("d", [512, 768, 1024])
+@pytest.mark.parametrize("metric", [METRIC_COSINE, METRIC_DOT])
+def test_screen_int8_and_bf16_equal_exact(ctx, bf16_ctx, exact_ctx, orc, metric, d):
+    """The int8 screen (default context) and the bf16 one (batch_screen = 1) on
+    the same rows: both bit-identical to the exact path, over batch sizes that
+    take one or several 128-query blocks, k = 1 .. 16, deletes and an allow list."""
+    n = 40_000 + 13
+    rows = orc.synth_rows(1600 + d, 0, n, d, 0)
+    qs = orc.synth_rows(1601 + d, 0, 260, d, 0)
+    a, b = _pair(ctx, exact_ctx, metric, d, rows)
+    c = Corpus(bf16_ctx, KIND_F32, metric, d, n)
+    c.upsert(np.arange(n, dtype=np.uint64), rows)
+    dead = np.arange(0, n, 97, dtype=np.uint64)
+    for x in (a, b, c):
+        x.delete(dead)
+    try:
+        al = allow_bitmap(np.arange(2, n, 5, dtype=np.uint64))
+        for nq, k, allow in [(32, 10, None), (260, 16, None), (33, 1, None), (64, 10, al)]:
+            want = b.search(qs[:nq], k, allow)
+            _same(a.search(qs[:nq], k, allow), want)
+            _same(c.search(qs[:nq], k, allow), want)
+    finally:
+        for x in (a, b, c):
+            x.destroy()
+
+
+def test_screen_int8_scale_outliers_and_saturation(ctx, exact_ctx, orc):
+    """The int8 shadow's one corpus scale S is set at its first build: rows with
+    one huge element (S large, every other row coarsely coded), rows written
+    later that exceed 127 S (clamped codes, large error bounds), rows of equal
+    maximal codes (|int32 score| = d 127^2 near 2^24 at d = 1024), heavy ties
+    and zero rows -- the bound stays valid, results exact."""
+    for d in (768, 1024):
+        n = 20_000
+        rows = orc.synth_rows(1700 + d, 0, n, d, 0)
+        rows[5, 3] = 40.0                      # one outlier: S = 40 / 127
+        rows[6:9] = 1.0                        # all codes at the clamp value after scaling
+        rows[9] = -1.0
+        rows[10:14] = 0.0
+        rows[100:400] = rows[100]              # 300 exact ties
+        qs = orc.synth_rows(1701 + d, 0, 48, d, 0)
+        qs[0] = 1.0                            # |q8 . x8| = d 127^2 against rows 6..8
+        qs[1] = rows[100]
+        qs[2] = 0.0
+        qs[3, :] = 1e-30                       # a scale near the underflow guard
+        qs[4, 7] = np.nan
+        for metric in (METRIC_DOT, METRIC_COSINE):
+            a, b = _pair(ctx, exact_ctx, metric, d, rows)
+            try:
+                for k in (1, 10, 16):
+                    _same(a.search(qs, k), b.search(qs, k))  # first build: S from these rows
+                big = (orc.synth_rows(1702 + d, 0, 50, d, 0) * 1000).astype(np.float32)
+                bids = np.arange(15_000, 15_050, dtype=np.uint64)
+                a.upsert(bids, big)                # beyond 127 S: clamped codes
+                b.upsert(bids, big)
+                for k in (1, 10):
+                    _same(a.search(qs, k), b.search(qs, k))
+                qs2 = big[:40] / 1000
+                _same(a.search(qs2, 10), b.search(qs2, 10))
+            finally:
+                a.destroy()
+                b.destroy()
+
+
+def test_screen_int8_varied_norms_dot(ctx, exact_ctx, orc):
+    """Dot products over rows whose norms span six orders of magnitude (the
+    corpus scale codes small rows with few levels: wide bounds, many
+    candidates, the flag path) -- exact."""
+    n, d = 30_000, 768
+    rows = orc.synth_rows(1800, 0, n, d, 0)
+    scale = (10.0 ** np.random.default_rng(1801).uniform(-3, 3, n)).astype(np.float32)
+    rows *= scale[:, None]
+    qs = orc.synth_rows(1802, 0, 128, d, 0)
+    a, b = _pair(ctx, exact_ctx, METRIC_DOT, d, rows)
+    try:
+        for k in (1, 10, 16):
+            _same(a.search(qs, k), b.search(qs, k))
     finally:
         a.destroy()
         b.destroy()

@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
 """BASELINE configs[1]: batched 10-NN over 10M x 768 fp32 cosine, 1024-query
-batches -- the K3c bf16 screen + exact rescore against the exact fp32 MFMA
-path (K3b), same corpus, same queries, results compared bit for bit.
+batches -- the K3i int8 screen and the K3d / K3c bf16 screen (+ exact rescore)
+against the exact fp32 MFMA path (K3b), same corpus, same queries, results
+compared bit for bit.
 Device API (queries in HBM), HIP events bound to the scoring launch(es);
-mfma_util against the dense peak of the kernel's MFMA type (bf16 2.5 PFLOP/s
-for the screen, fp32 157.3 TFLOP/s for K3b); rescored_rows = the candidates
+bf16_peak_frac = the batch's 2 Q N d FLOP / kernel time against the dense
+bf16 peak (2.5 PFLOP/s; fp32 157.3 TFLOP/s for K3b); rescored_rows = the candidates
 the exact fp32 rescore recomputed in the last batch.
 Tooling only (product library; no tuning knobs)."""
 import argparse
@@ -64,6 +65,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--metric", default="cosine", choices=["cosine", "dot"])
     ap.add_argument("--exact", type=int, default=1, help="also time the exact path")
+    ap.add_argument("--screens", default="int8,bf16", help="screens to time: int8 (K3i), bf16 (K3d / K3c)")
     a = ap.parse_args()
     import torch
 
@@ -81,8 +83,9 @@ def main():
     st = torch.cuda.current_stream(dev).cuda_stream
     out = {}
     res = {}
-    for mode in (["screen", "exact"] if a.exact else ["screen"]):
-        ctx = Context(0, batch_screen=1 if mode == "screen" else 0)
+    modes = [m for m in a.screens.split(",") if m] + (["exact"] if a.exact else [])
+    for mode in modes:
+        ctx = Context(0, batch_screen={"int8": 2, "bf16": 1, "exact": 0}[mode])
         lib = ctx.lib
         c = Corpus(ctx, KIND_F32, metric, d, n)
         t0 = time.time()
@@ -112,27 +115,26 @@ def main():
         ms, nl = ctypes.c_double(), ctypes.c_uint64()
         check(lib.wvg_profile_stop(ctx.handle, ctypes.byref(ms), ctypes.byref(nl)))
         res[mode] = (oi.cpu().numpy().copy(), od.cpu().numpy().copy(), oc.cpu().numpy().copy())
-        if mode == "screen":  # flagged (rescanned) queries of the last batch: the screen workspace's nflag word
-            out["flagged_queries"] = int(ws[256 + screen_nflag_offset(n, nq, k, d):][:4].cpu().numpy().view(np.uint32)[0])
+        if mode != "exact":  # flagged (rescanned) queries of the last batch: the screen workspace's nflag word
+            out[mode + "_flagged_queries"] = int(ws[256 + screen_nflag_offset(n, nq, k, d):][:4].cpu().numpy().view(np.uint32)[0])
             # candidates the exact fp32 rescore recomputed (keys the collect kept, K6's input)
             co, ncand, _ = screen_offsets(n, nq, k, d)
             cand = ws[256 + co:256 + co + nq * ncand * 8].cpu().numpy().view(np.uint64)
-            out["rescored_rows"] = int((cand != np.iinfo(np.uint64).max).sum())
-            out["rescored_rows_per_query"] = round(out["rescored_rows"] / nq, 2)
+            out[mode + "_rescored_rows_per_query"] = round(int((cand != np.iinfo(np.uint64).max).sum()) / nq, 2)
         kern_ms = ms.value / max(1, nl.value)
         flop = 2.0 * nq * n * d
         out[mode] = {"batch_ms": round(wall * 1e3, 3), "qps": round(nq / wall, 1),
                      "scoring_kernel_ms": round(kern_ms, 3),
                      "tflops_kernel": round(flop / (kern_ms / 1e3) / 1e12, 1),
-                     "mfma_util": round(flop / (kern_ms / 1e3) / 1e12 / (2500.0 if mode == "screen" else 157.3), 3),
+                     "bf16_peak_frac": round(flop / (kern_ms / 1e3) / 1e12 / (2500.0 if mode != "exact" else 157.3), 3),
                      "first_call_s": round(first_s, 3), "fill_s": round(gen_s, 2)}
         print(json.dumps({mode: out[mode]}), flush=True)
         c.destroy()
         ctx.close()
-    if "exact" in res:
-        same = all(np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8))
-                   for x, y in zip(res["screen"], res["exact"]))
-        out["bit_identical"] = bool(same)
+    first = modes[0]
+    for m in modes[1:]:
+        out[f"{m}_bit_identical_to_{first}"] = bool(all(
+            np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8)) for x, y in zip(res[first], res[m])))
     print(json.dumps({"config": f"{n} x {d} {a.metric}, {nq} queries, k={k}", **out}), flush=True)
 
 

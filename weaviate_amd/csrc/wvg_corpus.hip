@@ -4,6 +4,8 @@
 // (NewProductQuantizer validation, CH/product_quantization.go:187-197) and
 // the bf16 shadow state of F32 dot / cosine corpora (K3c / K3d).
 
+#include <cstring>
+
 #include "wvg_host.hpp"
 
 namespace wvg {
@@ -56,9 +58,12 @@ void shadow_free(wvg_corpus *c)
     if (c->d_shadow) (void)hipFree(c->d_shadow);
     if (c->d_norms) (void)hipFree(c->d_norms);
     if (c->d_nmax) (void)hipFree(c->d_nmax);
+    if (c->d_errs) (void)hipFree(c->d_errs);
     c->d_shadow = nullptr;
     c->d_norms = nullptr;
     c->d_nmax = nullptr;
+    c->d_errs = nullptr;
+    c->sh_i8 = false;
     c->sh_dirty_lo = c->sh_dirty_hi = 0;
     c->sh_failed = false;  // a failed allocation is retried at the next screened search
 }
@@ -86,33 +91,62 @@ bool ensure_shadow(wvg_corpus *c, hipStream_t s)
         return hipEventSynchronize(c->sh_ready) == hipSuccess;
     }
     const uint64_t tiles = tiles_of(c->capacity);
-    const uint32_t kbn = screen_kblocks(c->dim);
     if (!c->d_shadow) {
-        const size_t sbytes = (size_t)(tiles + 4) * kbn * 4 * 1024, nbytes = (size_t)(tiles + 4) * 64 * 4;
-        void *sh = nullptr, *nr = nullptr, *mx = nullptr;
-        if (hipMalloc(&sh, sbytes) != hipSuccess || hipMalloc(&nr, nbytes) != hipSuccess ||
-            hipMalloc(&mx, 256) != hipSuccess || hipMemsetAsync(sh, 0, sbytes, s) != hipSuccess ||
-            hipMemsetAsync(nr, 0, nbytes, s) != hipSuccess || hipMemsetAsync(mx, 0, 256, s) != hipSuccess ||
-            (!c->sh_ready && hipEventCreateWithFlags(&c->sh_ready, hipEventDisableTiming) != hipSuccess)) {
+        void *sh = nullptr, *nr = nullptr, *mx = nullptr, *er = nullptr;
+        auto fail = [&]() {
             (void)hipGetLastError();
             (void)hipStreamSynchronize(s);
             if (sh) (void)hipFree(sh);
             if (nr) (void)hipFree(nr);
             if (mx) (void)hipFree(mx);
+            if (er) (void)hipFree(er);
             c->sh_failed = true;
             return false;
+        };
+        if (hipMalloc(&mx, 256) != hipSuccess || hipMemsetAsync(mx, 0, 256, s) != hipSuccess) return fail();
+        // K3i (the int8 screen, option batch_screen = 2) where its dims apply: the corpus
+        // scale S = the largest finite |x| / 127 of the rows written so far (one pass and
+        // one host wait, at the shadow's first build); no rows / all zeros / an extreme
+        // scale keep the bf16 shadow
+        bool i8 = c->ctx->opt.batch_screen == 2 && screen_i8_supported(c->dim) && c->high_water > 0;
+        float sc[2] = {1.f, 1.f};
+        if (i8) {
+            uint32_t amax_bits = 0;
+            if (launch_shadow_maxabs((const float *)c->d_data, c->dim, tiles_of(c->high_water), (uint32_t *)mx, s) !=
+                    hipSuccess ||
+                hipMemcpyAsync(&amax_bits, mx, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipStreamSynchronize(s) != hipSuccess || hipMemsetAsync(mx, 0, 256, s) != hipSuccess)
+                return fail();
+            float amax;
+            std::memcpy(&amax, &amax_bits, 4);
+            sc[0] = amax / 127.f;
+            sc[1] = 1.f / sc[0];
+            i8 = sc[0] >= 0x1p-100f && sc[0] <= 0x1p100f;
+            if (i8 && hipMemcpyAsync((uint32_t *)mx + 2, sc, 8, hipMemcpyHostToDevice, s) != hipSuccess) return fail();
+            if (i8 && hipStreamSynchronize(s) != hipSuccess) return fail();  // (sc is on this stack)
         }
+        const uint32_t kbn = i8 ? c->dim / 64 : screen_kblocks(c->dim);
+        const size_t sbytes = (size_t)(tiles + 4) * kbn * 4 * 1024, nbytes = (size_t)(tiles + 4) * 64 * 4;
+        if (hipMalloc(&sh, sbytes) != hipSuccess || hipMalloc(&nr, nbytes) != hipSuccess ||
+            (i8 && hipMalloc(&er, nbytes) != hipSuccess) || hipMemsetAsync(sh, 0, sbytes, s) != hipSuccess ||
+            hipMemsetAsync(nr, 0, nbytes, s) != hipSuccess || (er && hipMemsetAsync(er, 0, nbytes, s) != hipSuccess) ||
+            (!c->sh_ready && hipEventCreateWithFlags(&c->sh_ready, hipEventDisableTiming) != hipSuccess))
+            return fail();
         c->d_shadow = sh;
         c->d_norms = (float *)nr;
         c->d_nmax = (uint32_t *)mx;
+        c->d_errs = (float *)er;
+        c->sh_i8 = i8;
         c->sh_dirty_lo = 0;
         c->sh_dirty_hi = tiles_of(c->high_water);
     }
     if (c->sh_dirty_lo < c->sh_dirty_hi) {
-        if (launch_shadow_build((const float *)c->d_data, c->dim, c->sh_dirty_lo, c->sh_dirty_hi, c->d_shadow,
-                                c->d_norms, c->d_nmax, s) != hipSuccess ||
-            hipEventRecord(c->sh_ready, s) != hipSuccess)
-            return false;
+        const hipError_t e =
+            c->sh_i8 ? launch_shadow_build_i8((const float *)c->d_data, c->dim, c->sh_dirty_lo, c->sh_dirty_hi,
+                                              c->d_shadow, c->d_norms, c->d_errs, c->d_nmax, s)
+                     : launch_shadow_build((const float *)c->d_data, c->dim, c->sh_dirty_lo, c->sh_dirty_hi,
+                                           c->d_shadow, c->d_norms, c->d_nmax, s);
+        if (e != hipSuccess || hipEventRecord(c->sh_ready, s) != hipSuccess) return false;
         c->sh_dirty_lo = c->sh_dirty_hi = 0;
         return true;
     }

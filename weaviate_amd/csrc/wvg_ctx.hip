@@ -155,7 +155,7 @@ void wvg_options_default(wvg_options *o)
     o->mfma_min_queries = 32;
     o->cache_reuse = 1;
     o->merge_wait_us = 0;
-    o->batch_screen = 1;
+    o->batch_screen = 2;
     o->coalesce = 1;
     o->heap_replay = 1;
 }

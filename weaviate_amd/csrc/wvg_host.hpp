@@ -161,7 +161,7 @@ bool ensure_shadow(wvg_corpus *c, hipStream_t s);
 // flagged-query list, the rescan's partial lists and the pilot's results.
 struct ScreenWs {
     size_t part = 0, cand = 0, keys = 0, gb = 0, qf = 0, k1 = 0, k2 = 0, em = 0, fl = 0, nf = 0, fbp = 0;
-    size_t pids = 0, pd = 0, pc = 0, total = 0;
+    size_t pids = 0, pd = 0, pc = 0, kb = 0, css = 0, qinv = 0, total = 0;
 };
 ScreenWs screen_ws(uint32_t nq, uint32_t k, uint32_t nrr, uint32_t kbn, uint32_t fb_groups);
 

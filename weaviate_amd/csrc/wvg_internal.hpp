@@ -113,7 +113,9 @@ struct wvg_corpus {
     // the first batched search that uses it and kept in step with later writes
     void *d_shadow = nullptr;      // [tiles + 4][screen_kblocks][4][64] 16-B bf16 fragments
     float *d_norms = nullptr;      // [(tiles + 4) * 64] row-norm upper bounds
-    uint32_t *d_nmax = nullptr;    // max of d_norms (float bits)
+    uint32_t *d_nmax = nullptr;    // {max of d_norms, max of d_errs (float bits), S, 1 / S (K3i's row scale)}
+    float *d_errs = nullptr;       // K3i: [(tiles + 4) * 64] row quantization-error bounds
+    bool sh_i8 = false;            // the shadow is K3i's int8 one (d_shadow: [tiles + 4][dim / 64][4][64] 16 B)
     uint64_t sh_dirty_lo = 0, sh_dirty_hi = 0;  // tiles written since the last build
     bool sh_failed = false;        // the shadow could not be allocated: batches stay on the exact path
     std::mutex sh_mu;              // builds (searches hold rw shared)
@@ -364,6 +366,13 @@ void single_timing_read(uint64_t out[5], bool reset);
 #endif
 hipError_t launch_shadow_build(const float *tiled, uint32_t dim, uint64_t t0, uint64_t t1, void *shadow, float *norms,
                                uint32_t *nmax, hipStream_t s);
+// K3i (the int8 screen): dims it runs, the corpus scale's pass (largest finite
+// |x| of tiles [0, tiles) as float bits into *out) and the shadow build
+// (mx = {max norm, max error, S, 1 / S})
+inline bool screen_i8_supported(uint32_t dim) { return dim == 512 || dim == 768 || dim == 1024; }
+hipError_t launch_shadow_maxabs(const float *tiled, uint32_t dim, uint64_t tiles, uint32_t *out, hipStream_t s);
+hipError_t launch_shadow_build_i8(const float *tiled, uint32_t dim, uint64_t t0, uint64_t t1, void *shadow,
+                                  float *norms, float *errs, uint32_t *mx, hipStream_t s);
 struct ScreenLaunch {
     const void *shadow;
     const float *norms;
@@ -379,6 +388,11 @@ struct ScreenLaunch {
     int num_cus;           // sizes the split screen's first launch
     void *qfrag;           // [nq_pad / 16][kblocks][64] x 16 B
     float *k1, *k2, *emax; // [nq_pad]
+    // K3i (int8 shadow): the rows' error bounds, the corpus scale ({.., .., S, 1 / S}
+    // after the two maxima in nmax's words) and per-query B, score scale, 1 / Sq
+    bool i8 = false;
+    const float *errs = nullptr;
+    float *kb = nullptr, *css = nullptr, *qinv = nullptr;  // [nq_pad]
     uint32_t *gbound;      // [nq]
     uint64_t *partials;    // [nq][nrr][SCREEN_M]
     uint64_t *cand;        // [nq][nrr * SCREEN_M]

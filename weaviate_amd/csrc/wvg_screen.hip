@@ -36,6 +36,7 @@
 // flags a query whose range list was full below tau (rows may have been
 // dropped): it is rescanned exactly (K1).
 // Roofline: bf16 MFMA, 2 Q N d FLOP per batch (2.5 PFLOP/s dense).
+#include <type_traits>
 #include <utility>
 
 #include "wvg_internal.hpp"
@@ -187,6 +188,244 @@ __global__ __launch_bounds__(256) void screen_qconst_kernel(const float *q, uint
 }
 
 // ---------------------------------------------------------------------------
+// The int8 screen (K3i, round 6).  bf16 MFMA runs at 2.5 PFLOP/s, int8 at
+// twice that; K3d's time is almost all per K block (10M x 768 / 512 cosine:
+// 15.34 / 10.83 ms per 1024-query batch = 1.8 ms + 0.56 ms per K block,
+// profiles/r06/screen_i8/), and an int8 K block is 64 deep for the same
+// instructions and the same 16 KiB stage.  The rows get one corpus-wide
+// scale S (the largest |x| / 127 at the shadow's first build; later rows
+// clamp at +-127), each query its own Sq; codes x8 = clamp(rint(x / S)),
+// q8 = clamp(rint(q / Sq)); the MFMA sums q8 . x8 exactly in int32 (|sum| <=
+// d 127^2 < 2^24 for d <= 1024, so its float is exact too).  With xt = S x8,
+// qt = Sq q8 and r the exact fp32 dot in the AVX2 order:
+//   q.x = qt.xt + qt.(x - xt) + (q - qt).x
+//   |qt.(x - xt)| <= |qt| Ex,  |(q - qt).x| <= Eq |x|   (Cauchy-Schwarz)
+//   |r - q.x| <= 4 d 2^-24 |q| |x|    (fp32 dot: ~(d / 32 + 5) 2^-24 for its 32 chains)
+//   s = fl(fl(acc) fl(S Sq)) = qt.xt (1 + <= 2^-22.9)
+// with per-row Ex >= |x - xt| and Nx >= |x| (fp64 sums rounded up, +inf for
+// a non-finite row) and per-query Nqt >= |qt|, Eq >= |q - qt|, Nq >= |q|:
+//   u = s + fma(Ex, A, fma(Nx, B, K2)) >= r,
+//   A = Nqt (1 + 2^-19),  B = Eq (1 + 2^-19) + 4 d 2^-24 Nq + 2^-19 Nqt,
+// the 2^-19 terms absorbing s's and u's own fp32 roundings (relative, all
+// terms >= 0), K2 = K3c's (2^-120 Nq + 2^-110; cosine + 2^-19).  The bound is
+// two-sided, so tau = (k-th smallest lower) + 2 Emax holds as in K3c, Emax_q
+// = fma(max Ex, A, fma(max Nx, B, K2)).  A query that is not finite or whose
+// scale underflows gets A = +inf: every row is a candidate (the flag path).
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// x's int8 code at 1 / inv: nearest, clamped to +-127 (NaN -> 0: a non-finite
+// row's error bound is +inf, so its codes decide nothing)
+__device__ __forceinline__ int si_code(float x, float inv)
+{
+    const float r = __builtin_rintf(x * inv);
+    return r >= 127.f ? 127 : (r <= -127.f ? -127 : (r == r ? (int)r : 0));
+}
+__device__ __forceinline__ uint32_t si_pack4(float4 x, float inv)
+{
+    return (uint32_t)(si_code(x.x, inv) & 255) | (uint32_t)(si_code(x.y, inv) & 255) << 8 |
+           (uint32_t)(si_code(x.z, inv) & 255) << 16 | (uint32_t)(si_code(x.w, inv) & 255) << 24;
+}
+
+// The largest finite |x| of rows [0, n) (tiled layout, whole tiles: the zero
+// fill of a partial tile does not change it), as float bits into *out.
+__global__ __launch_bounds__(256) void shadow_maxabs_kernel(const float4 *__restrict__ tiled, uint64_t count,
+                                                            uint32_t *out)
+{
+    float m = 0.f;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < count; i += (uint64_t)gridDim.x * 256) {
+        const float4 x = tiled[i];
+        const float v[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const float a = __builtin_fabsf(v[e]);
+            if (a <= 3.4028235e38f) m = __builtin_fmaxf(m, a);  // (NaN / inf skipped)
+        }
+    }
+    uint32_t b = __float_as_uint(m);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) b = max(b, (uint32_t)__shfl_xor((int)b, off));
+    if ((threadIdx.x & 63) == 0) atomicMax(out, b);
+}
+
+// int8 fragments of tiles [t0, t1): fragment (t, kb, rg), lane l -> row
+// 16 rg + (l & 15), elements 64 kb + 16 (l >> 4) .. + 15 (byte e = element e).
+// scale = {S, 1 / S}.
+__global__ __launch_bounds__(256) void shadow_i8_frag_kernel(const float4 *__restrict__ tiled, uint32_t nchunks,
+                                                             uint32_t kbn, uint64_t t0, uint64_t nfrag,
+                                                             const float *scale, uint4 *shadow)
+{
+    const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= nfrag * 64) return;
+    const uint32_t lane = (uint32_t)(g & 63);
+    const uint64_t f = g >> 6;
+    const uint32_t rg = (uint32_t)(f & 3);
+    const uint64_t tk = f >> 2;
+    const uint32_t kb = (uint32_t)(tk % kbn);
+    const uint64_t t = t0 + tk / kbn;
+    const uint32_t row = 16 * rg + (lane & 15);
+    const uint32_t c0 = (64 * kb + 16 * (lane >> 4)) / 4;
+    const float inv = scale[1];
+    uint32_t wv[4];
+#pragma unroll
+    for (int h = 0; h < 4; h++) {
+        const uint32_t c = c0 + h;
+        const float4 x = c < nchunks ? tiled[((size_t)t * nchunks + c) * 64 + row] : make_float4(0.f, 0.f, 0.f, 0.f);
+        wv[h] = si_pack4(x, inv);
+    }
+    shadow[((t * kbn + kb) * 4 + rg) * 64 + lane] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+}
+
+// Per row: Nx >= |x| and Ex >= |x - S x8| (fp64 sums, rounded up); their
+// maxima into mx[0], mx[1] (float bits; only ever raised).
+__global__ __launch_bounds__(256) void shadow_i8_norm_kernel(const float4 *__restrict__ tiled, uint32_t nchunks,
+                                                             uint64_t slot0, uint64_t n, const float *scale,
+                                                             float *norms, float *errs, uint32_t *mx)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    float nv = 0.f, ev = 0.f;
+    if (i < n) {
+        const uint64_t slot = slot0 + i;
+        const float4 *rp = tiled + (slot >> 6) * nchunks * 64 + (slot & 63);
+        const double S = scale[0];
+        const float inv = scale[1];
+        double ss = 0.0, se = 0.0;
+        for (uint32_t c = 0; c < nchunks; c++) {
+            const float4 x = rp[(size_t)c * 64];
+            const float v[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const double d = (double)v[e] - S * (double)si_code(v[e], inv);
+                ss += (double)v[e] * v[e];
+                se += d * d;
+            }
+        }
+        nv = norm_upper(ss);
+        ev = norm_upper(se);
+        norms[slot] = nv;
+        errs[slot] = ev;
+    }
+    uint32_t b = __float_as_uint(nv), c = __float_as_uint(ev);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        b = max(b, (uint32_t)__shfl_xor((int)b, off));
+        c = max(c, (uint32_t)__shfl_xor((int)c, off));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(mx, b);
+        atomicMax(mx + 1, c);
+    }
+}
+
+// Per query (one wave each): Sq, the bound constants A (k1), B (kb), K2 (k2),
+// Emax, the score scale fl(S Sq) (css) and 1 / Sq (qinv, for the fragments).
+__global__ __launch_bounds__(256) void screen_qconst_i8_kernel(const float *q, uint32_t nq, uint32_t qpitch,
+                                                               uint32_t dim, uint32_t nq_pad, int cosine,
+                                                               const uint32_t *mx, const float *scale, float *k1,
+                                                               float *k2, float *kb, float *css, float *qinv,
+                                                               float *emax)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t qi = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (qi >= nq_pad) return;
+    float amax = 0.f;
+    bool bad = false;
+    if (qi < nq)
+        for (uint32_t i = lane; i < dim; i += 64) {
+            const float a = __builtin_fabsf(q[(size_t)qi * qpitch + i]);
+            if (a <= 3.4028235e38f) amax = __builtin_fmaxf(amax, a);
+            else bad = true;
+        }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) amax = __builtin_fmaxf(amax, __shfl_xor(amax, off));
+    bad = __ballot(bad) != 0;
+    const float sq = amax > 0.f ? amax / 127.f : 1.f, inv = 1.f / sq;
+    double st = 0.0, se = 0.0, sn = 0.0;
+    if (qi < nq)
+        for (uint32_t i = lane; i < dim; i += 64) {
+            const float x = q[(size_t)qi * qpitch + i];
+            const double t = (double)sq * (double)si_code(x, inv);
+            st += t * t;
+            se += ((double)x - t) * ((double)x - t);
+            sn += (double)x * x;
+        }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        st += __shfl_xor(st, off);
+        se += __shfl_xor(se, off);
+        sn += __shfl_xor(sn, off);
+    }
+    if (lane) return;
+    const double nqt = norm_upper(st), eq = norm_upper(se), nqu = norm_upper(sn);
+    const float S = scale[0];
+    float A = (float)(nqt * (1.0 + 0x1p-19) + 0x1p-120);
+    float B = (float)(eq * (1.0 + 0x1p-19) + 4.0 * dim * 0x1p-24 * nqu + 0x1p-19 * nqt + 0x1p-120);
+    float K2 = (float)(0x1p-120 * nqu + (cosine ? 0x1p-19 : 0x1p-110));
+    float cs = S * sq;
+    // non-finite query or a scale outside the normal range: no fast rejection
+    if (bad || !(cs >= 0x1p-100f && cs <= 0x1p100f) || !(A < __builtin_inff())) A = __builtin_inff();
+    if (qi >= nq) A = B = K2 = cs = 0.f;
+    k1[qi] = A;
+    k2[qi] = K2;
+    kb[qi] = B;
+    css[qi] = cs;
+    qinv[qi] = inv;
+    emax[qi] = __builtin_fmaf(__uint_as_float(mx[1]), A, __builtin_fmaf(__uint_as_float(mx[0]), B, K2));
+}
+
+hipError_t launch_shadow_maxabs(const float *tiled, uint32_t dim, uint64_t tiles, uint32_t *out, hipStream_t s)
+{
+    const uint64_t count = tiles * f32_chunks(dim) * 64;
+    if (count == 0) return hipSuccess;
+    const uint64_t blocks = std::min<uint64_t>(4096, (count + 255) / 256);
+    hipLaunchKernelGGL(shadow_maxabs_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
+                       reinterpret_cast<const float4 *>(tiled), count, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_shadow_build_i8(const float *tiled, uint32_t dim, uint64_t t0, uint64_t t1, void *shadow,
+                                  float *norms, float *errs, uint32_t *mx, hipStream_t s)
+{
+    if (t1 <= t0) return hipSuccess;
+    const uint32_t nch = f32_chunks(dim), kbn = dim / 64;
+    const float *scale = reinterpret_cast<const float *>(mx + 2);
+    const uint64_t nfrag = (t1 - t0) * kbn * 4;
+    hipLaunchKernelGGL(shadow_i8_frag_kernel, dim3((unsigned)((nfrag * 64 + 255) / 256)), dim3(256), 0, s,
+                       reinterpret_cast<const float4 *>(tiled), nch, kbn, t0, nfrag, scale,
+                       reinterpret_cast<uint4 *>(shadow));
+    const uint64_t n = (t1 - t0) * 64;
+    hipLaunchKernelGGL(shadow_i8_norm_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                       reinterpret_cast<const float4 *>(tiled), nch, t0 * 64, n, scale, norms, errs, mx);
+    return hipGetLastError();
+}
+
+// int8 query fragments [nq16][kbn][64]: lane l -> query 16 qg + (l & 15),
+// elements 64 kb + 16 (l >> 4) .. + 15 (the rows' element map)
+__global__ __launch_bounds__(256) void screen_qfrag_i8_kernel(const float *q, uint32_t nq, uint32_t qpitch,
+                                                              uint32_t dim, uint32_t kbn, uint32_t nq16,
+                                                              const float *qinv, uint4 *qfrag)
+{
+    const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= (uint64_t)nq16 * kbn * 64) return;
+    const uint32_t lane = (uint32_t)(g & 63);
+    const uint32_t kb = (uint32_t)((g >> 6) % kbn);
+    const uint32_t qg = (uint32_t)((g >> 6) / kbn);
+    const uint32_t qi = 16 * qg + (lane & 15);
+    const uint32_t e0 = 64 * kb + 16 * (lane >> 4);
+    const float inv = qi < nq ? qinv[qi] : 0.f;
+    uint32_t wv[4];
+#pragma unroll
+    for (int h = 0; h < 4; h++) {
+        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (qi < nq && e0 + 4 * h + 3 < dim) {
+            const float *p = q + (size_t)qi * qpitch + e0 + 4 * h;
+            x = make_float4(p[0], p[1], p[2], p[3]);
+        }
+        wv[h] = si_pack4(x, inv);
+    }
+    qfrag[g] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+}
+
+// ---------------------------------------------------------------------------
 // K3c
 struct ScreenArgs {
     const uint4 *shadow;      // [tiles][kbn][4][64]
@@ -198,6 +437,8 @@ struct ScreenArgs {
     uint32_t kbn;             // 32-element K blocks (even)
     const uint4 *qfrag;       // [nq16][kbn][64]
     const float *k1, *k2, *emax;  // [nq_pad]
+    const float *errs;        // K3i: [slots] row quantization-error norms (upper bounds)
+    const float *kb, *css;    // K3i: [nq_pad] row-norm coefficient B, score scale S * Sq
     uint32_t nq, k, nqb, nrr;
     uint32_t rr0, nrr_l;      // this launch's ranges: [rr0, rr0 + nrr_l) of nrr
     int cosine;
@@ -692,6 +933,16 @@ constexpr int SD_LISTS = SD_WAVES * 32 * SCREEN_M * 8;
 constexpr int SD_LDS = SD_RING + SD_LISTS + SD_WAVES * 32 * 4 * 2 + SD_BQ * 4 * 3;
 static_assert(SD_LDS <= 160 * 1024, "K3d's LDS");
 
+// K3i (round 6): K3d on an int8 shadow (below, "The int8 screen").  Its LDS:
+// the ring holds NB stages (KBN % NB == 0: 6 for d = 768's 12 K blocks, else
+// 8), a norm slot holds the block's row norms, tile words and row errors, and
+// the per-query constants gain B (the row-norm coefficient) and the score scale.
+constexpr int si_nbuf(int kbn) { return kbn % 8 == 0 ? 8 : 6; }
+constexpr int SI_NSLOT = 2304;  // norms [0, 1024), tile words [1024, 1088), row errors [1280, 2304)
+constexpr int si_ring(int nb) { return nb * SD_STAGE + 2 * SI_NSLOT; }
+constexpr int si_lds(int nb) { return si_ring(nb) + SD_LISTS + SD_WAVES * 32 * 4 * 2 + SD_BQ * 4 * 5; }
+static_assert(si_lds(8) <= 160 * 1024, "K3i's LDS");
+
 // One accumulator element read where it is used.  Through C++ the compiler
 // copies the whole accumulator tile into VGPRs at the top of the epilogue (~100
 // live VGPRs next to the resident queries: spills); the asm names the element
@@ -699,6 +950,13 @@ static_assert(SD_LDS <= 160 * 1024, "K3d's LDS");
 __device__ __forceinline__ float agpr_read(float x)
 {
     float r;
+    asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(r) : "a"(x));
+    return r;
+}
+// (K3i) an int32 accumulator element
+__device__ __forceinline__ int agpr_read(int x)
+{
+    int r;
     asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(r) : "a"(x));
     return r;
 }
@@ -742,20 +1000,20 @@ __device__ __forceinline__ void sd_static_for(F &&f)
 // block): its 4 row-fragment pieces, and with unit 0 the block's row norms of
 // its tile (+ wave 0: the block's tile words).  DIAG 256 (tools): round 3's
 // norms / words with every unit.
-template <int DIAG>
+template <int DIAG, bool I8 = false>
 constexpr int sd_unit_loads(int u, bool w0)
 {
     if ((DIAG & 128) != 0) return 0;
     if ((DIAG & 32) != 0) return 4;
     if ((DIAG & 256) != 0) return 5 + (w0 ? 1 : 0);
-    return 4 + (u == 0 ? 1 + (w0 ? 1 : 0) : 0);
+    return 4 + (u == 0 ? 1 + (I8 ? 1 : 0) + (w0 ? 1 : 0) : 0);  // (K3i: + the row errors)
 }
 // The loads issued after unit `first`'s, over units first + 1 .. first + n (mod KBN)
-template <int KBN, int DIAG>
+template <int KBN, int DIAG, bool I8 = false>
 constexpr int sd_younger(int first, int n, bool w0)
 {
     int c = 0;
-    for (int i = 1; i <= n; i++) c += sd_unit_loads<DIAG>((first + i) % KBN, w0);
+    for (int i = 1; i <= n; i++) c += sd_unit_loads<DIAG, I8>((first + i) % KBN, w0);
     return c;
 }
 
@@ -766,17 +1024,31 @@ constexpr int sd_younger(int first, int n, bool w0)
 // bit 2 = tests but no survivor queue, bit 4 = count row blocks / blocks with
 // survivors / queued survivors.  Compile-time, so the tools build's DIAG = 0
 // kernel is the product kernel, register allocation included.
-template <int KBN, int DIAG = 0>
+//
+// I8 (K3i, round 6): the same kernel on the int8 shadow -- 64-deep K blocks
+// of v_mfma_i32_16x16x64_i8 (twice the bf16 rate: a K block is the same
+// instruction count and the same 16 KiB stage for twice the depth), exact
+// int32 scores scaled once per element, and the two-term bound of "The int8
+// screen" below (row norm and row quantization error).
+template <int KBN, int DIAG = 0, bool I8 = false>
 __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs a)
 {
-    static_assert(KBN % SD_NBUF == 0, "the stage buffer of a K block must be a compile-time constant");
+    constexpr int NB = I8 ? si_nbuf(KBN) : SD_NBUF;  // stage buffers
+    constexpr int NSLOT = I8 ? SI_NSLOT : SD_NSLOT;
+    constexpr int RING = NB * SD_STAGE + 2 * NSLOT;
+    static_assert(KBN % NB == 0, "the stage buffer of a K block must be a compile-time constant");
+    static_assert(!I8 || (DIAG & ~(2 | 8)) == 0, "K3i: only the stage-loop diagnostic");
+    using frag_t = std::conditional_t<I8, i32x4, bf16x8>;
+    using acc_t = std::conditional_t<I8, i32x4, floatx4>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint64_t *lists = reinterpret_cast<uint64_t *>(smem + SD_RING);  // [4][32][M]
-    float *tau = reinterpret_cast<float *>(smem + SD_RING + SD_LISTS);
+    uint64_t *lists = reinterpret_cast<uint64_t *>(smem + RING);  // [4][32][M]
+    float *tau = reinterpret_cast<float *>(smem + RING + SD_LISTS);
     float *sig = tau + SD_WAVES * 32;
     float *ck1 = sig + SD_WAVES * 32;
     float *ck2 = ck1 + SD_BQ;
     float *cem = ck2 + SD_BQ;
+    float *ckb = cem + SD_BQ;  // (I8) B
+    float *ccs = ckb + SD_BQ;  // (I8) score scale
     uint32_t n_blk = 0, n_slow = 0, n_call = 0, n_grp = 0;  // (DIAG & 16)
     (void)n_blk, (void)n_slow, (void)n_call, (void)n_grp;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -803,6 +1075,10 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
         ck1[i] = a.k1[q];
         ck2[i] = a.k2[q];
         cem[i] = a.emax[q];
+        if constexpr (I8) {
+            ckb[i] = a.kb[q];
+            ccs[i] = a.css[q];
+        }
     }
     for (int i = tid; i < SD_WAVES * 32; i += SD_WAVES * 64) {
         const uint32_t q = q0 + (uint32_t)i;
@@ -816,11 +1092,12 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
     SurvivorLists S;
     S.laddr = (uint32_t)(uintptr_t)(lists + (size_t)w * 32 * M);
     // the wave's per-query thresholds WT (tau), their u-space form WS (sig) and Emax
-    // (cem): LDS byte address of tau[w][0]; sig, cem at + 512, + 2048
+    // (cem): LDS byte address of tau[w][0]; sig, ck1, ck2, cem at + 512, + 1024, + 1536,
+    // + 2048 (I8: ckb, ccs at + 2560, + 3072)
     const uint32_t tbase = (uint32_t)(uintptr_t)(tau + w * 32);
     if (blk0 < blk1) {
         // the wave's 32 queries, every K block, resident for the whole range
-        bf16x8 areg[KBN][2];
+        frag_t areg[KBN][2];
         // The first SD_AKB K blocks' fragments live in AGPRs (an MFMA A operand may be
         // an AGPR), the rest in VGPRs: 128 accumulator + 64 B-fragment + 48 such AGPRs,
         // which leaves the epilogue ~100 VGPRs -- with all 192 in VGPRs the compiler
@@ -855,19 +1132,22 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
         // and words with every unit: 25 % more LDS-DMA issues per unit.
         const uint4 *lsrc = a.shadow + ((size_t)(a.tile_begin + blk0 * 4 + w) * KBN * 4) * 64 + lane;
         const float *lnorm = a.norms + (a.tile_begin + blk0 * 4 + w) * 64 + lane;
+        const float *lerr = I8 ? a.errs + (a.tile_begin + blk0 * 4 + w) * 64 + lane : nullptr;
         uint64_t lblk = blk0;
         auto load_stage = [&](int ks) {
             if constexpr ((DIAG & 128) != 0) return;
-            unsigned char *dst = smem + (ks % SD_NBUF) * SD_STAGE;
+            unsigned char *dst = smem + (ks % NB) * SD_STAGE;
 #pragma unroll
             for (int rg = 0; rg < 4; rg++)
                 __builtin_amdgcn_global_load_lds(lsrc + ((size_t)ks * 4 + rg) * 64,
                                                  reinterpret_cast<uint4 *>(dst + (4 * w + rg) * 1024), 16, 0, 0);
-            unsigned char *nslot = smem + SD_NBUF * SD_STAGE + (lblk & 1) * SD_NSLOT;
+            unsigned char *nslot = smem + NB * SD_STAGE + (lblk & 1) * NSLOT;
             // the block's norms / tile words with its unit 0 (sd_unit_loads: the waits count them)
             const bool with_norms = (DIAG & 32) == 0 && ((DIAG & 256) != 0 || ks == 0);
             if (with_norms)
                 __builtin_amdgcn_global_load_lds(lnorm, reinterpret_cast<float *>(nslot + w * 256), 4, 0, 0);
+            if (I8 && with_norms)
+                __builtin_amdgcn_global_load_lds(lerr, reinterpret_cast<float *>(nslot + 1280 + w * 256), 4, 0, 0);
             if (with_norms && w == 0) {
                 const uint32_t wi = (uint32_t)(lane & 7) >> 1, half = lane & 1;
                 const uint64_t t = a.tile_begin + lblk * 4 + wi;
@@ -883,6 +1163,7 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
                 ++lblk;
                 lsrc += (size_t)4 * KBN * 4 * 64;
                 lnorm += 256;
+                if constexpr (I8) lerr += 256;
             }
         };
         // six stages in flight at every wait: unit ks + 1 (waited for at K block ks) + the 5
@@ -890,14 +1171,15 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
         // PAIR (tools A/B, DIAG 1024): one wait + barrier per two K blocks -- at even ks for
         // unit ks + 2 (units ks + 3 .. ks + 6 outstanding), which also covers the odd
         // iteration's reads of unit ks + 1; the two units ks + 7, ks + 8 load after it
+        // (K3i with NB = 6: four stages in flight, three left outstanding)
         constexpr bool PAIR = (DIAG & 1024) != 0;
         auto wait_next = [&](auto KS) {
             if constexpr ((DIAG & 129) != 0) return;
             constexpr int ks = decltype(KS)::value;
             if constexpr (PAIR && (ks & 1) != 0) return;
-            constexpr int first = PAIR ? ks + 2 : ks + 1, n = PAIR ? SD_NBUF - 4 : SD_NBUF - 3;
-            constexpr int n0 = sd_younger<KBN, DIAG>(first, n, true);
-            constexpr int n1 = sd_younger<KBN, DIAG>(first, n, false);
+            constexpr int first = PAIR ? ks + 2 : ks + 1, n = PAIR ? NB - 4 : NB - 3;
+            constexpr int n0 = sd_younger<KBN, DIAG, I8>(first, n, true);
+            constexpr int n1 = sd_younger<KBN, DIAG, I8>(first, n, false);
             if (w == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n0) : "memory");
             else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n1) : "memory");
         };
@@ -915,8 +1197,8 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
         // One lane base address for every read: the stage / half offset is added
         // inside the asm from an SGPR (16 precomputed addresses cost 16 VGPRs).
         const uint32_t rbase = (uint32_t)(uintptr_t)smem + 16u * lane;
-        auto read_half = [&](int ks, int h, bf16x8 (&br)[8]) {
-            const uint32_t soff = (uint32_t)((ks % SD_NBUF) * SD_STAGE + h * 8 * 1024);
+        auto read_half = [&](int ks, int h, frag_t (&br)[8]) {
+            const uint32_t soff = (uint32_t)((ks % NB) * SD_STAGE + h * 8 * 1024);
             uint32_t tmp;
             asm volatile("v_add_u32 %8, %9, %10\n\t"
                          "ds_read_b128 %0, %8\n\t"
@@ -933,7 +1215,7 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
                          : "memory");
         };
         // the first half landed (the second half's eight reads may still be in flight)
-        auto wait_b0 = [&](bf16x8 (&br)[8]) {
+        auto wait_b0 = [&](frag_t (&br)[8]) {
             asm volatile("s_waitcnt lgkmcnt(8)"
                          : "+a"(br[0]), "+a"(br[1]), "+a"(br[2]), "+a"(br[3]), "+a"(br[4]), "+a"(br[5]), "+a"(br[6]),
                            "+a"(br[7])
@@ -956,19 +1238,26 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
             for (int r = 0; r < 4; r++)
                 if (!(ck1[32 * w + 16 * mq + qlane + r] <= 0x1p50f)) lane_force = true;
 
-        floatx4 acc[2][16];
+        acc_t acc[2][16];
 #pragma unroll
         for (int mq = 0; mq < 2; mq++)
 #pragma unroll
-            for (int nr = 0; nr < 16; nr++) acc[mq][nr] = (floatx4){0.f, 0.f, 0.f, 0.f};
-        bf16x8 b0[8], b1[8];
-        // prologue: units 0 .. 6 of the range (a unit = one K block of one row
-        // block; the ring holds K block ks of any row block in buffer ks % 8)
+            for (int nr = 0; nr < 16; nr++) acc[mq][nr] = acc_t{0, 0, 0, 0};
+        frag_t b0[8], b1[8];
+        // one K block of one 16 x 16 tile: bf16 16x16x32, or (I8) int8 16x16x64 with exact int32 sums
+        auto mfma = [](const frag_t &x, const frag_t &y, const acc_t &c) -> acc_t {
+            if constexpr (I8)
+                return __builtin_amdgcn_mfma_i32_16x16x64_i8(x, y, c, 0, 0, 0);
+            else
+                return __builtin_amdgcn_mfma_f32_16x16x32_bf16(x, y, c, 0, 0, 0);
+        };
+        // prologue: units 0 .. NB - 2 of the range (a unit = one K block of one row
+        // block; the ring holds K block ks of any row block in buffer ks % NB)
 #pragma unroll
-        for (int ks = 0; ks < SD_NBUF - 1; ks++) load_stage(ks);
-        // unit 0 landed: the 6 younger units 1 .. 6 outstanding
-        if (w == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(sd_younger<KBN, DIAG>(0, SD_NBUF - 2, true)) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(sd_younger<KBN, DIAG>(0, SD_NBUF - 2, false)) : "memory");
+        for (int ks = 0; ks < NB - 1; ks++) load_stage(ks);
+        // unit 0 landed: the NB - 2 younger units outstanding
+        if (w == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(sd_younger<KBN, DIAG, I8>(0, NB - 2, true)) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(sd_younger<KBN, DIAG, I8>(0, NB - 2, false)) : "memory");
         raw_barrier();
         read_half(0, 0, b0);
         for (uint64_t blk = blk0; blk < blk1; blk++) {
@@ -979,8 +1268,7 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
 #pragma unroll
                 for (int mq = 0; mq < 2; mq++)
 #pragma unroll
-                    for (int nr = 0; nr < 8; nr++)
-                        acc[mq][nr] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(areg[ks][mq], b0[nr], acc[mq][nr], 0, 0, 0);
+                    for (int nr = 0; nr < 8; nr++) acc[mq][nr] = mfma(areg[ks][mq], b0[nr], acc[mq][nr]);
                 wait_next(KS);  // the next unit landed
                 if constexpr (!PAIR || (ks & 1) == 0)
                     raw_barrier();  // (lgkmcnt(0): this wave's second-half reads done)
@@ -991,18 +1279,16 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
                 // unit + 7 into the buffer of unit - 1 (fully read before this barrier); PAIR:
                 // also unit + 8 into the buffer of this unit (its reads done: the barrier's wait)
                 if constexpr (!PAIR) {
-                    load_stage((ks + SD_NBUF - 1) % KBN);
+                    load_stage((ks + NB - 1) % KBN);
                 } else if constexpr ((ks & 1) == 0) {
-                    load_stage((ks + SD_NBUF - 1) % KBN);
-                    load_stage((ks + SD_NBUF) % KBN);
+                    load_stage((ks + NB - 1) % KBN);
+                    load_stage((ks + NB) % KBN);
                 }
                 if (ks + 1 < KBN) read_half(ks + 1, 0, b0);  // (the next block's first half: after the epilogue)
 #pragma unroll
                 for (int mq = 0; mq < 2; mq++)
 #pragma unroll
-                    for (int nr = 0; nr < 8; nr++)
-                        acc[mq][8 + nr] =
-                            __builtin_amdgcn_mfma_f32_16x16x32_bf16(areg[ks][mq], b1[nr], acc[mq][8 + nr], 0, 0, 0);
+                    for (int nr = 0; nr < 8; nr++) acc[mq][8 + nr] = mfma(areg[ks][mq], b1[nr], acc[mq][8 + nr]);
             });
             // The epilogue reads the accumulators through inline asm (agpr_read), which the
             // compiler's hazard recognizer does not see: an MFMA's result may be read by a
@@ -1022,8 +1308,9 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
                 // epilogue LDS access is inline asm with its own lgkmcnt wait (through C++
                 // the compiler cannot tell them from the stage ring's LDS DMA and waits
                 // vmcnt(0), draining the prefetch), at a lane base + an SGPR offset.
-                const uint32_t nsoff = (uint32_t)(SD_NBUF * SD_STAGE + (blk & 1) * SD_NSLOT);  // the block's norms
-                auto read_norms8 = [&](int hh, float (&nrm)[8]) {  // row norms of row groups 8 hh .. 8 hh + 7
+                const uint32_t nsoff = (uint32_t)(NB * SD_STAGE + (blk & 1) * NSLOT);  // the block's norms
+                // row norms of row groups 8 hh .. 8 hh + 7 (hh 2, 3: I8's row errors, slot bytes 1280 ..)
+                auto read_norms8 = [&](int hh, float (&nrm)[8]) {
                     uint32_t tmp;
                     asm volatile("v_add_u32 %8, %9, %10\n\t"
                                  "ds_read_b32 %0, %8\n\t"
@@ -1037,7 +1324,7 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
                                  "s_waitcnt lgkmcnt(0)"
                                  : "=v"(nrm[0]), "=v"(nrm[1]), "=v"(nrm[2]), "=v"(nrm[3]), "=v"(nrm[4]),
                                    "=v"(nrm[5]), "=v"(nrm[6]), "=v"(nrm[7]), "=&v"(tmp)
-                                 : "s"(nsoff + 512u * hh), "v"(nbase)
+                                 : "s"(nsoff + (hh < 2 ? 512u * hh : 1280u + 512u * (hh - 2))), "v"(nbase)
                                  : "memory");
                 };
                 auto read_consts = [&](int mq, float (&k1r)[4], float (&k2r)[4], float (&svr)[4]) {
@@ -1057,6 +1344,23 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
                     k2r[0] = k2v.x, k2r[1] = k2v.y, k2r[2] = k2v.z, k2r[3] = k2v.w;
                     svr[0] = sv.x, svr[1] = sv.y, svr[2] = sv.z, svr[3] = sv.w;
                 };
+                // (I8) B and the score scale of the lane's four queries of half mq: ckb, ccs at
+                // sig + 2048, + 2560
+                auto read_consts_i8 = [&](int mq, float (&kbr)[4], float (&csr)[4]) {
+                    const uint32_t coff = (uint32_t)(csoff + 4 * (32 * w + 16 * mq));
+                    float4 kbv, csv;
+                    uint32_t tmp;
+                    asm volatile("v_add_u32 %2, %3, %4\n\t"
+                                 "ds_read_b128 %0, %2 offset:2048\n\t"
+                                 "ds_read_b128 %1, %2 offset:2560\n\t"
+                                 "s_waitcnt lgkmcnt(0)"
+                                 : "=v"(kbv), "=v"(csv), "=&v"(tmp)
+                                 : "s"(coff), "v"(qbase)
+                                 : "memory");
+                    kbr[0] = kbv.x, kbr[1] = kbv.y, kbr[2] = kbv.z, kbr[3] = kbv.w;
+                    csr[0] = csv.x, csr[1] = csv.y, csr[2] = csv.z, csr[3] = csv.w;
+                };
+                (void)read_consts_i8;
                 if constexpr ((DIAG & 16) != 0) n_blk++;
                 // fast check: the lane's 16 rows' largest norm bound bounds each of their E
                 // (E = fma(norm, K1q, K2q) is monotone in the norm), so per query the largest
@@ -1083,15 +1387,45 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
                         for (int j2 = 0; j2 < 8; j2++) nrmt[j2] = n0[j2], nrmt[8 + j2] = n1[j2];
                     }
                 }
+                // (I8) the lane's 16 rows' largest error bound: E = fma(err, A, fma(norm, B, K2))
+                // is monotone in both
+                float emx = 0.f, esum = 0.f;
+                if constexpr (I8) {
+                    float e0[8], e1[8];
+                    read_norms8(2, e0);
+                    read_norms8(3, e1);
+                    emx = e0[0];
+                    esum = e0[0];
+#pragma unroll
+                    for (int j2 = 1; j2 < 8; j2++) emx = __builtin_fmaxf(emx, e0[j2]), esum += e0[j2];
+#pragma unroll
+                    for (int j2 = 0; j2 < 8; j2++) emx = __builtin_fmaxf(emx, e1[j2]), esum += e1[j2];
+                }
                 // per (query half mq, query r of the lane's four): whether some lane cannot rule
                 // out its 16 elements -- only those groups run the exact test (a wave-uniform
                 // bit each; typically one or two of the eight)
-                const bool force = lane_force || !(nmax <= 0x1p60f) || nsum != nsum;
+                const bool force = lane_force || !(nmax <= 0x1p60f) || nsum != nsum || !(emx <= 0x1p60f) || esum != esum;
                 uint32_t wact = 0;
 #pragma unroll
                 for (int mq = 0; mq < 2; mq++) {
                     float k1r[4], k2r[4], svr[4];
                     read_consts(mq, k1r, k2r, svr);
+                    if constexpr (I8) {
+                        // the largest exact int32 score, scaled once (rounding is monotone)
+                        float kbr[4], csr[4];
+                        read_consts_i8(mq, kbr, csr);
+#pragma unroll
+                        for (int r = 0; r < 4; r++) {
+                            int mi = agpr_read(acc[mq][0][r]);
+#pragma unroll
+                            for (int nr = 1; nr < 16; nr++) mi = max(mi, agpr_read(acc[mq][nr][r]));
+                            const float m = (float)mi * csr[r];
+                            const float t =
+                                (m + __builtin_fmaf(emx, k1r[r], __builtin_fmaf(nmax, kbr[r], k2r[r]))) - svr[r];
+                            if (__ballot(force || t >= 0.f)) wact |= 1u << (4 * mq + r);
+                        }
+                        continue;
+                    }
 #pragma unroll
                     for (int r = 0; r < 4; r++) {
                         float t;
@@ -1153,14 +1487,19 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
                     float nrm16[16];
                     read_norms8(0, *reinterpret_cast<float(*)[8]>(&nrm16[0]));
                     read_norms8(1, *reinterpret_cast<float(*)[8]>(&nrm16[8]));
+                    float err16[I8 ? 16 : 1];  // (I8) the rows' error bounds
+                    if constexpr (I8) {
+                        read_norms8(2, *reinterpret_cast<float(*)[8]>(&err16[0]));
+                        read_norms8(3, *reinterpret_cast<float(*)[8]>(&err16[8]));
+                    }
                     for (uint32_t gw = wact; gw; gw &= gw - 1) {
                         const int gi = __builtin_ctz(gw);
                         if constexpr ((DIAG & 16) != 0) n_grp++;
-                        float uv[16];
+                        float uv[16];  // (I8: the exact int32 scores, exactly as floats: |score| < 2^24)
                         switch (gi) {
 #define WVG_SD_GROUP(G)                                                                        \
     case G:                                                                                    \
-        _Pragma("unroll") for (int nr = 0; nr < 16; nr++) uv[nr] = agpr_read(acc[(G) >> 2][nr][(G) & 3]); \
+        _Pragma("unroll") for (int nr = 0; nr < 16; nr++) uv[nr] = (float)agpr_read(acc[(G) >> 2][nr][(G) & 3]); \
         break;
                         WVG_SD_GROUP(0) WVG_SD_GROUP(1) WVG_SD_GROUP(2) WVG_SD_GROUP(3)
                         WVG_SD_GROUP(4) WVG_SD_GROUP(5) WVG_SD_GROUP(6) WVG_SD_GROUP(7)
@@ -1182,12 +1521,24 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
                                      : "=v"(v2), "=v"(wt), "=v"(ws), "=v"(em), "=v"(k1), "=v"(k2)
                                      : "v"(la), "v"(ta)
                                      : "memory");
+                        float kbq = 0.f, csq = 1.f;  // (I8) B and the score scale: ckb + 2560, ccs + 3072
+                        if constexpr (I8)
+                            asm volatile("ds_read_b32 %0, %2 offset:2560\n\t"
+                                         "ds_read_b32 %1, %2 offset:3072\n\t"
+                                         "s_waitcnt lgkmcnt(0)"
+                                         : "=v"(kbq), "=v"(csq)
+                                         : "v"(ta)
+                                         : "memory");
                         uint64_t v = ((uint64_t)v2.y << 32) | v2.x;
                         const int li = lane & 15;
 #pragma unroll
                         for (int nr = 0; nr < 16; nr++) {
                             const uint64_t m64 = ((vm[nr >> 2] >> (16 * (nr & 3))) & 0xFFFFull) * 0x0001000100010001ull;
-                            const float u = uv[nr] + __builtin_fmaf(nrm16[nr], k1, k2);
+                            float u;
+                            if constexpr (I8)
+                                u = uv[nr] * csq + __builtin_fmaf(err16[nr], k1, __builtin_fmaf(nrm16[nr], kbq, k2));
+                            else
+                                u = uv[nr] + __builtin_fmaf(nrm16[nr], k1, k2);
                             uint64_t pass = __ballot(!(u < ws)) & m64;
                             while (pass) {
                                 const int j = __builtin_ctzll(pass);
@@ -1233,13 +1584,13 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
 #pragma unroll
                 for (int mq = 0; mq < 2; mq++)
 #pragma unroll
-                    for (int nr = 0; nr < 16; nr++) x += agpr_read(acc[mq][nr][0]);
+                    for (int nr = 0; nr < 16; nr++) x += (float)agpr_read(acc[mq][nr][0]);
                 if (x == 0x1p-120f) a.partials[0] = 0;
             }
 #pragma unroll
             for (int mq = 0; mq < 2; mq++)
 #pragma unroll
-                for (int nr = 0; nr < 16; nr++) acc[mq][nr] = (floatx4){0.f, 0.f, 0.f, 0.f};
+                for (int nr = 0; nr < 16; nr++) acc[mq][nr] = acc_t{0, 0, 0, 0};
             // the next block's first K block: its stage landed before the last barrier and is not
             // overwritten before the next block's second barrier
             read_half(0, 0, b0);
@@ -2659,16 +3010,28 @@ uint32_t screen_row_ranges(uint32_t nq, uint64_t ntiles, int num_cus)
 
 hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
 {
-    const uint32_t kbn = screen_kblocks(L.dim);
+    const bool i8 = L.i8 && screen_i8_supported(L.dim);
+    const uint32_t kbn = i8 ? L.dim / 64 : screen_kblocks(L.dim);  // (K3i: 64-deep int8 K blocks)
     const uint32_t nq16 = (L.nq + 15) / 16, nq_pad = (L.nq + SC_BQ - 1) / SC_BQ * SC_BQ;
     uint32_t nqb = nq_pad / SC_BQ;  // (K3g, tools: 64-query blocks)
     hipError_t e;
-    // query fragments for every 16-query group of the padded batch
-    hipLaunchKernelGGL(screen_qfrag_kernel, dim3((unsigned)(((uint64_t)nq_pad / 16 * kbn * 64 + 255) / 256)), dim3(256),
-                       0, s, L.queries, L.nq, L.qpitch, L.dim, kbn, nq_pad / 16, reinterpret_cast<uint4 *>(L.qfrag));
     (void)nq16;
-    hipLaunchKernelGGL(screen_qconst_kernel, dim3(nq_pad / 4), dim3(256), 0, s, L.queries, L.nq, L.qpitch, L.dim,
-                       nq_pad, L.cosine, L.nmax, L.k1, L.k2, L.emax);
+    if (i8) {
+        // K3i: per-query scale and bound constants first, then the int8 fragments at that scale
+        hipLaunchKernelGGL(screen_qconst_i8_kernel, dim3(nq_pad / 4), dim3(256), 0, s, L.queries, L.nq, L.qpitch,
+                           L.dim, nq_pad, L.cosine, L.nmax, reinterpret_cast<const float *>(L.nmax + 2), L.k1, L.k2,
+                           L.kb, L.css, L.qinv, L.emax);
+        hipLaunchKernelGGL(screen_qfrag_i8_kernel, dim3((unsigned)(((uint64_t)nq_pad / 16 * kbn * 64 + 255) / 256)),
+                           dim3(256), 0, s, L.queries, L.nq, L.qpitch, L.dim, kbn, nq_pad / 16, L.qinv,
+                           reinterpret_cast<uint4 *>(L.qfrag));
+    } else {
+        // query fragments for every 16-query group of the padded batch
+        hipLaunchKernelGGL(screen_qfrag_kernel, dim3((unsigned)(((uint64_t)nq_pad / 16 * kbn * 64 + 255) / 256)),
+                           dim3(256), 0, s, L.queries, L.nq, L.qpitch, L.dim, kbn, nq_pad / 16,
+                           reinterpret_cast<uint4 *>(L.qfrag));
+        hipLaunchKernelGGL(screen_qconst_kernel, dim3(nq_pad / 4), dim3(256), 0, s, L.queries, L.nq, L.qpitch, L.dim,
+                           nq_pad, L.cosine, L.nmax, L.k1, L.k2, L.emax);
+    }
     if ((e = hipMemsetAsync(L.gbound, 0xFF, (size_t)L.nq * 4, s)) != hipSuccess) return e;
     // profiling: one event pair spans every phase and the seeds between them (taken
     // before the pilot, whose K3b launch would otherwise bind them)
@@ -2760,24 +3123,43 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
 #endif
     a.gbound = L.gbound;
     a.partials = L.partials;
+    a.errs = L.errs;
+    a.kb = L.kb;
+    a.css = L.css;
     static bool attr = [] {
         return hipFuncSetAttribute(reinterpret_cast<const void *>(&screen_kernel),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, SC_LDS) == hipSuccess &&
                hipFuncSetAttribute(reinterpret_cast<const void *>(&screen_ar_kernel<16>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, SD_LDS) == hipSuccess &&
                hipFuncSetAttribute(reinterpret_cast<const void *>(&screen_ar_kernel<24>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, SD_LDS) == hipSuccess;
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, SD_LDS) == hipSuccess &&
+               hipFuncSetAttribute(reinterpret_cast<const void *>(&screen_ar_kernel<8, 0, true>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, si_lds(si_nbuf(8))) == hipSuccess &&
+               hipFuncSetAttribute(reinterpret_cast<const void *>(&screen_ar_kernel<12, 0, true>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, si_lds(si_nbuf(12))) == hipSuccess &&
+               hipFuncSetAttribute(reinterpret_cast<const void *>(&screen_ar_kernel<16, 0, true>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, si_lds(si_nbuf(16))) == hipSuccess;
     }();
     (void)attr;
-    // K3d (queries resident in registers) where its template applies, else K3c
+    // K3i on an int8 shadow; else K3d (queries resident in registers) where its template applies, else K3c
     void (*kern)(ScreenArgs) = kbn == 24 ? &screen_ar_kernel<24> : kbn == 16 ? &screen_ar_kernel<16> : nullptr;
+    if (i8)
+        kern = kbn == 8 ? &screen_ar_kernel<8, 0, true>
+                        : (kbn == 12 ? &screen_ar_kernel<12, 0, true> : &screen_ar_kernel<16, 0, true>);
     bool k3f = false;
 #ifdef WVG_TOOLS
+    bool k3g = false;
+    if (i8 && tuning().screen_diag == 10 && kbn == 12) {  // K3i's stage loop alone (A/B)
+        kern = &screen_ar_kernel<12, 10, true>;
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  si_lds(si_nbuf(12)));
+    }
+    if (!i8) {
     if (tuning().screen_variant == 2 && kern)  // K3e (32x32x16 MFMAs)
         kern = kbn == 24 ? &screen_ar32_kernel<24> : &screen_ar32_kernel<16>;
     if (tuning().screen_variant == 3 && kern)  // K3f (two waves per SIMD)
         kern = kbn == 24 ? &screen_ar16_kernel<24> : &screen_ar16_kernel<16>;
-    const bool k3g = tuning().screen_variant == 4 && kern;  // K3g (two 4-wave workgroups per CU)
+    k3g = tuning().screen_variant == 4 && kern;  // K3g (two 4-wave workgroups per CU)
     if (k3g) kern = kbn == 24 ? &screen_ar16x2_kernel<24> : &screen_ar16x2_kernel<16>;
     if (tuning().screen_variant >= 2 && kern)
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2810,15 +3192,16 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
     }
     if (tuning().screen_variant == 1) kern = nullptr;
     k3f = kern == &screen_ar16_kernel<24> || kern == &screen_ar16_kernel<16> || kern == &screen_ar16_kernel<24, 10>;
+    }  // (!i8)
 #endif
 #ifdef WVG_TOOLS
     if (k3g) {  // 64-query workgroups: twice the query blocks
         nqb = nq_pad / SG_BQ;
         a.nqb = nqb;
     }
-    const uint32_t lds = k3g ? SG_LDS : kern ? SD_LDS : SC_LDS;
+    const uint32_t lds = i8 ? si_lds(si_nbuf(kbn)) : k3g ? SG_LDS : kern ? SD_LDS : SC_LDS;
 #else
-    const uint32_t lds = kern ? SD_LDS : SC_LDS;
+    const uint32_t lds = i8 ? si_lds(si_nbuf(kbn)) : kern ? SD_LDS : SC_LDS;
 #endif
     const uint32_t threads = k3f ? SF_WAVES * 64 : kern ? SD_WAVES * 64 : SC_WAVES * 64;
     if (!kern) kern = &screen_kernel;

@@ -204,6 +204,9 @@ ScreenWs screen_ws(uint32_t nq, uint32_t k, uint32_t nrr, uint32_t kbn, uint32_t
     w.pids = cv.take((size_t)nq * k * 8);  // the pilot's own results (the caller's arrays may be null)
     w.pd = cv.take((size_t)nq * k * 4);
     w.pc = cv.take((size_t)nq * 4);
+    w.kb = cv.take(nq_pad * 4);  // K3i's per-query constants
+    w.css = cv.take(nq_pad * 4);
+    w.qinv = cv.take(nq_pad * 4);
     w.total = cv.off;
     return w;
 }
@@ -305,6 +308,11 @@ static int run_screen(wvg_corpus *c, const ScanArgs &a, const SearchPlan &p, cha
     L.pilot_ids = (uint64_t *)(ws + w.pids);
     L.pilot_dists = (float *)(ws + w.pd);
     L.pilot_counts = (uint32_t *)(ws + w.pc);
+    L.i8 = c->sh_i8;
+    L.errs = c->d_errs;
+    L.kb = (float *)(ws + w.kb);
+    L.css = (float *)(ws + w.css);
+    L.qinv = (float *)(ws + w.qinv);
     uint64_t *keys = (uint64_t *)(ws + w.keys);
     L.metric = c->metric;
     L.data = (const float *)c->d_data;
