@@ -249,6 +249,7 @@ def cpu_pq_leg(target_s, threads, gpu_check):
 # per-GPU size through the host C ABI (what the Go binding calls), each timed
 # with HIP events bound to its dominant kernel and spot-checked afterwards.
 BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md; no 2:1 sparsity)
+I8_PEAK_TOPS = 5000.0      # dense int8 MFMA: twice bf16 (cdna_hip_programming.md "MFMA rate per dtype")
 # PQ encode: 5.5 VALU instructions per (row, segment, centroid) -- the reference's
 # unfused sub, mul, add per dimension, two centroids per packed op -- at one wave64
 # VALU instruction per SIMD per 4 cycles, 1024 SIMDs, 2.4 GHz
@@ -305,9 +306,11 @@ def _bits(x):
 
 
 def config_batched(ctx, orc, metric_name, metric, reps=3):
-    """configs[1]: 10M x 768 fp32 dot / cosine, 1024-query batches (bf16 MFMA
-    screen + exact fp32 rescore); frac = 2 Q N d FLOP / the screen launches'
-    time vs the dense bf16 peak."""
+    """configs[1]: 10M x 768 fp32 dot / cosine, 1024-query batches (the int8
+    MFMA screen K3i + exact fp32 rescore; results identical to the exact path);
+    frac = 2 Q N d ops / the screen launches' time vs the dense int8 peak the
+    kernel computes at, and bf16_equiv_frac the same rate against the dense bf16
+    peak (the unit the bf16 screen of rounds 3-5 was quoted in)."""
     from weaviate_amd._lib import KIND_F32
     from weaviate_amd.device import Corpus
 
@@ -316,7 +319,7 @@ def config_batched(ctx, orc, metric_name, metric, reps=3):
     c = Corpus(ctx, KIND_F32, metric, d, n)
     c.fill_synthetic(42, n, 0)
     qs = orc.synth_rows(43, 0, Q, d, 0)
-    c.search(qs, k)  # untimed: builds the bf16 shadow
+    c.search(qs, k)  # untimed: builds the int8 shadow
     lib.wvg_profile_start(ctx.handle)
     t0 = time.perf_counter()
     for _ in range(reps):
@@ -345,11 +348,14 @@ def config_batched(ctx, orc, metric_name, metric, reps=3):
     tflops = flop / screen_s / 1e12
     return {"workload": f"{n:,} x {d} fp32 {metric_name}, {Q}-query batches, exact {k}-NN (host API wvg_search)",
             "qps": round(Q / wall, 1), "batch_ms": round(wall * 1e3, 3), "batches": reps,
-            "kernel": "bf16 MFMA screen (K3d screen_ar_kernel<24>) + exact fp32 AVX2-order rescore",
-            "roofline": {"bound": "mfma", "achieved": round(tflops, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(tflops / BF16_PEAK_TFLOPS, 4), "screen_ms_per_batch": round(screen_s * 1e3, 3),
-                         "frac_whole_batch": round(flop / wall / 1e12 / BF16_PEAK_TFLOPS, 4),
-                         "flop_per_batch": flop},
+            "kernel": "int8 MFMA screen (K3i screen_ar_kernel<12, 0, true>: exact int32 scores + a per-row "
+                      "quantization-error bound) + exact fp32 AVX2-order rescore",
+            "roofline": {"bound": "mfma", "achieved": round(tflops, 1), "peak": I8_PEAK_TOPS, "unit": "TOP/s (int8)",
+                         "frac": round(tflops / I8_PEAK_TOPS, 4),
+                         "bf16_equiv_frac": round(tflops / BF16_PEAK_TFLOPS, 4),
+                         "screen_ms_per_batch": round(screen_s * 1e3, 3),
+                         "frac_whole_batch_bf16_equiv": round(flop / wall / 1e12 / BF16_PEAK_TFLOPS, 4),
+                         "ops_per_batch": flop},
             "check": {"ok": ok, "how": "queries 0 and 1023: results sorted, every distance a bit-exact oracle "
                                        "recomputation of its row, no row of 30k sampled (start / middle / end) "
                                        "ahead of the k-th; all counts = k"}}

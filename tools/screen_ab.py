@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--variants", default="0", help="screen kernel (tuning key 20): 0 K3d where it applies, 1 K3c")
     ap.add_argument("--pilots", default="16", help="tiles of the exact pilot scan that seeds the bound (tuning key 21; 0 = none)")
     ap.add_argument("--gpilots", default="512", help="tiles of the K3b pilot (tuning key 23; 0 = the K1 pilot)")
+    ap.add_argument("--spilots", default="0", help="tiles of the screen pilot (tuning key 26; 0 = the K3b pilot)")
+    ap.add_argument("--splits2", default="", help="(unused)")
     ap.add_argument("--seeds", default="3", help="exact seeds (tuning key 22): bit 0 between phases, bit 1 before the final collect")
     a = ap.parse_args()
     import torch
@@ -56,13 +58,15 @@ def main():
     od = torch.empty((nq, k), dtype=torch.float32, device=dev)
     oc = torch.empty(nq, dtype=torch.int32, device=dev)
     ref = None
-    for gp, sd, pl, vr, sp, rb, dg in [(gp, sd, pl, vr, sp, rb, dg) for gp in [int(x) for x in a.gpilots.split(",")]
+    for spl, gp, sd, pl, vr, sp, rb, dg in [(spl, gp, sd, pl, vr, sp, rb, dg) for spl in [int(x) for x in a.spilots.split(",")]
+                                       for gp in [int(x) for x in a.gpilots.split(",")]
                                        for sd in [int(x) for x in a.seeds.split(",")]
                                    for pl in [int(x) for x in a.pilots.split(",")]
                                for vr in [int(x) for x in a.variants.split(",")]
                                for sp in [int(x) for x in a.splits.split(",")]
                            for rb in [int(x) for x in a.ranges.split(",")] for dg in [int(x) for x in a.diags.split(",")]]:
         if True:
+            lib.wvgx_set_tuning(26, spl)
             lib.wvgx_set_tuning(23, gp)
             lib.wvgx_set_tuning(22, sd)
             lib.wvgx_set_tuning(21, pl)
@@ -98,10 +102,11 @@ def main():
                 if ref is None:
                     ref = got
                 same = bool(np.array_equal(got, ref))
-            print(json.dumps({"gemm_pilot": gp, "seed": sd, "pilot": pl, "search_ms": round(wall, 3), "variant": vr, "split": sp, "range_blocks": rb, "diag": dg, "scoring_kernel_ms": round(kern, 3),
+            print(json.dumps({"screen_pilot": spl, "gemm_pilot": gp, "seed": sd, "pilot": pl, "search_ms": round(wall, 3), "variant": vr, "split": sp, "range_blocks": rb, "diag": dg, "scoring_kernel_ms": round(kern, 3),
                               "tflops": round(2.0 * nq * n * d / (kern / 1e3) / 1e12, 1),
                               "ids_equal_first": same, "wave_row_blocks": cnt[0], "slow_path_blocks": cnt[1],
                               "insert_calls": cnt[2], "exact_groups": cnt[3]}), flush=True)
+    lib.wvgx_set_tuning(26, 0)
     lib.wvgx_set_tuning(17, 0)
     lib.wvgx_set_tuning(18, 0)
     lib.wvgx_set_tuning(19, 1)

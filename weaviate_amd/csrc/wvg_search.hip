@@ -1023,9 +1023,21 @@ static int wvg::search_batch_filtered(wvg_corpus *c, const std::vector<wvg_searc
     write_empty(B, k, out_ids, out_dists, out_counts);
     if (TE <= TB) return WVG_OK;
     const uint64_t W = TE - TB, wb = c->id_base / 64;
-    std::vector<uint64_t> win((size_t)B * W, 0ull);  // query i's allow words of tiles [TB, TE) (0 outside its own)
-    for (uint32_t i = 0; i < B; i++)
-        if (live[i]) std::memcpy(win.data() + (size_t)i * W + (tb[i] - TB), batch[i]->allow + wb + tb[i], (te[i] - tb[i]) * 8);
+    // query i's allow words of tiles [TB, TE) (0 outside its own), written straight into
+    // the pinned staging (below): one pass over the callers' words, zeros only outside
+    // each window (round 5 filled a zeroed vector, then staged it: three passes)
+    auto fill_windows = [&](uint64_t *win) {
+        for (uint32_t i = 0; i < B; i++) {
+            uint64_t *row = win + (size_t)i * W;
+            if (!live[i]) {
+                std::memset(row, 0, W * 8);
+                continue;
+            }
+            std::memset(row, 0, (tb[i] - TB) * 8);
+            std::memcpy(row + (tb[i] - TB), batch[i]->allow + wb + tb[i], (te[i] - tb[i]) * 8);
+            std::memset(row + (te[i] - TB), 0, (TE - te[i]) * 8);
+        }
+    };
     // per-query allow windows: K1Q's filtered variant (d = 128 / 768, L2 / dot / cosine) or the COS K1
     SearchPlan p = plan_search(c, B, k, nullptr, 0, true, false);
     if (p.empty) return WVG_OK;
@@ -1057,7 +1069,16 @@ static int wvg::search_batch_filtered(wvg_corpus *c, const std::vector<wvg_searc
     uint32_t qpitch = 0;
     rc = stage_queries(c, g.slot, q.data(), B, b + o_q, qpitch, nullptr, nullptr, &st);
     if (rc) return rc;
-    WVG_HIP(st.h2d(b + o_allow, win.data(), (size_t)B * W * 8, s));
+    std::vector<uint64_t> wbig;  // (beyond the staging: pageable, copied by HIP)
+    uint64_t *win = nullptr;
+    if ((size_t)B * W * 8 <= STAGE_MAX) {
+        win = reinterpret_cast<uint64_t *>(st.take((size_t)B * W * 8));
+    } else {
+        wbig.resize((size_t)B * W);
+        win = wbig.data();
+    }
+    fill_windows(win);
+    WVG_HIP(hipMemcpyAsync(b + o_allow, win, (size_t)B * W * 8, hipMemcpyHostToDevice, s));
     rc = run_search(c, b + o_q, qpitch, B, k, (const uint64_t *)(b + o_allow), p, (uint64_t *)(b + o_part),
                     (uint64_t *)(b + o_ids), (float *)(b + o_d), (uint32_t *)(b + o_cnt), s);
     if (rc) return rc;
