@@ -3,6 +3,11 @@
 // negative codes with a thread-local message; no HIP failure aborts the
 // process (no panics across cgo).
 
+#include <condition_variable>
+#include <thread>
+#include <functional>
+#include <atomic>
+#include <mutex>
 #include "wvg_host.hpp"
 
 namespace wvg {
@@ -95,6 +100,64 @@ int prof_pair(wvg_ctx *ctx, std::pair<hipEvent_t, hipEvent_t> *out)
     return WVG_OK;
 }
 
+}  // namespace wvg
+
+namespace wvg {
+namespace {
+// parallel_for's workers: a job is open from its post until the caller has run
+// out of items and closed it; a worker joins only an open job (active + 1), so
+// once the job is closed and active is 0, no worker can touch it again.
+struct HostPool {
+    std::mutex mu;
+    std::condition_variable cv, done_cv;
+    const std::function<void(uint32_t)> *job = nullptr;
+    uint32_t n = 0, active = 0;
+    std::atomic<uint32_t> next{0};
+    uint64_t gen = 0;
+    bool closed = true;
+    explicit HostPool(int threads)
+    {
+        for (int t = 0; t < threads; t++) std::thread([this] { run(); }).detach();  // process lifetime
+    }
+    void run()
+    {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(mu);
+        for (;;) {
+            cv.wait(lk, [&] { return gen != seen; });
+            seen = gen;
+            if (closed) continue;
+            const std::function<void(uint32_t)> *f = job;
+            const uint32_t total = n;
+            active++;
+            lk.unlock();
+            for (uint32_t i; (i = next.fetch_add(1, std::memory_order_relaxed)) < total;) (*f)(i);
+            lk.lock();
+            if (--active == 0) done_cv.notify_all();
+        }
+    }
+};
+}  // namespace
+
+void parallel_for(uint32_t n, const std::function<void(uint32_t)> &f)
+{
+    static HostPool *pool = new HostPool(3);  // (never destroyed: its threads are detached)
+    static std::mutex call_mu;                // one job at a time
+    std::lock_guard<std::mutex> one(call_mu);
+    {
+        std::lock_guard<std::mutex> lk(pool->mu);
+        pool->job = &f;
+        pool->n = n;
+        pool->next.store(0, std::memory_order_relaxed);
+        pool->closed = false;
+        pool->gen++;
+    }
+    pool->cv.notify_all();
+    for (uint32_t i; (i = pool->next.fetch_add(1, std::memory_order_relaxed)) < n;) f(i);
+    std::unique_lock<std::mutex> lk(pool->mu);
+    pool->closed = true;
+    pool->done_cv.wait(lk, [&] { return pool->active == 0; });
+}
 }  // namespace wvg
 
 using namespace wvg;

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -87,6 +88,12 @@ struct Staging {
         return hipMemcpyAsync(dst, r, bytes, hipMemcpyHostToDevice, s);
     }
 };
+
+// A small process-wide pool of host threads for bulk memory work on a call's
+// critical path (the filtered batch's allow windows: ~2 MB of caller words per
+// 16-query batch).  parallel_for(n, f) runs f(0) .. f(n - 1) on the pool and
+// the calling thread and returns when all are done.
+void parallel_for(uint32_t n, const std::function<void(uint32_t)> &f);
 
 struct Bulk {
     SlotGuard g;

@@ -1026,17 +1026,22 @@ static int wvg::search_batch_filtered(wvg_corpus *c, const std::vector<wvg_searc
     // query i's allow words of tiles [TB, TE) (0 outside its own), written straight into
     // the pinned staging (below): one pass over the callers' words, zeros only outside
     // each window (round 5 filled a zeroed vector, then staged it: three passes)
-    auto fill_windows = [&](uint64_t *win) {
-        for (uint32_t i = 0; i < B; i++) {
-            uint64_t *row = win + (size_t)i * W;
-            if (!live[i]) {
-                std::memset(row, 0, W * 8);
-                continue;
-            }
-            std::memset(row, 0, (tb[i] - TB) * 8);
-            std::memcpy(row + (tb[i] - TB), batch[i]->allow + wb + tb[i], (te[i] - tb[i]) * 8);
-            std::memset(row + (te[i] - TB), 0, (TE - te[i]) * 8);
+    auto fill_window = [&](uint64_t *win, uint32_t i) {
+        uint64_t *row = win + (size_t)i * W;
+        if (!live[i]) {
+            std::memset(row, 0, W * 8);
+            return;
         }
+        std::memset(row, 0, (tb[i] - TB) * 8);
+        std::memcpy(row + (tb[i] - TB), batch[i]->allow + wb + tb[i], (te[i] - tb[i]) * 8);
+        std::memset(row + (te[i] - TB), 0, (TE - te[i]) * 8);
+    };
+    // large windows (e.g. 16 x 125 KB for 10 % lists over 1M rows) on several host threads
+    auto fill_windows = [&](uint64_t *win) {
+        if ((size_t)B * W * 8 >= ((size_t)256 << 10) && B > 1)
+            parallel_for(B, [&](uint32_t i) { fill_window(win, i); });
+        else
+            for (uint32_t i = 0; i < B; i++) fill_window(win, i);
     };
     // per-query allow windows: K1Q's filtered variant (d = 128 / 768, L2 / dot / cosine) or the COS K1
     SearchPlan p = plan_search(c, B, k, nullptr, 0, true, false);
