@@ -375,19 +375,29 @@ int rerun_full(wvg_ctx *ctx, const ScanArgs &a0, int groups, const float *d_thr_
     return rc;
 }
 
+// The recording scan's grid: one 4-wave workgroup per CU for a lone query (the
+// plain K5 scan runs three, which would leave each wave too little LDS for its
+// records); a batch keeps the co-scheduled grid of the plan.
+int replay_groups(const wvg_corpus *bq, uint32_t nq, const SearchPlan &p)
+{
+    if (nq != 1) return p.groups;
+    return (int)std::min<uint64_t>((uint64_t)bq->ctx->num_cus, std::max<uint64_t>(1, (p.te - p.tb + 7) / 8));
+}
+
 }  // namespace
 
 size_t replay_workspace_bytes(const wvg_corpus *bq, uint32_t nq, uint32_t R, const SearchPlan &p)
 {
-    const EmitPlan e = emit_plan_for(p.te - p.tb, p.groups, nq, R, bq->ctx->num_cus);
-    return replay_ws(nq, (uint32_t)p.groups, R, e.cap, REPLAY_OUT_CAP).total;
+    const int groups = replay_groups(bq, nq, p);
+    const EmitPlan e = emit_plan_for(p.te - p.tb, groups, nq, R, bq->ctx->num_cus);
+    return replay_ws(nq, (uint32_t)groups, R, e.cap, REPLAY_OUT_CAP).total;
 }
 
 int bq_heap_candidates(wvg_corpus *bq, StreamSlot *sl, const void *d_qb, uint32_t qpb, uint32_t nq, uint32_t R,
                        const uint64_t *d_allow, const SearchPlan &p, char *ws, std::vector<std::vector<GoItem>> &pops)
 {
     hipStream_t s = sl->stream;
-    const int groups = p.groups;
+    const int groups = replay_groups(bq, nq, p);
     const EmitPlan e = emit_plan_for(p.te - p.tb, groups, nq, R, bq->ctx->num_cus);
     const ReplayWs w = replay_ws(nq, (uint32_t)groups, R, e.cap, REPLAY_OUT_CAP);
     ScanArgs a{};

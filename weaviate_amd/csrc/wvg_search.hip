@@ -230,6 +230,10 @@ SearchPlan plan_search(wvg_corpus *c, uint32_t nq, uint32_t k, const uint64_t *a
         p.groups = (int)gemm_row_ranges(nq, std::max<uint64_t>(1, p.te - p.tb), c->ctx->num_cus, c->dim, k);
     else
         p.groups = scan_groups_for(a, c->ctx->num_cus);
+    // K5 (BQ) single-query scans: three 4-wave workgroups per CU, not K8e's one 8-wave one
+    // (100M x 1536: 2.80 / 2.87 -> 2.78 / 2.82 ms, profiles/r06/bq/bq_groups_per_cu*.jsonl)
+    if (c->kind == WVG_KIND_BQ && nq == 1 && tuning().groups_per_cu <= 0)  // (each wave >= 2 tiles)
+        p.groups = (int)std::min<uint64_t>(3ull * (uint64_t)c->ctx->num_cus, std::max<uint64_t>(1, (p.te - p.tb) / 8));
     // bf16 screen + exact rescore for the batches it applies to (results identical to K3b)
     if (p.gemm && c->ctx->opt.batch_screen && screen_supported(c->dim, c->metric, k) && c->dim % 4 == 0 &&
         !c->sh_failed) {
