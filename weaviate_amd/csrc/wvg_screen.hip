@@ -1622,6 +1622,447 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
     }
 }
 
+// ---------------------------------------------------------------------------
+// K3i (round 6) for d = 512 / 768: the int8 screen with 2 x 2 waves.  K3d's
+// waves each own 32 queries x all 256 rows of a block, so every wave reads the
+// whole 16 KiB stage from LDS: 64 KiB of LDS reads per K block and CU for 32
+// MFMAs per wave, the loop's bound (profiles/r06/screen_i8: the stage loop
+// alone ran the matrix pipe ~44 % busy).  int8 queries take half the registers
+// of bf16 ones, so here a wave owns 64 queries (4 groups, resident) x 128 rows
+// (one half of the block: its own 8 KiB of the stage): the same 32 MFMAs per
+// K block from half the LDS reads.  The two row halves keep separate survivor
+// lists per query (K3c's rule: each list holds its half's smallest lower
+// bounds, its thresholds are valid for its rows); the kernel merges each
+// query's two lists at the end.  The ring has 7 stages for every KBN (the
+// buffer of a unit is (block * KBN + ks) % 7, a scalar); LDS = 7 x 16 KiB
+// ring + 2 norm / error slots + 4 x 64 lists + thresholds and constants.
+constexpr int SJ_NB = 7;
+constexpr int SJ_LISTS = SD_WAVES * 64 * SCREEN_M * 8;
+constexpr int SJ_RING = SJ_NB * SD_STAGE + 2 * SI_NSLOT;
+constexpr int SJ_LDS = SJ_RING + SJ_LISTS + SD_WAVES * 64 * 4 * 2 + SD_BQ * 4 * 5;
+static_assert(SJ_LDS <= 160 * 1024, "K3i 2x2's LDS");
+
+template <int KBN>
+__global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_i8_kernel(ScreenArgs a)
+{
+    static_assert(KBN <= 12, "64 resident queries x KBN K blocks must fit the registers");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint64_t *lists = reinterpret_cast<uint64_t *>(smem + SJ_RING);  // [4 waves][64][M]
+    float *tau = reinterpret_cast<float *>(smem + SJ_RING + SJ_LISTS);  // [4 waves][64]
+    float *sig = tau + SD_WAVES * 64;                                     // [4 waves][64]
+    float *ck1 = sig + SD_WAVES * 64;                                     // [128]: A
+    float *ck2 = ck1 + SD_BQ;                                             // K2
+    float *cem = ck2 + SD_BQ;                                             // Emax
+    float *ckb = cem + SD_BQ;                                             // B
+    float *ccs = ckb + SD_BQ;                                             // score scale
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wq = w & 1, wr = w >> 1;  // query half (64 queries), row half (tiles 2 wr, 2 wr + 1)
+    const int K = (int)a.k, M = SCREEN_M;
+    const int cosine = a.cosine;
+    const uint32_t b = blockIdx.x;
+    uint32_t qb, rr;
+    if (a.nrr_l % 8 == 0) {
+        const uint32_t xcd = b % 8, wv = b / 8;
+        qb = wv % a.nqb;
+        rr = a.rr0 + (wv / a.nqb) * 8 + xcd;
+    } else {
+        qb = b % a.nqb;
+        rr = a.rr0 + b / a.nqb;
+    }
+    const uint64_t ntiles = a.tile_end - a.tile_begin;
+    const uint64_t nblk = (ntiles + 3) / 4;
+    const uint64_t blk0 = nblk * rr / a.nrr, blk1 = nblk * (rr + 1) / a.nrr;
+    const uint32_t q0 = qb * SD_BQ;
+
+    for (int i = tid; i < SD_BQ; i += SD_WAVES * 64) {
+        const uint32_t q = q0 + (uint32_t)i;
+        ck1[i] = a.k1[q];
+        ck2[i] = a.k2[q];
+        cem[i] = a.emax[q];
+        ckb[i] = a.kb[q];
+        ccs[i] = a.css[q];
+    }
+    for (int i = tid; i < SD_WAVES * 64; i += SD_WAVES * 64) {  // (wave v, query ql) = (i / 64, i % 64)
+        const uint32_t q = q0 + (uint32_t)(64 * ((i >> 6) & 1) + (i & 63));
+        const uint32_t g = q < a.nq ? __hip_atomic_load(a.gbound + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        const float t = q >= a.nq ? -__builtin_inff() : (g == 0xFFFFFFFFu ? __builtin_inff() : wvg_unord_f32(g));
+        tau[i] = t;
+        sig[i] = q >= a.nq ? __builtin_inff() : sc_sigma(t, cosine);
+    }
+    for (int i = tid; i < SD_WAVES * 64 * M; i += SD_WAVES * 64) lists[i] = WVG_KEY_NONE;
+    __syncthreads();
+    SurvivorLists S;
+    S.laddr = (uint32_t)(uintptr_t)(lists + (size_t)w * 64 * M);
+    // LDS byte addresses: tau[w][0] (sig at + 1024) and ck1[64 wq] (ck2, cem, ckb, ccs at
+    // + 512, + 1024, + 1536, + 2048)
+    const uint32_t tbase = (uint32_t)(uintptr_t)(tau + w * 64);
+    const uint32_t cbase = (uint32_t)(uintptr_t)(ck1 + 64 * wq);
+    if (blk0 < blk1) {
+        // the wave's 64 queries (4 groups of 16), every K block, resident: the first
+        // 6 K blocks in AGPRs (128 accumulator + 32 B-fragment + 96 such AGPRs), the
+        // rest in VGPRs
+        constexpr int AKB = 6;
+        i32x4 areg[KBN][4];
+        const uint4 *qsrc = a.qfrag + (size_t)(qb * 8 + 4 * wq) * KBN * 64 + lane;
+#pragma unroll
+        for (int ks = 0; ks < KBN; ks++)
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const uint4 *src = qsrc + ((size_t)g * KBN + ks) * 64;
+                if (ks < AKB)
+                    asm volatile("global_load_dwordx4 %0, %1, off" : "=a"(areg[ks][g]) : "v"(src) : "memory");
+                else
+                    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(areg[ks][g]) : "v"(src) : "memory");
+            }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int ks = 0; ks < KBN; ks++)
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                if (ks < AKB)
+                    asm volatile("" : "+a"(areg[ks][g]));
+                else
+                    asm volatile("" : "+v"(areg[ks][g]));
+            }
+
+        // loads of one unit (K block ks of a row block): wave w moves the 4 fragments of
+        // the block's tile w; with ks = 0 also tile w's norms and errors, and wave 0 the
+        // block's tile words (sd_unit_loads<.., true>)
+        const uint4 *lsrc = a.shadow + ((size_t)(a.tile_begin + blk0 * 4 + w) * KBN * 4) * 64 + lane;
+        const float *lnorm = a.norms + (a.tile_begin + blk0 * 4 + w) * 64 + lane;
+        const float *lerr = a.errs + (a.tile_begin + blk0 * 4 + w) * 64 + lane;
+        uint64_t lblk = blk0;
+        uint32_t lbuf = 0;  // ring buffer of the next unit to load (the units run in order)
+        auto load_stage = [&](int ks) {
+            unsigned char *dst = smem + lbuf * SD_STAGE;
+            lbuf = lbuf + 1 == (uint32_t)SJ_NB ? 0u : lbuf + 1;
+#pragma unroll
+            for (int rg = 0; rg < 4; rg++)
+                __builtin_amdgcn_global_load_lds(lsrc + ((size_t)ks * 4 + rg) * 64,
+                                                 reinterpret_cast<uint4 *>(dst + (4 * w + rg) * 1024), 16, 0, 0);
+            unsigned char *nslot = smem + SJ_NB * SD_STAGE + (lblk & 1) * SI_NSLOT;
+            if (ks == 0) {
+                __builtin_amdgcn_global_load_lds(lnorm, reinterpret_cast<float *>(nslot + w * 256), 4, 0, 0);
+                __builtin_amdgcn_global_load_lds(lerr, reinterpret_cast<float *>(nslot + 1280 + w * 256), 4, 0, 0);
+                if (w == 0) {
+                    const uint32_t wi = (uint32_t)(lane & 7) >> 1, half = lane & 1;
+                    const uint64_t t = a.tile_begin + lblk * 4 + wi;
+                    const uint32_t *src =
+                        reinterpret_cast<const uint32_t *>(a.valid + (t < a.tile_end ? t : a.tile_end - 1)) + half;
+                    if (lane >= 8 && lane < 16 && a.allow) {
+                        const uint64_t aw = t - a.allow_t0;
+                        src = reinterpret_cast<const uint32_t *>(a.allow + (aw < a.allow_words ? aw : 0)) + half;
+                    }
+                    __builtin_amdgcn_global_load_lds(src, reinterpret_cast<uint32_t *>(nslot + 1024), 4, 0, 0);
+                }
+            }
+            if (ks == KBN - 1 && lblk + 1 < blk1) {  // the load cursor moves on; past the end it stays
+                ++lblk;
+                lsrc += (size_t)4 * KBN * 4 * 64;
+                lnorm += 256;
+                lerr += 256;
+            }
+        };
+        // NB - 2 = 5 units in flight at every wait: unit ks + 1 (waited for at K block ks)
+        // and the NB - 3 younger ones
+        auto wait_next = [&](auto KS) {
+            constexpr int ks = decltype(KS)::value;
+            constexpr int n0 = sd_younger<KBN, 0, true>(ks + 1, SJ_NB - 3, true);
+            constexpr int n1 = sd_younger<KBN, 0, true>(ks + 1, SJ_NB - 3, false);
+            if (w == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n0) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n1) : "memory");
+        };
+        auto raw_barrier = [&]() {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+        };
+        // Half of the wave's row fragments of a unit (tile 2 wr + h: row groups 4 h .. 4 h + 3)
+        // straight into AGPRs, from the unit's ring buffer rb (a scalar)
+        const uint32_t rbase = (uint32_t)(uintptr_t)smem + 16u * lane + 8192u * (uint32_t)wr;
+        auto read_half = [&](uint32_t rb, int h, i32x4 (&br)[4]) {
+            const uint32_t soff = rb * (uint32_t)SD_STAGE + (uint32_t)h * 4096u;
+            uint32_t tmp;
+            asm volatile("v_add_u32 %4, %5, %6\n\t"
+                         "ds_read_b128 %0, %4\n\t"
+                         "ds_read_b128 %1, %4 offset:1024\n\t"
+                         "ds_read_b128 %2, %4 offset:2048\n\t"
+                         "ds_read_b128 %3, %4 offset:3072"
+                         : "=a"(br[0]), "=a"(br[1]), "=a"(br[2]), "=a"(br[3]), "=&v"(tmp)
+                         : "s"(soff), "v"(rbase)
+                         : "memory");
+        };
+        auto wait_b0 = [&](i32x4 (&br)[4]) {  // the first half landed (the second half's 4 reads may not)
+            asm volatile("s_waitcnt lgkmcnt(4)" : "+a"(br[0]), "+a"(br[1]), "+a"(br[2]), "+a"(br[3]) : : "memory");
+        };
+        const int qlane = 4 * (lane >> 4);
+        const uint32_t sbase = (uint32_t)(uintptr_t)smem;
+        const uint32_t nbase = sbase + 4u * (uint32_t)(lane & 15);
+        // +inf when one of this lane's queries is not fast-eligible (A > 2^50)
+        bool lane_force = false;
+#pragma unroll
+        for (int g = 0; g < 4; g++)
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+                if (!(ck1[64 * wq + 16 * g + qlane + r] <= 0x1p50f)) lane_force = true;
+
+        i32x4 acc[4][8];
+#pragma unroll
+        for (int g = 0; g < 4; g++)
+#pragma unroll
+            for (int nr = 0; nr < 8; nr++) acc[g][nr] = i32x4{0, 0, 0, 0};
+        i32x4 b0[4], b1[4];
+        // prologue: units 0 .. NB - 2 of the range into buffers 0 .. NB - 2
+#pragma unroll
+        for (int ks = 0; ks < SJ_NB - 1; ks++) load_stage(ks % KBN);
+        if (w == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(sd_younger<KBN, 0, true>(0, SJ_NB - 2, true)) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(sd_younger<KBN, 0, true>(0, SJ_NB - 2, false)) : "memory");
+        raw_barrier();
+        uint32_t cbuf = 0;  // ring buffer of K block 0 of the current row block
+        read_half(0u, 0, b0);
+        for (uint64_t blk = blk0; blk < blk1; blk++) {
+            sd_static_for<KBN>([&](auto KS) {
+                constexpr int ks = decltype(KS)::value;
+                const uint32_t ub = __builtin_amdgcn_readfirstlane((cbuf + (uint32_t)ks) % (uint32_t)SJ_NB);  // its buffer
+                read_half(ub, 1, b1);
+                wait_b0(b0);
+#pragma unroll
+                for (int g = 0; g < 4; g++)
+#pragma unroll
+                    for (int nr = 0; nr < 4; nr++)
+                        acc[g][nr] = __builtin_amdgcn_mfma_i32_16x16x64_i8(areg[ks][g], b0[nr], acc[g][nr], 0, 0, 0);
+                wait_next(KS);  // the next unit landed
+                raw_barrier();  // (lgkmcnt(0): this wave's second-half reads done)
+#pragma unroll
+                for (int j = 0; j < 4; j++) asm volatile("" : "+a"(b1[j]));
+                // unit + NB - 1 into the buffer of unit - 1 (fully read before this barrier)
+                load_stage((ks + SJ_NB - 1) % KBN);
+                if (ks + 1 < KBN) {
+                    uint32_t nb = ub + 1 == (uint32_t)SJ_NB ? 0u : ub + 1;
+                    read_half(__builtin_amdgcn_readfirstlane(nb), 0, b0);
+                }
+#pragma unroll
+                for (int g = 0; g < 4; g++)
+#pragma unroll
+                    for (int nr = 0; nr < 4; nr++)
+                        acc[g][4 + nr] =
+                            __builtin_amdgcn_mfma_i32_16x16x64_i8(areg[ks][g], b1[nr], acc[g][4 + nr], 0, 0, 0);
+            });
+            cbuf = (cbuf + (uint32_t)KBN) % (uint32_t)SJ_NB;
+            // (the XDL write -> VALU read hazard of the block's last MFMAs: see K3d)
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            // epilogue of row block blk: C layout row (query) 16 g + qlane + r, column (row)
+            // 128 wr + 16 nr + (lane & 15)
+            const uint32_t nsoff = (uint32_t)(SJ_NB * SD_STAGE + (blk & 1) * SI_NSLOT);
+            auto read8 = [&](uint32_t off, float (&v)[8]) {  // 8 row groups of the wave's half at off
+                uint32_t tmp;
+                asm volatile("v_add_u32 %8, %9, %10\n\t"
+                             "ds_read_b32 %0, %8\n\t"
+                             "ds_read_b32 %1, %8 offset:64\n\t"
+                             "ds_read_b32 %2, %8 offset:128\n\t"
+                             "ds_read_b32 %3, %8 offset:192\n\t"
+                             "ds_read_b32 %4, %8 offset:256\n\t"
+                             "ds_read_b32 %5, %8 offset:320\n\t"
+                             "ds_read_b32 %6, %8 offset:384\n\t"
+                             "ds_read_b32 %7, %8 offset:448\n\t"
+                             "s_waitcnt lgkmcnt(0)"
+                             : "=v"(v[0]), "=v"(v[1]), "=v"(v[2]), "=v"(v[3]), "=v"(v[4]), "=v"(v[5]), "=v"(v[6]),
+                               "=v"(v[7]), "=&v"(tmp)
+                             : "s"(off), "v"(nbase)
+                             : "memory");
+            };
+            float nrm[8], err[8];
+            read8(nsoff + 512u * (uint32_t)wr, nrm);
+            read8(nsoff + 1280u + 512u * (uint32_t)wr, err);
+            float nmax = nrm[0], nsum = nrm[0], emx = err[0], esum = err[0];
+#pragma unroll
+            for (int j = 1; j < 8; j++) {
+                nmax = __builtin_fmaxf(nmax, nrm[j]), nsum += nrm[j];
+                emx = __builtin_fmaxf(emx, err[j]), esum += err[j];
+            }
+            const bool force = lane_force || !(nmax <= 0x1p60f) || nsum != nsum || !(emx <= 0x1p60f) || esum != esum;
+            // fast check per (query group g, query r of the lane's four): the largest exact
+            // int32 score of the lane's 8 rows, scaled once, + the bound of the lane's largest
+            // error and norm, against WS -- a superset test of every element (monotone roundings)
+            uint32_t wact = 0;
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                float4 k1v, k2v, kbv, csv, sv;
+                {
+                    const uint32_t ca = cbase + 4u * (uint32_t)(16 * g + qlane);
+                    const uint32_t sa = tbase + 1024u + 4u * (uint32_t)(16 * g + qlane);
+                    asm volatile("ds_read_b128 %0, %5\n\t"
+                                 "ds_read_b128 %1, %5 offset:512\n\t"
+                                 "ds_read_b128 %2, %5 offset:1536\n\t"
+                                 "ds_read_b128 %3, %5 offset:2048\n\t"
+                                 "ds_read_b128 %4, %6\n\t"
+                                 "s_waitcnt lgkmcnt(0)"
+                                 : "=v"(k1v), "=v"(k2v), "=v"(kbv), "=v"(csv), "=v"(sv)
+                                 : "v"(ca), "v"(sa)
+                                 : "memory");
+                }
+                const float k1r[4] = {k1v.x, k1v.y, k1v.z, k1v.w}, k2r[4] = {k2v.x, k2v.y, k2v.z, k2v.w};
+                const float kbr[4] = {kbv.x, kbv.y, kbv.z, kbv.w}, csr[4] = {csv.x, csv.y, csv.z, csv.w};
+                const float svr[4] = {sv.x, sv.y, sv.z, sv.w};
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    int mi = agpr_read(acc[g][0][r]);
+#pragma unroll
+                    for (int nr = 1; nr < 8; nr++) mi = max(mi, agpr_read(acc[g][nr][r]));
+                    const float m = (float)mi * csr[r];
+                    const float t = (m + __builtin_fmaf(emx, k1r[r], __builtin_fmaf(nmax, kbr[r], k2r[r]))) - svr[r];
+                    if (__ballot(force || t >= 0.f)) wact |= 1u << (4 * g + r);
+                }
+            }
+            if (wact != 0) {
+                // the wave's two tiles' live words (valid & allow)
+                uint64_t vm[2];
+                {
+                    uint4 vw, aw;
+                    uint32_t tmp;
+                    asm volatile("v_add_u32 %2, %3, %4\n\t"
+                                 "ds_read_b128 %0, %2 offset:1024\n\t"
+                                 "ds_read_b128 %1, %2 offset:1056\n\t"
+                                 "s_waitcnt lgkmcnt(0)"
+                                 : "=v"(vw), "=v"(aw), "=&v"(tmp)
+                                 : "s"(nsoff + 16u * (uint32_t)wr), "v"(sbase)
+                                 : "memory");
+                    const uint64_t words[2] = {((uint64_t)vw.y << 32) | vw.x, ((uint64_t)vw.w << 32) | vw.z};
+                    const uint64_t allows[2] = {((uint64_t)aw.y << 32) | aw.x, ((uint64_t)aw.w << 32) | aw.z};
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const uint64_t t = a.tile_begin + blk * 4 + 2 * wr + h;
+                        uint64_t m = t < a.tile_end ? readfirstlane64(words[h]) : 0ull;
+                        if (a.allow) {
+                            const uint64_t aw2 = t - a.allow_t0;
+                            m &= aw2 < a.allow_words ? readfirstlane64(allows[h]) : 0ull;
+                        }
+                        vm[h] = m;
+                    }
+                }
+                const uint64_t slot0 = (a.tile_begin + blk * 4 + 2 * wr) * 64;
+                // per active group gi = (g, r): lane l tests its column's 8 rows against query
+                // ql = 16 g + r + qlane of the wave, whose list is row l >> 4 of v (K3d's slow path)
+                for (uint32_t gw = wact; gw; gw &= gw - 1) {
+                    const int gi = __builtin_ctz(gw);
+                    float uv[8];  // the exact int32 scores as floats (|score| < 2^24)
+                    switch (gi) {
+#define WVG_SJ_GROUP(G)                                                                               \
+    case G:                                                                                           \
+        _Pragma("unroll") for (int nr = 0; nr < 8; nr++) uv[nr] = (float)agpr_read(acc[(G) >> 2][nr][(G) & 3]); \
+        break;
+                    WVG_SJ_GROUP(0) WVG_SJ_GROUP(1) WVG_SJ_GROUP(2) WVG_SJ_GROUP(3)
+                    WVG_SJ_GROUP(4) WVG_SJ_GROUP(5) WVG_SJ_GROUP(6) WVG_SJ_GROUP(7)
+                    WVG_SJ_GROUP(8) WVG_SJ_GROUP(9) WVG_SJ_GROUP(10) WVG_SJ_GROUP(11)
+                    WVG_SJ_GROUP(12) WVG_SJ_GROUP(13) WVG_SJ_GROUP(14) WVG_SJ_GROUP(15)
+#undef WVG_SJ_GROUP
+                    default: break;
+                    }
+                    const uint32_t ql = 16u * (uint32_t)(gi >> 2) + (uint32_t)(gi & 3) + (uint32_t)qlane;
+                    const uint32_t la = S.laddr + ql * (SCREEN_M * 8) + 8u * (uint32_t)(lane & 15);
+                    const uint32_t ta = tbase + 4u * ql;  // tau; sig + 1024
+                    const uint32_t ca = cbase + 4u * ql;  // A; K2 + 512, Emax + 1024, B + 1536, scale + 2048
+                    uint2 v2;
+                    float wt, ws, em, k1, k2, kbq, csq;
+                    asm volatile("ds_read_b64 %0, %7\n\t"
+                                 "ds_read_b32 %1, %8\n\t"
+                                 "ds_read_b32 %2, %8 offset:1024\n\t"
+                                 "ds_read_b32 %3, %9 offset:1024\n\t"
+                                 "ds_read_b32 %4, %9\n\t"
+                                 "ds_read_b32 %5, %9 offset:512\n\t"
+                                 "ds_read_b32 %6, %9 offset:1536\n\t"
+                                 "s_waitcnt lgkmcnt(0)"
+                                 : "=v"(v2), "=v"(wt), "=v"(ws), "=v"(em), "=v"(k1), "=v"(k2), "=v"(kbq)
+                                 : "v"(la), "v"(ta), "v"(ca)
+                                 : "memory");
+                    asm volatile("ds_read_b32 %0, %1 offset:2048\n\t"
+                                 "s_waitcnt lgkmcnt(0)"
+                                 : "=v"(csq)
+                                 : "v"(ca)
+                                 : "memory");
+                    uint64_t v = ((uint64_t)v2.y << 32) | v2.x;
+                    const int li = lane & 15;
+#pragma unroll
+                    for (int nr = 0; nr < 8; nr++) {
+                        const uint64_t m64 = ((vm[nr >> 2] >> (16 * (nr & 3))) & 0xFFFFull) * 0x0001000100010001ull;
+                        const float u = uv[nr] * csq + __builtin_fmaf(err[nr], k1, __builtin_fmaf(nrm[nr], kbq, k2));
+                        uint64_t pass = __ballot(!(u < ws)) & m64;
+                        while (pass) {
+                            const int j = __builtin_ctzll(pass);
+                            pass &= pass - 1;
+                            const int gq = j >> 4;
+                            const float lower =
+                                sc_lower(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(u), j)), cosine);
+                            float wtg = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wt), j));
+                            if (!(lower <= wtg)) continue;
+                            const uint64_t key = ((uint64_t)wvg_ord_f32(lower) << 32) |
+                                                 (uint32_t)(slot0 + 16u * (uint32_t)nr + (uint32_t)(j & 15));
+                            if (!(key < readlane64(v, 16 * gq + SCREEN_M - 1))) continue;
+                            const bool inrow = (lane >> 4) == gq;
+                            const int pos = __popcll(__ballot(inrow && v < key));
+                            const uint64_t sh = row_shr1_64(v);
+                            v = inrow ? (li > pos ? sh : (li == pos ? key : v)) : v;
+                            const uint64_t nk = readlane64(v, 16 * gq + K - 1);
+                            const uint64_t nm = readlane64(v, 16 * gq + SCREEN_M - 1);
+                            const float emg = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(em), j));
+                            if (nk != WVG_KEY_NONE) wtg = fminf(wtg, sc_tau_k(key_lower(nk), emg, cosine));
+                            if (nm != WVG_KEY_NONE) wtg = fminf(wtg, key_lower(nm));
+                            const float wsg = sc_sigma(wtg, cosine);
+                            wt = inrow ? wtg : wt;
+                            ws = inrow ? wsg : ws;
+                            pass &= ~(0xFFFFull << (16 * gq)) | __ballot(!(u < ws));
+                        }
+                    }
+                    const uint2 o2 = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+                    asm volatile("ds_write_b64 %0, %1" ::"v"(la), "v"(o2) : "memory");
+                    if (li == 0)
+                        asm volatile("ds_write_b32 %0, %1\n\t"
+                                     "ds_write_b32 %0, %2 offset:1024" ::"v"(ta), "v"(wt), "v"(ws)
+                                     : "memory");
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            }
+#pragma unroll
+            for (int g = 0; g < 4; g++)
+#pragma unroll
+                for (int nr = 0; nr < 8; nr++) acc[g][nr] = i32x4{0, 0, 0, 0};
+            // the next block's first K block: landed before the last barrier, not overwritten
+            // before the next block's second barrier
+            read_half(__builtin_amdgcn_readfirstlane(cbuf), 0, b0);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // per query of the block: the merge of its two row halves' lists (waves wq and wq + 2),
+    // the 16 smallest of 32 distinct-or-empty keys by rank (A's before B's on equal keys),
+    // straight to partials; wave w takes block queries 32 w .. 32 w + 31
+    for (int i = 0; i < 32; i++) {
+        const uint32_t bq = (uint32_t)(32 * w + i), q = q0 + bq;
+        if (q >= a.nq) break;
+        const uint32_t hq = bq >> 6, ql = bq & 63;
+        const uint64_t *la_ = lists + ((size_t)hq * 64 + ql) * M;        // wave hq (row half 0)
+        const uint64_t *lb_ = lists + ((size_t)(hq + 2) * 64 + ql) * M;  // wave hq + 2 (row half 1)
+        const int li = lane & 15;
+        const uint64_t x = lane < 16 ? la_[li] : (lane < 32 ? lb_[li] : WVG_KEY_NONE);
+        uint32_t rank = (uint32_t)li;
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const uint64_t ya = readlane64(x, j), yb = readlane64(x, 16 + j);
+            if (lane < 16) rank += yb < x ? 1u : 0u;
+            else if (lane < 32) rank += ya <= x ? 1u : 0u;
+        }
+        uint64_t *out = a.partials + ((size_t)q * a.nrr + rr) * M;
+        if (lane < 32 && rank < (uint32_t)M) out[rank] = x;
+        if (lane < 32 && rank == (uint32_t)(K - 1) && x != WVG_KEY_NONE) {
+            const float t = sc_tau_k(key_lower(x), cem[bq], cosine);
+            atomicMin(a.gbound + q, wvg_ord_f32(t));
+        }
+    }
+}
+
 constexpr int SF_WAVES = 8;  // K3f's waves per workgroup
 
 #ifdef WVG_TOOLS  // K3e and K3f: round-5 A/B variants (tools build only; the product runs K3d)
@@ -3138,14 +3579,25 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
                hipFuncSetAttribute(reinterpret_cast<const void *>(&screen_ar_kernel<12, 0, true>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, si_lds(si_nbuf(12))) == hipSuccess &&
                hipFuncSetAttribute(reinterpret_cast<const void *>(&screen_ar_kernel<16, 0, true>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, si_lds(si_nbuf(16))) == hipSuccess;
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, si_lds(si_nbuf(16))) == hipSuccess &&
+               hipFuncSetAttribute(reinterpret_cast<const void *>(&screen_i8_kernel<8>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, SJ_LDS) == hipSuccess &&
+               hipFuncSetAttribute(reinterpret_cast<const void *>(&screen_i8_kernel<12>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, SJ_LDS) == hipSuccess;
     }();
     (void)attr;
     // K3i on an int8 shadow; else K3d (queries resident in registers) where its template applies, else K3c
     void (*kern)(ScreenArgs) = kbn == 24 ? &screen_ar_kernel<24> : kbn == 16 ? &screen_ar_kernel<16> : nullptr;
+    // (d = 512 / 768: the 2 x 2-wave layout; d = 1024: 64 resident queries would not fit the
+    // registers, K3d's layout)
+    bool i8_22 = i8 && kbn <= 12;
+#ifdef WVG_TOOLS
+    if (tuning().screen_variant == 5) i8_22 = false;  // A/B: K3i on K3d's 1 x 4 layout
+#endif
     if (i8)
-        kern = kbn == 8 ? &screen_ar_kernel<8, 0, true>
-                        : (kbn == 12 ? &screen_ar_kernel<12, 0, true> : &screen_ar_kernel<16, 0, true>);
+        kern = i8_22 ? (kbn == 8 ? &screen_i8_kernel<8> : &screen_i8_kernel<12>)
+                     : (kbn == 8 ? &screen_ar_kernel<8, 0, true>
+                                 : (kbn == 12 ? &screen_ar_kernel<12, 0, true> : &screen_ar_kernel<16, 0, true>));
     bool k3f = false;
 #ifdef WVG_TOOLS
     bool k3g = false;
@@ -3199,9 +3651,9 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
         nqb = nq_pad / SG_BQ;
         a.nqb = nqb;
     }
-    const uint32_t lds = i8 ? si_lds(si_nbuf(kbn)) : k3g ? SG_LDS : kern ? SD_LDS : SC_LDS;
+    const uint32_t lds = i8_22 ? SJ_LDS : i8 ? si_lds(si_nbuf(kbn)) : k3g ? SG_LDS : kern ? SD_LDS : SC_LDS;
 #else
-    const uint32_t lds = i8 ? si_lds(si_nbuf(kbn)) : kern ? SD_LDS : SC_LDS;
+    const uint32_t lds = i8_22 ? SJ_LDS : i8 ? si_lds(si_nbuf(kbn)) : kern ? SD_LDS : SC_LDS;
 #endif
     const uint32_t threads = k3f ? SF_WAVES * 64 : kern ? SD_WAVES * 64 : SC_WAVES * 64;
     if (!kern) kern = &screen_kernel;
