@@ -141,7 +141,7 @@ struct HostPool {
 
 void parallel_for(uint32_t n, const std::function<void(uint32_t)> &f)
 {
-    static HostPool *pool = new HostPool(3);  // (never destroyed: its threads are detached)
+    static HostPool *pool = new HostPool(7);  // (never destroyed: its threads are detached)
     static std::mutex call_mu;                // one job at a time
     std::lock_guard<std::mutex> one(call_mu);
     {

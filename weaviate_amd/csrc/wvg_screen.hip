@@ -1887,34 +1887,50 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_i8_kernel(ScreenArgs 
             // fast check per (query group g, query r of the lane's four): the largest exact
             // int32 score of the lane's 8 rows, scaled once, + the bound of the lane's largest
             // error and norm, against WS -- a superset test of every element (monotone roundings)
+            // (query groups two at a time, their 8 (g, r) maxima as independent chains: with
+            // one wave per SIMD a group-by-group chain of dependent reads and maxima exposes
+            // every VALU latency; all 16 at once spill)
             uint32_t wact = 0;
 #pragma unroll
-            for (int g = 0; g < 4; g++) {
-                float4 k1v, k2v, kbv, csv, sv;
-                {
-                    const uint32_t ca = cbase + 4u * (uint32_t)(16 * g + qlane);
-                    const uint32_t sa = tbase + 1024u + 4u * (uint32_t)(16 * g + qlane);
-                    asm volatile("ds_read_b128 %0, %5\n\t"
-                                 "ds_read_b128 %1, %5 offset:512\n\t"
-                                 "ds_read_b128 %2, %5 offset:1536\n\t"
-                                 "ds_read_b128 %3, %5 offset:2048\n\t"
-                                 "ds_read_b128 %4, %6\n\t"
-                                 "s_waitcnt lgkmcnt(0)"
-                                 : "=v"(k1v), "=v"(k2v), "=v"(kbv), "=v"(csv), "=v"(sv)
-                                 : "v"(ca), "v"(sa)
-                                 : "memory");
-                }
-                const float k1r[4] = {k1v.x, k1v.y, k1v.z, k1v.w}, k2r[4] = {k2v.x, k2v.y, k2v.z, k2v.w};
-                const float kbr[4] = {kbv.x, kbv.y, kbv.z, kbv.w}, csr[4] = {csv.x, csv.y, csv.z, csv.w};
-                const float svr[4] = {sv.x, sv.y, sv.z, sv.w};
+            for (int gp = 0; gp < 2; gp++) {
+                int mi[2][4];
 #pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    int mi = agpr_read(acc[g][0][r]);
+                for (int h = 0; h < 2; h++)
 #pragma unroll
-                    for (int nr = 1; nr < 8; nr++) mi = max(mi, agpr_read(acc[g][nr][r]));
-                    const float m = (float)mi * csr[r];
-                    const float t = (m + __builtin_fmaf(emx, k1r[r], __builtin_fmaf(nmax, kbr[r], k2r[r]))) - svr[r];
-                    if (__ballot(force || t >= 0.f)) wact |= 1u << (4 * g + r);
+                    for (int r = 0; r < 4; r++) mi[h][r] = agpr_read(acc[2 * gp + h][0][r]);
+#pragma unroll
+                for (int nr = 1; nr < 8; nr++)
+#pragma unroll
+                    for (int h = 0; h < 2; h++)
+#pragma unroll
+                        for (int r = 0; r < 4; r++) mi[h][r] = max(mi[h][r], agpr_read(acc[2 * gp + h][nr][r]));
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int g = 2 * gp + h;
+                    float4 k1v, k2v, kbv, csv, sv;
+                    {
+                        const uint32_t ca = cbase + 4u * (uint32_t)(16 * g + qlane);
+                        const uint32_t sa = tbase + 1024u + 4u * (uint32_t)(16 * g + qlane);
+                        asm volatile("ds_read_b128 %0, %5\n\t"
+                                     "ds_read_b128 %1, %5 offset:512\n\t"
+                                     "ds_read_b128 %2, %5 offset:1536\n\t"
+                                     "ds_read_b128 %3, %5 offset:2048\n\t"
+                                     "ds_read_b128 %4, %6\n\t"
+                                     "s_waitcnt lgkmcnt(0)"
+                                     : "=v"(k1v), "=v"(k2v), "=v"(kbv), "=v"(csv), "=v"(sv)
+                                     : "v"(ca), "v"(sa)
+                                     : "memory");
+                    }
+                    const float k1r[4] = {k1v.x, k1v.y, k1v.z, k1v.w}, k2r[4] = {k2v.x, k2v.y, k2v.z, k2v.w};
+                    const float kbr[4] = {kbv.x, kbv.y, kbv.z, kbv.w}, csr[4] = {csv.x, csv.y, csv.z, csv.w};
+                    const float svr[4] = {sv.x, sv.y, sv.z, sv.w};
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const float t = ((float)mi[h][r] * csr[r] +
+                                         __builtin_fmaf(emx, k1r[r], __builtin_fmaf(nmax, kbr[r], k2r[r]))) -
+                                        svr[r];
+                        if (__ballot(force || t >= 0.f)) wact |= 1u << (4 * g + r);
+                    }
                 }
             }
             if (wact != 0) {
