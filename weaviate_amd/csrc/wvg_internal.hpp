@@ -339,7 +339,7 @@ hipError_t launch_scan_bq_emit(const ScanArgs &a, uint64_t *partials, int groups
 // whose count exceeded emit_cap sets oflow[q]).  gather: per query the kept keys
 // of all waves in wave (= docID) order into out [nq][out_cap], totals [nq].
 hipError_t launch_emit_prefix(const uint64_t *partials, uint32_t nq, uint32_t groups, uint32_t k, float *thr,
-                              hipStream_t s);
+                              hipStream_t s, uint32_t max_dist = 0);  // max_dist > 0: integer distances <= it
 hipError_t launch_emit_filter(uint64_t *emit, const uint32_t *emit_cnt, uint32_t emit_cap, const float *thr,
                               uint32_t nq, uint32_t groups, uint32_t waves_per_group, uint32_t *fcnt, uint32_t *oflow,
                               hipStream_t s);

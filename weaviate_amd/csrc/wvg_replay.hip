@@ -136,11 +136,115 @@ __global__ __launch_bounds__(PREFIX_WAVES * 64) void emit_prefix_kernel(const ui
     }
 }
 
+// The same thresholds from distance histograms (round 6): Hamming distances are
+// integers in [0, max_dist], and thr[g] needs only the R-th smallest DISTANCE of
+// ranges 0..g-1, not their keys.  (A) wave w counts its block's list entries
+// into its own LDS histogram; (B) each bin becomes the exclusive prefix over
+// the blocks (the counts of every range before the wave's block); (C) wave w
+// walks its block in order: v = the smallest bin whose cumulative count
+// reaches R (+inf while fewer than R), thr[g] = v, then list g's entries below
+// v join the histogram and v steps down while the count at or below v - 1
+// still reaches R.  The chain is the block's 16 lists, not ~3 x groups / 16
+// key-list merges (emit_prefix_kernel: 114 us per query at 100M x 1536,
+// profiles/r06/final/trace).  Identical thresholds: the R-th smallest
+// distance of the prefix, +inf below R entries.
+__global__ __launch_bounds__(PREFIX_WAVES * 64) void emit_prefix_hist_kernel(const uint64_t *partials, uint32_t groups,
+                                                                             uint32_t k, uint32_t nbins, float *thr)
+{
+    extern __shared__ uint32_t hist[];  // [PREFIX_WAVES][nbins]
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t qi = blockIdx.x;
+    const uint64_t *pq = partials + (size_t)qi * groups * k;
+    const uint32_t per = (groups + PREFIX_WAVES - 1) / PREFIX_WAVES;
+    const uint32_t g0 = min(groups, (uint32_t)wave * per), g1 = min(groups, g0 + per);
+    for (uint32_t i = threadIdx.x; i < PREFIX_WAVES * nbins; i += PREFIX_WAVES * 64) hist[i] = 0u;
+    __syncthreads();
+    uint32_t *h = hist + (size_t)wave * nbins;
+    auto bin_of = [&](uint64_t key) -> uint32_t {  // KEY_NONE -> nbins (no bin)
+        if (key == WVG_KEY_NONE) return nbins;
+        const float d = wvg_unord_f32((uint32_t)(key >> 32));
+        return d >= 0.f && d < (float)nbins ? (uint32_t)d : nbins;
+    };
+    for (uint32_t g = g0; g < g1; g++)  // (A)
+        for (uint32_t i = (uint32_t)lane; i < k; i += 64) {
+            const uint32_t b = bin_of(pq[(size_t)g * k + i]);
+            if (b < nbins) atomicAdd(&h[b], 1u);
+        }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nbins; b += PREFIX_WAVES * 64) {  // (B)
+        uint32_t run = 0;
+        for (int w = 0; w < PREFIX_WAVES; w++) {
+            const uint32_t c = hist[(size_t)w * nbins + b];
+            hist[(size_t)w * nbins + b] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+    // (C) v = the smallest bin whose cumulative count reaches k (nbins: none yet); cnt = the
+    // count at or below v (while v = nbins: every entry counted so far)
+    uint32_t v = nbins, cnt = 0;
+    auto find_v = [&]() {  // the first bin with cumulative count >= k, from scratch (wave-wide)
+        uint32_t base = 0;
+        v = nbins;
+        for (uint32_t b0 = 0; b0 < nbins; b0 += 64) {
+            const uint32_t b = b0 + (uint32_t)lane;
+            uint32_t c = b < nbins ? h[b] : 0u;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {  // inclusive prefix sum over the 64 lanes
+                const uint32_t o = (uint32_t)__shfl_up((int)c, off, 64);
+                if (lane >= off) c += o;
+            }
+            const uint64_t hit = __ballot(base + c >= k);
+            if (hit) {
+                const int l = __builtin_ctzll(hit);
+                v = b0 + (uint32_t)l;
+                cnt = base + (uint32_t)__shfl((int)c, l, 64);
+                return;
+            }
+            base += (uint32_t)__shfl((int)c, 63, 64);
+        }
+        cnt = base;
+    };
+    find_v();
+    for (uint32_t g = g0; g < g1; g++) {
+        if (lane == 0) thr[(size_t)qi * groups + g] = v < nbins ? (float)v : __builtin_inff();
+        uint32_t added = 0;
+        for (uint32_t i = (uint32_t)lane; i < k; i += 64) {
+            const uint32_t b = bin_of(pq[(size_t)g * k + i]);
+            const bool take = b < v;  // (v = nbins: every entry)
+            if (take) atomicAdd(&h[b], 1u);
+            added += (uint32_t)__popcll(__ballot(take));
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the wave's atomics landed
+        __builtin_amdgcn_wave_barrier();
+        if (v == nbins) {
+            if (cnt + added >= k) find_v();
+            else cnt += added;
+        } else {
+            cnt += added;
+            while (v > 0 && cnt - h[v] >= k) {  // (uniform: every lane reads the same words)
+                cnt -= h[v];
+                --v;
+            }
+        }
+    }
+}
+
 hipError_t launch_emit_prefix(const uint64_t *partials, uint32_t nq, uint32_t groups, uint32_t k, float *thr,
-                              hipStream_t s)
+                              hipStream_t s, uint32_t max_dist)
 {
     if (nq == 0 || groups == 0 || k == 0 || k > 256) return hipSuccess;
     const dim3 grid(nq), block(PREFIX_WAVES * 64);
+    const uint32_t nbins = max_dist + 1;
+    const size_t lds = (size_t)PREFIX_WAVES * nbins * 4;
+    if (max_dist > 0 && lds <= (size_t)(120u << 10)) {
+        static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&emit_prefix_hist_kernel),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 120 << 10) == hipSuccess;
+        (void)attr;
+        hipLaunchKernelGGL(emit_prefix_hist_kernel, grid, block, lds, s, partials, groups, k, nbins, thr);
+        return hipGetLastError();
+    }
     if (k <= 64)
         hipLaunchKernelGGL(emit_prefix_kernel<1>, grid, block, 0, s, partials, groups, k, thr);
     else if (k <= 128)
@@ -299,7 +403,7 @@ int run_emit(wvg_ctx *ctx, const ScanArgs &a0, int groups, uint32_t cap, bool ld
         if (arm.rc) return arm.rc;
         WVG_HIP(launch_scan_bq_emit(a, part, groups, lds, s));
     }
-    WVG_HIP(launch_emit_prefix(part, nq, (uint32_t)groups, R, (float *)(ws + w.thr), s));
+    WVG_HIP(launch_emit_prefix(part, nq, (uint32_t)groups, R, (float *)(ws + w.thr), s, 128u * a.nchunks));
     WVG_HIP(launch_emit_filter(a.emit, a.emit_cnt, cap, (const float *)(ws + w.thr), nq, (uint32_t)groups,
                                BQ_SCAN_WAVES, (uint32_t *)(ws + w.fcnt), tot + nq, s));
     WVG_HIP(launch_emit_gather(a.emit, (const uint32_t *)(ws + w.fcnt), cap, nq, waves, (uint64_t *)(ws + w.out),

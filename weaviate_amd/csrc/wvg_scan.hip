@@ -1050,15 +1050,37 @@ hipError_t launch_merge_pairs(const float *dists, const uint64_t *ids, uint64_t 
 // order through v_readlane, so every lane ends with the same, in-order sum.
 // One wave per row: the loads are coalesced and the 1536-long dependent add
 // chain runs on registers (one thread per row waited on a load per element).
-__device__ __forceinline__ float wave_seq_sum(float acc, float p, uint32_t cnt)
+// Round 6: the 64 values go through the wave's 256 bytes of LDS and every lane
+// adds them in element order from broadcast reads -- a readlane per element
+// made each add wait on a VALU -> SGPR -> VALU round trip (45 us per 1536-float
+// row, profiles/r06/final/trace: normalize_rows_kernel); the adds and their
+// order are unchanged, so the sum is the same bits.
+__device__ __forceinline__ float wave_seq_sum(float acc, float p, uint32_t cnt, float *lds)
 {
-    for (uint32_t l = 0; l < cnt; l++) acc = acc + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p), (int)l));
+    const uint32_t lane = threadIdx.x & 63u;
+    __builtin_amdgcn_wave_barrier();  // (the previous block's reads of lds are done)
+    lds[lane] = p;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's write landed
+    if (cnt == 64) {
+#pragma unroll
+        for (uint32_t l = 0; l < 64; l += 4) {
+            const float4 v = *reinterpret_cast<const float4 *>(lds + l);
+            acc = acc + v.x;
+            acc = acc + v.y;
+            acc = acc + v.z;
+            acc = acc + v.w;
+        }
+    } else {
+        for (uint32_t l = 0; l < cnt; l++) acc = acc + lds[l];
+    }
     return acc;
 }
 
 __global__ __launch_bounds__(256) void normalize_rows_kernel(const float *in, uint64_t n, uint32_t dim, float *out)
 {
     const uint32_t lane = threadIdx.x & 63u;
+    __shared__ __attribute__((aligned(16))) float sh[4][64];
     const uint64_t r = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // one row per wave
     if (r >= n) return;
     const float *v = in + r * dim;
@@ -1068,7 +1090,7 @@ __global__ __launch_bounds__(256) void normalize_rows_kernel(const float *in, ui
         const uint32_t i = b + lane;
         const float x = i < dim ? v[i] : 0.0f;
         const float p = x * x;
-        norm = wave_seq_sum(norm, p, dim - b < 64u ? dim - b : 64u);
+        norm = wave_seq_sum(norm, p, dim - b < 64u ? dim - b : 64u, sh[threadIdx.x >> 6]);
     }
     if (norm == 0.0f) {
         for (uint32_t i = lane; i < dim; i += 64) o[i] = 0.0f;
@@ -1257,6 +1279,7 @@ hipError_t launch_dist_keys(int metric, const float *q, const float *tiled, uint
 __global__ __launch_bounds__(256) void synth_rows_kernel(uint64_t seed_mixed, int dist, const uint64_t *ids,
                                                          uint64_t n, uint32_t dim, int normalize, float *out)
 {
+    __shared__ __attribute__((aligned(16))) float sh[4][64];
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t r = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= n) return;
@@ -1269,7 +1292,7 @@ __global__ __launch_bounds__(256) void synth_rows_kernel(uint64_t seed_mixed, in
             const uint32_t i = b + lane;
             const float v = i < dim ? wvg_synth_value(seed_mixed, row, i, dist) : 0.0f;
             const float p = v * v;
-            acc = wave_seq_sum(acc, p, dim - b < 64u ? dim - b : 64u);
+            acc = wave_seq_sum(acc, p, dim - b < 64u ? dim - b : 64u, sh[threadIdx.x >> 6]);
         }
         zero = acc == 0.0f;
         norm = (float)__builtin_sqrt((double)acc);
