@@ -166,11 +166,32 @@ __global__ __launch_bounds__(PREFIX_WAVES * 64) void emit_prefix_hist_kernel(con
         const float d = wvg_unord_f32((uint32_t)(key >> 32));
         return d >= 0.f && d < (float)nbins ? (uint32_t)d : nbins;
     };
-    for (uint32_t g = g0; g < g1; g++)  // (A)
-        for (uint32_t i = (uint32_t)lane; i < k; i += 64) {
-            const uint32_t b = bin_of(pq[(size_t)g * k + i]);
-            if (b < nbins) atomicAdd(&h[b], 1u);
-        }
+    // the block's lists as bins in registers when it has at most 16 (one range per CU:
+    // 256 ranges = 16 per wave), all loads issued at once; larger blocks read them twice
+    constexpr int CL = 16;
+    const uint32_t nl = g1 - g0;
+    const bool cached = nl <= (uint32_t)CL && k <= 256;
+    uint32_t rb[CL][4];
+    if (cached) {
+#pragma unroll
+        for (int L = 0; L < CL; L++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t i = (uint32_t)lane + 64u * (uint32_t)j;
+                rb[L][j] = ((uint32_t)L < nl && i < k) ? bin_of(pq[(size_t)(g0 + L) * k + i]) : nbins;
+            }
+#pragma unroll
+        for (int L = 0; L < CL; L++)  // (A)
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if (rb[L][j] < nbins) atomicAdd(&h[rb[L][j]], 1u);
+    } else {
+        for (uint32_t g = g0; g < g1; g++)  // (A)
+            for (uint32_t i = (uint32_t)lane; i < k; i += 64) {
+                const uint32_t b = bin_of(pq[(size_t)g * k + i]);
+                if (b < nbins) atomicAdd(&h[b], 1u);
+            }
+    }
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < nbins; b += PREFIX_WAVES * 64) {  // (B)
         uint32_t run = 0;
@@ -207,11 +228,12 @@ __global__ __launch_bounds__(PREFIX_WAVES * 64) void emit_prefix_hist_kernel(con
         cnt = base;
     };
     find_v();
-    for (uint32_t g = g0; g < g1; g++) {
+    auto step = [&](uint32_t g, auto &&bin_at) {  // thr[g], then range g's entries below v join
         if (lane == 0) thr[(size_t)qi * groups + g] = v < nbins ? (float)v : __builtin_inff();
         uint32_t added = 0;
-        for (uint32_t i = (uint32_t)lane; i < k; i += 64) {
-            const uint32_t b = bin_of(pq[(size_t)g * k + i]);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t b = bin_at(j);
             const bool take = b < v;  // (v = nbins: every entry)
             if (take) atomicAdd(&h[b], 1u);
             added += (uint32_t)__popcll(__ballot(take));
@@ -228,6 +250,17 @@ __global__ __launch_bounds__(PREFIX_WAVES * 64) void emit_prefix_hist_kernel(con
                 --v;
             }
         }
+    };
+    if (cached) {
+#pragma unroll
+        for (int L = 0; L < CL; L++)
+            if ((uint32_t)L < nl) step(g0 + (uint32_t)L, [&](int j) { return rb[L][j]; });
+    } else {
+        for (uint32_t g = g0; g < g1; g++)
+            step(g, [&](int j) {
+                const uint32_t i = (uint32_t)lane + 64u * (uint32_t)j;
+                return i < k ? bin_of(pq[(size_t)g * k + i]) : nbins;
+            });
     }
 }
 

@@ -1642,7 +1642,9 @@ constexpr int SJ_RING = SJ_NB * SD_STAGE + 2 * SI_NSLOT;
 constexpr int SJ_LDS = SJ_RING + SJ_LISTS + SD_WAVES * 64 * 4 * 2 + SD_BQ * 4 * 5;
 static_assert(SJ_LDS <= 160 * 1024, "K3i 2x2's LDS");
 
-template <int KBN>
+// DIAG (tools build only; 0 in the product): 4 = fast check but no slow path, 10 = no epilogue
+// (the accumulators consumed by one sum) -- timing only, results are not search results.
+template <int KBN, int DIAG = 0>
 __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_i8_kernel(ScreenArgs a)
 {
     static_assert(KBN <= 12, "64 resident queries x KBN K blocks must fit the registers");
@@ -1856,6 +1858,14 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_i8_kernel(ScreenArgs 
             __builtin_amdgcn_sched_barrier(0);
             // epilogue of row block blk: C layout row (query) 16 g + qlane + r, column (row)
             // 128 wr + 16 nr + (lane & 15)
+            if constexpr (DIAG == 10) {
+                int x = 0;
+#pragma unroll
+                for (int g = 0; g < 4; g++)
+#pragma unroll
+                    for (int nr = 0; nr < 8; nr++) x += agpr_read(acc[g][nr][0]);
+                if (x == 0x7FFFFFF1) a.partials[0] = 0;
+            } else {
             const uint32_t nsoff = (uint32_t)(SJ_NB * SD_STAGE + (blk & 1) * SI_NSLOT);
             auto read8 = [&](uint32_t off, float (&v)[8]) {  // 8 row groups of the wave's half at off
                 uint32_t tmp;
@@ -1933,7 +1943,7 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_i8_kernel(ScreenArgs 
                     }
                 }
             }
-            if (wact != 0) {
+            if (DIAG != 4 && wact != 0) {
                 // the wave's two tiles' live words (valid & allow)
                 uint64_t vm[2];
                 {
@@ -2041,6 +2051,7 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_i8_kernel(ScreenArgs 
                 }
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             }
+            }  // (DIAG != 10)
 #pragma unroll
             for (int g = 0; g < 4; g++)
 #pragma unroll
@@ -3614,6 +3625,13 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
         kern = i8_22 ? (kbn == 8 ? &screen_i8_kernel<8> : &screen_i8_kernel<12>)
                      : (kbn == 8 ? &screen_ar_kernel<8, 0, true>
                                  : (kbn == 12 ? &screen_ar_kernel<12, 0, true> : &screen_ar_kernel<16, 0, true>));
+#ifdef WVG_TOOLS
+    if (i8_22 && kbn == 12 && (tuning().screen_diag == 4 || tuning().screen_diag == 10)) {  // K3i diagnostics
+        kern = tuning().screen_diag == 4 ? &screen_i8_kernel<12, 4> : &screen_i8_kernel<12, 10>;
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  SJ_LDS);
+    }
+#endif
     bool k3f = false;
 #ifdef WVG_TOOLS
     bool k3g = false;
