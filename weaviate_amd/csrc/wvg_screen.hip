@@ -1991,30 +1991,43 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_i8_kernel(ScreenArgs 
                     const uint32_t la = S.laddr + ql * (SCREEN_M * 8) + 8u * (uint32_t)(lane & 15);
                     const uint32_t ta = tbase + 4u * ql;  // tau; sig + 1024
                     const uint32_t ca = cbase + 4u * ql;  // A; K2 + 512, Emax + 1024, B + 1536, scale + 2048
-                    uint2 v2;
-                    float wt, ws, em, k1, k2, kbq, csq;
-                    asm volatile("ds_read_b64 %0, %7\n\t"
-                                 "ds_read_b32 %1, %8\n\t"
-                                 "ds_read_b32 %2, %8 offset:1024\n\t"
-                                 "ds_read_b32 %3, %9 offset:1024\n\t"
-                                 "ds_read_b32 %4, %9\n\t"
-                                 "ds_read_b32 %5, %9 offset:512\n\t"
-                                 "ds_read_b32 %6, %9 offset:1536\n\t"
+                    // u of the group's 8 row groups first: a group the coarse fast check let
+                    // through often has no element at or above WS, and then its list and
+                    // thresholds are neither read nor written back
+                    float ws, k1, k2, kbq, csq;
+                    asm volatile("ds_read_b32 %0, %5 offset:1024\n\t"
+                                 "ds_read_b32 %1, %6\n\t"
+                                 "ds_read_b32 %2, %6 offset:512\n\t"
+                                 "ds_read_b32 %3, %6 offset:1536\n\t"
+                                 "ds_read_b32 %4, %6 offset:2048\n\t"
                                  "s_waitcnt lgkmcnt(0)"
-                                 : "=v"(v2), "=v"(wt), "=v"(ws), "=v"(em), "=v"(k1), "=v"(k2), "=v"(kbq)
-                                 : "v"(la), "v"(ta), "v"(ca)
+                                 : "=v"(ws), "=v"(k1), "=v"(k2), "=v"(kbq), "=v"(csq)
+                                 : "v"(ta), "v"(ca)
                                  : "memory");
-                    asm volatile("ds_read_b32 %0, %1 offset:2048\n\t"
+                    float uu[8];
+                    uint64_t any = 0;
+#pragma unroll
+                    for (int nr = 0; nr < 8; nr++) {
+                        const uint64_t m64 = ((vm[nr >> 2] >> (16 * (nr & 3))) & 0xFFFFull) * 0x0001000100010001ull;
+                        uu[nr] = uv[nr] * csq + __builtin_fmaf(err[nr], k1, __builtin_fmaf(nrm[nr], kbq, k2));
+                        any |= __ballot(!(uu[nr] < ws)) & m64;
+                    }
+                    if (!any) continue;
+                    uint2 v2;
+                    float wt, em;
+                    asm volatile("ds_read_b64 %0, %3\n\t"
+                                 "ds_read_b32 %1, %4\n\t"
+                                 "ds_read_b32 %2, %5 offset:1024\n\t"
                                  "s_waitcnt lgkmcnt(0)"
-                                 : "=v"(csq)
-                                 : "v"(ca)
+                                 : "=v"(v2), "=v"(wt), "=v"(em)
+                                 : "v"(la), "v"(ta), "v"(ca)
                                  : "memory");
                     uint64_t v = ((uint64_t)v2.y << 32) | v2.x;
                     const int li = lane & 15;
 #pragma unroll
                     for (int nr = 0; nr < 8; nr++) {
                         const uint64_t m64 = ((vm[nr >> 2] >> (16 * (nr & 3))) & 0xFFFFull) * 0x0001000100010001ull;
-                        const float u = uv[nr] * csq + __builtin_fmaf(err[nr], k1, __builtin_fmaf(nrm[nr], kbq, k2));
+                        const float u = uu[nr];
                         uint64_t pass = __ballot(!(u < ws)) & m64;
                         while (pass) {
                             const int j = __builtin_ctzll(pass);
