@@ -1040,12 +1040,13 @@ static int wvg::search_batch_filtered(wvg_corpus *c, const std::vector<wvg_searc
         std::memcpy(row + (tb[i] - TB), batch[i]->allow + wb + tb[i], (te[i] - tb[i]) * 8);
         std::memset(row + (te[i] - TB), 0, (TE - te[i]) * 8);
     };
-    // large windows (e.g. 16 x 125 KB for 10 % lists over 1M rows) on several host threads
-    auto fill_windows = [&](uint64_t *win) {
-        if ((size_t)B * W * 8 >= ((size_t)256 << 10) && B > 1)
-            parallel_for(B, [&](uint32_t i) { fill_window(win, i); });
+    // windows of queries [i0, i1); large ones (e.g. 16 x 125 KB for 10 % lists over 1M rows)
+    // on several host threads
+    auto fill_windows = [&](uint64_t *win, uint32_t i0, uint32_t i1) {
+        if ((size_t)(i1 - i0) * W * 8 >= ((size_t)128 << 10) && i1 - i0 > 1)
+            parallel_for(i1 - i0, [&](uint32_t i) { fill_window(win, i0 + i); });
         else
-            for (uint32_t i = 0; i < B; i++) fill_window(win, i);
+            for (uint32_t i = i0; i < i1; i++) fill_window(win, i);
     };
     // per-query allow windows: K1Q's filtered variant (d = 128 / 768, L2 / dot / cosine) or the COS K1
     SearchPlan p = plan_search(c, B, k, nullptr, 0, true, false);
@@ -1086,8 +1087,15 @@ static int wvg::search_batch_filtered(wvg_corpus *c, const std::vector<wvg_searc
         wbig.resize((size_t)B * W);
         win = wbig.data();
     }
-    fill_windows(win);
-    WVG_HIP(hipMemcpyAsync(b + o_allow, win, (size_t)B * W * 8, hipMemcpyHostToDevice, s));
+    // two halves: the first half's copy runs while the second half is filled
+    const uint32_t hB = (size_t)B * W * 8 >= ((size_t)512 << 10) ? B / 2 : 0;
+    if (hB > 0) {
+        fill_windows(win, 0, hB);
+        WVG_HIP(hipMemcpyAsync(b + o_allow, win, (size_t)hB * W * 8, hipMemcpyHostToDevice, s));
+    }
+    fill_windows(win, hB, B);
+    WVG_HIP(hipMemcpyAsync(b + o_allow + (size_t)hB * W * 8, win + (size_t)hB * W, (size_t)(B - hB) * W * 8,
+                           hipMemcpyHostToDevice, s));
     rc = run_search(c, b + o_q, qpitch, B, k, (const uint64_t *)(b + o_allow), p, (uint64_t *)(b + o_part),
                     (uint64_t *)(b + o_ids), (float *)(b + o_d), (uint32_t *)(b + o_cnt), s);
     if (rc) return rc;
