@@ -442,13 +442,21 @@ int wvgx_single_timing(uint64_t *out5, int reset)
     return WVG_OK;
 }
 
+int wvgx_filtered_timing(uint64_t *out5, int reset)
+{
+    if (!out5) return WVG_ERR_INVALID;
+    wvg::filtered_timing_read(out5, reset != 0);
+    return WVG_OK;
+}
+
 // A/B knob of the tools build (not part of include/wvgpu.h): 0 = K1 scan variant,
 // 1 = K1 resident workgroups per CU, ... 7 = K8 ADC variant, 8 = query-stream merge wait (us),
 // 9 = serpentine scan order, 10 = K3b row-range length, 11 = K1 load policy, 12 = K3b SIMD pairing,
 // 13 = K3b partner priority, 14 = PQ encode min3 argmin, 15 = co-scheduled PQ / BQ batches, 16 = co-scheduled BQ workgroups per CU, 17 = K3c row-range length,
 // 18 = K3c diagnostics (results not distances), 19 = K3c split launch,
 // 20 = screen kernel (0 K3d where it applies, 1 K3c), 21 = screen pilot seed, 22 = exact seeds between
-// screen phases, 23 = K3b pilot tiles, 24 = single-query host path.  Returns the previous value.
+// screen phases, 23 = K3b pilot tiles, 24 = single-query host path, ..., 29 / 30 = K3i warm-up range
+// blocks (first / second phase), 31 = filtered batches' windows from pinned staging.  Returns the previous value.
 int wvgx_set_tuning(int key, int value)
 {
     Tuning &t = tuning();
@@ -540,6 +548,15 @@ int wvgx_set_tuning(int key, int value)
     } else if (key == 28 && value > 0) {
         old = t.gather_div;
         t.gather_div = value;
+    } else if (key == 29) {
+        old = t.screen_warm;
+        t.screen_warm = value;
+    } else if (key == 30) {
+        old = t.screen_warm2;
+        t.screen_warm2 = value;
+    } else if (key == 31) {
+        old = t.filter_zc;
+        t.filter_zc = value;
     }
     return old;
 }

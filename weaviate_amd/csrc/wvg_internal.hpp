@@ -363,6 +363,7 @@ void screen_counters(uint64_t out[4], bool reset);
 void single_counters(uint64_t out[4], bool reset);
 void coalesce_counters(uint64_t out[4], bool reset);
 void single_timing_read(uint64_t out[5], bool reset);
+void filtered_timing_read(uint64_t out[5], bool reset);
 #endif
 hipError_t launch_shadow_build(const float *tiled, uint32_t dim, uint64_t t0, uint64_t t1, void *shadow, float *norms,
                                uint32_t *nmax, hipStream_t s);
@@ -479,6 +480,11 @@ struct Tuning {
     int gather_div = 4;      // coalescer gathering window: at most the last batch's run time / this (key 28;
                              // with K1Q batches 4 beat 8: 16 callers 47.6-54.7k -> 64.7k QPS,
                              // profiles/r05/coalesce/gather_window_k1q.txt)
+    int screen_warm = 32;    // K3i (tuning key 29): row blocks per first-phase range (short warm-up ranges
+                             // screened against the pilot's bound); 0 = equal ranges (A/B)
+    int filter_zc = 1;       // filtered coalesced batches (tuning key 31): bit 0 = K1Q reads the allow
+                             // windows from pinned staging (no copy); 0 = copied to HBM first (A/B)
+    int screen_warm2 = 0;    // K3i (tuning key 30): row blocks per second-phase range; 0 = the rest uniform
     int k1_mq = 4;           // F32 co-scheduled batches (tuning key 27): queries per K1Q workgroup, 2 or 4
                              // (0 = the COS K1, one query per workgroup)
     int screen_pilot_screen = 0;  // K3c/K3d (tuning key 26): tiles of the SCREEN pilot -- the bf16 screen itself over

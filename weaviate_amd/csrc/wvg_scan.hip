@@ -318,16 +318,37 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_kernel(ScanArgs a, u
     group_combine_store<E, SCAN_WAVES>(tk, partials + ((size_t)qi * G + rng) * a.k);
 }
 
-// K1Q's per-query tile masks: the validity word, and with FILT each query's own
-// allow word (a function, not a lambda: an out-of-line lambda once moved a
-// kernel's arguments to scratch).
-template <int Q, bool FILT>
-__device__ __forceinline__ void mq_tile_masks(const ScanArgs &a, uint64_t t, const uint32_t (&qix)[Q],
-                                              uint64_t (&mq)[Q])
+// K1Q's tile masks: the validity word for each of the Q queries (FILT ANDs each
+// query's own allow word, mq_allow_chunk) -- a function, not a lambda: an
+// out-of-line lambda once moved a kernel's arguments to scratch, DESIGN.md section 5.
+template <int Q>
+__device__ __forceinline__ void mq_tile_masks(const ScanArgs &a, uint64_t t, uint64_t (&mq)[Q])
 {
     const uint64_t v = a.valid[t];
 #pragma unroll
-    for (int j = 0; j < Q; j++) mq[j] = FILT ? tile_mask(a, t, qix[j]) : v;
+    for (int j = 0; j < Q; j++) mq[j] = v;
+}
+
+// K1Q FILT's allow words of iterations [c0, c0 + 64) of a wave's tile loop: lane
+// l holds (lo, hi) of query j's word for iteration c0 + l (0 past the range or the
+// window), one vector load per query for up to 64 tiles -- the windows may sit in
+// pinned host memory (ScanArgs::allow over the bus), where a tile-ahead scalar
+// prefetch left most of the bus latency exposed (profiles/r06/host_api/)
+template <int Q>
+__device__ __forceinline__ void mq_allow_chunk(const ScanArgs &a, uint64_t t0, uint64_t t1, bool rev, uint64_t c0,
+                                               int lane, const uint32_t (&qix)[Q], uint32_t (&lo)[Q],
+                                               uint32_t (&hi)[Q])
+{
+    const uint64_t idx = c0 + (uint64_t)lane;
+    const uint64_t t = rev ? t1 - 1 - idx : t0 + idx;
+    const uint64_t w = t - a.allow_t0;
+    const bool ok = idx < t1 - t0 && w < a.allow_words;
+#pragma unroll
+    for (int j = 0; j < Q; j++) {
+        const uint64_t v = ok ? a.allow[(uint64_t)qix[j] * a.allow_qstride + w] : 0ull;
+        lo[j] = (uint32_t)v;
+        hi[j] = (uint32_t)(v >> 32);
+    }
 }
 
 // K1Q (round 5): co-scheduled small batches with Q queries per workgroup.  The
@@ -368,14 +389,25 @@ __global__ __launch_bounds__(SCAN_WAVES * 64) void scan_f32_mq_kernel(ScanArgs a
     const uint64_t n = t1 - t0;
     // per-query tile masks (scalar; the next tile's prefetched): the validity word, and with
     // FILT each query's own allow word
+    // (FILT: the validity words so, the allow words 64 tiles at a time from mq_allow_chunk)
     uint64_t mq_next[Q];
-    if (n) mq_tile_masks<Q, FILT>(a, rev ? t1 - 1 : t0, qix, mq_next);
+    if (n) mq_tile_masks<Q>(a, rev ? t1 - 1 : t0, mq_next);
+    uint32_t alo[Q], ahi[Q];
+    if (FILT && n) mq_allow_chunk<Q>(a, t0, t1, rev, 0, lane, qix, alo, ahi);
     for (uint64_t i = 0; i < n; ++i) {
         const uint64_t t = rev ? t1 - 1 - i : t0 + i;
         uint64_t mq[Q];
 #pragma unroll
         for (int j = 0; j < Q; j++) mq[j] = mq_next[j];
-        if (i + 1 < n) mq_tile_masks<Q, FILT>(a, rev ? t - 1 : t + 1, qix, mq_next);
+        if (i + 1 < n) mq_tile_masks<Q>(a, rev ? t - 1 : t + 1, mq_next);
+        if (FILT) {
+            const int il = (int)(i & 63u);
+            if (il == 0 && i > 0) mq_allow_chunk<Q>(a, t0, t1, rev, i, lane, qix, alo, ahi);
+#pragma unroll
+            for (int j = 0; j < Q; j++)
+                mq[j] &= ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)ahi[j], il) << 32) |
+                         (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)alo[j], il);
+        }
         uint64_t m = 0ull;
 #pragma unroll
         for (int j = 0; j < Q; j++) m |= mq[j];

@@ -441,6 +441,9 @@ struct ScreenArgs {
     const float *kb, *css;    // K3i: [nq_pad] row-norm coefficient B, score scale S * Sq
     uint32_t nq, k, nqb, nrr;
     uint32_t rr0, nrr_l;      // this launch's ranges: [rr0, rr0 + nrr_l) of nrr
+    uint32_t rsplit[2];       // (K3i) ranges [0, rsplit[0]) split row blocks [0, bsplit[0]), ranges
+    uint64_t bsplit[2];       // [rsplit[0], rsplit[1]) blocks [bsplit[0], bsplit[1]) (short warm-up
+                              // ranges), the others the rest; rsplit[0] = 0: nrr equal ranges
     int cosine;
 #ifdef WVG_TOOLS
     int diag;                 // Tuning::screen_diag
@@ -448,6 +451,30 @@ struct ScreenArgs {
     uint32_t *gbound;         // [nq] ordered tau; 0xFFFFFFFF = none yet
     uint64_t *partials;       // [nq][nrr][SCREEN_M]
 };
+
+// Row blocks [b0, b1) of range rr (ScreenArgs::rsplit; the host checks
+// 0 < rsplit[0] <= rsplit[1] < nrr and 0 < bsplit[0] <= bsplit[1] < nblk)
+__device__ __forceinline__ void sc_range(const ScreenArgs &a, uint64_t nblk, uint32_t rr, uint64_t &b0, uint64_t &b1)
+{
+    uint64_t lo = 0, hi = nblk, r = rr, n = a.nrr;
+    if (a.rsplit[0] != 0) {
+        if (rr < a.rsplit[0]) {
+            hi = a.bsplit[0];
+            n = a.rsplit[0];
+        } else if (rr < a.rsplit[1]) {
+            lo = a.bsplit[0];
+            hi = a.bsplit[1];
+            r = rr - a.rsplit[0];
+            n = a.rsplit[1] - a.rsplit[0];
+        } else {
+            lo = a.bsplit[1];
+            r = rr - a.rsplit[1];
+            n = a.nrr - a.rsplit[1];
+        }
+    }
+    b0 = lo + (hi - lo) * r / n;
+    b1 = lo + (hi - lo) * (r + 1) / n;
+}
 
 // lower bound (distance space) of a survivor's u; NaN u (a non-finite row or
 // query) -> -inf: always a candidate, rescored exactly
@@ -1067,7 +1094,8 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_ar_kernel(ScreenArgs 
     }
     const uint64_t ntiles = a.tile_end - a.tile_begin;
     const uint64_t nblk = (ntiles + 3) / 4;
-    const uint64_t blk0 = nblk * rr / a.nrr, blk1 = nblk * (rr + 1) / a.nrr;
+    uint64_t blk0, blk1;
+    sc_range(a, nblk, rr, blk0, blk1);
     const uint32_t q0 = qb * SD_BQ;
 
     for (int i = tid; i < SD_BQ; i += SD_WAVES * 64) {
@@ -1642,7 +1670,8 @@ constexpr int SJ_RING = SJ_NB * SD_STAGE + 2 * SI_NSLOT;
 constexpr int SJ_LDS = SJ_RING + SJ_LISTS + SD_WAVES * 64 * 4 * 2 + SD_BQ * 4 * 5;
 static_assert(SJ_LDS <= 160 * 1024, "K3i 2x2's LDS");
 
-// DIAG (tools build only; 0 in the product): 4 = fast check but no slow path, 10 = no epilogue
+// DIAG (tools build only; 0 in the product): 16 = counters (wave row blocks, active groups,
+// inserts, groups with a passing element), 4 = fast check but no slow path, 10 = no epilogue
 // (the accumulators consumed by one sum) -- timing only, results are not search results.
 template <int KBN, int DIAG = 0>
 __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_i8_kernel(ScreenArgs a)
@@ -1659,6 +1688,8 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_i8_kernel(ScreenArgs 
     float *ccs = ckb + SD_BQ;                                             // score scale
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    uint32_t n_blk = 0, n_grp = 0, n_pass = 0, n_ins = 0;  // (DIAG 16, tools)
+    (void)n_blk, (void)n_grp, (void)n_pass, (void)n_ins;
     const int wq = w & 1, wr = w >> 1;  // query half (64 queries), row half (tiles 2 wr, 2 wr + 1)
     const int K = (int)a.k, M = SCREEN_M;
     const int cosine = a.cosine;
@@ -1674,7 +1705,8 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_i8_kernel(ScreenArgs 
     }
     const uint64_t ntiles = a.tile_end - a.tile_begin;
     const uint64_t nblk = (ntiles + 3) / 4;
-    const uint64_t blk0 = nblk * rr / a.nrr, blk1 = nblk * (rr + 1) / a.nrr;
+    uint64_t blk0, blk1;
+    sc_range(a, nblk, rr, blk0, blk1);
     const uint32_t q0 = qb * SD_BQ;
 
     for (int i = tid; i < SD_BQ; i += SD_WAVES * 64) {
@@ -1894,6 +1926,7 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_i8_kernel(ScreenArgs 
                 emx = __builtin_fmaxf(emx, err[j]), esum += err[j];
             }
             const bool force = lane_force || !(nmax <= 0x1p60f) || nsum != nsum || !(emx <= 0x1p60f) || esum != esum;
+            if constexpr (DIAG == 16) n_blk++;
             // fast check per (query group g, query r of the lane's four): the largest exact
             // int32 score of the lane's 8 rows, scaled once, + the bound of the lane's largest
             // error and norm, against WS -- a superset test of every element (monotone roundings)
@@ -1974,6 +2007,7 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_i8_kernel(ScreenArgs 
                 // ql = 16 g + r + qlane of the wave, whose list is row l >> 4 of v (K3d's slow path)
                 for (uint32_t gw = wact; gw; gw &= gw - 1) {
                     const int gi = __builtin_ctz(gw);
+                    if constexpr (DIAG == 16) n_grp++;
                     float uv[8];  // the exact int32 scores as floats (|score| < 2^24)
                     switch (gi) {
 #define WVG_SJ_GROUP(G)                                                                               \
@@ -2013,6 +2047,7 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_i8_kernel(ScreenArgs 
                         any |= __ballot(!(uu[nr] < ws)) & m64;
                     }
                     if (!any) continue;
+                    if constexpr (DIAG == 16) n_pass++;
                     uint2 v2;
                     float wt, em;
                     asm volatile("ds_read_b64 %0, %3\n\t"
@@ -2040,6 +2075,7 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_i8_kernel(ScreenArgs 
                             const uint64_t key = ((uint64_t)wvg_ord_f32(lower) << 32) |
                                                  (uint32_t)(slot0 + 16u * (uint32_t)nr + (uint32_t)(j & 15));
                             if (!(key < readlane64(v, 16 * gq + SCREEN_M - 1))) continue;
+                            if constexpr (DIAG == 16) n_ins++;
                             const bool inrow = (lane >> 4) == gq;
                             const int pos = __popcll(__ballot(inrow && v < key));
                             const uint64_t sh = row_shr1_64(v);
@@ -2075,6 +2111,16 @@ __global__ __launch_bounds__(SD_WAVES * 64, 1) void screen_i8_kernel(ScreenArgs 
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef WVG_TOOLS
+    if constexpr (DIAG == 16) {
+        if (lane == 0) {
+            atomicAdd(&g_screen_ctr[0], (unsigned long long)n_blk);
+            atomicAdd(&g_screen_ctr[1], (unsigned long long)n_grp);
+            atomicAdd(&g_screen_ctr[2], (unsigned long long)n_ins);
+            atomicAdd(&g_screen_ctr[3], (unsigned long long)n_pass);
+        }
+    }
+#endif
     __syncthreads();
     // per query of the block: the merge of its two row halves' lists (waves wq and wq + 2),
     // the 16 smallest of 32 distinct-or-empty keys by rank (A's before B's on equal keys),
@@ -3639,8 +3685,10 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
                      : (kbn == 8 ? &screen_ar_kernel<8, 0, true>
                                  : (kbn == 12 ? &screen_ar_kernel<12, 0, true> : &screen_ar_kernel<16, 0, true>));
 #ifdef WVG_TOOLS
-    if (i8_22 && kbn == 12 && (tuning().screen_diag == 4 || tuning().screen_diag == 10)) {  // K3i diagnostics
-        kern = tuning().screen_diag == 4 ? &screen_i8_kernel<12, 4> : &screen_i8_kernel<12, 10>;
+    if (i8_22 && kbn == 12 && (tuning().screen_diag == 4 || tuning().screen_diag == 10 || tuning().screen_diag == 16)) {
+        kern = tuning().screen_diag == 4    ? &screen_i8_kernel<12, 4>
+               : tuning().screen_diag == 10 ? &screen_i8_kernel<12, 10>
+                                            : &screen_i8_kernel<12, 16>;  // K3i diagnostics
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   SJ_LDS);
     }
@@ -3719,6 +3767,7 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
         // valid bound, as the K3b pilot's exact k-th over its rows (which cost ~0.76 ms
         // per 1024-query batch: K3b's start-up on a short range)
         ScreenArgs f = a;
+        f.rsplit[0] = 0;
         f.tile_end = L.tile_begin + sp_tiles;
         f.nrr = sp_rr;
         f.rr0 = 0;
@@ -3747,6 +3796,21 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
     if (split == 0) nph = 1;
     if (split == 2 && nph > 2) nph = 2;
     bounds[nph] = L.nrr;
+    // K3i warm-up (round 6): the first phase's ranges cover only screen_warm row blocks each
+    // (8k rows at 32), so few rows are screened against the pilot's loose bound before the
+    // first exact seed -- the survivors of that phase were most of the screen's list
+    // insertions (tools counters: ~1.1k of ~1.2k per query at 10M x 768)
+    const uint64_t nblk_all = (L.tile_end - L.tile_begin + 3) / 4;
+    if (i8 && nph >= 2 && tuning().screen_warm > 0 && (uint64_t)bounds[1] * tuning().screen_warm * 4 <= nblk_all) {
+        a.rsplit[0] = a.rsplit[1] = bounds[1];
+        a.bsplit[0] = a.bsplit[1] = (uint64_t)bounds[1] * (uint64_t)tuning().screen_warm;
+        // the second phase's ranges: screen_warm2 row blocks each
+        const uint64_t b2 = nph >= 3 ? a.bsplit[0] + (uint64_t)(bounds[2] - bounds[1]) * (uint64_t)tuning().screen_warm2 : 0;
+        if (nph >= 3 && tuning().screen_warm2 > 0 && bounds[2] < L.nrr && b2 * 2 <= nblk_all) {
+            a.rsplit[1] = bounds[2];
+            a.bsplit[1] = b2;
+        }
+    }
     // seeds between phases: the exact k-th over the earlier ranges' candidates
     // (rescored with the final rescore's distances) where the rows are at hand
     const bool rows = L.data != nullptr;

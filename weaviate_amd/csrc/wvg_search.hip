@@ -611,6 +611,21 @@ void single_timing_read(uint64_t out[5], bool reset)
     for (int i = 0; i < 5; i++) out[i] = reset ? g_stime[i].exchange(0) : g_stime[i].load();
 }
 #define WVG_STAMP(i) tstamp[i] = std::chrono::steady_clock::now()
+// host time of filtered coalesced batches (wvgx_filtered_timing): ns summed over
+// batches -- [0] entry -> queries staged, [1] windows filled (+ copies issued),
+// [2] the launch call, [3] the wait for the results; [4] batches
+static std::atomic<uint64_t> g_ftime[5];
+static void filtered_timing(const std::chrono::steady_clock::time_point (&t)[5])
+{
+    for (int i = 0; i < 4; i++)
+        g_ftime[i].fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t[i + 1] - t[i]).count(),
+                             std::memory_order_relaxed);
+    g_ftime[4].fetch_add(1, std::memory_order_relaxed);
+}
+void filtered_timing_read(uint64_t out[5], bool reset)
+{
+    for (int i = 0; i < 5; i++) out[i] = reset ? g_ftime[i].exchange(0) : g_ftime[i].load();
+}
 #else
 inline void single_counter(int, bool) {}
 inline void coalesce_counter(size_t, uint64_t) {}
@@ -1011,6 +1026,10 @@ static int wvg::search_batch(wvg_corpus *c, const float *queries, uint32_t nq, u
 static int wvg::search_batch_filtered(wvg_corpus *c, const std::vector<wvg_search_request *> &batch, uint32_t k,
                                       uint64_t *out_ids, float *out_dists, uint32_t *out_counts)
 {
+#ifdef WVG_TOOLS
+    std::chrono::steady_clock::time_point tstamp[5];
+#endif
+    WVG_STAMP(0);
     const uint32_t B = (uint32_t)batch.size(), d = c->dim;
     // every query's window [tb_i, te_i) and their union [TB, TE)
     std::vector<uint64_t> tb(B), te(B);
@@ -1087,23 +1106,39 @@ static int wvg::search_batch_filtered(wvg_corpus *c, const std::vector<wvg_searc
         wbig.resize((size_t)B * W);
         win = wbig.data();
     }
-    // two halves: the first half's copy runs while the second half is filled
-    const uint32_t hB = (size_t)B * W * 8 >= ((size_t)512 << 10) ? B / 2 : 0;
-    if (hB > 0) {
-        fill_windows(win, 0, hB);
-        WVG_HIP(hipMemcpyAsync(b + o_allow, win, (size_t)hB * W * 8, hipMemcpyHostToDevice, s));
+    WVG_STAMP(1);
+    const uint64_t *d_allow = (const uint64_t *)(b + o_allow);
+    if (!wbig.empty() || (tuning().filter_zc & 1) == 0) {
+        // two halves: the first half's copy runs while the second half is filled
+        const uint32_t hB = (size_t)B * W * 8 >= ((size_t)512 << 10) ? B / 2 : 0;
+        if (hB > 0) {
+            fill_windows(win, 0, hB);
+            WVG_HIP(hipMemcpyAsync(b + o_allow, win, (size_t)hB * W * 8, hipMemcpyHostToDevice, s));
+        }
+        fill_windows(win, hB, B);
+        WVG_HIP(hipMemcpyAsync(b + o_allow + (size_t)hB * W * 8, win + (size_t)hB * W, (size_t)(B - hB) * W * 8,
+                               hipMemcpyHostToDevice, s));
+    } else {
+        // the windows stay in the slot's pinned staging and K1Q reads them over the bus (each
+        // wave's next tile words prefetched a tile ahead, as a lone filtered query's): no
+        // host-to-device copy in front of the scan (16 x 125 KB: ~45 us of copy)
+        fill_windows(win, 0, B);
+        d_allow = win;
     }
-    fill_windows(win, hB, B);
-    WVG_HIP(hipMemcpyAsync(b + o_allow + (size_t)hB * W * 8, win + (size_t)hB * W, (size_t)(B - hB) * W * 8,
-                           hipMemcpyHostToDevice, s));
-    rc = run_search(c, b + o_q, qpitch, B, k, (const uint64_t *)(b + o_allow), p, (uint64_t *)(b + o_part),
-                    (uint64_t *)(b + o_ids), (float *)(b + o_d), (uint32_t *)(b + o_cnt), s);
+    WVG_STAMP(2);
+    rc = run_search(c, b + o_q, qpitch, B, k, d_allow, p, (uint64_t *)(b + o_part), (uint64_t *)(b + o_ids),
+                    (float *)(b + o_d), (uint32_t *)(b + o_cnt), s);
     if (rc) return rc;
     const char *pin = out_b <= STAGE_MAX ? st.take(out_b) : nullptr;
     std::vector<char> big(pin ? 0 : out_b);
     if (!pin) pin = big.data();
     WVG_HIP(hipMemcpyAsync((void *)pin, b + o_ids, out_b, hipMemcpyDeviceToHost, s));
+    WVG_STAMP(3);
     WVG_HIP(hipStreamSynchronize(s));  // also keeps q / win alive until their copies are done
+#ifdef WVG_TOOLS
+    WVG_STAMP(4);
+    filtered_timing(tstamp);
+#endif
     std::memcpy(out_ids, pin, (size_t)B * k * 8);
     std::memcpy(out_dists, pin + (o_d - o_ids), (size_t)B * k * 4);
     std::memcpy(out_counts, pin + (o_cnt - o_ids), (size_t)B * 4);
