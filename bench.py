@@ -348,7 +348,7 @@ def config_batched(ctx, orc, metric_name, metric, reps=3):
     tflops = flop / screen_s / 1e12
     return {"workload": f"{n:,} x {d} fp32 {metric_name}, {Q}-query batches, exact {k}-NN (host API wvg_search)",
             "qps": round(Q / wall, 1), "batch_ms": round(wall * 1e3, 3), "batches": reps,
-            "kernel": "int8 MFMA screen (K3i screen_ar_kernel<12, 0, true>: exact int32 scores + a per-row "
+            "kernel": "int8 MFMA screen (K3i screen_i8_kernel<12, 0>, 2 x 2 waves per workgroup: exact int32 scores + a per-row "
                       "quantization-error bound) + exact fp32 AVX2-order rescore",
             "roofline": {"bound": "mfma", "achieved": round(tflops, 1), "peak": I8_PEAK_TOPS, "unit": "TOP/s (int8)",
                          "frac": round(tflops / I8_PEAK_TOPS, 4),
