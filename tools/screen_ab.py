@@ -72,6 +72,7 @@ def main():
             lib.wvgx_set_tuning(30, w2)
             lib.wvgx_set_tuning(26, spl)
             lib.wvgx_set_tuning(23, gp)
+            lib.wvgx_set_tuning(32, gp)
             lib.wvgx_set_tuning(22, sd)
             lib.wvgx_set_tuning(21, pl)
             lib.wvgx_set_tuning(20, vr)
@@ -120,6 +121,7 @@ def main():
     lib.wvgx_set_tuning(21, 16)
     lib.wvgx_set_tuning(22, 3)
     lib.wvgx_set_tuning(23, 512)
+    lib.wvgx_set_tuning(32, 256)
     c.destroy()
     ctx.close()
 

@@ -3565,7 +3565,7 @@ hipError_t launch_screen(const ScreenLaunch &L, hipStream_t s)
     const LaunchEvents ev = armed_events();
     armed_events() = LaunchEvents{};
     const uint64_t pilot_tiles = (uint64_t)std::max(tuning().screen_pilot, 0);
-    const uint64_t pilot_gemm_tiles = (uint64_t)std::max(tuning().screen_pilot_gemm, 0);
+    const uint64_t pilot_gemm_tiles = (uint64_t)std::max(L.i8 ? tuning().screen_pilot_gemm_i8 : tuning().screen_pilot_gemm, 0);
     // Screen pilot: short ranges of the screen itself over the first sp_tiles tiles
     // (one workgroup per CU), lists into the pilot scratch ([nq][sp_rr][SCREEN_M]),
     // then one exact seed from them (below, once the kernel is chosen)
