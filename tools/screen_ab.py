@@ -31,11 +31,12 @@ def main():
     ap.add_argument("--splits", default="1", help="K3c split launch (tuning key 19)")
     ap.add_argument("--variants", default="0", help="screen kernel (tuning key 20): 0 K3d where it applies, 1 K3c")
     ap.add_argument("--pilots", default="16", help="tiles of the exact pilot scan that seeds the bound (tuning key 21; 0 = none)")
-    ap.add_argument("--gpilots", default="512", help="tiles of the K3b pilot (tuning key 23; 0 = the K1 pilot)")
+    ap.add_argument("--gpilots", default="256", help="tiles of the K3b pilot (tuning keys 23 and 32; 0 = the K1 pilot)")
     ap.add_argument("--spilots", default="0", help="tiles of the screen pilot (tuning key 26; 0 = the K3b pilot)")
     ap.add_argument("--warms", default="32", help="K3i warm-up row blocks per first-phase range (tuning key 29; 0 = equal ranges)")
     ap.add_argument("--seeds", default="3", help="exact seeds (tuning key 22): bit 0 between phases, bit 1 before the final collect")
     ap.add_argument("--warm2s", default="0", help="K3i second-phase row blocks per range (tuning key 30; 0 = rest uniform)")
+    ap.add_argument("--rounds", default="1", help="screen ranges in whole CU rounds (tuning key 33)")
     a = ap.parse_args()
     import torch
 
@@ -59,7 +60,7 @@ def main():
     od = torch.empty((nq, k), dtype=torch.float32, device=dev)
     oc = torch.empty(nq, dtype=torch.int32, device=dev)
     ref = None
-    for w2, wm, spl, gp, sd, pl, vr, sp, rb, dg in [(w2, wm, spl, gp, sd, pl, vr, sp, rb, dg) for w2 in [int(x) for x in a.warm2s.split(",")] for wm in [int(x) for x in a.warms.split(",")]
+    for rd, w2, wm, spl, gp, sd, pl, vr, sp, rb, dg in [(rd, w2, wm, spl, gp, sd, pl, vr, sp, rb, dg) for rd in [int(x) for x in a.rounds.split(",")] for w2 in [int(x) for x in a.warm2s.split(",")] for wm in [int(x) for x in a.warms.split(",")]
                                        for spl in [int(x) for x in a.spilots.split(",")]
                                        for gp in [int(x) for x in a.gpilots.split(",")]
                                        for sd in [int(x) for x in a.seeds.split(",")]
@@ -68,6 +69,7 @@ def main():
                                for sp in [int(x) for x in a.splits.split(",")]
                            for rb in [int(x) for x in a.ranges.split(",")] for dg in [int(x) for x in a.diags.split(",")]]:
         if True:
+            lib.wvgx_set_tuning(33, rd)
             lib.wvgx_set_tuning(29, wm)
             lib.wvgx_set_tuning(30, w2)
             lib.wvgx_set_tuning(26, spl)
@@ -107,10 +109,11 @@ def main():
                 if ref is None:
                     ref = got
                 same = bool(np.array_equal(got, ref))
-            print(json.dumps({"warm": wm, "warm2": w2, "screen_pilot": spl, "gemm_pilot": gp, "seed": sd, "pilot": pl, "search_ms": round(wall, 3), "variant": vr, "split": sp, "range_blocks": rb, "diag": dg, "scoring_kernel_ms": round(kern, 3),
+            print(json.dumps({"round": rd, "warm": wm, "warm2": w2, "screen_pilot": spl, "gemm_pilot": gp, "seed": sd, "pilot": pl, "search_ms": round(wall, 3), "variant": vr, "split": sp, "range_blocks": rb, "diag": dg, "scoring_kernel_ms": round(kern, 3),
                               "tflops": round(2.0 * nq * n * d / (kern / 1e3) / 1e12, 1),
                               "ids_equal_first": same, "wave_row_blocks": cnt[0], "slow_path_blocks": cnt[1],
                               "insert_calls": cnt[2], "exact_groups": cnt[3]}), flush=True)
+    lib.wvgx_set_tuning(33, 1)
     lib.wvgx_set_tuning(29, 32)
     lib.wvgx_set_tuning(30, 0)
     lib.wvgx_set_tuning(26, 0)

@@ -11,6 +11,7 @@ Tooling only (product library; no tuning knobs)."""
 import argparse
 import ctypes
 import json
+import math
 import os
 import sys
 import time
@@ -21,14 +22,26 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def screen_nrr(n, nq, num_cus=256, whole_rounds=True):
+    """The screen's row ranges for n rows and nq queries: screen_row_ranges
+    (wvg_screen.hip), whole_rounds = its tuning screen_round."""
+    nqb = (nq + 127) // 128
+    nblk = ((n + 63) // 64 + 3) // 4
+    want = max((num_cus + nqb - 1) // nqb, (nblk + 127) // 128)
+    want = min((want + 7) // 8 * 8, 512)
+    if whole_rounds:
+        step = 8 * (num_cus // math.gcd(num_cus, nqb)) // math.gcd(8, num_cus // math.gcd(num_cus, nqb))
+        w2 = (want + step - 1) // step * step
+        if w2 <= 512 and w2 * 8 <= want * 9:
+            want = w2
+    return max(1, min(want, nblk))
+
+
 def screen_offsets(n, nq, k, d, num_cus=256):
     """(candidate-array byte offset, candidates per query, flagged-count byte
     offset) in a K3c / K3d workspace (screen_ws in wvg_search.hip, after the
     256-byte status block); mirrors screen_row_ranges."""
-    nqb = (nq + 127) // 128
-    nblk = ((n + 63) // 64 + 3) // 4
-    want = max((num_cus + nqb - 1) // nqb, (nblk + 127) // 128)
-    nrr = max(1, min(min((want + 7) // 8 * 8, 512), nblk))
+    nrr = screen_nrr(n, nq, num_cus)
     ncand = nrr * 16
     part = (nq * ncand * 8 + 255) // 256 * 256
     return part, ncand, screen_nflag_offset(n, nq, k, d, num_cus)
@@ -37,10 +50,7 @@ def screen_offsets(n, nq, k, d, num_cus=256):
 def screen_nflag_offset(n, nq, k, d, num_cus=256):
     """Byte offset of the flagged-query count in a K3c workspace (screen_ws in
     wvg_search.hip, after the 256-byte status block); mirrors screen_row_ranges."""
-    nqb = (nq + 127) // 128
-    nblk = ((n + 63) // 64 + 3) // 4
-    want = max((num_cus + nqb - 1) // nqb, (nblk + 127) // 128)
-    nrr = max(1, min(min((want + 7) // 8 * 8, 512), nblk))
+    nrr = screen_nrr(n, nq, num_cus)
     off = 0
 
     def take(b):

@@ -456,7 +456,8 @@ int wvgx_filtered_timing(uint64_t *out5, int reset)
 // 18 = K3c diagnostics (results not distances), 19 = K3c split launch,
 // 20 = screen kernel (0 K3d where it applies, 1 K3c), 21 = screen pilot seed, 22 = exact seeds between
 // screen phases, 23 = K3b pilot tiles, 24 = single-query host path, ..., 29 / 30 = K3i warm-up range
-// blocks (first / second phase), 31 = filtered batches' windows from pinned staging, 32 = K3i's K3b pilot tiles.  Returns the previous value.
+// blocks (first / second phase), 31 = filtered batches' windows from pinned staging, 32 = K3i's K3b pilot tiles,
+// 33 = screen ranges in whole rounds of the CUs.  Returns the previous value.
 int wvgx_set_tuning(int key, int value)
 {
     Tuning &t = tuning();
@@ -560,6 +561,9 @@ int wvgx_set_tuning(int key, int value)
     } else if (key == 32) {
         old = t.screen_pilot_gemm_i8;
         t.screen_pilot_gemm_i8 = value;
+    } else if (key == 33) {
+        old = t.screen_round;
+        t.screen_round = value;
     }
     return old;
 }

@@ -459,6 +459,7 @@ struct Tuning {
     int screen_pilot = 16;   // K3c/K3d: tiles of the exact pilot scan that seeds the bound (0 = none; A/B)
     int screen_pilot_gemm = 512;  // K3c/K3d: tiles of the K3b (exact fp32 MFMA) pilot, which replaces the K1
                                   // pilot (0 = the K1 pilot; A/B)
+    int screen_round = 1;    // screen row ranges (tuning key 33): 1 = nrr * query blocks a multiple of the CUs
     int screen_pilot_gemm_i8 = 256;  // the same for K3i (tuning key 32): with its warm-up ranges half the
                                      // pilot is ~1 % faster per batch (profiles/r06/screen_i8/pilot_tiles_ab*.jsonl)
     int screen_variant = 0;  // batched screen kernel: 0 = K3d where it applies (d = 512, 768), 1 = K3c,

@@ -1350,10 +1350,14 @@ hipError_t launch_synth_rows(uint64_t seed, int dist, const uint64_t *ids, uint6
 template <int METRIC>
 __global__ void rescore_keys_kernel(int metric, const float4 *q4, uint32_t qpitch, const float4 *tiled, uint32_t dim,
                                     uint32_t nchunks, const uint64_t *cand, uint32_t ncand, uint32_t cand_stride,
-                                    uint64_t *out, int o512)
+                                    uint64_t *out, int o512, int qmajor)
 {
-    const uint32_t qi = blockIdx.y;
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    // qmajor: grid (nq, chunks), so consecutive workgroups -- on different XCDs -- are different
+    // queries whatever ncand is (grid (chunks, nq) put chunk x of every query on XCD x mod 8 when
+    // the chunk count was a multiple of 8: the screen's rescore at 5120 candidates per query ran
+    // 0.95 ms instead of 0.24); the other order only for more than 65535 chunks (grid y's limit)
+    const uint32_t qi = qmajor ? blockIdx.x : blockIdx.y;
+    const uint32_t j = (qmajor ? blockIdx.y : blockIdx.x) * blockDim.x + threadIdx.x;
     if (j >= ncand) return;
     const uint64_t key = cand[(size_t)qi * cand_stride + j];
     uint64_t res = WVG_KEY_NONE;
@@ -1372,11 +1376,13 @@ hipError_t launch_rescore_keys(int metric, const float *q, uint32_t qpitch, cons
                                uint32_t cand_stride, uint64_t *out_keys, hipStream_t s, int o512)
 {
     if (nq == 0 || ncand == 0) return hipSuccess;
-    dim3 grid((ncand + 63) / 64, nq), block(64);
+    const uint32_t chunks = (ncand + 63) / 64;
+    const int qmajor = chunks <= 65535 ? 1 : 0;
+    dim3 grid(qmajor ? nq : chunks, qmajor ? chunks : nq), block(64);
     with_metric(metric, [&](auto M) {
         hipLaunchKernelGGL((rescore_keys_kernel<decltype(M)::value>), grid, block, 0, s, metric,
                            reinterpret_cast<const float4 *>(q), qpitch, reinterpret_cast<const float4 *>(tiled), dim,
-                           nchunks, cand_keys, ncand, cand_stride, out_keys, o512);
+                           nchunks, cand_keys, ncand, cand_stride, out_keys, o512, qmajor);
     });
     return hipGetLastError();
 }
