@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--seeds", default="3", help="exact seeds (tuning key 22): bit 0 between phases, bit 1 before the final collect")
     ap.add_argument("--warm2s", default="0", help="K3i second-phase row blocks per range (tuning key 30; 0 = rest uniform)")
     ap.add_argument("--rounds", default="1", help="screen ranges in whole CU rounds (tuning key 33)")
+    ap.add_argument("--set", default="", help="extra tuning keys for the whole run: key=value,key=value")
     a = ap.parse_args()
     import torch
 
@@ -53,6 +54,9 @@ def main():
     ctx = Context(0)
     lib = ctx.lib
     lib.wvgx_set_tuning.restype = ctypes.c_int
+    for kv in filter(None, a.set.split(",")):
+        kk, vv = kv.split("=")
+        lib.wvgx_set_tuning(int(kk), int(vv))
     c = Corpus(ctx, KIND_F32, METRIC_COSINE, d, n)
     c.fill_synthetic(42, n, 0)
     ctx.synchronize()
