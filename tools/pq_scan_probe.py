@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--rows", type=int, default=25_000_000)
     ap.add_argument("--queries", type=int, default=64)
     ap.add_argument("--variants", default="0,52")
+    ap.add_argument("--gpcs", default="0", help="workgroups per CU (tuning key 1; 0 = the product's choice)")
     a = ap.parse_args()
     from weaviate_amd._lib import KIND_PQ, METRIC_L2, check
     from weaviate_amd.device import Context, Corpus
@@ -41,8 +42,9 @@ def main():
         cnt = min(step, n - r0)
         c.upsert_codes(np.arange(r0, r0 + cnt, dtype=np.uint64), rng.integers(0, ks, (cnt, m), dtype=np.uint8))
     qs = rng.uniform(-1, 1, (a.queries, d)).astype(np.float32)
-    for v in (int(x) for x in a.variants.split(",")):
+    for g, v in ((int(g), int(x)) for g in a.gpcs.split(",") for x in a.variants.split(",")):
         prev = lib.wvgx_set_tuning(7, v)
+        prev_g = lib.wvgx_set_tuning(1, g)
         ref = c.search(qs[0], 10)
         for i in range(8):
             c.search(qs[i % len(qs)], 10)
@@ -52,9 +54,10 @@ def main():
         ms, nl = ctypes.c_double(), ctypes.c_uint64()
         check(lib.wvg_profile_stop(ctx.handle, ctypes.byref(ms), ctypes.byref(nl)))
         lib.wvgx_set_tuning(7, prev)
+        lib.wvgx_set_tuning(1, prev_g)
         same = bool(np.array_equal(ref[0], c.search(qs[0], 10)[0]))
         scan_ms = ms.value / max(1, nl.value)
-        print(json.dumps({"variant": v, "rows": n, "scan_ms": round(scan_ms, 4),
+        print(json.dumps({"variant": v, "groups_per_cu": g, "rows": n, "scan_ms": round(scan_ms, 4),
                           "GBps": round(n * m / scan_ms / 1e6, 1), "launches": int(nl.value),
                           "same_as_product": same}), flush=True)
     c.destroy()
